@@ -1,0 +1,87 @@
+"""ctypes binding of ``libvgan_hip.so`` (the C ABI declared in ``include/vgan.h``).
+
+The library is REQUIRED: importing this module raises if it was not built, and
+every wrapper refuses non-CUDA tensors.  There is no CPU or eager-torch fallback
+for the message-passing core.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvgan_hip.so")
+VG_EINVAL = -1
+
+_c_i32, _c_i64, _c_f32, _c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
+
+# name -> (restype, argtypes); every function listed here is declared in include/vgan.h
+SIGNATURES = {
+    "vg_csr_ws_ints": (_c_i64, [_c_i64, _c_i32]),
+    "vg_csr_build": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "vg_gat_fwd": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p]),
+    "vg_gat_bwd": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p,
+                                  _c_f32, _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "vg_spmm": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p]),
+    "vg_spmm_t": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p]),
+    "vg_sddmm": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p]),
+    "vg_seg_sum": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_p, _c_p]),
+    "vg_seg_max": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_p, _c_p]),
+    "vg_gather": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p]),
+    "vg_scatter_src": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_p, _c_p, _c_p]),
+    "vg_graphnorm_ws_floats": (_c_i64, [_c_i32, _c_i32]),
+    "vg_graphnorm_fwd": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p]),
+    "vg_graphnorm_bwd": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p,
+                                        _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "vg_type_mean": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_i32, _c_p, _c_p]),
+    "vg_gumbel_fwd": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_f32, _c_p, _c_p, _c_p, _c_p]),
+    "vg_gumbel_bwd": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_i32, _c_i32, _c_f32, _c_p, _c_p]),
+    "vg_far_per_graph": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32,
+                                        _c_f32, _c_i32, _c_p, _c_p, _c_p]),
+    "vg_confusion": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_p]),
+    "vg_adam": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_i64, _c_f32, _c_f32, _c_f32, _c_f32, _c_f32, _c_f32,
+                               _c_f32, _c_p]),
+}
+
+
+def _load() -> ctypes.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(hipcc --offload-arch=gfx950). The HIP library is required; there is no fallback."
+        )
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+LIB = _load()
+
+
+def ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_handle(device: torch.device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def check(rc: int, name: str) -> None:
+    if rc != 0:
+        what = "invalid argument" if rc == VG_EINVAL else f"hipError {rc}"
+        raise RuntimeError(f"{name} failed: {what}")
+
+
+def require_cuda(*tensors: Optional[torch.Tensor]) -> None:
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError("vgan HIP ops require tensors on a ROCm device (no CPU fallback)")
+        if not t.is_contiguous():
+            raise RuntimeError("vgan HIP ops require contiguous tensors")

@@ -1,0 +1,70 @@
+"""Per-mini-batch device structures shared by every G/D pass of a step.
+
+A step runs 6 generator and 16 discriminator forwards over the SAME batch
+(``trainer.py:467-491``).  Everything that depends only on the batch is built
+once here and cached on the batch object:
+
+* ``csr``              destination CSR + source CSC (``vgan.ops.CSR``), replacing
+                       GATConv's per-layer remove/add self loops;
+* ``matched_voxel_x``  [N, F_local + F_voxel] = [type-matched mean | voxel.x],
+                       the first block of the discriminator input
+                       (``models.py:230-239``) and, sliced, the generator's
+                       matched features (``models.py:122-131``);
+* ``onehot_f``         float one-hot of the ground-truth voxel types.
+
+The type-matched mean is a pure function of the batch (program features and
+ground-truth voxel types), so caching it is exact.
+"""
+from __future__ import annotations
+
+import weakref
+from dataclasses import dataclass
+
+import torch
+
+from . import ops
+
+
+@dataclass
+class Prepared:
+    csr: ops.CSR
+    matched_x: torch.Tensor
+    voxel_x: torch.Tensor
+    matched_voxel_x: torch.Tensor
+    onehot_f: torch.Tensor
+
+
+_FALLBACK_CACHE: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+
+
+def _build(local_graph, voxel_graph, n_classes: int) -> Prepared:
+    vx = voxel_graph.x
+    if vx.dtype != torch.float32:
+        vx = vx.float()
+    vx = vx.contiguous()
+    lx = local_graph.x.float().contiguous()
+    n, fv = vx.shape
+    fl = lx.shape[1]
+    csr = ops.CSR(voxel_graph.edge_index, n)
+    mv = torch.empty(n, fl + fv, dtype=torch.float32, device=vx.device)
+    ops.type_mean(lx, local_graph.type, voxel_graph.type, n_classes, out=mv, col0=0)
+    mv[:, fl:].copy_(vx)
+    onehot = voxel_graph.types_onehot if hasattr(voxel_graph, "types_onehot") else None
+    onehot_f = onehot.to(torch.float32).contiguous() if onehot is not None else None
+    return Prepared(csr=csr, matched_x=mv[:, :fl].contiguous(), voxel_x=vx, matched_voxel_x=mv, onehot_f=onehot_f)
+
+
+def prepared(local_graph, voxel_graph, n_classes: int) -> Prepared:
+    getter = getattr(voxel_graph, "derived", None)
+    if callable(getter):
+        prep = getter("prepared")
+        if prep is None:
+            prep = _build(local_graph, voxel_graph, n_classes)
+            voxel_graph.set_derived("prepared", prep)
+        return prep
+    key = voxel_graph.x
+    prep = _FALLBACK_CACHE.get(key)
+    if prep is None:
+        prep = _build(local_graph, voxel_graph, n_classes)
+        _FALLBACK_CACHE[key] = prep
+    return prep

@@ -1,0 +1,204 @@
+"""VoxelGNNGenerator / VoxelGNNDiscriminator on the HIP message-passing core.
+
+Drop-in for ``building_gan/src/models.py``:
+
+* constructor signatures ``(configuration, local_graph_dim, voxel_graph_dim)``
+  and ``forward`` signatures/returns are the reference's (``models.py:15,119,
+  159,229``);
+* parameter names are the reference state_dict keys
+  (``matched_features_encoder.{i}``, ``mlp_encoder.{i}``,
+  ``encoder.module_{i}.{lin.weight,att_src,att_dst,bias | weight,bias,mean_scale}``,
+  ``decoder.{i}``), so reference checkpoints load unchanged;
+* construction consumes the CPU generator in the reference's order with the
+  same initialisers (torch defaults for Linear, glorot for GATConv), so the
+  same seed yields the same initial weights.
+
+Every GATConv block runs ``gat_aggregate`` (fused logits + segment softmax +
+aggregation) followed by ``graphnorm_relu_dropout`` (GraphNorm with batch=None,
+ReLU and Dropout in one op).  The type-matched mean, CSR and float one-hot are
+per-batch data and are computed once per mini-batch (``vgan.data``).
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+
+from . import data as vdata
+from . import ops
+from .rng import RNG
+
+_CONV_TYPES = ("GCNCONV", "GRAPHCONV", "GATCONV", "GATV2CONV")
+
+
+def _glorot_(t: torch.Tensor) -> None:
+    bound = math.sqrt(6.0 / (t.size(-2) + t.size(-1)))
+    with torch.no_grad():
+        t.uniform_(-bound, bound)
+
+
+class _GATLin(nn.Module):
+    """The bias-free, glorot-initialised projection of GATConv (``lin.weight``)."""
+
+    def __init__(self, cin: int, cout: int):
+        super().__init__()
+        self.weight = nn.Parameter(torch.empty(cout, cin))
+        _glorot_(self.weight)  # torch_geometric Linear.__init__ -> reset_parameters
+
+
+class GATConv(nn.Module):
+    """GATConv(in, out) with heads=1 (torch_geometric 2.6.1 defaults) on the HIP core."""
+
+    def __init__(self, in_channels: int, out_channels: int, negative_slope: float = 0.2):
+        super().__init__()
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.negative_slope = negative_slope
+        self.lin = _GATLin(in_channels, out_channels)
+        self.att_src = nn.Parameter(torch.empty(1, 1, out_channels))
+        self.att_dst = nn.Parameter(torch.empty(1, 1, out_channels))
+        self.bias = nn.Parameter(torch.empty(out_channels))
+        self.reset_parameters()
+
+    def reset_parameters(self) -> None:
+        _glorot_(self.lin.weight)
+        _glorot_(self.att_src)
+        _glorot_(self.att_dst)
+        with torch.no_grad():
+            self.bias.zero_()
+
+    def forward(self, x: torch.Tensor, csr: ops.CSR) -> torch.Tensor:
+        h = torch.nn.functional.linear(x, self.lin.weight)
+        a_src = torch.mv(h, self.att_src.view(-1))
+        a_dst = torch.mv(h, self.att_dst.view(-1))
+        return ops.gat_aggregate(csr, h, a_src, a_dst, self.bias, self.negative_slope)
+
+
+class GraphNorm(nn.Module):
+    def __init__(self, channels: int, eps: float = 1e-5):
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(channels))
+        self.bias = nn.Parameter(torch.zeros(channels))
+        self.mean_scale = nn.Parameter(torch.ones(channels))
+
+
+class GATEncoder(nn.Module):
+    """The ``tgnn.Sequential("x, edge_index", [...])`` stack of models.py:68-90 /
+    187-210: ``depth`` halving blocks then ``depth`` doubling blocks, each
+    [GATConv -> GraphNorm -> ReLU -> Dropout] (children ``module_{4b+0..3}``)."""
+
+    def __init__(self, width: int, depth: int, dropout: float = 0.2):
+        super().__init__()
+        self.dropout = dropout
+        chans = [width]
+        for _ in range(depth):
+            chans.append(chans[-1] // 2)
+        for _ in range(depth):
+            chans.append(chans[-1] * 2)
+        self.widths = chans
+        self.num_blocks = 2 * depth
+        for b, (cin, cout) in enumerate(zip(chans[:-1], chans[1:])):
+            self.add_module(f"module_{4 * b}", GATConv(cin, cout))
+            self.add_module(f"module_{4 * b + 1}", GraphNorm(cout))
+            self.add_module(f"module_{4 * b + 2}", nn.ReLU(True))
+            self.add_module(f"module_{4 * b + 3}", nn.Dropout(dropout))
+
+    @property
+    def out_channels(self) -> int:
+        return self.widths[-1]
+
+    def forward(self, x: torch.Tensor, csr: ops.CSR, rng: RNG) -> torch.Tensor:
+        for b in range(self.num_blocks):
+            conv: GATConv = getattr(self, f"module_{4 * b}")
+            norm: GraphNorm = getattr(self, f"module_{4 * b + 1}")
+            h = conv(x, csr)
+            keep = rng.keep_mask(h.shape, self.dropout, h.device) if self.training else None
+            x = ops.graphnorm_relu_dropout(h, norm.weight, norm.bias, norm.mean_scale, keep, norm.eps)
+        return x
+
+
+def _mlp(widths: List[int], norm: bool, act) -> nn.Sequential:
+    mods: List[nn.Module] = []
+    for a, b in zip(widths[:-1], widths[1:]):
+        mods.append(nn.Linear(a, b))
+        if norm:
+            mods.append(nn.LayerNorm(b))
+        mods.append(act())
+    return nn.Sequential(*mods)
+
+
+def _check_conv(kind: str) -> None:
+    if kind not in _CONV_TYPES:
+        raise ValueError(f"Invalid conv_type: {kind}")
+    if kind != "GATCONV":
+        raise NotImplementedError(f"{kind}: only GATCONV (the configured default) has a HIP path")
+
+
+class VoxelGNNGenerator(nn.Module):
+    """models.py:14-155."""
+
+    def __init__(self, configuration, local_graph_dim: int, voxel_graph_dim: int):
+        super().__init__()
+        cfg = configuration
+        _check_conv(cfg.GENERATOR_CONV_TYPE)
+        self.configuration = cfg
+        self.local_graph_dim, self.voxel_graph_dim = local_graph_dim, voxel_graph_dim
+        hl, hg, zd = cfg.LOCAL_ENCODER_HIDDEN_DIM, cfg.GENERATOR_HIDDEN_DIM, cfg.Z_DIM
+        lrelu = lambda: nn.LeakyReLU(0.2)  # noqa: E731
+        self.matched_features_encoder = _mlp([local_graph_dim] + [hl] * (cfg.LOCAL_GRAPH_ENCODER_REPEAT + 1), True,
+                                             lrelu)
+        self.mlp_encoder = _mlp([hl + voxel_graph_dim + zd] + [hg] * (cfg.GENERATOR_MLP_ENCODER_REPEAT + 1), True,
+                                lrelu)
+        self.encoder = GATEncoder(hg, cfg.GENERATOR_ENCODER_REPEAT, cfg.ENCODER_DROPOUT_RATE)
+        dec = list(_mlp([hl + voxel_graph_dim + zd + self.encoder.out_channels + hg, hg, hg // 2, hg // 4, hg // 8],
+                        True, lrelu).children())
+        dec.append(nn.Linear(hg // 8, cfg.NUM_CLASSES))
+        self.decoder = nn.Sequential(*dec)
+        self.rng = RNG(getattr(cfg, "runtime", {}).get("rng", "device"))
+        self.tau = 1.0
+        self.to(cfg.DEVICE)
+
+    def forward(self, local_graph, voxel_graph, z, noise: Optional[torch.Tensor] = None):
+        prep = vdata.prepared(local_graph, voxel_graph, self.configuration.NUM_CLASSES)
+        em = self.matched_features_encoder(prep.matched_x)
+        zz = z.squeeze(0)
+        vx = prep.voxel_x
+        x = self.mlp_encoder(torch.cat([em, vx, zz], dim=-1))
+        enc = self.encoder(x, prep.csr, self.rng)
+        logits = self.decoder(torch.cat([enc, x, em, vx, zz], dim=-1))
+        if noise is None:
+            noise = self.rng.exponential(logits.shape, logits.device)
+        label_hard, label_soft = ops.gumbel_head(logits, noise, self.tau)
+        return logits, label_hard, label_soft
+
+
+class VoxelGNNDiscriminator(nn.Module):
+    """models.py:158-245 (per-node critic scores [N, 1])."""
+
+    def __init__(self, configuration, local_graph_dim: int, voxel_graph_dim: int):
+        super().__init__()
+        cfg = configuration
+        _check_conv(cfg.DISCRIMINATOR_CONV_TYPE)
+        self.configuration = cfg
+        self.local_graph_dim, self.voxel_graph_dim = local_graph_dim, voxel_graph_dim
+        hd = cfg.DISCRIMINATOR_HIDDEN_DIM
+        relu = lambda: nn.ReLU(True)  # noqa: E731
+        self.mlp_encoder = _mlp([local_graph_dim + voxel_graph_dim + cfg.NUM_CLASSES, hd, hd], False, relu)
+        self.encoder = GATEncoder(hd, cfg.DISCRIMINATOR_ENCODER_REPEAT, cfg.ENCODER_DROPOUT_RATE)
+        dec = list(_mlp([hd, hd // 2, hd // 4, hd // 8], False, relu).children())
+        dec.append(nn.Linear(hd // 8, 1))
+        if not cfg.USE_WGANGP:
+            dec.append(nn.Sigmoid())
+        self.decoder = nn.Sequential(*dec)
+        self.rng = RNG(getattr(cfg, "runtime", {}).get("rng", "device"))
+        self.to(cfg.DEVICE)
+
+    def forward(self, local_graph, voxel_graph, label_hard):
+        prep = vdata.prepared(local_graph, voxel_graph, self.configuration.NUM_CLASSES)
+        label = label_hard.squeeze(0)
+        if label.dtype != torch.float32:
+            label = label.to(torch.float32)
+        feats = torch.cat([prep.matched_voxel_x, label], dim=-1)
+        return self.decoder(self.encoder(self.mlp_encoder(feats), prep.csr, self.rng))

@@ -1,0 +1,473 @@
+"""Differentiable operators over the HIP C ABI.
+
+Fast path
+    ``gat_aggregate``        one fused kernel forward (logits + segment softmax +
+                             weighted gather-sum + bias), two fused kernels for the
+                             first-order backward (no atomics).
+    ``graphnorm_relu_dropout`` stats + apply forward, partial/final/apply backward.
+    ``gumbel_head``          row kernel forward/backward.
+
+Twice-differentiable path (WGAN-GP, ``trainer.py:306-312`` with
+``create_graph=True``).  When autograd asks for a graph of the backward
+(``torch.is_grad_enabled()`` inside ``backward``), the GAT and GraphNorm
+backward re-express the forward through the closed primitive set
+
+    spmm <-> spmm_t, sddmm, gather(src|dst) <-> scatter_src / seg_sum
+
+whose adjoints are each other (all HIP kernels), so any order of derivative is
+available and every derivative runs through the same C ABI.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+from torch.autograd import Function
+
+from . import _lib
+from ._lib import LIB, check, ptr, require_cuda, stream_handle
+
+NEG_SLOPE = 0.2
+SOFTMAX_EPS = 1e-16
+
+
+# --------------------------------------------------------------------- CSR
+class CSR:
+    """Destination CSR with self loops + its source CSC, built on the device once
+    per mini-batch (replaces remove_self_loops/add_self_loops in every layer)."""
+
+    def __init__(self, edge_index: torch.Tensor, num_nodes: int):
+        require_cuda(edge_index)
+        if edge_index.dtype != torch.long or edge_index.dim() != 2 or edge_index.shape[0] != 2:
+            raise ValueError("edge_index must be int64 [2, E]")
+        dev = edge_index.device
+        n = int(num_nodes)
+        e = int(edge_index.shape[1])
+        ei = edge_index.contiguous()
+        i32 = dict(dtype=torch.int32, device=dev)
+        row_ptr = torch.empty(n + 1, **i32)
+        col = torch.empty(e + n, **i32)
+        csc_ptr = torch.empty(n + 1, **i32)
+        csc_slot = torch.empty(e + n, **i32)
+        csc_dst = torch.empty(e + n, **i32)
+        ws = torch.empty(int(LIB.vg_csr_ws_ints(e, n)), **i32)
+        status = torch.zeros(2, **i32)
+        check(LIB.vg_csr_build(ptr(ei), e, n, ptr(row_ptr), ptr(col), ptr(csc_ptr), ptr(csc_slot),
+                               ptr(csc_dst), ptr(ws), ptr(status), stream_handle(dev)), "vg_csr_build")
+        st = status.cpu()  # one host sync per mini-batch (sizes the edge arrays)
+        if int(st[1]) != 0:
+            raise ValueError("edge_index contains node ids outside [0, num_nodes)")
+        ep = int(st[0])
+        self.num_nodes, self.num_edges = n, ep
+        self.row_ptr, self.col = row_ptr, col[:ep]
+        self.csc_ptr, self.csc_slot, self.csc_dst = csc_ptr, csc_slot[:ep], csc_dst[:ep]
+        self.device = dev
+
+    def stream(self):
+        return stream_handle(self.device)
+
+
+def _f32(t: torch.Tensor) -> torch.Tensor:
+    if t.dtype != torch.float32:
+        raise TypeError(f"expected float32, got {t.dtype}")
+    return t.contiguous()
+
+
+# ----------------------------------------------------- sparse primitives
+def _empty_like_rows(csr: CSR, c: Optional[int], like: torch.Tensor) -> torch.Tensor:
+    shape = (csr.num_nodes,) if c is None else (csr.num_nodes, c)
+    return torch.empty(shape, dtype=torch.float32, device=like.device)
+
+
+def _spmm_raw(csr: CSR, w: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    w, x = _f32(w), _f32(x)
+    require_cuda(w, x)
+    y = _empty_like_rows(csr, x.shape[1], x)
+    check(LIB.vg_spmm(ptr(csr.row_ptr), ptr(csr.col), csr.num_nodes, x.shape[1], ptr(w), ptr(x), ptr(y),
+                      csr.stream()), "vg_spmm")
+    return y
+
+
+def _spmm_t_raw(csr: CSR, w: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
+    w, g = _f32(w), _f32(g)
+    require_cuda(w, g)
+    z = _empty_like_rows(csr, g.shape[1], g)
+    check(LIB.vg_spmm_t(ptr(csr.csc_ptr), ptr(csr.csc_slot), ptr(csr.csc_dst), csr.num_nodes, g.shape[1],
+                        ptr(w), ptr(g), ptr(z), csr.stream()), "vg_spmm_t")
+    return z
+
+
+def _sddmm_raw(csr: CSR, a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    a, b = _f32(a), _f32(b)
+    require_cuda(a, b)
+    e = torch.empty(csr.num_edges, dtype=torch.float32, device=a.device)
+    check(LIB.vg_sddmm(ptr(csr.row_ptr), ptr(csr.col), csr.num_nodes, a.shape[1], ptr(a), ptr(b), ptr(e),
+                       csr.stream()), "vg_sddmm")
+    return e
+
+
+def _gather_raw(csr: CSR, v: torch.Tensor, by_src: bool) -> torch.Tensor:
+    v = _f32(v)
+    require_cuda(v)
+    e = torch.empty(csr.num_edges, dtype=torch.float32, device=v.device)
+    check(LIB.vg_gather(ptr(csr.row_ptr), ptr(csr.col), csr.num_nodes, 1 if by_src else 0, ptr(v), ptr(e),
+                        csr.stream()), "vg_gather")
+    return e
+
+
+def _seg_sum_raw(csr: CSR, x: torch.Tensor) -> torch.Tensor:
+    x = _f32(x)
+    require_cuda(x)
+    s = _empty_like_rows(csr, None, x)
+    check(LIB.vg_seg_sum(ptr(csr.row_ptr), csr.num_nodes, ptr(x), ptr(s), csr.stream()), "vg_seg_sum")
+    return s
+
+
+def _seg_max_raw(csr: CSR, x: torch.Tensor) -> torch.Tensor:
+    x = _f32(x)
+    require_cuda(x)
+    m = _empty_like_rows(csr, None, x)
+    check(LIB.vg_seg_max(ptr(csr.row_ptr), csr.num_nodes, ptr(x), ptr(m), csr.stream()), "vg_seg_max")
+    return m
+
+
+def _scatter_src_raw(csr: CSR, x: torch.Tensor) -> torch.Tensor:
+    x = _f32(x)
+    require_cuda(x)
+    s = _empty_like_rows(csr, None, x)
+    check(LIB.vg_scatter_src(ptr(csr.csc_ptr), ptr(csr.csc_slot), csr.num_nodes, ptr(x), ptr(s), csr.stream()),
+          "vg_scatter_src")
+    return s
+
+
+class _SpMM(Function):
+    @staticmethod
+    def forward(ctx, w, x, csr):
+        ctx.csr = csr
+        ctx.save_for_backward(w, x)
+        return _spmm_raw(csr, w, x)
+
+    @staticmethod
+    def backward(ctx, gy):
+        w, x = ctx.saved_tensors
+        gw = sddmm(ctx.csr, gy, x) if ctx.needs_input_grad[0] else None
+        gx = spmm_t(ctx.csr, w, gy) if ctx.needs_input_grad[1] else None
+        return gw, gx, None
+
+
+class _SpMMT(Function):
+    @staticmethod
+    def forward(ctx, w, g, csr):
+        ctx.csr = csr
+        ctx.save_for_backward(w, g)
+        return _spmm_t_raw(csr, w, g)
+
+    @staticmethod
+    def backward(ctx, gz):
+        w, g = ctx.saved_tensors
+        gw = sddmm(ctx.csr, g, gz) if ctx.needs_input_grad[0] else None
+        gg = spmm(ctx.csr, w, gz) if ctx.needs_input_grad[1] else None
+        return gw, gg, None
+
+
+class _SDDMM(Function):
+    @staticmethod
+    def forward(ctx, a, b, csr):
+        ctx.csr = csr
+        ctx.save_for_backward(a, b)
+        return _sddmm_raw(csr, a, b)
+
+    @staticmethod
+    def backward(ctx, ge):
+        a, b = ctx.saved_tensors
+        ga = spmm(ctx.csr, ge, b) if ctx.needs_input_grad[0] else None
+        gb = spmm_t(ctx.csr, ge, a) if ctx.needs_input_grad[1] else None
+        return ga, gb, None
+
+
+class _Gather(Function):
+    @staticmethod
+    def forward(ctx, v, csr, by_src):
+        ctx.csr, ctx.by_src = csr, by_src
+        return _gather_raw(csr, v, by_src)
+
+    @staticmethod
+    def backward(ctx, ge):
+        gv = scatter_src(ctx.csr, ge) if ctx.by_src else seg_sum(ctx.csr, ge)
+        return gv, None, None
+
+
+class _SegSum(Function):
+    @staticmethod
+    def forward(ctx, x, csr):
+        ctx.csr = csr
+        return _seg_sum_raw(csr, x)
+
+    @staticmethod
+    def backward(ctx, gs):
+        return gather(ctx.csr, gs, by_src=False), None
+
+
+class _ScatterSrc(Function):
+    @staticmethod
+    def forward(ctx, x, csr):
+        ctx.csr = csr
+        return _scatter_src_raw(csr, x)
+
+    @staticmethod
+    def backward(ctx, gs):
+        return gather(ctx.csr, gs, by_src=True), None
+
+
+def spmm(csr: CSR, w: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """Y_i = sum_{k in row i} w_k X[col_k]."""
+    return _SpMM.apply(w, x, csr)
+
+
+def spmm_t(csr: CSR, w: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
+    """Z_j = sum_{k: col_k = j} w_k G[dst_k]."""
+    return _SpMMT.apply(w, g, csr)
+
+
+def sddmm(csr: CSR, a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """e_k = <A[dst_k], B[col_k]>."""
+    return _SDDMM.apply(a, b, csr)
+
+
+def gather(csr: CSR, v: torch.Tensor, by_src: bool) -> torch.Tensor:
+    return _Gather.apply(v, csr, by_src)
+
+
+def seg_sum(csr: CSR, x: torch.Tensor) -> torch.Tensor:
+    return _SegSum.apply(x, csr)
+
+
+def seg_max(csr: CSR, x: torch.Tensor) -> torch.Tensor:
+    """Non-differentiable (used on detached logits, like utils/_softmax.py)."""
+    return _seg_max_raw(csr, x.detach())
+
+
+def scatter_src(csr: CSR, x: torch.Tensor) -> torch.Tensor:
+    return _ScatterSrc.apply(x, csr)
+
+
+def edge_softmax_composed(csr: CSR, a_src: torch.Tensor, a_dst: torch.Tensor, slope: float) -> torch.Tensor:
+    """utils/_softmax.py (index branch) over GATConv logits, from primitives."""
+    pre = gather(csr, a_src, by_src=True) + gather(csr, a_dst, by_src=False)
+    e = torch.nn.functional.leaky_relu(pre, slope)
+    m = seg_max(csr, e)
+    p = torch.exp(e - _gather_raw(csr, m, by_src=False))
+    s = seg_sum(csr, p) + SOFTMAX_EPS
+    return p / gather(csr, s, by_src=False)
+
+
+def gat_aggregate_composed(csr, h, a_src, a_dst, bias, slope: float = NEG_SLOPE):
+    alpha = edge_softmax_composed(csr, a_src, a_dst, slope)
+    out = spmm(csr, alpha, h)
+    return out + bias if bias is not None else out
+
+
+# --------------------------------------------------------- fused GATConv
+class _GATAggregate(Function):
+    @staticmethod
+    def forward(ctx, h, a_src, a_dst, bias, csr, slope):
+        h, a_src, a_dst = _f32(h), _f32(a_src), _f32(a_dst)
+        b = _f32(bias) if bias is not None else None
+        require_cuda(h, a_src, a_dst, b)
+        n, c = h.shape
+        if n != csr.num_nodes or a_src.numel() != n or a_dst.numel() != n or (b is not None and b.numel() != c):
+            raise ValueError("gat_aggregate: inconsistent shapes")
+        out = torch.empty_like(h)
+        alpha = torch.empty(csr.num_edges, dtype=torch.float32, device=h.device)
+        check(LIB.vg_gat_fwd(ptr(csr.row_ptr), ptr(csr.col), n, c, ptr(h), ptr(a_src), ptr(a_dst), ptr(b),
+                             float(slope), ptr(out), ptr(alpha), csr.stream()), "vg_gat_fwd")
+        ctx.csr, ctx.slope, ctx.has_bias = csr, slope, bias is not None
+        ctx.save_for_backward(h, a_src, a_dst, bias if bias is not None else h.new_empty(0), alpha)
+        return out
+
+    @staticmethod
+    def backward(ctx, g_out):
+        h, a_src, a_dst, bias, alpha = ctx.saved_tensors
+        csr = ctx.csr
+        if torch.is_grad_enabled():
+            # create_graph=True: differentiate a primitive re-expression of the
+            # forward so the returned gradients carry their own graph.
+            ins = [h, a_src, a_dst] + ([bias] if ctx.has_bias else [])
+            with torch.enable_grad():
+                out = gat_aggregate_composed(csr, h, a_src, a_dst, bias if ctx.has_bias else None, ctx.slope)
+                need = [t for t in ins if t.requires_grad]
+                grads = torch.autograd.grad(out, need, g_out, create_graph=True, allow_unused=True)
+            it = iter(grads)
+            res = [next(it) if t.requires_grad else None for t in ins]
+            if not ctx.has_bias:
+                res.append(None)
+            return res[0], res[1], res[2], res[3], None, None
+        g_out = _f32(g_out)
+        n, c = h.shape
+        dev = h.device
+        g_pre = torch.empty(csr.num_edges, dtype=torch.float32, device=dev)
+        g_h = torch.empty_like(h)
+        g_as = torch.empty(n, dtype=torch.float32, device=dev)
+        g_ad = torch.empty(n, dtype=torch.float32, device=dev)
+        check(LIB.vg_gat_bwd(ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot), ptr(csr.csc_dst),
+                             n, c, ptr(h), ptr(a_src), ptr(a_dst), ptr(alpha), ptr(g_out), float(ctx.slope),
+                             ptr(g_pre), ptr(g_h), ptr(g_as), ptr(g_ad), csr.stream()), "vg_gat_bwd")
+        g_b = g_out.sum(0) if (ctx.has_bias and ctx.needs_input_grad[3]) else None
+        return g_h, g_as.view_as(a_src), g_ad.view_as(a_dst), g_b, None, None
+
+
+def gat_aggregate(csr: CSR, h, a_src, a_dst, bias, slope: float = NEG_SLOPE) -> torch.Tensor:
+    """GATConv (heads=1) attention + aggregation: see ``vg_gat_fwd``."""
+    return _GATAggregate.apply(h, a_src, a_dst, bias, csr, slope)
+
+
+# ------------------------------------------ GraphNorm + ReLU + Dropout
+def graphnorm_relu_dropout_torch(x, weight, bias, mean_scale, keep, eps):
+    """torch expression of the fused op (used only to build the create_graph
+    backward; same formula as torch_geometric GraphNorm, batch=None)."""
+    centred = x - x.mean(dim=0, keepdim=True) * mean_scale
+    z = centred / (centred.std(dim=0, unbiased=False, keepdim=True) + eps) * weight + bias
+    y = torch.relu(z)
+    return y * keep if keep is not None else y
+
+
+class _GraphNormReLUDropout(Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, mean_scale, keep, eps):
+        x = _f32(x)
+        w, b, ms = _f32(weight), _f32(bias), _f32(mean_scale)
+        kp = _f32(keep) if keep is not None else None
+        require_cuda(x, w, b, ms, kp)
+        n, c = x.shape
+        if w.numel() != c or b.numel() != c or ms.numel() != c or (kp is not None and kp.shape != x.shape):
+            raise ValueError("graphnorm: inconsistent shapes")
+        y = torch.empty_like(x)
+        stats = torch.empty(2 * c, dtype=torch.float32, device=x.device)
+        ws = torch.empty(int(LIB.vg_graphnorm_ws_floats(n, c)), dtype=torch.float32, device=x.device)
+        check(LIB.vg_graphnorm_fwd(ptr(x), n, c, ptr(w), ptr(b), ptr(ms), ptr(kp), float(eps), ptr(y), ptr(stats),
+                                   ptr(ws), stream_handle(x.device)), "vg_graphnorm_fwd")
+        ctx.eps, ctx.has_keep = eps, keep is not None
+        ctx.save_for_backward(x, weight, bias, mean_scale, keep if keep is not None else x.new_empty(0), stats)
+        return y
+
+    @staticmethod
+    def backward(ctx, g_y):
+        x, w, b, ms, keep, stats = ctx.saved_tensors
+        kp = keep if ctx.has_keep else None
+        if torch.is_grad_enabled():
+            ins = [x, w, b, ms]
+            with torch.enable_grad():
+                y = graphnorm_relu_dropout_torch(x, w, b, ms, kp, ctx.eps)
+                need = [t for t in ins if t.requires_grad]
+                grads = torch.autograd.grad(y, need, g_y, create_graph=True, allow_unused=True)
+            it = iter(grads)
+            res = [next(it) if t.requires_grad else None for t in ins]
+            return res[0], res[1], res[2], res[3], None, None
+        g_y = _f32(g_y)
+        n, c = x.shape
+        g_x = torch.empty_like(x)
+        g_w = torch.empty(c, dtype=torch.float32, device=x.device)
+        g_b = torch.empty_like(g_w)
+        g_ms = torch.empty_like(g_w)
+        ws = torch.empty(int(LIB.vg_graphnorm_ws_floats(n, c)), dtype=torch.float32, device=x.device)
+        check(LIB.vg_graphnorm_bwd(ptr(x), n, c, ptr(w), ptr(b), ptr(ms), ptr(kp), float(ctx.eps), ptr(stats),
+                                   ptr(g_y), ptr(g_x), ptr(g_w), ptr(g_b), ptr(g_ms), ptr(ws), stream_handle(x.device)),
+              "vg_graphnorm_bwd")
+        return g_x, g_w, g_b, g_ms, None, None
+
+
+def graphnorm_relu_dropout(x, weight, bias, mean_scale, keep: Optional[torch.Tensor], eps: float = 1e-5):
+    return _GraphNormReLUDropout.apply(x, weight, bias, mean_scale, keep, eps)
+
+
+# ------------------------------------------------------ type-matched mean
+def type_mean(local_x: torch.Tensor, local_type: torch.Tensor, voxel_type: torch.Tensor, n_types: int,
+              out: Optional[torch.Tensor] = None, col0: int = 0) -> torch.Tensor:
+    """models.py:122-129 without host syncs (data only, no gradient)."""
+    lx = _f32(local_x)
+    require_cuda(lx, local_type, voxel_type)
+    if local_type.dtype != torch.long or voxel_type.dtype != torch.long:
+        raise TypeError("type tensors must be int64")
+    nl, f = lx.shape
+    nv = voxel_type.numel()
+    if out is None:
+        out = torch.empty(nv, f, dtype=torch.float32, device=lx.device)
+        col0 = 0
+    ws = torch.empty(n_types * (f + 1), dtype=torch.float32, device=lx.device)
+    check(LIB.vg_type_mean(ptr(lx), ptr(local_type.contiguous()), nl, f, ptr(voxel_type.contiguous()), nv,
+                           int(n_types), ptr(out), out.shape[1], int(col0), ptr(ws), stream_handle(lx.device)),
+          "vg_type_mean")
+    return out
+
+
+# ------------------------------------------------------------ Gumbel head
+class _GumbelHead(Function):
+    @staticmethod
+    def forward(ctx, logits, noise, tau):
+        lg, nz = _f32(logits), _f32(noise)
+        require_cuda(lg, nz)
+        if lg.shape != nz.shape or lg.dim() != 2:
+            raise ValueError("gumbel_head: logits and noise must be [N, K]")
+        soft = torch.empty_like(lg)
+        hard = torch.empty_like(lg)
+        check(LIB.vg_gumbel_fwd(ptr(lg), ptr(nz), lg.shape[0], lg.shape[1], float(tau), ptr(soft), ptr(hard), None,
+                                stream_handle(lg.device)), "vg_gumbel_fwd")
+        ctx.tau = tau
+        ctx.save_for_backward(soft)
+        return hard, soft
+
+    @staticmethod
+    def backward(ctx, g_hard, g_soft):
+        (soft,) = ctx.saved_tensors
+        g_logits = torch.empty_like(soft)
+        gh = _f32(g_hard) if g_hard is not None else None
+        gs = _f32(g_soft) if g_soft is not None else None
+        check(LIB.vg_gumbel_bwd(ptr(soft), ptr(gh), ptr(gs), soft.shape[0], soft.shape[1], float(ctx.tau),
+                                ptr(g_logits), stream_handle(soft.device)), "vg_gumbel_bwd")
+        return g_logits, None, None
+
+
+def gumbel_head(logits: torch.Tensor, noise: torch.Tensor, tau: float = 1.0) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(label_hard, label_soft) of models.py:150-153 given Exp(1) noise."""
+    return _GumbelHead.apply(logits, noise, tau)
+
+
+# ------------------------------------------------------- per-building work
+def far_per_graph(x, label, ptr_, site_area, far_col=9, dy_col=4, dx_col=5, dim_scale=11.0, void_class=6):
+    require_cuda(x, label, ptr_, site_area)
+    g = ptr_.numel() - 1
+    gen = torch.empty(g, dtype=torch.float32, device=x.device)
+    ref = torch.empty_like(gen)
+    lbl = _f32(label.detach())
+    check(LIB.vg_far_per_graph(ptr(_f32(x)), x.shape[1], ptr(lbl), lbl.shape[1], ptr(ptr_.contiguous()), g,
+                               ptr(_f32(site_area)), far_col, dy_col, dx_col, float(dim_scale), void_class,
+                               ptr(gen), ptr(ref), stream_handle(x.device)), "vg_far_per_graph")
+    return gen, ref
+
+
+def confusion(truth, label, ptr_):
+    require_cuda(truth, label, ptr_)
+    g = ptr_.numel() - 1
+    k = label.shape[1]
+    conf = torch.empty(g, k, k, dtype=torch.int32, device=label.device)
+    conf_all = torch.empty(k, k, dtype=torch.int32, device=label.device)
+    lbl = _f32(label.detach())
+    check(LIB.vg_confusion(ptr(truth.contiguous()), ptr(lbl), k, ptr(ptr_.contiguous()), g, ptr(conf), ptr(conf_all),
+                           stream_handle(label.device)), "vg_confusion")
+    return conf, conf_all
+
+
+def adam_flat(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step: int):
+    require_cuda(param, grad, exp_avg, exp_avg_sq)
+    bc1 = 1.0 - beta1 ** step
+    bc2 = 1.0 - beta2 ** step
+    check(LIB.vg_adam(ptr(param), ptr(grad), ptr(exp_avg), ptr(exp_avg_sq), param.numel(), float(beta2),
+                      float(1.0 - beta1), float(1.0 - beta2), float(eps), float(weight_decay), float(lr / bc1),
+                      float(bc2 ** 0.5), stream_handle(param.device)), "vg_adam")
+
+
+__all__ = [
+    "CSR", "gat_aggregate", "gat_aggregate_composed", "graphnorm_relu_dropout", "type_mean", "gumbel_head",
+    "spmm", "spmm_t", "sddmm", "gather", "seg_sum", "seg_max", "scatter_src", "far_per_graph", "confusion",
+    "adam_flat", "_lib",
+]

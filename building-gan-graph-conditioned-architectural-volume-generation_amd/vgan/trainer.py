@@ -1,0 +1,262 @@
+"""Trainer with the reference surface plus an explicit, sync-free ``step``.
+
+Mirrors ``building_gan/src/trainer.py``:
+
+* ``Trainer(generator, discriminator, dataloaders, optimizer_generator,
+  optimizer_discriminator, scheduler_generator, configuration, log_dir=None)``
+  (``trainer.py:581-591``), ``.train()`` (``:641``), ``.test(n)`` (``:750``);
+* ``_compute_gradient_penalty`` / ``_compute_discriminator_loss`` /
+  ``_compute_generator_loss`` / ``_compute_metrics`` with the reference's
+  arithmetic (``:291-443``);
+* ``step(local_graph, voxel_graph)`` is the loop body of ``_train_each_epoch``
+  (``:461-502``) factored out: N_CRITIC x {no-grad G forward, D zero_grad,
+  WGAN-GP D loss, backward, Adam} then {G forward, G zero_grad, G loss,
+  backward, Adam}.  It performs no host synchronisation: losses stay on the
+  device until the caller reads them.
+
+Differences that do not change results:
+
+* parameters live in flat buffers, Adam is one kernel (``vgan.flat``); the
+  caller's optimizers are the hyper-parameter source (a scheduler on them keeps
+  working);
+* in the generator iteration the discriminator's parameter gradients are not
+  formed: the reference computes them at ``:492`` and discards them (the next
+  critic iteration zeroes them at ``:475`` before any use);
+* with more than one rank the flat gradients are averaged over RCCL after
+  every backward (``vgan.dist``).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+import time
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import data as vdata
+from . import metrics as vmetrics
+from . import ops
+from .dist import GradSync
+from .flat import FlatAdam, FlatParams
+from .rng import RNG
+
+
+class Trainer:
+    def __init__(self, generator, discriminator, dataloaders, optimizer_generator, optimizer_discriminator,
+                 scheduler_generator, configuration, log_dir: Optional[str] = None):
+        self.generator = generator
+        self.discriminator = discriminator
+        self.dataloaders = dataloaders
+        self.optimizer_generator = optimizer_generator
+        self.optimizer_discriminator = optimizer_discriminator
+        self.scheduler_generator = scheduler_generator
+        self.configuration = configuration
+        self.sanity_checking = getattr(configuration, "SANITY_CHECKING", False)
+        self.log_dir = log_dir or os.path.join(configuration.LOG_DIR,
+                                               datetime.datetime.now().strftime("%m-%d-%Y__%H-%M-%S"))
+        runtime = getattr(configuration, "runtime", {})
+        self.rng = RNG(runtime.get("rng", "device"))
+        generator.rng = self.rng
+        discriminator.rng = self.rng
+        self.flat_g = FlatParams(generator)
+        self.flat_d = FlatParams(discriminator)
+        self.adam_g = FlatAdam.from_optimizer(self.flat_g, optimizer_generator)
+        self.adam_d = FlatAdam.from_optimizer(self.flat_d, optimizer_discriminator)
+        self.sync = GradSync()
+        self.sync.broadcast_params(self.flat_g)
+        self.sync.broadcast_params(self.flat_d)
+        self.skip_dead_d_grads = runtime.get("skip_dead_d_grads", True)
+        self.states = {"epoch_start": 1, "best_f1_score": 0.0}
+
+    # ------------------------------------------------------------- losses
+    def _compute_gradient_penalty(self, local_graph, voxel_graph, label_soft):
+        """trainer.py:291-316."""
+        cfg = self.configuration
+        prep = vdata.prepared(local_graph, voxel_graph, cfg.NUM_CLASSES)
+        n = prep.onehot_f.shape[0]
+        eps = self.rng.uniform((n, 1), label_soft.device)
+        mix = (eps * prep.onehot_f + (1 - eps) * label_soft.squeeze(0)).requires_grad_(True)
+        score = self.discriminator(local_graph, voxel_graph, mix.unsqueeze(0))
+        (grad,) = torch.autograd.grad(score, mix, torch.ones_like(score), create_graph=True, only_inputs=True)
+        return ((grad.norm(dim=1) - 1) ** 2).mean() * cfg.LAMBDA_GP
+
+    def _compute_discriminator_loss(self, local_graph, voxel_graph, label_hard, label_soft):
+        """trainer.py:318-332."""
+        prep = vdata.prepared(local_graph, voxel_graph, self.configuration.NUM_CLASSES)
+        d_real = self.discriminator(local_graph, voxel_graph, prep.onehot_f.unsqueeze(0))
+        d_fake = self.discriminator(local_graph, voxel_graph, label_hard)
+        if self.configuration.USE_WGANGP:
+            d_loss = d_fake.mean() - d_real.mean()
+            return d_loss + self._compute_gradient_penalty(local_graph, voxel_graph, label_soft)
+        return (F.binary_cross_entropy(d_fake, torch.zeros_like(d_fake))
+                + F.binary_cross_entropy(d_real, torch.ones_like(d_real)))
+
+    def _compute_generator_loss(self, local_graph, voxel_graph, logits, label_hard):
+        """trainer.py:334-385 (the per-building FAR loop is one kernel)."""
+        cfg = self.configuration
+        prep = vdata.prepared(local_graph, voxel_graph, cfg.NUM_CLASSES)
+        d_fake = self.discriminator(local_graph, voxel_graph, label_hard)
+        if cfg.USE_WGANGP:
+            adv = -d_fake.mean()
+        else:
+            adv = F.binary_cross_entropy(d_fake, torch.ones_like(d_fake))
+        adv = adv * cfg.LAMBDA_ADV
+        ce = F.cross_entropy(logits, voxel_graph.type) * cfg.LAMBDA_LABEL
+        n = prep.onehot_f.shape[0]
+        hard = label_hard.squeeze(0)
+        ratio_gen = hard.sum(dim=0) / n
+        ratio_ref = prep.onehot_f.sum(dim=0) / n
+        ratio = F.mse_loss(ratio_gen[:-2], ratio_ref[:-2]) * cfg.LAMBDA_RATIO
+        ratio_void = F.mse_loss(ratio_gen[-2:], ratio_ref[-2:]) * cfg.LAMBDA_RATIO_VOID
+        far_gen, far_ref = ops.far_per_graph(prep.voxel_x, hard, voxel_graph.ptr, voxel_graph.site_area,
+                                             far_col=9, dy_col=4, dx_col=5,
+                                             dim_scale=float(cfg.NORMALIZATION_FACTOR_DIMENSION),
+                                             void_class=cfg.VOID)
+        far = F.mse_loss(far_gen, far_ref) * cfg.LAMBDA_FAR  # no gradient, as at trainer.py:380
+        return adv + ratio + ce + ratio_void + far
+
+    def _compute_metrics(self, voxel_graph, label_hard):
+        """trainer.py:387-443 via device confusion matrices (one D2H copy)."""
+        conf, conf_all = ops.confusion(voxel_graph.type, label_hard.squeeze(0), voxel_graph.ptr)
+        return vmetrics.batch_metrics(conf.cpu().numpy(), conf_all.cpu().numpy())
+
+    # --------------------------------------------------------------- step
+    def _generate(self, local_graph, voxel_graph):
+        z = self.rng.normal((1, voxel_graph.num_nodes, self.configuration.Z_DIM), voxel_graph.x.device)
+        logits, hard, soft = self.generator(local_graph, voxel_graph, z)
+        return logits, hard.unsqueeze(0), soft.unsqueeze(0)
+
+    def step(self, local_graph, voxel_graph) -> Dict[str, torch.Tensor]:
+        """One full G+D step (trainer.py:466-495); returns device tensors."""
+        cfg = self.configuration
+        d_losses: List[torch.Tensor] = []
+        for _ in range(cfg.N_CRITIC):
+            with torch.no_grad():
+                _, hard, soft = self._generate(local_graph, voxel_graph)
+            self.adam_d.zero_grad()
+            d_loss = self._compute_discriminator_loss(local_graph, voxel_graph, hard, soft)
+            d_loss.backward()
+            d_losses.append(d_loss.detach())
+            self.sync.all_reduce_grad(self.flat_d)
+            self.adam_d.step()
+
+        logits, hard, soft = self._generate(local_graph, voxel_graph)
+        self.adam_g.zero_grad()
+        d_params = list(self.discriminator.parameters())
+        if self.skip_dead_d_grads:
+            for p in d_params:
+                p.requires_grad_(False)
+        try:
+            g_loss = self._compute_generator_loss(local_graph, voxel_graph, logits, hard)
+            g_loss.backward()
+        finally:
+            if self.skip_dead_d_grads:
+                for p in d_params:
+                    p.requires_grad_(True)
+        self.sync.all_reduce_grad(self.flat_g)
+        self.adam_g.step()
+        return {"d_losses": torch.stack(d_losses), "g_loss": g_loss.detach(), "label_hard": hard.detach()}
+
+    # ------------------------------------------------------ orchestration
+    def _train_each_epoch(self):
+        start = time.time()
+        g_losses, d_losses, f1s, f1_graphs, precs, recs, accs = [], [], [], [], [], [], []
+        for local_graph, voxel_graph in self.dataloaders.train_dataloader:
+            local_graph = local_graph.to(self.configuration.DEVICE)
+            voxel_graph = voxel_graph.to(self.configuration.DEVICE)
+            assert [set(d) for d in local_graph.data_number] == [set(d) for d in voxel_graph.data_number]
+            out = self.step(local_graph, voxel_graph)
+            d_losses.append(out["d_losses"])
+            g_losses.append(out["g_loss"])
+            f1, per_graph, prec, rec, acc = self._compute_metrics(voxel_graph, out["label_hard"])
+            f1s.append(f1)
+            f1_graphs.extend(per_graph)
+            precs.append(prec)
+            recs.append(rec)
+            accs.append(acc)
+        g_mean = torch.stack(g_losses).mean().item()
+        d_mean = torch.cat(d_losses).mean().item()
+        print(f"The function _train_each_epoch took {time.time() - start} seconds to run.")
+        return (g_mean, d_mean, float(np.mean(f1s)), min(f1_graphs), float(np.mean(precs)), float(np.mean(recs)),
+                float(np.mean(accs)))
+
+    @torch.no_grad()
+    def _validate_each_epoch(self):
+        if self.sanity_checking or getattr(self.dataloaders, "validation_dataloader", None) is None:
+            return 0.0, 0.0, 0.0, 0.0, 0.0, 0.0
+        self.generator.eval()
+        self.discriminator.eval()
+        g_losses, f1s, f1_graphs, precs, recs, accs = [], [], [], [], [], []
+        for local_graph, voxel_graph in self.dataloaders.validation_dataloader:
+            local_graph = local_graph.to(self.configuration.DEVICE)
+            voxel_graph = voxel_graph.to(self.configuration.DEVICE)
+            logits, hard, _ = self._generate(local_graph, voxel_graph)
+            g_losses.append(self._compute_generator_loss(local_graph, voxel_graph, logits, hard))
+            f1, per_graph, prec, rec, acc = self._compute_metrics(voxel_graph, hard)
+            f1s.append(f1)
+            f1_graphs.extend(per_graph)
+            precs.append(prec)
+            recs.append(rec)
+            accs.append(acc)
+        self.generator.train()
+        self.discriminator.train()
+        return (torch.stack(g_losses).mean().item(), float(np.mean(f1s)), min(f1_graphs), float(np.mean(precs)),
+                float(np.mean(recs)), float(np.mean(accs)))
+
+    def train(self):
+        """Epoch loop of trainer.py:641-747 (metrics printed; checkpoint on best
+        weighted min-F1 with the reference's states.pt keys)."""
+        cfg = self.configuration
+        best = self.states["best_f1_score"]
+        for epoch in range(self.states["epoch_start"], cfg.EPOCHS + 1):
+            tr = self._train_each_epoch()
+            va = self._validate_each_epoch()
+            score = tr[3] * cfg.F1_SCORE_TRAIN_WEIGHT + va[2] * cfg.F1_SCORE_VALIDATION_WEIGHT
+            print(f"epoch {epoch}: g_loss {tr[0]:.5f} d_loss {tr[1]:.5f} f1 {tr[2]:.4f} f1_val {va[1]:.4f}")
+            if best < score:
+                best = score
+                if not self.sanity_checking:
+                    self.save_checkpoint(epoch, best)
+            if self.scheduler_generator is not None:
+                self.scheduler_generator.step()
+
+    def save_checkpoint(self, epoch: int, best: float) -> str:
+        os.makedirs(self.log_dir, exist_ok=True)
+        path = os.path.join(self.log_dir, "states.pt")
+        torch.save({
+            "epoch_start": epoch,
+            "epoch_end": self.configuration.EPOCHS + 1,
+            "best_f1_score": best,
+            "generator": self.generator.state_dict(),
+            "discriminator": self.discriminator.state_dict(),
+            "optimizer_generator_flat": self.adam_g.state_dict_flat(),
+            "optimizer_discriminator_flat": self.adam_d.state_dict_flat(),
+        }, path)
+        return path
+
+    @torch.no_grad()
+    def test(self, num_samples_to_viz: int = 0):
+        """trainer.py:749-795 metrics (visualisation is out of scope)."""
+        self.generator.eval()
+        self.discriminator.eval()
+        f1s, f1_graphs, precs, recs, accs = [], [], [], [], []
+        for local_graph, voxel_graph in self.dataloaders.test_dataloader:
+            local_graph = local_graph.to(self.configuration.DEVICE)
+            voxel_graph = voxel_graph.to(self.configuration.DEVICE)
+            _, hard, _ = self._generate(local_graph, voxel_graph)
+            f1, per_graph, prec, rec, acc = self._compute_metrics(voxel_graph, hard)
+            f1s.append(f1)
+            f1_graphs.extend(per_graph)
+            precs.append(prec)
+            recs.append(rec)
+            accs.append(acc)
+        self.generator.train()
+        self.discriminator.train()
+        result = {"f1_score_test": float(np.mean(f1s)), "f1_score_min_test": min(f1_graphs),
+                  "precision_score_test": float(np.mean(precs)), "recall_score_test": float(np.mean(recs)),
+                  "accuracy_score_test": float(np.mean(accs))}
+        print(result)
+        return result

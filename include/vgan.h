@@ -1,0 +1,178 @@
+/*
+ * vgan -- C ABI of the MI355X-native voxel-graph GAN message-passing core.
+ *
+ * libvgan_hip.so (gfx950) exports exactly these functions.  They replace the
+ * torch-geometric 2.6.1 operator calls the reference issues from
+ * building_gan/src/models.py (paths below are relative to /root/reference) and
+ * the per-step device work of building_gan/src/trainer.py.
+ *
+ * Conventions (all functions):
+ *   - every pointer is a DEVICE pointer unless named host_*; tensors are
+ *     contiguous row-major; features f32; CSR indices int32; edge_index int64;
+ *   - the caller allocates every output and workspace (query the *_ws_* sizes);
+ *     no function allocates, frees or synchronises, so all are capturable in a
+ *     hipGraph;
+ *   - work is enqueued on `stream` (hipStream_t passed as void*);
+ *   - return 0 on success, a hipError_t value on a launch failure, or
+ *     VG_EINVAL for an invalid argument (checked on the host before launch).
+ *
+ * CSR layout ("destination CSR"): row i lists the incoming edges of node i in
+ * original edge order with the self loop LAST -- exactly the edge order of
+ * GATConv after remove_self_loops + add_self_loops -- so the per-row sums run
+ * in the order torch-geometric's scatter would.  The "source CSC" is its
+ * transpose: for source node j, the CSR slots k with col[k] == j (ascending k).
+ */
+#ifndef VGAN_H_
+#define VGAN_H_
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VG_EINVAL (-1)
+
+/* ---- graph structure ---------------------------------------------------- */
+
+/* Workspace (int32 elements) needed by vg_csr_build. */
+int64_t vg_csr_ws_ints(int64_t num_edges, int32_t num_nodes);
+
+/* Build destination CSR (+1 self loop per node, input self loops dropped) and
+ * its source CSC from edge_index [2, E] int64.
+ * Replaces: GATConv.forward's remove_self_loops/add_self_loops, run on every
+ * call of every layer (models.py:144,242 -> torch_geometric/nn/conv/gat_conv.py)
+ * -- here once per mini-batch.
+ * Outputs: row_ptr[N+1], col[E+N], csc_ptr[N+1], csc_slot[E+N], csc_dst[E+N]
+ * (sized for the worst case; the used length E' is written to status[0]);
+ * status[1] != 0 flags an out-of-range node index. */
+int vg_csr_build(const int64_t* edge_index, int64_t num_edges, int32_t num_nodes,
+                 int32_t* row_ptr, int32_t* col, int32_t* csc_ptr, int32_t* csc_slot,
+                 int32_t* csc_dst, int32_t* workspace, int32_t* status, void* stream);
+
+/* ---- GATConv(heads=1) message passing ----------------------------------- */
+
+/* Fused attention + aggregation for one GATConv layer:
+ *   e_k   = leaky_relu(a_src[col_k] + a_dst[i], slope)
+ *   alpha = segment softmax of e over row i  (max-shifted, denominator + 1e-16)
+ *   out_i = sum_k alpha_k * h[col_k] + bias
+ * Replaces GATConv.edge_update (utils/_softmax.py scatter max/sum) +
+ * propagate/message/aggregate ('add' scatter) + bias, as called from
+ * models.py:144 (generator, 14 layers) and models.py:242 (discriminator, 6).
+ * alpha (E') is written when non-NULL (kept for the backward); bias may be NULL. */
+int vg_gat_fwd(const int32_t* row_ptr, const int32_t* col, int32_t num_nodes, int32_t channels,
+               const float* h, const float* a_src, const float* a_dst, const float* bias,
+               float slope, float* out, float* alpha, void* stream);
+
+/* First-order backward of vg_gat_fwd (the autograd path without create_graph):
+ *   g_pre[E'], g_a_dst[N]   (row pass)     and
+ *   g_h[N,C],  g_a_src[N]   (source pass over the CSC; no atomics). */
+int vg_gat_bwd(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,
+               const int32_t* csc_slot, const int32_t* csc_dst, int32_t num_nodes,
+               int32_t channels, const float* h, const float* a_src, const float* a_dst,
+               const float* alpha, const float* g_out, float slope, float* g_pre,
+               float* g_h, float* g_a_src, float* g_a_dst, void* stream);
+
+/* Differentiable sparse primitives (their adjoints are each other), used to
+ * build the twice-differentiable path the WGAN-GP needs (trainer.py:306-312,
+ * create_graph=True):
+ *   vg_spmm      Y_i = sum_{k in row i} w_k X[col_k]              [N,C]
+ *   vg_spmm_t    Z_j = sum_{k: col_k = j} w_k G[dst_k]            [N,C]
+ *   vg_sddmm     e_k = <A[dst_k], B[col_k]>                       [E']
+ *   vg_seg_sum   s_i = sum_{k in row i} x_k                       [N]
+ *   vg_seg_max   m_i = max_{k in row i} x_k                       [N]
+ *   vg_gather    e_k = v[col_k] (by_src=1) or v[dst_k] (by_src=0) [E']
+ *   vg_scatter_src  s_j = sum_{k: col_k = j} x_k                  [N]      */
+int vg_spmm(const int32_t* row_ptr, const int32_t* col, int32_t num_nodes, int32_t channels,
+            const float* w, const float* x, float* y, void* stream);
+int vg_spmm_t(const int32_t* csc_ptr, const int32_t* csc_slot, const int32_t* csc_dst,
+              int32_t num_nodes, int32_t channels, const float* w, const float* g, float* z,
+              void* stream);
+int vg_sddmm(const int32_t* row_ptr, const int32_t* col, int32_t num_nodes, int32_t channels,
+             const float* a, const float* b, float* e, void* stream);
+int vg_seg_sum(const int32_t* row_ptr, int32_t num_nodes, const float* x, float* s, void* stream);
+int vg_seg_max(const int32_t* row_ptr, int32_t num_nodes, const float* x, float* m, void* stream);
+int vg_gather(const int32_t* row_ptr, const int32_t* col, int32_t num_nodes, int32_t by_src,
+              const float* v, float* e, void* stream);
+int vg_scatter_src(const int32_t* csc_ptr, const int32_t* csc_slot, int32_t num_nodes,
+                   const float* x, float* s, void* stream);
+
+/* ---- GraphNorm(batch=None) + ReLU + Dropout ----------------------------- */
+
+/* Workspace (floats) for vg_graphnorm_fwd / _bwd. */
+int64_t vg_graphnorm_ws_floats(int32_t num_nodes, int32_t channels);
+
+/* y = keep * relu(weight * (x - mean_scale*mu) / (sigma + eps) + bias)
+ * with mu, sigma the population column statistics over all N rows.
+ * Replaces GraphNorm(x) (torch_geometric/nn/norm/graph_norm.py, batch=None) ->
+ * nn.ReLU(True) -> nn.Dropout(0.2) at models.py:73-75,83-85,193-195,203-205.
+ * keep (N*C, already scaled by 1/(1-p)) may be NULL (eval / no dropout).
+ * stats (2C) receives [mu | sigma]. */
+int vg_graphnorm_fwd(const float* x, int32_t num_nodes, int32_t channels, const float* weight,
+                     const float* bias, const float* mean_scale, const float* keep, float eps,
+                     float* y, float* stats, float* workspace, void* stream);
+
+/* First-order backward.  g_w / g_b / g_ms are [C]. */
+int vg_graphnorm_bwd(const float* x, int32_t num_nodes, int32_t channels, const float* weight,
+                     const float* bias, const float* mean_scale, const float* keep, float eps,
+                     const float* stats, const float* g_y, float* g_x, float* g_w, float* g_b,
+                     float* g_ms, float* workspace, void* stream);
+
+/* ---- program <-> voxel type-matched mean ("cross-graph pointer") -------- */
+
+/* For every voxel v: out[v, col0 : col0+F] = mean of local_x rows whose
+ * local_type == voxel_type[v] over the whole mini-batch, or 0 when no program
+ * node has that type.  Replaces the host-synchronising loop at
+ * models.py:122-129 (generator) and models.py:230-237 (discriminator).
+ * out has row stride out_stride (lets the caller write straight into a
+ * concatenated feature matrix).  workspace: n_types*(F+1) floats. */
+int vg_type_mean(const float* local_x, const int64_t* local_type, int32_t n_local, int32_t feat,
+                 const int64_t* voxel_type, int32_t n_voxel, int32_t n_types, float* out,
+                 int32_t out_stride, int32_t out_col0, float* workspace, void* stream);
+
+/* ---- Gumbel-softmax type head ------------------------------------------- */
+
+/* soft = softmax((logits - log(noise)) / tau) per row (noise ~ Exp(1));
+ * idx = first argmax; hard = (onehot(idx) - soft) + soft (straight-through).
+ * Replaces F.gumbel_softmax(logits, tau=1.0) + scatter one-hot + ST at
+ * models.py:150-153.  idx may be NULL. */
+int vg_gumbel_fwd(const float* logits, const float* noise, int32_t rows, int32_t classes,
+                  float tau, float* soft, float* hard, int32_t* idx, void* stream);
+
+/* g_logits = soft * (g - sum(soft*g)) / tau with g = g_hard + g_soft (either NULL = 0). */
+int vg_gumbel_bwd(const float* soft, const float* g_hard, const float* g_soft, int32_t rows,
+                  int32_t classes, float tau, float* g_logits, void* stream);
+
+/* ---- per-building reductions for the generator loss / metrics ----------- */
+
+/* For each building g (rows ptr[g]..ptr[g+1]):
+ *   far_ref[g] = x[ptr[g], far_col]
+ *   far_gen[g] = sum_{argmax(label_row) != void} (x[:,dy]*dim_scale)*(x[:,dx]*dim_scale)
+ *                / site_area[ptr[g]]
+ * Replaces the per-graph Python loop at trainer.py:357-378. */
+int vg_far_per_graph(const float* x, int32_t x_stride, const float* label, int32_t classes,
+                     const int64_t* ptr, int32_t num_graphs, const float* site_area,
+                     int32_t far_col, int32_t dy_col, int32_t dx_col, float dim_scale,
+                     int32_t void_class, float* far_gen, float* far_ref, void* stream);
+
+/* Confusion matrices for the metrics (trainer.py:387-443): conf[g][t][p] counts
+ * (truth t, prediction argmax(label_row)) per building; conf_all sums them. */
+int vg_confusion(const int64_t* truth, const float* label, int32_t classes, const int64_t* ptr,
+                 int32_t num_graphs, int32_t* conf, int32_t* conf_all, void* stream);
+
+/* ---- optimiser ---------------------------------------------------------- */
+
+/* torch.optim.Adam (single-tensor semantics, weight_decay, no amsgrad) over one
+ * flat parameter buffer -- the optimizer.step() of trainer.py:481,495.
+ * one_minus_beta1/2, step_size = lr / (1 - beta1^t) and bc2_sqrt =
+ * sqrt(1 - beta2^t) are computed by the caller in double precision and rounded
+ * to float, exactly as torch passes them to its kernels. */
+int vg_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+            float beta2, float one_minus_beta1, float one_minus_beta2, float eps,
+            float weight_decay, float step_size, float bc2_sqrt, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VGAN_H_ */

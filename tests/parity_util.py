@@ -1,0 +1,146 @@
+"""Shared helpers for the parity tests and ``__graft_entry__.smoke``.
+
+Fixtures (``tests/golden/*.pt``) hold collated batch tensors; these helpers
+rebuild both an oracle (reference-style) batch and a ``vgan.GraphBatch`` from
+them so the HIP path and the CPU oracle see identical inputs.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+PKG_ROOT = os.path.join(ROOT, "building-gan-graph-conditioned-architectural-volume-generation_amd")
+for p in (ROOT, PKG_ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(HERE, "golden")
+
+
+def load_fixture(name: str):
+    return torch.load(os.path.join(GOLDEN, name), weights_only=True, map_location="cpu")
+
+
+def _split(b):
+    vp, lp = b["voxel_ptr"].tolist(), b["local_ptr"].tolist()
+    vei = b["voxel_edge_index"]
+    graphs = []
+    for g in range(len(vp) - 1):
+        lo, hi = vp[g], vp[g + 1]
+        keep = (vei[0] >= lo) & (vei[0] < hi)
+        l_lo, l_hi = lp[g], lp[g + 1]
+        graphs.append(dict(
+            voxel=dict(x=b["voxel_x"][lo:hi], edge_index=vei[:, keep] - lo, type=b["voxel_type"][lo:hi],
+                       types_onehot=b["voxel_types_onehot"][lo:hi], site_area=b["voxel_site_area"][lo:hi],
+                       data_number=[str(g)] * (hi - lo)),
+            local=dict(x=b["local_x"][l_lo:l_hi], type=b["local_type"][l_lo:l_hi],
+                       data_number=[str(g)] * (l_hi - l_lo)),
+        ))
+    return graphs
+
+
+def oracle_batches(b):
+    from oracle import pyg
+
+    gs = _split(b)
+    return (pyg.Batch.from_data_list([pyg.Data(**g["local"]) for g in gs]),
+            pyg.Batch.from_data_list([pyg.Data(**g["voxel"]) for g in gs]))
+
+
+def vgan_batches(b, device="cuda"):
+    from vgan.graph import GraphBatch, GraphData
+
+    gs = _split(b)
+    loc = GraphBatch.from_data_list([GraphData(**g["local"]) for g in gs])
+    vox = GraphBatch.from_data_list([GraphData(**g["voxel"]) for g in gs])
+    return loc.to(device), vox.to(device)
+
+
+def batches_from_items(items, device="cuda"):
+    """synthetic (local, voxel) GraphData pairs -> (oracle pair, vgan pair)."""
+    from oracle import pyg
+    from vgan.graph import GraphBatch
+
+    keys_v = ("x", "edge_index", "type", "types_onehot", "site_area", "data_number")
+    keys_l = ("x", "type", "data_number")
+    ol = pyg.Batch.from_data_list([pyg.Data(**{k: getattr(l, k) for k in keys_l}) for l, _ in items])
+    ov = pyg.Batch.from_data_list([pyg.Data(**{k: getattr(v, k) for k in keys_v}) for _, v in items])
+    vl = GraphBatch.from_data_list([l for l, _ in items]).to(device)
+    vv = GraphBatch.from_data_list([v for _, v in items]).to(device)
+    return (ol, ov), (vl, vv)
+
+
+def tiny_config(cfg):
+    cfg.GENERATOR_HIDDEN_DIM = 16
+    cfg.GENERATOR_ENCODER_REPEAT = 2
+    cfg.LOCAL_ENCODER_HIDDEN_DIM = 16
+    cfg.LOCAL_GRAPH_ENCODER_REPEAT = 1
+    cfg.GENERATOR_MLP_ENCODER_REPEAT = 1
+    cfg.DISCRIMINATOR_HIDDEN_DIM = 16
+    cfg.DISCRIMINATOR_ENCODER_REPEAT = 2
+    cfg.Z_DIM = 8
+    return cfg
+
+
+def rel_err(a: torch.Tensor, b: torch.Tensor) -> float:
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def run_smoke() -> None:
+    """One small G forward + D WGAN-GP loss backward on cuda:0 vs the oracle."""
+    from oracle import reference as R
+    from vgan.config import Configuration
+    from vgan.models import VoxelGNNDiscriminator, VoxelGNNGenerator
+    from vgan.trainer import Trainer
+
+    f = load_fixture("forward_eval.pt")
+    cfg = Configuration()
+    cfg.DEVICE = "cuda"
+    G = VoxelGNNGenerator(cfg, 17, 12)
+    D = VoxelGNNDiscriminator(cfg, 17, 12)
+    G.load_state_dict(f["G"])
+    D.load_state_dict(f["D"])
+    G.eval()
+    D.eval()
+    loc, vox = vgan_batches(f["batch"])
+    z = f["z"].cuda()
+    noise = f["gumbel_noise"].cuda()
+    with torch.no_grad():
+        logits, hard, soft = G(loc, vox, z, noise=noise)
+    torch.cuda.synchronize()
+    err = (logits.cpu() - f["logits"]).abs().max().item()
+    if not err <= 1e-3:
+        raise AssertionError(f"smoke: generator logits differ from the reference by {err}")
+    tr = Trainer(G, D, None, None, None, None, cfg)
+    tr.rng = _FixedUniform(f["gp_eps"].cuda())
+    d_loss = tr._compute_discriminator_loss(loc, vox, hard.unsqueeze(0), soft.unsqueeze(0))
+    tr.adam_d.zero_grad()
+    d_loss.backward()
+    torch.cuda.synchronize()
+    if abs(d_loss.item() - float(f["d_loss"])) > 1e-3 * max(1.0, abs(float(f["d_loss"]))):
+        raise AssertionError(f"smoke: d_loss {d_loss.item()} vs reference {float(f['d_loss'])}")
+    worst = max(rel_err(p.grad, f["d_grads"][k]) for k, p in D.named_parameters())
+    if worst > 1e-3:
+        raise AssertionError(f"smoke: D gradient rel err {worst}")
+    print(f"smoke ok: logits max|err| {err:.2e}, d_loss {d_loss.item():.6f}, D grad rel err {worst:.2e}")
+    del R
+
+
+class _FixedUniform:
+    """RNG stand-in that hands out a fixed GP eps (everything else unused in eval)."""
+
+    def __init__(self, eps):
+        self.eps = eps
+
+    def uniform(self, shape, device):
+        assert tuple(shape) == tuple(self.eps.shape)
+        return self.eps
+
+    def keep_mask(self, *a, **k):
+        raise AssertionError("eval mode draws no dropout masks")

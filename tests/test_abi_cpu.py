@@ -1,0 +1,64 @@
+"""The C-ABI library loads and exports exactly what include/vgan.h declares
+(no compute calls: this runs without a GPU)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from parity_util import PKG_ROOT, ROOT
+
+HEADER = os.path.join(ROOT, "include", "vgan.h")
+LIB = os.path.join(PKG_ROOT, "vgan", "libvgan_hip.so")
+
+
+def header_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(vg_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_functions():
+    syms = header_symbols()
+    assert "vg_gat_fwd" in syms and "vg_csr_build" in syms and len(syms) >= 20
+
+
+def test_library_exports_every_header_symbol():
+    assert os.path.exists(LIB), "run __graft_entry__.build() first"
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (vg_[a-z0-9_]+)$", out, flags=re.M))
+    missing = [s for s in header_symbols() if s not in exported]
+    assert not missing, missing
+    lib = ctypes.CDLL(LIB)
+    for s in header_symbols():
+        assert hasattr(lib, s)
+
+
+def test_binding_table_matches_header():
+    from vgan import _lib
+
+    assert sorted(_lib.SIGNATURES) == header_symbols()
+
+
+def test_library_is_gfx950_code_object():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-S", LIB], capture_output=True, text=True).stdout
+    assert ".hip_fatbin" in out
+    blob = open(LIB, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_workspace_queries_are_host_only():
+    from vgan._lib import LIB as lib
+
+    assert lib.vg_csr_ws_ints(100, 10) == 4 * 10 + 100 + 10
+    assert lib.vg_graphnorm_ws_floats(1000, 16) >= 2 * 16
+
+
+def test_ops_refuse_cpu_tensors():
+    import torch
+
+    from vgan import ops
+
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        ops.CSR(torch.zeros(2, 3, dtype=torch.long), 4)

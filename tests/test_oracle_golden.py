@@ -1,0 +1,135 @@
+"""The CPU oracle against fixtures produced by EXECUTING the reference code.
+
+The fixtures (tests/golden/make_golden.py) come from the reference's own
+models.py / trainer.py run on the CPU; these tests pin the oracle's restatement
+of the reference orchestration bit-for-bit, and cross-check the restated
+torch-geometric operators against an independent dense derivation.
+"""
+import pytest
+import torch
+
+from oracle import dense, pyg
+from oracle import reference as R
+from parity_util import load_fixture, oracle_batches, tiny_config
+from vgan.config import Configuration
+
+
+def _run_step(name):
+    f = load_fixture(name)
+    cfg = Configuration(sanity_checking=(name == "step_sanity.pt"))
+    if name == "step_tiny.pt":
+        tiny_config(cfg)
+    local, voxel = oracle_batches(f["batch"])
+    G, D = R.Generator(cfg), R.Discriminator(cfg)
+    G.load_state_dict(f["G0"])
+    D.load_state_dict(f["D0"])
+    og = torch.optim.Adam(G.parameters(), lr=cfg.LEARNING_RATE_GENERATOR, betas=cfg.BETAS)
+    od = torch.optim.Adam(D.parameters(), lr=cfg.LEARNING_RATE_DISCRIMINATOR, betas=cfg.BETAS)
+    torch.manual_seed(int(f["step_seed"]))
+    out = R.train_step(G, D, og, od, cfg, local, voxel, with_metrics=True)
+    return f, out, G, D
+
+
+@pytest.mark.parametrize("name", ["step_sanity.pt", "step_tiny.pt"])
+def test_oracle_step_matches_reference_bitwise(name):
+    f, out, G, D = _run_step(name)
+    assert out["d_losses"] == f["d_losses"].tolist()
+    assert out["g_loss"] == float(f["g_loss"][0])
+    for k, v in f["G1"].items():
+        assert torch.equal(G.state_dict()[k], v), k
+    for k, v in f["D1"].items():
+        assert torch.equal(D.state_dict()[k], v), k
+    f1, per_graph, prec, rec, acc = out["metrics"]
+    ref = f["epoch_result"].tolist()
+    # the reference averages through torch.tensor(list).mean() -> float32 rounding
+    assert f1 == pytest.approx(ref[2], rel=1e-6)
+    assert min(per_graph) == pytest.approx(ref[3], rel=1e-12)
+    assert (prec, rec, acc) == pytest.approx(tuple(ref[4:7]), abs=1e-7)
+
+
+def test_oracle_forward_eval_matches_reference():
+    f = load_fixture("forward_eval.pt")
+    cfg = Configuration()
+    local, voxel = oracle_batches(f["batch"])
+    G, D = R.Generator(cfg), R.Discriminator(cfg)
+    G.load_state_dict(f["G"])
+    D.load_state_dict(f["D"])
+    G.eval()
+    D.eval()
+    with torch.no_grad():
+        logits, hard, soft = G(local, voxel, f["z"], noise=f["gumbel_noise"])
+    assert torch.equal(logits, f["logits"])
+    assert torch.equal(soft, f["label_soft"])
+    assert torch.equal(hard, f["label_hard"])
+    D.zero_grad()
+    d_real = D(local, voxel, voxel.types_onehot.unsqueeze(0))
+    d_fake = D(local, voxel, hard.unsqueeze(0))
+    d_loss = d_fake.mean() - d_real.mean() + R.gradient_penalty(D, cfg, local, voxel, soft.unsqueeze(0),
+                                                                 eps=f["gp_eps"])
+    d_loss.backward()
+    assert torch.equal(d_loss.detach(), f["d_loss"])
+    for k, p in D.named_parameters():
+        assert torch.equal(p.grad, f["d_grads"][k]), k
+
+
+@pytest.mark.parametrize("idx", range(6))
+def test_oracle_gat_matches_fixture_and_dense(idx):
+    f = load_fixture("ops_small.pt")
+    g = f["gat"][idx]
+    _, voxel = oracle_batches(f["batch"])
+    cin, cout = g["x"].shape[1], g["out"].shape[1]
+    conv = pyg.GATConv(cin, cout).double()
+    with torch.no_grad():
+        conv.lin.weight.copy_(g["lin_weight"].double())
+        conv.att_src.copy_(g["att_src"].double())
+        conv.att_dst.copy_(g["att_dst"].double())
+        conv.bias.copy_(g["bias"].double())
+    x = g["x"].double()
+    y = conv(x, voxel.edge_index)
+    assert torch.allclose(y.float(), g["out"], atol=1e-6)
+    yd, p = dense.gat_dense(x, conv.lin.weight, conv.att_src, conv.att_dst, conv.bias, voxel.edge_index)
+    assert torch.allclose(y, yd, atol=1e-10)
+    assert torch.allclose(p.sum(1), torch.ones(p.shape[0], dtype=p.dtype))
+
+
+def test_oracle_graphnorm_matches_dense_and_zero_variance():
+    f = load_fixture("ops_small.pt")["graphnorm"]
+    gn = pyg.GraphNorm(16).double()
+    with torch.no_grad():
+        gn.weight.copy_(f["weight"].double())
+        gn.bias.copy_(f["bias"].double())
+        gn.mean_scale.copy_(f["mean_scale"].double())
+    x = f["x"].double().requires_grad_(True)
+    y = gn(x)
+    assert torch.allclose(y.float(), f["out"], atol=1e-5)
+    assert torch.allclose(y, dense.graphnorm_dense(x, gn.weight, gn.bias, gn.mean_scale), atol=1e-10)
+    # a constant column: std 0 -> torch masks the std gradient to 0 (finite grads)
+    xc = torch.randn(50, 3, dtype=torch.float64)
+    xc[:, 1] = 2.5
+    xc.requires_grad_(True)
+    gn3 = pyg.GraphNorm(3).double()
+    gn3(xc).sum().backward()
+    assert torch.isfinite(xc.grad).all()
+
+
+def test_oracle_type_mean_fixture():
+    f = load_fixture("ops_small.pt")
+    local, voxel = oracle_batches(f["batch"])
+    got = R.type_matched_mean(local.x, local.type, voxel.type)
+    assert torch.equal(got, f["type_mean"])
+    # voxels of a type with no program node (VOID = 6 never appears in programs) stay 0
+    assert (got[voxel.type == 6] == 0).all()
+
+
+def test_configuration_matches_reference_values():
+    ref = load_fixture("step_sanity.pt")["config"]
+    cfg = Configuration(sanity_checking=True)
+    cfg.DATA_POINT = 4001
+    mine = cfg.to_dict()
+    skip = {"DATA_PATH", "GLOBAL_GRAPH_DATA_PATH", "LOCAL_GRAPH_DATA_PATH", "VOXEL_GRAPH_DATA_PATH",
+            "SAVE_DATA_PATH", "LOG_DIR", "DEVICE"}
+    for k, v in ref.items():
+        if k in skip:
+            continue
+        assert k in mine, k
+        assert mine[k] == v, (k, mine[k], v)
