@@ -261,6 +261,23 @@ def edge_softmax_composed(csr: CSR, a_src: torch.Tensor, a_dst: torch.Tensor, sl
     return p / gather(csr, s, by_src=False)
 
 
+def _gat_backward_composed(csr, h, a_src, a_dst, g_out, slope: float):
+    """d(out)/d(h, a_src, a_dst) applied to g_out, from differentiable primitives:
+        ga_k = <g_out[dst_k], h[src_k]>            (sddmm)
+        g_h  = spmm_t(alpha, g_out)
+        ge_k = alpha_k (ga_k - sum_{row} alpha ga)  (segment-softmax adjoint)
+        gp_k = ge_k * lrelu'(pre_k)
+        g_a_src = scatter_src(gp), g_a_dst = seg_sum(gp)."""
+    alpha = edge_softmax_composed(csr, a_src, a_dst, slope)
+    ga = sddmm(csr, g_out, h)
+    g_h = spmm_t(csr, alpha, g_out)
+    t = seg_sum(csr, alpha * ga)
+    ge = alpha * (ga - gather(csr, t, by_src=False))
+    pre = _gather_raw(csr, a_src.detach(), True) + _gather_raw(csr, a_dst.detach(), False)
+    gp = ge * torch.where(pre > 0, torch.ones_like(pre), torch.full_like(pre, slope))
+    return g_h, scatter_src(csr, gp), seg_sum(csr, gp)
+
+
 def gat_aggregate_composed(csr, h, a_src, a_dst, bias, slope: float = NEG_SLOPE):
     alpha = edge_softmax_composed(csr, a_src, a_dst, slope)
     out = spmm(csr, alpha, h)
@@ -290,18 +307,14 @@ class _GATAggregate(Function):
         h, a_src, a_dst, bias, alpha = ctx.saved_tensors
         csr = ctx.csr
         if torch.is_grad_enabled():
-            # create_graph=True: differentiate a primitive re-expression of the
-            # forward so the returned gradients carry their own graph.
-            ins = [h, a_src, a_dst] + ([bias] if ctx.has_bias else [])
-            with torch.enable_grad():
-                out = gat_aggregate_composed(csr, h, a_src, a_dst, bias if ctx.has_bias else None, ctx.slope)
-                need = [t for t in ins if t.requires_grad]
-                grads = torch.autograd.grad(out, need, g_out, create_graph=True, allow_unused=True)
-            it = iter(grads)
-            res = [next(it) if t.requires_grad else None for t in ins]
-            if not ctx.has_bias:
-                res.append(None)
-            return res[0], res[1], res[2], res[3], None, None
+            # create_graph=True: the same backward formulas as vg_gat_bwd, written
+            # with the differentiable primitives on the saved inputs (alpha is
+            # recomputed from a_src / a_dst so its dependence on them is kept).
+            # autograd.grad on a re-run forward would double count: a_src and
+            # a_dst are themselves functions of h (a = h @ att).
+            g_h, g_as, g_ad = _gat_backward_composed(csr, h, a_src, a_dst, g_out, ctx.slope)
+            g_b = g_out.sum(0) if ctx.has_bias else None
+            return g_h, g_as.view_as(a_src), g_ad.view_as(a_dst), g_b, None, None
         g_out = _f32(g_out)
         n, c = h.shape
         dev = h.device

@@ -92,6 +92,26 @@ def rel_err(a: torch.Tensor, b: torch.Tensor) -> float:
     return float((a - b).norm() / b.norm().clamp_min(1e-30))
 
 
+def grads_close(got: dict, ref: dict, rtol: float = 1e-3, floor: float = 1e-6):
+    """Per-parameter gradient check with a floor tied to the whole gradient's
+    norm: parameters whose exact gradient is 0 (a GATConv bias or att_dst
+    feeding a GraphNorm / softmax that cancels it) carry only ~1e-10 rounding
+    noise on both sides, so a pure relative test is meaningless for them.
+    Returns (ok, worst_param, concatenated relative error)."""
+    keys = [k for k in ref if ref[k] is not None]
+    r_all = torch.cat([ref[k].double().reshape(-1) for k in keys])
+    g_all = torch.cat([got[k].detach().double().cpu().reshape(-1) for k in keys])
+    scale = float(r_all.norm())
+    worst, worst_k = 0.0, None
+    for k in keys:
+        d = float((got[k].detach().double().cpu() - ref[k].double()).norm())
+        lim = rtol * float(ref[k].double().norm()) + floor * scale
+        if d / lim > worst:
+            worst, worst_k = d / lim, k
+    total = float((g_all - r_all).norm() / max(scale, 1e-30))
+    return worst <= 1.0 and total <= rtol, worst_k, total
+
+
 def run_smoke() -> None:
     """One small G forward + D WGAN-GP loss backward on cuda:0 vs the oracle."""
     from oracle import reference as R
@@ -125,10 +145,10 @@ def run_smoke() -> None:
     torch.cuda.synchronize()
     if abs(d_loss.item() - float(f["d_loss"])) > 1e-3 * max(1.0, abs(float(f["d_loss"]))):
         raise AssertionError(f"smoke: d_loss {d_loss.item()} vs reference {float(f['d_loss'])}")
-    worst = max(rel_err(p.grad, f["d_grads"][k]) for k, p in D.named_parameters())
-    if worst > 1e-3:
-        raise AssertionError(f"smoke: D gradient rel err {worst}")
-    print(f"smoke ok: logits max|err| {err:.2e}, d_loss {d_loss.item():.6f}, D grad rel err {worst:.2e}")
+    ok, worst_k, total = grads_close({k: p.grad for k, p in D.named_parameters()}, f["d_grads"])
+    if not ok:
+        raise AssertionError(f"smoke: D gradients differ (worst {worst_k}, total rel err {total})")
+    print(f"smoke ok: logits max|err| {err:.2e}, d_loss {d_loss.item():.6f}, D grad rel err {total:.2e}")
     del R
 
 

@@ -100,7 +100,8 @@ def test_gat_double_backward(cuda, C):
         out = fn(*tensors)
         g = torch.autograd.grad((out * w1).sum(), tensors, create_graph=True)
         s = sum((gi * wi).sum() for gi, wi in zip(g, w2))
-        return torch.autograd.grad(s, tensors)
+        res = torch.autograd.grad(s, tensors, allow_unused=True)
+        return [torch.zeros_like(t) if r is None else r for r, t in zip(res, tensors)]
 
     ref_t = [t.clone().requires_grad_(True) for t in base]
     ref = second_order(lambda h, a, d, b: pyg.gat_propagate(h, a, d, vox.edge_index) + b, ref_t, w1, w2)
@@ -109,6 +110,47 @@ def test_gat_double_backward(cuda, C):
                        [w.float().to(cuda) for w in w2])
     for g, r in zip(got, ref):
         assert rel_err(g, r) < 1e-4
+
+
+@pytest.mark.parametrize("C", [1, 16, 64])
+def test_gat_layer_double_backward_through_projection(cuda, C):
+    """a_src = h @ att_src inside the graph (as in GATConv): second-order grads
+    w.r.t. x and every parameter vs the oracle GATConv in float64."""
+    torch.manual_seed(11 + C)
+    _, vox = _graph((4,))
+    n = vox.num_nodes
+    csr = ops.CSR(vox.edge_index.to(cuda), n)
+    cin = 2 * C
+    conv = pyg.GATConv(cin, C).double()
+    with torch.no_grad():
+        conv.bias.uniform_(-0.3, 0.3)
+    x0 = torch.randn(n, cin, dtype=torch.float64)
+    w1 = torch.randn(n, C, dtype=torch.float64)
+
+    def run(x, W, att_s, att_d, b, fn):
+        out = fn(x, W, att_s, att_d, b)
+        gx, = torch.autograd.grad((out * w1.to(out.device)).sum(), x, create_graph=True)
+        pen = (gx.norm(dim=1) - 1).pow(2).mean()
+        return torch.autograd.grad(pen, (x, W, att_s, att_d, b), allow_unused=True)
+
+    def oracle_fn(x, W, a_s, a_d, b):
+        h = x @ W.t()
+        return pyg.gat_propagate(h, h @ a_s.view(-1), h @ a_d.view(-1), vox.edge_index) + b
+
+    def hip_fn(x, W, a_s, a_d, b):
+        h = x @ W.t()
+        return ops.gat_aggregate(csr, h, torch.mv(h, a_s.view(-1)), torch.mv(h, a_d.view(-1)), b)
+
+    params = [conv.lin.weight.detach(), conv.att_src.detach(), conv.att_dst.detach(), conv.bias.detach()]
+    rt = [x0.clone().requires_grad_(True)] + [p.clone().requires_grad_(True) for p in params]
+    ref = run(*rt, oracle_fn)
+    w1 = w1.float().to(cuda)
+    gt = [t.detach().float().to(cuda).requires_grad_(True) for t in rt]
+    got = run(*gt, hip_fn)
+    for g, r in zip(got, ref):
+        if r is None:
+            continue
+        assert rel_err(g, r) < 1e-3
 
 
 def test_sparse_primitives_adjoint_identities(cuda):
@@ -172,7 +214,8 @@ def test_graphnorm_double_backward(cuda):
 
     def second(fn, ts, w1, w2):
         g = torch.autograd.grad((fn(*ts) * w1).sum(), ts, create_graph=True)
-        return torch.autograd.grad(sum((a * b).sum() for a, b in zip(g, w2)), ts)
+        res = torch.autograd.grad(sum((a * b).sum() for a, b in zip(g, w2)), ts, allow_unused=True)
+        return [torch.zeros_like(t) if r is None else r for r, t in zip(res, ts)]
 
     rt = [t.clone().requires_grad_(True) for t in base]
     ref = second(lambda *a: ops.graphnorm_relu_dropout_torch(*a, keep, 1e-5), rt, w1, w2)
