@@ -47,8 +47,9 @@ def log(msg: str) -> None:
 
 def gat_fwd_bytes(n: int, e: int, c: int) -> int:
     """Algorithmic bytes of one vg_gat_fwd: read h [N,C], write out [N,C],
-    read a_src/a_dst [N], row_ptr [N+1], col [E'], write alpha [E'], bias [C]."""
-    return 4 * (2 * n * c + 2 * n + (n + 1) + 2 * e + c)
+    read row_ptr [N+1] and col [E'], write alpha [E'] and a_src/a_dst [N],
+    read att_src/att_dst/bias [C]."""
+    return 4 * (2 * n * c + (n + 1) + 2 * e + 2 * n + 3 * c)
 
 
 class GatTimer:
@@ -60,25 +61,25 @@ class GatTimer:
     def install(self):
         from vgan import ops
 
-        orig = ops._GATAggregate.forward
+        orig = ops._GATConv.forward
         timer = self
 
-        def timed_forward(ctx, h, a_src, a_dst, bias, csr, slope):
+        def timed_forward(ctx, h, att_src, att_dst, bias, csr, slope):
             stream = torch.cuda.current_stream(h.device)
             start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             start.record(stream)
-            out = orig(ctx, h, a_src, a_dst, bias, csr, slope)
+            out = orig(ctx, h, att_src, att_dst, bias, csr, slope)
             end.record(stream)
             timer.records.append((start, end, gat_fwd_bytes(csr.num_nodes, csr.num_edges, h.shape[1])))
             return out
 
         self._orig = orig
-        ops._GATAggregate.forward = staticmethod(timed_forward)
+        ops._GATConv.forward = staticmethod(timed_forward)
 
     def uninstall(self):
         from vgan import ops
 
-        ops._GATAggregate.forward = staticmethod(self._orig)
+        ops._GATConv.forward = staticmethod(self._orig)
 
     def summary(self):
         torch.cuda.synchronize()
@@ -116,11 +117,14 @@ def build_trainer(cfg):
     return Trainer(G, D, None, og, od, sched, cfg)
 
 
+GRAPHED = True
+
+
 def run_steps(tr, pool, k: int, offset: int = 0):
     out = None
     for s in range(k):
         loc, vox = pool[(offset + s) % len(pool)]
-        out = tr.step(loc, vox)
+        out = tr.step_graphed(loc, vox) if GRAPHED else tr.step(loc, vox)
     return out
 
 
@@ -137,17 +141,17 @@ def stress_roofline(device, channels=(128, 64, 1), reps: int = 20):
     res = {}
     for c in channels:
         h = torch.randn(n, c, device=device)
-        a_s, a_d = torch.randn(n, device=device), torch.randn(n, device=device)
+        att_s, att_d = torch.randn(c, device=device) * 0.1, torch.randn(c, device=device) * 0.1
         bias = torch.randn(c, device=device)
         with torch.no_grad():
             for _ in range(3):
-                ops.gat_aggregate(csr, h, a_s, a_d, bias)
+                ops.gat_conv(csr, h, att_s, att_d, bias)
             times = []
             for _ in range(reps):
                 scratch.fill_(1.0)
                 st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 st.record()
-                ops.gat_aggregate(csr, h, a_s, a_d, bias)
+                ops.gat_conv(csr, h, att_s, att_d, bias)
                 en.record()
                 torch.cuda.synchronize()
                 times.append(st.elapsed_time(en))
@@ -212,7 +216,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-stress", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="no hipGraph capture of the step")
     args = ap.parse_args()
+    global GRAPHED
+    GRAPHED = not args.eager
 
     rank, world, local = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(
         os.environ.get("LOCAL_RANK", 0))
@@ -262,12 +269,15 @@ def main():
         elapsed = float(t.item())
     value = args.batch * world * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
-    log(f"timed: {ms_per_step:.2f} ms/step, {value:.1f} graphs/s")
+    log(f"timed ({'hipGraph' if GRAPHED else 'eager'}): {ms_per_step:.2f} ms/step, {value:.1f} graphs/s")
 
-    # instrumented pass for the dominant kernel's roofline
+    # instrumented pass for the dominant kernel's roofline (eager: per-launch
+    # HIP events around vg_gat_fwd on its launch stream)
     timer = GatTimer()
     timer.install()
+    GRAPHED, was = False, GRAPHED
     run_steps(tr, pool, args.steps)
+    GRAPHED = was
     timer.uninstall()
     kern = timer.summary()
     log(f"vg_gat_fwd: {kern['launches']} launches, avg {kern['avg_us']:.2f} us, {kern['achieved_gbs']:.1f} GB/s")
@@ -300,6 +310,8 @@ def main():
                 "global_batch": args.batch * world,
                 "avg_voxel_nodes_per_batch": round(n_nodes, 1),
                 "parallelism": f"dp{world}",
+                "execution": "hipGraph replay (1 critic-iteration graph x N_CRITIC + 1 generator graph)"
+                             if GRAPHED else "eager",
             },
             "roofline": {
                 "kernel": "vg_gat_fwd (fused GAT edge softmax + CSR gather-sum)",

@@ -1,0 +1,726 @@
+// GATConv (heads = 1) message passing, fused: attention projections, edge
+// logits, segmented softmax, weighted gather-sum and bias in one or two
+// kernels; the first-order backward in four.
+//
+// Forward, per destination row i (torch_geometric 2.6.1 GATConv semantics):
+//   a_dst_i = <h_i, att_dst>,  a_src_s = <h_s, att_src>
+//   e_k     = leaky_relu(a_src[col_k] + a_dst_i, 0.2)        (self loop last)
+//   alpha_k = exp(e_k - max_row e) / (sum_row exp(e - max) + 1e-16)
+//   out_i   = sum_k alpha_k h[col_k] + bias
+// The reference issues two (h * att).sum(-1) reductions per layer as separate
+// ops (rocBLAS gemv at 10-80 us each was the top kernel of the first profile);
+// here they are a light per-row pass (C >= 9) or fused into the aggregation
+// (C <= 8).
+//
+// Two decompositions (rowgroup.h):
+// * C >= 9, "channel-parallel": L = 8/16/32 lanes x CPL = 2..8 channels per
+//   row (pick_fused_shape), so a wave holds 2-8 rows.  A per-row pass forms
+//   a_src / a_dst (two group reductions per row); the aggregation pass then
+//   takes logits edge-parallel from those [N] vectors (an earlier single-pass
+//   variant that formed a_src from each gathered neighbour row paid one
+//   cross-lane reduction per EDGE and ran 1.6x slower).
+// * C <= 8, "edge-parallel": 8 lanes per row, one edge per lane (up to 3 per
+//   lane kept in registers, degree <= 24 covers the dense stress graph); each
+//   lane gathers the whole (<= 8-float) neighbour row, so logits need no
+//   cross-lane reduction; max / sum / per-channel sums are 3-step shuffles.
+//
+// Backward (no atomics; deterministic):
+//   B1 (destination rows)  ga_k = <g_out_i, h[col_k]>,  t_i = sum alpha ga,
+//                          gp_k = alpha_k (ga_k - t_i) lrelu'(pre_k),
+//                          g_a_dst_i = sum_k gp_k;  block partials of
+//                          sum_i g_out_i (bias) and sum_i g_a_dst_i h_i (att_dst)
+//   B2 (source nodes, CSC) g_a_src_j = sum gp,  g_h_j = sum alpha g_out[dst]
+//                          + g_a_src_j att_src + g_a_dst_j att_dst;
+//                          block partials of sum_j g_a_src_j h_j (att_src)
+//   B3 (columns)           fold the block partials into g_bias, g_att_src, g_att_dst.
+#include "rowgroup.h"
+
+namespace {
+
+using namespace vg;
+
+constexpr int kMaxBwdBlocks = 512;    // grid cap of the backward row passes (partials count)
+constexpr int kEP = 3;                // edge slots per lane in the edge-parallel kernels
+
+template <int CPL>
+__device__ __forceinline__ void load_param(Vec<CPL>& r, const float* __restrict__ p, int c0, int C) {
+  load_row<CPL, false>(r, p, c0, C);  // parameters live at arbitrary offsets of the flat buffer
+}
+
+// ===================================================================== forward
+// C >= 9, pass A: per-row attention projections a_src_i = <h_i, att_src>,
+// a_dst_i = <h_i, att_dst> (two group reductions per ROW, not per edge).
+template <int L, int CPL, bool VEC>
+__global__ void __launch_bounds__(kBlock) k_gat_att(const float* __restrict__ h, int N, int C,
+                                                    const float* __restrict__ att_s,
+                                                    const float* __restrict__ att_d,
+                                                    float* __restrict__ a_src,
+                                                    float* __restrict__ a_dst) {
+  const GroupIdx g = group_index<L>();
+  if (g.row >= N) return;
+  const int c0 = g.lane * CPL;
+  Vec<CPL> vs, vd, hi;
+  load_param<CPL>(vs, att_s, c0, C);
+  load_param<CPL>(vd, att_d, c0, C);
+  load_row<CPL, VEC>(hi, h + (size_t)g.row * C, c0, C);
+  const float as_i = group_sum<L>(dot_row<CPL, VEC>(hi, vs));
+  const float ad_i = group_sum<L>(dot_row<CPL, VEC>(hi, vd));
+  if (g.lane == 0) {
+    a_src[g.row] = as_i;
+    a_dst[g.row] = ad_i;
+  }
+}
+
+// C >= 9, pass B: logits + exact two-pass segment softmax edge-parallel over
+// the group's lanes, then the channel-parallel weighted gather-sum (4 rows
+// gathered per step, independent loads in flight).
+template <int L, int CPL, bool VEC>
+__global__ void __launch_bounds__(kBlock) k_gat_fwd_cp(
+    const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, int N, int C,
+    const float* __restrict__ h, const float* __restrict__ a_src, const float* __restrict__ a_dst,
+    const float* __restrict__ bias, float slope, float* __restrict__ out,
+    float* __restrict__ alpha) {
+  constexpr int T = 4;  // edges per lane kept in registers (rows up to 4L edges)
+  const GroupIdx g = group_index<L>();
+  if (g.row >= N) return;
+  const int i = g.row;
+  const int beg = row_ptr[i], end = row_ptr[i + 1];
+  const int deg = end - beg;
+  const float ad = a_dst[i];
+
+  // edge-parallel logits, kept per lane: edge j lives in lane j % L, slot j / L
+  int s_t[T];
+  float e_t[T];
+  float m = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int k = beg + g.lane + t * L;
+    s_t[t] = 0;
+    e_t[t] = -INFINITY;
+    if (k < end) {
+      s_t[t] = col[k];
+      e_t[t] = lrelu(a_src[s_t[t]] + ad, slope);
+      m = fmaxf(m, e_t[t]);
+    }
+  }
+  for (int k = beg + g.lane + T * L; k < end; k += L) m = fmaxf(m, lrelu(a_src[col[k]] + ad, slope));
+  m = group_max<L>(m);
+  float ssum = 0.f;
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+    if (beg + g.lane + t * L < end) {
+      e_t[t] = expf(e_t[t] - m);  // now holds p = exp(e - max)
+      ssum += e_t[t];
+    }
+  for (int k = beg + g.lane + T * L; k < end; k += L) ssum += expf(lrelu(a_src[col[k]] + ad, slope) - m);
+  const float denom = group_sum<L>(ssum) + kSoftmaxEps;
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int k = beg + g.lane + t * L;
+    if (k < end) {
+      e_t[t] = e_t[t] / denom;  // alpha
+      alpha[k] = e_t[t];
+    }
+  }
+  for (int k = beg + g.lane + T * L; k < end; k += L)
+    alpha[k] = expf(lrelu(a_src[col[k]] + ad, slope) - m) / denom;
+
+  // channel-parallel gather-sum, 4 neighbour rows in flight
+  const int c0 = g.lane * CPL;
+  Vec<CPL> acc;
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) acc.v[q] = 0.f;
+  const int dreg = deg < T * L ? deg : T * L;
+  for (int j0 = 0; j0 < dreg; j0 += 4) {
+    const int nj = dreg - j0 < 4 ? dreg - j0 : 4;
+    Vec<CPL> hv[4];
+    float a[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (u < nj) {
+        const int j = j0 + u;
+        const int t = j / L;
+        const int sv = t == 0 ? s_t[0] : t == 1 ? s_t[1] : t == 2 ? s_t[2] : s_t[3];
+        const float av = t == 0 ? e_t[0] : t == 1 ? e_t[1] : t == 2 ? e_t[2] : e_t[3];
+        const int s = __shfl(sv, g.base + (j & (L - 1)), 64);
+        a[u] = __shfl(av, g.base + (j & (L - 1)), 64);
+        load_row<CPL, VEC>(hv[u], h + (size_t)s * C, c0, C);
+      }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (u < nj)
+#pragma unroll
+        for (int q = 0; q < CPL; ++q) acc.v[q] = fmaf(a[u], hv[u].v[q], acc.v[q]);
+  }
+  for (int j = T * L; j < deg; ++j) {  // very long rows: alpha from memory (written above by this group)
+    const int s = col[beg + j];
+    const float a = expf(lrelu(a_src[s] + ad, slope) - m) / denom;
+    Vec<CPL> hv;
+    load_row<CPL, VEC>(hv, h + (size_t)s * C, c0, C);
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) acc.v[q] = fmaf(a, hv.v[q], acc.v[q]);
+  }
+  Vec<CPL> b;
+  load_param<CPL>(b, bias, c0, C);
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) acc.v[q] += b.v[q];
+  store_row<CPL, VEC>(acc, out + (size_t)i * C, c0, C);
+}
+
+// C <= 8: 8 lanes per destination row, one edge per lane.
+template <int CMAX>
+__global__ void __launch_bounds__(kBlock) k_gat_fwd_ep(
+    const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, int N, int C,
+    const float* __restrict__ h, const float* __restrict__ att_s, const float* __restrict__ att_d,
+    const float* __restrict__ bias, float slope, float* __restrict__ out, float* __restrict__ alpha,
+    float* __restrict__ a_src_out, float* __restrict__ a_dst_out) {
+  constexpr int L = 8;
+  const GroupIdx g = group_index<L>();
+  if (g.row >= N) return;
+  const int i = g.row;
+  float vs[CMAX], vd[CMAX];
+  float ad = 0.f, as_i = 0.f;
+#pragma unroll
+  for (int c = 0; c < CMAX; ++c) {
+    const bool ok = c < C;
+    vs[c] = ok ? att_s[c] : 0.f;
+    vd[c] = ok ? att_d[c] : 0.f;
+    const float hv = ok ? h[(size_t)i * C + c] : 0.f;
+    ad = fmaf(hv, vd[c], ad);
+    as_i = fmaf(hv, vs[c], as_i);
+  }
+  if (g.lane == 0) {
+    a_dst_out[i] = ad;
+    a_src_out[i] = as_i;
+  }
+  const int beg = row_ptr[i], end = row_ptr[i + 1];
+  float hv[kEP][CMAX];
+  float e[kEP];
+  float m = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < kEP; ++t) {
+    const int k = beg + g.lane + t * L;
+    e[t] = -INFINITY;
+    if (k < end) {
+      const int s = col[k];
+      float a = 0.f;
+#pragma unroll
+      for (int c = 0; c < CMAX; ++c) {
+        hv[t][c] = c < C ? h[(size_t)s * C + c] : 0.f;
+        a = fmaf(hv[t][c], vs[c], a);
+      }
+      e[t] = lrelu(a + ad, slope);
+      m = fmaxf(m, e[t]);
+    } else {
+#pragma unroll
+      for (int c = 0; c < CMAX; ++c) hv[t][c] = 0.f;
+    }
+  }
+  // rows longer than 8*kEP: stream the rest (logits only for the max)
+  for (int k = beg + g.lane + kEP * L; k < end; k += L) {
+    const int s = col[k];
+    float a = 0.f;
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c)
+      if (c < C) a = fmaf(h[(size_t)s * C + c], vs[c], a);
+    m = fmaxf(m, lrelu(a + ad, slope));
+  }
+  m = group_max<L>(m);
+  float ssum = 0.f;
+  float acc[CMAX];
+#pragma unroll
+  for (int c = 0; c < CMAX; ++c) acc[c] = 0.f;
+#pragma unroll
+  for (int t = 0; t < kEP; ++t) {
+    if (beg + g.lane + t * L < end) {
+      const float p = expf(e[t] - m);
+      e[t] = p;
+      ssum += p;
+#pragma unroll
+      for (int c = 0; c < CMAX; ++c) acc[c] = fmaf(p, hv[t][c], acc[c]);
+    }
+  }
+  for (int k = beg + g.lane + kEP * L; k < end; k += L) {
+    const int s = col[k];
+    float a = 0.f, hv2[CMAX];
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c) {
+      hv2[c] = c < C ? h[(size_t)s * C + c] : 0.f;
+      a = fmaf(hv2[c], vs[c], a);
+    }
+    const float p = expf(lrelu(a + ad, slope) - m);
+    ssum += p;
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c) acc[c] = fmaf(p, hv2[c], acc[c]);
+  }
+  const float denom = group_sum<L>(ssum) + kSoftmaxEps;
+#pragma unroll
+  for (int c = 0; c < CMAX; ++c) acc[c] = group_sum<L>(acc[c]);
+  if (g.lane < C) {
+    float v = 0.f;
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c)
+      if (c == g.lane) v = acc[c];
+    out[(size_t)i * C + g.lane] = v / denom + bias[g.lane];
+  }
+#pragma unroll
+  for (int t = 0; t < kEP; ++t) {
+    const int k = beg + g.lane + t * L;
+    if (k < end) alpha[k] = e[t] / denom;
+  }
+  for (int k = beg + g.lane + kEP * L; k < end; k += L) {
+    const int s = col[k];
+    float a = 0.f;
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c)
+      if (c < C) a = fmaf(h[(size_t)s * C + c], vs[c], a);
+    alpha[k] = expf(lrelu(a + ad, slope) - m) / denom;
+  }
+}
+
+// ============================================================ block partials
+// Every group accumulates per-channel partials in registers over the rows it
+// visits (grid-stride); the block folds its groups through LDS and writes one
+// row of `part` ([gridDim.x][W]).  W <= 3 * 256.
+template <int L, int CPL>
+__device__ void block_partials(const Vec<CPL>* vals, int nvec, int C, float* __restrict__ part) {
+  constexpr int G = kBlock / L;
+  __shared__ float red[kBlock * 8 * 2];  // (256/L) groups x L*CPL channels (CPL <= 8) x up to 2 vectors
+  const int grp = threadIdx.x / L, lane = threadIdx.x & (L - 1);
+  const int Wg = L * CPL;
+  for (int v = 0; v < nvec; ++v)
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) red[(grp * nvec + v) * Wg + lane * CPL + q] = vals[v].v[q];
+  __syncthreads();
+  for (int w = threadIdx.x; w < nvec * Wg; w += kBlock) {
+    const int v = w / Wg, c = w % Wg;
+    float s = 0.f;
+    for (int k = 0; k < G; ++k) s += red[(k * nvec + v) * Wg + c];
+    if (c < C) part[(size_t)blockIdx.x * nvec * C + v * C + c] = s;
+  }
+}
+
+// ================================================== backward B1 (destination)
+template <int L, int CPL, bool VEC>
+__global__ void __launch_bounds__(kBlock) k_gat_bwd_rows_cp(
+    const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, int N, int C,
+    const float* __restrict__ h, const float* __restrict__ a_src, const float* __restrict__ a_dst,
+    const float* __restrict__ alpha, const float* __restrict__ g_out, float slope,
+    float* __restrict__ g_pre, float* __restrict__ g_ad, float* __restrict__ part) {
+  constexpr int G = kBlock / L;
+  const int grp = threadIdx.x / L, lane = threadIdx.x & (L - 1);
+  const int base = (threadIdx.x & 63) & ~(L - 1);
+  const int c0 = lane * CPL;
+  Vec<CPL> pb, pd;  // sum g_out, sum g_a_dst * h
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) pb.v[q] = pd.v[q] = 0.f;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  for (int i = lb * G + grp; i < N; i += gridDim.x * G) {
+    const int beg = row_ptr[i], end = row_ptr[i + 1];
+    const int deg = end - beg;
+    Vec<CPL> go, hi;
+    load_row<CPL, VEC>(go, g_out + (size_t)i * C, c0, C);
+    load_row<CPL, VEC>(hi, h + (size_t)i * C, c0, C);
+    const int s_own = lane < deg ? col[beg + lane] : 0;
+    const float al_own = lane < deg ? alpha[beg + lane] : 0.f;
+    float ga_slot[4] = {0.f, 0.f, 0.f, 0.f};
+    float t = 0.f;
+    for (int j0 = 0; j0 < deg; j0 += 4) {
+      const int nj = deg - j0 < 4 ? deg - j0 : 4;
+      Vec<CPL> hv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (u < nj) {
+          const int j = j0 + u;
+          const int s = (deg <= L) ? __shfl(s_own, base + j, 64) : col[beg + j];
+          load_row<CPL, VEC>(hv[u], h + (size_t)s * C, c0, C);
+        }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (u < nj) {
+          const int j = j0 + u;
+          const float ga = group_sum<L>(dot_row<CPL, VEC>(go, hv[u]));
+          const float al = (deg <= L) ? __shfl(al_own, base + j, 64) : alpha[beg + j];
+          t = fmaf(al, ga, t);
+          if (lane == (j & (L - 1))) {
+            const int slot = j / L;
+            if (slot == 0) ga_slot[0] = ga;
+            else if (slot == 1) ga_slot[1] = ga;
+            else if (slot == 2) ga_slot[2] = ga;
+            else if (slot == 3) ga_slot[3] = ga;
+          }
+        }
+    }
+    const float adi = a_dst[i];
+    float gad = 0.f;
+#pragma unroll
+    for (int slot = 0; slot < 4; ++slot) {
+      const int j = slot * L + lane;
+      if (j < deg) {
+        const int k = beg + j;
+        const float pre = a_src[col[k]] + adi;
+        const float gp = alpha[k] * (ga_slot[slot] - t) * (pre > 0.f ? 1.f : slope);
+        g_pre[k] = gp;
+        gad += gp;
+      }
+    }
+    for (int j = 4 * L; j < deg; ++j) {
+      const int k = beg + j;
+      Vec<CPL> hv;
+      load_row<CPL, VEC>(hv, h + (size_t)col[k] * C, c0, C);
+      const float ga = group_sum<L>(dot_row<CPL, VEC>(go, hv));
+      if (lane == 0) {
+        const float pre = a_src[col[k]] + adi;
+        const float gp = alpha[k] * (ga - t) * (pre > 0.f ? 1.f : slope);
+        g_pre[k] = gp;
+        gad += gp;
+      }
+    }
+    gad = group_sum<L>(gad);
+    if (lane == 0) g_ad[i] = gad;
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) {
+      pb.v[q] += go.v[q];
+      pd.v[q] = fmaf(gad, hi.v[q], pd.v[q]);
+    }
+  }
+  Vec<CPL> vals[2] = {pb, pd};
+  block_partials<L, CPL>(vals, 2, C, part);
+}
+
+template <int CMAX>
+__global__ void __launch_bounds__(kBlock) k_gat_bwd_rows_ep(
+    const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, int N, int C,
+    const float* __restrict__ h, const float* __restrict__ a_src, const float* __restrict__ a_dst,
+    const float* __restrict__ alpha, const float* __restrict__ g_out, float slope,
+    float* __restrict__ g_pre, float* __restrict__ g_ad, float* __restrict__ part) {
+  constexpr int L = 8, G = kBlock / L;
+  const int grp = threadIdx.x / L, lane = threadIdx.x & (L - 1);
+  float pb[CMAX], pd[CMAX];
+#pragma unroll
+  for (int c = 0; c < CMAX; ++c) pb[c] = pd[c] = 0.f;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  for (int i = lb * G + grp; i < N; i += gridDim.x * G) {
+    const int beg = row_ptr[i], end = row_ptr[i + 1];
+    float go[CMAX];
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c) go[c] = c < C ? g_out[(size_t)i * C + c] : 0.f;
+    float ga[kEP], al[kEP];
+    float t = 0.f;
+#pragma unroll
+    for (int u = 0; u < kEP; ++u) {
+      const int k = beg + lane + u * L;
+      ga[u] = 0.f;
+      al[u] = 0.f;
+      if (k < end) {
+        const int s = col[k];
+        float d = 0.f;
+#pragma unroll
+        for (int c = 0; c < CMAX; ++c)
+          if (c < C) d = fmaf(go[c], h[(size_t)s * C + c], d);
+        ga[u] = d;
+        al[u] = alpha[k];
+        t = fmaf(al[u], d, t);
+      }
+    }
+    for (int k = beg + lane + kEP * L; k < end; k += L) {
+      float d = 0.f;
+#pragma unroll
+      for (int c = 0; c < CMAX; ++c)
+        if (c < C) d = fmaf(go[c], h[(size_t)col[k] * C + c], d);
+      t = fmaf(alpha[k], d, t);
+    }
+    t = group_sum<L>(t);
+    const float adi = a_dst[i];
+    float gad = 0.f;
+#pragma unroll
+    for (int u = 0; u < kEP; ++u) {
+      const int k = beg + lane + u * L;
+      if (k < end) {
+        const float pre = a_src[col[k]] + adi;
+        const float gp = al[u] * (ga[u] - t) * (pre > 0.f ? 1.f : slope);
+        g_pre[k] = gp;
+        gad += gp;
+      }
+    }
+    for (int k = beg + lane + kEP * L; k < end; k += L) {
+      float d = 0.f;
+#pragma unroll
+      for (int c = 0; c < CMAX; ++c)
+        if (c < C) d = fmaf(go[c], h[(size_t)col[k] * C + c], d);
+      const float pre = a_src[col[k]] + adi;
+      const float gp = alpha[k] * (d - t) * (pre > 0.f ? 1.f : slope);
+      g_pre[k] = gp;
+      gad += gp;
+    }
+    gad = group_sum<L>(gad);
+    if (lane == 0) {
+      g_ad[i] = gad;
+#pragma unroll
+      for (int c = 0; c < CMAX; ++c) {
+        pb[c] += go[c];
+        pd[c] = fmaf(gad, c < C ? h[(size_t)i * C + c] : 0.f, pd[c]);
+      }
+    }
+  }
+  // fold: only lane 0 of each group carries partials
+  __shared__ float red[G][2][CMAX];
+  if (lane == 0)
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c) {
+      red[grp][0][c] = pb[c];
+      red[grp][1][c] = pd[c];
+    }
+  __syncthreads();
+  if (threadIdx.x < 2 * CMAX) {
+    const int v = threadIdx.x / CMAX, c = threadIdx.x % CMAX;
+    float s = 0.f;
+    for (int k = 0; k < G; ++k) s += red[k][v][c];
+    if (c < C) part[(size_t)blockIdx.x * 2 * C + v * C + c] = s;
+  }
+}
+
+// ===================================================== backward B2 (sources)
+template <int L, int CPL, bool VEC>
+__global__ void __launch_bounds__(kBlock) k_gat_bwd_src_cp(
+    const int32_t* __restrict__ csc_ptr, const int32_t* __restrict__ csc_slot,
+    const int32_t* __restrict__ csc_dst, int N, int C, const float* __restrict__ h,
+    const float* __restrict__ att_s, const float* __restrict__ att_d,
+    const float* __restrict__ alpha, const float* __restrict__ g_out,
+    const float* __restrict__ g_pre, const float* __restrict__ g_ad, float* __restrict__ g_h,
+    float* __restrict__ part) {
+  constexpr int G = kBlock / L;
+  const int grp = threadIdx.x / L, lane = threadIdx.x & (L - 1);
+  const int base = (threadIdx.x & 63) & ~(L - 1);
+  const int c0 = lane * CPL;
+  Vec<CPL> vs, vd, ps;
+  load_param<CPL>(vs, att_s, c0, C);
+  load_param<CPL>(vd, att_d, c0, C);
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) ps.v[q] = 0.f;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  for (int j = lb * G + grp; j < N; j += gridDim.x * G) {
+    const int beg = csc_ptr[j], end = csc_ptr[j + 1];
+    const int deg = end - beg;
+    int d_own = 0;
+    float a_own = 0.f, gas = 0.f;
+    for (int p = beg + lane; p < end; p += L) {
+      const int k = csc_slot[p];
+      if (p == beg + lane) {
+        d_own = csc_dst[p];
+        a_own = alpha[k];
+      }
+      gas += g_pre[k];
+    }
+    gas = group_sum<L>(gas);
+    Vec<CPL> acc;
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) acc.v[q] = 0.f;
+    for (int e0 = 0; e0 < deg; e0 += 4) {
+      const int ne = deg - e0 < 4 ? deg - e0 : 4;
+      Vec<CPL> gv[4];
+      float a[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (u < ne) {
+          const int e = e0 + u;
+          int d;
+          if (deg <= L) {
+            d = __shfl(d_own, base + e, 64);
+            a[u] = __shfl(a_own, base + e, 64);
+          } else {
+            d = csc_dst[beg + e];
+            a[u] = alpha[csc_slot[beg + e]];
+          }
+          load_row<CPL, VEC>(gv[u], g_out + (size_t)d * C, c0, C);
+        }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (u < ne)
+#pragma unroll
+          for (int q = 0; q < CPL; ++q) acc.v[q] = fmaf(a[u], gv[u].v[q], acc.v[q]);
+    }
+    const float gadj = g_ad[j];
+    Vec<CPL> hj;
+    load_row<CPL, VEC>(hj, h + (size_t)j * C, c0, C);
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) {
+      acc.v[q] = fmaf(gas, vs.v[q], fmaf(gadj, vd.v[q], acc.v[q]));
+      ps.v[q] = fmaf(gas, hj.v[q], ps.v[q]);
+    }
+    store_row<CPL, VEC>(acc, g_h + (size_t)j * C, c0, C);
+  }
+  Vec<CPL> vals[1] = {ps};
+  block_partials<L, CPL>(vals, 1, C, part);
+}
+
+template <int CMAX>
+__global__ void __launch_bounds__(kBlock) k_gat_bwd_src_ep(
+    const int32_t* __restrict__ csc_ptr, const int32_t* __restrict__ csc_slot,
+    const int32_t* __restrict__ csc_dst, int N, int C, const float* __restrict__ h,
+    const float* __restrict__ att_s, const float* __restrict__ att_d,
+    const float* __restrict__ alpha, const float* __restrict__ g_out,
+    const float* __restrict__ g_pre, const float* __restrict__ g_ad, float* __restrict__ g_h,
+    float* __restrict__ part) {
+  constexpr int L = 8, G = kBlock / L;
+  const int grp = threadIdx.x / L, lane = threadIdx.x & (L - 1);
+  float ps[CMAX];
+#pragma unroll
+  for (int c = 0; c < CMAX; ++c) ps[c] = 0.f;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  for (int j = lb * G + grp; j < N; j += gridDim.x * G) {
+    const int beg = csc_ptr[j], end = csc_ptr[j + 1];
+    float gas = 0.f, acc[CMAX];
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c) acc[c] = 0.f;
+    for (int p = beg + lane; p < end; p += L) {
+      const int k = csc_slot[p];
+      const int d = csc_dst[p];
+      const float a = alpha[k];
+      gas += g_pre[k];
+#pragma unroll
+      for (int c = 0; c < CMAX; ++c)
+        if (c < C) acc[c] = fmaf(a, g_out[(size_t)d * C + c], acc[c]);
+    }
+    gas = group_sum<L>(gas);
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c) acc[c] = group_sum<L>(acc[c]);
+    const float gadj = g_ad[j];
+    if (lane < C) {
+      float v = 0.f;
+#pragma unroll
+      for (int c = 0; c < CMAX; ++c)
+        if (c == lane) v = acc[c];
+      g_h[(size_t)j * C + lane] = fmaf(gas, att_s[lane], fmaf(gadj, att_d[lane], v));
+    }
+    if (lane == 0)
+#pragma unroll
+      for (int c = 0; c < CMAX; ++c)
+        if (c < C) ps[c] = fmaf(gas, h[(size_t)j * C + c], ps[c]);
+  }
+  __shared__ float red[G][CMAX];
+  if (lane == 0)
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c) red[grp][c] = ps[c];
+  __syncthreads();
+  if (threadIdx.x < CMAX) {
+    float s = 0.f;
+    for (int k = 0; k < G; ++k) s += red[k][threadIdx.x];
+    if ((int)threadIdx.x < C) part[(size_t)blockIdx.x * C + threadIdx.x] = s;
+  }
+}
+
+// ===================================================== B3: fold the partials
+// out[w] = sum_b part[b][w] for w < W (w < split -> out_a, else out_b); one
+// 1024-thread block per 64 columns, 16 waves stride over the partial rows,
+// LDS fold in a fixed order (deterministic).
+__global__ void __launch_bounds__(1024) k_fold_cols(const float* __restrict__ part, int rows, int W,
+                                                    int split, float* __restrict__ out_a,
+                                                    float* __restrict__ out_b) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int w = blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (w < W)
+    for (int r = wave; r < rows; r += 16) s += part[(size_t)r * W + w];
+  __shared__ float red[16][64];
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && w < W) {
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v += red[k][lane];
+    if (w < split) out_a[w] = v; else out_b[w - split] = v;
+  }
+}
+
+inline int bwd_grid(int N, int L) {
+  const int g = grid_for(N, L);
+  return g < kMaxBwdBlocks ? g : kMaxBwdBlocks;
+}
+
+}  // namespace
+
+extern "C" int64_t vg_gat_bwd_ws_floats(int32_t num_nodes, int32_t num_edges, int32_t channels) {
+  // g_pre [E'] + g_a_dst [N] + partials (B1: 2C per block, B2: C per block)
+  return (int64_t)num_edges + num_nodes + (int64_t)kMaxBwdBlocks * 3 * channels;
+}
+
+extern "C" int vg_gat_fwd(const int32_t* row_ptr, const int32_t* col, int32_t N, int32_t C,
+                          const float* h, const float* att_src, const float* att_dst,
+                          const float* bias, float slope, float* out, float* alpha,
+                          float* a_src, float* a_dst, void* stream) {
+  if (N <= 0 || !row_ptr || !col || !h || !att_src || !att_dst || !bias || !out || !alpha ||
+      !a_src || !a_dst)
+    return VG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (C <= 8) {
+    const int grid = grid_for(N, 8);
+    if (C <= 1)
+      k_gat_fwd_ep<1><<<grid, kBlock, 0, s>>>(row_ptr, col, N, C, h, att_src, att_dst, bias, slope,
+                                              out, alpha, a_src, a_dst);
+    else if (C <= 2)
+      k_gat_fwd_ep<2><<<grid, kBlock, 0, s>>>(row_ptr, col, N, C, h, att_src, att_dst, bias, slope,
+                                              out, alpha, a_src, a_dst);
+    else if (C <= 4)
+      k_gat_fwd_ep<4><<<grid, kBlock, 0, s>>>(row_ptr, col, N, C, h, att_src, att_dst, bias, slope,
+                                              out, alpha, a_src, a_dst);
+    else
+      k_gat_fwd_ep<8><<<grid, kBlock, 0, s>>>(row_ptr, col, N, C, h, att_src, att_dst, bias, slope,
+                                              out, alpha, a_src, a_dst);
+  } else {
+    VG_DISPATCH_FUSED(C, (k_gat_att<L_, CPL_, V_><<<grid_for(N, L_), kBlock, 0, s>>>(
+                             h, N, C, att_src, att_dst, a_src, a_dst)));
+    VG_DISPATCH_FUSED(C, (k_gat_fwd_cp<L_, CPL_, V_><<<grid_for(N, L_), kBlock, 0, s>>>(
+                             row_ptr, col, N, C, h, a_src, a_dst, bias, slope, out, alpha)));
+  }
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int vg_gat_bwd(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,
+                          const int32_t* csc_slot, const int32_t* csc_dst, int32_t N, int32_t E,
+                          int32_t C, const float* h, const float* att_src, const float* att_dst,
+                          const float* a_src, const float* a_dst, const float* alpha,
+                          const float* g_out, float slope, float* g_h, float* g_att_src,
+                          float* g_att_dst, float* g_bias, float* workspace, void* stream) {
+  if (N <= 0 || E <= 0 || !row_ptr || !col || !csc_ptr || !csc_slot || !csc_dst || !h ||
+      !att_src || !att_dst || !a_src || !a_dst || !alpha || !g_out || !g_h || !g_att_src ||
+      !g_att_dst || !g_bias || !workspace)
+    return VG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  float* g_pre = workspace;
+  float* g_ad = workspace + E;
+  float* part1 = g_ad + N;                                // [grid1][2C]
+  float* part2 = part1 + (size_t)kMaxBwdBlocks * 2 * C;   // [grid2][C]
+  int grid1 = 0, grid2 = 0;
+  if (C <= 8) {
+    grid1 = grid2 = bwd_grid(N, 8);
+#define VG_EP(CM)                                                                                 \
+  do {                                                                                            \
+    k_gat_bwd_rows_ep<CM><<<grid1, kBlock, 0, s>>>(row_ptr, col, N, C, h, a_src, a_dst, alpha,     \
+                                                   g_out, slope, g_pre, g_ad, part1);             \
+    k_gat_bwd_src_ep<CM><<<grid2, kBlock, 0, s>>>(csc_ptr, csc_slot, csc_dst, N, C, h, att_src,    \
+                                                  att_dst, alpha, g_out, g_pre, g_ad, g_h, part2); \
+  } while (0)
+    if (C <= 1) VG_EP(1);
+    else if (C <= 2) VG_EP(2);
+    else if (C <= 4) VG_EP(4);
+    else VG_EP(8);
+#undef VG_EP
+  } else {
+    Shape sh;
+    if (!pick_fused_shape(C, sh)) return VG_EINVAL;
+    grid1 = grid2 = bwd_grid(N, sh.L);
+    VG_DISPATCH_FUSED(C, (k_gat_bwd_rows_cp<L_, CPL_, V_><<<grid1, kBlock, 0, s>>>(
+                             row_ptr, col, N, C, h, a_src, a_dst, alpha, g_out, slope, g_pre,
+                             g_ad, part1)));
+    VG_DISPATCH_FUSED(C, (k_gat_bwd_src_cp<L_, CPL_, V_><<<grid2, kBlock, 0, s>>>(
+                             csc_ptr, csc_slot, csc_dst, N, C, h, att_src, att_dst, alpha, g_out,
+                             g_pre, g_ad, g_h, part2)));
+  }
+  // fold: part1 rows -> [g_bias | g_att_dst], part2 rows -> g_att_src
+  k_fold_cols<<<vg_blocks(2 * C, 64), 1024, 0, s>>>(part1, grid1, 2 * C, C, g_bias, g_att_dst);
+  k_fold_cols<<<vg_blocks(C, 64), 1024, 0, s>>>(part2, grid2, C, C, g_att_src, g_att_src);
+  VG_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,242 @@
+// Dense per-node GEMMs of the MLPs on the f32 MFMA (v_mfma_f32_32x32x2_f32).
+//
+// The path's dense layers are tall-skinny: N ~ 12.7k node rows against
+// K, M <= 524 x 128 weights.  Library GEMMs paid 19 us minimum per call and
+// 77-692 us for the weight gradient (a handful of output tiles with the whole
+// K = N reduction in one workgroup; profiles/r01_*).  Two kernels cover all
+// three products of nn.Linear:
+//
+//   k_gemm      C[N, M] = A[N, K] . op(B) (+ bias[M]) (+ activation)
+//               forward  (A = X, B = W [M, K], op = transpose)
+//               dX       (A = dY, B = W [M, K] read as [K', M'] = no transpose)
+//   k_gemm_tn   C[M, K] = A[N, M]^T . B[N, K] split over N (~768 workgroups),
+//               plus db[M] = sum_n A[n, :]; partials folded in chunk order.
+//               weight / bias gradient (A = dY, B = X)
+//
+// f32 in, f32 accumulate: the MFMA is an exact fmaf chain (no TF32 on gfx950),
+// so results differ from a CPU GEMM only by summation order.
+//
+// Tiling: 256-thread workgroup = 4 waves, 64 x 64 output tile, each wave one
+// 32 x 32 MFMA tile; K staged through LDS 32 at a time.  LDS rows are padded
+// to 33 floats so the MFMA operand reads (32 lanes down a column) and the
+// transposing stores are bank-conflict free.
+#include "common.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int TM = 64, TN = 64, TK = 32, LDP = TK + 1;
+
+template <int ACT>
+__device__ __forceinline__ float act_fn(float v) {
+  if constexpr (ACT == 1) return v > 0.f ? v : 0.f;
+  else if constexpr (ACT == 2) return v > 0.f ? v : 0.2f * v;
+  else return v;
+}
+
+// C = A . op(B) (+bias) (+act).  BT: B is [M, K] (op = B^T); else B is [K, M].
+// Software pipelined: the next K-tile is loaded into registers while the MFMAs
+// of the current one run; LDS is double-buffered (one barrier per K-tile).
+template <bool BT, int ACT>
+__global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int lda,
+                                              const float* __restrict__ B, int ldb,
+                                              const float* __restrict__ bias,
+                                              float* __restrict__ C, int ldc, int N, int M, int K) {
+  __shared__ float As[2][TM][LDP];
+  __shared__ float Bs[2][TN][LDP];  // Bs[j][k] = op(B)[k][j]
+  constexpr int PER = (TM * TK) / 256;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int n0 = blockIdx.x * TM, m0 = blockIdx.y * TN;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  float ra[PER], rb[PER];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int e = t + 256 * q;
+      const int row = e / TK, kc = e % TK;
+      const int n = n0 + row, k = k0 + kc;
+      ra[q] = (n < N && k < K) ? A[(size_t)n * lda + k] : 0.f;
+      if (BT) {
+        const int m = m0 + row;
+        rb[q] = (m < M && k < K) ? B[(size_t)m * ldb + k] : 0.f;
+      } else {
+        const int kr = e / TN, j = e % TN;
+        const int m = m0 + j, kk = k0 + kr;
+        rb[q] = (m < M && kk < K) ? B[(size_t)kk * ldb + m] : 0.f;
+      }
+    }
+  };
+  load(0);
+  int buf = 0;
+  for (int k0 = 0; k0 < K; k0 += TK) {
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int e = t + 256 * q;
+      As[buf][e / TK][e % TK] = ra[q];
+      if (BT) Bs[buf][e / TK][e % TK] = rb[q];
+      else Bs[buf][e % TN][e / TN] = rb[q];
+    }
+    __syncthreads();
+    if (k0 + TK < K) load(k0 + TK);
+    const float* ar = &As[buf][wr * 32 + (lane & 31)][lane >> 5];
+    const float* br = &Bs[buf][wc * 32 + (lane & 31)][lane >> 5];
+#pragma unroll
+    for (int kk = 0; kk < TK; kk += 2)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[kk], br[kk], acc, 0, 0, 0);
+    buf ^= 1;
+  }
+  const int m = m0 + wc * 32 + (lane & 31);
+  const float bv = (bias && m < M) ? bias[m] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int n = n0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    if (n < N && m < M) C[(size_t)n * ldc + m] = act_fn<ACT>(acc[r] + bv);
+  }
+}
+
+// part[chunk][M][K] = A[chunk rows]^T . B[chunk rows];  pdb[chunk][M] = column sums of A.
+// `rows` rows of the N reduction per chunk (a multiple of TK), pipelined like k_gemm.
+__global__ void __launch_bounds__(256) k_gemm_tn(const float* __restrict__ A, int lda,
+                                                 const float* __restrict__ B, int ldb, int N,
+                                                 int M, int K, int rows, float* __restrict__ part,
+                                                 float* __restrict__ pdb) {
+  __shared__ float As[2][TK][TM + 1];  // As[n][m]
+  __shared__ float Bs[2][TK][TN + 1];  // Bs[n][k]
+  constexpr int PER = (TK * TM) / 256;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int m0 = blockIdx.x * TM, k0 = blockIdx.y * TN, chunk = blockIdx.z;
+  const int nb = chunk * rows, ne = min(N, nb + rows);
+  const bool do_db = pdb && blockIdx.y == 0;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  float dbs = 0.f;
+  float ra[PER], rb[PER];
+  auto load = [&](int n1) {
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int e = t + 256 * q;
+      const int r = e / TM, c = e % TM;
+      const int n = n1 + r;
+      ra[q] = (n < ne && m0 + c < M) ? A[(size_t)n * lda + m0 + c] : 0.f;
+      rb[q] = (n < ne && k0 + c < K) ? B[(size_t)n * ldb + k0 + c] : 0.f;
+    }
+  };
+  load(nb);
+  int buf = 0;
+  for (int n1 = nb; n1 < ne; n1 += TK) {
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int e = t + 256 * q;
+      As[buf][e / TM][e % TM] = ra[q];
+      Bs[buf][e / TM][e % TM] = rb[q];
+      if (do_db) dbs += ra[q];  // column (t & 63) of this thread, rows e / TM
+    }
+    __syncthreads();
+    if (n1 + TK < ne) load(n1 + TK);
+#pragma unroll
+    for (int kk = 0; kk < TK; kk += 2) {
+      const float a = As[buf][kk + (lane >> 5)][wr * 32 + (lane & 31)];
+      const float b = Bs[buf][kk + (lane >> 5)][wc * 32 + (lane & 31)];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+    }
+    buf ^= 1;
+  }
+  const int k = k0 + wc * 32 + (lane & 31);
+  float* out = part + (size_t)chunk * M * K;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    if (m < M && k < K) out[(size_t)m * K + k] = acc[r];
+  }
+  if (do_db) {
+    __shared__ float red[4][64];
+    red[t >> 6][t & 63] = dbs;
+    __syncthreads();
+    if (t < 64 && m0 + t < M)
+      pdb[(size_t)chunk * M + m0 + t] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+  }
+}
+
+// out[w] = sum_c part[c][w], fixed order; 1024 threads per 64 outputs, 16 rows in flight.
+__global__ void __launch_bounds__(1024) k_fold_rows(const float* __restrict__ part, int rows,
+                                                    long long W, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long long w = blockIdx.x * 64LL + lane;
+  float s = 0.f;
+  if (w < W)
+    for (int r = wave; r < rows; r += 16) s += part[(size_t)r * W + w];
+  __shared__ float red[16][64];
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && w < W) {
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v += red[k][lane];
+    out[w] = v;
+  }
+}
+
+}  // namespace
+
+extern "C" int vg_gemm(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t b_trans,
+                       const float* bias, int32_t act, float* C, int32_t ldc, int32_t N, int32_t M,
+                       int32_t K, void* stream) {
+  if (N < 0 || M <= 0 || K <= 0 || !A || !B || !C || act < 0 || act > 2) return VG_EINVAL;
+  if (N == 0) return 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  dim3 grid((N + TM - 1) / TM, (M + TN - 1) / TN);
+#define VG_G(BT, ACT) k_gemm<BT, ACT><<<grid, 256, 0, s>>>(A, lda, B, ldb, bias, C, ldc, N, M, K)
+  if (b_trans) {
+    if (act == 0) VG_G(true, 0); else if (act == 1) VG_G(true, 1); else VG_G(true, 2);
+  } else {
+    if (act == 0) VG_G(false, 0); else if (act == 1) VG_G(false, 1); else VG_G(false, 2);
+  }
+#undef VG_G
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+// rows per split-K chunk: aim at ~768 workgroups in total, multiples of TK
+static inline int tn_rows(int N, int M, int K) {
+  const int tiles = ((M + TM - 1) / TM) * ((K + TN - 1) / TN);
+  int target = 768 / tiles;
+  if (target < 1) target = 1;
+  int rows = (N + target - 1) / target;
+  rows = ((rows + TK - 1) / TK) * TK;
+  return rows < TK ? TK : rows;
+}
+
+extern "C" int64_t vg_gemm_tn_ws_floats(int32_t N, int32_t M, int32_t K) {
+  if (N <= 0) return 1;
+  const int64_t chunks = (N + tn_rows(N, M, K) - 1) / tn_rows(N, M, K);
+  return chunks * ((int64_t)M * K + M);
+}
+
+extern "C" int vg_gemm_tn(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N,
+                          int32_t M, int32_t K, float* C, float* db, float* workspace,
+                          void* stream) {
+  if (N < 0 || M <= 0 || K <= 0 || !A || !B || !C || !workspace) return VG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (N == 0) {
+    (void)hipMemsetAsync(C, 0, sizeof(float) * M * K, s);
+    if (db) (void)hipMemsetAsync(db, 0, sizeof(float) * M, s);
+    return 0;
+  }
+  const int rows = tn_rows(N, M, K);
+  const int chunks = (N + rows - 1) / rows;
+  float* part = workspace;
+  float* pdb = workspace + (size_t)chunks * M * K;
+  dim3 grid((M + TM - 1) / TM, (K + TN - 1) / TN, chunks);
+  k_gemm_tn<<<grid, 256, 0, s>>>(A, lda, B, ldb, N, M, K, rows, part, db ? pdb : nullptr);
+  const long long W = (long long)M * K;
+  k_fold_rows<<<(int)((W + 63) / 64), 1024, 0, s>>>(part, chunks, W, C);
+  if (db) k_fold_rows<<<(M + 63) / 64, 1024, 0, s>>>(pdb, chunks, M, db);
+  VG_CHECK_LAUNCH();
+  return 0;
+}

@@ -9,7 +9,7 @@
 //
 // The column statistics are a two-level deterministic reduction: R row-chunk
 // blocks per 64-column slab produce (count, mean, M2) Welford partials, a
-// finalize kernel merges them in chunk order (Chan's formula), and the
+// finalize kernel merges them in a fixed order (Chan's formula), and the
 // elementwise kernel applies.  Lanes are packed (col, row-sub) so narrow layers
 // (C = 1..32) still use every lane of the wave.
 #include "common.h"
@@ -88,17 +88,26 @@ __global__ void __launch_bounds__(kBlock) k_stats_partial(const float* __restric
   }
 }
 
-__global__ void k_stats_final(const float* __restrict__ part, int chunks, int C,
-                              float* __restrict__ stats) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// Merge the per-chunk Welford partials: one 256-thread block per 64 columns,
+// wave w merges chunks w, w+4, ... (fixed order), then the 4 waves in LDS.
+__global__ void __launch_bounds__(256) k_stats_final(const float* __restrict__ part, int chunks,
+                                                     int C, float* __restrict__ stats) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   Welford acc = {0.f, 0.f, 0.f};
-  for (int k = 0; k < chunks; ++k) {
-    const float* p = part + ((size_t)k * C + c) * 3;
-    acc = merge(acc, Welford{p[0], p[1], p[2]});
+  if (c < C)
+    for (int k = wave; k < chunks; k += 4) {
+      const float* p = part + ((size_t)k * C + c) * 3;
+      acc = merge(acc, Welford{p[0], p[1], p[2]});
+    }
+  __shared__ Welford sw[4][64];
+  sw[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0 && c < C) {
+    Welford r = merge(merge(sw[0][lane], sw[1][lane]), merge(sw[2][lane], sw[3][lane]));
+    stats[c] = r.mean;
+    stats[C + c] = sqrtf(fmaxf(r.m2 / r.n, 0.f));
   }
-  stats[c] = acc.mean;
-  stats[C + c] = sqrtf(fmaxf(acc.m2 / acc.n, 0.f));
 }
 
 __global__ void k_gn_apply(const float* __restrict__ x, long long total, int C,
@@ -166,23 +175,32 @@ __global__ void __launch_bounds__(kBlock) k_gn_bwd_partial(
   }
 }
 
-__global__ void k_gn_bwd_final(const float* __restrict__ part, int chunks, int C,
-                               const float* __restrict__ w, const float* __restrict__ ms,
-                               float eps, const float* __restrict__ stats,
-                               float* __restrict__ sums, float* __restrict__ g_w,
-                               float* __restrict__ g_b, float* __restrict__ g_ms) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+__global__ void __launch_bounds__(256) k_gn_bwd_final(
+    const float* __restrict__ part, int chunks, int C, const float* __restrict__ w,
+    const float* __restrict__ ms, float eps, const float* __restrict__ stats,
+    float* __restrict__ sums, float* __restrict__ g_w, float* __restrict__ g_b,
+    float* __restrict__ g_ms) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   float a = 0.f, bb = 0.f;
-  for (int k = 0; k < chunks; ++k) {
-    a += part[((size_t)k * C + c) * 2];
-    bb += part[((size_t)k * C + c) * 2 + 1];
+  if (c < C)
+    for (int k = wave; k < chunks; k += 4) {
+      a += part[((size_t)k * C + c) * 2];
+      bb += part[((size_t)k * C + c) * 2 + 1];
+    }
+  __shared__ float red[4][64][2];
+  red[wave][lane][0] = a;
+  red[wave][lane][1] = bb;
+  __syncthreads();
+  if (wave == 0 && c < C) {
+    a = (red[0][lane][0] + red[1][lane][0]) + (red[2][lane][0] + red[3][lane][0]);
+    bb = (red[0][lane][1] + red[1][lane][1]) + (red[2][lane][1] + red[3][lane][1]);
+    sums[c] = a;
+    sums[C + c] = bb;
+    g_w[c] = bb;
+    g_b[c] = a;
+    g_ms[c] = -stats[c] * w[c] * a / (stats[C + c] + eps);
   }
-  sums[c] = a;
-  sums[C + c] = bb;
-  g_w[c] = bb;
-  g_b[c] = a;
-  g_ms[c] = -stats[c] * w[c] * a / (stats[C + c] + eps);
 }
 
 __global__ void k_gn_bwd_apply(const float* __restrict__ x, const float* __restrict__ gy,
@@ -227,7 +245,7 @@ extern "C" int vg_graphnorm_fwd(const float* x, int32_t N, int32_t C, const floa
   const int chunks = chunks_for(N);
   dim3 grid(chunks, (C + 63) / 64);
   k_stats_partial<<<grid, kBlock, 0, s>>>(x, N, C, ws);
-  k_stats_final<<<vg_blocks(C, 64), 64, 0, s>>>(ws, chunks, C, stats);
+  k_stats_final<<<vg_blocks(C, 64), 256, 0, s>>>(ws, chunks, C, stats);
   const long long total = (long long)N * C;
   int blocks = vg_blocks(total, 256);
   if (blocks > 2048) blocks = 2048;
@@ -250,8 +268,8 @@ extern "C" int vg_graphnorm_bwd(const float* x, int32_t N, int32_t C, const floa
   dim3 grid(chunks, (C + 63) / 64);
   k_gn_bwd_partial<<<grid, kBlock, 0, s>>>(x, g_y, N, C, weight, bias, mean_scale, keep, eps,
                                            stats, part);
-  k_gn_bwd_final<<<vg_blocks(C, 64), 64, 0, s>>>(part, chunks, C, weight, mean_scale, eps, stats,
-                                                 sums, g_w, g_b, g_ms);
+  k_gn_bwd_final<<<vg_blocks(C, 64), 256, 0, s>>>(part, chunks, C, weight, mean_scale, eps,
+                                                  stats, sums, g_w, g_b, g_ms);
   const long long total = (long long)N * C;
   int blocks = vg_blocks(total, 256);
   if (blocks > 2048) blocks = 2048;

@@ -145,6 +145,33 @@ __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float
   }
 }
 
+// Same update with the step count and learning rate read from device memory
+// (hipGraph replays: host scalars would be frozen into the graph).  Bias
+// corrections are formed in double exactly as torch forms them in Python.
+__global__ void k_adam_dev(float* __restrict__ p, const float* __restrict__ g,
+                           float* __restrict__ m, float* __restrict__ v, long long n, double b1,
+                           double b2, float eps, float wd, const double* __restrict__ lr_p,
+                           const int32_t* __restrict__ step_p) {
+  const double t = static_cast<double>(*step_p);
+  const double lr = *lr_p;
+  const float neg_step = static_cast<float>(-(lr / (1.0 - pow(b1, t))));
+  const float bc2_sqrt = static_cast<float>(sqrt(1.0 - pow(b2, t)));
+  const float fb2 = static_cast<float>(b2), omb1 = static_cast<float>(1.0 - b1),
+              omb2 = static_cast<float>(1.0 - b2);
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    float gi = g[i];
+    if (wd != 0.f) gi = gi + wd * p[i];
+    const float mi = m[i];
+    const float mn = (fabsf(omb1) < 0.5f) ? mi + omb1 * (gi - mi) : gi - (gi - mi) * (1.f - omb1);
+    const float vn = v[i] * fb2 + (omb2 * gi) * gi;
+    m[i] = mn;
+    v[i] = vn;
+    const float denom = sqrtf(vn) / bc2_sqrt + eps;
+    p[i] = p[i] + (neg_step * mn) / denom;
+  }
+}
+
 }  // namespace
 
 extern "C" int vg_gumbel_fwd(const float* logits, const float* noise, int32_t rows,
@@ -207,6 +234,20 @@ extern "C" int vg_adam(float* param, const float* grad, float* exp_avg, float* e
   k_adam<<<blocks, 256, 0, static_cast<hipStream_t>(stream)>>>(
       param, grad, exp_avg, exp_avg_sq, n, beta2, one_minus_beta1, one_minus_beta2, eps,
       weight_decay, -step_size, bc2_sqrt);
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int vg_adam_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                           int64_t n, double beta1, double beta2, float eps, float weight_decay,
+                           const double* lr, const int32_t* step, void* stream) {
+  if (n < 0 || !lr || !step || (n > 0 && (!param || !grad || !exp_avg || !exp_avg_sq)))
+    return VG_EINVAL;
+  if (n == 0) return 0;
+  int blocks = vg_blocks(n, 256);
+  if (blocks > 2048) blocks = 2048;
+  k_adam_dev<<<blocks, 256, 0, static_cast<hipStream_t>(stream)>>>(
+      param, grad, exp_avg, exp_avg_sq, n, beta1, beta2, eps, weight_decay, lr, step);
   VG_CHECK_LAUNCH();
   return 0;
 }

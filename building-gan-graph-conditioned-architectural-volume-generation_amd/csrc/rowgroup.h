@@ -1,0 +1,168 @@
+// Row-group helpers shared by the message-passing kernels (wave64).
+//
+// A ROW (destination node of the CSR, or source node of the CSC) is owned by a
+// group of L contiguous lanes (L = 8/16/32/64); each lane owns CPL contiguous
+// channels and moves them with one vector load (VEC) when the row stride and
+// base pointer allow it.
+#pragma once
+#include "common.h"
+
+namespace vg {
+
+constexpr int kBlock = 256;
+constexpr float kSoftmaxEps = 1e-16f;
+
+// ---- vector helpers over CPL contiguous floats --------------------------
+template <int CPL>
+struct Vec {
+  float v[CPL];
+};
+
+template <int CPL, bool VEC>
+__device__ __forceinline__ void load_row(Vec<CPL>& r, const float* __restrict__ base, int c0, int C) {
+  if (VEC) {
+    if (c0 < C) {
+      if constexpr (CPL == 8) {  // VEC with CPL 8 requires C % 8 == 0 (pick_fused_shape)
+        const float4 t = *reinterpret_cast<const float4*>(base + c0);
+        const float4 u = *reinterpret_cast<const float4*>(base + c0 + 4);
+        r.v[0] = t.x; r.v[1] = t.y; r.v[2] = t.z; r.v[3] = t.w;
+        r.v[4] = u.x; r.v[5] = u.y; r.v[6] = u.z; r.v[7] = u.w;
+      } else if constexpr (CPL == 4) {
+        const float4 t = *reinterpret_cast<const float4*>(base + c0);
+        r.v[0] = t.x; r.v[1] = t.y; r.v[2] = t.z; r.v[3] = t.w;
+      } else if constexpr (CPL == 2) {
+        const float2 t = *reinterpret_cast<const float2*>(base + c0);
+        r.v[0] = t.x; r.v[1] = t.y;
+      } else {
+        r.v[0] = base[c0];
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < CPL; ++q) r.v[q] = 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) r.v[q] = (c0 + q < C) ? base[c0 + q] : 0.f;
+  }
+}
+
+template <int CPL, bool VEC>
+__device__ __forceinline__ void store_row(const Vec<CPL>& r, float* __restrict__ base, int c0, int C) {
+  if (VEC) {
+    if (c0 < C) {
+      if constexpr (CPL == 8) {
+        *reinterpret_cast<float4*>(base + c0) = make_float4(r.v[0], r.v[1], r.v[2], r.v[3]);
+        *reinterpret_cast<float4*>(base + c0 + 4) = make_float4(r.v[4], r.v[5], r.v[6], r.v[7]);
+      } else if constexpr (CPL == 4) {
+        *reinterpret_cast<float4*>(base + c0) = make_float4(r.v[0], r.v[1], r.v[2], r.v[3]);
+      } else if constexpr (CPL == 2) {
+        *reinterpret_cast<float2*>(base + c0) = make_float2(r.v[0], r.v[1]);
+      } else {
+        base[c0] = r.v[0];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < CPL; ++q)
+      if (c0 + q < C) base[c0 + q] = r.v[q];
+  }
+}
+
+struct GroupIdx {
+  int row;   // logical row (destination or source node) owned by the group
+  int lane;  // lane inside the group
+  int base;  // wave lane id of the group's lane 0
+};
+
+template <int L>
+__device__ __forceinline__ GroupIdx group_index() {
+  constexpr int groups_per_block = kBlock / L;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  GroupIdx g;
+  g.row = lb * groups_per_block + threadIdx.x / L;
+  g.lane = threadIdx.x & (L - 1);
+  g.base = (threadIdx.x & 63) & ~(L - 1);
+  return g;
+}
+
+
+template <int CPL, bool VEC>
+__device__ __forceinline__ float dot_row(const Vec<CPL>& a, const Vec<CPL>& b) {
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) s = fmaf(a.v[q], b.v[q], s);
+  return s;
+}
+
+// ---- shape dispatch -------------------------------------------------------
+struct Shape {
+  int L, CPL;
+  bool vec;
+};
+
+inline bool pick_shape(int C, Shape& sh) {
+  if (C <= 0) return false;
+  if (C <= 8) sh = {8, 1, true};
+  else if (C <= 16) sh = {16, 1, true};
+  else if (C <= 32) sh = {32, 1, true};
+  else if (C <= 64) sh = {64, 1, true};
+  else if (C <= 128) sh = {64, 2, (C % 2) == 0};
+  else if (C <= 256) sh = {64, 4, (C % 4) == 0};
+  else return false;
+  return true;
+}
+
+#define VG_DISPATCH(C, KERNEL_CALL)                                    \
+  do {                                                                 \
+    ::vg::Shape sh;                                                    \
+    if (!::vg::pick_shape(C, sh)) return VG_EINVAL;                    \
+    if (sh.L == 8) { constexpr int L_ = 8, CPL_ = 1; constexpr bool V_ = true; KERNEL_CALL; } \
+    else if (sh.L == 16) { constexpr int L_ = 16, CPL_ = 1; constexpr bool V_ = true; KERNEL_CALL; } \
+    else if (sh.L == 32) { constexpr int L_ = 32, CPL_ = 1; constexpr bool V_ = true; KERNEL_CALL; } \
+    else if (sh.CPL == 1) { constexpr int L_ = 64, CPL_ = 1; constexpr bool V_ = true; KERNEL_CALL; } \
+    else if (sh.CPL == 2 && sh.vec) { constexpr int L_ = 64, CPL_ = 2; constexpr bool V_ = true; KERNEL_CALL; } \
+    else if (sh.CPL == 2) { constexpr int L_ = 64, CPL_ = 2; constexpr bool V_ = false; KERNEL_CALL; } \
+    else if (sh.vec) { constexpr int L_ = 64, CPL_ = 4; constexpr bool V_ = true; KERNEL_CALL; } \
+    else { constexpr int L_ = 64, CPL_ = 4; constexpr bool V_ = false; KERNEL_CALL; } \
+  } while (0)
+
+inline int grid_for(int N, int L) { return vg_blocks(N, kBlock / L); }
+
+// Shapes of the fused GAT kernels: narrow lane groups with wide per-lane
+// vectors, so a wave keeps 4-8 destination rows (and their independent
+// latency chains) in flight and the per-edge group reductions are short.
+//   C in  9..16 : L  8 x 2      17..32 : L  8 x 4      33..64 : L 16 x 4
+//        65..128: L 16 x 8     129..256: L 32 x 8
+inline bool pick_fused_shape(int C, Shape& sh) {
+  if (C <= 8 || C > 256) return false;
+  if (C <= 16) sh = {8, 2, (C % 2) == 0};
+  else if (C <= 32) sh = {8, 4, (C % 4) == 0};
+  else if (C <= 64) sh = {16, 4, (C % 4) == 0};
+  else if (C <= 128) sh = {16, 8, (C % 8) == 0};
+  else sh = {32, 8, (C % 8) == 0};
+  return true;
+}
+
+#define VG_DISPATCH_FUSED(C, KERNEL_CALL)                                                        \
+  do {                                                                                           \
+    ::vg::Shape sh;                                                                              \
+    if (!::vg::pick_fused_shape(C, sh)) return VG_EINVAL;                                        \
+    if (sh.L == 8 && sh.CPL == 2) {                                                              \
+      if (sh.vec) { constexpr int L_ = 8, CPL_ = 2; constexpr bool V_ = true; KERNEL_CALL; }     \
+      else { constexpr int L_ = 8, CPL_ = 2; constexpr bool V_ = false; KERNEL_CALL; }           \
+    } else if (sh.L == 8) {                                                                      \
+      if (sh.vec) { constexpr int L_ = 8, CPL_ = 4; constexpr bool V_ = true; KERNEL_CALL; }     \
+      else { constexpr int L_ = 8, CPL_ = 4; constexpr bool V_ = false; KERNEL_CALL; }           \
+    } else if (sh.L == 16 && sh.CPL == 4) {                                                      \
+      if (sh.vec) { constexpr int L_ = 16, CPL_ = 4; constexpr bool V_ = true; KERNEL_CALL; }    \
+      else { constexpr int L_ = 16, CPL_ = 4; constexpr bool V_ = false; KERNEL_CALL; }          \
+    } else if (sh.L == 16) {                                                                     \
+      if (sh.vec) { constexpr int L_ = 16, CPL_ = 8; constexpr bool V_ = true; KERNEL_CALL; }    \
+      else { constexpr int L_ = 16, CPL_ = 8; constexpr bool V_ = false; KERNEL_CALL; }          \
+    } else {                                                                                     \
+      if (sh.vec) { constexpr int L_ = 32, CPL_ = 8; constexpr bool V_ = true; KERNEL_CALL; }    \
+      else { constexpr int L_ = 32, CPL_ = 8; constexpr bool V_ = false; KERNEL_CALL; }          \
+    }                                                                                            \
+  } while (0)
+
+}  // namespace vg

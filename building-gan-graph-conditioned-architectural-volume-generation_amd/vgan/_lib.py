@@ -21,9 +21,11 @@ _c_i32, _c_i64, _c_f32, _c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, c
 SIGNATURES = {
     "vg_csr_ws_ints": (_c_i64, [_c_i64, _c_i32]),
     "vg_csr_build": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
-    "vg_gat_fwd": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p]),
-    "vg_gat_bwd": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p,
-                                  _c_f32, _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "vg_gat_fwd": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p,
+                                  _c_p, _c_p]),
+    "vg_gat_bwd_ws_floats": (_c_i64, [_c_i32, _c_i32, _c_i32]),
+    "vg_gat_bwd": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p,
+                                  _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "vg_spmm": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p]),
     "vg_spmm_t": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p]),
     "vg_sddmm": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p]),
@@ -41,6 +43,12 @@ SIGNATURES = {
     "vg_far_per_graph": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32,
                                         _c_f32, _c_i32, _c_p, _c_p, _c_p]),
     "vg_confusion": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_p]),
+    "vg_gemm": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32,
+                               _c_i32, _c_p]),
+    "vg_gemm_tn_ws_floats": (_c_i64, [_c_i32, _c_i32, _c_i32]),
+    "vg_gemm_tn": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p]),
+    "vg_adam_dev": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_i64, ctypes.c_double, ctypes.c_double, _c_f32, _c_f32,
+                                   _c_p, _c_p, _c_p]),
     "vg_adam": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_i64, _c_f32, _c_f32, _c_f32, _c_f32, _c_f32, _c_f32,
                                _c_f32, _c_p]),
 }

@@ -74,6 +74,12 @@ class FlatAdam(torch.optim.Optimizer):
         self.exp_avg = torch.zeros_like(flat.param)
         self.exp_avg_sq = torch.zeros_like(flat.param)
         self.step_count = 0
+        dev = flat.param.device
+        # device-resident step count and learning rate: a captured hipGraph
+        # replays correct bias corrections and follows the LR scheduler
+        self.step_t = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.lr_t = torch.full((1,), float(lr), dtype=torch.float64, device=dev)
+        self._lr_host = float(lr)
 
     @classmethod
     def from_optimizer(cls, flat: FlatParams, opt: Optional[torch.optim.Optimizer]) -> "FlatAdam":
@@ -89,20 +95,34 @@ class FlatAdam(torch.optim.Optimizer):
         g = (self.source or self).param_groups[0]
         return {"lr": g["lr"], "betas": g["betas"], "eps": g["eps"], "weight_decay": g.get("weight_decay", 0.0)}
 
+    def sync_lr(self) -> None:
+        """Copy the (scheduler-driven) learning rate to the device; call outside
+        graph capture (the trainer does it before every step)."""
+        lr = float(self.hyper()["lr"])
+        if lr != self._lr_host:
+            self.lr_t.fill_(lr)
+            self._lr_host = lr
+
     @torch.no_grad()
     def step(self, closure=None):
         self.step_count += 1
         h = self.hyper()
         b1, b2 = h["betas"]
-        ops.adam_flat(self.flat.param, self.flat.grad, self.exp_avg, self.exp_avg_sq, h["lr"], b1, b2, h["eps"],
-                      h["weight_decay"], self.step_count)
+        if not self.flat.param.is_cuda:
+            raise RuntimeError("FlatAdam runs on the HIP path only")
+        if not torch.cuda.is_current_stream_capturing():
+            self.sync_lr()
+        self.step_t.add_(1)
+        ops.adam_flat_dev(self.flat.param, self.flat.grad, self.exp_avg, self.exp_avg_sq, b1, b2, h["eps"],
+                          h["weight_decay"], self.lr_t, self.step_t)
         return None
 
     def zero_grad(self, set_to_none: bool = False):
         self.flat.zero_grad()
 
     def state_dict_flat(self) -> Dict[str, object]:
-        return {"step": self.step_count, "exp_avg": self.exp_avg.clone(), "exp_avg_sq": self.exp_avg_sq.clone()}
+        return {"step": int(self.step_t.item()), "exp_avg": self.exp_avg.clone(),
+                "exp_avg_sq": self.exp_avg_sq.clone()}
 
 
 def param_iter(modules: Iterable[nn.Module]):

@@ -13,8 +13,8 @@ Drop-in for ``building_gan/src/models.py``:
   same initialisers (torch defaults for Linear, glorot for GATConv), so the
   same seed yields the same initial weights.
 
-Every GATConv block runs ``gat_aggregate`` (fused logits + segment softmax +
-aggregation) followed by ``graphnorm_relu_dropout`` (GraphNorm with batch=None,
+Every GATConv block runs ``gat_conv`` (fused attention projections, logits,
+segment softmax, aggregation and bias) followed by ``graphnorm_relu_dropout`` (GraphNorm with batch=None,
 ReLU and Dropout in one op).  The type-matched mean, CSR and float one-hot are
 per-batch data and are computed once per mini-batch (``vgan.data``).
 """
@@ -28,6 +28,7 @@ import torch.nn as nn
 
 from . import data as vdata
 from . import ops
+from .nn import Linear, linear
 from .rng import RNG
 
 _CONV_TYPES = ("GCNCONV", "GRAPHCONV", "GATCONV", "GATV2CONV")
@@ -69,10 +70,8 @@ class GATConv(nn.Module):
             self.bias.zero_()
 
     def forward(self, x: torch.Tensor, csr: ops.CSR) -> torch.Tensor:
-        h = torch.nn.functional.linear(x, self.lin.weight)
-        a_src = torch.mv(h, self.att_src.view(-1))
-        a_dst = torch.mv(h, self.att_dst.view(-1))
-        return ops.gat_aggregate(csr, h, a_src, a_dst, self.bias, self.negative_slope)
+        h = linear(x, self.lin.weight)
+        return ops.gat_conv(csr, h, self.att_src, self.att_dst, self.bias, self.negative_slope)
 
 
 class GraphNorm(nn.Module):
@@ -122,7 +121,7 @@ class GATEncoder(nn.Module):
 def _mlp(widths: List[int], norm: bool, act) -> nn.Sequential:
     mods: List[nn.Module] = []
     for a, b in zip(widths[:-1], widths[1:]):
-        mods.append(nn.Linear(a, b))
+        mods.append(Linear(a, b))
         if norm:
             mods.append(nn.LayerNorm(b))
         mods.append(act())
@@ -154,7 +153,7 @@ class VoxelGNNGenerator(nn.Module):
         self.encoder = GATEncoder(hg, cfg.GENERATOR_ENCODER_REPEAT, cfg.ENCODER_DROPOUT_RATE)
         dec = list(_mlp([hl + voxel_graph_dim + zd + self.encoder.out_channels + hg, hg, hg // 2, hg // 4, hg // 8],
                         True, lrelu).children())
-        dec.append(nn.Linear(hg // 8, cfg.NUM_CLASSES))
+        dec.append(Linear(hg // 8, cfg.NUM_CLASSES))
         self.decoder = nn.Sequential(*dec)
         self.rng = RNG(getattr(cfg, "runtime", {}).get("rng", "device"))
         self.tau = 1.0
@@ -188,7 +187,7 @@ class VoxelGNNDiscriminator(nn.Module):
         self.mlp_encoder = _mlp([local_graph_dim + voxel_graph_dim + cfg.NUM_CLASSES, hd, hd], False, relu)
         self.encoder = GATEncoder(hd, cfg.DISCRIMINATOR_ENCODER_REPEAT, cfg.ENCODER_DROPOUT_RATE)
         dec = list(_mlp([hd, hd // 2, hd // 4, hd // 8], False, relu).children())
-        dec.append(nn.Linear(hd // 8, 1))
+        dec.append(Linear(hd // 8, 1))
         if not cfg.USE_WGANGP:
             dec.append(nn.Sigmoid())
         self.decoder = nn.Sequential(*dec)

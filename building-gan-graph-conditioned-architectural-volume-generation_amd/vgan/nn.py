@@ -1,0 +1,106 @@
+"""Dense layers of the path on the hand-written f32 MFMA GEMMs.
+
+``Linear`` is ``torch.nn.Linear`` (same parameters, same initialisation, same
+state_dict keys) whose forward, input gradient and weight/bias gradient run on
+``vg_gemm`` / ``vg_gemm_tn`` (csrc/gemm.hip).  Library GEMMs cost 19 us at
+minimum per call on these tall-skinny shapes and 77-692 us for the weight
+gradient (profiles/r01_*).  With ``create_graph=True`` (the WGAN-GP second
+order) the backward is built from the differentiable matmuls _MMnt / _MMnn /
+_MMtn (same kernels, each one's adjoints expressed with the others), so double
+backward keeps working and stays on the MFMA path.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch.autograd import Function
+
+from . import ops
+
+
+class _MMnt(Function):
+    """C = A B^T on vg_gemm; closed under differentiation with _MMnn / _MMtn."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        ctx.save_for_backward(a, b)
+        return ops.gemm(a, b, True)
+
+    @staticmethod
+    def backward(ctx, gc):
+        a, b = ctx.saved_tensors
+        ga = _MMnn.apply(gc, b) if ctx.needs_input_grad[0] else None
+        gb = _MMtn.apply(gc, a) if ctx.needs_input_grad[1] else None
+        return ga, gb
+
+
+class _MMnn(Function):
+    """C = A B."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        ctx.save_for_backward(a, b)
+        return ops.gemm(a, b, False)
+
+    @staticmethod
+    def backward(ctx, gc):
+        a, b = ctx.saved_tensors
+        ga = _MMnt.apply(gc, b) if ctx.needs_input_grad[0] else None
+        gb = _MMtn.apply(a, gc) if ctx.needs_input_grad[1] else None
+        return ga, gb
+
+
+class _MMtn(Function):
+    """C = A^T B (split-K over the long dimension)."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        ctx.save_for_backward(a, b)
+        return ops.gemm_tn(a, b, want_colsum=False)[0]
+
+    @staticmethod
+    def backward(ctx, gc):
+        a, b = ctx.saved_tensors
+        ga = _MMnt.apply(b, gc) if ctx.needs_input_grad[0] else None
+        gb = _MMnn.apply(a, gc) if ctx.needs_input_grad[1] else None
+        return ga, gb
+
+
+class _LinearFn(Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, act):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return ops.gemm(x, weight, True, bias, act)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        gx = gw = gb = None
+        if torch.is_grad_enabled():  # create_graph: differentiable MFMA matmuls
+            gy = gy.contiguous()
+            if ctx.needs_input_grad[0]:
+                gx = _MMnn.apply(gy, weight)
+            if ctx.needs_input_grad[1]:
+                gw = _MMtn.apply(gy, x)
+            if ctx.has_bias and ctx.needs_input_grad[2]:
+                gb = gy.sum(0)
+            return gx, gw, gb, None
+        gy = gy.contiguous()
+        if ctx.needs_input_grad[0]:
+            gx = ops.gemm(gy, weight, False)
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            gw, gb = ops.gemm_tn(gy, x, want_colsum=ctx.has_bias)
+        return gx, gw, (gb if ctx.has_bias else None), None
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
+    if x.dim() != 2 or not x.is_cuda:
+        return F.linear(x, weight, bias)
+    return _LinearFn.apply(x.contiguous(), weight, bias, ops.ACT_NONE)
+
+
+class Linear(nn.Linear):
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return linear(x, self.weight, self.bias)

@@ -1,9 +1,9 @@
 """Differentiable operators over the HIP C ABI.
 
 Fast path
-    ``gat_aggregate``        one fused kernel forward (logits + segment softmax +
-                             weighted gather-sum + bias), two fused kernels for the
-                             first-order backward (no atomics).
+    ``gat_conv``             one fused kernel forward (attention projections,
+                             logits, segment softmax, weighted gather-sum, bias),
+                             three kernels for the first-order backward (no atomics).
     ``graphnorm_relu_dropout`` stats + apply forward, partial/final/apply backward.
     ``gumbel_head``          row kernel forward/backward.
 
@@ -37,7 +37,8 @@ class CSR:
     per mini-batch (replaces remove_self_loops/add_self_loops in every layer)."""
 
     def __init__(self, edge_index: torch.Tensor, num_nodes: int):
-        require_cuda(edge_index)
+        if not edge_index.is_cuda:
+            raise RuntimeError("vgan HIP ops require tensors on a ROCm device (no CPU fallback)")
         if edge_index.dtype != torch.long or edge_index.dim() != 2 or edge_index.shape[0] != 2:
             raise ValueError("edge_index must be int64 [2, E]")
         dev = edge_index.device
@@ -285,53 +286,69 @@ def gat_aggregate_composed(csr, h, a_src, a_dst, bias, slope: float = NEG_SLOPE)
 
 
 # --------------------------------------------------------- fused GATConv
-class _GATAggregate(Function):
+def gat_conv_composed(csr, h, att_src, att_dst, bias, slope: float = NEG_SLOPE):
+    """GATConv after the projection, from differentiable primitives only."""
+    a_src = (h * att_src.view(1, -1)).sum(1)
+    a_dst = (h * att_dst.view(1, -1)).sum(1)
+    return gat_aggregate_composed(csr, h, a_src, a_dst, bias, slope)
+
+
+class _GATConv(Function):
     @staticmethod
-    def forward(ctx, h, a_src, a_dst, bias, csr, slope):
-        h, a_src, a_dst = _f32(h), _f32(a_src), _f32(a_dst)
-        b = _f32(bias) if bias is not None else None
-        require_cuda(h, a_src, a_dst, b)
+    def forward(ctx, h, att_src, att_dst, bias, csr, slope):
+        h = _f32(h)
+        vs, vd, b = _f32(att_src.reshape(-1)), _f32(att_dst.reshape(-1)), _f32(bias)
+        require_cuda(h, vs, vd, b)
         n, c = h.shape
-        if n != csr.num_nodes or a_src.numel() != n or a_dst.numel() != n or (b is not None and b.numel() != c):
-            raise ValueError("gat_aggregate: inconsistent shapes")
+        if n != csr.num_nodes or vs.numel() != c or vd.numel() != c or b.numel() != c:
+            raise ValueError("gat_conv: inconsistent shapes")
+        dev = h.device
         out = torch.empty_like(h)
-        alpha = torch.empty(csr.num_edges, dtype=torch.float32, device=h.device)
-        check(LIB.vg_gat_fwd(ptr(csr.row_ptr), ptr(csr.col), n, c, ptr(h), ptr(a_src), ptr(a_dst), ptr(b),
-                             float(slope), ptr(out), ptr(alpha), csr.stream()), "vg_gat_fwd")
-        ctx.csr, ctx.slope, ctx.has_bias = csr, slope, bias is not None
-        ctx.save_for_backward(h, a_src, a_dst, bias if bias is not None else h.new_empty(0), alpha)
+        alpha = torch.empty(csr.num_edges, dtype=torch.float32, device=dev)
+        a_src = torch.empty(n, dtype=torch.float32, device=dev)
+        a_dst = torch.empty(n, dtype=torch.float32, device=dev)
+        check(LIB.vg_gat_fwd(ptr(csr.row_ptr), ptr(csr.col), n, c, ptr(h), ptr(vs), ptr(vd), ptr(b), float(slope),
+                             ptr(out), ptr(alpha), ptr(a_src), ptr(a_dst), csr.stream()), "vg_gat_fwd")
+        ctx.csr, ctx.slope = csr, slope
+        ctx.save_for_backward(h, att_src, att_dst, bias, alpha, a_src, a_dst)
         return out
 
     @staticmethod
     def backward(ctx, g_out):
-        h, a_src, a_dst, bias, alpha = ctx.saved_tensors
+        h, att_src, att_dst, bias, alpha, a_src, a_dst = ctx.saved_tensors
         csr = ctx.csr
         if torch.is_grad_enabled():
-            # create_graph=True: the same backward formulas as vg_gat_bwd, written
-            # with the differentiable primitives on the saved inputs (alpha is
-            # recomputed from a_src / a_dst so its dependence on them is kept).
-            # autograd.grad on a re-run forward would double count: a_src and
-            # a_dst are themselves functions of h (a = h @ att).
-            g_h, g_as, g_ad = _gat_backward_composed(csr, h, a_src, a_dst, g_out, ctx.slope)
-            g_b = g_out.sum(0) if ctx.has_bias else None
-            return g_h, g_as.view_as(a_src), g_ad.view_as(a_dst), g_b, None, None
+            # create_graph=True: the backward formulas of vg_gat_bwd written with
+            # differentiable primitives on the saved inputs, so the returned
+            # gradients carry their own graph (WGAN-GP second order).
+            vs, vd = att_src.reshape(1, -1), att_dst.reshape(1, -1)
+            a_s = (h * vs).sum(1)
+            a_d = (h * vd).sum(1)
+            g_h, g_as, g_ad = _gat_backward_composed(csr, h, a_s, a_d, g_out, ctx.slope)
+            g_h = g_h + g_as.unsqueeze(1) * vs + g_ad.unsqueeze(1) * vd
+            g_vs = (h * g_as.unsqueeze(1)).sum(0).view_as(att_src)
+            g_vd = (h * g_ad.unsqueeze(1)).sum(0).view_as(att_dst)
+            return g_h, g_vs, g_vd, g_out.sum(0), None, None
         g_out = _f32(g_out)
         n, c = h.shape
         dev = h.device
-        g_pre = torch.empty(csr.num_edges, dtype=torch.float32, device=dev)
         g_h = torch.empty_like(h)
-        g_as = torch.empty(n, dtype=torch.float32, device=dev)
-        g_ad = torch.empty(n, dtype=torch.float32, device=dev)
+        g_vs = torch.empty(c, dtype=torch.float32, device=dev)
+        g_vd = torch.empty_like(g_vs)
+        g_b = torch.empty_like(g_vs)
+        ws = torch.empty(int(LIB.vg_gat_bwd_ws_floats(n, csr.num_edges, c)), dtype=torch.float32, device=dev)
         check(LIB.vg_gat_bwd(ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot), ptr(csr.csc_dst),
-                             n, c, ptr(h), ptr(a_src), ptr(a_dst), ptr(alpha), ptr(g_out), float(ctx.slope),
-                             ptr(g_pre), ptr(g_h), ptr(g_as), ptr(g_ad), csr.stream()), "vg_gat_bwd")
-        g_b = g_out.sum(0) if (ctx.has_bias and ctx.needs_input_grad[3]) else None
-        return g_h, g_as.view_as(a_src), g_ad.view_as(a_dst), g_b, None, None
+                             n, csr.num_edges, c, ptr(h), ptr(_f32(att_src.reshape(-1))),
+                             ptr(_f32(att_dst.reshape(-1))), ptr(a_src), ptr(a_dst), ptr(alpha), ptr(g_out),
+                             float(ctx.slope), ptr(g_h), ptr(g_vs), ptr(g_vd), ptr(g_b), ptr(ws), csr.stream()),
+              "vg_gat_bwd")
+        return g_h, g_vs.view_as(att_src), g_vd.view_as(att_dst), g_b, None, None
 
 
-def gat_aggregate(csr: CSR, h, a_src, a_dst, bias, slope: float = NEG_SLOPE) -> torch.Tensor:
-    """GATConv (heads=1) attention + aggregation: see ``vg_gat_fwd``."""
-    return _GATAggregate.apply(h, a_src, a_dst, bias, csr, slope)
+def gat_conv(csr: CSR, h, att_src, att_dst, bias, slope: float = NEG_SLOPE) -> torch.Tensor:
+    """GATConv (heads=1) after the projection h = x W^T: attention projections,
+    segment softmax, aggregation and bias in one kernel (see ``vg_gat_fwd``)."""
+    return _GATConv.apply(h, att_src, att_dst, bias, csr, slope)
 
 
 # ------------------------------------------ GraphNorm + ReLU + Dropout
@@ -470,6 +487,50 @@ def confusion(truth, label, ptr_):
     return conf, conf_all
 
 
+# --------------------------------------------------------------- dense GEMMs
+ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
+
+
+def gemm(a: torch.Tensor, b: torch.Tensor, b_trans: bool, bias: Optional[torch.Tensor] = None,
+         act: int = ACT_NONE) -> torch.Tensor:
+    """C = a . (b^T if b_trans else b) (+ bias) (+ act), f32 MFMA (vg_gemm)."""
+    a, b = _f32(a), _f32(b)
+    bb = _f32(bias) if bias is not None else None
+    require_cuda(a, b, bb)
+    n, k = a.shape
+    m = b.shape[0] if b_trans else b.shape[1]
+    if (b.shape[1] if b_trans else b.shape[0]) != k:
+        raise ValueError("gemm: inner dimensions differ")
+    c = torch.empty(n, m, dtype=torch.float32, device=a.device)
+    check(LIB.vg_gemm(ptr(a), k, ptr(b), b.shape[1], 1 if b_trans else 0, ptr(bb), int(act), ptr(c), m, n, m, k,
+                      stream_handle(a.device)), "vg_gemm")
+    return c
+
+
+def gemm_tn(a: torch.Tensor, b: torch.Tensor, want_colsum: bool = True):
+    """(a^T . b, column sums of a): the weight / bias gradient of nn.Linear."""
+    a, b = _f32(a), _f32(b)
+    require_cuda(a, b)
+    n, m = a.shape
+    k = b.shape[1]
+    if b.shape[0] != n:
+        raise ValueError("gemm_tn: row counts differ")
+    c = torch.empty(m, k, dtype=torch.float32, device=a.device)
+    db = torch.empty(m, dtype=torch.float32, device=a.device) if want_colsum else None
+    ws = torch.empty(max(1, int(LIB.vg_gemm_tn_ws_floats(n, m, k))), dtype=torch.float32, device=a.device)
+    check(LIB.vg_gemm_tn(ptr(a), m, ptr(b), k, n, m, k, ptr(c), ptr(db), ptr(ws), stream_handle(a.device)),
+          "vg_gemm_tn")
+    return c, db
+
+
+def adam_flat_dev(param, grad, exp_avg, exp_avg_sq, beta1, beta2, eps, weight_decay, lr_t, step_t):
+    """vg_adam_dev: lr (float64 [1]) and the incremented step (int32 [1]) on the device."""
+    require_cuda(param, grad, exp_avg, exp_avg_sq, lr_t, step_t)
+    check(LIB.vg_adam_dev(ptr(param), ptr(grad), ptr(exp_avg), ptr(exp_avg_sq), param.numel(), float(beta1),
+                          float(beta2), float(eps), float(weight_decay), ptr(lr_t), ptr(step_t),
+                          stream_handle(param.device)), "vg_adam_dev")
+
+
 def adam_flat(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step: int):
     require_cuda(param, grad, exp_avg, exp_avg_sq)
     bc1 = 1.0 - beta1 ** step
@@ -480,7 +541,7 @@ def adam_flat(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_de
 
 
 __all__ = [
-    "CSR", "gat_aggregate", "gat_aggregate_composed", "graphnorm_relu_dropout", "type_mean", "gumbel_head",
+    "CSR", "gat_conv", "gat_conv_composed", "gat_aggregate_composed", "graphnorm_relu_dropout", "type_mean", "gumbel_head",
     "spmm", "spmm_t", "sddmm", "gather", "seg_sum", "seg_max", "scatter_src", "far_per_graph", "confusion",
     "adam_flat", "_lib",
 ]

@@ -11,6 +11,9 @@ penalty (``trainer.py:298``).
   the CPU default generator and copies them to the device -- the GPU path then
   sees bit-identical randomness to the reference CPU run (parity mode).
 * ``RNG("device")`` draws them on the GPU generator (fast mode; hipGraph-safe).
+* ``RNG("fixed")`` (tests only) hands out the same seeded tensors for the k-th
+  draw of every iteration body (``reset()`` at each body start), so an eager
+  step and a hipGraph replay see identical randomness.
 """
 from __future__ import annotations
 
@@ -20,10 +23,26 @@ import torch
 
 
 class RNG:
-    def __init__(self, mode: str = "device"):
-        if mode not in ("device", "host"):
-            raise ValueError("RNG mode must be 'device' or 'host'")
+    def __init__(self, mode: str = "device", seed: int = 0):
+        if mode not in ("device", "host", "fixed"):
+            raise ValueError("RNG mode must be 'device', 'host' or 'fixed'")
         self.mode = mode
+        self.seed = seed
+        self._k = 0
+        self._fixed = {}
+
+    def reset(self) -> None:
+        self._k = 0
+
+    def _fixed_draw(self, kind: str, shape, device, make):
+        key = (self._k, kind, tuple(shape))
+        self._k += 1
+        t = self._fixed.get(key)
+        if t is None:
+            g = torch.Generator(device="cpu").manual_seed(self.seed * 1000003 + len(self._fixed))
+            t = make(g).to(device)
+            self._fixed[key] = t
+        return t
 
     def _dev(self, device):
         return torch.device("cpu") if self.mode == "host" else device
@@ -32,16 +51,25 @@ class RNG:
         return t.to(device, non_blocking=True) if self.mode == "host" else t
 
     def normal(self, shape: Sequence[int], device) -> torch.Tensor:
+        if self.mode == "fixed":
+            return self._fixed_draw("n", shape, device, lambda g: torch.randn(*shape, generator=g))
         return self._out(torch.randn(*shape, device=self._dev(device)), device)
 
     def uniform(self, shape: Sequence[int], device) -> torch.Tensor:
+        if self.mode == "fixed":
+            return self._fixed_draw("u", shape, device, lambda g: torch.rand(*shape, generator=g))
         return self._out(torch.rand(*shape, device=self._dev(device)), device)
 
     def exponential(self, shape: Sequence[int], device) -> torch.Tensor:
+        if self.mode == "fixed":
+            return self._fixed_draw("e", shape, device, lambda g: torch.empty(*shape).exponential_(generator=g))
         return self._out(torch.empty(*shape, device=self._dev(device)).exponential_(), device)
 
     def keep_mask(self, shape: Sequence[int], p: float, device) -> torch.Tensor:
         """Dropout multiplier: Bernoulli(1 - p) / (1 - p), as ATen's CPU dropout."""
+        if self.mode == "fixed":
+            return self._fixed_draw("k", shape, device,
+                                    lambda g: torch.empty(*shape).bernoulli_(1 - p, generator=g).div_(1 - p))
         noise = torch.empty(*shape, device=self._dev(device)).bernoulli_(1 - p)
         noise.div_(1 - p)
         return self._out(noise, device)

@@ -134,6 +134,7 @@ class Trainer:
         cfg = self.configuration
         d_losses: List[torch.Tensor] = []
         for _ in range(cfg.N_CRITIC):
+            self.rng.reset()
             with torch.no_grad():
                 _, hard, soft = self._generate(local_graph, voxel_graph)
             self.adam_d.zero_grad()
@@ -143,6 +144,7 @@ class Trainer:
             self.sync.all_reduce_grad(self.flat_d)
             self.adam_d.step()
 
+        self.rng.reset()
         logits, hard, soft = self._generate(local_graph, voxel_graph)
         self.adam_g.zero_grad()
         d_params = list(self.discriminator.parameters())
@@ -159,6 +161,103 @@ class Trainer:
         self.sync.all_reduce_grad(self.flat_g)
         self.adam_g.step()
         return {"d_losses": torch.stack(d_losses), "g_loss": g_loss.detach(), "label_hard": hard.detach()}
+
+    # ------------------------------------------------- hipGraph-captured step
+    def _critic_body(self, local_graph, voxel_graph, acc, with_adam: bool):
+        self.rng.reset()
+        with torch.no_grad():
+            _, hard, soft = self._generate(local_graph, voxel_graph)
+        self.adam_d.zero_grad()
+        d_loss = self._compute_discriminator_loss(local_graph, voxel_graph, hard, soft)
+        d_loss.backward()
+        acc[0].add_(d_loss.detach())
+        if with_adam:
+            self.adam_d.step()
+
+    def _gen_body(self, local_graph, voxel_graph, acc, with_adam: bool):
+        self.rng.reset()
+        logits, hard, _ = self._generate(local_graph, voxel_graph)
+        self.adam_g.zero_grad()
+        d_params = list(self.discriminator.parameters())
+        if self.skip_dead_d_grads:
+            for p in d_params:
+                p.requires_grad_(False)
+        try:
+            g_loss = self._compute_generator_loss(local_graph, voxel_graph, logits, hard)
+            g_loss.backward()
+        finally:
+            if self.skip_dead_d_grads:
+                for p in d_params:
+                    p.requires_grad_(True)
+        acc[1].copy_(g_loss.detach())
+        if with_adam:
+            self.adam_g.step()
+        return hard.detach()
+
+    def _snapshot(self):
+        return [t.clone() for t in (self.flat_g.param, self.flat_d.param, self.adam_g.exp_avg, self.adam_g.exp_avg_sq,
+                                    self.adam_d.exp_avg, self.adam_d.exp_avg_sq, self.adam_g.step_t,
+                                    self.adam_d.step_t)]
+
+    def _restore(self, snap):
+        dst = (self.flat_g.param, self.flat_d.param, self.adam_g.exp_avg, self.adam_g.exp_avg_sq,
+               self.adam_d.exp_avg, self.adam_d.exp_avg_sq, self.adam_g.step_t, self.adam_d.step_t)
+        for d, s_ in zip(dst, snap):
+            d.copy_(s_)
+
+    def capture(self, local_graph, voxel_graph):
+        """Record the step of this (static) batch as two hipGraphs: one critic
+        iteration (replayed N_CRITIC times -- RNG, parameters and Adam state
+        advance in place) and the generator iteration.  Needs device RNG.  With
+        several ranks the RCCL all-reduce and Adam run eagerly between replays."""
+        if self.rng.mode == "host":
+            raise RuntimeError("graph capture needs device-side randomness (runtime['rng'] 'device')")
+        dev = voxel_graph.x.device
+        with_adam = not self.sync.active
+        acc = torch.zeros(2, dtype=torch.float32, device=dev)
+        vdata.prepared(local_graph, voxel_graph, self.configuration.NUM_CLASSES)  # CSR etc. before capture
+        self.adam_g.sync_lr()
+        self.adam_d.sync_lr()
+        snap = self._snapshot()
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):  # warm-up (lazy init) on a side stream, then undo it
+            self._critic_body(local_graph, voxel_graph, acc, with_adam)
+            self._gen_body(local_graph, voxel_graph, acc, with_adam)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self._restore(snap)
+        pool = getattr(self, "_graph_pool", None)
+        if pool is None:
+            pool = self._graph_pool = torch.cuda.graph_pool_handle()
+        g_critic, g_gen = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_critic, pool=pool):
+            self._critic_body(local_graph, voxel_graph, acc, with_adam)
+        with torch.cuda.graph(g_gen, pool=pool):
+            hard = self._gen_body(local_graph, voxel_graph, acc, with_adam)
+        self._restore(snap)
+        graphs = {"critic": g_critic, "gen": g_gen, "acc": acc, "hard": hard, "with_adam": with_adam}
+        voxel_graph.set_derived("step_graphs", graphs)
+        return graphs
+
+    def step_graphed(self, local_graph, voxel_graph) -> Dict[str, torch.Tensor]:
+        """``step`` replayed from hipGraphs (captured on first use per batch)."""
+        graphs = voxel_graph.derived("step_graphs") if callable(getattr(voxel_graph, "derived", None)) else None
+        if graphs is None:
+            graphs = self.capture(local_graph, voxel_graph)
+        self.adam_g.sync_lr()
+        self.adam_d.sync_lr()
+        acc = graphs["acc"]
+        acc.zero_()
+        for _ in range(self.configuration.N_CRITIC):
+            graphs["critic"].replay()
+            if not graphs["with_adam"]:
+                self.sync.all_reduce_grad(self.flat_d)
+                self.adam_d.step()
+        graphs["gen"].replay()
+        if not graphs["with_adam"]:
+            self.sync.all_reduce_grad(self.flat_g)
+            self.adam_g.step()
+        return {"d_loss_mean": acc[0] / self.configuration.N_CRITIC, "g_loss": acc[1], "label_hard": graphs["hard"]}
 
     # ------------------------------------------------------ orchestration
     def _train_each_epoch(self):

@@ -53,26 +53,33 @@ int vg_csr_build(const int64_t* edge_index, int64_t num_edges, int32_t num_nodes
 
 /* ---- GATConv(heads=1) message passing ----------------------------------- */
 
-/* Fused attention + aggregation for one GATConv layer:
- *   e_k   = leaky_relu(a_src[col_k] + a_dst[i], slope)
- *   alpha = segment softmax of e over row i  (max-shifted, denominator + 1e-16)
- *   out_i = sum_k alpha_k * h[col_k] + bias
- * Replaces GATConv.edge_update (utils/_softmax.py scatter max/sum) +
- * propagate/message/aggregate ('add' scatter) + bias, as called from
+/* One GATConv(heads=1) message-passing layer after the projection h = x W^T,
+ * fused into a single kernel:
+ *   a_dst_i = <h_i, att_dst>,  a_src_i = <h_i, att_src>       (written, [N] each)
+ *   e_k     = leaky_relu(a_src[col_k] + a_dst_i, slope)
+ *   alpha   = segment softmax of e over row i (max-shifted, denominator + 1e-16)
+ *   out_i   = sum_k alpha_k * h[col_k] + bias                   (alpha written, [E'])
+ * Replaces the (h*att).sum(-1) projections, GATConv.edge_update
+ * (utils/_softmax.py scatter max/sum) and propagate/message/aggregate ('add'
+ * scatter) + bias of torch_geometric/nn/conv/gat_conv.py as called from
  * models.py:144 (generator, 14 layers) and models.py:242 (discriminator, 6).
- * alpha (E') is written when non-NULL (kept for the backward); bias may be NULL. */
+ * att_src / att_dst / bias: [C] (any alignment). */
 int vg_gat_fwd(const int32_t* row_ptr, const int32_t* col, int32_t num_nodes, int32_t channels,
-               const float* h, const float* a_src, const float* a_dst, const float* bias,
-               float slope, float* out, float* alpha, void* stream);
+               const float* h, const float* att_src, const float* att_dst, const float* bias,
+               float slope, float* out, float* alpha, float* a_src, float* a_dst, void* stream);
+
+/* Workspace (floats) for vg_gat_bwd. */
+int64_t vg_gat_bwd_ws_floats(int32_t num_nodes, int32_t num_edges, int32_t channels);
 
 /* First-order backward of vg_gat_fwd (the autograd path without create_graph):
- *   g_pre[E'], g_a_dst[N]   (row pass)     and
- *   g_h[N,C],  g_a_src[N]   (source pass over the CSC; no atomics). */
+ * g_h [N,C] (including the att_src/att_dst projection terms), g_att_src,
+ * g_att_dst, g_bias [C].  Three passes, no atomics, deterministic. */
 int vg_gat_bwd(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,
                const int32_t* csc_slot, const int32_t* csc_dst, int32_t num_nodes,
-               int32_t channels, const float* h, const float* a_src, const float* a_dst,
-               const float* alpha, const float* g_out, float slope, float* g_pre,
-               float* g_h, float* g_a_src, float* g_a_dst, void* stream);
+               int32_t num_edges, int32_t channels, const float* h, const float* att_src,
+               const float* att_dst, const float* a_src, const float* a_dst, const float* alpha,
+               const float* g_out, float slope, float* g_h, float* g_att_src, float* g_att_dst,
+               float* g_bias, float* workspace, void* stream);
 
 /* Differentiable sparse primitives (their adjoints are each other), used to
  * build the twice-differentiable path the WGAN-GP needs (trainer.py:306-312,
@@ -161,6 +168,26 @@ int vg_far_per_graph(const float* x, int32_t x_stride, const float* label, int32
 int vg_confusion(const int64_t* truth, const float* label, int32_t classes, const int64_t* ptr,
                  int32_t num_graphs, int32_t* conf, int32_t* conf_all, void* stream);
 
+/* ---- dense layers (nn.Linear of the MLPs and the GATConv projection) ----- */
+
+/* C[N, M] = A[N, K] . op(B) (+ bias[M]) then act (0 none, 1 ReLU, 2 LeakyReLU 0.2).
+ * b_trans = 1: B is [M, K] (op = transpose; the nn.Linear forward X W^T);
+ * b_trans = 0: B is [K, M] (dX = dY W).  f32 MFMA (v_mfma_f32_32x32x2_f32).
+ * Replaces the torch.nn.Linear GEMMs at models.py:33-47,49-66,92-113,
+ * 177-185,212-220 and GATConv.lin. bias may be NULL. */
+int vg_gemm(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t b_trans,
+            const float* bias, int32_t act, float* C, int32_t ldc, int32_t N, int32_t M,
+            int32_t K, void* stream);
+
+/* Workspace (floats) for vg_gemm_tn. */
+int64_t vg_gemm_tn_ws_floats(int32_t N, int32_t M, int32_t K);
+
+/* C[M, K] = A[N, M]^T . B[N, K] and db[M] = sum_n A[n, :] (db may be NULL):
+ * the weight and bias gradients of nn.Linear, split over N in 256-row chunks,
+ * partials folded in chunk order (deterministic). */
+int vg_gemm_tn(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N, int32_t M,
+               int32_t K, float* C, float* db, float* workspace, void* stream);
+
 /* ---- optimiser ---------------------------------------------------------- */
 
 /* torch.optim.Adam (single-tensor semantics, weight_decay, no amsgrad) over one
@@ -171,6 +198,12 @@ int vg_confusion(const int64_t* truth, const float* label, int32_t classes, cons
 int vg_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
             float beta2, float one_minus_beta1, float one_minus_beta2, float eps,
             float weight_decay, float step_size, float bc2_sqrt, void* stream);
+
+/* vg_adam with the learning rate and the (already incremented) step count
+ * read from device memory, so a captured hipGraph replays correct updates. */
+int vg_adam_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                double beta1, double beta2, float eps, float weight_decay, const double* lr,
+                const int32_t* step, void* stream);
 
 #ifdef __cplusplus
 }

@@ -59,98 +59,76 @@ def test_csr_rejects_out_of_range(cuda):
         ops.CSR(torch.tensor([[0, 9], [1, 0]], device=cuda), 3)
 
 
-@pytest.mark.parametrize("C", [1, 2, 3, 4, 8, 16, 24, 32, 64, 100, 128, 130, 256])
-@pytest.mark.parametrize("stress", [False, True])
-def test_gat_forward_backward(cuda, C, stress):
-    torch.manual_seed(C)
-    _, vox = _graph(stress=stress)
-    n = vox.num_nodes
-    csr = ops.CSR(vox.edge_index.to(cuda), n)
-    h = torch.randn(n, C, dtype=torch.float64, requires_grad=True)
-    a_s = torch.randn(n, dtype=torch.float64, requires_grad=True)
-    a_d = torch.randn(n, dtype=torch.float64, requires_grad=True)
-    b = torch.randn(C, dtype=torch.float64, requires_grad=True)
-    ref = pyg.gat_propagate(h, a_s, a_d, vox.edge_index) + b
-    g_out = torch.randn(n, C, dtype=torch.float64)
-    ref_grads = torch.autograd.grad(ref, (h, a_s, a_d, b), g_out)
+def _star_graph(n=300):
+    """Lattice-free star: node 0 receives from every node (degree n-1 > 4*64)
+    plus a ring -- exercises every long-row fallback of the fused kernels."""
+    src = list(range(1, n)) + list(range(n)) + [(i + 1) % n for i in range(n)]
+    dst = [0] * (n - 1) + [(i + 1) % n for i in range(n)] + list(range(n))
+    ei = torch.tensor([src, dst], dtype=torch.long)
+    ei = torch.unique(ei, dim=1)
+    return ei, n
 
-    hc, asc, adc, bc = (t.detach().float().to(cuda).requires_grad_(True) for t in (h, a_s, a_d, b))
-    out = ops.gat_aggregate(csr, hc, asc, adc, bc)
+
+def _oracle_gat(h, att_s, att_d, b, ei):
+    return pyg.gat_propagate(h, h @ att_s, h @ att_d, ei) + b
+
+
+@pytest.mark.parametrize("C", [1, 2, 3, 4, 5, 8, 9, 16, 24, 32, 64, 100, 128, 130, 256])
+@pytest.mark.parametrize("graph", ["lattice", "stress", "star"])
+def test_gat_conv_forward_backward(cuda, C, graph):
+    torch.manual_seed(C)
+    if graph == "star":
+        ei, n = _star_graph()
+    else:
+        _, vox = _graph(stress=(graph == "stress"))
+        ei, n = vox.edge_index, vox.num_nodes
+    csr = ops.CSR(ei.to(cuda), n)
+    h = torch.randn(n, C, dtype=torch.float64, requires_grad=True)
+    att_s = (torch.randn(C, dtype=torch.float64) / C ** 0.5).requires_grad_(True)
+    att_d = (torch.randn(C, dtype=torch.float64) / C ** 0.5).requires_grad_(True)
+    b = torch.randn(C, dtype=torch.float64, requires_grad=True)
+    ref = _oracle_gat(h, att_s, att_d, b, ei)
+    g_out = torch.randn(n, C, dtype=torch.float64)
+    ref_grads = torch.autograd.grad(ref, (h, att_s, att_d, b), g_out)
+
+    gt = [t.detach().float().to(cuda).requires_grad_(True) for t in (h, att_s, att_d, b)]
+    out = ops.gat_conv(csr, *gt)
     assert rel_err(out, ref) < 1e-5
-    grads = torch.autograd.grad(out, (hc, asc, adc, bc), g_out.float().to(cuda))
+    grads = torch.autograd.grad(out, gt, g_out.float().to(cuda))
     for got, want in zip(grads, ref_grads):
         assert rel_err(got, want) < 1e-4
-    # the primitive re-expression (create_graph path) agrees with the fused kernel
-    comp = ops.gat_aggregate_composed(csr, hc, asc, adc, bc)
-    assert rel_err(comp, out) < 1e-6
+    comp = ops.gat_conv_composed(csr, *gt)
+    assert rel_err(comp, out) < 1e-5
 
 
-@pytest.mark.parametrize("C", [1, 8, 64])
-def test_gat_double_backward(cuda, C):
+@pytest.mark.parametrize("C", [1, 8, 64, 128])
+def test_gat_conv_double_backward(cuda, C):
+    """Second order (the WGAN-GP pattern): grad w.r.t. inputs with
+    create_graph, a penalty on it, and its grad w.r.t. everything."""
     torch.manual_seed(3 + C)
     _, vox = _graph((4,))
     n = vox.num_nodes
     csr = ops.CSR(vox.edge_index.to(cuda), n)
-    base = [torch.randn(n, C, dtype=torch.float64), torch.randn(n, dtype=torch.float64),
-            torch.randn(n, dtype=torch.float64), torch.randn(C, dtype=torch.float64)]
-    w1 = torch.randn(n, C, dtype=torch.float64)
-    w2 = [torch.randn_like(t) for t in base]
-
-    def second_order(fn, tensors, w1, w2):
-        out = fn(*tensors)
-        g = torch.autograd.grad((out * w1).sum(), tensors, create_graph=True)
-        s = sum((gi * wi).sum() for gi, wi in zip(g, w2))
-        res = torch.autograd.grad(s, tensors, allow_unused=True)
-        return [torch.zeros_like(t) if r is None else r for r, t in zip(res, tensors)]
-
-    ref_t = [t.clone().requires_grad_(True) for t in base]
-    ref = second_order(lambda h, a, d, b: pyg.gat_propagate(h, a, d, vox.edge_index) + b, ref_t, w1, w2)
-    gpu_t = [t.float().to(cuda).requires_grad_(True) for t in base]
-    got = second_order(lambda h, a, d, b: ops.gat_aggregate(csr, h, a, d, b), gpu_t, w1.float().to(cuda),
-                       [w.float().to(cuda) for w in w2])
-    for g, r in zip(got, ref):
-        assert rel_err(g, r) < 1e-4
-
-
-@pytest.mark.parametrize("C", [1, 16, 64])
-def test_gat_layer_double_backward_through_projection(cuda, C):
-    """a_src = h @ att_src inside the graph (as in GATConv): second-order grads
-    w.r.t. x and every parameter vs the oracle GATConv in float64."""
-    torch.manual_seed(11 + C)
-    _, vox = _graph((4,))
-    n = vox.num_nodes
-    csr = ops.CSR(vox.edge_index.to(cuda), n)
-    cin = 2 * C
-    conv = pyg.GATConv(cin, C).double()
-    with torch.no_grad():
-        conv.bias.uniform_(-0.3, 0.3)
-    x0 = torch.randn(n, cin, dtype=torch.float64)
+    cin = max(2, C // 2)
+    base = [torch.randn(n, cin, dtype=torch.float64), torch.randn(C, cin, dtype=torch.float64) / cin ** 0.5,
+            torch.randn(C, dtype=torch.float64) / C ** 0.5, torch.randn(C, dtype=torch.float64) / C ** 0.5,
+            torch.randn(C, dtype=torch.float64)]
     w1 = torch.randn(n, C, dtype=torch.float64)
 
-    def run(x, W, att_s, att_d, b, fn):
-        out = fn(x, W, att_s, att_d, b)
-        gx, = torch.autograd.grad((out * w1.to(out.device)).sum(), x, create_graph=True)
+    def run(x, W, a_s, a_d, b, fn, w1):
+        out = fn(x, W, a_s, a_d, b)
+        gx, = torch.autograd.grad((out * w1).sum(), x, create_graph=True)
         pen = (gx.norm(dim=1) - 1).pow(2).mean()
-        return torch.autograd.grad(pen, (x, W, att_s, att_d, b), allow_unused=True)
+        res = torch.autograd.grad(pen, (x, W, a_s, a_d, b), allow_unused=True)
+        return [torch.zeros_like(t) if r is None else r for r, t in zip(res, (x, W, a_s, a_d, b))]
 
-    def oracle_fn(x, W, a_s, a_d, b):
-        h = x @ W.t()
-        return pyg.gat_propagate(h, h @ a_s.view(-1), h @ a_d.view(-1), vox.edge_index) + b
-
-    def hip_fn(x, W, a_s, a_d, b):
-        h = x @ W.t()
-        return ops.gat_aggregate(csr, h, torch.mv(h, a_s.view(-1)), torch.mv(h, a_d.view(-1)), b)
-
-    params = [conv.lin.weight.detach(), conv.att_src.detach(), conv.att_dst.detach(), conv.bias.detach()]
-    rt = [x0.clone().requires_grad_(True)] + [p.clone().requires_grad_(True) for p in params]
-    ref = run(*rt, oracle_fn)
-    w1 = w1.float().to(cuda)
-    gt = [t.detach().float().to(cuda).requires_grad_(True) for t in rt]
-    got = run(*gt, hip_fn)
+    ref = run(*[t.clone().requires_grad_(True) for t in base],
+              lambda x, W, a_s, a_d, b: _oracle_gat(x @ W.t(), a_s, a_d, b, vox.edge_index), w1)
+    got = run(*[t.float().to(cuda).requires_grad_(True) for t in base],
+              lambda x, W, a_s, a_d, b: ops.gat_conv(csr, x @ W.t(), a_s, a_d, b), w1.float().to(cuda))
+    scale = max(float(r.norm()) for r in ref)
     for g, r in zip(got, ref):
-        if r is None:
-            continue
-        assert rel_err(g, r) < 1e-3
+        assert float((g.double().cpu() - r).norm()) <= 1e-4 * float(r.norm()) + 1e-7 * scale
 
 
 def test_sparse_primitives_adjoint_identities(cuda):
@@ -294,3 +272,60 @@ def test_adam_matches_torch(cuda):
         opt.step()
         ops.adam_flat(pc, g.to(cuda), m, v, 2e-4, 0.5, 0.999, 1e-8, 0.0, t)
     assert torch.allclose(pc.cpu(), ref.detach(), atol=1e-7, rtol=0)
+
+
+@pytest.mark.parametrize("n,k,m", [(12700, 128, 128), (1000, 524, 128), (333, 17, 128), (777, 64, 36),
+                                   (12700, 16, 8), (65, 8, 7), (3, 5, 1), (130, 33, 70)])
+def test_gemm_kernels_vs_fp64(cuda, n, k, m):
+    torch.manual_seed(n + k + m)
+    x = torch.randn(n, k, dtype=torch.float64)
+    w = torch.randn(m, k, dtype=torch.float64)
+    b = torch.randn(m, dtype=torch.float64)
+    gy = torch.randn(n, m, dtype=torch.float64)
+    xc, wc, bc, gc = (t.float().to(cuda) for t in (x, w, b, gy))
+    for act, ref_fn in ((ops.ACT_NONE, lambda v: v), (ops.ACT_RELU, torch.relu),
+                        (ops.ACT_LRELU, lambda v: torch.nn.functional.leaky_relu(v, 0.2))):
+        y = ops.gemm(xc, wc, True, bc, act)
+        assert rel_err(y, ref_fn(x @ w.t() + b)) < 1e-6
+    assert rel_err(ops.gemm(gc, wc, False), gy @ w) < 1e-6
+    gw, gb = ops.gemm_tn(gc, xc)
+    assert rel_err(gw, gy.t() @ x) < 1e-6 and rel_err(gb, gy.sum(0)) < 1e-6
+
+
+def test_linear_module_grads(cuda):
+    from vgan.nn import Linear
+
+    torch.manual_seed(0)
+    lin = Linear(40, 24).to(cuda)
+    ref = torch.nn.Linear(40, 24).double()
+    ref.load_state_dict({k: v.double().cpu() for k, v in lin.state_dict().items()})
+    x = torch.randn(500, 40, dtype=torch.float64, requires_grad=True)
+    xc = x.detach().float().to(cuda).requires_grad_(True)
+    gy = torch.randn(500, 24, dtype=torch.float64)
+    y = lin(xc)
+    yr = ref(x)
+    assert rel_err(y, yr) < 1e-6
+    gx, gw, gb = torch.autograd.grad(y, (xc, lin.weight, lin.bias), gy.float().to(cuda))
+    rx, rw, rb = torch.autograd.grad(yr, (x, ref.weight, ref.bias), gy)
+    assert rel_err(gx, rx) < 1e-6 and rel_err(gw, rw) < 1e-6 and rel_err(gb, rb) < 1e-6
+
+
+def test_linear_double_backward(cuda):
+    from vgan.nn import Linear
+
+    torch.manual_seed(1)
+    lin = Linear(24, 16).to(cuda)
+    ref = torch.nn.Linear(24, 16).double()
+    ref.load_state_dict({k: v.double().cpu() for k, v in lin.state_dict().items()})
+    x0 = torch.randn(300, 24, dtype=torch.float64)
+
+    def second(mod, x):
+        y = torch.tanh(mod(x))
+        gx, = torch.autograd.grad(y.sum(), x, create_graph=True)
+        pen = (gx.norm(dim=1) - 1).pow(2).mean()
+        return torch.autograd.grad(pen, (x, mod.weight, mod.bias))
+
+    r = second(ref, x0.clone().requires_grad_(True))
+    g = second(lin, x0.float().to(cuda).requires_grad_(True))
+    for a, b in zip(g, r):
+        assert rel_err(a, b) < 1e-5
