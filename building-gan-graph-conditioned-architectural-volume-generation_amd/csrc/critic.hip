@@ -1,0 +1,105 @@
+// Small kernels of the explicit WGAN-GP critic engine (vgan/critic.py).
+//
+// vg_critic_input  builds the stacked discriminator input of one critic
+//                  iteration: rows [0,N) real, [N,2N) fake, [2N,3N) the
+//                  gradient-penalty interpolate (trainer.py:298-301, 319-320):
+//                  X[c*N + n] = [ matched_voxel_x[n] | label_c[n] ],
+//                  label_mix = eps*real + (1-eps)*soft  (rounded as torch does:
+//                  two products then one add, no fused multiply-add).
+// vg_gp_head       from g = dD(mix)/dlabel [N,K] and the stacked scores:
+//                  gp = lambda * mean_n (|g_n| - 1)^2            (trainer.py:313-316)
+//                  loss = mean(D(fake)) - mean(D(real)) + gp       (trainer.py:326-328)
+//                  u0 = dgp/dg = (2 lambda / N) (|g_n| - 1)/|g_n| g_n   (the seed of the
+//                  engine's tangent pass; 0 where |g_n| = 0, as torch's norm backward).
+//                  One 1024-thread block, fixed reduction order.
+#include "common.h"
+
+namespace {
+
+__global__ void k_critic_input(const float* __restrict__ mvx, int N, int F,
+                               const float* __restrict__ real, const float* __restrict__ hard,
+                               const float* __restrict__ soft, const float* __restrict__ eps,
+                               int K, float* __restrict__ X) {
+  const int W = F + K;
+  const long long total = 3LL * N * W;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const long long r = t / W;
+    const int c = static_cast<int>(t - r * W);
+    const int cp = static_cast<int>(r / N);
+    const long long n = r - (long long)cp * N;
+    float v;
+    if (c < F) {
+      v = mvx[n * F + c];
+    } else {
+      const long long e = n * K + (c - F);
+      if (cp == 0) v = real[e];
+      else if (cp == 1) v = hard[e];
+      else {
+        const float a = eps[n];
+        v = __fadd_rn(__fmul_rn(a, real[e]), __fmul_rn(__fsub_rn(1.f, a), soft[e]));
+      }
+    }
+    X[t] = v;
+  }
+}
+
+__global__ void __launch_bounds__(1024) k_gp_head(const float* __restrict__ g, int N, int K,
+                                                  const float* __restrict__ scores, float lambda,
+                                                  float* __restrict__ u0, float* __restrict__ out) {
+  const int t = threadIdx.x;
+  const float coef = 2.f * lambda / static_cast<float>(N);
+  float gp = 0.f, sr = 0.f, sf = 0.f;
+  for (int n = t; n < N; n += 1024) {
+    const float* gr = g + (size_t)n * K;
+    float ss = 0.f;
+    for (int k = 0; k < K; ++k) ss = fmaf(gr[k], gr[k], ss);
+    const float nrm = sqrtf(ss);
+    const float d = nrm - 1.f;
+    gp = fmaf(d, d, gp);
+    const float f = nrm > 0.f ? coef * d / nrm : 0.f;
+    for (int k = 0; k < K; ++k) u0[(size_t)n * K + k] = f * gr[k];
+    sr += scores[n];
+    sf += scores[N + n];
+  }
+  __shared__ float red[3][1024];
+  red[0][t] = gp;
+  red[1][t] = sr;
+  red[2][t] = sf;
+  __syncthreads();
+  for (int s = 512; s > 0; s >>= 1) {
+    if (t < s)
+      for (int q = 0; q < 3; ++q) red[q][t] += red[q][t + s];
+    __syncthreads();
+  }
+  if (t == 0) {
+    const float fn = static_cast<float>(N);
+    const float gpv = red[0][0] / fn * lambda;
+    out[0] = (red[2][0] / fn - red[1][0] / fn) + gpv;
+    out[1] = gpv;
+  }
+}
+
+}  // namespace
+
+extern "C" int vg_critic_input(const float* mvx, int32_t N, int32_t F, const float* real,
+                               const float* hard, const float* soft, const float* eps, int32_t K,
+                               float* X, void* stream) {
+  if (N <= 0 || F < 0 || K <= 0 || (F > 0 && !mvx) || !real || !hard || !soft || !eps || !X)
+    return VG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  int blocks = vg_blocks(3LL * N * (F + K), 256);
+  if (blocks > 4096) blocks = 4096;
+  k_critic_input<<<blocks, 256, 0, s>>>(mvx, N, F, real, hard, soft, eps, K, X);
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int vg_gp_head(const float* g, int32_t N, int32_t K, const float* scores, float lambda,
+                          float* u0, float* out, void* stream) {
+  if (N <= 0 || K <= 0 || !g || !scores || !u0 || !out) return VG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  k_gp_head<<<1, 1024, 0, s>>>(g, N, K, scores, lambda, u0, out);
+  VG_CHECK_LAUNCH();
+  return 0;
+}

@@ -278,28 +278,6 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_ep(
   }
 }
 
-// ============================================================ block partials
-// Every group accumulates per-channel partials in registers over the rows it
-// visits (grid-stride); the block folds its groups through LDS and writes one
-// row of `part` ([gridDim.x][W]).  W <= 3 * 256.
-template <int L, int CPL>
-__device__ void block_partials(const Vec<CPL>* vals, int nvec, int C, float* __restrict__ part) {
-  constexpr int G = kBlock / L;
-  __shared__ float red[kBlock * 8 * 2];  // (256/L) groups x L*CPL channels (CPL <= 8) x up to 2 vectors
-  const int grp = threadIdx.x / L, lane = threadIdx.x & (L - 1);
-  const int Wg = L * CPL;
-  for (int v = 0; v < nvec; ++v)
-#pragma unroll
-    for (int q = 0; q < CPL; ++q) red[(grp * nvec + v) * Wg + lane * CPL + q] = vals[v].v[q];
-  __syncthreads();
-  for (int w = threadIdx.x; w < nvec * Wg; w += kBlock) {
-    const int v = w / Wg, c = w % Wg;
-    float s = 0.f;
-    for (int k = 0; k < G; ++k) s += red[(k * nvec + v) * Wg + c];
-    if (c < C) part[(size_t)blockIdx.x * nvec * C + v * C + c] = s;
-  }
-}
-
 // ================================================== backward B1 (destination)
 template <int L, int CPL, bool VEC>
 __global__ void __launch_bounds__(kBlock) k_gat_bwd_rows_cp(
@@ -487,8 +465,8 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src_cp(
     const int32_t* __restrict__ csc_dst, int N, int C, const float* __restrict__ h,
     const float* __restrict__ att_s, const float* __restrict__ att_d,
     const float* __restrict__ alpha, const float* __restrict__ g_out,
-    const float* __restrict__ g_pre, const float* __restrict__ g_ad, float* __restrict__ g_h,
-    float* __restrict__ part) {
+    const float* __restrict__ g_pre, const float* __restrict__ g_ad, const float* __restrict__ inj,
+    int inj_row0, float* __restrict__ g_h, float* __restrict__ part) {
   constexpr int G = kBlock / L;
   const int grp = threadIdx.x / L, lane = threadIdx.x & (L - 1);
   const int base = (threadIdx.x & 63) & ~(L - 1);
@@ -548,6 +526,12 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src_cp(
       acc.v[q] = fmaf(gas, vs.v[q], fmaf(gadj, vd.v[q], acc.v[q]));
       ps.v[q] = fmaf(gas, hj.v[q], ps.v[q]);
     }
+    if (inj && j >= inj_row0) {
+      Vec<CPL> iv;
+      load_row<CPL, VEC>(iv, inj + (size_t)(j - inj_row0) * C, c0, C);
+#pragma unroll
+      for (int q = 0; q < CPL; ++q) acc.v[q] += iv.v[q];
+    }
     store_row<CPL, VEC>(acc, g_h + (size_t)j * C, c0, C);
   }
   Vec<CPL> vals[1] = {ps};
@@ -560,8 +544,8 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src_ep(
     const int32_t* __restrict__ csc_dst, int N, int C, const float* __restrict__ h,
     const float* __restrict__ att_s, const float* __restrict__ att_d,
     const float* __restrict__ alpha, const float* __restrict__ g_out,
-    const float* __restrict__ g_pre, const float* __restrict__ g_ad, float* __restrict__ g_h,
-    float* __restrict__ part) {
+    const float* __restrict__ g_pre, const float* __restrict__ g_ad, const float* __restrict__ inj,
+    int inj_row0, float* __restrict__ g_h, float* __restrict__ part) {
   constexpr int L = 8, G = kBlock / L;
   const int grp = threadIdx.x / L, lane = threadIdx.x & (L - 1);
   float ps[CMAX];
@@ -591,6 +575,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src_ep(
 #pragma unroll
       for (int c = 0; c < CMAX; ++c)
         if (c == lane) v = acc[c];
+      if (inj && j >= inj_row0) v += inj[(size_t)(j - inj_row0) * C + lane];
       g_h[(size_t)j * C + lane] = fmaf(gas, att_s[lane], fmaf(gadj, att_d[lane], v));
     }
     if (lane == 0)
@@ -615,7 +600,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src_ep(
 // 1024-thread block per 64 columns, 16 waves stride over the partial rows,
 // LDS fold in a fixed order (deterministic).
 __global__ void __launch_bounds__(1024) k_fold_cols(const float* __restrict__ part, int rows, int W,
-                                                    int split, float* __restrict__ out_a,
+                                                    int split, int acc, float* __restrict__ out_a,
                                                     float* __restrict__ out_b) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int w = blockIdx.x * 64 + lane;
@@ -629,7 +614,8 @@ __global__ void __launch_bounds__(1024) k_fold_cols(const float* __restrict__ pa
     float v = 0.f;
 #pragma unroll
     for (int k = 0; k < 16; ++k) v += red[k][lane];
-    if (w < split) out_a[w] = v; else out_b[w - split] = v;
+    float* o = w < split ? out_a + w : out_b + (w - split);
+    *o = acc ? *o + v : v;
   }
 }
 
@@ -677,15 +663,17 @@ extern "C" int vg_gat_fwd(const int32_t* row_ptr, const int32_t* col, int32_t N,
   return 0;
 }
 
-extern "C" int vg_gat_bwd(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,
-                          const int32_t* csc_slot, const int32_t* csc_dst, int32_t N, int32_t E,
-                          int32_t C, const float* h, const float* att_src, const float* att_dst,
-                          const float* a_src, const float* a_dst, const float* alpha,
-                          const float* g_out, float slope, float* g_h, float* g_att_src,
-                          float* g_att_dst, float* g_bias, float* workspace, void* stream) {
+extern "C" int vg_gat_bwd_ex(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,
+                             const int32_t* csc_slot, const int32_t* csc_dst, int32_t N, int32_t E,
+                             int32_t C, const float* h, const float* att_src, const float* att_dst,
+                             const float* a_src, const float* a_dst, const float* alpha,
+                             const float* g_out, float slope, float* g_h, float* g_att_src,
+                             float* g_att_dst, float* g_bias, int32_t accumulate, const float* inj,
+                             int32_t inj_row0, float* workspace, void* stream) {
+  const bool pgrads = g_att_src != nullptr;
   if (N <= 0 || E <= 0 || !row_ptr || !col || !csc_ptr || !csc_slot || !csc_dst || !h ||
-      !att_src || !att_dst || !a_src || !a_dst || !alpha || !g_out || !g_h || !g_att_src ||
-      !g_att_dst || !g_bias || !workspace)
+      !att_src || !att_dst || !a_src || !a_dst || !alpha || !g_out || !g_h || !workspace ||
+      (pgrads && (!g_att_dst || !g_bias)) || inj_row0 < 0)
     return VG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
   float* g_pre = workspace;
@@ -700,7 +688,8 @@ extern "C" int vg_gat_bwd(const int32_t* row_ptr, const int32_t* col, const int3
     k_gat_bwd_rows_ep<CM><<<grid1, kBlock, 0, s>>>(row_ptr, col, N, C, h, a_src, a_dst, alpha,     \
                                                    g_out, slope, g_pre, g_ad, part1);             \
     k_gat_bwd_src_ep<CM><<<grid2, kBlock, 0, s>>>(csc_ptr, csc_slot, csc_dst, N, C, h, att_src,    \
-                                                  att_dst, alpha, g_out, g_pre, g_ad, g_h, part2); \
+                                                  att_dst, alpha, g_out, g_pre, g_ad, inj,         \
+                                                  inj_row0, g_h, part2);                           \
   } while (0)
     if (C <= 1) VG_EP(1);
     else if (C <= 2) VG_EP(2);
@@ -716,11 +705,27 @@ extern "C" int vg_gat_bwd(const int32_t* row_ptr, const int32_t* col, const int3
                              g_ad, part1)));
     VG_DISPATCH_FUSED(C, (k_gat_bwd_src_cp<L_, CPL_, V_><<<grid2, kBlock, 0, s>>>(
                              csc_ptr, csc_slot, csc_dst, N, C, h, att_src, att_dst, alpha, g_out,
-                             g_pre, g_ad, g_h, part2)));
+                             g_pre, g_ad, inj, inj_row0, g_h, part2)));
   }
-  // fold: part1 rows -> [g_bias | g_att_dst], part2 rows -> g_att_src
-  k_fold_cols<<<vg_blocks(2 * C, 64), 1024, 0, s>>>(part1, grid1, 2 * C, C, g_bias, g_att_dst);
-  k_fold_cols<<<vg_blocks(C, 64), 1024, 0, s>>>(part2, grid2, C, C, g_att_src, g_att_src);
+  if (pgrads) {
+    // fold: part1 rows -> [g_bias | g_att_dst], part2 rows -> g_att_src
+    k_fold_cols<<<vg_blocks(2 * C, 64), 1024, 0, s>>>(part1, grid1, 2 * C, C, accumulate, g_bias,
+                                                      g_att_dst);
+    k_fold_cols<<<vg_blocks(C, 64), 1024, 0, s>>>(part2, grid2, C, C, accumulate, g_att_src,
+                                                  g_att_src);
+  }
   VG_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int vg_gat_bwd(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,
+                          const int32_t* csc_slot, const int32_t* csc_dst, int32_t N, int32_t E,
+                          int32_t C, const float* h, const float* att_src, const float* att_dst,
+                          const float* a_src, const float* a_dst, const float* alpha,
+                          const float* g_out, float slope, float* g_h, float* g_att_src,
+                          float* g_att_dst, float* g_bias, float* workspace, void* stream) {
+  if (!g_att_src || !g_att_dst || !g_bias) return VG_EINVAL;
+  return vg_gat_bwd_ex(row_ptr, col, csc_ptr, csc_slot, csc_dst, N, E, C, h, att_src, att_dst,
+                       a_src, a_dst, alpha, g_out, slope, g_h, g_att_src, g_att_dst, g_bias, 0,
+                       nullptr, 0, workspace, stream);
 }

@@ -1,0 +1,289 @@
+// GATConv (heads = 1): tangent and second-order terms for the WGAN-GP double
+// backward (the critic engine, vgan/critic.py; trainer.py:306-316 with
+// create_graph=True).
+//
+// out = A(h) h + bias with alpha = softmax_row(lrelu(a_src[j] + a_dst[i])),
+// a_src = h att_src, a_dst = h att_dst.  Given a tangent u of h and the adjoint
+// g (= g_out, from the first backward) this computes
+//   J u      = sum_k alpha_k u_j + alpha'_k h_j,      alpha'_k = alpha_k (e'_k - ebar_i)
+//              e'_k = lam_k (u_j att_src + u_i att_dst),  lam_k = lrelu'(pre_k),
+//              ebar_i = sum alpha e'
+// and, for Q = <g, J u>, with per-edge U_k = <g_i, u_j>, H_k = <g_i, h_j>,
+// R_k = U_k + e'_k H_k and row means Hbar = sum alpha H, Rbar = sum alpha R:
+//   dQ/dpre_k   gz_k  = lam_k alpha_k (R_k - Rbar - (e'_k - ebar) Hbar - ebar (H_k - Hbar))
+//   dQ/dpre'_k  gzp_k = lam_k alpha_k (H_k - Hbar)
+//   dQ/dh_j     = sum_{k: src j} alpha'_k g_dst + (sum_{src j} gz) att_src + (sum_{row j} gz) att_dst
+//   dQ/datt_src = sum_j (sum_{src j} gz) h_j + (sum_{src j} gzp) u_j
+//   dQ/datt_dst = sum_i (sum_{row i} gz) h_i + (sum_{row i} gzp) u_i        (dQ/dbias = 0)
+// (checked against autograd double backward in float64, tests/critic_ref.py).
+//
+// Three row passes, deterministic (no atomics): per-node tangent projections,
+// destination rows (J u, per-edge gz / gzp / alpha', block partials of
+// dQ/datt_dst), source nodes over the CSC (dQ/dh, partials of dQ/datt_src),
+// then one fold that ADDS into g_att_src / g_att_dst.
+#include "rowgroup.h"
+
+namespace {
+
+using namespace vg;
+
+constexpr int kMaxBlocks = 512;
+
+template <int L, int CPL, bool VEC>
+__global__ void __launch_bounds__(kBlock) k_jvp_att(const float* __restrict__ u, int N, int C,
+                                                    const float* __restrict__ att_s,
+                                                    const float* __restrict__ att_d,
+                                                    float* __restrict__ up_src,
+                                                    float* __restrict__ up_dst) {
+  const GroupIdx g = group_index<L>();
+  if (g.row >= N) return;
+  const int c0 = g.lane * CPL;
+  Vec<CPL> vs, vd, ui;
+  load_row<CPL, false>(vs, att_s, c0, C);
+  load_row<CPL, false>(vd, att_d, c0, C);
+  load_row<CPL, VEC>(ui, u + (size_t)g.row * C, c0, C);
+  const float s = group_sum<L>(dot_row<CPL, VEC>(ui, vs));
+  const float d = group_sum<L>(dot_row<CPL, VEC>(ui, vd));
+  if (g.lane == 0) {
+    up_src[g.row] = s;
+    up_dst[g.row] = d;
+  }
+}
+
+// e_u / e_h: per-edge U, H written by the lane that reads them back (no restrict).
+template <int L, int CPL, bool VEC>
+__global__ void __launch_bounds__(kBlock) k_jvp_rows(
+    const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, int N, int C,
+    const float* __restrict__ h, const float* __restrict__ u, const float* __restrict__ gv,
+    const float* __restrict__ a_src, const float* __restrict__ a_dst,
+    const float* __restrict__ up_src, const float* __restrict__ up_dst,
+    const float* __restrict__ alpha, float slope, float* __restrict__ u_out, float* e_u,
+    float* e_h, float* __restrict__ e_gz, float* __restrict__ e_gzp, float* __restrict__ e_alp,
+    float* __restrict__ n_gad, float* __restrict__ part) {
+  constexpr int G = kBlock / L;
+  const int grp = threadIdx.x / L, lane = threadIdx.x & (L - 1);
+  const int c0 = lane * CPL;
+  Vec<CPL> pd;
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) pd.v[q] = 0.f;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  for (int i = lb * G + grp; i < N; i += gridDim.x * G) {
+    const int beg = row_ptr[i], end = row_ptr[i + 1];
+    const float adi = a_dst[i], updi = up_dst[i];
+    float eb = 0.f;
+    for (int k = beg + lane; k < end; k += L) {
+      const int j = col[k];
+      const float lam = (a_src[j] + adi) > 0.f ? 1.f : slope;
+      eb = fmaf(alpha[k], lam * (up_src[j] + updi), eb);
+    }
+    eb = group_sum<L>(eb);
+    Vec<CPL> gi, acc;
+    load_row<CPL, VEC>(gi, gv + (size_t)i * C, c0, C);
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) acc.v[q] = 0.f;
+    float hb = 0.f, rb = 0.f;
+    for (int k0 = beg; k0 < end; k0 += 4) {
+      const int nk = end - k0 < 4 ? end - k0 : 4;
+      Vec<CPL> uv[4], hv[4];
+      float a[4], ep[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (t < nk) {
+          const int k = k0 + t, j = col[k];
+          a[t] = alpha[k];
+          const float lam = (a_src[j] + adi) > 0.f ? 1.f : slope;
+          ep[t] = lam * (up_src[j] + updi);
+          load_row<CPL, VEC>(uv[t], u + (size_t)j * C, c0, C);
+          load_row<CPL, VEC>(hv[t], h + (size_t)j * C, c0, C);
+        }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (t < nk) {
+          const float U = group_sum<L>(dot_row<CPL, VEC>(gi, uv[t]));
+          const float H = group_sum<L>(dot_row<CPL, VEC>(gi, hv[t]));
+          const float alp = a[t] * (ep[t] - eb);
+#pragma unroll
+          for (int q = 0; q < CPL; ++q) acc.v[q] = fmaf(a[t], uv[t].v[q], fmaf(alp, hv[t].v[q], acc.v[q]));
+          hb = fmaf(a[t], H, hb);
+          rb = fmaf(a[t], fmaf(ep[t], H, U), rb);
+          const int k = k0 + t;
+          if (lane == ((k - beg) & (L - 1))) {
+            e_u[k] = U;
+            e_h[k] = H;
+          }
+        }
+    }
+    store_row<CPL, VEC>(acc, u_out + (size_t)i * C, c0, C);
+    float gad = 0.f, gpd = 0.f;
+    for (int k = beg + lane; k < end; k += L) {
+      const int j = col[k];
+      const float a = alpha[k];
+      const float lam = (a_src[j] + adi) > 0.f ? 1.f : slope;
+      const float ep = lam * (up_src[j] + updi);
+      const float U = e_u[k], H = e_h[k];
+      const float R = fmaf(ep, H, U);
+      const float gz = lam * a * (R - rb - (ep - eb) * hb - eb * (H - hb));
+      const float gzp = lam * a * (H - hb);
+      e_gz[k] = gz;
+      e_gzp[k] = gzp;
+      e_alp[k] = a * (ep - eb);
+      gad += gz;
+      gpd += gzp;
+    }
+    gad = group_sum<L>(gad);
+    gpd = group_sum<L>(gpd);
+    if (lane == 0) n_gad[i] = gad;
+    Vec<CPL> hi, ui;
+    load_row<CPL, VEC>(hi, h + (size_t)i * C, c0, C);
+    load_row<CPL, VEC>(ui, u + (size_t)i * C, c0, C);
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) pd.v[q] = fmaf(gad, hi.v[q], fmaf(gpd, ui.v[q], pd.v[q]));
+  }
+  block_partials<L, CPL>(&pd, 1, C, part);
+}
+
+template <int L, int CPL, bool VEC>
+__global__ void __launch_bounds__(kBlock) k_jvp_src(
+    const int32_t* __restrict__ csc_ptr, const int32_t* __restrict__ csc_slot,
+    const int32_t* __restrict__ csc_dst, int N, int C, const float* __restrict__ h,
+    const float* __restrict__ u, const float* __restrict__ gv, const float* __restrict__ att_s,
+    const float* __restrict__ att_d, const float* __restrict__ e_gz,
+    const float* __restrict__ e_gzp, const float* __restrict__ e_alp,
+    const float* __restrict__ n_gad, float* __restrict__ h_inj, float* __restrict__ part) {
+  constexpr int G = kBlock / L;
+  const int grp = threadIdx.x / L, lane = threadIdx.x & (L - 1);
+  const int c0 = lane * CPL;
+  Vec<CPL> vs, vd, ps;
+  load_row<CPL, false>(vs, att_s, c0, C);
+  load_row<CPL, false>(vd, att_d, c0, C);
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) ps.v[q] = 0.f;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  for (int j = lb * G + grp; j < N; j += gridDim.x * G) {
+    const int beg = csc_ptr[j], end = csc_ptr[j + 1];
+    float gas = 0.f, gps = 0.f;
+    for (int p = beg + lane; p < end; p += L) {
+      const int k = csc_slot[p];
+      gas += e_gz[k];
+      gps += e_gzp[k];
+    }
+    gas = group_sum<L>(gas);
+    gps = group_sum<L>(gps);
+    Vec<CPL> acc;
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) acc.v[q] = 0.f;
+    for (int p0 = beg; p0 < end; p0 += 4) {
+      const int np = end - p0 < 4 ? end - p0 : 4;
+      Vec<CPL> gd[4];
+      float a[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (t < np) {
+          const int p = p0 + t;
+          a[t] = e_alp[csc_slot[p]];
+          load_row<CPL, VEC>(gd[t], gv + (size_t)csc_dst[p] * C, c0, C);
+        }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (t < np)
+#pragma unroll
+          for (int q = 0; q < CPL; ++q) acc.v[q] = fmaf(a[t], gd[t].v[q], acc.v[q]);
+    }
+    const float gadj = n_gad[j];
+    Vec<CPL> hj, uj;
+    load_row<CPL, VEC>(hj, h + (size_t)j * C, c0, C);
+    load_row<CPL, VEC>(uj, u + (size_t)j * C, c0, C);
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) {
+      acc.v[q] = fmaf(gas, vs.v[q], fmaf(gadj, vd.v[q], acc.v[q]));
+      ps.v[q] = fmaf(gas, hj.v[q], fmaf(gps, uj.v[q], ps.v[q]));
+    }
+    store_row<CPL, VEC>(acc, h_inj + (size_t)j * C, c0, C);
+  }
+  block_partials<L, CPL>(&ps, 1, C, part);
+}
+
+// g_a[c] += sum_b part_a[b][c] (blockIdx.y == 0), g_b[c] += sum_b part_b[b][c] (== 1)
+__global__ void __launch_bounds__(1024) k_fold_add2(const float* __restrict__ part_a, int rows_a,
+                                                    const float* __restrict__ part_b, int rows_b,
+                                                    int C, float* __restrict__ g_a,
+                                                    float* __restrict__ g_b) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const float* part = blockIdx.y == 0 ? part_a : part_b;
+  const int rows = blockIdx.y == 0 ? rows_a : rows_b;
+  float s = 0.f;
+  if (c < C)
+    for (int r = wave; r < rows; r += 16) s += part[(size_t)r * C + c];
+  __shared__ float red[16][64];
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && c < C) {
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v += red[k][lane];
+    float* o = blockIdx.y == 0 ? g_a : g_b;
+    o[c] += v;
+  }
+}
+
+inline bool jvp_shape(int C, Shape& sh) {
+  if (C <= 0) return false;
+  if (C <= 8) {
+    sh = {8, 1, true};
+    return true;
+  }
+  return pick_fused_shape(C, sh);
+}
+
+#define VG_DISPATCH_JVP(C, KERNEL_CALL)                                                           \
+  do {                                                                                            \
+    if ((C) <= 8) { constexpr int L_ = 8, CPL_ = 1; constexpr bool V_ = true; KERNEL_CALL; }      \
+    else VG_DISPATCH_FUSED(C, KERNEL_CALL);                                                       \
+  } while (0)
+
+}  // namespace
+
+extern "C" int64_t vg_gat_jvp2_ws_floats(int32_t num_nodes, int32_t num_edges, int32_t channels) {
+  // e_u, e_h, e_gz, e_gzp, e_alp [E'] + up_src, up_dst, n_gad [N] + 2 partial blocks
+  return 5 * (int64_t)num_edges + 3 * (int64_t)num_nodes + 2 * (int64_t)kMaxBlocks * channels;
+}
+
+extern "C" int vg_gat_jvp2(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,
+                           const int32_t* csc_slot, const int32_t* csc_dst, int32_t N, int32_t E,
+                           int32_t C, const float* h, const float* u, const float* g_out,
+                           const float* att_src, const float* att_dst, const float* a_src,
+                           const float* a_dst, const float* alpha, float slope, float* u_out,
+                           float* h_inj, float* g_att_src, float* g_att_dst, float* workspace,
+                           void* stream) {
+  Shape sh;
+  if (N <= 0 || E <= 0 || !row_ptr || !col || !csc_ptr || !csc_slot || !csc_dst || !h || !u ||
+      !g_out || !att_src || !att_dst || !a_src || !a_dst || !alpha || !u_out || !h_inj ||
+      !g_att_src || !g_att_dst || !workspace || !jvp_shape(C, sh))
+    return VG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  float* e_u = workspace;
+  float* e_h = e_u + E;
+  float* e_gz = e_h + E;
+  float* e_gzp = e_gz + E;
+  float* e_alp = e_gzp + E;
+  float* up_src = e_alp + E;
+  float* up_dst = up_src + N;
+  float* n_gad = up_dst + N;
+  float* part_r = n_gad + N;
+  float* part_s = part_r + (size_t)kMaxBlocks * C;
+  int grid = grid_for(N, sh.L);
+  if (grid > kMaxBlocks) grid = kMaxBlocks;
+  VG_DISPATCH_JVP(C, (k_jvp_att<L_, CPL_, V_><<<grid_for(N, L_), kBlock, 0, s>>>(
+                         u, N, C, att_src, att_dst, up_src, up_dst)));
+  VG_DISPATCH_JVP(C, (k_jvp_rows<L_, CPL_, V_><<<grid, kBlock, 0, s>>>(
+                         row_ptr, col, N, C, h, u, g_out, a_src, a_dst, up_src, up_dst, alpha,
+                         slope, u_out, e_u, e_h, e_gz, e_gzp, e_alp, n_gad, part_r)));
+  VG_DISPATCH_JVP(C, (k_jvp_src<L_, CPL_, V_><<<grid, kBlock, 0, s>>>(
+                         csc_ptr, csc_slot, csc_dst, N, C, h, u, g_out, att_src, att_dst, e_gz,
+                         e_gzp, e_alp, n_gad, h_inj, part_s)));
+  k_fold_add2<<<dim3(vg_blocks(C, 64), 2), 1024, 0, s>>>(part_r, grid, part_s, grid, C, g_att_dst,
+                                                         g_att_src);
+  VG_CHECK_LAUNCH();
+  return 0;
+}

@@ -9,8 +9,11 @@
 //   k_gemm      C[N, M] = A[N, K] . op(B) (+ bias[M]) (+ activation)
 //               forward  (A = X, B = W [M, K], op = transpose)
 //               dX       (A = dY, B = W [M, K] read as [K', M'] = no transpose)
+//               ACT 3 multiplies by [aux > 0] (aux [N, M]): the ReLU mask of a
+//               layer folded into the GEMM that produces its adjoint/tangent
 //   k_gemm_tn   C[M, K] = A[N, M]^T . B[N, K] split over N (~768 workgroups),
-//               plus db[M] = sum_n A[n, :]; partials folded in chunk order.
+//               plus db[M] = sum_n A[n, :]; partials folded in chunk order,
+//               written or accumulated into C (row stride ldc).
 //               weight / bias gradient (A = dY, B = X)
 //
 // f32 in, f32 accumulate: the MFMA is an exact fmaf chain (no TF32 on gfx950),
@@ -29,9 +32,10 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int TM = 64, TN = 64, TK = 32, LDP = TK + 1;
 
 template <int ACT>
-__device__ __forceinline__ float act_fn(float v) {
+__device__ __forceinline__ float act_fn(float v, float aux) {
   if constexpr (ACT == 1) return v > 0.f ? v : 0.f;
   else if constexpr (ACT == 2) return v > 0.f ? v : 0.2f * v;
+  else if constexpr (ACT == 3) return aux > 0.f ? v : 0.f;
   else return v;
 }
 
@@ -42,6 +46,7 @@ template <bool BT, int ACT>
 __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int lda,
                                               const float* __restrict__ B, int ldb,
                                               const float* __restrict__ bias,
+                                              const float* __restrict__ aux, int ldaux,
                                               float* __restrict__ C, int ldc, int N, int M, int K) {
   __shared__ float As[2][TM][LDP];
   __shared__ float Bs[2][TN][LDP];  // Bs[j][k] = op(B)[k][j]
@@ -94,7 +99,10 @@ __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int l
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int n = n0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    if (n < N && m < M) C[(size_t)n * ldc + m] = act_fn<ACT>(acc[r] + bv);
+    if (n < N && m < M) {
+      const float av = ACT == 3 ? aux[(size_t)n * ldaux + m] : 0.f;
+      C[(size_t)n * ldc + m] = act_fn<ACT>(acc[r] + bv, av);
+    }
   }
 }
 
@@ -163,9 +171,11 @@ __global__ void __launch_bounds__(256) k_gemm_tn(const float* __restrict__ A, in
   }
 }
 
-// out[w] = sum_c part[c][w], fixed order; 1024 threads per 64 outputs, 16 rows in flight.
+// out[w / K][w % K] (row stride ldo) = sum_c part[c][w], fixed order (+= when acc);
+// 1024 threads per 64 outputs, 16 rows in flight.
 __global__ void __launch_bounds__(1024) k_fold_rows(const float* __restrict__ part, int rows,
-                                                    long long W, float* __restrict__ out) {
+                                                    long long W, int K, int ldo, int acc,
+                                                    float* __restrict__ out) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long long w = blockIdx.x * 64LL + lane;
   float s = 0.f;
@@ -178,24 +188,29 @@ __global__ void __launch_bounds__(1024) k_fold_rows(const float* __restrict__ pa
     float v = 0.f;
 #pragma unroll
     for (int k = 0; k < 16; ++k) v += red[k][lane];
-    out[w] = v;
+    float* o = out + (w / K) * ldo + (w % K);
+    *o = acc ? *o + v : v;
   }
 }
 
 }  // namespace
 
 extern "C" int vg_gemm(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t b_trans,
-                       const float* bias, int32_t act, float* C, int32_t ldc, int32_t N, int32_t M,
-                       int32_t K, void* stream) {
-  if (N < 0 || M <= 0 || K <= 0 || !A || !B || !C || act < 0 || act > 2) return VG_EINVAL;
+                       const float* bias, int32_t act, const float* aux, int32_t ldaux, float* C,
+                       int32_t ldc, int32_t N, int32_t M, int32_t K, void* stream) {
+  if (N < 0 || M <= 0 || K <= 0 || !A || !B || !C || act < 0 || act > 3) return VG_EINVAL;
+  if (act == 3 && !aux) return VG_EINVAL;
   if (N == 0) return 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
   dim3 grid((N + TM - 1) / TM, (M + TN - 1) / TN);
-#define VG_G(BT, ACT) k_gemm<BT, ACT><<<grid, 256, 0, s>>>(A, lda, B, ldb, bias, C, ldc, N, M, K)
+#define VG_G(BT, ACT) \
+  k_gemm<BT, ACT><<<grid, 256, 0, s>>>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, N, M, K)
   if (b_trans) {
-    if (act == 0) VG_G(true, 0); else if (act == 1) VG_G(true, 1); else VG_G(true, 2);
+    if (act == 0) VG_G(true, 0); else if (act == 1) VG_G(true, 1);
+    else if (act == 2) VG_G(true, 2); else VG_G(true, 3);
   } else {
-    if (act == 0) VG_G(false, 0); else if (act == 1) VG_G(false, 1); else VG_G(false, 2);
+    if (act == 0) VG_G(false, 0); else if (act == 1) VG_G(false, 1);
+    else if (act == 2) VG_G(false, 2); else VG_G(false, 3);
   }
 #undef VG_G
   VG_CHECK_LAUNCH();
@@ -219,11 +234,13 @@ extern "C" int64_t vg_gemm_tn_ws_floats(int32_t N, int32_t M, int32_t K) {
 }
 
 extern "C" int vg_gemm_tn(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N,
-                          int32_t M, int32_t K, float* C, float* db, float* workspace,
-                          void* stream) {
-  if (N < 0 || M <= 0 || K <= 0 || !A || !B || !C || !workspace) return VG_EINVAL;
+                          int32_t M, int32_t K, float* C, int32_t ldc, float* db, int32_t accumulate,
+                          float* workspace, void* stream) {
+  if (N < 0 || M <= 0 || K <= 0 || ldc < K || !A || !B || !C || !workspace) return VG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (N == 0) {
+    if (accumulate) return 0;
+    if (ldc != K) return VG_EINVAL;
     (void)hipMemsetAsync(C, 0, sizeof(float) * M * K, s);
     if (db) (void)hipMemsetAsync(db, 0, sizeof(float) * M, s);
     return 0;
@@ -235,8 +252,8 @@ extern "C" int vg_gemm_tn(const float* A, int32_t lda, const float* B, int32_t l
   dim3 grid((M + TM - 1) / TM, (K + TN - 1) / TN, chunks);
   k_gemm_tn<<<grid, 256, 0, s>>>(A, lda, B, ldb, N, M, K, rows, part, db ? pdb : nullptr);
   const long long W = (long long)M * K;
-  k_fold_rows<<<(int)((W + 63) / 64), 1024, 0, s>>>(part, chunks, W, C);
-  if (db) k_fold_rows<<<(M + 63) / 64, 1024, 0, s>>>(pdb, chunks, M, db);
+  k_fold_rows<<<(int)((W + 63) / 64), 1024, 0, s>>>(part, chunks, W, K, ldc, accumulate, C);
+  if (db) k_fold_rows<<<(M + 63) / 64, 1024, 0, s>>>(pdb, chunks, M, M, M, accumulate, db);
   VG_CHECK_LAUNCH();
   return 0;
 }

@@ -7,6 +7,19 @@
 //           g_x = (w/s)(gz - ms*A/N) - (w*B/(N*s*sigma)) (x - mu)   (0 if sigma == 0,
 //           matching torch's std backward mask), g_w = B, g_b = A, g_ms = -mu*w*A/s
 //
+// Segments: S independent row blocks of Ns rows each (the discriminator's
+// real / fake / mix copies stacked as one [3N, C] tensor) each normalise with
+// their own column statistics (stats [S][2C]); parameter gradients sum over
+// segments.
+//
+// Second order (the WGAN-GP critic engine, vgan/critic.py): for a tangent u of
+// x and the adjoint g_y of y, with p = g_y * keep * [z > 0], xt = x - mu,
+// c = x - ms*mu, d = sigma + eps:
+//   y'   = keep [z > 0] w (c'/d - c sigma'/d^2),  c' = u - ms*mean(u),
+//          sigma' = M / sigma,  M = mean(xt u)
+//   Q    = <g_y, y'>;  dQ/dw, dQ/dms and dQ/dx in closed form from the column
+//          sums (sum u, sum xt u, sum p, sum p u, sum p xt)   (k_gn_jvp2_*)
+//
 // The column statistics are a two-level deterministic reduction: R row-chunk
 // blocks per 64-column slab produce (count, mean, M2) Welford partials, a
 // finalize kernel merges them in a fixed order (Chan's formula), and the
@@ -57,6 +70,8 @@ __global__ void __launch_bounds__(kBlock) k_stats_partial(const float* __restric
   const int r0 = blockIdx.x * rows_per_chunk;
   const int r1 = min(N, r0 + rows_per_chunk);
   const bool col_ok = c < C && (lane & (ly.cw - 1)) < 64;
+  x += (size_t)blockIdx.z * N * C;  // segment
+  part += (size_t)blockIdx.z * gridDim.x * C * 3;
   Welford w = {0.f, 0.f, 0.f};
   if (col_ok) {
     for (int r = r0 + rsub; r < r1; r += rstep) {
@@ -94,6 +109,8 @@ __global__ void __launch_bounds__(256) k_stats_final(const float* __restrict__ p
                                                      int C, float* __restrict__ stats) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
+  part += (size_t)blockIdx.y * chunks * C * 3;  // segment
+  stats += (size_t)blockIdx.y * 2 * C;
   Welford acc = {0.f, 0.f, 0.f};
   if (c < C)
     for (int k = wave; k < chunks; k += 4) {
@@ -110,14 +127,15 @@ __global__ void __launch_bounds__(256) k_stats_final(const float* __restrict__ p
   }
 }
 
-__global__ void k_gn_apply(const float* __restrict__ x, long long total, int C,
+__global__ void k_gn_apply(const float* __restrict__ x, long long total, int C, long long seg_elems,
                            const float* __restrict__ w, const float* __restrict__ b,
                            const float* __restrict__ ms, const float* __restrict__ keep,
                            float eps, const float* __restrict__ stats, float* __restrict__ y) {
   for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
        t += (long long)gridDim.x * blockDim.x) {
     const int c = static_cast<int>(t % C);
-    const float mu = stats[c], sd = stats[C + c];
+    const float* st = stats + 2 * C * (t / seg_elems);
+    const float mu = st[c], sd = st[C + c];
     const float o = x[t] - mu * ms[c];
     const float z = (o / (sd + eps)) * w[c] + b[c];
     float r = z > 0.f ? z : 0.f;
@@ -140,6 +158,12 @@ __global__ void __launch_bounds__(kBlock) k_gn_bwd_partial(
   const int rows_per_chunk = (N + gridDim.x - 1) / gridDim.x;
   const int r0 = blockIdx.x * rows_per_chunk;
   const int r1 = min(N, r0 + rows_per_chunk);
+  const size_t so = (size_t)blockIdx.z * N * C;  // segment
+  x += so;
+  gy += so;
+  if (keep) keep += so;
+  stats += (size_t)blockIdx.z * 2 * C;
+  part += (size_t)blockIdx.z * gridDim.x * C * 2;
   float sa = 0.f, sb = 0.f;
   if (c < C) {
     const float mu = stats[c], s = stats[C + c] + eps, wc = w[c], bc = b[c], msc = ms[c];
@@ -176,80 +200,262 @@ __global__ void __launch_bounds__(kBlock) k_gn_bwd_partial(
 }
 
 __global__ void __launch_bounds__(256) k_gn_bwd_final(
-    const float* __restrict__ part, int chunks, int C, const float* __restrict__ w,
+    const float* __restrict__ part, int chunks, int C, int S, const float* __restrict__ w,
     const float* __restrict__ ms, float eps, const float* __restrict__ stats,
     float* __restrict__ sums, float* __restrict__ g_w, float* __restrict__ g_b,
-    float* __restrict__ g_ms) {
+    float* __restrict__ g_ms, int accumulate) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
-  float a = 0.f, bb = 0.f;
-  if (c < C)
-    for (int k = wave; k < chunks; k += 4) {
-      a += part[((size_t)k * C + c) * 2];
-      bb += part[((size_t)k * C + c) * 2 + 1];
-    }
   __shared__ float red[4][64][2];
-  red[wave][lane][0] = a;
-  red[wave][lane][1] = bb;
-  __syncthreads();
-  if (wave == 0 && c < C) {
-    a = (red[0][lane][0] + red[1][lane][0]) + (red[2][lane][0] + red[3][lane][0]);
-    bb = (red[0][lane][1] + red[1][lane][1]) + (red[2][lane][1] + red[3][lane][1]);
-    sums[c] = a;
-    sums[C + c] = bb;
-    g_w[c] = bb;
-    g_b[c] = a;
-    g_ms[c] = -stats[c] * w[c] * a / (stats[C + c] + eps);
+  float tw = 0.f, tb = 0.f, tm = 0.f;
+  for (int sg = 0; sg < S; ++sg) {
+    const float* pp = part + (size_t)sg * chunks * C * 2;
+    float a = 0.f, bb = 0.f;
+    if (c < C)
+      for (int k = wave; k < chunks; k += 4) {
+        a += pp[((size_t)k * C + c) * 2];
+        bb += pp[((size_t)k * C + c) * 2 + 1];
+      }
+    red[wave][lane][0] = a;
+    red[wave][lane][1] = bb;
+    __syncthreads();
+    if (wave == 0 && c < C) {
+      a = (red[0][lane][0] + red[1][lane][0]) + (red[2][lane][0] + red[3][lane][0]);
+      bb = (red[0][lane][1] + red[1][lane][1]) + (red[2][lane][1] + red[3][lane][1]);
+      const float* st = stats + (size_t)sg * 2 * C;
+      sums[(size_t)sg * 2 * C + c] = a;
+      sums[(size_t)sg * 2 * C + C + c] = bb;
+      tw += bb;
+      tb += a;
+      tm += -st[c] * w[c] * a / (st[C + c] + eps);
+    }
+    __syncthreads();
+  }
+  if (wave == 0 && c < C && g_w) {
+    g_w[c] = accumulate ? g_w[c] + tw : tw;
+    g_b[c] = accumulate ? g_b[c] + tb : tb;
+    g_ms[c] = accumulate ? g_ms[c] + tm : tm;
   }
 }
 
+// g_x (+ inj for elements t >= inj_off: the second-order adjoint of the
+// critic engine's mix copy)
 __global__ void k_gn_bwd_apply(const float* __restrict__ x, const float* __restrict__ gy,
                                long long total, int N, int C, const float* __restrict__ w,
                                const float* __restrict__ b, const float* __restrict__ ms,
                                const float* __restrict__ keep, float eps,
                                const float* __restrict__ stats, const float* __restrict__ sums,
+                               const float* __restrict__ inj, long long inj_off,
                                float* __restrict__ gx) {
   const float inv_n = 1.f / static_cast<float>(N);
+  const long long seg_elems = (long long)N * C;
   for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
        t += (long long)gridDim.x * blockDim.x) {
     const int c = static_cast<int>(t % C);
-    const float mu = stats[c], sd = stats[C + c], s = sd + eps;
+    const long long sg = t / seg_elems;
+    const float* st = stats + 2 * C * sg;
+    const float* sm = sums + 2 * C * sg;
+    const float mu = st[c], sd = st[C + c], s = sd + eps;
     const float wc = w[c], msc = ms[c];
     const float xv = x[t];
     const float xh = (xv - mu * msc) / s;
     const float z = xh * wc + b[c];
     float gz = z > 0.f ? gy[t] : 0.f;
     if (keep) gz *= keep[t];
-    const float A = sums[c], B = sums[C + c];
+    const float A = sm[c], B = sm[C + c];
     float g = (wc / s) * (gz - msc * A * inv_n);
     if (sd > 0.f) g -= (wc * B * inv_n / (s * sd)) * (xv - mu);
+    if (inj && t >= inj_off) g += inj[t - inj_off];
     gx[t] = g;
   }
 }
 
-}  // namespace
 
-extern "C" int64_t vg_graphnorm_ws_floats(int32_t num_nodes, int32_t channels) {
-  (void)num_nodes;
-  return (int64_t)kChunks * channels * 3 + 2 * (int64_t)channels;
+// ---------------------------------------------------------- second order
+// column sums for the tangent / second-order pass: [sum u, sum xt u, sum p,
+// sum p u, sum p xt] per column (plain sums, chunk order)
+__global__ void __launch_bounds__(kBlock) k_gn_jvp2_partial(
+    const float* __restrict__ x, const float* __restrict__ u, const float* __restrict__ gy, int N,
+    int C, const float* __restrict__ w, const float* __restrict__ b, const float* __restrict__ ms,
+    const float* __restrict__ keep, float eps, const float* __restrict__ stats,
+    float* __restrict__ part) {
+  const Lay ly = lay_for(C);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + (lane & (ly.cw - 1));
+  const int rsub = wave * ly.rpw + lane / ly.cw;
+  const int rstep = 4 * ly.rpw;
+  const int rows_per_chunk = (N + gridDim.x - 1) / gridDim.x;
+  const int r0 = blockIdx.x * rows_per_chunk;
+  const int r1 = min(N, r0 + rows_per_chunk);
+  float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    const float mu = stats[c], s = stats[C + c] + eps, wc = w[c], bc = b[c], msc = ms[c];
+    for (int r = r0 + rsub; r < r1; r += rstep) {
+      const size_t t = (size_t)r * C + c;
+      const float xv = x[t], uv = u[t];
+      const float xt = xv - mu;
+      const float z = ((xv - mu * msc) / s) * wc + bc;
+      float p = z > 0.f ? gy[t] : 0.f;
+      if (keep) p *= keep[t];
+      v[0] += uv;
+      v[1] = fmaf(xt, uv, v[1]);
+      v[2] += p;
+      v[3] = fmaf(p, uv, v[3]);
+      v[4] = fmaf(p, xt, v[4]);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 5; ++q)
+    for (int off = ly.cw; off < 64; off <<= 1) v[q] += __shfl_xor(v[q], off, 64);
+  __shared__ float s5[4][64][5];
+  if (lane < ly.cw)
+#pragma unroll
+    for (int q = 0; q < 5; ++q) s5[wave][lane][q] = v[q];
+  __syncthreads();
+  if (wave == 0 && lane < ly.cw && c < C) {
+    float* pp = part + ((size_t)blockIdx.x * C + c) * 5;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) pp[q] = (s5[0][lane][q] + s5[1][lane][q]) + (s5[2][lane][q] + s5[3][lane][q]);
+  }
 }
 
+// per column: mu' = mean u, M = mean(xt u), Sp, P1 = sum p c', P2 = sum p c;
+// g_w += P1/d - P2 M/(sigma d^2);  g_ms += w (-mu' Sp/d + mu Sp M/(sigma d^2))
+__global__ void __launch_bounds__(256) k_gn_jvp2_final(
+    const float* __restrict__ part, int chunks, int N, int C, const float* __restrict__ w,
+    const float* __restrict__ ms, float eps, const float* __restrict__ stats,
+    float* __restrict__ sums, float* __restrict__ g_w, float* __restrict__ g_ms) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < C)
+    for (int k = wave; k < chunks; k += 4) {
+      const float* pp = part + ((size_t)k * C + c) * 5;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) v[q] += pp[q];
+    }
+  __shared__ float red[4][64][5];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) red[wave][lane][q] = v[q];
+  __syncthreads();
+  if (wave == 0 && c < C) {
+#pragma unroll
+    for (int q = 0; q < 5; ++q) v[q] = (red[0][lane][q] + red[1][lane][q]) + (red[2][lane][q] + red[3][lane][q]);
+    const float inv_n = 1.f / static_cast<float>(N);
+    const float mu = stats[c], sd = stats[C + c], d = sd + eps, msc = ms[c], wc = w[c];
+    const float mup = v[0] * inv_n, M = v[1] * inv_n, Sp = v[2];
+    const float P1 = v[3] - msc * mup * Sp;
+    const float P2 = v[4] + (1.f - msc) * mu * Sp;
+    const float isd = sd > 0.f ? 1.f / sd : 0.f;
+    float* sm = sums + (size_t)c * 5;
+    sm[0] = mup;
+    sm[1] = M;
+    sm[2] = Sp;
+    sm[3] = P1;
+    sm[4] = P2;
+    g_w[c] += P1 / d - P2 * M * isd / (d * d);
+    g_ms[c] += wc * (-mup * Sp / d + mu * Sp * M * isd / (d * d));
+  }
+}
+
+// u_out = keep [z>0] w (c'/d - c sigma'/d^2);  x_inj = dQ/dx
+__global__ void k_gn_jvp2_apply(const float* __restrict__ x, const float* __restrict__ u,
+                                const float* __restrict__ gy, long long total, int N, int C,
+                                const float* __restrict__ w, const float* __restrict__ b,
+                                const float* __restrict__ ms, const float* __restrict__ keep,
+                                float eps, const float* __restrict__ stats,
+                                const float* __restrict__ sums, float* __restrict__ u_out,
+                                float* __restrict__ x_inj) {
+  const float fn = static_cast<float>(N);
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int c = static_cast<int>(t % C);
+    const float mu = stats[c], sd = stats[C + c], d = sd + eps;
+    const float wc = w[c], msc = ms[c];
+    const float* sm = sums + (size_t)c * 5;
+    const float mup = sm[0], M = sm[1], Sp = sm[2], P1 = sm[3], P2 = sm[4];
+    const float xv = x[t], uv = u[t];
+    const float xt = xv - mu, ut = uv - mup;
+    const float cc = xv - msc * mu, cp = uv - msc * mup;
+    const float z = (cc / d) * wc + b[c];
+    float mk = z > 0.f ? 1.f : 0.f;
+    if (keep) mk *= keep[t];
+    const float isd = sd > 0.f ? 1.f / sd : 0.f;
+    const float sigp = M * isd;
+    u_out[t] = mk * wc * (cp / d - cc * sigp / (d * d));
+    const float p = gy[t] * mk;
+    const float k1 = isd / (fn * d * d);  // 1 / (N sigma d^2)
+    float g = -P1 * xt * k1 - (p - msc * Sp / fn) * M * isd / (d * d) - P2 * ut * k1;
+    g += P2 * M * xt * (isd * isd / (d * d) + 2.f * isd / (d * d * d)) * isd / fn;
+    x_inj[t] = wc * g;
+  }
+}
+}  // namespace
+
 static inline int chunks_for(int N) { return N < kChunks * 16 ? (N + 15) / 16 : kChunks; }
+
+static inline int apply_blocks(long long total) {
+  int blocks = vg_blocks(total, 256);
+  return blocks > 2048 ? 2048 : blocks;
+}
+
+extern "C" int64_t vg_graphnorm_seg_ws_floats(int32_t segments, int32_t rows_per_segment,
+                                              int32_t channels) {
+  (void)rows_per_segment;
+  return (int64_t)segments * kChunks * channels * 5 + 5 * (int64_t)segments * channels;
+}
+
+extern "C" int64_t vg_graphnorm_ws_floats(int32_t num_nodes, int32_t channels) {
+  return vg_graphnorm_seg_ws_floats(1, num_nodes, channels);
+}
+
+extern "C" int vg_graphnorm_fwd_seg(const float* x, int32_t S, int32_t N, int32_t C,
+                                    const float* weight, const float* bias,
+                                    const float* mean_scale, const float* keep, float eps,
+                                    float* y, float* stats, float* ws, void* stream) {
+  if (S <= 0 || N <= 0 || C <= 0 || !x || !weight || !bias || !mean_scale || !y || !stats || !ws)
+    return VG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int chunks = chunks_for(N);
+  dim3 grid(chunks, (C + 63) / 64, S);
+  k_stats_partial<<<grid, kBlock, 0, s>>>(x, N, C, ws);
+  k_stats_final<<<dim3(vg_blocks(C, 64), S), 256, 0, s>>>(ws, chunks, C, stats);
+  const long long total = (long long)S * N * C;
+  k_gn_apply<<<apply_blocks(total), 256, 0, s>>>(x, total, C, (long long)N * C, weight, bias,
+                                                 mean_scale, keep, eps, stats, y);
+  VG_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int vg_graphnorm_fwd(const float* x, int32_t N, int32_t C, const float* weight,
                                 const float* bias, const float* mean_scale, const float* keep,
                                 float eps, float* y, float* stats, float* ws, void* stream) {
-  if (N <= 0 || C <= 0 || !x || !weight || !bias || !mean_scale || !y || !stats || !ws)
+  return vg_graphnorm_fwd_seg(x, 1, N, C, weight, bias, mean_scale, keep, eps, y, stats, ws,
+                              stream);
+}
+
+extern "C" int vg_graphnorm_bwd_seg(const float* x, int32_t S, int32_t N, int32_t C,
+                                    const float* weight, const float* bias,
+                                    const float* mean_scale, const float* keep, float eps,
+                                    const float* stats, const float* g_y, float* g_x, float* g_w,
+                                    float* g_b, float* g_ms, int32_t accumulate, const float* inj,
+                                    int64_t inj_offset, float* ws, void* stream) {
+  if (S <= 0 || N <= 0 || C <= 0 || !x || !weight || !bias || !mean_scale || !stats || !g_y ||
+      !g_x || !ws || (g_w && (!g_b || !g_ms)) || inj_offset < 0)
     return VG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int chunks = chunks_for(N);
-  dim3 grid(chunks, (C + 63) / 64);
-  k_stats_partial<<<grid, kBlock, 0, s>>>(x, N, C, ws);
-  k_stats_final<<<vg_blocks(C, 64), 256, 0, s>>>(ws, chunks, C, stats);
-  const long long total = (long long)N * C;
-  int blocks = vg_blocks(total, 256);
-  if (blocks > 2048) blocks = 2048;
-  k_gn_apply<<<blocks, 256, 0, s>>>(x, total, C, weight, bias, mean_scale, keep, eps, stats, y);
+  float* part = ws;
+  float* sums = ws + (size_t)S * kChunks * C * 5;
+  dim3 grid(chunks, (C + 63) / 64, S);
+  k_gn_bwd_partial<<<grid, kBlock, 0, s>>>(x, g_y, N, C, weight, bias, mean_scale, keep, eps,
+                                           stats, part);
+  k_gn_bwd_final<<<vg_blocks(C, 64), 256, 0, s>>>(part, chunks, C, S, weight, mean_scale, eps,
+                                                  stats, sums, g_w, g_b, g_ms, accumulate);
+  const long long total = (long long)S * N * C;
+  k_gn_bwd_apply<<<apply_blocks(total), 256, 0, s>>>(x, g_y, total, N, C, weight, bias,
+                                                     mean_scale, keep, eps, stats, sums, inj,
+                                                     (long long)inj_offset, g_x);
   VG_CHECK_LAUNCH();
   return 0;
 }
@@ -258,23 +464,32 @@ extern "C" int vg_graphnorm_bwd(const float* x, int32_t N, int32_t C, const floa
                                 const float* bias, const float* mean_scale, const float* keep,
                                 float eps, const float* stats, const float* g_y, float* g_x,
                                 float* g_w, float* g_b, float* g_ms, float* ws, void* stream) {
-  if (N <= 0 || C <= 0 || !x || !weight || !bias || !mean_scale || !stats || !g_y || !g_x ||
-      !g_w || !g_b || !g_ms || !ws)
+  if (!g_w || !g_b || !g_ms) return VG_EINVAL;
+  return vg_graphnorm_bwd_seg(x, 1, N, C, weight, bias, mean_scale, keep, eps, stats, g_y, g_x,
+                              g_w, g_b, g_ms, 0, nullptr, 0, ws, stream);
+}
+
+extern "C" int vg_graphnorm_jvp2(const float* x, int32_t N, int32_t C, const float* weight,
+                                 const float* bias, const float* mean_scale, const float* keep,
+                                 float eps, const float* stats, const float* u, const float* g_y,
+                                 float* u_out, float* x_inj, float* g_w, float* g_ms, float* ws,
+                                 void* stream) {
+  if (N <= 0 || C <= 0 || !x || !weight || !bias || !mean_scale || !stats || !u || !g_y ||
+      !u_out || !x_inj || !g_w || !g_ms || !ws)
     return VG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int chunks = chunks_for(N);
   float* part = ws;
-  float* sums = ws + (size_t)kChunks * C * 3;
+  float* sums = ws + (size_t)kChunks * C * 5;
   dim3 grid(chunks, (C + 63) / 64);
-  k_gn_bwd_partial<<<grid, kBlock, 0, s>>>(x, g_y, N, C, weight, bias, mean_scale, keep, eps,
-                                           stats, part);
-  k_gn_bwd_final<<<vg_blocks(C, 64), 256, 0, s>>>(part, chunks, C, weight, mean_scale, eps,
-                                                  stats, sums, g_w, g_b, g_ms);
+  k_gn_jvp2_partial<<<grid, kBlock, 0, s>>>(x, u, g_y, N, C, weight, bias, mean_scale, keep, eps,
+                                            stats, part);
+  k_gn_jvp2_final<<<vg_blocks(C, 64), 256, 0, s>>>(part, chunks, N, C, weight, mean_scale, eps,
+                                                   stats, sums, g_w, g_ms);
   const long long total = (long long)N * C;
-  int blocks = vg_blocks(total, 256);
-  if (blocks > 2048) blocks = 2048;
-  k_gn_bwd_apply<<<blocks, 256, 0, s>>>(x, g_y, total, N, C, weight, bias, mean_scale, keep, eps,
-                                        stats, sums, g_x);
+  k_gn_jvp2_apply<<<apply_blocks(total), 256, 0, s>>>(x, u, g_y, total, N, C, weight, bias,
+                                                      mean_scale, keep, eps, stats, sums, u_out,
+                                                      x_inj);
   VG_CHECK_LAUNCH();
   return 0;
 }

@@ -165,4 +165,26 @@ inline bool pick_fused_shape(int C, Shape& sh) {
     }                                                                                            \
   } while (0)
 
+// ---- block partials ---------------------------------------------------------
+// Every group accumulates per-channel partials in registers over the rows it
+// visits (grid-stride); the block folds its groups through LDS and writes one
+// row of `part` ([gridDim.x][W]).  W <= 3 * 256.
+template <int L, int CPL>
+__device__ void block_partials(const Vec<CPL>* vals, int nvec, int C, float* __restrict__ part) {
+  constexpr int G = kBlock / L;
+  __shared__ float red[kBlock * 8 * 2];  // (256/L) groups x L*CPL channels (CPL <= 8) x up to 2 vectors
+  const int grp = threadIdx.x / L, lane = threadIdx.x & (L - 1);
+  const int Wg = L * CPL;
+  for (int v = 0; v < nvec; ++v)
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) red[(grp * nvec + v) * Wg + lane * CPL + q] = vals[v].v[q];
+  __syncthreads();
+  for (int w = threadIdx.x; w < nvec * Wg; w += kBlock) {
+    const int v = w / Wg, c = w % Wg;
+    float s = 0.f;
+    for (int k = 0; k < G; ++k) s += red[(k * nvec + v) * Wg + c];
+    if (c < C) part[(size_t)blockIdx.x * nvec * C + v * C + c] = s;
+  }
+}
+
 }  // namespace vg

@@ -43,10 +43,26 @@ SIGNATURES = {
     "vg_far_per_graph": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32,
                                         _c_f32, _c_i32, _c_p, _c_p, _c_p]),
     "vg_confusion": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_p]),
-    "vg_gemm": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32,
-                               _c_i32, _c_p]),
+    "vg_gemm": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_i32, _c_p, _c_i32, _c_i32,
+                               _c_i32, _c_i32, _c_p]),
     "vg_gemm_tn_ws_floats": (_c_i64, [_c_i32, _c_i32, _c_i32]),
-    "vg_gemm_tn": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p]),
+    "vg_gemm_tn": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_i32, _c_p,
+                                  _c_p]),
+    "vg_gat_bwd_ex": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p,
+                                     _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_i32, _c_p,
+                                     _c_p]),
+    "vg_gat_jvp2_ws_floats": (_c_i64, [_c_i32, _c_i32, _c_i32]),
+    "vg_gat_jvp2": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p,
+                                   _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "vg_graphnorm_seg_ws_floats": (_c_i64, [_c_i32, _c_i32, _c_i32]),
+    "vg_graphnorm_fwd_seg": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p,
+                                            _c_p, _c_p]),
+    "vg_graphnorm_bwd_seg": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p,
+                                            _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_i64, _c_p, _c_p]),
+    "vg_graphnorm_jvp2": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p,
+                                         _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "vg_critic_input": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_p]),
+    "vg_gp_head": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_f32, _c_p, _c_p, _c_p]),
     "vg_adam_dev": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_i64, ctypes.c_double, ctypes.c_double, _c_f32, _c_f32,
                                    _c_p, _c_p, _c_p]),
     "vg_adam": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_i64, _c_f32, _c_f32, _c_f32, _c_f32, _c_f32, _c_f32,

@@ -67,6 +67,31 @@ class CSR:
     def stream(self):
         return stream_handle(self.device)
 
+    def stacked(self, copies: int) -> "CSR":
+        """Block-diagonal CSR/CSC of ``copies`` copies of this graph (node ids and
+        edge slots offset per copy): several forwards over the same batch run
+        as one (the critic engine's real / fake / mix discriminator passes).
+        Cached; built with a few device ops, no host sync."""
+        cache = self.__dict__.setdefault("_stacked", {})
+        if copies in cache:
+            return cache[copies]
+        n, e = self.num_nodes, self.num_edges
+        k = torch.arange(copies, device=self.device, dtype=torch.int32)
+
+        def tile(a, step):
+            return (a.unsqueeze(0) + (k * step).unsqueeze(1)).reshape(-1).contiguous()
+
+        out = CSR.__new__(CSR)
+        out.num_nodes, out.num_edges, out.device = n * copies, e * copies, self.device
+        tail = torch.full((1,), e * copies, dtype=torch.int32, device=self.device)
+        out.row_ptr = torch.cat([tile(self.row_ptr[:-1], e), tail])
+        out.csc_ptr = torch.cat([tile(self.csc_ptr[:-1], e), tail])
+        out.col = tile(self.col, n)
+        out.csc_slot = tile(self.csc_slot, e)
+        out.csc_dst = tile(self.csc_dst, n)
+        cache[copies] = out
+        return out
+
 
 def _f32(t: torch.Tensor) -> torch.Tensor:
     if t.dtype != torch.float32:
@@ -502,8 +527,8 @@ def gemm(a: torch.Tensor, b: torch.Tensor, b_trans: bool, bias: Optional[torch.T
     if (b.shape[1] if b_trans else b.shape[0]) != k:
         raise ValueError("gemm: inner dimensions differ")
     c = torch.empty(n, m, dtype=torch.float32, device=a.device)
-    check(LIB.vg_gemm(ptr(a), k, ptr(b), b.shape[1], 1 if b_trans else 0, ptr(bb), int(act), ptr(c), m, n, m, k,
-                      stream_handle(a.device)), "vg_gemm")
+    check(LIB.vg_gemm(ptr(a), k, ptr(b), b.shape[1], 1 if b_trans else 0, ptr(bb), int(act), None, 0, ptr(c), m, n,
+                      m, k, stream_handle(a.device)), "vg_gemm")
     return c
 
 
@@ -518,7 +543,7 @@ def gemm_tn(a: torch.Tensor, b: torch.Tensor, want_colsum: bool = True):
     c = torch.empty(m, k, dtype=torch.float32, device=a.device)
     db = torch.empty(m, dtype=torch.float32, device=a.device) if want_colsum else None
     ws = torch.empty(max(1, int(LIB.vg_gemm_tn_ws_floats(n, m, k))), dtype=torch.float32, device=a.device)
-    check(LIB.vg_gemm_tn(ptr(a), m, ptr(b), k, n, m, k, ptr(c), ptr(db), ptr(ws), stream_handle(a.device)),
+    check(LIB.vg_gemm_tn(ptr(a), m, ptr(b), k, n, m, k, ptr(c), k, ptr(db), 0, ptr(ws), stream_handle(a.device)),
           "vg_gemm_tn")
     return c, db
 

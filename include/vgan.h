@@ -81,6 +81,47 @@ int vg_gat_bwd(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_pt
                const float* g_out, float slope, float* g_h, float* g_att_src, float* g_att_dst,
                float* g_bias, float* workspace, void* stream);
 
+/* vg_gat_bwd with options for the critic engine: g_att_src may be NULL (no
+ * parameter gradients; g_att_dst / g_bias are then ignored), parameter
+ * gradients are written (accumulate = 0) or added (1), and inj [N - inj_row0,
+ * C] (nullable) is added to the rows g_h[inj_row0:] (the second-order adjoint
+ * of the gradient-penalty copy).  Same workspace as vg_gat_bwd. */
+int vg_gat_bwd_ex(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,
+                  const int32_t* csc_slot, const int32_t* csc_dst, int32_t num_nodes,
+                  int32_t num_edges, int32_t channels, const float* h, const float* att_src,
+                  const float* att_dst, const float* a_src, const float* a_dst,
+                  const float* alpha, const float* g_out, float slope, float* g_h,
+                  float* g_att_src, float* g_att_dst, float* g_bias, int32_t accumulate,
+                  const float* inj, int32_t inj_row0, float* workspace, void* stream);
+
+/* Workspace (floats) for vg_gat_jvp2. */
+int64_t vg_gat_jvp2_ws_floats(int32_t num_nodes, int32_t num_edges, int32_t channels);
+
+/* Tangent and second-order terms of out = GATConv(h) for the gradient
+ * penalty's double backward (trainer.py:306-316, create_graph=True): given a
+ * tangent u of h and the first-backward adjoint g_out, u_out = J u and, for
+ * Q = <g_out, J u>, h_inj = dQ/dh; dQ/datt_src, dQ/datt_dst are ADDED to
+ * g_att_src, g_att_dst (dQ/dbias = 0).  Deterministic (no atomics). */
+int vg_gat_jvp2(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,
+                const int32_t* csc_slot, const int32_t* csc_dst, int32_t num_nodes,
+                int32_t num_edges, int32_t channels, const float* h, const float* u,
+                const float* g_out, const float* att_src, const float* att_dst, const float* a_src,
+                const float* a_dst, const float* alpha, float slope, float* u_out, float* h_inj,
+                float* g_att_src, float* g_att_dst, float* workspace, void* stream);
+
+/* ---- WGAN-GP critic engine helpers (trainer.py:291-332) ------------------ */
+
+/* X [3N, F+K]: rows c*N+n = [mvx[n] | label_c[n]] for c = real, fake (hard),
+ * mix = eps[n]*real + (1-eps[n])*soft (two products then one add, as torch). */
+int vg_critic_input(const float* mvx, int32_t N, int32_t F, const float* real, const float* hard,
+                    const float* soft, const float* eps, int32_t K, float* X, void* stream);
+
+/* From g [N,K] = dD(mix)/dlabel and the stacked scores [3N]:
+ * out[1] = gp = lambda mean_n (|g_n|-1)^2, out[0] = mean(fake) - mean(real) + gp,
+ * u0 [N,K] = dgp/dg.  One workgroup, deterministic. */
+int vg_gp_head(const float* g, int32_t N, int32_t K, const float* scores, float lambda, float* u0,
+               float* out, void* stream);
+
 /* Differentiable sparse primitives (their adjoints are each other), used to
  * build the twice-differentiable path the WGAN-GP needs (trainer.py:306-312,
  * create_graph=True):
@@ -126,6 +167,35 @@ int vg_graphnorm_bwd(const float* x, int32_t num_nodes, int32_t channels, const 
                      const float* stats, const float* g_y, float* g_x, float* g_w, float* g_b,
                      float* g_ms, float* workspace, void* stream);
 
+/* Segmented variants: `segments` row blocks of `rows` rows each (x is
+ * [segments*rows, C]) normalise independently -- the discriminator's real /
+ * fake / mix forwards of one critic iteration (trainer.py:319-320,304) run as
+ * one stacked tensor.  stats is [segments][2C].  Workspace from
+ * vg_graphnorm_seg_ws_floats (also valid for vg_graphnorm_jvp2 with 1). */
+int64_t vg_graphnorm_seg_ws_floats(int32_t segments, int32_t rows, int32_t channels);
+int vg_graphnorm_fwd_seg(const float* x, int32_t segments, int32_t rows, int32_t channels,
+                         const float* weight, const float* bias, const float* mean_scale,
+                         const float* keep, float eps, float* y, float* stats, float* workspace,
+                         void* stream);
+/* Backward over the segments; parameter gradients sum over segments and are
+ * written (accumulate = 0) or added (1); g_w may be NULL (no parameter
+ * gradients: g_b, g_ms are then ignored).  inj (nullable) is added to g_x
+ * from flat element inj_offset on (the critic engine's second-order adjoint
+ * of the mix copy). */
+int vg_graphnorm_bwd_seg(const float* x, int32_t segments, int32_t rows, int32_t channels,
+                         const float* weight, const float* bias, const float* mean_scale,
+                         const float* keep, float eps, const float* stats, const float* g_y,
+                         float* g_x, float* g_w, float* g_b, float* g_ms, int32_t accumulate,
+                         const float* inj, int64_t inj_offset, float* workspace, void* stream);
+/* Tangent and second-order terms of y = GraphNormReLUDropout(x) for the
+ * gradient penalty's double backward (trainer.py:306-316 with
+ * create_graph=True): u_out = J u and, for Q = <g_y, J u>, x_inj = dQ/dx;
+ * dQ/dweight and dQ/dmean_scale are ADDED to g_w, g_ms (dQ/dbias = 0). */
+int vg_graphnorm_jvp2(const float* x, int32_t num_nodes, int32_t channels, const float* weight,
+                      const float* bias, const float* mean_scale, const float* keep, float eps,
+                      const float* stats, const float* u, const float* g_y, float* u_out,
+                      float* x_inj, float* g_w, float* g_ms, float* workspace, void* stream);
+
 /* ---- program <-> voxel type-matched mean ("cross-graph pointer") -------- */
 
 /* For every voxel v: out[v, col0 : col0+F] = mean of local_x rows whose
@@ -170,23 +240,27 @@ int vg_confusion(const int64_t* truth, const float* label, int32_t classes, cons
 
 /* ---- dense layers (nn.Linear of the MLPs and the GATConv projection) ----- */
 
-/* C[N, M] = A[N, K] . op(B) (+ bias[M]) then act (0 none, 1 ReLU, 2 LeakyReLU 0.2).
+/* C[N, M] = A[N, K] . op(B) (+ bias[M]) then act (0 none, 1 ReLU, 2 LeakyReLU
+ * 0.2, 3 multiply by [aux > 0] with aux [N, M] row stride ldaux -- a ReLU mask
+ * applied to an adjoint or tangent; aux may be NULL otherwise).
  * b_trans = 1: B is [M, K] (op = transpose; the nn.Linear forward X W^T);
  * b_trans = 0: B is [K, M] (dX = dY W).  f32 MFMA (v_mfma_f32_32x32x2_f32).
  * Replaces the torch.nn.Linear GEMMs at models.py:33-47,49-66,92-113,
  * 177-185,212-220 and GATConv.lin. bias may be NULL. */
 int vg_gemm(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t b_trans,
-            const float* bias, int32_t act, float* C, int32_t ldc, int32_t N, int32_t M,
-            int32_t K, void* stream);
+            const float* bias, int32_t act, const float* aux, int32_t ldaux, float* C,
+            int32_t ldc, int32_t N, int32_t M, int32_t K, void* stream);
 
 /* Workspace (floats) for vg_gemm_tn. */
 int64_t vg_gemm_tn_ws_floats(int32_t N, int32_t M, int32_t K);
 
-/* C[M, K] = A[N, M]^T . B[N, K] and db[M] = sum_n A[n, :] (db may be NULL):
- * the weight and bias gradients of nn.Linear, split over N in 256-row chunks,
- * partials folded in chunk order (deterministic). */
+/* C[M, K] (row stride ldc) = A[N, M]^T . B[N, K] and db[M] = sum_n A[n, :]
+ * (db may be NULL): the weight and bias gradients of nn.Linear, split over N
+ * in row chunks, partials folded in chunk order (deterministic); written
+ * (accumulate = 0) or added (1). */
 int vg_gemm_tn(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N, int32_t M,
-               int32_t K, float* C, float* db, float* workspace, void* stream);
+               int32_t K, float* C, int32_t ldc, float* db, int32_t accumulate,
+               float* workspace, void* stream);
 
 /* ---- optimiser ---------------------------------------------------------- */
 

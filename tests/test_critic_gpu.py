@@ -1,0 +1,350 @@
+"""The explicit WGAN-GP critic engine (vgan/critic.py) and its kernels.
+
+Kernels are checked against torch autograd on the oracle's ops in float64
+(tests/critic_ref.py units); the engine against (i) the four-pass reference in
+float64 and (ii) plain double backward of the oracle discriminator, both on the
+engine's own dropout masks and eps.  Tolerances: kernels 1e-5 relative to the
+output scale (f32 summation order), engine loss 1e-5, gradients grads_close
+at 1e-3.
+"""
+import pytest
+import torch
+
+import critic_ref as CR
+from oracle import pyg
+from oracle import reference as R
+from parity_util import grads_close
+from vgan import ops, synth
+from vgan._lib import LIB, check, ptr, stream_handle
+from vgan.config import Configuration
+from vgan.graph import GraphBatch
+
+pytestmark = pytest.mark.gpu
+
+
+def _graph(numbers=(1, 2, 3), stress=False):
+    items = [(synth.make_stress_building(777, n, F=3, Y=9, X=9) if stress else synth.make_building(777, n))
+             for n in numbers]
+    return (GraphBatch.from_data_list([l for l, _ in items]), GraphBatch.from_data_list([v for _, v in items]))
+
+
+def _close(got, ref, tol=1e-5):
+    got = got.detach().double().cpu()
+    ref = ref.detach().double().cpu()
+    scale = max(ref.abs().max().item(), 1e-12)
+    return (got - ref).abs().max().item() <= tol * scale, (got - ref).abs().max().item() / scale
+
+
+# ------------------------------------------------------------------ GEMM
+def test_gemm_mask_epilogue_and_strided_accumulate(cuda):
+    g = torch.Generator().manual_seed(0)
+    n, k, m = 300, 37, 45
+    A = torch.randn(n, k, generator=g, dtype=torch.float64)
+    W = torch.randn(m, k, generator=g, dtype=torch.float64)
+    aux = torch.randn(n, m, generator=g, dtype=torch.float64)
+    Ad, Wd, auxd = (t.float().to(cuda) for t in (A, W, aux))
+    C = torch.empty(n, m, device=cuda)
+    st = stream_handle(cuda)
+    check(LIB.vg_gemm(ptr(Ad), k, ptr(Wd), k, 1, None, 3, ptr(auxd), m, ptr(C), m, n, m, k, st), "vg_gemm")
+    ok, err = _close(C, (A @ W.T) * (aux > 0))
+    assert ok, err
+    # C[:, 5:5+k] of a wider [m, 60] buffer += A2^T B, with column sums
+    A2 = torch.randn(n, m, generator=g, dtype=torch.float64)
+    B2 = torch.randn(n, k, generator=g, dtype=torch.float64)
+    base = torch.randn(m, 60, generator=g, dtype=torch.float64)
+    db0 = torch.randn(m, generator=g, dtype=torch.float64)
+    out, db = base.float().to(cuda), db0.float().to(cuda)
+    ws = torch.empty(int(LIB.vg_gemm_tn_ws_floats(n, m, k)), device=cuda)
+    import ctypes
+    check(LIB.vg_gemm_tn(ptr(A2.float().to(cuda)), m, ptr(B2.float().to(cuda)), k, n, m, k,
+                         ctypes.c_void_p(out.data_ptr() + 4 * 5), 60, ptr(db), 1, ptr(ws), st), "vg_gemm_tn")
+    exp = base.clone()
+    exp[:, 5:5 + k] += A2.T @ B2
+    assert _close(out, exp)[0]
+    assert _close(db, db0 + A2.sum(0))[0]
+
+
+# ------------------------------------------------------------------- GAT
+def _gat_inputs(C, stress, seed=0):
+    _, vox = _graph(stress=stress)
+    n = vox.num_nodes
+    g = torch.Generator().manual_seed(seed)
+    d = torch.float64
+    h = torch.randn(n, C, generator=g, dtype=d)
+    u = torch.randn(n, C, generator=g, dtype=d)
+    go = torch.randn(n, C, generator=g, dtype=d)
+    P = {"as": torch.randn(1, 1, C, generator=g, dtype=d), "ad": torch.randn(1, 1, C, generator=g, dtype=d),
+         "bias": torch.randn(C, generator=g, dtype=d)}
+    return vox.edge_index, n, h, u, go, P
+
+
+@pytest.mark.parametrize("C", [1, 3, 8, 16, 32, 64, 100])
+@pytest.mark.parametrize("stress", [False, True])
+def test_gat_jvp2_matches_autograd(cuda, C, stress):
+    ei, n, h, u, go, P = _gat_inputs(C, stress)
+    ju, hinj, pg = CR.Unit("gat", CR.gat_fn(ei, n), ["as", "ad", "bias"]).jvp2(h, u, go, P)
+    csr = ops.CSR(ei.to(cuda), n)
+    hd, ud, god = (t.float().to(cuda).contiguous() for t in (h, u, go))
+    vs, vd, b = (P[k].float().to(cuda).reshape(-1).contiguous() for k in ("as", "ad", "bias"))
+    out = torch.empty(n, C, device=cuda)
+    alpha = torch.empty(csr.num_edges, device=cuda)
+    a_s, a_d = torch.empty(n, device=cuda), torch.empty(n, device=cuda)
+    st = stream_handle(cuda)
+    check(LIB.vg_gat_fwd(ptr(csr.row_ptr), ptr(csr.col), n, C, ptr(hd), ptr(vs), ptr(vd), ptr(b), 0.2, ptr(out),
+                         ptr(alpha), ptr(a_s), ptr(a_d), st), "vg_gat_fwd")
+    u_out, h_inj = torch.empty(n, C, device=cuda), torch.empty(n, C, device=cuda)
+    g_as0, g_ad0 = torch.randn(C, dtype=torch.float64), torch.randn(C, dtype=torch.float64)
+    g_as, g_ad = g_as0.float().to(cuda), g_ad0.float().to(cuda)
+    ws = torch.empty(int(LIB.vg_gat_jvp2_ws_floats(n, csr.num_edges, C)), device=cuda)
+    check(LIB.vg_gat_jvp2(ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot), ptr(csr.csc_dst), n,
+                          csr.num_edges, C, ptr(hd), ptr(ud), ptr(god), ptr(vs), ptr(vd), ptr(a_s), ptr(a_d),
+                          ptr(alpha), 0.2, ptr(u_out), ptr(h_inj), ptr(g_as), ptr(g_ad), ptr(ws), st), "vg_gat_jvp2")
+    for got, ref in ((u_out, ju), (h_inj, hinj), (g_as, g_as0 + pg["as"].reshape(-1)),
+                     (g_ad, g_ad0 + pg["ad"].reshape(-1))):
+        ok, err = _close(got, ref, 2e-5)
+        assert ok, err
+    assert pg["bias"].abs().max().item() == 0.0
+
+
+@pytest.mark.parametrize("C", [4, 16, 64])
+def test_gat_bwd_ex_injection_and_accumulate(cuda, C):
+    ei, n, h, _, go, P = _gat_inputs(C, False, seed=1)
+    dx, pg = CR.Unit("gat", CR.gat_fn(ei, n), ["as", "ad", "bias"]).vjp(h, go, P)
+    csr = ops.CSR(ei.to(cuda), n)
+    hd, god = h.float().to(cuda), go.float().to(cuda)
+    vs, vd, b = (P[k].float().to(cuda).reshape(-1).contiguous() for k in ("as", "ad", "bias"))
+    out = torch.empty(n, C, device=cuda)
+    alpha = torch.empty(csr.num_edges, device=cuda)
+    a_s, a_d = torch.empty(n, device=cuda), torch.empty(n, device=cuda)
+    st = stream_handle(cuda)
+    check(LIB.vg_gat_fwd(ptr(csr.row_ptr), ptr(csr.col), n, C, ptr(hd), ptr(vs), ptr(vd), ptr(b), 0.2, ptr(out),
+                         ptr(alpha), ptr(a_s), ptr(a_d), st), "vg_gat_fwd")
+    row0 = n // 3
+    inj = torch.randn(n - row0, C, dtype=torch.float64)
+    base = [torch.randn(C, dtype=torch.float64) for _ in range(3)]
+    gs = [t.float().to(cuda) for t in base]
+    g_h = torch.empty(n, C, device=cuda)
+    ws = torch.empty(int(LIB.vg_gat_bwd_ws_floats(n, csr.num_edges, C)), device=cuda)
+    check(LIB.vg_gat_bwd_ex(ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot), ptr(csr.csc_dst), n,
+                            csr.num_edges, C, ptr(hd), ptr(vs), ptr(vd), ptr(a_s), ptr(a_d), ptr(alpha), ptr(god), 0.2,
+                            ptr(g_h), ptr(gs[0]), ptr(gs[1]), ptr(gs[2]), 1, ptr(inj.float().to(cuda)), row0, ptr(ws),
+                            st), "vg_gat_bwd_ex")
+    exp = dx.clone()
+    exp[row0:] += inj
+    assert _close(g_h, exp)[0]
+    for got, b0, k in zip(gs, base, ("as", "ad", "bias")):
+        assert _close(got, b0 + pg[k].reshape(-1))[0], k
+    # no parameter gradients: only g_h
+    g_h2 = torch.empty(n, C, device=cuda)
+    check(LIB.vg_gat_bwd_ex(ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot), ptr(csr.csc_dst), n,
+                            csr.num_edges, C, ptr(hd), ptr(vs), ptr(vd), ptr(a_s), ptr(a_d), ptr(alpha), ptr(god), 0.2,
+                            ptr(g_h2), None, None, None, 0, None, 0, ptr(ws), st), "vg_gat_bwd_ex")
+    assert _close(g_h2, dx)[0]
+
+
+# ------------------------------------------------------------- GraphNorm
+def _gn_inputs(n, C, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    d = torch.float64
+    x = torch.randn(n, C, generator=g, dtype=d) * 2 + 0.4
+    P = {"w": torch.rand(C, generator=g, dtype=d) + 0.5, "b": torch.randn(C, generator=g, dtype=d) * 0.3,
+         "s": torch.rand(C, generator=g, dtype=d)}
+    keep = (torch.rand(n, C, generator=g) > 0.2).to(d) / 0.8
+    return x, P, keep
+
+
+@pytest.mark.parametrize("C", [1, 8, 32, 64])
+def test_graphnorm_segments_fwd_bwd_injection(cuda, C):
+    S, n = 3, 700
+    x, P, keep = _gn_inputs(S * n, C)
+    gy = torch.randn(S * n, C, dtype=torch.float64)
+    ys, gxs = [], []
+    pgs = {k: torch.zeros_like(v) for k, v in P.items()}
+    for s in range(S):
+        rows = slice(s * n, (s + 1) * n)
+        unit = CR.Unit("gn", CR.gnrd_fn(keep[rows]), ["w", "b", "s"])
+        ys.append(unit.fwd(x[rows], P))
+        gx, pg = unit.vjp(x[rows], gy[rows], P)
+        gxs.append(gx)
+        for k in pgs:
+            pgs[k] += pg[k]
+    dev = [t.float().to(cuda).contiguous() for t in (x, keep, gy, P["w"], P["b"], P["s"])]
+    xd, kd, gyd, wd, bd, sd = dev
+    st = stream_handle(cuda)
+    y = torch.empty(S * n, C, device=cuda)
+    stats = torch.empty(S * 2 * C, device=cuda)
+    ws = torch.empty(int(LIB.vg_graphnorm_seg_ws_floats(S, n, C)), device=cuda)
+    check(LIB.vg_graphnorm_fwd_seg(ptr(xd), S, n, C, ptr(wd), ptr(bd), ptr(sd), ptr(kd), 1e-5, ptr(y), ptr(stats),
+                                   ptr(ws), st), "vg_graphnorm_fwd_seg")
+    assert _close(y, torch.cat(ys))[0]
+    inj = torch.randn(n, C, dtype=torch.float64)
+    base = {k: torch.randn(C, dtype=torch.float64) for k in P}
+    gw, gb, gs = (base[k].float().to(cuda) for k in ("w", "b", "s"))
+    gx = torch.empty(S * n, C, device=cuda)
+    check(LIB.vg_graphnorm_bwd_seg(ptr(xd), S, n, C, ptr(wd), ptr(bd), ptr(sd), ptr(kd), 1e-5, ptr(stats), ptr(gyd),
+                                   ptr(gx), ptr(gw), ptr(gb), ptr(gs), 1, ptr(inj.float().to(cuda)), 2 * n * C, ptr(ws),
+                                   st), "vg_graphnorm_bwd_seg")
+    exp = torch.cat(gxs)
+    exp[2 * n:] += inj
+    assert _close(gx, exp)[0]
+    for got, k in ((gw, "w"), (gb, "b"), (gs, "s")):
+        assert _close(got, base[k] + pgs[k])[0], k
+
+
+@pytest.mark.parametrize("C", [1, 8, 32, 64])
+def test_graphnorm_jvp2_matches_autograd(cuda, C):
+    n = 900
+    x, P, keep = _gn_inputs(n, C, seed=3)
+    u = torch.randn(n, C, dtype=torch.float64)
+    gy = torch.randn(n, C, dtype=torch.float64)
+    ju, xinj, pg = CR.Unit("gn", CR.gnrd_fn(keep), ["w", "b", "s"]).jvp2(x, u, gy, P)
+    xd, kd, ud, gyd, wd, bd, sd = (t.float().to(cuda).contiguous() for t in (x, keep, u, gy, P["w"], P["b"], P["s"]))
+    st = stream_handle(cuda)
+    y = torch.empty(n, C, device=cuda)
+    stats = torch.empty(2 * C, device=cuda)
+    ws = torch.empty(int(LIB.vg_graphnorm_seg_ws_floats(1, n, C)), device=cuda)
+    check(LIB.vg_graphnorm_fwd_seg(ptr(xd), 1, n, C, ptr(wd), ptr(bd), ptr(sd), ptr(kd), 1e-5, ptr(y), ptr(stats),
+                                   ptr(ws), st), "vg_graphnorm_fwd_seg")
+    u_out, x_inj = torch.empty(n, C, device=cuda), torch.empty(n, C, device=cuda)
+    gw0, gs0 = torch.randn(C, dtype=torch.float64), torch.randn(C, dtype=torch.float64)
+    gw, gs = gw0.float().to(cuda), gs0.float().to(cuda)
+    check(LIB.vg_graphnorm_jvp2(ptr(xd), n, C, ptr(wd), ptr(bd), ptr(sd), ptr(kd), 1e-5, ptr(stats), ptr(ud), ptr(gyd),
+                                ptr(u_out), ptr(x_inj), ptr(gw), ptr(gs), ptr(ws), st), "vg_graphnorm_jvp2")
+    for got, ref in ((u_out, ju), (x_inj, xinj), (gw, gw0 + pg["w"]), (gs, gs0 + pg["s"])):
+        ok, err = _close(got, ref, 2e-5)
+        assert ok, err
+
+
+# -------------------------------------------------------------- helpers
+def test_critic_input_and_gp_head(cuda):
+    g = torch.Generator().manual_seed(5)
+    n, F, K = 333, 29, 7
+    mvx = torch.rand(n, F, generator=g)
+    real = torch.nn.functional.one_hot(torch.randint(0, K, (n,), generator=g), K).float()
+    hard = torch.nn.functional.one_hot(torch.randint(0, K, (n,), generator=g), K).float()
+    soft = torch.softmax(torch.randn(n, K, generator=g), 1)
+    eps = torch.rand(n, 1, generator=g)
+    X = torch.empty(3 * n, F + K, device=cuda)
+    st = stream_handle(cuda)
+    dv = [t.to(cuda).contiguous() for t in (mvx, real, hard, soft, eps)]
+    check(LIB.vg_critic_input(ptr(dv[0]), n, F, ptr(dv[1]), ptr(dv[2]), ptr(dv[3]), ptr(dv[4]), K, ptr(X), st),
+          "vg_critic_input")
+    mix = eps * real + (1 - eps) * soft  # the reference's rounding (trainer.py:298-301)
+    exp = torch.cat([torch.cat([mvx, real], 1), torch.cat([mvx, hard], 1), torch.cat([mvx, mix], 1)])
+    assert torch.equal(X.cpu(), exp)
+    gg = torch.randn(n, K, generator=g, dtype=torch.float64)
+    gg[3] = 0.0
+    sc = torch.randn(3 * n, dtype=torch.float64)
+    u0, out = torch.empty(n, K, device=cuda), torch.empty(2, device=cuda)
+    check(LIB.vg_gp_head(ptr(gg.float().to(cuda)), n, K, ptr(sc.float().to(cuda)), 10.0, ptr(u0), ptr(out), st),
+          "vg_gp_head")
+    leaf = gg.clone().requires_grad_(True)
+    gp = ((leaf.norm(dim=1) - 1) ** 2).mean() * 10.0
+    (gref,) = torch.autograd.grad(gp, leaf)
+    loss = sc[n:2 * n].mean() - sc[:n].mean() + gp
+    assert abs(out[1].item() - gp.item()) <= 1e-5 * abs(gp.item())
+    assert abs(out[0].item() - loss.item()) <= 1e-5 * max(1.0, abs(loss.item()))
+    gref[3] = 0.0  # torch's norm backward at 0 is 0 as well (subgradient)
+    assert _close(u0, gref)[0]
+
+
+# --------------------------------------------------------------- engine
+class _RecRNG:
+    """Seeded CPU draws in the engine's (= the reference's) order, recorded."""
+    mode = "fixed"
+
+    def __init__(self, seed):
+        self.g = torch.Generator().manual_seed(seed)
+        self.draws = []
+
+    def keep_mask(self, shape, p, device):
+        t = torch.empty(*shape).bernoulli_(1 - p, generator=self.g).div_(1 - p)
+        self.draws.append(t)
+        return t.to(device)
+
+    def uniform(self, shape, device):
+        t = torch.rand(*shape, generator=self.g)
+        self.draws.append(t)
+        return t.to(device)
+
+
+def _engine_setup(cuda, numbers=(1, 2, 3, 4), seed=11):
+    from vgan import data as vdata
+    from vgan.critic import CriticEngine
+    from vgan.models import VoxelGNNDiscriminator
+
+    cfg = Configuration()
+    cfg.DEVICE = cuda
+    torch.manual_seed(seed)
+    D = VoxelGNNDiscriminator(cfg, 17, 12)
+    from vgan.flat import FlatParams
+    flat = FlatParams(D)
+    loc, vox = _graph(numbers)
+    loc, vox = loc.to(cuda), vox.to(cuda)
+    prep = vdata.prepared(loc, vox, cfg.NUM_CLASSES)
+    n = vox.num_nodes
+    g = torch.Generator().manual_seed(seed + 1)
+    logits = torch.randn(n, 7, generator=g) * 2
+    soft = torch.softmax(logits, 1)
+    hard = torch.nn.functional.one_hot(soft.argmax(1), 7).float()
+    return cfg, D, flat, loc, vox, prep, hard, soft, CriticEngine(D, cfg)
+
+
+def test_engine_matches_f64_references(cuda):
+    cfg, D, flat, loc, vox, prep, hard, soft, eng = _engine_setup(cuda)
+    n = vox.num_nodes
+    rng = _RecRNG(3)
+    flat.zero_grad()
+    loss = eng.loss_and_grad(loc, vox, hard.to(cuda).unsqueeze(0), soft.to(cuda).unsqueeze(0), rng)
+    torch.cuda.synchronize()
+    grads = {k: p.grad.detach().cpu().double() for k, p in D.named_parameters()}
+    nb = len(eng.blocks)
+    real_k, fake_k, eps, mix_k = rng.draws[:nb], rng.draws[nb:2 * nb], rng.draws[2 * nb], rng.draws[2 * nb + 1:]
+    d = torch.float64
+    ei = vox.edge_index.cpu()
+    P = {k: v.detach().cpu().double() for k, v in D.state_dict().items()}
+    units = {c: CR.d_units(nb, len(eng.dec), ei, n, [k.double() for k in ks])
+             for c, ks in (("real", real_k), ("fake", fake_k), ("mix", mix_k))}
+    mvx = prep.matched_voxel_x.cpu().double()
+    real = prep.onehot_f.cpu().double()
+    e = eps.double()
+    mix = e * real + (1 - e) * soft.double()
+    x0s = {"real": torch.cat([mvx, real], 1), "fake": torch.cat([mvx, hard.double()], 1),
+           "mix": torch.cat([mvx, mix], 1)}
+    lab = slice(mvx.shape[1], mvx.shape[1] + 7)
+    l1, gp1, g1 = CR.run(units, x0s, lab, float(cfg.LAMBDA_GP), P)
+    l2, gp2, g2 = CR.autograd_loss(units, x0s, lab, float(cfg.LAMBDA_GP), P)
+    assert abs(l1.item() - l2.item()) <= 1e-10 * max(1.0, abs(l2.item()))
+    assert abs(loss.item() - l2.item()) <= 1e-5 * max(1.0, abs(l2.item())), (loss.item(), l2.item())
+    assert abs(eng.last_gp.item() - gp2.item()) <= 1e-5 * max(1.0, abs(gp2.item()))
+    ok, worst, total = grads_close(grads, g2, rtol=1e-3)
+    assert ok, (worst, total)
+
+
+def test_engine_matches_autograd_path_on_gpu(cuda):
+    """Same host RNG stream: the engine consumes it exactly like
+    Trainer._compute_discriminator_loss (reference order)."""
+    cfg, D, flat, loc, vox, prep, hard, soft, eng = _engine_setup(cuda, numbers=(5, 6), seed=4)
+    from vgan.rng import RNG
+    from vgan.trainer import Trainer
+    from vgan.models import VoxelGNNGenerator
+
+    cfg.runtime["rng"] = "host"
+    G = VoxelGNNGenerator(cfg, 17, 12)
+    tr = Trainer(G, D, None, torch.optim.Adam(G.parameters()), torch.optim.Adam(D.parameters()), None, cfg)
+    rng = RNG("host")
+    hd, sd = hard.to(cuda).unsqueeze(0), soft.to(cuda).unsqueeze(0)
+    torch.manual_seed(123)
+    tr.flat_d.zero_grad()
+    l_eng = eng.loss_and_grad(loc, vox, hd, sd, rng)
+    g_eng = {k: p.grad.detach().clone() for k, p in D.named_parameters()}
+    after = torch.get_rng_state()
+    torch.manual_seed(123)
+    tr.flat_d.zero_grad()
+    l_ag = tr._compute_discriminator_loss(loc, vox, hd, sd)
+    l_ag.backward()
+    assert torch.equal(torch.get_rng_state(), after)
+    g_ag = {k: p.grad.detach().clone() for k, p in D.named_parameters()}
+    assert abs(l_eng.item() - l_ag.item()) <= 1e-5 * max(1.0, abs(l_ag.item()))
+    ok, worst, total = grads_close(g_eng, g_ag, rtol=1e-3)
+    assert ok, (worst, total)
