@@ -97,6 +97,11 @@ class Configuration(ProgramMap):
     * ``rng``: ``"device"`` (draw z / dropout / Gumbel / GP noise on the GPU)
       or ``"host"`` (draw them on the CPU default generator in the reference's
       order, then copy -- used for bit-identical parity with the CPU path).
+    * ``critic``: ``"engine"`` (default; the explicit four-pass WGAN-GP
+      gradient of ``vgan.critic``) or ``"autograd"`` (double backward through
+      the differentiable HIP ops).
+    * ``skip_dead_d_grads``: skip D's parameter gradients in the generator
+      iteration (the next critic iteration zeroes them, ``trainer.py:475``).
     * ``world_size`` / ``rank``: data-parallel layout (set by ``vgan.dist``).
     """
 

@@ -39,6 +39,7 @@ import torch.nn.functional as F
 from . import data as vdata
 from . import metrics as vmetrics
 from . import ops
+from .critic import CriticEngine
 from .dist import GradSync
 from .flat import FlatAdam, FlatParams
 from .rng import RNG
@@ -69,7 +70,19 @@ class Trainer:
         self.sync.broadcast_params(self.flat_g)
         self.sync.broadcast_params(self.flat_d)
         self.skip_dead_d_grads = runtime.get("skip_dead_d_grads", True)
+        # critic iterations: the explicit four-pass engine (vgan/critic.py) or
+        # autograd double backward through the differentiable HIP ops
+        use_engine = runtime.get("critic", "engine") == "engine" and getattr(configuration, "USE_WGANGP", True)
+        self.critic = CriticEngine(discriminator, configuration) if use_engine else None
         self.states = {"epoch_start": 1, "best_f1_score": 0.0}
+
+    def _critic_loss_backward(self, local_graph, voxel_graph, label_hard, label_soft) -> torch.Tensor:
+        """d_loss of trainer.py:476-479 with D's gradients accumulated into .grad."""
+        if self.critic is not None:
+            return self.critic.loss_and_grad(local_graph, voxel_graph, label_hard, label_soft, self.rng)
+        d_loss = self._compute_discriminator_loss(local_graph, voxel_graph, label_hard, label_soft)
+        d_loss.backward()
+        return d_loss
 
     # ------------------------------------------------------------- losses
     def _compute_gradient_penalty(self, local_graph, voxel_graph, label_soft):
@@ -138,8 +151,7 @@ class Trainer:
             with torch.no_grad():
                 _, hard, soft = self._generate(local_graph, voxel_graph)
             self.adam_d.zero_grad()
-            d_loss = self._compute_discriminator_loss(local_graph, voxel_graph, hard, soft)
-            d_loss.backward()
+            d_loss = self._critic_loss_backward(local_graph, voxel_graph, hard, soft)
             d_losses.append(d_loss.detach())
             self.sync.all_reduce_grad(self.flat_d)
             self.adam_d.step()
@@ -168,8 +180,7 @@ class Trainer:
         with torch.no_grad():
             _, hard, soft = self._generate(local_graph, voxel_graph)
         self.adam_d.zero_grad()
-        d_loss = self._compute_discriminator_loss(local_graph, voxel_graph, hard, soft)
-        d_loss.backward()
+        d_loss = self._critic_loss_backward(local_graph, voxel_graph, hard, soft)
         acc[0].add_(d_loss.detach())
         if with_adam:
             self.adam_d.step()
