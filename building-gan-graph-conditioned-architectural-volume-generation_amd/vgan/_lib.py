@@ -61,6 +61,10 @@ SIGNATURES = {
                                             _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_i64, _c_p, _c_p]),
     "vg_graphnorm_jvp2": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p,
                                          _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "vg_ln_act_fwd": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_f32, _c_f32, _c_p, _c_p, _c_p, _c_p]),
+    "vg_ln_act_bwd_ws_floats": (_c_i64, [_c_i32]),
+    "vg_ln_act_bwd": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
+                                     _c_i32, _c_p, _c_p]),
     "vg_critic_input": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_p]),
     "vg_gp_head": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_f32, _c_p, _c_p, _c_p]),
     "vg_adam_dev": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_i64, ctypes.c_double, ctypes.c_double, _c_f32, _c_f32,

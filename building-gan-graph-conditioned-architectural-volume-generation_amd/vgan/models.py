@@ -28,7 +28,7 @@ import torch.nn as nn
 
 from . import data as vdata
 from . import ops
-from .nn import Linear, linear
+from .nn import MLP, Linear, linear
 from .rng import RNG
 
 _CONV_TYPES = ("GCNCONV", "GRAPHCONV", "GATCONV", "GATV2CONV")
@@ -118,14 +118,14 @@ class GATEncoder(nn.Module):
         return x
 
 
-def _mlp(widths: List[int], norm: bool, act) -> nn.Sequential:
+def _mlp(widths: List[int], norm: bool, act) -> MLP:
     mods: List[nn.Module] = []
     for a, b in zip(widths[:-1], widths[1:]):
         mods.append(Linear(a, b))
         if norm:
             mods.append(nn.LayerNorm(b))
         mods.append(act())
-    return nn.Sequential(*mods)
+    return MLP(*mods)
 
 
 def _check_conv(kind: str) -> None:
@@ -154,7 +154,7 @@ class VoxelGNNGenerator(nn.Module):
         dec = list(_mlp([hl + voxel_graph_dim + zd + self.encoder.out_channels + hg, hg, hg // 2, hg // 4, hg // 8],
                         True, lrelu).children())
         dec.append(Linear(hg // 8, cfg.NUM_CLASSES))
-        self.decoder = nn.Sequential(*dec)
+        self.decoder = MLP(*dec)
         self.rng = RNG(getattr(cfg, "runtime", {}).get("rng", "device"))
         self.tau = 1.0
         self.to(cfg.DEVICE)
@@ -190,7 +190,7 @@ class VoxelGNNDiscriminator(nn.Module):
         dec.append(Linear(hd // 8, 1))
         if not cfg.USE_WGANGP:
             dec.append(nn.Sigmoid())
-        self.decoder = nn.Sequential(*dec)
+        self.decoder = MLP(*dec)
         self.rng = RNG(getattr(cfg, "runtime", {}).get("rng", "device"))
         self.to(cfg.DEVICE)
 

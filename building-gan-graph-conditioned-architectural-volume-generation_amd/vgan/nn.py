@@ -13,7 +13,6 @@ from __future__ import annotations
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 from torch.autograd import Function
 
 from . import ops
@@ -96,11 +95,37 @@ class _LinearFn(Function):
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
-    if x.dim() != 2 or not x.is_cuda:
-        return F.linear(x, weight, bias)
-    return _LinearFn.apply(x.contiguous(), weight, bias, ops.ACT_NONE)
+    if not x.is_cuda:
+        raise RuntimeError("vgan HIP ops require tensors on a ROCm device (no CPU fallback)")
+    if x.dim() == 2:
+        return _LinearFn.apply(x.contiguous(), weight, bias, ops.ACT_NONE)
+    y = _LinearFn.apply(x.reshape(-1, x.shape[-1]).contiguous(), weight, bias, ops.ACT_NONE)
+    return y.reshape(*x.shape[:-1], y.shape[-1])
 
 
 class Linear(nn.Linear):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return linear(x, self.weight, self.bias)
+
+
+class MLP(nn.Sequential):
+    """nn.Sequential of the reference's [Linear, (LayerNorm,) activation]
+    blocks (same children, same state_dict keys); every Linear -> LayerNorm
+    -> LeakyReLU triple runs as one GEMM plus one fused LayerNorm+activation
+    kernel (vg_ln_act_fwd)."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        mods = list(self)
+        i = 0
+        while i < len(mods):
+            m = mods[i]
+            if (isinstance(m, nn.Linear) and i + 2 < len(mods) and isinstance(mods[i + 1], nn.LayerNorm)
+                    and isinstance(mods[i + 2], nn.LeakyReLU) and len(mods[i + 1].normalized_shape) == 1
+                    and mods[i + 1].elementwise_affine):
+                ln = mods[i + 1]
+                x = ops.ln_act(linear(x, m.weight, m.bias), ln.weight, ln.bias, ln.eps, mods[i + 2].negative_slope)
+                i += 3
+            else:
+                x = m(x)
+                i += 1
+        return x

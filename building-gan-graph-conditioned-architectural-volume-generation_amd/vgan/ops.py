@@ -516,6 +516,55 @@ def confusion(truth, label, ptr_):
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
 
 
+class _LNAct(Function):
+    """leaky_relu(LayerNorm(x)) in one kernel (vg_ln_act_fwd / _bwd)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps, slope):
+        x, g, b = _f32(x), _f32(gamma), _f32(beta)
+        require_cuda(x, g, b)
+        n, c = x.shape
+        if g.numel() != c or b.numel() != c:
+            raise ValueError("ln_act: inconsistent shapes")
+        y = torch.empty_like(x)
+        save = torch.is_grad_enabled() and any(t.requires_grad for t in (x, gamma, beta))
+        mean = torch.empty(n, dtype=torch.float32, device=x.device) if save else None
+        rstd = torch.empty(n, dtype=torch.float32, device=x.device) if save else None
+        check(LIB.vg_ln_act_fwd(ptr(x), n, c, ptr(g), ptr(b), float(eps), float(slope), ptr(y), ptr(mean), ptr(rstd),
+                                stream_handle(x.device)), "vg_ln_act_fwd")
+        ctx.eps, ctx.slope = eps, slope
+        if save:
+            ctx.save_for_backward(x, gamma, beta, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, g_y):
+        x, gamma, beta, mean, rstd = ctx.saved_tensors
+        n, c = x.shape
+        if torch.is_grad_enabled():  # create_graph: differentiable torch restatement
+            leaves = [t.detach().requires_grad_(t.requires_grad) for t in (x, gamma, beta)]
+            with torch.enable_grad():
+                y = torch.nn.functional.leaky_relu(
+                    torch.nn.functional.layer_norm(leaves[0], (c,), leaves[1], leaves[2], ctx.eps), ctx.slope)
+                need = [t for t in leaves if t.requires_grad]
+                grads = iter(torch.autograd.grad(y, need, g_y, create_graph=True))
+            res = [next(grads) if t.requires_grad else None for t in leaves]
+            return res[0], res[1], res[2], None, None
+        g_y = _f32(g_y)
+        g_x = torch.empty_like(x)
+        g_g = torch.empty(c, dtype=torch.float32, device=x.device)
+        g_b = torch.empty_like(g_g)
+        ws = torch.empty(int(LIB.vg_ln_act_bwd_ws_floats(c)), dtype=torch.float32, device=x.device)
+        check(LIB.vg_ln_act_bwd(ptr(x), n, c, ptr(gamma), ptr(beta), float(ctx.slope), ptr(mean), ptr(rstd), ptr(g_y),
+                                ptr(g_x), ptr(g_g), ptr(g_b), 0, ptr(ws), stream_handle(x.device)), "vg_ln_act_bwd")
+        return g_x, g_g, g_b, None, None
+
+
+def ln_act(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-5, slope: float = 0.2):
+    """nn.LayerNorm(C) followed by nn.LeakyReLU(slope) (models.py:33-113)."""
+    return _LNAct.apply(x, gamma, beta, eps, slope)
+
+
 def gemm(a: torch.Tensor, b: torch.Tensor, b_trans: bool, bias: Optional[torch.Tensor] = None,
          act: int = ACT_NONE) -> torch.Tensor:
     """C = a . (b^T if b_trans else b) (+ bias) (+ act), f32 MFMA (vg_gemm)."""

@@ -262,6 +262,24 @@ int vg_gemm_tn(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t
                int32_t K, float* C, int32_t ldc, float* db, int32_t accumulate,
                float* workspace, void* stream);
 
+/* ---- LayerNorm + LeakyReLU ------------------------------------------------ */
+
+/* y = leaky_relu(LayerNorm(x; gamma, beta, eps), slope) per row of x [N, C]
+ * (C <= 512): the nn.LayerNorm -> nn.LeakyReLU(0.2) pairs of the generator's
+ * MLPs (models.py:33-47,49-66,92-113) in one kernel.  mean / rstd [N]
+ * (nullable together) are saved for the backward. */
+int vg_ln_act_fwd(const float* x, int32_t N, int32_t C, const float* gamma, const float* beta,
+                  float eps, float slope, float* y, float* mean, float* rstd, void* stream);
+
+/* Workspace (floats) for vg_ln_act_bwd. */
+int64_t vg_ln_act_bwd_ws_floats(int32_t C);
+
+/* Backward: g_x, and g_gamma / g_beta [C] written (accumulate = 0) or added. */
+int vg_ln_act_bwd(const float* x, int32_t N, int32_t C, const float* gamma, const float* beta,
+                  float slope, const float* mean, const float* rstd, const float* g_y, float* g_x,
+                  float* g_gamma, float* g_beta, int32_t accumulate, float* workspace,
+                  void* stream);
+
 /* ---- optimiser ---------------------------------------------------------- */
 
 /* torch.optim.Adam (single-tensor semantics, weight_decay, no amsgrad) over one

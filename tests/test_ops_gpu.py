@@ -329,3 +329,22 @@ def test_linear_double_backward(cuda):
     g = second(lin, x0.float().to(cuda).requires_grad_(True))
     for a, b in zip(g, r):
         assert rel_err(a, b) < 1e-5
+
+
+@pytest.mark.parametrize("C", [7, 16, 64, 128, 300])
+def test_ln_act_matches_torch(cuda, C):
+    g = torch.Generator().manual_seed(C)
+    n = 1000
+    x = torch.randn(n, C, generator=g, dtype=torch.float64) * 3 + 1
+    w = torch.rand(C, generator=g, dtype=torch.float64) + 0.5
+    b = torch.randn(C, generator=g, dtype=torch.float64) * 0.2
+    gy = torch.randn(n, C, generator=g, dtype=torch.float64)
+    ts = [t.clone().requires_grad_(True) for t in (x, w, b)]
+    y = torch.nn.functional.leaky_relu(torch.nn.functional.layer_norm(ts[0], (C,), ts[1], ts[2], 1e-5), 0.2)
+    gr = torch.autograd.grad(y, ts, gy)
+    td = [t.float().to(cuda).requires_grad_(True) for t in (x, w, b)]
+    yd = ops.ln_act(td[0], td[1], td[2], 1e-5, 0.2)
+    gd = torch.autograd.grad(yd, td, gy.float().to(cuda))
+    assert rel_err(yd.cpu(), y) < 1e-5
+    for a, r in zip(gd, gr):
+        assert rel_err(a.cpu(), r) < 1e-4
