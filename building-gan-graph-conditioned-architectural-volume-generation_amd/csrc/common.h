@@ -45,6 +45,32 @@ __device__ __forceinline__ int xcd_remap(int b, int nblocks) {
   return start + slot;
 }
 
+// Counter-based Philox4x32-10 (Salmon et al., SC'11): stateless, so a kernel
+// replayed from a hipGraph draws fresh numbers whenever the counter it reads
+// from device memory has advanced.
+__device__ __forceinline__ uint4 vg_philox(uint4 c, uint2 k) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+    k.x += 0x9E3779B9u;
+    k.y += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// Dropout multiplier of element t: Bernoulli(1 - p) / (1 - p) from the
+// counter (t, salt, iteration) under key = seed.
+__device__ __forceinline__ float vg_keep(long long t, uint32_t salt, long long iter, uint64_t seed,
+                                         float p) {
+  const uint4 r = vg_philox(make_uint4(static_cast<uint32_t>(t), static_cast<uint32_t>(t >> 32), salt,
+                                       static_cast<uint32_t>(iter)),
+                            make_uint2(static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32)));
+  const float u = static_cast<float>(r.x >> 8) * (1.0f / 16777216.0f);
+  return u < 1.f - p ? 1.f / (1.f - p) : 0.f;
+}
+
 static inline int vg_blocks(long long work, int per_block) {
   long long b = (work + per_block - 1) / per_block;
   return b < 1 ? 1 : static_cast<int>(b);

@@ -127,10 +127,15 @@ __global__ void __launch_bounds__(256) k_stats_final(const float* __restrict__ p
   }
 }
 
+// keep_out != NULL: draw the dropout multiplier in-kernel (vg_keep with
+// p_drop, seed, *iter, salt), apply it and store it for the backward.
 __global__ void k_gn_apply(const float* __restrict__ x, long long total, int C, long long seg_elems,
                            const float* __restrict__ w, const float* __restrict__ b,
                            const float* __restrict__ ms, const float* __restrict__ keep,
-                           float eps, const float* __restrict__ stats, float* __restrict__ y) {
+                           float eps, const float* __restrict__ stats, float* __restrict__ y,
+                           float p_drop, unsigned long long seed, const long long* __restrict__ iter,
+                           unsigned int salt, float* __restrict__ keep_out) {
+  const long long it = keep_out ? *iter : 0;
   for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
        t += (long long)gridDim.x * blockDim.x) {
     const int c = static_cast<int>(t % C);
@@ -139,7 +144,13 @@ __global__ void k_gn_apply(const float* __restrict__ x, long long total, int C, 
     const float o = x[t] - mu * ms[c];
     const float z = (o / (sd + eps)) * w[c] + b[c];
     float r = z > 0.f ? z : 0.f;
-    if (keep) r *= keep[t];
+    if (keep_out) {
+      const float k = vg_keep(t, salt, it, seed, p_drop);
+      keep_out[t] = k;
+      r *= k;
+    } else if (keep) {
+      r *= keep[t];
+    }
     y[t] = r;
   }
 }
@@ -409,10 +420,10 @@ extern "C" int64_t vg_graphnorm_ws_floats(int32_t num_nodes, int32_t channels) {
   return vg_graphnorm_seg_ws_floats(1, num_nodes, channels);
 }
 
-extern "C" int vg_graphnorm_fwd_seg(const float* x, int32_t S, int32_t N, int32_t C,
-                                    const float* weight, const float* bias,
-                                    const float* mean_scale, const float* keep, float eps,
-                                    float* y, float* stats, float* ws, void* stream) {
+static int gn_fwd(const float* x, int32_t S, int32_t N, int32_t C, const float* weight,
+                  const float* bias, const float* mean_scale, const float* keep, float eps, float* y,
+                  float* stats, float* ws, float p_drop, uint64_t seed, const int64_t* iter,
+                  uint32_t salt, float* keep_out, void* stream) {
   if (S <= 0 || N <= 0 || C <= 0 || !x || !weight || !bias || !mean_scale || !y || !stats || !ws)
     return VG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -422,9 +433,30 @@ extern "C" int vg_graphnorm_fwd_seg(const float* x, int32_t S, int32_t N, int32_
   k_stats_final<<<dim3(vg_blocks(C, 64), S), 256, 0, s>>>(ws, chunks, C, stats);
   const long long total = (long long)S * N * C;
   k_gn_apply<<<apply_blocks(total), 256, 0, s>>>(x, total, C, (long long)N * C, weight, bias,
-                                                 mean_scale, keep, eps, stats, y);
+                                                 mean_scale, keep, eps, stats, y, p_drop,
+                                                 (unsigned long long)seed,
+                                                 reinterpret_cast<const long long*>(iter), salt,
+                                                 keep_out);
   VG_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int vg_graphnorm_fwd_seg(const float* x, int32_t S, int32_t N, int32_t C,
+                                    const float* weight, const float* bias,
+                                    const float* mean_scale, const float* keep, float eps,
+                                    float* y, float* stats, float* ws, void* stream) {
+  return gn_fwd(x, S, N, C, weight, bias, mean_scale, keep, eps, y, stats, ws, 0.f, 0, nullptr, 0,
+                nullptr, stream);
+}
+
+extern "C" int vg_graphnorm_fwd_drop(const float* x, int32_t S, int32_t N, int32_t C,
+                                     const float* weight, const float* bias,
+                                     const float* mean_scale, float p_drop, uint64_t seed,
+                                     const int64_t* iter, uint32_t salt, float eps, float* y,
+                                     float* keep_out, float* stats, float* ws, void* stream) {
+  if (!iter || !keep_out || !(p_drop >= 0.f && p_drop < 1.f)) return VG_EINVAL;
+  return gn_fwd(x, S, N, C, weight, bias, mean_scale, nullptr, eps, y, stats, ws, p_drop, seed,
+                iter, salt, keep_out, stream);
 }
 
 extern "C" int vg_graphnorm_fwd(const float* x, int32_t N, int32_t C, const float* weight,

@@ -57,6 +57,8 @@ SIGNATURES = {
     "vg_graphnorm_seg_ws_floats": (_c_i64, [_c_i32, _c_i32, _c_i32]),
     "vg_graphnorm_fwd_seg": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p,
                                             _c_p, _c_p]),
+    "vg_graphnorm_fwd_drop": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_f32, ctypes.c_uint64,
+                                             _c_p, ctypes.c_uint32, _c_f32, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "vg_graphnorm_bwd_seg": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p,
                                             _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_i64, _c_p, _c_p]),
     "vg_graphnorm_jvp2": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p,

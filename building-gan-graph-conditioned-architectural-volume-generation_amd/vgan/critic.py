@@ -82,7 +82,7 @@ class CriticEngine:
         widths = [conv.out_channels for conv, _ in self.blocks]
         if not training:
             return [None] * len(widths), rng.uniform((n, 1), dev)
-        if rng.mode == "device":
+        if rng.mode == "device":  # DropSpecs: drawn inside the GraphNorm kernel
             keeps = [rng.keep_mask((3 * n, c), self.dropout, dev) for c in widths]
             return keeps, rng.uniform((n, 1), dev)
         real = [rng.keep_mask((n, c), self.dropout, dev) for c in widths]
@@ -150,9 +150,16 @@ class CriticEngine:
                                  ptr(a_s), ptr(a_d), st), "vg_gat_fwd")
             Y, stats = _f(R, c, dev=dev), _f(3 * 2 * c, dev=dev)
             ws = _f(int(LIB.vg_graphnorm_seg_ws_floats(3, n, c)), dev=dev)
-            check(LIB.vg_graphnorm_fwd_seg(ptr(O), 3, n, c, ptr(norm.weight), ptr(norm.bias), ptr(norm.mean_scale),
-                                           ptr(keep), float(norm.eps), ptr(Y), ptr(stats), ptr(ws), st),
-                  "vg_graphnorm_fwd_seg")
+            if keep is not None and not isinstance(keep, torch.Tensor):  # DropSpec
+                spec, keep = keep, _f(R, c, dev=dev)
+                check(LIB.vg_graphnorm_fwd_drop(ptr(O), 3, n, c, ptr(norm.weight), ptr(norm.bias),
+                                                ptr(norm.mean_scale), float(spec.p), int(spec.seed), ptr(spec.iter),
+                                                int(spec.salt) & 0xFFFFFFFF, float(norm.eps), ptr(Y), ptr(keep),
+                                                ptr(stats), ptr(ws), st), "vg_graphnorm_fwd_drop")
+            else:
+                check(LIB.vg_graphnorm_fwd_seg(ptr(O), 3, n, c, ptr(norm.weight), ptr(norm.bias),
+                                               ptr(norm.mean_scale), ptr(keep), float(norm.eps), ptr(Y), ptr(stats),
+                                               ptr(ws), st), "vg_graphnorm_fwd_seg")
             blk.append(dict(X=x, xw=xw, H=H, O=O, alpha=alpha, a_s=a_s, a_d=a_d, Y=Y, stats=stats, keep=keep, c=c))
             x, xw = Y, c
         dec_out = []

@@ -108,13 +108,15 @@ class GATEncoder(nn.Module):
     def out_channels(self) -> int:
         return self.widths[-1]
 
-    def forward(self, x: torch.Tensor, csr: ops.CSR, rng: RNG) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, csr: ops.CSR, rng: RNG, segments: int = 1) -> torch.Tensor:
+        """``segments`` > 1: x holds that many stacked copies of the batch (csr
+        block-diagonal), each normalised on its own as a separate forward."""
         for b in range(self.num_blocks):
             conv: GATConv = getattr(self, f"module_{4 * b}")
             norm: GraphNorm = getattr(self, f"module_{4 * b + 1}")
             h = conv(x, csr)
             keep = rng.keep_mask(h.shape, self.dropout, h.device) if self.training else None
-            x = ops.graphnorm_relu_dropout(h, norm.weight, norm.bias, norm.mean_scale, keep, norm.eps)
+            x = ops.graphnorm_relu_dropout(h, norm.weight, norm.bias, norm.mean_scale, keep, norm.eps, segments)
         return x
 
 
@@ -160,16 +162,31 @@ class VoxelGNNGenerator(nn.Module):
         self.to(cfg.DEVICE)
 
     def forward(self, local_graph, voxel_graph, z, noise: Optional[torch.Tensor] = None):
+        """z [1, N, Z] (the reference's shape) -> ([N, 7] x 3).  z [k, N, Z]
+        with k > 1 draws k independent samples in ONE stacked forward (the
+        critic iterations' generator passes, or an inference sweep) and
+        returns [k, N, 7] tensors; the program-feature encoder runs once."""
         prep = vdata.prepared(local_graph, voxel_graph, self.configuration.NUM_CLASSES)
+        k = z.shape[0] if z.dim() == 3 else 1
         em = self.matched_features_encoder(prep.matched_x)
-        zz = z.squeeze(0)
         vx = prep.voxel_x
+        n = vx.shape[0]
+        if k == 1:
+            zz = z.reshape(n, -1)
+            csr = prep.csr
+        else:
+            zz = z.reshape(k * n, -1)
+            em = em.repeat(k, 1)
+            vx = vx.repeat(k, 1)
+            csr = prep.csr.stacked(k)
         x = self.mlp_encoder(torch.cat([em, vx, zz], dim=-1))
-        enc = self.encoder(x, prep.csr, self.rng)
+        enc = self.encoder(x, csr, self.rng, segments=k)
         logits = self.decoder(torch.cat([enc, x, em, vx, zz], dim=-1))
         if noise is None:
             noise = self.rng.exponential(logits.shape, logits.device)
-        label_hard, label_soft = ops.gumbel_head(logits, noise, self.tau)
+        label_hard, label_soft = ops.gumbel_head(logits, noise.reshape(logits.shape), self.tau)
+        if k > 1:
+            return logits.view(k, n, -1), label_hard.view(k, n, -1), label_soft.view(k, n, -1)
         return logits, label_hard, label_soft
 
 

@@ -387,52 +387,73 @@ def graphnorm_relu_dropout_torch(x, weight, bias, mean_scale, keep, eps):
 
 
 class _GraphNormReLUDropout(Function):
+    """GraphNorm(batch=None) + ReLU + Dropout; ``segments`` > 1 normalises that
+    many equal row blocks independently (stacked forwards of one batch)."""
+
     @staticmethod
-    def forward(ctx, x, weight, bias, mean_scale, keep, eps):
+    def forward(ctx, x, weight, bias, mean_scale, keep, eps, spec, segments):
         x = _f32(x)
         w, b, ms = _f32(weight), _f32(bias), _f32(mean_scale)
         kp = _f32(keep) if keep is not None else None
         require_cuda(x, w, b, ms, kp)
-        n, c = x.shape
+        rows, c = x.shape
+        S = int(segments)
+        if S < 1 or rows % S:
+            raise ValueError("graphnorm: rows must split into equal segments")
+        n = rows // S
         if w.numel() != c or b.numel() != c or ms.numel() != c or (kp is not None and kp.shape != x.shape):
             raise ValueError("graphnorm: inconsistent shapes")
         y = torch.empty_like(x)
-        stats = torch.empty(2 * c, dtype=torch.float32, device=x.device)
-        ws = torch.empty(int(LIB.vg_graphnorm_ws_floats(n, c)), dtype=torch.float32, device=x.device)
-        check(LIB.vg_graphnorm_fwd(ptr(x), n, c, ptr(w), ptr(b), ptr(ms), ptr(kp), float(eps), ptr(y), ptr(stats),
-                                   ptr(ws), stream_handle(x.device)), "vg_graphnorm_fwd")
-        ctx.eps, ctx.has_keep = eps, keep is not None
-        ctx.save_for_backward(x, weight, bias, mean_scale, keep if keep is not None else x.new_empty(0), stats)
+        stats = torch.empty(S * 2 * c, dtype=torch.float32, device=x.device)
+        ws = torch.empty(int(LIB.vg_graphnorm_seg_ws_floats(S, n, c)), dtype=torch.float32, device=x.device)
+        if spec is not None:  # dropout drawn in-kernel (device RNG)
+            if tuple(spec.shape) != tuple(x.shape):
+                raise ValueError("graphnorm: dropout spec shape differs from x")
+            kp = torch.empty_like(x)
+            check(LIB.vg_graphnorm_fwd_drop(ptr(x), S, n, c, ptr(w), ptr(b), ptr(ms), float(spec.p), int(spec.seed),
+                                            ptr(spec.iter), int(spec.salt) & 0xFFFFFFFF, float(eps), ptr(y), ptr(kp),
+                                            ptr(stats), ptr(ws), stream_handle(x.device)), "vg_graphnorm_fwd_drop")
+        else:
+            check(LIB.vg_graphnorm_fwd_seg(ptr(x), S, n, c, ptr(w), ptr(b), ptr(ms), ptr(kp), float(eps), ptr(y),
+                                           ptr(stats), ptr(ws), stream_handle(x.device)), "vg_graphnorm_fwd_seg")
+        ctx.eps, ctx.has_keep, ctx.segments = eps, kp is not None, S
+        ctx.save_for_backward(x, weight, bias, mean_scale, kp if kp is not None else x.new_empty(0), stats)
         return y
 
     @staticmethod
     def backward(ctx, g_y):
         x, w, b, ms, keep, stats = ctx.saved_tensors
         kp = keep if ctx.has_keep else None
+        S = ctx.segments
         if torch.is_grad_enabled():
             ins = [x, w, b, ms]
             with torch.enable_grad():
-                y = graphnorm_relu_dropout_torch(x, w, b, ms, kp, ctx.eps)
+                parts = zip(x.chunk(S), kp.chunk(S) if kp is not None else [None] * S)
+                y = torch.cat([graphnorm_relu_dropout_torch(xs, w, b, ms, ks, ctx.eps) for xs, ks in parts])
                 need = [t for t in ins if t.requires_grad]
                 grads = torch.autograd.grad(y, need, g_y, create_graph=True, allow_unused=True)
             it = iter(grads)
             res = [next(it) if t.requires_grad else None for t in ins]
-            return res[0], res[1], res[2], res[3], None, None
+            return res[0], res[1], res[2], res[3], None, None, None, None
         g_y = _f32(g_y)
-        n, c = x.shape
+        rows, c = x.shape
+        n = rows // S
         g_x = torch.empty_like(x)
         g_w = torch.empty(c, dtype=torch.float32, device=x.device)
         g_b = torch.empty_like(g_w)
         g_ms = torch.empty_like(g_w)
-        ws = torch.empty(int(LIB.vg_graphnorm_ws_floats(n, c)), dtype=torch.float32, device=x.device)
-        check(LIB.vg_graphnorm_bwd(ptr(x), n, c, ptr(w), ptr(b), ptr(ms), ptr(kp), float(ctx.eps), ptr(stats),
-                                   ptr(g_y), ptr(g_x), ptr(g_w), ptr(g_b), ptr(g_ms), ptr(ws), stream_handle(x.device)),
-              "vg_graphnorm_bwd")
-        return g_x, g_w, g_b, g_ms, None, None
+        ws = torch.empty(int(LIB.vg_graphnorm_seg_ws_floats(S, n, c)), dtype=torch.float32, device=x.device)
+        check(LIB.vg_graphnorm_bwd_seg(ptr(x), S, n, c, ptr(w), ptr(b), ptr(ms), ptr(kp), float(ctx.eps), ptr(stats),
+                                       ptr(g_y), ptr(g_x), ptr(g_w), ptr(g_b), ptr(g_ms), 0, None, 0, ptr(ws),
+                                       stream_handle(x.device)), "vg_graphnorm_bwd_seg")
+        return g_x, g_w, g_b, g_ms, None, None, None, None
 
 
-def graphnorm_relu_dropout(x, weight, bias, mean_scale, keep: Optional[torch.Tensor], eps: float = 1e-5):
-    return _GraphNormReLUDropout.apply(x, weight, bias, mean_scale, keep, eps)
+def graphnorm_relu_dropout(x, weight, bias, mean_scale, keep, eps: float = 1e-5, segments: int = 1):
+    """keep: dropout multipliers [N, C], a ``vgan.rng.DropSpec`` (drawn in-kernel) or None."""
+    if keep is not None and not isinstance(keep, torch.Tensor):
+        return _GraphNormReLUDropout.apply(x, weight, bias, mean_scale, None, eps, keep, segments)
+    return _GraphNormReLUDropout.apply(x, weight, bias, mean_scale, keep, eps, None, segments)
 
 
 # ------------------------------------------------------ type-matched mean

@@ -10,16 +10,33 @@ penalty (``trainer.py:298``).
 * ``RNG("host")`` draws exactly those tensors, with the same ops and shapes, on
   the CPU default generator and copies them to the device -- the GPU path then
   sees bit-identical randomness to the reference CPU run (parity mode).
-* ``RNG("device")`` draws them on the GPU generator (fast mode; hipGraph-safe).
+* ``RNG("device")`` draws them on the GPU (fast mode; hipGraph-safe): z, eps and
+  the Gumbel noise on torch's CUDA generator; each dropout mask as a
+  ``DropSpec`` that the GraphNorm kernel materialises in-kernel from a
+  counter-based Philox keyed by (seed, device iteration counter, call-site
+  salt) -- no extra launches.  ``reset()`` at the start of every iteration
+  body advances the device counter (one tiny launch, captured in the graph),
+  so hipGraph replays draw fresh masks.
 * ``RNG("fixed")`` (tests only) hands out the same seeded tensors for the k-th
   draw of every iteration body (``reset()`` at each body start), so an eager
   step and a hipGraph replay see identical randomness.
 """
 from __future__ import annotations
 
-from typing import Sequence
+from dataclasses import dataclass
+from typing import Dict, Sequence
 
 import torch
+
+
+@dataclass
+class DropSpec:
+    """A dropout mask to be drawn inside the consuming kernel."""
+    p: float
+    seed: int
+    iter: torch.Tensor  # int64 [1] on the device
+    salt: int
+    shape: tuple
 
 
 class RNG:
@@ -30,9 +47,22 @@ class RNG:
         self.seed = seed
         self._k = 0
         self._fixed = {}
+        self._salt = 0
+        self._iters: Dict[torch.device, torch.Tensor] = {}
 
     def reset(self) -> None:
+        """Start of an iteration body (fixed draws restart; device masks advance)."""
         self._k = 0
+        self._salt = 0
+        for t in self._iters.values():
+            t.add_(1)
+
+    def _iter(self, device) -> torch.Tensor:
+        device = torch.device(device)
+        t = self._iters.get(device)
+        if t is None:
+            t = self._iters[device] = torch.zeros(1, dtype=torch.int64, device=device)
+        return t
 
     def _fixed_draw(self, kind: str, shape, device, make):
         key = (self._k, kind, tuple(shape))
@@ -65,8 +95,12 @@ class RNG:
             return self._fixed_draw("e", shape, device, lambda g: torch.empty(*shape).exponential_(generator=g))
         return self._out(torch.empty(*shape, device=self._dev(device)).exponential_(), device)
 
-    def keep_mask(self, shape: Sequence[int], p: float, device) -> torch.Tensor:
-        """Dropout multiplier: Bernoulli(1 - p) / (1 - p), as ATen's CPU dropout."""
+    def keep_mask(self, shape: Sequence[int], p: float, device):
+        """Dropout multiplier: Bernoulli(1 - p) / (1 - p), as ATen's CPU dropout
+        (a ``DropSpec`` drawn in-kernel in device mode)."""
+        if self.mode == "device":
+            self._salt += 1
+            return DropSpec(float(p), int(self.seed) & ((1 << 64) - 1), self._iter(device), self._salt, tuple(shape))
         if self.mode == "fixed":
             return self._fixed_draw("k", shape, device,
                                     lambda g: torch.empty(*shape).bernoulli_(1 - p, generator=g).div_(1 - p))

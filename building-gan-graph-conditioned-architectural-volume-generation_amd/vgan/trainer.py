@@ -59,7 +59,8 @@ class Trainer:
         self.log_dir = log_dir or os.path.join(configuration.LOG_DIR,
                                                datetime.datetime.now().strftime("%m-%d-%Y__%H-%M-%S"))
         runtime = getattr(configuration, "runtime", {})
-        self.rng = RNG(runtime.get("rng", "device"))
+        self.rng = RNG(runtime.get("rng", "device"),
+                       seed=torch.initial_seed() + 7919 * int(runtime.get("rank", 0)))
         generator.rng = self.rng
         discriminator.rng = self.rng
         self.flat_g = FlatParams(generator)
@@ -142,50 +143,36 @@ class Trainer:
         logits, hard, soft = self.generator(local_graph, voxel_graph, z)
         return logits, hard.unsqueeze(0), soft.unsqueeze(0)
 
-    def step(self, local_graph, voxel_graph) -> Dict[str, torch.Tensor]:
-        """One full G+D step (trainer.py:466-495); returns device tensors."""
-        cfg = self.configuration
-        d_losses: List[torch.Tensor] = []
-        for _ in range(cfg.N_CRITIC):
-            self.rng.reset()
+    def _stacked_labels(self) -> bool:
+        """Generate all N_CRITIC critic-iteration labels in one stacked G
+        forward?  G is not updated during the critic iterations
+        (trainer.py:466-481), so the N_CRITIC no-grad forwards differ only in
+        their random draws; with device RNG they run as one forward over
+        N_CRITIC stacked copies.  Host / fixed RNG keep the reference's
+        per-iteration draw order."""
+        return (self.rng.mode == "device" and self.configuration.N_CRITIC > 1
+                and getattr(self.configuration, "runtime", {}).get("stack_critic_g", True))
+
+    def _critic_labels(self, local_graph, voxel_graph):
+        """[N_CRITIC, N, 7] (hard, soft) from one stacked no-grad G forward."""
+        self.rng.reset()
+        z = self.rng.normal((self.configuration.N_CRITIC, voxel_graph.num_nodes, self.configuration.Z_DIM),
+                            voxel_graph.x.device)
+        with torch.no_grad():
+            _, hard, soft = self.generator(local_graph, voxel_graph, z)
+        return hard, soft
+
+    def _critic_iteration(self, local_graph, voxel_graph, labels, i: int) -> torch.Tensor:
+        self.rng.reset()
+        if labels is not None:
+            hard, soft = labels[0][i:i + 1], labels[1][i:i + 1]
+        else:
             with torch.no_grad():
                 _, hard, soft = self._generate(local_graph, voxel_graph)
-            self.adam_d.zero_grad()
-            d_loss = self._critic_loss_backward(local_graph, voxel_graph, hard, soft)
-            d_losses.append(d_loss.detach())
-            self.sync.all_reduce_grad(self.flat_d)
-            self.adam_d.step()
-
-        self.rng.reset()
-        logits, hard, soft = self._generate(local_graph, voxel_graph)
-        self.adam_g.zero_grad()
-        d_params = list(self.discriminator.parameters())
-        if self.skip_dead_d_grads:
-            for p in d_params:
-                p.requires_grad_(False)
-        try:
-            g_loss = self._compute_generator_loss(local_graph, voxel_graph, logits, hard)
-            g_loss.backward()
-        finally:
-            if self.skip_dead_d_grads:
-                for p in d_params:
-                    p.requires_grad_(True)
-        self.sync.all_reduce_grad(self.flat_g)
-        self.adam_g.step()
-        return {"d_losses": torch.stack(d_losses), "g_loss": g_loss.detach(), "label_hard": hard.detach()}
-
-    # ------------------------------------------------- hipGraph-captured step
-    def _critic_body(self, local_graph, voxel_graph, acc, with_adam: bool):
-        self.rng.reset()
-        with torch.no_grad():
-            _, hard, soft = self._generate(local_graph, voxel_graph)
         self.adam_d.zero_grad()
-        d_loss = self._critic_loss_backward(local_graph, voxel_graph, hard, soft)
-        acc[0].add_(d_loss.detach())
-        if with_adam:
-            self.adam_d.step()
+        return self._critic_loss_backward(local_graph, voxel_graph, hard, soft)
 
-    def _gen_body(self, local_graph, voxel_graph, acc, with_adam: bool):
+    def _gen_iteration(self, local_graph, voxel_graph):
         self.rng.reset()
         logits, hard, _ = self._generate(local_graph, voxel_graph)
         self.adam_g.zero_grad()
@@ -200,6 +187,32 @@ class Trainer:
             if self.skip_dead_d_grads:
                 for p in d_params:
                     p.requires_grad_(True)
+        return g_loss, hard
+
+    def step(self, local_graph, voxel_graph) -> Dict[str, torch.Tensor]:
+        """One full G+D step (trainer.py:466-495); returns device tensors."""
+        cfg = self.configuration
+        labels = self._critic_labels(local_graph, voxel_graph) if self._stacked_labels() else None
+        d_losses: List[torch.Tensor] = []
+        for i in range(cfg.N_CRITIC):
+            d_loss = self._critic_iteration(local_graph, voxel_graph, labels, i)
+            d_losses.append(d_loss.detach())
+            self.sync.all_reduce_grad(self.flat_d)
+            self.adam_d.step()
+        g_loss, hard = self._gen_iteration(local_graph, voxel_graph)
+        self.sync.all_reduce_grad(self.flat_g)
+        self.adam_g.step()
+        return {"d_losses": torch.stack(d_losses), "g_loss": g_loss.detach(), "label_hard": hard.detach()}
+
+    # ------------------------------------------------- hipGraph-captured step
+    def _critic_body(self, local_graph, voxel_graph, acc, with_adam: bool, labels=None, i: int = 0):
+        d_loss = self._critic_iteration(local_graph, voxel_graph, labels, i)
+        acc[0].add_(d_loss.detach())
+        if with_adam:
+            self.adam_d.step()
+
+    def _gen_body(self, local_graph, voxel_graph, acc, with_adam: bool):
+        g_loss, hard = self._gen_iteration(local_graph, voxel_graph)
         acc[1].copy_(g_loss.detach())
         if with_adam:
             self.adam_g.step()
@@ -217,14 +230,22 @@ class Trainer:
             d.copy_(s_)
 
     def capture(self, local_graph, voxel_graph):
-        """Record the step of this (static) batch as two hipGraphs: one critic
-        iteration (replayed N_CRITIC times -- RNG, parameters and Adam state
-        advance in place) and the generator iteration.  Needs device RNG.  With
-        several ranks the RCCL all-reduce and Adam run eagerly between replays."""
+        """Record the step of this (static) batch as hipGraphs.
+
+        * stacked labels (device RNG): one graph for the stacked critic-label
+          G forward, one per critic iteration (each reads its own label slice)
+          and one for the generator iteration;
+        * otherwise: one critic-iteration graph replayed N_CRITIC times and the
+          generator graph.
+        RNG counters, parameters and Adam state advance in place on the device.
+        With several ranks the RCCL all-reduce and Adam run eagerly between
+        replays.  Needs device-side randomness (device or fixed RNG)."""
         if self.rng.mode == "host":
             raise RuntimeError("graph capture needs device-side randomness (runtime['rng'] 'device')")
         dev = voxel_graph.x.device
+        n_critic = self.configuration.N_CRITIC
         with_adam = not self.sync.active
+        stacked = self._stacked_labels()
         acc = torch.zeros(2, dtype=torch.float32, device=dev)
         vdata.prepared(local_graph, voxel_graph, self.configuration.NUM_CLASSES)  # CSR etc. before capture
         self.adam_g.sync_lr()
@@ -233,20 +254,31 @@ class Trainer:
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):  # warm-up (lazy init) on a side stream, then undo it
-            self._critic_body(local_graph, voxel_graph, acc, with_adam)
+            labels = self._critic_labels(local_graph, voxel_graph) if stacked else None
+            self._critic_body(local_graph, voxel_graph, acc, with_adam, labels, 0)
             self._gen_body(local_graph, voxel_graph, acc, with_adam)
         torch.cuda.current_stream(dev).wait_stream(side)
         self._restore(snap)
         pool = getattr(self, "_graph_pool", None)
         if pool is None:
             pool = self._graph_pool = torch.cuda.graph_pool_handle()
-        g_critic, g_gen = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g_critic, pool=pool):
-            self._critic_body(local_graph, voxel_graph, acc, with_adam)
+        g_labels, labels = None, None
+        if stacked:
+            g_labels = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_labels, pool=pool):
+                labels = self._critic_labels(local_graph, voxel_graph)
+        critic = []
+        for i in range(n_critic if stacked else 1):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                self._critic_body(local_graph, voxel_graph, acc, with_adam, labels, i)
+            critic.append(g)
+        g_gen = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g_gen, pool=pool):
             hard = self._gen_body(local_graph, voxel_graph, acc, with_adam)
         self._restore(snap)
-        graphs = {"critic": g_critic, "gen": g_gen, "acc": acc, "hard": hard, "with_adam": with_adam}
+        graphs = {"labels": g_labels, "label_tensors": labels, "critic": critic, "gen": g_gen, "acc": acc,
+                  "hard": hard, "with_adam": with_adam}
         voxel_graph.set_derived("step_graphs", graphs)
         return graphs
 
@@ -259,8 +291,11 @@ class Trainer:
         self.adam_d.sync_lr()
         acc = graphs["acc"]
         acc.zero_()
-        for _ in range(self.configuration.N_CRITIC):
-            graphs["critic"].replay()
+        if graphs["labels"] is not None:
+            graphs["labels"].replay()
+        critic = graphs["critic"]
+        for i in range(self.configuration.N_CRITIC):
+            critic[i if len(critic) > 1 else 0].replay()
             if not graphs["with_adam"]:
                 self.sync.all_reduce_grad(self.flat_d)
                 self.adam_d.step()

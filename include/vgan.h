@@ -177,6 +177,17 @@ int vg_graphnorm_fwd_seg(const float* x, int32_t segments, int32_t rows, int32_t
                          const float* weight, const float* bias, const float* mean_scale,
                          const float* keep, float eps, float* y, float* stats, float* workspace,
                          void* stream);
+/* vg_graphnorm_fwd_seg with the dropout drawn in-kernel: keep = Bernoulli(1-p)
+ * / (1-p) from a counter-based Philox4x32-10 keyed by seed on the counter
+ * (element, salt, *iter) -- *iter is read from device memory, so a hipGraph
+ * replay draws fresh masks once the caller advances it.  keep_out [S*N, C]
+ * receives the multipliers for the backward.  Replaces nn.Dropout(0.2)'s two
+ * launches (bernoulli_, div_) at models.py:75,85,195,205. */
+int vg_graphnorm_fwd_drop(const float* x, int32_t segments, int32_t rows, int32_t channels,
+                          const float* weight, const float* bias, const float* mean_scale,
+                          float p_drop, uint64_t seed, const int64_t* iter, uint32_t salt,
+                          float eps, float* y, float* keep_out, float* stats, float* workspace,
+                          void* stream);
 /* Backward over the segments; parameter gradients sum over segments and are
  * written (accumulate = 0) or added (1); g_w may be NULL (no parameter
  * gradients: g_b, g_ms are then ignored).  inj (nullable) is added to g_x

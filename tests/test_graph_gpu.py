@@ -55,7 +55,7 @@ def test_graph_iterations_match_eager_bodies(cuda, tiny):
         graphed.adam_d.step_t.copy_(eager.adam_d.step_t)
         graphs["acc"].zero_()
         acc_e.zero_()
-        graphs["critic"].replay()
+        graphs["critic"][0].replay()
         eager._critic_body(loc, vox, acc_e, True)
         torch.cuda.synchronize()
         assert abs(graphs["acc"][0].item() - acc_e[0].item()) <= 1e-4 * max(1.0, abs(acc_e[0].item())), it

@@ -348,3 +348,38 @@ def test_ln_act_matches_torch(cuda, C):
     assert rel_err(yd.cpu(), y) < 1e-5
     for a, r in zip(gd, gr):
         assert rel_err(a.cpu(), r) < 1e-4
+
+
+def test_graphnorm_in_kernel_dropout(cuda):
+    """Device-RNG dropout drawn inside the GraphNorm kernel: Bernoulli(0.8)/0.8
+    statistics, a fresh mask after the iteration counter advances, the same
+    mask for the same (seed, counter, salt), and the backward uses it."""
+    from vgan.rng import RNG
+
+    n, c = 20000, 32
+    x = torch.randn(n, c, device=cuda)
+    w, b, ms = torch.ones(c, device=cuda), torch.full((c,), 3.0, device=cuda), torch.ones(c, device=cuda)
+    rng = RNG("device", seed=1234)
+    rng.reset()
+    spec = rng.keep_mask((n, c), 0.2, cuda)
+    y1 = ops.graphnorm_relu_dropout(x, w, b, ms, spec)
+    y1b = ops.graphnorm_relu_dropout(x, w, b, ms, spec)
+    assert torch.equal(y1, y1b)
+    y_nodrop = ops.graphnorm_relu_dropout(x, w, b, ms, None)
+    keep = (y1 / y_nodrop).cpu()  # y_nodrop > 0 everywhere (bias 3)
+    assert set(torch.unique(torch.round(keep * 1000) / 1000).tolist()) <= {0.0, 1.25}
+    frac = (keep == 0).float().mean().item()
+    assert abs(frac - 0.2) < 0.01
+    rng.reset()
+    spec2 = rng.keep_mask((n, c), 0.2, cuda)
+    assert spec2.salt == spec.salt
+    y2 = ops.graphnorm_relu_dropout(x, w, b, ms, spec2)
+    assert (y2 != y1).float().mean().item() > 0.2
+    xr = x.clone().requires_grad_(True)
+    y3 = ops.graphnorm_relu_dropout(xr, w, b, ms, spec2)
+    (gx,) = torch.autograd.grad(y3.sum(), xr)
+    k3 = (y3.detach() / y_nodrop)
+    xr2 = x.clone().requires_grad_(True)
+    y4 = ops.graphnorm_relu_dropout(xr2, w, b, ms, k3.contiguous())
+    (gx2,) = torch.autograd.grad(y4.sum(), xr2)
+    assert torch.allclose(gx, gx2, rtol=1e-4, atol=1e-6)
