@@ -310,8 +310,8 @@ def main():
                 "global_batch": args.batch * world,
                 "avg_voxel_nodes_per_batch": round(n_nodes, 1),
                 "parallelism": f"dp{world}",
-                "execution": "hipGraph replay (1 critic-iteration graph x N_CRITIC + 1 generator graph)"
-                             if GRAPHED else "eager",
+                "execution": ("hipGraph replay: one stacked no-grad G forward for the N_CRITIC critic labels, "
+                              "N_CRITIC critic-engine graphs, one generator-iteration graph") if GRAPHED else "eager",
             },
             "roofline": {
                 "kernel": "vg_gat_fwd (fused GAT edge softmax + CSR gather-sum)",

@@ -71,6 +71,7 @@ class _LinearFn(Function):
     def forward(ctx, x, weight, bias, act):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
+        ctx.params = (weight, bias)
         return ops.gemm(x, weight, True, bias, act)
 
     @staticmethod
@@ -89,6 +90,10 @@ class _LinearFn(Function):
         gy = gy.contiguous()
         if ctx.needs_input_grad[0]:
             gx = ops.gemm(gy, weight, False)
+        pw, pb = ctx.params
+        if ctx.needs_input_grad[1] and ops._direct(pw, pb):  # accumulate into .grad directly
+            ops.gemm_tn_into(gy, x, pw.grad, pb.grad if ctx.has_bias else None)
+            return gx, None, None, None
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             gw, gb = ops.gemm_tn(gy, x, want_colsum=ctx.has_bias)
         return gx, gw, (gb if ctx.has_bias else None), None

@@ -99,6 +99,42 @@ def _f32(t: torch.Tensor) -> torch.Tensor:
     return t.contiguous()
 
 
+# ------------------------------------------------ direct parameter gradients
+_DIRECT_GRADS = False
+
+
+class direct_param_grads:
+    """Within this context a first-order ``backward()`` through the fused ops
+    accumulates parameter gradients straight into ``param.grad`` (views into
+    the flat gradient buffer) with the kernels' accumulate flag, and hands
+    autograd ``None`` for them -- no per-parameter AccumulateGrad ``add_``
+    launch.  Only for ``loss.backward()`` into existing ``.grad`` tensors (the
+    trainer's step), not for ``torch.autograd.grad``."""
+
+    def __enter__(self):
+        global _DIRECT_GRADS
+        self._prev, _DIRECT_GRADS = _DIRECT_GRADS, True
+        return self
+
+    def __exit__(self, *exc):
+        global _DIRECT_GRADS
+        _DIRECT_GRADS = self._prev
+        return False
+
+
+def _direct(*params) -> bool:
+    """All params take direct accumulation (flag on, leaf, fp32 contiguous .grad)."""
+    if not _DIRECT_GRADS:
+        return False
+    for p in params:
+        if p is None:
+            continue
+        g = p.grad
+        if not p.requires_grad or g is None or g.dtype != torch.float32 or not g.is_contiguous():
+            return False
+    return True
+
+
 # ----------------------------------------------------- sparse primitives
 def _empty_like_rows(csr: CSR, c: Optional[int], like: torch.Tensor) -> torch.Tensor:
     shape = (csr.num_nodes,) if c is None else (csr.num_nodes, c)
@@ -335,6 +371,7 @@ class _GATConv(Function):
         check(LIB.vg_gat_fwd(ptr(csr.row_ptr), ptr(csr.col), n, c, ptr(h), ptr(vs), ptr(vd), ptr(b), float(slope),
                              ptr(out), ptr(alpha), ptr(a_src), ptr(a_dst), csr.stream()), "vg_gat_fwd")
         ctx.csr, ctx.slope = csr, slope
+        ctx.params = (att_src, att_dst, bias)
         ctx.save_for_backward(h, att_src, att_dst, bias, alpha, a_src, a_dst)
         return out
 
@@ -358,15 +395,22 @@ class _GATConv(Function):
         n, c = h.shape
         dev = h.device
         g_h = torch.empty_like(h)
-        g_vs = torch.empty(c, dtype=torch.float32, device=dev)
-        g_vd = torch.empty_like(g_vs)
-        g_b = torch.empty_like(g_vs)
+        p_s, p_d, p_b = ctx.params
+        direct = _direct(p_s, p_d, p_b)
+        if direct:
+            g_vs, g_vd, g_b = p_s.grad, p_d.grad, p_b.grad
+        else:
+            g_vs = torch.empty(c, dtype=torch.float32, device=dev)
+            g_vd = torch.empty_like(g_vs)
+            g_b = torch.empty_like(g_vs)
         ws = torch.empty(int(LIB.vg_gat_bwd_ws_floats(n, csr.num_edges, c)), dtype=torch.float32, device=dev)
-        check(LIB.vg_gat_bwd(ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot), ptr(csr.csc_dst),
-                             n, csr.num_edges, c, ptr(h), ptr(_f32(att_src.reshape(-1))),
-                             ptr(_f32(att_dst.reshape(-1))), ptr(a_src), ptr(a_dst), ptr(alpha), ptr(g_out),
-                             float(ctx.slope), ptr(g_h), ptr(g_vs), ptr(g_vd), ptr(g_b), ptr(ws), csr.stream()),
-              "vg_gat_bwd")
+        check(LIB.vg_gat_bwd_ex(ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot), ptr(csr.csc_dst),
+                                n, csr.num_edges, c, ptr(h), ptr(_f32(att_src.reshape(-1))),
+                                ptr(_f32(att_dst.reshape(-1))), ptr(a_src), ptr(a_dst), ptr(alpha), ptr(g_out),
+                                float(ctx.slope), ptr(g_h), ptr(g_vs), ptr(g_vd), ptr(g_b), 1 if direct else 0, None, 0,
+                                ptr(ws), csr.stream()), "vg_gat_bwd_ex")
+        if direct:
+            return g_h, None, None, None, None, None
         return g_h, g_vs.view_as(att_src), g_vd.view_as(att_dst), g_b, None, None
 
 
@@ -417,6 +461,7 @@ class _GraphNormReLUDropout(Function):
             check(LIB.vg_graphnorm_fwd_seg(ptr(x), S, n, c, ptr(w), ptr(b), ptr(ms), ptr(kp), float(eps), ptr(y),
                                            ptr(stats), ptr(ws), stream_handle(x.device)), "vg_graphnorm_fwd_seg")
         ctx.eps, ctx.has_keep, ctx.segments = eps, kp is not None, S
+        ctx.params = (weight, bias, mean_scale)
         ctx.save_for_backward(x, weight, bias, mean_scale, kp if kp is not None else x.new_empty(0), stats)
         return y
 
@@ -439,13 +484,20 @@ class _GraphNormReLUDropout(Function):
         rows, c = x.shape
         n = rows // S
         g_x = torch.empty_like(x)
-        g_w = torch.empty(c, dtype=torch.float32, device=x.device)
-        g_b = torch.empty_like(g_w)
-        g_ms = torch.empty_like(g_w)
+        pw, pb, pms = ctx.params
+        direct = _direct(pw, pb, pms)
+        if direct:
+            g_w, g_b, g_ms = pw.grad, pb.grad, pms.grad
+        else:
+            g_w = torch.empty(c, dtype=torch.float32, device=x.device)
+            g_b = torch.empty_like(g_w)
+            g_ms = torch.empty_like(g_w)
         ws = torch.empty(int(LIB.vg_graphnorm_seg_ws_floats(S, n, c)), dtype=torch.float32, device=x.device)
         check(LIB.vg_graphnorm_bwd_seg(ptr(x), S, n, c, ptr(w), ptr(b), ptr(ms), ptr(kp), float(ctx.eps), ptr(stats),
-                                       ptr(g_y), ptr(g_x), ptr(g_w), ptr(g_b), ptr(g_ms), 0, None, 0, ptr(ws),
-                                       stream_handle(x.device)), "vg_graphnorm_bwd_seg")
+                                       ptr(g_y), ptr(g_x), ptr(g_w), ptr(g_b), ptr(g_ms), 1 if direct else 0, None, 0,
+                                       ptr(ws), stream_handle(x.device)), "vg_graphnorm_bwd_seg")
+        if direct:
+            return g_x, None, None, None, None, None, None, None
         return g_x, g_w, g_b, g_ms, None, None, None, None
 
 
@@ -554,6 +606,7 @@ class _LNAct(Function):
         check(LIB.vg_ln_act_fwd(ptr(x), n, c, ptr(g), ptr(b), float(eps), float(slope), ptr(y), ptr(mean), ptr(rstd),
                                 stream_handle(x.device)), "vg_ln_act_fwd")
         ctx.eps, ctx.slope = eps, slope
+        ctx.params = (gamma, beta)
         if save:
             ctx.save_for_backward(x, gamma, beta, mean, rstd)
         return y
@@ -573,11 +626,19 @@ class _LNAct(Function):
             return res[0], res[1], res[2], None, None
         g_y = _f32(g_y)
         g_x = torch.empty_like(x)
-        g_g = torch.empty(c, dtype=torch.float32, device=x.device)
-        g_b = torch.empty_like(g_g)
+        pg, pb = ctx.params
+        direct = _direct(pg, pb)
+        if direct:
+            g_g, g_b = pg.grad, pb.grad
+        else:
+            g_g = torch.empty(c, dtype=torch.float32, device=x.device)
+            g_b = torch.empty_like(g_g)
         ws = torch.empty(int(LIB.vg_ln_act_bwd_ws_floats(c)), dtype=torch.float32, device=x.device)
         check(LIB.vg_ln_act_bwd(ptr(x), n, c, ptr(gamma), ptr(beta), float(ctx.slope), ptr(mean), ptr(rstd), ptr(g_y),
-                                ptr(g_x), ptr(g_g), ptr(g_b), 0, ptr(ws), stream_handle(x.device)), "vg_ln_act_bwd")
+                                ptr(g_x), ptr(g_g), ptr(g_b), 1 if direct else 0, ptr(ws), stream_handle(x.device)),
+              "vg_ln_act_bwd")
+        if direct:
+            return g_x, None, None, None, None
         return g_x, g_g, g_b, None, None
 
 
@@ -616,6 +677,19 @@ def gemm_tn(a: torch.Tensor, b: torch.Tensor, want_colsum: bool = True):
     check(LIB.vg_gemm_tn(ptr(a), m, ptr(b), k, n, m, k, ptr(c), k, ptr(db), 0, ptr(ws), stream_handle(a.device)),
           "vg_gemm_tn")
     return c, db
+
+
+def gemm_tn_into(a: torch.Tensor, b: torch.Tensor, c_out: torch.Tensor, db_out: Optional[torch.Tensor]) -> None:
+    """c_out += a^T b and db_out += column sums of a (accumulating vg_gemm_tn)."""
+    a, b = _f32(a), _f32(b)
+    require_cuda(a, b, c_out, db_out)
+    n, m = a.shape
+    k = b.shape[1]
+    if b.shape[0] != n or tuple(c_out.shape) != (m, k):
+        raise ValueError("gemm_tn_into: inconsistent shapes")
+    ws = torch.empty(max(1, int(LIB.vg_gemm_tn_ws_floats(n, m, k))), dtype=torch.float32, device=a.device)
+    check(LIB.vg_gemm_tn(ptr(a), m, ptr(b), k, n, m, k, ptr(c_out), k, ptr(db_out), 1, ptr(ws),
+                         stream_handle(a.device)), "vg_gemm_tn")
 
 
 def adam_flat_dev(param, grad, exp_avg, exp_avg_sq, beta1, beta2, eps, weight_decay, lr_t, step_t):

@@ -182,7 +182,8 @@ class Trainer:
                 p.requires_grad_(False)
         try:
             g_loss = self._compute_generator_loss(local_graph, voxel_graph, logits, hard)
-            g_loss.backward()
+            with ops.direct_param_grads():
+                g_loss.backward()
         finally:
             if self.skip_dead_d_grads:
                 for p in d_params:
