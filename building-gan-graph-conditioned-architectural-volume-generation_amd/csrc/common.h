@@ -71,6 +71,27 @@ __device__ __forceinline__ float vg_keep(long long t, uint32_t salt, long long i
   return u < 1.f - p ? 1.f / (1.f - p) : 0.f;
 }
 
+// "Last block folds": every block calls this after writing its partials; it
+// returns true in exactly one block -- the last to arrive -- which then sees
+// all partials (release/acquire fences) and folds them in a fixed order, so
+// the result is deterministic and no separate fold launch is needed.
+// `counter` is a caller-owned int32 that is 0 on entry and reset to 0 by the
+// last block (launches that share a counter must be stream-ordered).
+__device__ __forceinline__ bool vg_last_block(int* counter) {
+  __shared__ int last;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int nblocks = static_cast<int>(gridDim.x * gridDim.y * gridDim.z);
+    const int prev = atomicAdd(counter, 1);
+    last = prev == nblocks - 1;
+    if (last) atomicExch(counter, 0);
+  }
+  __syncthreads();
+  if (last) __threadfence();
+  return last != 0;
+}
+
 static inline int vg_blocks(long long work, int per_block) {
   long long b = (work + per_block - 1) / per_block;
   return b < 1 ? 1 : static_cast<int>(b);

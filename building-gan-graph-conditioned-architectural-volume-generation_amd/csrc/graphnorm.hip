@@ -59,8 +59,15 @@ __host__ __device__ inline Lay lay_for(int C) {
   return {cw, 64 / cw};
 }
 
+__device__ void stats_final_body(const float* __restrict__ part, int chunks, int C,
+                                 float* __restrict__ stats, int slab, int seg);
+
+// counter != NULL: the last block to finish also merges every segment / slab
+// (stats_final_body), saving the separate finalize launch.
 __global__ void __launch_bounds__(kBlock) k_stats_partial(const float* __restrict__ x, int N, int C,
-                                                          float* __restrict__ part) {
+                                                          float* __restrict__ part,
+                                                          float* __restrict__ stats, int* counter) {
+  float* const part0 = part;
   const Lay ly = lay_for(C);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = blockIdx.y * 64 + (lane & (ly.cw - 1));
@@ -101,16 +108,20 @@ __global__ void __launch_bounds__(kBlock) k_stats_partial(const float* __restric
     p[1] = acc.mean;
     p[2] = acc.m2;
   }
+  if (counter && vg_last_block(counter))
+    for (int sg = 0; sg < (int)gridDim.z; ++sg)
+      for (int sl = 0; sl < (int)gridDim.y; ++sl) stats_final_body(part0, gridDim.x, C, stats, sl, sg);
 }
 
-// Merge the per-chunk Welford partials: one 256-thread block per 64 columns,
-// wave w merges chunks w, w+4, ... (fixed order), then the 4 waves in LDS.
-__global__ void __launch_bounds__(256) k_stats_final(const float* __restrict__ part, int chunks,
-                                                     int C, float* __restrict__ stats) {
+// Merge the per-chunk Welford partials of one 64-column slab of one segment
+// with 256 threads: wave w merges chunks w, w+4, ... (fixed order), then the
+// 4 waves in LDS.
+__device__ void stats_final_body(const float* __restrict__ part, int chunks, int C,
+                                 float* __restrict__ stats, int slab, int seg) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
-  part += (size_t)blockIdx.y * chunks * C * 3;  // segment
-  stats += (size_t)blockIdx.y * 2 * C;
+  const int c = slab * 64 + lane;
+  part += (size_t)seg * chunks * C * 3;  // segment
+  stats += (size_t)seg * 2 * C;
   Welford acc = {0.f, 0.f, 0.f};
   if (c < C)
     for (int k = wave; k < chunks; k += 4) {
@@ -125,6 +136,12 @@ __global__ void __launch_bounds__(256) k_stats_final(const float* __restrict__ p
     stats[c] = r.mean;
     stats[C + c] = sqrtf(fmaxf(r.m2 / r.n, 0.f));
   }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) k_stats_final(const float* __restrict__ part, int chunks,
+                                                     int C, float* __restrict__ stats) {
+  stats_final_body(part, chunks, C, stats, blockIdx.x, blockIdx.y);
 }
 
 // keep_out != NULL: draw the dropout multiplier in-kernel (vg_keep with
@@ -155,12 +172,22 @@ __global__ void k_gn_apply(const float* __restrict__ x, long long total, int C, 
   }
 }
 
-// backward: column partial sums of gz and gz*xhat (plain sums, chunk order)
+__device__ void bwd_final_body(const float* __restrict__ part, int chunks, int C, int S,
+                               const float* __restrict__ w, const float* __restrict__ ms, float eps,
+                               const float* __restrict__ stats, float* __restrict__ sums,
+                               float* __restrict__ g_w, float* __restrict__ g_b,
+                               float* __restrict__ g_ms, int accumulate, int slab);
+
+// backward: column partial sums of gz and gz*xhat (plain sums, chunk order);
+// counter != NULL: the last block also runs the finalize (bwd_final_body).
 __global__ void __launch_bounds__(kBlock) k_gn_bwd_partial(
     const float* __restrict__ x, const float* __restrict__ gy, int N, int C,
     const float* __restrict__ w, const float* __restrict__ b, const float* __restrict__ ms,
     const float* __restrict__ keep, float eps, const float* __restrict__ stats,
-    float* __restrict__ part) {
+    float* __restrict__ part, float* __restrict__ sums, float* __restrict__ g_w,
+    float* __restrict__ g_b, float* __restrict__ g_ms, int accumulate, int* counter) {
+  const float* const stats0 = stats;
+  float* const part0 = part;
   const Lay ly = lay_for(C);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = blockIdx.y * 64 + (lane & (ly.cw - 1));
@@ -208,15 +235,19 @@ __global__ void __launch_bounds__(kBlock) k_gn_bwd_partial(
     p[0] = a;
     p[1] = bb;
   }
+  if (counter && vg_last_block(counter))
+    for (int sl = 0; sl < (int)gridDim.y; ++sl)
+      bwd_final_body(part0, gridDim.x, C, gridDim.z, w, ms, eps, stats0, sums, g_w, g_b, g_ms,
+                     accumulate, sl);
 }
 
-__global__ void __launch_bounds__(256) k_gn_bwd_final(
-    const float* __restrict__ part, int chunks, int C, int S, const float* __restrict__ w,
-    const float* __restrict__ ms, float eps, const float* __restrict__ stats,
-    float* __restrict__ sums, float* __restrict__ g_w, float* __restrict__ g_b,
-    float* __restrict__ g_ms, int accumulate) {
+__device__ void bwd_final_body(const float* __restrict__ part, int chunks, int C, int S,
+                               const float* __restrict__ w, const float* __restrict__ ms, float eps,
+                               const float* __restrict__ stats, float* __restrict__ sums,
+                               float* __restrict__ g_w, float* __restrict__ g_b,
+                               float* __restrict__ g_ms, int accumulate, int slab) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+  const int c = slab * 64 + lane;
   __shared__ float red[4][64][2];
   float tw = 0.f, tb = 0.f, tm = 0.f;
   for (int sg = 0; sg < S; ++sg) {
@@ -247,6 +278,16 @@ __global__ void __launch_bounds__(256) k_gn_bwd_final(
     g_b[c] = accumulate ? g_b[c] + tb : tb;
     g_ms[c] = accumulate ? g_ms[c] + tm : tm;
   }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) k_gn_bwd_final(
+    const float* __restrict__ part, int chunks, int C, int S, const float* __restrict__ w,
+    const float* __restrict__ ms, float eps, const float* __restrict__ stats,
+    float* __restrict__ sums, float* __restrict__ g_w, float* __restrict__ g_b,
+    float* __restrict__ g_ms, int accumulate) {
+  bwd_final_body(part, chunks, C, S, w, ms, eps, stats, sums, g_w, g_b, g_ms, accumulate,
+                 blockIdx.x);
 }
 
 // g_x (+ inj for elements t >= inj_off: the second-order adjoint of the
@@ -285,11 +326,18 @@ __global__ void k_gn_bwd_apply(const float* __restrict__ x, const float* __restr
 // ---------------------------------------------------------- second order
 // column sums for the tangent / second-order pass: [sum u, sum xt u, sum p,
 // sum p u, sum p xt] per column (plain sums, chunk order)
+__device__ void jvp2_final_body(const float* __restrict__ part, int chunks, int N, int C,
+                                const float* __restrict__ w, const float* __restrict__ ms,
+                                float eps, const float* __restrict__ stats,
+                                float* __restrict__ sums, float* __restrict__ g_w,
+                                float* __restrict__ g_ms, int slab);
+
 __global__ void __launch_bounds__(kBlock) k_gn_jvp2_partial(
     const float* __restrict__ x, const float* __restrict__ u, const float* __restrict__ gy, int N,
     int C, const float* __restrict__ w, const float* __restrict__ b, const float* __restrict__ ms,
     const float* __restrict__ keep, float eps, const float* __restrict__ stats,
-    float* __restrict__ part) {
+    float* __restrict__ part, float* __restrict__ sums, float* __restrict__ g_w,
+    float* __restrict__ g_ms, int* counter) {
   const Lay ly = lay_for(C);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = blockIdx.y * 64 + (lane & (ly.cw - 1));
@@ -328,16 +376,20 @@ __global__ void __launch_bounds__(kBlock) k_gn_jvp2_partial(
 #pragma unroll
     for (int q = 0; q < 5; ++q) pp[q] = (s5[0][lane][q] + s5[1][lane][q]) + (s5[2][lane][q] + s5[3][lane][q]);
   }
+  if (counter && vg_last_block(counter))
+    for (int sl = 0; sl < (int)gridDim.y; ++sl)
+      jvp2_final_body(part, gridDim.x, N, C, w, ms, eps, stats, sums, g_w, g_ms, sl);
 }
 
 // per column: mu' = mean u, M = mean(xt u), Sp, P1 = sum p c', P2 = sum p c;
 // g_w += P1/d - P2 M/(sigma d^2);  g_ms += w (-mu' Sp/d + mu Sp M/(sigma d^2))
-__global__ void __launch_bounds__(256) k_gn_jvp2_final(
-    const float* __restrict__ part, int chunks, int N, int C, const float* __restrict__ w,
-    const float* __restrict__ ms, float eps, const float* __restrict__ stats,
-    float* __restrict__ sums, float* __restrict__ g_w, float* __restrict__ g_ms) {
+__device__ void jvp2_final_body(const float* __restrict__ part, int chunks, int N, int C,
+                                const float* __restrict__ w, const float* __restrict__ ms,
+                                float eps, const float* __restrict__ stats,
+                                float* __restrict__ sums, float* __restrict__ g_w,
+                                float* __restrict__ g_ms, int slab) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+  const int c = slab * 64 + lane;
   float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   if (c < C)
     for (int k = wave; k < chunks; k += 4) {
@@ -367,6 +419,14 @@ __global__ void __launch_bounds__(256) k_gn_jvp2_final(
     g_w[c] += P1 / d - P2 * M * isd / (d * d);
     g_ms[c] += wc * (-mup * Sp / d + mu * Sp * M * isd / (d * d));
   }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) k_gn_jvp2_final(
+    const float* __restrict__ part, int chunks, int N, int C, const float* __restrict__ w,
+    const float* __restrict__ ms, float eps, const float* __restrict__ stats,
+    float* __restrict__ sums, float* __restrict__ g_w, float* __restrict__ g_ms) {
+  jvp2_final_body(part, chunks, N, C, w, ms, eps, stats, sums, g_w, g_ms, blockIdx.x);
 }
 
 // u_out = keep [z>0] w (c'/d - c sigma'/d^2);  x_inj = dQ/dx
@@ -423,14 +483,14 @@ extern "C" int64_t vg_graphnorm_ws_floats(int32_t num_nodes, int32_t channels) {
 static int gn_fwd(const float* x, int32_t S, int32_t N, int32_t C, const float* weight,
                   const float* bias, const float* mean_scale, const float* keep, float eps, float* y,
                   float* stats, float* ws, float p_drop, uint64_t seed, const int64_t* iter,
-                  uint32_t salt, float* keep_out, void* stream) {
+                  uint32_t salt, float* keep_out, int32_t* sync, void* stream) {
   if (S <= 0 || N <= 0 || C <= 0 || !x || !weight || !bias || !mean_scale || !y || !stats || !ws)
     return VG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int chunks = chunks_for(N);
   dim3 grid(chunks, (C + 63) / 64, S);
-  k_stats_partial<<<grid, kBlock, 0, s>>>(x, N, C, ws);
-  k_stats_final<<<dim3(vg_blocks(C, 64), S), 256, 0, s>>>(ws, chunks, C, stats);
+  k_stats_partial<<<grid, kBlock, 0, s>>>(x, N, C, ws, stats, sync);
+  if (!sync) k_stats_final<<<dim3(vg_blocks(C, 64), S), 256, 0, s>>>(ws, chunks, C, stats);
   const long long total = (long long)S * N * C;
   k_gn_apply<<<apply_blocks(total), 256, 0, s>>>(x, total, C, (long long)N * C, weight, bias,
                                                  mean_scale, keep, eps, stats, y, p_drop,
@@ -444,26 +504,28 @@ static int gn_fwd(const float* x, int32_t S, int32_t N, int32_t C, const float* 
 extern "C" int vg_graphnorm_fwd_seg(const float* x, int32_t S, int32_t N, int32_t C,
                                     const float* weight, const float* bias,
                                     const float* mean_scale, const float* keep, float eps,
-                                    float* y, float* stats, float* ws, void* stream) {
+                                    float* y, float* stats, float* ws, int32_t* sync,
+                                    void* stream) {
   return gn_fwd(x, S, N, C, weight, bias, mean_scale, keep, eps, y, stats, ws, 0.f, 0, nullptr, 0,
-                nullptr, stream);
+                nullptr, sync, stream);
 }
 
 extern "C" int vg_graphnorm_fwd_drop(const float* x, int32_t S, int32_t N, int32_t C,
                                      const float* weight, const float* bias,
                                      const float* mean_scale, float p_drop, uint64_t seed,
                                      const int64_t* iter, uint32_t salt, float eps, float* y,
-                                     float* keep_out, float* stats, float* ws, void* stream) {
+                                     float* keep_out, float* stats, float* ws, int32_t* sync,
+                                     void* stream) {
   if (!iter || !keep_out || !(p_drop >= 0.f && p_drop < 1.f)) return VG_EINVAL;
   return gn_fwd(x, S, N, C, weight, bias, mean_scale, nullptr, eps, y, stats, ws, p_drop, seed,
-                iter, salt, keep_out, stream);
+                iter, salt, keep_out, sync, stream);
 }
 
 extern "C" int vg_graphnorm_fwd(const float* x, int32_t N, int32_t C, const float* weight,
                                 const float* bias, const float* mean_scale, const float* keep,
                                 float eps, float* y, float* stats, float* ws, void* stream) {
   return vg_graphnorm_fwd_seg(x, 1, N, C, weight, bias, mean_scale, keep, eps, y, stats, ws,
-                              stream);
+                              nullptr, stream);
 }
 
 extern "C" int vg_graphnorm_bwd_seg(const float* x, int32_t S, int32_t N, int32_t C,
@@ -471,7 +533,7 @@ extern "C" int vg_graphnorm_bwd_seg(const float* x, int32_t S, int32_t N, int32_
                                     const float* mean_scale, const float* keep, float eps,
                                     const float* stats, const float* g_y, float* g_x, float* g_w,
                                     float* g_b, float* g_ms, int32_t accumulate, const float* inj,
-                                    int64_t inj_offset, float* ws, void* stream) {
+                                    int64_t inj_offset, float* ws, int32_t* sync, void* stream) {
   if (S <= 0 || N <= 0 || C <= 0 || !x || !weight || !bias || !mean_scale || !stats || !g_y ||
       !g_x || !ws || (g_w && (!g_b || !g_ms)) || inj_offset < 0)
     return VG_EINVAL;
@@ -481,9 +543,10 @@ extern "C" int vg_graphnorm_bwd_seg(const float* x, int32_t S, int32_t N, int32_
   float* sums = ws + (size_t)S * kChunks * C * 5;
   dim3 grid(chunks, (C + 63) / 64, S);
   k_gn_bwd_partial<<<grid, kBlock, 0, s>>>(x, g_y, N, C, weight, bias, mean_scale, keep, eps,
-                                           stats, part);
-  k_gn_bwd_final<<<vg_blocks(C, 64), 256, 0, s>>>(part, chunks, C, S, weight, mean_scale, eps,
-                                                  stats, sums, g_w, g_b, g_ms, accumulate);
+                                           stats, part, sums, g_w, g_b, g_ms, accumulate, sync);
+  if (!sync)
+    k_gn_bwd_final<<<vg_blocks(C, 64), 256, 0, s>>>(part, chunks, C, S, weight, mean_scale, eps,
+                                                    stats, sums, g_w, g_b, g_ms, accumulate);
   const long long total = (long long)S * N * C;
   k_gn_bwd_apply<<<apply_blocks(total), 256, 0, s>>>(x, g_y, total, N, C, weight, bias,
                                                      mean_scale, keep, eps, stats, sums, inj,
@@ -498,14 +561,14 @@ extern "C" int vg_graphnorm_bwd(const float* x, int32_t N, int32_t C, const floa
                                 float* g_w, float* g_b, float* g_ms, float* ws, void* stream) {
   if (!g_w || !g_b || !g_ms) return VG_EINVAL;
   return vg_graphnorm_bwd_seg(x, 1, N, C, weight, bias, mean_scale, keep, eps, stats, g_y, g_x,
-                              g_w, g_b, g_ms, 0, nullptr, 0, ws, stream);
+                              g_w, g_b, g_ms, 0, nullptr, 0, ws, nullptr, stream);
 }
 
 extern "C" int vg_graphnorm_jvp2(const float* x, int32_t N, int32_t C, const float* weight,
                                  const float* bias, const float* mean_scale, const float* keep,
                                  float eps, const float* stats, const float* u, const float* g_y,
                                  float* u_out, float* x_inj, float* g_w, float* g_ms, float* ws,
-                                 void* stream) {
+                                 int32_t* sync, void* stream) {
   if (N <= 0 || C <= 0 || !x || !weight || !bias || !mean_scale || !stats || !u || !g_y ||
       !u_out || !x_inj || !g_w || !g_ms || !ws)
     return VG_EINVAL;
@@ -515,9 +578,10 @@ extern "C" int vg_graphnorm_jvp2(const float* x, int32_t N, int32_t C, const flo
   float* sums = ws + (size_t)kChunks * C * 5;
   dim3 grid(chunks, (C + 63) / 64);
   k_gn_jvp2_partial<<<grid, kBlock, 0, s>>>(x, u, g_y, N, C, weight, bias, mean_scale, keep, eps,
-                                            stats, part);
-  k_gn_jvp2_final<<<vg_blocks(C, 64), 256, 0, s>>>(part, chunks, N, C, weight, mean_scale, eps,
-                                                   stats, sums, g_w, g_ms);
+                                            stats, part, sums, g_w, g_ms, sync);
+  if (!sync)
+    k_gn_jvp2_final<<<vg_blocks(C, 64), 256, 0, s>>>(part, chunks, N, C, weight, mean_scale, eps,
+                                                     stats, sums, g_w, g_ms);
   const long long total = (long long)N * C;
   k_gn_jvp2_apply<<<apply_blocks(total), 256, 0, s>>>(x, u, g_y, total, N, C, weight, bias,
                                                       mean_scale, keep, eps, stats, sums, u_out,

@@ -56,13 +56,13 @@ SIGNATURES = {
                                    _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "vg_graphnorm_seg_ws_floats": (_c_i64, [_c_i32, _c_i32, _c_i32]),
     "vg_graphnorm_fwd_seg": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p,
-                                            _c_p, _c_p]),
+                                            _c_p, _c_p, _c_p]),
     "vg_graphnorm_fwd_drop": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_f32, ctypes.c_uint64,
-                                             _c_p, ctypes.c_uint32, _c_f32, _c_p, _c_p, _c_p, _c_p, _c_p]),
+                                             _c_p, ctypes.c_uint32, _c_f32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "vg_graphnorm_bwd_seg": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p,
-                                            _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_i64, _c_p, _c_p]),
+                                            _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_i64, _c_p, _c_p, _c_p]),
     "vg_graphnorm_jvp2": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p,
-                                         _c_p, _c_p, _c_p, _c_p, _c_p]),
+                                         _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "vg_ln_act_fwd": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_f32, _c_f32, _c_p, _c_p, _c_p, _c_p]),
     "vg_ln_act_bwd_ws_floats": (_c_i64, [_c_i32]),
     "vg_ln_act_bwd": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
@@ -99,6 +99,19 @@ def ptr(t: Optional[torch.Tensor]):
 
 def stream_handle(device: torch.device) -> ctypes.c_void_p:
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+_SYNC = {}
+
+
+def sync_counter(device: torch.device):
+    """Persistent zeroed int32 device counter per (device, current stream) for
+    the kernels' last-block fold (left at 0 by every launch)."""
+    key = (torch.device(device), torch.cuda.current_stream(device).cuda_stream)
+    t = _SYNC.get(key)
+    if t is None:
+        t = _SYNC[key] = torch.zeros(1, dtype=torch.int32, device=device)
+    return ptr(t)
 
 
 def check(rc: int, name: str) -> None:

@@ -37,7 +37,7 @@ import torch
 import torch.nn as nn
 
 from . import data as vdata
-from ._lib import LIB, check, ptr, stream_handle
+from ._lib import LIB, check, ptr, stream_handle, sync_counter
 
 ACT_NONE, ACT_RELU, ACT_MASK = 0, 1, 3
 
@@ -116,6 +116,7 @@ class CriticEngine:
         hard, soft = hard.contiguous(), soft.contiguous()
         dev = mvx.device
         st = stream_handle(dev)
+        sy = sync_counter(dev)
         R, W0 = 3 * n, F + K
         csr = prep.csr
         csr3 = csr.stacked(3)
@@ -155,11 +156,11 @@ class CriticEngine:
                 check(LIB.vg_graphnorm_fwd_drop(ptr(O), 3, n, c, ptr(norm.weight), ptr(norm.bias),
                                                 ptr(norm.mean_scale), float(spec.p), int(spec.seed), ptr(spec.iter),
                                                 int(spec.salt) & 0xFFFFFFFF, float(norm.eps), ptr(Y), ptr(keep),
-                                                ptr(stats), ptr(ws), st), "vg_graphnorm_fwd_drop")
+                                                ptr(stats), ptr(ws), sy, st), "vg_graphnorm_fwd_drop")
             else:
                 check(LIB.vg_graphnorm_fwd_seg(ptr(O), 3, n, c, ptr(norm.weight), ptr(norm.bias),
                                                ptr(norm.mean_scale), ptr(keep), float(norm.eps), ptr(Y), ptr(stats),
-                                               ptr(ws), st), "vg_graphnorm_fwd_seg")
+                                               ptr(ws), sy, st), "vg_graphnorm_fwd_seg")
             blk.append(dict(X=x, xw=xw, H=H, O=O, alpha=alpha, a_s=a_s, a_d=a_d, Y=Y, stats=stats, keep=keep, c=c))
             x, xw = Y, c
         dec_out = []
@@ -206,7 +207,7 @@ class CriticEngine:
             check(LIB.vg_graphnorm_bwd_seg(mix(B["O"], c), 1, n, c, ptr(norm.weight), ptr(norm.bias),
                                            ptr(norm.mean_scale), mix(B["keep"], c) if B["keep"] is not None else None,
                                            float(norm.eps), _off(B["stats"], 2 * 2 * c), ptr(dY), ptr(dO), None, None,
-                                           None, 0, None, 0, ptr(ws), st), "vg_graphnorm_bwd_seg")
+                                           None, 0, None, 0, ptr(ws), sy, st), "vg_graphnorm_bwd_seg")
             dH = _f(n, c, dev=dev)
             ws = _f(int(LIB.vg_gat_bwd_ws_floats(n, E, c)), dev=dev)
             check(LIB.vg_gat_bwd_ex(ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot),
@@ -270,7 +271,7 @@ class CriticEngine:
             check(LIB.vg_graphnorm_jvp2(mix(B["O"], c), n, c, ptr(norm.weight), ptr(norm.bias), ptr(norm.mean_scale),
                                         mix(B["keep"], c) if B["keep"] is not None else None, float(norm.eps),
                                         _off(B["stats"], 2 * 2 * c), ptr(uO), ptr(dY_b[b]), ptr(uYn), ptr(oinj),
-                                        ptr(norm.weight.grad), ptr(norm.mean_scale.grad), ptr(ws), st),
+                                        ptr(norm.weight.grad), ptr(norm.mean_scale.grad), ptr(ws), sy, st),
                   "vg_graphnorm_jvp2")
             hinj_b[b], oinj_b[b] = hinj, oinj
             uY, uw = uYn, c
@@ -317,7 +318,7 @@ class CriticEngine:
             check(LIB.vg_graphnorm_bwd_seg(ptr(B["O"]), 3, n, c, ptr(norm.weight), ptr(norm.bias),
                                            ptr(norm.mean_scale), ptr(B["keep"]), float(norm.eps), ptr(B["stats"]),
                                            ptr(dY), ptr(dO), ptr(norm.weight.grad), ptr(norm.bias.grad),
-                                           ptr(norm.mean_scale.grad), 1, ptr(oinj_b[b]), mrow * c, ptr(ws), st),
+                                           ptr(norm.mean_scale.grad), 1, ptr(oinj_b[b]), mrow * c, ptr(ws), sy, st),
                   "vg_graphnorm_bwd_seg")
             dH = _f(R, c, dev=dev)
             ws = _f(int(LIB.vg_gat_bwd_ws_floats(R, 3 * E, c)), dev=dev)

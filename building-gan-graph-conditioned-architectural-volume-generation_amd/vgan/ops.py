@@ -25,7 +25,7 @@ import torch
 from torch.autograd import Function
 
 from . import _lib
-from ._lib import LIB, check, ptr, require_cuda, stream_handle
+from ._lib import LIB, check, ptr, require_cuda, stream_handle, sync_counter
 
 NEG_SLOPE = 0.2
 SOFTMAX_EPS = 1e-16
@@ -456,10 +456,12 @@ class _GraphNormReLUDropout(Function):
             kp = torch.empty_like(x)
             check(LIB.vg_graphnorm_fwd_drop(ptr(x), S, n, c, ptr(w), ptr(b), ptr(ms), float(spec.p), int(spec.seed),
                                             ptr(spec.iter), int(spec.salt) & 0xFFFFFFFF, float(eps), ptr(y), ptr(kp),
-                                            ptr(stats), ptr(ws), stream_handle(x.device)), "vg_graphnorm_fwd_drop")
+                                            ptr(stats), ptr(ws), sync_counter(x.device), stream_handle(x.device)),
+                  "vg_graphnorm_fwd_drop")
         else:
             check(LIB.vg_graphnorm_fwd_seg(ptr(x), S, n, c, ptr(w), ptr(b), ptr(ms), ptr(kp), float(eps), ptr(y),
-                                           ptr(stats), ptr(ws), stream_handle(x.device)), "vg_graphnorm_fwd_seg")
+                                           ptr(stats), ptr(ws), sync_counter(x.device), stream_handle(x.device)),
+                  "vg_graphnorm_fwd_seg")
         ctx.eps, ctx.has_keep, ctx.segments = eps, kp is not None, S
         ctx.params = (weight, bias, mean_scale)
         ctx.save_for_backward(x, weight, bias, mean_scale, kp if kp is not None else x.new_empty(0), stats)
@@ -495,7 +497,8 @@ class _GraphNormReLUDropout(Function):
         ws = torch.empty(int(LIB.vg_graphnorm_seg_ws_floats(S, n, c)), dtype=torch.float32, device=x.device)
         check(LIB.vg_graphnorm_bwd_seg(ptr(x), S, n, c, ptr(w), ptr(b), ptr(ms), ptr(kp), float(ctx.eps), ptr(stats),
                                        ptr(g_y), ptr(g_x), ptr(g_w), ptr(g_b), ptr(g_ms), 1 if direct else 0, None, 0,
-                                       ptr(ws), stream_handle(x.device)), "vg_graphnorm_bwd_seg")
+                                       ptr(ws), sync_counter(x.device), stream_handle(x.device)),
+              "vg_graphnorm_bwd_seg")
         if direct:
             return g_x, None, None, None, None, None, None, None
         return g_x, g_w, g_b, g_ms, None, None, None, None

@@ -176,7 +176,7 @@ int64_t vg_graphnorm_seg_ws_floats(int32_t segments, int32_t rows, int32_t chann
 int vg_graphnorm_fwd_seg(const float* x, int32_t segments, int32_t rows, int32_t channels,
                          const float* weight, const float* bias, const float* mean_scale,
                          const float* keep, float eps, float* y, float* stats, float* workspace,
-                         void* stream);
+                         int32_t* sync, void* stream);
 /* vg_graphnorm_fwd_seg with the dropout drawn in-kernel: keep = Bernoulli(1-p)
  * / (1-p) from a counter-based Philox4x32-10 keyed by seed on the counter
  * (element, salt, *iter) -- *iter is read from device memory, so a hipGraph
@@ -187,7 +187,7 @@ int vg_graphnorm_fwd_drop(const float* x, int32_t segments, int32_t rows, int32_
                           const float* weight, const float* bias, const float* mean_scale,
                           float p_drop, uint64_t seed, const int64_t* iter, uint32_t salt,
                           float eps, float* y, float* keep_out, float* stats, float* workspace,
-                          void* stream);
+                          int32_t* sync, void* stream);
 /* Backward over the segments; parameter gradients sum over segments and are
  * written (accumulate = 0) or added (1); g_w may be NULL (no parameter
  * gradients: g_b, g_ms are then ignored).  inj (nullable) is added to g_x
@@ -197,7 +197,8 @@ int vg_graphnorm_bwd_seg(const float* x, int32_t segments, int32_t rows, int32_t
                          const float* weight, const float* bias, const float* mean_scale,
                          const float* keep, float eps, const float* stats, const float* g_y,
                          float* g_x, float* g_w, float* g_b, float* g_ms, int32_t accumulate,
-                         const float* inj, int64_t inj_offset, float* workspace, void* stream);
+                         const float* inj, int64_t inj_offset, float* workspace, int32_t* sync,
+                         void* stream);
 /* Tangent and second-order terms of y = GraphNormReLUDropout(x) for the
  * gradient penalty's double backward (trainer.py:306-316 with
  * create_graph=True): u_out = J u and, for Q = <g_y, J u>, x_inj = dQ/dx;
@@ -205,7 +206,8 @@ int vg_graphnorm_bwd_seg(const float* x, int32_t segments, int32_t rows, int32_t
 int vg_graphnorm_jvp2(const float* x, int32_t num_nodes, int32_t channels, const float* weight,
                       const float* bias, const float* mean_scale, const float* keep, float eps,
                       const float* stats, const float* u, const float* g_y, float* u_out,
-                      float* x_inj, float* g_w, float* g_ms, float* workspace, void* stream);
+                      float* x_inj, float* g_w, float* g_ms, float* workspace, int32_t* sync,
+                      void* stream);
 
 /* ---- program <-> voxel type-matched mean ("cross-graph pointer") -------- */
 

@@ -15,7 +15,7 @@ from oracle import pyg
 from oracle import reference as R
 from parity_util import grads_close
 from vgan import ops, synth
-from vgan._lib import LIB, check, ptr, stream_handle
+from vgan._lib import LIB, check, ptr, stream_handle, sync_counter
 from vgan.config import Configuration
 from vgan.graph import GraphBatch
 
@@ -153,8 +153,9 @@ def _gn_inputs(n, C, seed=0):
     return x, P, keep
 
 
+@pytest.mark.parametrize("last_block_fold", [True, False])
 @pytest.mark.parametrize("C", [1, 8, 32, 64])
-def test_graphnorm_segments_fwd_bwd_injection(cuda, C):
+def test_graphnorm_segments_fwd_bwd_injection(cuda, C, last_block_fold):
     S, n = 3, 700
     x, P, keep = _gn_inputs(S * n, C)
     gy = torch.randn(S * n, C, dtype=torch.float64)
@@ -174,8 +175,9 @@ def test_graphnorm_segments_fwd_bwd_injection(cuda, C):
     y = torch.empty(S * n, C, device=cuda)
     stats = torch.empty(S * 2 * C, device=cuda)
     ws = torch.empty(int(LIB.vg_graphnorm_seg_ws_floats(S, n, C)), device=cuda)
+    sy = sync_counter(cuda) if last_block_fold else None
     check(LIB.vg_graphnorm_fwd_seg(ptr(xd), S, n, C, ptr(wd), ptr(bd), ptr(sd), ptr(kd), 1e-5, ptr(y), ptr(stats),
-                                   ptr(ws), st), "vg_graphnorm_fwd_seg")
+                                   ptr(ws), sy, st), "vg_graphnorm_fwd_seg")
     assert _close(y, torch.cat(ys))[0]
     inj = torch.randn(n, C, dtype=torch.float64)
     base = {k: torch.randn(C, dtype=torch.float64) for k in P}
@@ -183,7 +185,7 @@ def test_graphnorm_segments_fwd_bwd_injection(cuda, C):
     gx = torch.empty(S * n, C, device=cuda)
     check(LIB.vg_graphnorm_bwd_seg(ptr(xd), S, n, C, ptr(wd), ptr(bd), ptr(sd), ptr(kd), 1e-5, ptr(stats), ptr(gyd),
                                    ptr(gx), ptr(gw), ptr(gb), ptr(gs), 1, ptr(inj.float().to(cuda)), 2 * n * C, ptr(ws),
-                                   st), "vg_graphnorm_bwd_seg")
+                                   sy, st), "vg_graphnorm_bwd_seg")
     exp = torch.cat(gxs)
     exp[2 * n:] += inj
     assert _close(gx, exp)[0]
@@ -191,8 +193,9 @@ def test_graphnorm_segments_fwd_bwd_injection(cuda, C):
         assert _close(got, base[k] + pgs[k])[0], k
 
 
+@pytest.mark.parametrize("last_block_fold", [True, False])
 @pytest.mark.parametrize("C", [1, 8, 32, 64])
-def test_graphnorm_jvp2_matches_autograd(cuda, C):
+def test_graphnorm_jvp2_matches_autograd(cuda, C, last_block_fold):
     n = 900
     x, P, keep = _gn_inputs(n, C, seed=3)
     u = torch.randn(n, C, dtype=torch.float64)
@@ -203,13 +206,17 @@ def test_graphnorm_jvp2_matches_autograd(cuda, C):
     y = torch.empty(n, C, device=cuda)
     stats = torch.empty(2 * C, device=cuda)
     ws = torch.empty(int(LIB.vg_graphnorm_seg_ws_floats(1, n, C)), device=cuda)
+    sy = sync_counter(cuda) if last_block_fold else None
     check(LIB.vg_graphnorm_fwd_seg(ptr(xd), 1, n, C, ptr(wd), ptr(bd), ptr(sd), ptr(kd), 1e-5, ptr(y), ptr(stats),
-                                   ptr(ws), st), "vg_graphnorm_fwd_seg")
+                                   ptr(ws), sy, st), "vg_graphnorm_fwd_seg")
     u_out, x_inj = torch.empty(n, C, device=cuda), torch.empty(n, C, device=cuda)
     gw0, gs0 = torch.randn(C, dtype=torch.float64), torch.randn(C, dtype=torch.float64)
     gw, gs = gw0.float().to(cuda), gs0.float().to(cuda)
     check(LIB.vg_graphnorm_jvp2(ptr(xd), n, C, ptr(wd), ptr(bd), ptr(sd), ptr(kd), 1e-5, ptr(stats), ptr(ud), ptr(gyd),
-                                ptr(u_out), ptr(x_inj), ptr(gw), ptr(gs), ptr(ws), st), "vg_graphnorm_jvp2")
+                                ptr(u_out), ptr(x_inj), ptr(gw), ptr(gs), ptr(ws), sy, st), "vg_graphnorm_jvp2")
+    if sy is not None:
+        from vgan import _lib
+        assert all(int(t.item()) == 0 for t in _lib._SYNC.values())  # counters left at 0
     for got, ref in ((u_out, ju), (x_inj, xinj), (gw, gw0 + pg["w"]), (gs, gs0 + pg["s"])):
         ok, err = _close(got, ref, 2e-5)
         assert ok, err
