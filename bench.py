@@ -217,6 +217,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-stress", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture of the step")
+    ap.add_argument("--profile", action="store_true",
+                    help="for rocprofv3: only warm-up + timed steps (50 ms idle gap before the timed region), "
+                         "no instrumented / stress / CPU passes")
     args = ap.parse_args()
     global GRAPHED
     GRAPHED = not args.eager
@@ -254,6 +257,8 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if args.profile:
+        time.sleep(0.05)  # idle gap that tools/prof_summary.py --after-gap keys on
     t0 = time.perf_counter()
     for s in range(args.steps):
         run_steps(tr, pool, 1, offset=s)
@@ -270,6 +275,14 @@ def main():
     value = args.batch * world * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
     log(f"timed ({'hipGraph' if GRAPHED else 'eager'}): {ms_per_step:.2f} ms/step, {value:.1f} graphs/s")
+
+    if args.profile:
+        if rank == 0:
+            print(json.dumps({"profile": True, "value": round(value, 3), "ms_per_step": round(ms_per_step, 3),
+                              "steps": args.steps}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     # instrumented pass for the dominant kernel's roofline (eager: per-launch
     # HIP events around vg_gat_fwd on its launch stream)

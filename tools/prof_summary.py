@@ -1,21 +1,37 @@
 """Summarise a rocprofv3 --kernel-trace CSV (kernel busy time vs wall span,
-top kernels) so the multi-MB trace itself need not be kept."""
+top kernels) so the multi-MB trace itself need not be kept.
+
+usage: prof_summary.py TRACE.csv [TOP] [--after-gap] [--steps K]
+  --after-gap  keep only the kernels after the largest idle gap in the trace
+               (bench.py --profile sleeps 50 ms before its timed steps)
+  --steps K    also report per-step dispatch counts / busy time
+"""
 import csv
 import sys
 from collections import defaultdict
 
-path = sys.argv[1]
-rows = list(csv.DictReader(open(path)))
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+path = args[0]
+top = int(args[1]) if len(args) > 1 else 40
+after_gap = "--after-gap" in sys.argv
+steps = int(sys.argv[sys.argv.index("--steps") + 1]) if "--steps" in sys.argv else 0
+rows = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in csv.DictReader(open(path))]
+rows.sort()
+if after_gap and len(rows) > 1:
+    gaps = [(rows[i + 1][0] - rows[i][1], i) for i in range(len(rows) - 1)]
+    g, i = max(gaps)
+    print(f"largest gap {g / 1e6:.1f} ms after dispatch {i}; keeping the {len(rows) - i - 1} dispatches after it")
+    rows = rows[i + 1:]
 tot = defaultdict(lambda: [0, 0.0])
-t0, t1, busy = None, None, 0.0
-for r in rows:
-    s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-    name = r["Kernel_Name"]
+busy = 0.0
+for s, e, name in rows:
     tot[name][0] += 1
     tot[name][1] += (e - s) / 1e3
     busy += (e - s) / 1e3
-    t0 = s if t0 is None else min(t0, s)
-    t1 = e if t1 is None else max(t1, e)
+t0, t1 = rows[0][0], max(e for _, e, _ in rows)
 print(f"dispatches {len(rows)}  kernel-busy {busy / 1e3:.2f} ms  span {(t1 - t0) / 1e6:.2f} ms")
-for name, (n, us) in sorted(tot.items(), key=lambda kv: -kv[1][1])[:int(sys.argv[2]) if len(sys.argv) > 2 else 40]:
+if steps:
+    print(f"per step: {len(rows) / steps:.0f} dispatches, {busy / 1e3 / steps:.3f} ms busy, "
+          f"{(t1 - t0) / 1e6 / steps:.3f} ms span")
+for name, (n, us) in sorted(tot.items(), key=lambda kv: -kv[1][1])[:top]:
     print(f"{us / 1e3:9.3f} ms {n:7d} x {us / n:8.2f} us  {name[:110]}")
