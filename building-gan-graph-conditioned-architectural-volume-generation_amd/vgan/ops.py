@@ -525,7 +525,8 @@ def type_mean(local_x: torch.Tensor, local_type: torch.Tensor, voxel_type: torch
         out = torch.empty(nv, f, dtype=torch.float32, device=lx.device)
         col0 = 0
     ws = torch.empty(n_types * (f + 1), dtype=torch.float32, device=lx.device)
-    check(LIB.vg_type_mean(ptr(lx), ptr(local_type.contiguous()), nl, f, ptr(voxel_type.contiguous()), nv,
+    lt, vt = local_type.contiguous(), voxel_type.contiguous()  # bound: the kernel reads them after this line
+    check(LIB.vg_type_mean(ptr(lx), ptr(lt), nl, f, ptr(vt), nv,
                            int(n_types), ptr(out), out.shape[1], int(col0), ptr(ws), stream_handle(lx.device)),
           "vg_type_mean")
     return out
@@ -570,8 +571,9 @@ def far_per_graph(x, label, ptr_, site_area, far_col=9, dy_col=4, dx_col=5, dim_
     gen = torch.empty(g, dtype=torch.float32, device=x.device)
     ref = torch.empty_like(gen)
     lbl = _f32(label.detach())
-    check(LIB.vg_far_per_graph(ptr(_f32(x)), x.shape[1], ptr(lbl), lbl.shape[1], ptr(ptr_.contiguous()), g,
-                               ptr(_f32(site_area)), far_col, dy_col, dx_col, float(dim_scale), void_class,
+    xc, pc, sa = _f32(x), ptr_.contiguous(), _f32(site_area)
+    check(LIB.vg_far_per_graph(ptr(xc), xc.shape[1], ptr(lbl), lbl.shape[1], ptr(pc), g,
+                               ptr(sa), far_col, dy_col, dx_col, float(dim_scale), void_class,
                                ptr(gen), ptr(ref), stream_handle(x.device)), "vg_far_per_graph")
     return gen, ref
 
@@ -583,7 +585,8 @@ def confusion(truth, label, ptr_):
     conf = torch.empty(g, k, k, dtype=torch.int32, device=label.device)
     conf_all = torch.empty(k, k, dtype=torch.int32, device=label.device)
     lbl = _f32(label.detach())
-    check(LIB.vg_confusion(ptr(truth.contiguous()), ptr(lbl), k, ptr(ptr_.contiguous()), g, ptr(conf), ptr(conf_all),
+    tc, pc = truth.contiguous(), ptr_.contiguous()
+    check(LIB.vg_confusion(ptr(tc), ptr(lbl), k, ptr(pc), g, ptr(conf), ptr(conf_all),
                            stream_handle(label.device)), "vg_confusion")
     return conf, conf_all
 
@@ -603,7 +606,7 @@ class _LNAct(Function):
         if g.numel() != c or b.numel() != c:
             raise ValueError("ln_act: inconsistent shapes")
         y = torch.empty_like(x)
-        save = torch.is_grad_enabled() and any(t.requires_grad for t in (x, gamma, beta))
+        save = any(ctx.needs_input_grad[:3])  # (grad mode is off inside Function.forward)
         mean = torch.empty(n, dtype=torch.float32, device=x.device) if save else None
         rstd = torch.empty(n, dtype=torch.float32, device=x.device) if save else None
         check(LIB.vg_ln_act_fwd(ptr(x), n, c, ptr(g), ptr(b), float(eps), float(slope), ptr(y), ptr(mean), ptr(rstd),
