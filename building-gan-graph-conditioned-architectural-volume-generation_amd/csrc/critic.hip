@@ -5,13 +5,16 @@
 //                  gradient-penalty interpolate (trainer.py:298-301, 319-320):
 //                  X[c*N + n] = [ matched_voxel_x[n] | label_c[n] ],
 //                  label_mix = eps*real + (1-eps)*soft  (rounded as torch does:
-//                  two products then one add, no fused multiply-add).
+//                  two products then one add, no fused multiply-add); with
+//                  copies = 4 the rows [3N,4N) are zeroed (the engine's
+//                  tangent rows, whose label columns vg_gp_head fills).
 // vg_gp_head       from g = dD(mix)/dlabel [N,K] and the stacked scores:
 //                  gp = lambda * mean_n (|g_n| - 1)^2            (trainer.py:313-316)
 //                  loss = mean(D(fake)) - mean(D(real)) + gp       (trainer.py:326-328)
 //                  u0 = dgp/dg = (2 lambda / N) (|g_n| - 1)/|g_n| g_n   (the seed of the
 //                  engine's tangent pass; 0 where |g_n| = 0, as torch's norm backward).
-//                  One 1024-thread block, fixed reduction order.
+//                  Row-parallel; per-block sums folded in block order by the
+//                  last block to finish (deterministic).
 #include "common.h"
 
 namespace {
@@ -19,9 +22,9 @@ namespace {
 __global__ void k_critic_input(const float* __restrict__ mvx, int N, int F,
                                const float* __restrict__ real, const float* __restrict__ hard,
                                const float* __restrict__ soft, const float* __restrict__ eps,
-                               int K, float* __restrict__ X) {
+                               int K, int copies, float* __restrict__ X) {
   const int W = F + K;
-  const long long total = 3LL * N * W;
+  const long long total = (long long)copies * N * W;
   for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
        t += (long long)gridDim.x * blockDim.x) {
     const long long r = t / W;
@@ -29,7 +32,9 @@ __global__ void k_critic_input(const float* __restrict__ mvx, int N, int F,
     const int cp = static_cast<int>(r / N);
     const long long n = r - (long long)cp * N;
     float v;
-    if (c < F) {
+    if (cp == 3) {
+      v = 0.f;
+    } else if (c < F) {
       v = mvx[n * F + c];
     } else {
       const long long e = n * K + (c - F);
@@ -44,23 +49,32 @@ __global__ void k_critic_input(const float* __restrict__ mvx, int N, int F,
   }
 }
 
+// One row per thread over ceil(N/1024) blocks; per-block partial sums of
+// (gp, real, fake) go to `part`; the last block folds them in block order.
 __global__ void __launch_bounds__(1024) k_gp_head(const float* __restrict__ g, int N, int K,
                                                   const float* __restrict__ scores, float lambda,
-                                                  float* __restrict__ u0, float* __restrict__ out) {
+                                                  float* __restrict__ u0, int ldu,
+                                                  float* __restrict__ part, int* counter,
+                                                  float* __restrict__ out) {
   const int t = threadIdx.x;
   const float coef = 2.f * lambda / static_cast<float>(N);
   float gp = 0.f, sr = 0.f, sf = 0.f;
-  for (int n = t; n < N; n += 1024) {
+  const int n = blockIdx.x * 1024 + t;
+  if (n < N) {
     const float* gr = g + (size_t)n * K;
+    float v[16];
     float ss = 0.f;
-    for (int k = 0; k < K; ++k) ss = fmaf(gr[k], gr[k], ss);
+    for (int k = 0; k < K; ++k) {
+      v[k & 15] = gr[k];
+      ss = fmaf(gr[k], gr[k], ss);
+    }
     const float nrm = sqrtf(ss);
     const float d = nrm - 1.f;
-    gp = fmaf(d, d, gp);
+    gp = d * d;
     const float f = nrm > 0.f ? coef * d / nrm : 0.f;
-    for (int k = 0; k < K; ++k) u0[(size_t)n * K + k] = f * gr[k];
-    sr += scores[n];
-    sf += scores[N + n];
+    for (int k = 0; k < K; ++k) u0[(size_t)n * ldu + k] = f * (K <= 16 ? v[k] : gr[k]);
+    sr = scores[n];
+    sf = scores[N + n];
   }
   __shared__ float red[3][1024];
   red[0][t] = gp;
@@ -72,10 +86,18 @@ __global__ void __launch_bounds__(1024) k_gp_head(const float* __restrict__ g, i
       for (int q = 0; q < 3; ++q) red[q][t] += red[q][t + s];
     __syncthreads();
   }
-  if (t == 0) {
+  if (t == 0)
+    for (int q = 0; q < 3; ++q) part[blockIdx.x * 3 + q] = red[q][0];
+  if (vg_last_block(counter) && t == 0) {
+    float a = 0.f, b = 0.f, c = 0.f;
+    for (int k = 0; k < (int)gridDim.x; ++k) {
+      a += part[k * 3];
+      b += part[k * 3 + 1];
+      c += part[k * 3 + 2];
+    }
     const float fn = static_cast<float>(N);
-    const float gpv = red[0][0] / fn * lambda;
-    out[0] = (red[2][0] / fn - red[1][0] / fn) + gpv;
+    const float gpv = a / fn * lambda;
+    out[0] = (c / fn - b / fn) + gpv;
     out[1] = gpv;
   }
 }
@@ -84,22 +106,28 @@ __global__ void __launch_bounds__(1024) k_gp_head(const float* __restrict__ g, i
 
 extern "C" int vg_critic_input(const float* mvx, int32_t N, int32_t F, const float* real,
                                const float* hard, const float* soft, const float* eps, int32_t K,
-                               float* X, void* stream) {
-  if (N <= 0 || F < 0 || K <= 0 || (F > 0 && !mvx) || !real || !hard || !soft || !eps || !X)
+                               int32_t copies, float* X, void* stream) {
+  if (N <= 0 || F < 0 || K <= 0 || (F > 0 && !mvx) || !real || !hard || !soft || !eps || !X ||
+      (copies != 3 && copies != 4))
     return VG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  int blocks = vg_blocks(3LL * N * (F + K), 256);
+  int blocks = vg_blocks((long long)copies * N * (F + K), 256);
   if (blocks > 4096) blocks = 4096;
-  k_critic_input<<<blocks, 256, 0, s>>>(mvx, N, F, real, hard, soft, eps, K, X);
+  k_critic_input<<<blocks, 256, 0, s>>>(mvx, N, F, real, hard, soft, eps, K, copies, X);
   VG_CHECK_LAUNCH();
   return 0;
 }
 
+extern "C" int64_t vg_gp_head_ws_floats(int32_t N) { return 3 * (int64_t)vg_blocks(N, 1024); }
+
 extern "C" int vg_gp_head(const float* g, int32_t N, int32_t K, const float* scores, float lambda,
-                          float* u0, float* out, void* stream) {
-  if (N <= 0 || K <= 0 || !g || !scores || !u0 || !out) return VG_EINVAL;
+                          float* u0, int32_t ldu, float* out, float* workspace, int32_t* sync,
+                          void* stream) {
+  if (N <= 0 || K <= 0 || ldu < K || !g || !scores || !u0 || !out || !workspace || !sync)
+    return VG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  k_gp_head<<<1, 1024, 0, s>>>(g, N, K, scores, lambda, u0, out);
+  k_gp_head<<<vg_blocks(N, 1024), 1024, 0, s>>>(g, N, K, scores, lambda, u0, ldu, workspace, sync,
+                                                out);
   VG_CHECK_LAUNCH();
   return 0;
 }

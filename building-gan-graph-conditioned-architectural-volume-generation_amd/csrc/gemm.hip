@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int l
 __global__ void __launch_bounds__(256) k_gemm_tn(const float* __restrict__ A, int lda,
                                                  const float* __restrict__ B, int ldb, int N,
                                                  int M, int K, int rows, float* __restrict__ part,
-                                                 float* __restrict__ pdb) {
+                                                 float* __restrict__ pdb, int db_rows) {
   __shared__ float As[2][TK][TM + 1];  // As[n][m]
   __shared__ float Bs[2][TK][TN + 1];  // Bs[n][k]
   constexpr int PER = (TK * TM) / 256;
@@ -143,7 +143,7 @@ __global__ void __launch_bounds__(256) k_gemm_tn(const float* __restrict__ A, in
       const int e = t + 256 * q;
       As[buf][e / TM][e % TM] = ra[q];
       Bs[buf][e / TM][e % TM] = rb[q];
-      if (do_db) dbs += ra[q];  // column (t & 63) of this thread, rows e / TM
+      if (do_db && n1 + e / TM < db_rows) dbs += ra[q];  // column (t & 63), rows e / TM
     }
     __syncthreads();
     if (n1 + TK < ne) load(n1 + TK);
@@ -233,10 +233,11 @@ extern "C" int64_t vg_gemm_tn_ws_floats(int32_t N, int32_t M, int32_t K) {
   return chunks * ((int64_t)M * K + M);
 }
 
-extern "C" int vg_gemm_tn(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N,
-                          int32_t M, int32_t K, float* C, int32_t ldc, float* db, int32_t accumulate,
-                          float* workspace, void* stream) {
-  if (N < 0 || M <= 0 || K <= 0 || ldc < K || !A || !B || !C || !workspace) return VG_EINVAL;
+static int gemm_tn(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N, int32_t M,
+                   int32_t K, float* C, int32_t ldc, float* db, int32_t db_rows,
+                   int32_t accumulate, float* workspace, void* stream) {
+  if (N < 0 || M <= 0 || K <= 0 || ldc < K || !A || !B || !C || !workspace || db_rows < 0)
+    return VG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (N == 0) {
     if (accumulate) return 0;
@@ -250,10 +251,23 @@ extern "C" int vg_gemm_tn(const float* A, int32_t lda, const float* B, int32_t l
   float* part = workspace;
   float* pdb = workspace + (size_t)chunks * M * K;
   dim3 grid((M + TM - 1) / TM, (K + TN - 1) / TN, chunks);
-  k_gemm_tn<<<grid, 256, 0, s>>>(A, lda, B, ldb, N, M, K, rows, part, db ? pdb : nullptr);
+  k_gemm_tn<<<grid, 256, 0, s>>>(A, lda, B, ldb, N, M, K, rows, part, db ? pdb : nullptr,
+                                 db_rows < N ? db_rows : N);
   const long long W = (long long)M * K;
   k_fold_rows<<<(int)((W + 63) / 64), 1024, 0, s>>>(part, chunks, W, K, ldc, accumulate, C);
   if (db) k_fold_rows<<<(M + 63) / 64, 1024, 0, s>>>(pdb, chunks, M, M, M, accumulate, db);
   VG_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int vg_gemm_tn(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N,
+                          int32_t M, int32_t K, float* C, int32_t ldc, float* db, int32_t accumulate,
+                          float* workspace, void* stream) {
+  return gemm_tn(A, lda, B, ldb, N, M, K, C, ldc, db, N, accumulate, workspace, stream);
+}
+
+extern "C" int vg_gemm_tn_ex(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N,
+                             int32_t M, int32_t K, float* C, int32_t ldc, float* db,
+                             int32_t db_rows, int32_t accumulate, float* workspace, void* stream) {
+  return gemm_tn(A, lda, B, ldb, N, M, K, C, ldc, db, db_rows, accumulate, workspace, stream);
 }

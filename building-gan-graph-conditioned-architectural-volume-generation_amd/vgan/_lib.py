@@ -48,6 +48,8 @@ SIGNATURES = {
     "vg_gemm_tn_ws_floats": (_c_i64, [_c_i32, _c_i32, _c_i32]),
     "vg_gemm_tn": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_i32, _c_p,
                                   _c_p]),
+    "vg_gemm_tn_ex": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_i32,
+                                     _c_i32, _c_p, _c_p]),
     "vg_gat_bwd_ex": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p,
                                      _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_i32, _c_p,
                                      _c_p]),
@@ -67,8 +69,9 @@ SIGNATURES = {
     "vg_ln_act_bwd_ws_floats": (_c_i64, [_c_i32]),
     "vg_ln_act_bwd": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
                                      _c_i32, _c_p, _c_p]),
-    "vg_critic_input": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_p]),
-    "vg_gp_head": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_f32, _c_p, _c_p, _c_p]),
+    "vg_critic_input": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p]),
+    "vg_gp_head_ws_floats": (_c_i64, [_c_i32]),
+    "vg_gp_head": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_f32, _c_p, _c_i32, _c_p, _c_p, _c_p, _c_p]),
     "vg_adam_dev": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_i64, ctypes.c_double, ctypes.c_double, _c_f32, _c_f32,
                                    _c_p, _c_p, _c_p]),
     "vg_adam": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_i64, _c_f32, _c_f32, _c_f32, _c_f32, _c_f32, _c_f32,
@@ -104,9 +107,17 @@ def stream_handle(device: torch.device) -> ctypes.c_void_p:
 _SYNC = {}
 
 
+# measured slower at batch 32 (16.1 vs 18.2 ms/step: one contended counter for
+# ~640 blocks), so off unless VGAN_LAST_BLOCK_FOLD=1
+_LAST_BLOCK = os.environ.get("VGAN_LAST_BLOCK_FOLD", "0") == "1"
+
+
 def sync_counter(device: torch.device):
     """Persistent zeroed int32 device counter per (device, current stream) for
-    the kernels' last-block fold (left at 0 by every launch)."""
+    the kernels' last-block fold (left at 0 by every launch); None (separate
+    finalize launches) when VGAN_LAST_BLOCK_FOLD=0."""
+    if not _LAST_BLOCK:
+        return None
     key = (torch.device(device), torch.cuda.current_stream(device).cuda_stream)
     t = _SYNC.get(key)
     if t is None:

@@ -96,14 +96,23 @@ class CriticEngine:
         check(LIB.vg_gemm(A, lda, B, ldb, bt, bias, act, aux, ldaux, C, ldc, n, m, k, st), "vg_gemm")
 
     @staticmethod
-    def _gemm_tn(st, dev, A, lda, B, ldb, n, m, k, C, ldc, db=None):
+    def _gemm_tn(st, dev, A, lda, B, ldb, n, m, k, C, ldc, db=None, db_rows=None):
         ws = _f(max(1, int(LIB.vg_gemm_tn_ws_floats(n, m, k))), dev=dev)
-        check(LIB.vg_gemm_tn(A, lda, B, ldb, n, m, k, C, ldc, db, 1, ptr(ws), st), "vg_gemm_tn")
+        check(LIB.vg_gemm_tn_ex(A, lda, B, ldb, n, m, k, C, ldc, db, n if db_rows is None else db_rows, 1, ptr(ws),
+                                st), "vg_gemm_tn_ex")
 
     # ------------------------------------------------------------ engine
     def loss_and_grad(self, local_graph, voxel_graph, label_hard, label_soft, rng) -> torch.Tensor:
         """d_loss (device scalar) of trainer.py:318-332; D's parameter gradients
-        are added to their .grad."""
+        are added to their .grad.
+
+        Buffers hold 4N rows: rows [0, 3N) the real / fake / mix copies of pass
+        A (activations) and pass D (adjoints); rows [3N, 4N) of an activation
+        buffer take pass C's tangent of that activation, rows [3N, 4N) of an
+        adjoint buffer pass B's adjoint.  Every linear layer's weight gradient
+        -- first order (pass D) plus second order (d_B^T u_C) -- is then ONE
+        split-K product over the 4N rows; only the first 3N rows feed the bias
+        gradient."""
         D = self.D
         prep = vdata.prepared(local_graph, voxel_graph, self.n_classes)
         mvx, real = prep.matched_voxel_x, prep.onehot_f
@@ -117,7 +126,7 @@ class CriticEngine:
         dev = mvx.device
         st = stream_handle(dev)
         sy = sync_counter(dev)
-        R, W0 = 3 * n, F + K
+        R, W0, X4 = 3 * n, F + K, 4 * n
         csr = prep.csr
         csr3 = csr.stacked(3)
         E = csr.num_edges
@@ -126,16 +135,21 @@ class CriticEngine:
                 p.grad = torch.zeros_like(p)
         keeps, eps = self._keeps(rng, n, dev, D.training)
         eps = eps.reshape(n).contiguous()
+        nb, nd, nm = len(self.blocks), len(self.dec), len(self.mlp)
+        mrow, trow = 2 * n, 3 * n  # first row of the mix copy / of the tangent (or pass-B) rows
+
+        def rows(t: torch.Tensor, r0: int, width: int):
+            return _off(t, r0 * width)
 
         # ---------------------------------------------------------- pass A
-        X0 = _f(R, W0, dev=dev)
-        check(LIB.vg_critic_input(ptr(mvx), n, F, ptr(real), ptr(hard), ptr(soft), ptr(eps), K, ptr(X0), st),
+        X0 = _f(X4, W0, dev=dev)
+        check(LIB.vg_critic_input(ptr(mvx), n, F, ptr(real), ptr(hard), ptr(soft), ptr(eps), K, 4, ptr(X0), st),
               "vg_critic_input")
         mlp_out = []
         x, xw = X0, W0
         for lin in self.mlp:
             o = lin.out_features
-            y = _f(R, o, dev=dev)
+            y = _f(X4, o, dev=dev)
             self._gemm(st, ptr(x), xw, ptr(lin.weight), xw, 1, ptr(y), o, R, o, xw, ptr(lin.bias), ACT_RELU)
             mlp_out.append(y)
             x, xw = y, o
@@ -149,9 +163,9 @@ class CriticEngine:
             check(LIB.vg_gat_fwd(ptr(csr3.row_ptr), ptr(csr3.col), R, c, ptr(H), ptr(conv.att_src),
                                  ptr(conv.att_dst), ptr(conv.bias), float(conv.negative_slope), ptr(O), ptr(alpha),
                                  ptr(a_s), ptr(a_d), st), "vg_gat_fwd")
-            Y, stats = _f(R, c, dev=dev), _f(3 * 2 * c, dev=dev)
+            Y, stats = _f(X4, c, dev=dev), _f(3 * 2 * c, dev=dev)
             ws = _f(int(LIB.vg_graphnorm_seg_ws_floats(3, n, c)), dev=dev)
-            if keep is not None and not isinstance(keep, torch.Tensor):  # DropSpec
+            if keep is not None and not isinstance(keep, torch.Tensor):  # DropSpec: drawn in-kernel
                 spec, keep = keep, _f(R, c, dev=dev)
                 check(LIB.vg_graphnorm_fwd_drop(ptr(O), 3, n, c, ptr(norm.weight), ptr(norm.bias),
                                                 ptr(norm.mean_scale), float(spec.p), int(spec.seed), ptr(spec.iter),
@@ -166,150 +180,137 @@ class CriticEngine:
         dec_out = []
         for i, lin in enumerate(self.dec):
             o = lin.out_features
-            z = _f(R, o, dev=dev)
-            act = ACT_NONE if i == len(self.dec) - 1 else ACT_RELU
-            self._gemm(st, ptr(x), xw, ptr(lin.weight), xw, 1, ptr(z), o, R, o, xw, ptr(lin.bias), act)
+            last = i == nd - 1
+            z = _f(R if last else X4, o, dev=dev)
+            self._gemm(st, ptr(x), xw, ptr(lin.weight), xw, 1, ptr(z), o, R, o, xw, ptr(lin.bias),
+                       ACT_NONE if last else ACT_RELU)
             dec_out.append(z)
             x, xw = z, o
         scores = dec_out[-1]
         if scores.shape[1] != 1:
             raise ValueError("the critic must output one score per node")
 
-        mrow = 2 * n  # first row of the mix copy
+        # adjoint buffers of pass D (rows [0,3N)) whose rows [3N,4N) pass B fills
+        def make_seeds():  # [-1/N real | +1/N fake | 0 mix | 1 pass-B seed]
+            s_ = torch.zeros(X4, 1, dtype=torch.float32, device=dev)
+            s_[:n] = -1.0 / n
+            s_[n:2 * n] = 1.0 / n
+            s_[3 * n:] = 1.0
+            return s_
 
-        def mix(t: torch.Tensor, width: int):
-            return _off(t, mrow * width)
+        seeds = self._const(("seeds4", n), make_seeds)
+        adj_dec = [_f(X4, l.out_features, dev=dev) for l in self.dec[:-1]] + [seeds]
+        adj_H = [_f(X4, B["c"], dev=dev) for B in blk]
+        adj_mlp = [_f(X4, l.out_features, dev=dev) for l in self.mlp]
 
         # ---------------------------------------------------------- pass B
-        ones = self._const(("ones", n), lambda: torch.ones(n, 1, dtype=torch.float32, device=dev))
-        nd = len(self.dec)
-        p_dec: List[Optional[torch.Tensor]] = [None] * nd
-        adj, aw = ones, 1
         for i in range(nd - 1, 0, -1):
             Wt = self.dec[i].weight
-            m = Wt.shape[1]
-            a = _f(n, m, dev=dev)
-            self._gemm(st, ptr(adj), aw, ptr(Wt), m, 0, ptr(a), m, n, m, aw, None, ACT_MASK, mix(dec_out[i - 1], m), m)
-            p_dec[i - 1] = a
-            adj, aw = a, m
+            aw, m = Wt.shape
+            self._gemm(st, rows(adj_dec[i], trow, aw), aw, ptr(Wt), m, 0, rows(adj_dec[i - 1], trow, m), m, n, m, aw,
+                       None, ACT_MASK, rows(dec_out[i - 1], mrow, m), m)
         W = self.dec[0].weight
         dY = _f(n, W.shape[1], dev=dev)
-        self._gemm(st, ptr(adj), aw, ptr(W), W.shape[1], 0, ptr(dY), W.shape[1], n, W.shape[1], aw)
-        nb = len(self.blocks)
-        dY_b, dO_b, dH_b = [None] * nb, [None] * nb, [None] * nb
-        p_mlp: List[Optional[torch.Tensor]] = [None] * len(self.mlp)
+        self._gemm(st, rows(adj_dec[0], trow, W.shape[0]), W.shape[0], ptr(W), W.shape[1], 0, ptr(dY), W.shape[1], n,
+                   W.shape[1], W.shape[0])
+        dY_b, dO_b = [None] * nb, [None] * nb
         for b in range(nb - 1, -1, -1):
             (conv, norm), B = self.blocks[b], blk[b]
             c = B["c"]
             dY_b[b] = dY
             dO = _f(n, c, dev=dev)
             ws = _f(int(LIB.vg_graphnorm_seg_ws_floats(1, n, c)), dev=dev)
-            check(LIB.vg_graphnorm_bwd_seg(mix(B["O"], c), 1, n, c, ptr(norm.weight), ptr(norm.bias),
-                                           ptr(norm.mean_scale), mix(B["keep"], c) if B["keep"] is not None else None,
+            check(LIB.vg_graphnorm_bwd_seg(rows(B["O"], mrow, c), 1, n, c, ptr(norm.weight), ptr(norm.bias),
+                                           ptr(norm.mean_scale),
+                                           rows(B["keep"], mrow, c) if B["keep"] is not None else None,
                                            float(norm.eps), _off(B["stats"], 2 * 2 * c), ptr(dY), ptr(dO), None, None,
                                            None, 0, None, 0, ptr(ws), sy, st), "vg_graphnorm_bwd_seg")
-            dH = _f(n, c, dev=dev)
+            dH = rows(adj_H[b], trow, c)
             ws = _f(int(LIB.vg_gat_bwd_ws_floats(n, E, c)), dev=dev)
             check(LIB.vg_gat_bwd_ex(ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot),
-                                    ptr(csr.csc_dst), n, E, c, mix(B["H"], c), ptr(conv.att_src), ptr(conv.att_dst),
-                                    _off(B["a_s"], mrow), _off(B["a_d"], mrow), _off(B["alpha"], 2 * E), ptr(dO),
-                                    float(conv.negative_slope), ptr(dH), None, None, None, 0, None, 0, ptr(ws), st),
-                  "vg_gat_bwd_ex")
-            dO_b[b], dH_b[b] = dO, dH
+                                    ptr(csr.csc_dst), n, E, c, rows(B["H"], mrow, c), ptr(conv.att_src),
+                                    ptr(conv.att_dst), _off(B["a_s"], mrow), _off(B["a_d"], mrow),
+                                    _off(B["alpha"], 2 * E), ptr(dO), float(conv.negative_slope), dH, None, None, None,
+                                    0, None, 0, ptr(ws), st), "vg_gat_bwd_ex")
+            dO_b[b] = dO
             cin = B["xw"]
-            dX = _f(n, cin, dev=dev)
             if b > 0:
-                self._gemm(st, ptr(dH), c, ptr(conv.lin.weight), cin, 0, ptr(dX), cin, n, cin, c)
+                dX = _f(n, cin, dev=dev)
+                self._gemm(st, dH, c, ptr(conv.lin.weight), cin, 0, ptr(dX), cin, n, cin, c)
                 dY = dX
             else:
-                self._gemm(st, ptr(dH), c, ptr(conv.lin.weight), cin, 0, ptr(dX), cin, n, cin, c, None, ACT_MASK,
-                           mix(mlp_out[-1], cin), cin)
-                p_mlp[-1] = dX
-        for i in range(len(self.mlp) - 1, 0, -1):
+                self._gemm(st, dH, c, ptr(conv.lin.weight), cin, 0, rows(adj_mlp[-1], trow, cin), cin, n, cin, c,
+                           None, ACT_MASK, rows(mlp_out[-1], mrow, cin), cin)
+        for i in range(nm - 1, 0, -1):
             Wt = self.mlp[i].weight
-            m = Wt.shape[1]
-            a = _f(n, m, dev=dev)
-            self._gemm(st, ptr(p_mlp[i]), Wt.shape[0], ptr(Wt), m, 0, ptr(a), m, n, m, Wt.shape[0], None, ACT_MASK,
-                       mix(mlp_out[i - 1], m), m)
-            p_mlp[i - 1] = a
+            o, m = Wt.shape
+            self._gemm(st, rows(adj_mlp[i], trow, o), o, ptr(Wt), m, 0, rows(adj_mlp[i - 1], trow, m), m, n, m, o,
+                       None, ACT_MASK, rows(mlp_out[i - 1], mrow, m), m)
         W = self.mlp[0].weight
         hd = W.shape[0]
         g = _f(n, K, dev=dev)
-        self._gemm(st, ptr(p_mlp[0]), hd, _off(W, F), W0, 0, ptr(g), K, n, K, hd)
-        u0, out = _f(n, K, dev=dev), _f(2, dev=dev)
-        check(LIB.vg_gp_head(ptr(g), n, K, ptr(scores), self.lam, ptr(u0), ptr(out), st), "vg_gp_head")
+        self._gemm(st, rows(adj_mlp[0], trow, hd), hd, _off(W, F), W0, 0, ptr(g), K, n, K, hd)
+        out = _f(2, dev=dev)
+        gws = _f(int(LIB.vg_gp_head_ws_floats(n)), dev=dev)
+        gcnt = self._const(("gp_counter", dev), lambda: torch.zeros(1, dtype=torch.int32, device=dev))
+        u0 = _off(X0, trow * W0 + F)  # dGP/dg written into the label columns of X0's tangent rows
+        check(LIB.vg_gp_head(ptr(g), n, K, ptr(scores), self.lam, u0, W0, ptr(out), ptr(gws), ptr(gcnt), st),
+              "vg_gp_head")
 
         # ---------------------------------------------------------- pass C
-        uY = _f(n, hd, dev=dev)
-        self._gemm(st, ptr(u0), K, _off(W, F), W0, 1, ptr(uY), hd, n, hd, K, None, ACT_MASK, mix(mlp_out[0], hd), hd)
-        self._gemm_tn(st, dev, ptr(p_mlp[0]), hd, ptr(u0), K, n, hd, K, _off(W.grad, F), W0)
+        self._gemm(st, u0, W0, _off(W, F), W0, 1, rows(mlp_out[0], trow, hd), hd, n, hd, K, None, ACT_MASK,
+                   rows(mlp_out[0], mrow, hd), hd)
         uw = hd
-        for i in range(1, len(self.mlp)):
+        for i in range(1, nm):
             lin = self.mlp[i]
             o = lin.out_features
-            un = _f(n, o, dev=dev)
-            self._gemm(st, ptr(uY), uw, ptr(lin.weight), uw, 1, ptr(un), o, n, o, uw, None, ACT_MASK,
-                       mix(mlp_out[i], o), o)
-            self._gemm_tn(st, dev, ptr(p_mlp[i]), o, ptr(uY), uw, n, o, uw, ptr(lin.weight.grad), uw)
-            uY, uw = un, o
+            self._gemm(st, rows(mlp_out[i - 1], trow, uw), uw, ptr(lin.weight), uw, 1, rows(mlp_out[i], trow, o), o, n,
+                       o, uw, None, ACT_MASK, rows(mlp_out[i], mrow, o), o)
+            uw = o
+        u_in = rows(mlp_out[-1], trow, uw)
         hinj_b, oinj_b = [None] * nb, [None] * nb
         for b in range(nb):
             (conv, norm), B = self.blocks[b], blk[b]
             c, cin = B["c"], B["xw"]
             uH = _f(n, c, dev=dev)
-            self._gemm(st, ptr(uY), cin, ptr(conv.lin.weight), cin, 1, ptr(uH), c, n, c, cin)
-            self._gemm_tn(st, dev, ptr(dH_b[b]), c, ptr(uY), cin, n, c, cin, ptr(conv.lin.weight.grad), cin)
+            self._gemm(st, u_in, cin, ptr(conv.lin.weight), cin, 1, ptr(uH), c, n, c, cin)
             uO, hinj = _f(n, c, dev=dev), _f(n, c, dev=dev)
             ws = _f(int(LIB.vg_gat_jvp2_ws_floats(n, E, c)), dev=dev)
             check(LIB.vg_gat_jvp2(ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot),
-                                  ptr(csr.csc_dst), n, E, c, mix(B["H"], c), ptr(uH), ptr(dO_b[b]), ptr(conv.att_src),
-                                  ptr(conv.att_dst), _off(B["a_s"], mrow), _off(B["a_d"], mrow),
+                                  ptr(csr.csc_dst), n, E, c, rows(B["H"], mrow, c), ptr(uH), ptr(dO_b[b]),
+                                  ptr(conv.att_src), ptr(conv.att_dst), _off(B["a_s"], mrow), _off(B["a_d"], mrow),
                                   _off(B["alpha"], 2 * E), float(conv.negative_slope), ptr(uO), ptr(hinj),
                                   ptr(conv.att_src.grad), ptr(conv.att_dst.grad), ptr(ws), st), "vg_gat_jvp2")
-            uYn, oinj = _f(n, c, dev=dev), _f(n, c, dev=dev)
+            oinj = _f(n, c, dev=dev)
             ws = _f(int(LIB.vg_graphnorm_seg_ws_floats(1, n, c)), dev=dev)
-            check(LIB.vg_graphnorm_jvp2(mix(B["O"], c), n, c, ptr(norm.weight), ptr(norm.bias), ptr(norm.mean_scale),
-                                        mix(B["keep"], c) if B["keep"] is not None else None, float(norm.eps),
-                                        _off(B["stats"], 2 * 2 * c), ptr(uO), ptr(dY_b[b]), ptr(uYn), ptr(oinj),
-                                        ptr(norm.weight.grad), ptr(norm.mean_scale.grad), ptr(ws), sy, st),
+            check(LIB.vg_graphnorm_jvp2(rows(B["O"], mrow, c), n, c, ptr(norm.weight), ptr(norm.bias),
+                                        ptr(norm.mean_scale),
+                                        rows(B["keep"], mrow, c) if B["keep"] is not None else None, float(norm.eps),
+                                        _off(B["stats"], 2 * 2 * c), ptr(uO), ptr(dY_b[b]), rows(B["Y"], trow, c),
+                                        ptr(oinj), ptr(norm.weight.grad), ptr(norm.mean_scale.grad), ptr(ws), sy, st),
                   "vg_graphnorm_jvp2")
             hinj_b[b], oinj_b[b] = hinj, oinj
-            uY, uw = uYn, c
-        for i, lin in enumerate(self.dec):
+            u_in, uw = rows(B["Y"], trow, c), c
+        for i, lin in enumerate(self.dec[:-1]):
             o = lin.out_features
-            if i < nd - 1:
-                un = _f(n, o, dev=dev)
-                self._gemm(st, ptr(uY), uw, ptr(lin.weight), uw, 1, ptr(un), o, n, o, uw, None, ACT_MASK,
-                           mix(dec_out[i], o), o)
-                self._gemm_tn(st, dev, ptr(p_dec[i]), o, ptr(uY), uw, n, o, uw, ptr(lin.weight.grad), uw)
-                uY, uw = un, o
-            else:
-                self._gemm_tn(st, dev, ptr(ones), 1, ptr(uY), uw, n, 1, uw, ptr(lin.weight.grad), uw)
+            self._gemm(st, u_in, uw, ptr(lin.weight), uw, 1, rows(dec_out[i], trow, o), o, n, o, uw, None, ACT_MASK,
+                       rows(dec_out[i], mrow, o), o)
+            u_in, uw = rows(dec_out[i], trow, o), o
 
         # ---------------------------------------------------------- pass D
-        def make_seeds():
-            s = torch.zeros(R, 1, dtype=torch.float32, device=dev)
-            s[:n] = -1.0 / n
-            s[n:2 * n] = 1.0 / n
-            return s
-
-        seeds = self._const(("seeds", n), make_seeds)
+        # weight gradients over 4N rows: [pass-D adjoint ; pass-B adjoint]^T [activation ; tangent]
         dec_in = [blk[-1]["Y"] if blk else mlp_out[-1]] + dec_out[:-1]
-        dec_in_w = [self.dec[0].in_features] + [l.out_features for l in self.dec[:-1]]
-        adj, aw = seeds, 1
         for i in range(nd - 1, -1, -1):
             lin = self.dec[i]
-            self._gemm_tn(st, dev, ptr(adj), aw, ptr(dec_in[i]), dec_in_w[i], R, aw, dec_in_w[i], ptr(lin.weight.grad),
-                          dec_in_w[i], ptr(lin.bias.grad))
-            m = dec_in_w[i]
-            a = _f(R, m, dev=dev)
+            aw, m = lin.weight.shape
+            self._gemm_tn(st, dev, ptr(adj_dec[i]), aw, ptr(dec_in[i]), m, X4, aw, m, ptr(lin.weight.grad), m,
+                          ptr(lin.bias.grad), R)
             if i > 0:
-                self._gemm(st, ptr(adj), aw, ptr(lin.weight), m, 0, ptr(a), m, R, m, aw, None, ACT_MASK,
-                           ptr(dec_out[i - 1]), m)
+                self._gemm(st, ptr(adj_dec[i]), aw, ptr(lin.weight), m, 0, ptr(adj_dec[i - 1]), m, R, m, aw, None,
+                           ACT_MASK, ptr(dec_out[i - 1]), m)
             else:
-                self._gemm(st, ptr(adj), aw, ptr(lin.weight), m, 0, ptr(a), m, R, m, aw)
-            adj, aw = a, m
-        dY = adj
+                dY = _f(R, m, dev=dev)
+                self._gemm(st, ptr(adj_dec[0]), aw, ptr(lin.weight), m, 0, ptr(dY), m, R, m, aw)
         for b in range(nb - 1, -1, -1):
             (conv, norm), B = self.blocks[b], blk[b]
             c, cin = B["c"], B["xw"]
@@ -320,31 +321,27 @@ class CriticEngine:
                                            ptr(dY), ptr(dO), ptr(norm.weight.grad), ptr(norm.bias.grad),
                                            ptr(norm.mean_scale.grad), 1, ptr(oinj_b[b]), mrow * c, ptr(ws), sy, st),
                   "vg_graphnorm_bwd_seg")
-            dH = _f(R, c, dev=dev)
             ws = _f(int(LIB.vg_gat_bwd_ws_floats(R, 3 * E, c)), dev=dev)
             check(LIB.vg_gat_bwd_ex(ptr(csr3.row_ptr), ptr(csr3.col), ptr(csr3.csc_ptr), ptr(csr3.csc_slot),
                                     ptr(csr3.csc_dst), R, 3 * E, c, ptr(B["H"]), ptr(conv.att_src), ptr(conv.att_dst),
                                     ptr(B["a_s"]), ptr(B["a_d"]), ptr(B["alpha"]), ptr(dO), float(conv.negative_slope),
-                                    ptr(dH), ptr(conv.att_src.grad), ptr(conv.att_dst.grad), ptr(conv.bias.grad), 1,
-                                    ptr(hinj_b[b]), mrow, ptr(ws), st), "vg_gat_bwd_ex")
-            self._gemm_tn(st, dev, ptr(dH), c, ptr(B["X"]), cin, R, c, cin, ptr(conv.lin.weight.grad), cin)
-            dX = _f(R, cin, dev=dev)
+                                    ptr(adj_H[b]), ptr(conv.att_src.grad), ptr(conv.att_dst.grad),
+                                    ptr(conv.bias.grad), 1, ptr(hinj_b[b]), mrow, ptr(ws), st), "vg_gat_bwd_ex")
+            self._gemm_tn(st, dev, ptr(adj_H[b]), c, ptr(B["X"]), cin, X4, c, cin, ptr(conv.lin.weight.grad), cin)
             if b > 0:
-                self._gemm(st, ptr(dH), c, ptr(conv.lin.weight), cin, 0, ptr(dX), cin, R, cin, c)
+                dY = _f(R, cin, dev=dev)
+                self._gemm(st, ptr(adj_H[b]), c, ptr(conv.lin.weight), cin, 0, ptr(dY), cin, R, cin, c)
             else:
-                self._gemm(st, ptr(dH), c, ptr(conv.lin.weight), cin, 0, ptr(dX), cin, R, cin, c, None, ACT_MASK,
-                           ptr(mlp_out[-1]), cin)
-            dY = dX
-        pm = dY
-        for i in range(len(self.mlp) - 1, -1, -1):
+                self._gemm(st, ptr(adj_H[b]), c, ptr(conv.lin.weight), cin, 0, ptr(adj_mlp[-1]), cin, R, cin, c,
+                           None, ACT_MASK, ptr(mlp_out[-1]), cin)
+        for i in range(nm - 1, -1, -1):
             lin = self.mlp[i]
-            o, m = lin.out_features, lin.in_features
+            o, m = lin.weight.shape
             xin = X0 if i == 0 else mlp_out[i - 1]
-            self._gemm_tn(st, dev, ptr(pm), o, ptr(xin), m, R, o, m, ptr(lin.weight.grad), m, ptr(lin.bias.grad))
+            self._gemm_tn(st, dev, ptr(adj_mlp[i]), o, ptr(xin), m, X4, o, m, ptr(lin.weight.grad), m,
+                          ptr(lin.bias.grad), R)
             if i > 0:
-                a = _f(R, m, dev=dev)
-                self._gemm(st, ptr(pm), o, ptr(lin.weight), m, 0, ptr(a), m, R, m, o, None, ACT_MASK,
-                           ptr(mlp_out[i - 1]), m)
-                pm = a
+                self._gemm(st, ptr(adj_mlp[i]), o, ptr(lin.weight), m, 0, ptr(adj_mlp[i - 1]), m, R, m, o, None,
+                           ACT_MASK, ptr(mlp_out[i - 1]), m)
         self.last_gp = out[1]
         return out[0]

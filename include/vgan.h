@@ -111,16 +111,21 @@ int vg_gat_jvp2(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_p
 
 /* ---- WGAN-GP critic engine helpers (trainer.py:291-332) ------------------ */
 
-/* X [3N, F+K]: rows c*N+n = [mvx[n] | label_c[n]] for c = real, fake (hard),
- * mix = eps[n]*real + (1-eps[n])*soft (two products then one add, as torch). */
+/* X [copies*N, F+K]: rows c*N+n = [mvx[n] | label_c[n]] for c = real, fake
+ * (hard), mix = eps[n]*real + (1-eps[n])*soft (two products then one add, as
+ * torch); copies = 4 also zeroes rows [3N, 4N) (tangent rows). */
 int vg_critic_input(const float* mvx, int32_t N, int32_t F, const float* real, const float* hard,
-                    const float* soft, const float* eps, int32_t K, float* X, void* stream);
+                    const float* soft, const float* eps, int32_t K, int32_t copies, float* X,
+                    void* stream);
 
 /* From g [N,K] = dD(mix)/dlabel and the stacked scores [3N]:
  * out[1] = gp = lambda mean_n (|g_n|-1)^2, out[0] = mean(fake) - mean(real) + gp,
- * u0 [N,K] = dgp/dg.  One workgroup, deterministic. */
+ * u0 [N,K] (row stride ldu) = dgp/dg.  Deterministic (per-block sums folded in
+ * order by the last block).  workspace: vg_gp_head_ws_floats(N); sync: a
+ * caller-owned int32 device counter, 0 on entry (left at 0). */
+int64_t vg_gp_head_ws_floats(int32_t N);
 int vg_gp_head(const float* g, int32_t N, int32_t K, const float* scores, float lambda, float* u0,
-               float* out, void* stream);
+               int32_t ldu, float* out, float* workspace, int32_t* sync, void* stream);
 
 /* Differentiable sparse primitives (their adjoints are each other), used to
  * build the twice-differentiable path the WGAN-GP needs (trainer.py:306-312,
@@ -274,6 +279,13 @@ int64_t vg_gemm_tn_ws_floats(int32_t N, int32_t M, int32_t K);
 int vg_gemm_tn(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N, int32_t M,
                int32_t K, float* C, int32_t ldc, float* db, int32_t accumulate,
                float* workspace, void* stream);
+
+/* vg_gemm_tn with db summing only the first db_rows rows of A (the critic
+ * engine stacks first- and second-order weight-gradient terms as extra rows
+ * of one product; only the first-order rows carry a bias gradient). */
+int vg_gemm_tn_ex(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N, int32_t M,
+                  int32_t K, float* C, int32_t ldc, float* db, int32_t db_rows,
+                  int32_t accumulate, float* workspace, void* stream);
 
 /* ---- LayerNorm + LeakyReLU ------------------------------------------------ */
 

@@ -229,9 +229,10 @@ def test_graphnorm_jvp2_matches_autograd(cuda, C, last_block_fold):
 
 
 # -------------------------------------------------------------- helpers
-def test_critic_input_and_gp_head(cuda):
+@pytest.mark.parametrize("n", [333, 5000])
+def test_critic_input_and_gp_head(cuda, n):
     g = torch.Generator().manual_seed(5)
-    n, F, K = 333, 29, 7
+    F, K = 29, 7
     mvx = torch.rand(n, F, generator=g)
     real = torch.nn.functional.one_hot(torch.randint(0, K, (n,), generator=g), K).float()
     hard = torch.nn.functional.one_hot(torch.randint(0, K, (n,), generator=g), K).float()
@@ -240,7 +241,7 @@ def test_critic_input_and_gp_head(cuda):
     X = torch.empty(3 * n, F + K, device=cuda)
     st = stream_handle(cuda)
     dv = [t.to(cuda).contiguous() for t in (mvx, real, hard, soft, eps)]
-    check(LIB.vg_critic_input(ptr(dv[0]), n, F, ptr(dv[1]), ptr(dv[2]), ptr(dv[3]), ptr(dv[4]), K, ptr(X), st),
+    check(LIB.vg_critic_input(ptr(dv[0]), n, F, ptr(dv[1]), ptr(dv[2]), ptr(dv[3]), ptr(dv[4]), K, 3, ptr(X), st),
           "vg_critic_input")
     mix = eps * real + (1 - eps) * soft  # the reference's rounding (trainer.py:298-301)
     exp = torch.cat([torch.cat([mvx, real], 1), torch.cat([mvx, hard], 1), torch.cat([mvx, mix], 1)])
@@ -250,7 +251,9 @@ def test_critic_input_and_gp_head(cuda):
     sc = torch.randn(3 * n, dtype=torch.float64)
     u0, out = torch.empty(n, K, device=cuda), torch.empty(2, device=cuda)
     ggd, scd = gg.float().to(cuda), sc.float().to(cuda)
-    check(LIB.vg_gp_head(ptr(ggd), n, K, ptr(scd), 10.0, ptr(u0), ptr(out), st),
+    gws = torch.empty(int(LIB.vg_gp_head_ws_floats(n)), device=cuda)
+    cnt = torch.zeros(1, dtype=torch.int32, device=cuda)
+    check(LIB.vg_gp_head(ptr(ggd), n, K, ptr(scd), 10.0, ptr(u0), K, ptr(out), ptr(gws), ptr(cnt), st),
           "vg_gp_head")
     leaf = gg.clone().requires_grad_(True)
     gp = ((leaf.norm(dim=1) - 1) ** 2).mean() * 10.0
@@ -260,6 +263,7 @@ def test_critic_input_and_gp_head(cuda):
     assert abs(out[0].item() - loss.item()) <= 1e-5 * max(1.0, abs(loss.item()))
     gref[3] = 0.0  # torch's norm backward at 0 is 0 as well (subgradient)
     assert _close(u0, gref)[0]
+    assert int(cnt.item()) == 0  # counter left at 0
 
 
 # --------------------------------------------------------------- engine
