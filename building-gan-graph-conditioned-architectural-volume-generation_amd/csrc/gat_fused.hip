@@ -599,14 +599,36 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src_ep(
 // out[w] = sum_b part[b][w] for w < W (w < split -> out_a, else out_b); one
 // 1024-thread block per 64 columns, 16 waves stride over the partial rows,
 // LDS fold in a fixed order (deterministic).
+// blockIdx.y selects the partial set: 0 -> (part, rows, W, split, out_a, out_b),
+// 1 -> (part2, rows2, W2 -> out2).
 __global__ void __launch_bounds__(1024) k_fold_cols(const float* __restrict__ part, int rows, int W,
                                                     int split, int acc, float* __restrict__ out_a,
-                                                    float* __restrict__ out_b) {
+                                                    float* __restrict__ out_b,
+                                                    const float* __restrict__ part2 = nullptr,
+                                                    int rows2 = 0, int W2 = 0,
+                                                    float* __restrict__ out2 = nullptr) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (blockIdx.y == 1) {
+    part = part2;
+    rows = rows2;
+    W = W2;
+    split = W2;
+    out_a = out_b = out2;
+  }
   const int w = blockIdx.x * 64 + lane;
   float s = 0.f;
-  if (w < W)
-    for (int r = wave; r < rows; r += 16) s += part[(size_t)r * W + w];
+  if (w < W) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;  // loads in flight, fixed combine order
+    int r = wave;
+    for (; r + 48 < rows; r += 64) {
+      a0 += part[(size_t)r * W + w];
+      a1 += part[(size_t)(r + 16) * W + w];
+      a2 += part[(size_t)(r + 32) * W + w];
+      a3 += part[(size_t)(r + 48) * W + w];
+    }
+    for (; r < rows; r += 16) a0 += part[(size_t)r * W + w];
+    s = (a0 + a1) + (a2 + a3);
+  }
   __shared__ float red[16][64];
   red[wave][lane] = s;
   __syncthreads();
@@ -709,10 +731,9 @@ extern "C" int vg_gat_bwd_ex(const int32_t* row_ptr, const int32_t* col, const i
   }
   if (pgrads) {
     // fold: part1 rows -> [g_bias | g_att_dst], part2 rows -> g_att_src
-    k_fold_cols<<<vg_blocks(2 * C, 64), 1024, 0, s>>>(part1, grid1, 2 * C, C, accumulate, g_bias,
-                                                      g_att_dst);
-    k_fold_cols<<<vg_blocks(C, 64), 1024, 0, s>>>(part2, grid2, C, C, accumulate, g_att_src,
-                                                  g_att_src);
+    k_fold_cols<<<dim3(vg_blocks(2 * C, 64), 2), 1024, 0, s>>>(part1, grid1, 2 * C, C, accumulate,
+                                                               g_bias, g_att_dst, part2, grid2, C,
+                                                               g_att_src);
   }
   VG_CHECK_LAUNCH();
   return 0;

@@ -213,8 +213,18 @@ __global__ void __launch_bounds__(1024) k_fold_add2(const float* __restrict__ pa
   const float* part = blockIdx.y == 0 ? part_a : part_b;
   const int rows = blockIdx.y == 0 ? rows_a : rows_b;
   float s = 0.f;
-  if (c < C)
-    for (int r = wave; r < rows; r += 16) s += part[(size_t)r * C + c];
+  if (c < C) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;  // loads in flight, fixed combine order
+    int r = wave;
+    for (; r + 48 < rows; r += 64) {
+      a0 += part[(size_t)r * C + c];
+      a1 += part[(size_t)(r + 16) * C + c];
+      a2 += part[(size_t)(r + 32) * C + c];
+      a3 += part[(size_t)(r + 48) * C + c];
+    }
+    for (; r < rows; r += 16) a0 += part[(size_t)r * C + c];
+    s = (a0 + a1) + (a2 + a3);
+  }
   __shared__ float red[16][64];
   red[wave][lane] = s;
   __syncthreads();

@@ -179,8 +179,19 @@ __global__ void __launch_bounds__(1024) k_fold_rows(const float* __restrict__ pa
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long long w = blockIdx.x * 64LL + lane;
   float s = 0.f;
-  if (w < W)
-    for (int r = wave; r < rows; r += 16) s += part[(size_t)r * W + w];
+  if (w < W) {
+    // 4 independent accumulators (loads in flight), combined in a fixed order
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int r = wave;
+    for (; r + 48 < rows; r += 64) {
+      a0 += part[(size_t)r * W + w];
+      a1 += part[(size_t)(r + 16) * W + w];
+      a2 += part[(size_t)(r + 32) * W + w];
+      a3 += part[(size_t)(r + 48) * W + w];
+    }
+    for (; r < rows; r += 16) a0 += part[(size_t)r * W + w];
+    s = (a0 + a1) + (a2 + a3);
+  }
   __shared__ float red[16][64];
   red[wave][lane] = s;
   __syncthreads();
@@ -217,10 +228,13 @@ extern "C" int vg_gemm(const float* A, int32_t lda, const float* B, int32_t ldb,
   return 0;
 }
 
-// rows per split-K chunk: aim at ~768 workgroups in total, multiples of TK
+// rows per split-K chunk: aim at ~768 workgroups in total but at most
+// 256 chunks per output tile (the fold reads chunks x M x K partials; more chunks
+// made the fold, not the product, the long pole), multiples of TK
 static inline int tn_rows(int N, int M, int K) {
   const int tiles = ((M + TM - 1) / TM) * ((K + TN - 1) / TN);
   int target = 768 / tiles;
+  if (target > 256) target = 256;
   if (target < 1) target = 1;
   int rows = (N + target - 1) / target;
   rows = ((rows + TK - 1) / TK) * TK;

@@ -30,7 +30,8 @@
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kChunks = 64;  // row chunks per column slab
+constexpr int kChunks = 256;  // max row chunks per column slab (~64 rows each)
+constexpr int kFinalThreads = 1024;  // finalize: 16 waves fold the chunk partials
 
 struct Welford {
   float n, mean, m2;
@@ -81,6 +82,7 @@ __global__ void __launch_bounds__(kBlock) k_stats_partial(const float* __restric
   part += (size_t)blockIdx.z * gridDim.x * C * 3;
   Welford w = {0.f, 0.f, 0.f};
   if (col_ok) {
+#pragma unroll 4
     for (int r = r0 + rsub; r < r1; r += rstep) {
       const float v = x[(size_t)r * C + c];
       w.n += 1.f;
@@ -122,24 +124,26 @@ __device__ void stats_final_body(const float* __restrict__ part, int chunks, int
   const int c = slab * 64 + lane;
   part += (size_t)seg * chunks * C * 3;  // segment
   stats += (size_t)seg * 2 * C;
+  const int NW = blockDim.x >> 6;
   Welford acc = {0.f, 0.f, 0.f};
   if (c < C)
-    for (int k = wave; k < chunks; k += 4) {
+    for (int k = wave; k < chunks; k += NW) {
       const float* p = part + ((size_t)k * C + c) * 3;
       acc = merge(acc, Welford{p[0], p[1], p[2]});
     }
-  __shared__ Welford sw[4][64];
+  __shared__ Welford sw[16][64];
   sw[wave][lane] = acc;
   __syncthreads();
   if (wave == 0 && c < C) {
-    Welford r = merge(merge(sw[0][lane], sw[1][lane]), merge(sw[2][lane], sw[3][lane]));
+    Welford r = sw[0][lane];
+    for (int k = 1; k < NW; ++k) r = merge(r, sw[k][lane]);
     stats[c] = r.mean;
     stats[C + c] = sqrtf(fmaxf(r.m2 / r.n, 0.f));
   }
   __syncthreads();
 }
 
-__global__ void __launch_bounds__(256) k_stats_final(const float* __restrict__ part, int chunks,
+__global__ void __launch_bounds__(kFinalThreads) k_stats_final(const float* __restrict__ part, int chunks,
                                                      int C, float* __restrict__ stats) {
   stats_final_body(part, chunks, C, stats, blockIdx.x, blockIdx.y);
 }
@@ -205,6 +209,7 @@ __global__ void __launch_bounds__(kBlock) k_gn_bwd_partial(
   float sa = 0.f, sb = 0.f;
   if (c < C) {
     const float mu = stats[c], s = stats[C + c] + eps, wc = w[c], bc = b[c], msc = ms[c];
+#pragma unroll 4
     for (int r = r0 + rsub; r < r1; r += rstep) {
       const size_t t = (size_t)r * C + c;
       const float xh = (x[t] - mu * msc) / s;
@@ -248,13 +253,14 @@ __device__ void bwd_final_body(const float* __restrict__ part, int chunks, int C
                                float* __restrict__ g_ms, int accumulate, int slab) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = slab * 64 + lane;
-  __shared__ float red[4][64][2];
+  const int NW = blockDim.x >> 6;
+  __shared__ float red[16][64][2];
   float tw = 0.f, tb = 0.f, tm = 0.f;
   for (int sg = 0; sg < S; ++sg) {
     const float* pp = part + (size_t)sg * chunks * C * 2;
     float a = 0.f, bb = 0.f;
     if (c < C)
-      for (int k = wave; k < chunks; k += 4) {
+      for (int k = wave; k < chunks; k += NW) {
         a += pp[((size_t)k * C + c) * 2];
         bb += pp[((size_t)k * C + c) * 2 + 1];
       }
@@ -262,8 +268,12 @@ __device__ void bwd_final_body(const float* __restrict__ part, int chunks, int C
     red[wave][lane][1] = bb;
     __syncthreads();
     if (wave == 0 && c < C) {
-      a = (red[0][lane][0] + red[1][lane][0]) + (red[2][lane][0] + red[3][lane][0]);
-      bb = (red[0][lane][1] + red[1][lane][1]) + (red[2][lane][1] + red[3][lane][1]);
+      a = red[0][lane][0];
+      bb = red[0][lane][1];
+      for (int k = 1; k < NW; ++k) {
+        a += red[k][lane][0];
+        bb += red[k][lane][1];
+      }
       const float* st = stats + (size_t)sg * 2 * C;
       sums[(size_t)sg * 2 * C + c] = a;
       sums[(size_t)sg * 2 * C + C + c] = bb;
@@ -281,7 +291,7 @@ __device__ void bwd_final_body(const float* __restrict__ part, int chunks, int C
   __syncthreads();
 }
 
-__global__ void __launch_bounds__(256) k_gn_bwd_final(
+__global__ void __launch_bounds__(kFinalThreads) k_gn_bwd_final(
     const float* __restrict__ part, int chunks, int C, int S, const float* __restrict__ w,
     const float* __restrict__ ms, float eps, const float* __restrict__ stats,
     float* __restrict__ sums, float* __restrict__ g_w, float* __restrict__ g_b,
@@ -349,6 +359,7 @@ __global__ void __launch_bounds__(kBlock) k_gn_jvp2_partial(
   float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   if (c < C) {
     const float mu = stats[c], s = stats[C + c] + eps, wc = w[c], bc = b[c], msc = ms[c];
+#pragma unroll 4
     for (int r = r0 + rsub; r < r1; r += rstep) {
       const size_t t = (size_t)r * C + c;
       const float xv = x[t], uv = u[t];
@@ -390,20 +401,24 @@ __device__ void jvp2_final_body(const float* __restrict__ part, int chunks, int 
                                 float* __restrict__ g_ms, int slab) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = slab * 64 + lane;
+  const int NW = blockDim.x >> 6;
   float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   if (c < C)
-    for (int k = wave; k < chunks; k += 4) {
+    for (int k = wave; k < chunks; k += NW) {
       const float* pp = part + ((size_t)k * C + c) * 5;
 #pragma unroll
       for (int q = 0; q < 5; ++q) v[q] += pp[q];
     }
-  __shared__ float red[4][64][5];
+  __shared__ float red[16][64][5];
 #pragma unroll
   for (int q = 0; q < 5; ++q) red[wave][lane][q] = v[q];
   __syncthreads();
   if (wave == 0 && c < C) {
 #pragma unroll
-    for (int q = 0; q < 5; ++q) v[q] = (red[0][lane][q] + red[1][lane][q]) + (red[2][lane][q] + red[3][lane][q]);
+    for (int q = 0; q < 5; ++q) {
+      v[q] = red[0][lane][q];
+      for (int k = 1; k < NW; ++k) v[q] += red[k][lane][q];
+    }
     const float inv_n = 1.f / static_cast<float>(N);
     const float mu = stats[c], sd = stats[C + c], d = sd + eps, msc = ms[c], wc = w[c];
     const float mup = v[0] * inv_n, M = v[1] * inv_n, Sp = v[2];
@@ -422,7 +437,7 @@ __device__ void jvp2_final_body(const float* __restrict__ part, int chunks, int 
   __syncthreads();
 }
 
-__global__ void __launch_bounds__(256) k_gn_jvp2_final(
+__global__ void __launch_bounds__(kFinalThreads) k_gn_jvp2_final(
     const float* __restrict__ part, int chunks, int N, int C, const float* __restrict__ w,
     const float* __restrict__ ms, float eps, const float* __restrict__ stats,
     float* __restrict__ sums, float* __restrict__ g_w, float* __restrict__ g_ms) {
@@ -463,7 +478,10 @@ __global__ void k_gn_jvp2_apply(const float* __restrict__ x, const float* __rest
 }
 }  // namespace
 
-static inline int chunks_for(int N) { return N < kChunks * 16 ? (N + 15) / 16 : kChunks; }
+static inline int chunks_for(int N) {
+  const int c = (N + 63) / 64;
+  return c < 1 ? 1 : (c > kChunks ? kChunks : c);
+}
 
 static inline int apply_blocks(long long total) {
   int blocks = vg_blocks(total, 256);
@@ -490,7 +508,7 @@ static int gn_fwd(const float* x, int32_t S, int32_t N, int32_t C, const float* 
   const int chunks = chunks_for(N);
   dim3 grid(chunks, (C + 63) / 64, S);
   k_stats_partial<<<grid, kBlock, 0, s>>>(x, N, C, ws, stats, sync);
-  if (!sync) k_stats_final<<<dim3(vg_blocks(C, 64), S), 256, 0, s>>>(ws, chunks, C, stats);
+  if (!sync) k_stats_final<<<dim3(vg_blocks(C, 64), S), kFinalThreads, 0, s>>>(ws, chunks, C, stats);
   const long long total = (long long)S * N * C;
   k_gn_apply<<<apply_blocks(total), 256, 0, s>>>(x, total, C, (long long)N * C, weight, bias,
                                                  mean_scale, keep, eps, stats, y, p_drop,
@@ -545,7 +563,7 @@ extern "C" int vg_graphnorm_bwd_seg(const float* x, int32_t S, int32_t N, int32_
   k_gn_bwd_partial<<<grid, kBlock, 0, s>>>(x, g_y, N, C, weight, bias, mean_scale, keep, eps,
                                            stats, part, sums, g_w, g_b, g_ms, accumulate, sync);
   if (!sync)
-    k_gn_bwd_final<<<vg_blocks(C, 64), 256, 0, s>>>(part, chunks, C, S, weight, mean_scale, eps,
+    k_gn_bwd_final<<<vg_blocks(C, 64), kFinalThreads, 0, s>>>(part, chunks, C, S, weight, mean_scale, eps,
                                                     stats, sums, g_w, g_b, g_ms, accumulate);
   const long long total = (long long)S * N * C;
   k_gn_bwd_apply<<<apply_blocks(total), 256, 0, s>>>(x, g_y, total, N, C, weight, bias,
@@ -580,7 +598,7 @@ extern "C" int vg_graphnorm_jvp2(const float* x, int32_t N, int32_t C, const flo
   k_gn_jvp2_partial<<<grid, kBlock, 0, s>>>(x, u, g_y, N, C, weight, bias, mean_scale, keep, eps,
                                             stats, part, sums, g_w, g_ms, sync);
   if (!sync)
-    k_gn_jvp2_final<<<vg_blocks(C, 64), 256, 0, s>>>(part, chunks, N, C, weight, mean_scale, eps,
+    k_gn_jvp2_final<<<vg_blocks(C, 64), kFinalThreads, 0, s>>>(part, chunks, N, C, weight, mean_scale, eps,
                                                      stats, sums, g_w, g_ms);
   const long long total = (long long)N * C;
   k_gn_jvp2_apply<<<apply_blocks(total), 256, 0, s>>>(x, u, g_y, total, N, C, weight, bias,

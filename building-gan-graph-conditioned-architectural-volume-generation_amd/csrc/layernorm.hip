@@ -116,8 +116,18 @@ __global__ void __launch_bounds__(1024) k_ln_fold(const float* __restrict__ part
   const int w = blockIdx.x * 64 + lane;
   const int W = 2 * C;
   float s = 0.f;
-  if (w < W)
-    for (int r = wave; r < rows; r += 16) s += part[(size_t)r * W + w];
+  if (w < W) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;  // loads in flight, fixed combine order
+    int r = wave;
+    for (; r + 48 < rows; r += 64) {
+      a0 += part[(size_t)r * W + w];
+      a1 += part[(size_t)(r + 16) * W + w];
+      a2 += part[(size_t)(r + 32) * W + w];
+      a3 += part[(size_t)(r + 48) * W + w];
+    }
+    for (; r < rows; r += 16) a0 += part[(size_t)r * W + w];
+    s = (a0 + a1) + (a2 + a3);
+  }
   __shared__ float red[16][64];
   red[wave][lane] = s;
   __syncthreads();
