@@ -45,51 +45,91 @@ def log(msg: str) -> None:
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-def gat_fwd_bytes(n: int, e: int, c: int) -> int:
-    """Algorithmic bytes of one vg_gat_fwd: read h [N,C], write out [N,C],
-    read row_ptr [N+1] and col [E'], write alpha [E'] and a_src/a_dst [N],
-    read att_src/att_dst/bias [C]."""
-    return 4 * (2 * n * c + (n + 1) + 2 * e + 2 * n + 3 * c)
+def agg_bytes(n: int, e: int, c: int) -> int:
+    """Algorithmic (compulsory) bytes of one vg_gat_aggregate_fwd launch: read
+    h [N,C], write out [N,C], read row_ptr [N+1] and col [E'], read a_src /
+    a_dst [N], read bias [C], write alpha [E'] (plus alpha)."""
+    return 4 * (2 * n * c + (n + 1) + 2 * e + 2 * n + c)
 
 
-class GatTimer:
-    """HIP-event timing of every vg_gat_fwd launch (on its launch stream)."""
+def step_aggregate_calls(tr, csr):
+    """(CSR, channels) of every vg_gat_aggregate_fwd launch in one full step:
+    the stacked critic-label G forward (N_CRITIC copies), N_CRITIC critic
+    iterations (D over the real / fake / mix stack), the generator
+    iteration's G forward and its D forward."""
+    n_critic = tr.configuration.N_CRITIC
+    gw = tr.generator.encoder.widths[1:]
+    dw = tr.discriminator.encoder.widths[1:]
+    calls = []
+    if tr._stacked_labels():
+        calls += [(csr.stacked(n_critic), c) for c in gw]
+    calls += [(csr.stacked(3), c) for _ in range(n_critic) for c in dw]
+    calls += [(csr, c) for c in gw] + [(csr, c) for c in dw]
+    return calls
 
-    def __init__(self):
-        self.records = []
 
-    def install(self):
-        from vgan import ops
+def aggregate_roofline(tr, csr, device, reps: int = 20):
+    """Average device duration of the scatter kernel (vg_gat_aggregate_fwd)
+    over the step's own mix of launches: one launch per call of a step, on the
+    step's CSRs and channel counts, captured in a hipGraph and replayed
+    ``reps`` times between HIP events on the replay stream (back-to-back
+    launches, as inside the step's own graphs)."""
+    from vgan._lib import LIB, check, ptr, stream_handle
 
-        orig = ops._GATConv.forward
-        timer = self
+    calls = step_aggregate_calls(tr, csr)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(1234)
+    bufs = {}
+    for c_csr, c in calls:
+        key = (c_csr.num_nodes, c)
+        if key not in bufs:
+            n = c_csr.num_nodes
+            bufs[key] = [torch.randn(n, c, device=device, generator=gen),
+                         0.3 * torch.randn(n, device=device, generator=gen),
+                         0.3 * torch.randn(n, device=device, generator=gen),
+                         torch.randn(c, device=device, generator=gen),
+                         torch.empty(n, c, device=device),
+                         torch.empty(c_csr.num_edges, device=device)]
 
-        def timed_forward(ctx, h, att_src, att_dst, bias, csr, slope):
-            stream = torch.cuda.current_stream(h.device)
-            start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            start.record(stream)
-            out = orig(ctx, h, att_src, att_dst, bias, csr, slope)
-            end.record(stream)
-            timer.records.append((start, end, gat_fwd_bytes(csr.num_nodes, csr.num_edges, h.shape[1])))
-            return out
+    def launch_all():
+        st = stream_handle(device)
+        for c_csr, c in calls:
+            h, a_s, a_d, b, out, alpha = bufs[(c_csr.num_nodes, c)]
+            check(LIB.vg_gat_aggregate_fwd(ptr(c_csr.row_ptr), ptr(c_csr.col), c_csr.num_nodes, c, ptr(h), ptr(a_s),
+                                           ptr(a_d), ptr(b), 0.2, ptr(out), ptr(alpha), st), "vg_gat_aggregate_fwd")
 
-        self._orig = orig
-        ops._GATConv.forward = staticmethod(timed_forward)
+    side = torch.cuda.Stream(device)
+    side.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(side):
+        launch_all()
+    torch.cuda.current_stream(device).wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        launch_all()
+    g.replay()
+    torch.cuda.synchronize()
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    st.record()
+    for _ in range(reps):
+        g.replay()
+    en.record()
+    torch.cuda.synchronize()
+    total_ms = st.elapsed_time(en)
+    launches = reps * len(calls)
+    nbytes = reps * sum(agg_bytes(c_csr.num_nodes, c_csr.num_edges, c) for c_csr, c in calls)
+    return {"launches": launches, "launches_per_step": len(calls), "avg_us": total_ms * 1e3 / launches,
+            "avg_bytes": nbytes / launches, "achieved_gbs": nbytes / (total_ms * 1e-3) / 1e9}
 
-    def uninstall(self):
-        from vgan import ops
 
-        ops._GATConv.forward = staticmethod(self._orig)
-
-    def summary(self):
-        torch.cuda.synchronize()
-        ms = [s.elapsed_time(e) for s, e, _ in self.records]
-        nbytes = [b for _, _, b in self.records]
-        n = len(ms)
-        avg_ms = sum(ms) / n
-        avg_bytes = sum(nbytes) / n
-        achieved = avg_bytes / (avg_ms * 1e-3) / 1e9
-        return {"launches": n, "avg_us": avg_ms * 1e3, "avg_bytes": avg_bytes, "achieved_gbs": achieved}
+def load_pmc_traffic():
+    """Per-launch HBM-side bytes of the scatter kernel from the committed
+    rocprofv3 PMC summary (tools/pmc_roofline.sh), or None."""
+    path = os.path.join(ROOT, "profiles", "r01_pmc_aggregate.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    return d.get("traffic_bytes_per_launch"), "profiles/r01_pmc_aggregate.json"
 
 
 def make_pool(cfg, rank: int, world: int, pool: int, batch: int, device):
@@ -129,7 +169,9 @@ def run_steps(tr, pool, k: int, offset: int = 0):
 
 
 def stress_roofline(device, channels=(128, 64, 1), reps: int = 20):
+    """vg_gat_aggregate_fwd on config #4 (8 x 50k-node buildings), cold MALL."""
     from vgan import ops
+    from vgan._lib import LIB, check, ptr, stream_handle
     from vgan.synth import make_stress_building
     from vgan.graph import GraphBatch
 
@@ -141,22 +183,28 @@ def stress_roofline(device, channels=(128, 64, 1), reps: int = 20):
     res = {}
     for c in channels:
         h = torch.randn(n, c, device=device)
-        att_s, att_d = torch.randn(c, device=device) * 0.1, torch.randn(c, device=device) * 0.1
+        a_s, a_d = 0.3 * torch.randn(n, device=device), 0.3 * torch.randn(n, device=device)
         bias = torch.randn(c, device=device)
-        with torch.no_grad():
-            for _ in range(3):
-                ops.gat_conv(csr, h, att_s, att_d, bias)
-            times = []
-            for _ in range(reps):
-                scratch.fill_(1.0)
-                st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                st.record()
-                ops.gat_conv(csr, h, att_s, att_d, bias)
-                en.record()
-                torch.cuda.synchronize()
-                times.append(st.elapsed_time(en))
+        out, alpha = torch.empty(n, c, device=device), torch.empty(e, device=device)
+
+        def run():
+            check(LIB.vg_gat_aggregate_fwd(ptr(csr.row_ptr), ptr(csr.col), n, c, ptr(h), ptr(a_s), ptr(a_d),
+                                           ptr(bias), 0.2, ptr(out), ptr(alpha), stream_handle(device)),
+                  "vg_gat_aggregate_fwd")
+
+        for _ in range(3):
+            run()
+        times = []
+        for _ in range(reps):
+            scratch.fill_(1.0)
+            st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            st.record()
+            run()
+            en.record()
+            torch.cuda.synchronize()
+            times.append(st.elapsed_time(en))
         avg = sum(times) / len(times)
-        b = gat_fwd_bytes(n, e, c)
+        b = agg_bytes(n, e, c)
         res[c] = {"avg_us": avg * 1e3, "bytes": b, "achieved_gbs": b / (avg * 1e-3) / 1e9}
     del scratch
     return {"nodes": n, "edges": e, "per_channels": res}
@@ -220,6 +268,8 @@ def main():
     ap.add_argument("--profile", action="store_true",
                     help="for rocprofv3: only warm-up + timed steps (50 ms idle gap before the timed region), "
                          "no instrumented / stress / CPU passes")
+    ap.add_argument("--roofline-only", action="store_true",
+                    help="only the scatter-kernel roofline replays (--steps of them), for rocprofv3 --pmc passes")
     args = ap.parse_args()
     global GRAPHED
     GRAPHED = not args.eager
@@ -246,6 +296,13 @@ def main():
     pool = make_pool(cfg, rank, world, args.pool, args.batch, device)
     tr = build_trainer(cfg)
     n_nodes = sum(v.num_nodes for _, v in pool) / len(pool)
+    if args.roofline_only:  # for rocprofv3 --pmc passes: only the scatter-kernel roofline replays
+        from vgan import data as vdata
+
+        csr0 = vdata.prepared(pool[0][0], pool[0][1], cfg.NUM_CLASSES).csr
+        kern = aggregate_roofline(tr, csr0, device, reps=args.steps)
+        print(json.dumps({"roofline_only": True, **{k: round(v, 3) for k, v in kern.items()}}), flush=True)
+        return
 
     # warm-up (also builds every batch's CSR / type-mean once, as the first step of a batch would)
     for (loc, vox) in pool:
@@ -284,16 +341,15 @@ def main():
             dist.destroy_process_group()
         return
 
-    # instrumented pass for the dominant kernel's roofline (eager: per-launch
-    # HIP events around vg_gat_fwd on its launch stream)
-    timer = GatTimer()
-    timer.install()
-    GRAPHED, was = False, GRAPHED
-    run_steps(tr, pool, args.steps)
-    GRAPHED = was
-    timer.uninstall()
-    kern = timer.summary()
-    log(f"vg_gat_fwd: {kern['launches']} launches, avg {kern['avg_us']:.2f} us, {kern['achieved_gbs']:.1f} GB/s")
+    # the dominant message-passing kernel's roofline: the step's own mix of
+    # vg_gat_aggregate_fwd launches, graph-replayed between HIP events
+    from vgan import data as vdata
+
+    csr0 = vdata.prepared(pool[0][0], pool[0][1], cfg.NUM_CLASSES).csr
+    kern = aggregate_roofline(tr, csr0, device, reps=max(args.steps, 10))
+    log(f"vg_gat_aggregate_fwd: {kern['launches']} launches, avg {kern['avg_us']:.2f} us, "
+        f"{kern['achieved_gbs']:.1f} GB/s")
+    traffic, traffic_src = load_pmc_traffic()
 
     result = None
     if rank == 0:
@@ -327,16 +383,20 @@ def main():
                               "N_CRITIC critic-engine graphs, one generator-iteration graph") if GRAPHED else "eager",
             },
             "roofline": {
-                "kernel": "vg_gat_fwd (fused GAT edge softmax + CSR gather-sum)",
+                "kernel": "vg_gat_aggregate_fwd (GAT edge softmax + CSR gather-sum + bias: the scatter kernel)",
                 "bound": "hbm",
                 "achieved": round(kern["achieved_gbs"], 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(kern["achieved_gbs"] / HBM_PEAK_GBS, 5),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "avg_launch_us": round(kern["avg_us"], 3),
                 "avg_algorithmic_bytes": int(kern["avg_bytes"]),
                 "launches_timed": kern["launches"],
+                "launches_per_step": kern["launches_per_step"],
+                "timing": "the step's own mix of launches (CSRs, channel counts), hipGraph-replayed between HIP "
+                          "events on the replay stream",
             },
             "cpu_baseline": cpu,
         }

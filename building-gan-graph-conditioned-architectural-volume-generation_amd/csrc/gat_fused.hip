@@ -168,30 +168,38 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_cp(
 }
 
 // C <= 8: 8 lanes per destination row, one edge per lane.
-template <int CMAX>
+// PRE: a_src / a_dst are inputs (vg_gat_lin_att computed them in the
+// projection GEMM's epilogue); otherwise they are formed here and written.
+template <int CMAX, bool PRE = false>
 __global__ void __launch_bounds__(kBlock) k_gat_fwd_ep(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, int N, int C,
     const float* __restrict__ h, const float* __restrict__ att_s, const float* __restrict__ att_d,
     const float* __restrict__ bias, float slope, float* __restrict__ out, float* __restrict__ alpha,
-    float* __restrict__ a_src_out, float* __restrict__ a_dst_out) {
+    float* __restrict__ a_src_io, float* __restrict__ a_dst_io) {
   constexpr int L = 8;
   const GroupIdx g = group_index<L>();
   if (g.row >= N) return;
   const int i = g.row;
-  float vs[CMAX], vd[CMAX];
-  float ad = 0.f, as_i = 0.f;
+  float vs[CMAX];
+  float ad = 0.f;
+  if constexpr (PRE) {
 #pragma unroll
-  for (int c = 0; c < CMAX; ++c) {
-    const bool ok = c < C;
-    vs[c] = ok ? att_s[c] : 0.f;
-    vd[c] = ok ? att_d[c] : 0.f;
-    const float hv = ok ? h[(size_t)i * C + c] : 0.f;
-    ad = fmaf(hv, vd[c], ad);
-    as_i = fmaf(hv, vs[c], as_i);
-  }
-  if (g.lane == 0) {
-    a_dst_out[i] = ad;
-    a_src_out[i] = as_i;
+    for (int c = 0; c < CMAX; ++c) vs[c] = 0.f;
+    ad = a_dst_io[i];
+  } else {
+    float as_i = 0.f;
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c) {
+      const bool ok = c < C;
+      vs[c] = ok ? att_s[c] : 0.f;
+      const float hv = ok ? h[(size_t)i * C + c] : 0.f;
+      ad = fmaf(hv, ok ? att_d[c] : 0.f, ad);
+      as_i = fmaf(hv, vs[c], as_i);
+    }
+    if (g.lane == 0) {
+      a_dst_io[i] = ad;
+      a_src_io[i] = as_i;
+    }
   }
   const int beg = row_ptr[i], end = row_ptr[i + 1];
   float hv[kEP][CMAX];
@@ -203,11 +211,11 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_ep(
     e[t] = -INFINITY;
     if (k < end) {
       const int s = col[k];
-      float a = 0.f;
+      float a = PRE ? a_src_io[s] : 0.f;
 #pragma unroll
       for (int c = 0; c < CMAX; ++c) {
         hv[t][c] = c < C ? h[(size_t)s * C + c] : 0.f;
-        a = fmaf(hv[t][c], vs[c], a);
+        if (!PRE) a = fmaf(hv[t][c], vs[c], a);
       }
       e[t] = lrelu(a + ad, slope);
       m = fmaxf(m, e[t]);
@@ -219,10 +227,11 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_ep(
   // rows longer than 8*kEP: stream the rest (logits only for the max)
   for (int k = beg + g.lane + kEP * L; k < end; k += L) {
     const int s = col[k];
-    float a = 0.f;
+    float a = PRE ? a_src_io[s] : 0.f;
+    if (!PRE)
 #pragma unroll
-    for (int c = 0; c < CMAX; ++c)
-      if (c < C) a = fmaf(h[(size_t)s * C + c], vs[c], a);
+      for (int c = 0; c < CMAX; ++c)
+        if (c < C) a = fmaf(h[(size_t)s * C + c], vs[c], a);
     m = fmaxf(m, lrelu(a + ad, slope));
   }
   m = group_max<L>(m);
@@ -242,11 +251,11 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_ep(
   }
   for (int k = beg + g.lane + kEP * L; k < end; k += L) {
     const int s = col[k];
-    float a = 0.f, hv2[CMAX];
+    float a = PRE ? a_src_io[s] : 0.f, hv2[CMAX];
 #pragma unroll
     for (int c = 0; c < CMAX; ++c) {
       hv2[c] = c < C ? h[(size_t)s * C + c] : 0.f;
-      a = fmaf(hv2[c], vs[c], a);
+      if (!PRE) a = fmaf(hv2[c], vs[c], a);
     }
     const float p = expf(lrelu(a + ad, slope) - m);
     ssum += p;
@@ -270,10 +279,11 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_ep(
   }
   for (int k = beg + g.lane + kEP * L; k < end; k += L) {
     const int s = col[k];
-    float a = 0.f;
+    float a = PRE ? a_src_io[s] : 0.f;
+    if (!PRE)
 #pragma unroll
-    for (int c = 0; c < CMAX; ++c)
-      if (c < C) a = fmaf(h[(size_t)s * C + c], vs[c], a);
+      for (int c = 0; c < CMAX; ++c)
+        if (c < C) a = fmaf(h[(size_t)s * C + c], vs[c], a);
     alpha[k] = expf(lrelu(a + ad, slope) - m) / denom;
   }
 }
@@ -678,6 +688,53 @@ extern "C" int vg_gat_fwd(const int32_t* row_ptr, const int32_t* col, int32_t N,
   } else {
     VG_DISPATCH_FUSED(C, (k_gat_att<L_, CPL_, V_><<<grid_for(N, L_), kBlock, 0, s>>>(
                              h, N, C, att_src, att_dst, a_src, a_dst)));
+    VG_DISPATCH_FUSED(C, (k_gat_fwd_cp<L_, CPL_, V_><<<grid_for(N, L_), kBlock, 0, s>>>(
+                             row_ptr, col, N, C, h, a_src, a_dst, bias, slope, out, alpha)));
+  }
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int vg_gat_att(const float* h, int32_t N, int32_t C, const float* att_src,
+                          const float* att_dst, float* a_src, float* a_dst, void* stream) {
+  if (N <= 0 || C <= 0 || C > 256 || !h || !att_src || !att_dst || !a_src || !a_dst)
+    return VG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (C <= 8)
+    k_gat_att<8, 1, false><<<grid_for(N, 8), kBlock, 0, s>>>(h, N, C, att_src, att_dst, a_src,
+                                                              a_dst);
+  else
+    VG_DISPATCH_FUSED(C, (k_gat_att<L_, CPL_, V_><<<grid_for(N, L_), kBlock, 0, s>>>(
+                             h, N, C, att_src, att_dst, a_src, a_dst)));
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int vg_gat_aggregate_fwd(const int32_t* row_ptr, const int32_t* col, int32_t N,
+                                    int32_t C, const float* h, const float* a_src,
+                                    const float* a_dst, const float* bias, float slope, float* out,
+                                    float* alpha, void* stream) {
+  if (N <= 0 || C <= 0 || C > 256 || !row_ptr || !col || !h || !a_src || !a_dst || !bias ||
+      !out || !alpha)
+    return VG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  float* as = const_cast<float*>(a_src);  // read-only under PRE
+  float* ad = const_cast<float*>(a_dst);
+  if (C <= 8) {
+    const int grid = grid_for(N, 8);
+    if (C <= 1)
+      k_gat_fwd_ep<1, true><<<grid, kBlock, 0, s>>>(row_ptr, col, N, C, h, nullptr, nullptr, bias,
+                                                     slope, out, alpha, as, ad);
+    else if (C <= 2)
+      k_gat_fwd_ep<2, true><<<grid, kBlock, 0, s>>>(row_ptr, col, N, C, h, nullptr, nullptr, bias,
+                                                     slope, out, alpha, as, ad);
+    else if (C <= 4)
+      k_gat_fwd_ep<4, true><<<grid, kBlock, 0, s>>>(row_ptr, col, N, C, h, nullptr, nullptr, bias,
+                                                     slope, out, alpha, as, ad);
+    else
+      k_gat_fwd_ep<8, true><<<grid, kBlock, 0, s>>>(row_ptr, col, N, C, h, nullptr, nullptr, bias,
+                                                     slope, out, alpha, as, ad);
+  } else {
     VG_DISPATCH_FUSED(C, (k_gat_fwd_cp<L_, CPL_, V_><<<grid_for(N, L_), kBlock, 0, s>>>(
                              row_ptr, col, N, C, h, a_src, a_dst, bias, slope, out, alpha)));
   }

@@ -266,6 +266,19 @@ extern "C" int vg_gat_jvp2(const int32_t* row_ptr, const int32_t* col, const int
                            const float* a_dst, const float* alpha, float slope, float* u_out,
                            float* h_inj, float* g_att_src, float* g_att_dst, float* workspace,
                            void* stream) {
+  return vg_gat_jvp2_ex(row_ptr, col, csc_ptr, csc_slot, csc_dst, N, E, C, h, u, g_out, att_src,
+                        att_dst, a_src, a_dst, alpha, slope, u_out, h_inj, g_att_src, g_att_dst,
+                        nullptr, nullptr, workspace, stream);
+}
+
+extern "C" int vg_gat_jvp2_ex(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,
+                              const int32_t* csc_slot, const int32_t* csc_dst, int32_t N, int32_t E,
+                              int32_t C, const float* h, const float* u, const float* g_out,
+                              const float* att_src, const float* att_dst, const float* a_src,
+                              const float* a_dst, const float* alpha, float slope, float* u_out,
+                              float* h_inj, float* g_att_src, float* g_att_dst,
+                              const float* up_src_in, const float* up_dst_in, float* workspace,
+                              void* stream) {
   Shape sh;
   if (N <= 0 || E <= 0 || !row_ptr || !col || !csc_ptr || !csc_slot || !csc_dst || !h || !u ||
       !g_out || !att_src || !att_dst || !a_src || !a_dst || !alpha || !u_out || !h_inj ||
@@ -277,15 +290,19 @@ extern "C" int vg_gat_jvp2(const int32_t* row_ptr, const int32_t* col, const int
   float* e_gz = e_h + E;
   float* e_gzp = e_gz + E;
   float* e_alp = e_gzp + E;
-  float* up_src = e_alp + E;
-  float* up_dst = up_src + N;
-  float* n_gad = up_dst + N;
+  float* up_src_ws = e_alp + E;
+  float* up_dst_ws = up_src_ws + N;
+  float* n_gad = up_dst_ws + N;
   float* part_r = n_gad + N;
   float* part_s = part_r + (size_t)kMaxBlocks * C;
   int grid = grid_for(N, sh.L);
   if (grid > kMaxBlocks) grid = kMaxBlocks;
-  VG_DISPATCH_JVP(C, (k_jvp_att<L_, CPL_, V_><<<grid_for(N, L_), kBlock, 0, s>>>(
-                         u, N, C, att_src, att_dst, up_src, up_dst)));
+  if ((up_src_in == nullptr) != (up_dst_in == nullptr)) return VG_EINVAL;
+  const float* up_src = up_src_in ? up_src_in : up_src_ws;
+  const float* up_dst = up_dst_in ? up_dst_in : up_dst_ws;
+  if (!up_src_in)  // tangent projections not supplied by the tangent GEMM's epilogue
+    VG_DISPATCH_JVP(C, (k_jvp_att<L_, CPL_, V_><<<grid_for(N, L_), kBlock, 0, s>>>(
+                           u, N, C, att_src, att_dst, up_src_ws, up_dst_ws)));
   VG_DISPATCH_JVP(C, (k_jvp_rows<L_, CPL_, V_><<<grid, kBlock, 0, s>>>(
                          row_ptr, col, N, C, h, u, g_out, a_src, a_dst, up_src, up_dst, alpha,
                          slope, u_out, e_u, e_h, e_gz, e_gzp, e_alp, n_gad, part_r)));

@@ -39,21 +39,44 @@ __device__ __forceinline__ float act_fn(float v, float aux) {
   else return v;
 }
 
+// Logical (row tile, column tile) of this workgroup, XCD-aware: the hardware
+// deals workgroups round-robin over the 8 XCDs in dispatch order (x fastest),
+// so linear id b runs on XCD b % 8; every XCD gets one contiguous range of
+// row tiles -- the same row ranges the message-passing kernels (xcd_remap)
+// give it, so the rows a GEMM writes are read back through the same L2.
+// Speed only, never correctness.
+__device__ __forceinline__ void tile_xy(int& tx, int& ty) {
+  const int gy = gridDim.y;
+  const int hw = blockIdx.x + gridDim.x * blockIdx.y;
+  const int logical = xcd_remap(hw, gridDim.x * gy);
+  tx = logical / gy;
+  ty = logical % gy;
+}
+
 // C = A . op(B) (+bias) (+act).  BT: B is [M, K] (op = B^T); else B is [K, M].
 // Software pipelined: the next K-tile is loaded into registers while the MFMAs
 // of the current one run; LDS is double-buffered (one barrier per K-tile).
-template <bool BT, int ACT>
+// ATT (BT, ACT 0, M <= 64): also a_src[n] = <C[n,:], att_s>, a_dst[n] =
+// <C[n,:], att_d> -- GATConv's attention projections as the epilogue of its
+// own projection GEMM (the output tile is staged through LDS once).
+template <bool BT, int ACT, bool ATT = false>
 __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int lda,
                                               const float* __restrict__ B, int ldb,
                                               const float* __restrict__ bias,
                                               const float* __restrict__ aux, int ldaux,
-                                              float* __restrict__ C, int ldc, int N, int M, int K) {
+                                              float* __restrict__ C, int ldc, int N, int M, int K,
+                                              const float* __restrict__ att_s = nullptr,
+                                              const float* __restrict__ att_d = nullptr,
+                                              float* __restrict__ a_src = nullptr,
+                                              float* __restrict__ a_dst = nullptr) {
   __shared__ float As[2][TM][LDP];
   __shared__ float Bs[2][TN][LDP];  // Bs[j][k] = op(B)[k][j]
   constexpr int PER = (TM * TK) / 256;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wr = wave >> 1, wc = wave & 1;
-  const int n0 = blockIdx.x * TM, m0 = blockIdx.y * TN;
+  int tx, ty;
+  tile_xy(tx, ty);
+  const int n0 = tx * TM, m0 = ty * TN;
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -104,6 +127,35 @@ __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int l
       C[(size_t)n * ldc + m] = act_fn<ACT>(acc[r] + bv, av);
     }
   }
+  if constexpr (ATT) {
+    // stage the 64 x 64 tile in LDS (reusing As), then 4 threads per row dot
+    // 16 columns each with att_s / att_d and combine by two shuffles
+    float(*Ct)[TN + 1] = reinterpret_cast<float(*)[TN + 1]>(&As[0][0][0]);
+    __syncthreads();  // every wave is done with the last K-tile's As
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      Ct[wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)][wc * 32 + (lane & 31)] = acc[r] + bv;
+    __syncthreads();
+    const int row = t >> 2, q = t & 3;
+    float ss = 0.f, sd = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int c = q * 16 + j;
+      if (c < M) {
+        const float v = Ct[row][c];
+        ss = fmaf(v, att_s[c], ss);
+        sd = fmaf(v, att_d[c], sd);
+      }
+    }
+    ss += __shfl_xor(ss, 1, 64);
+    sd += __shfl_xor(sd, 1, 64);
+    ss += __shfl_xor(ss, 2, 64);
+    sd += __shfl_xor(sd, 2, 64);
+    if (q == 0 && n0 + row < N) {
+      a_src[n0 + row] = ss;
+      a_dst[n0 + row] = sd;
+    }
+  }
 }
 
 // part[chunk][M][K] = A[chunk rows]^T . B[chunk rows];  pdb[chunk][M] = column sums of A.
@@ -117,9 +169,14 @@ __global__ void __launch_bounds__(256) k_gemm_tn(const float* __restrict__ A, in
   constexpr int PER = (TK * TM) / 256;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wr = wave >> 1, wc = wave & 1;
-  const int m0 = blockIdx.x * TM, k0 = blockIdx.y * TN, chunk = blockIdx.z;
+  // XCD-aware: each XCD takes a contiguous range of row chunks (tile_xy)
+  const int gxy = gridDim.x * gridDim.y;
+  const int logical = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
+                                gxy * gridDim.z);
+  const int chunk = logical / gxy, rem = logical % gxy;
+  const int m0 = (rem % gridDim.x) * TM, k0 = (rem / gridDim.x) * TN;
   const int nb = chunk * rows, ne = min(N, nb + rows);
-  const bool do_db = pdb && blockIdx.y == 0;
+  const bool do_db = pdb && k0 == 0;
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -172,12 +229,23 @@ __global__ void __launch_bounds__(256) k_gemm_tn(const float* __restrict__ A, in
 }
 
 // out[w / K][w % K] (row stride ldo) = sum_c part[c][w], fixed order (+= when acc);
-// 1024 threads per 64 outputs, 16 rows in flight.
+// 1024 threads per 64 outputs, 16 rows in flight.  Blocks from nb1 on fold a
+// second, dense set (part2 [rows][W2] -> out2, the bias gradient) in the same
+// launch.
 __global__ void __launch_bounds__(1024) k_fold_rows(const float* __restrict__ part, int rows,
                                                     long long W, int K, int ldo, int acc,
-                                                    float* __restrict__ out) {
+                                                    float* __restrict__ out, int nb1 = 1 << 30,
+                                                    const float* __restrict__ part2 = nullptr,
+                                                    int W2 = 0, float* __restrict__ out2 = nullptr) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const long long w = blockIdx.x * 64LL + lane;
+  int bx = blockIdx.x;
+  if (bx >= nb1) {
+    bx -= nb1;
+    part = part2;
+    W = K = ldo = W2;
+    out = out2;
+  }
+  const long long w = bx * 64LL + lane;
   float s = 0.f;
   if (w < W) {
     // 4 independent accumulators (loads in flight), combined in a fixed order
@@ -268,8 +336,27 @@ static int gemm_tn(const float* A, int32_t lda, const float* B, int32_t ldb, int
   k_gemm_tn<<<grid, 256, 0, s>>>(A, lda, B, ldb, N, M, K, rows, part, db ? pdb : nullptr,
                                  db_rows < N ? db_rows : N);
   const long long W = (long long)M * K;
-  k_fold_rows<<<(int)((W + 63) / 64), 1024, 0, s>>>(part, chunks, W, K, ldc, accumulate, C);
-  if (db) k_fold_rows<<<(M + 63) / 64, 1024, 0, s>>>(pdb, chunks, M, M, M, accumulate, db);
+  const int nb1 = (int)((W + 63) / 64), nb2 = db ? (M + 63) / 64 : 0;
+  k_fold_rows<<<nb1 + nb2, 1024, 0, s>>>(part, chunks, W, K, ldc, accumulate, C, nb1, pdb, M, db);
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int vg_gat_lin_att(const float* X, int32_t ldx, const float* W, int32_t N,
+                              int32_t Cin, int32_t C, const float* att_src, const float* att_dst,
+                              float* H, float* a_src, float* a_dst, void* stream) {
+  if (N < 0 || Cin <= 0 || C <= 0 || ldx < Cin || !X || !W || !att_src || !att_dst || !H ||
+      !a_src || !a_dst)
+    return VG_EINVAL;
+  if (N == 0) return 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (C > TN) {  // several column tiles: GEMM, then the per-row projection pass
+    const int rc = vg_gemm(X, ldx, W, Cin, 1, nullptr, 0, nullptr, 0, H, C, N, C, Cin, stream);
+    if (rc) return rc;
+    return vg_gat_att(H, N, C, att_src, att_dst, a_src, a_dst, stream);
+  }
+  k_gemm<true, 0, true><<<dim3((N + TM - 1) / TM, 1), 256, 0, s>>>(
+      X, ldx, W, Cin, nullptr, nullptr, 0, H, C, N, C, Cin, att_src, att_dst, a_src, a_dst);
   VG_CHECK_LAUNCH();
   return 0;
 }

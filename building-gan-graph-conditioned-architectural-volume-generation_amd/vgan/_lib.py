@@ -23,6 +23,11 @@ SIGNATURES = {
     "vg_csr_build": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "vg_gat_fwd": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p,
                                   _c_p, _c_p]),
+    "vg_gat_att": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "vg_gat_lin_att": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p,
+                                      _c_p]),
+    "vg_gat_aggregate_fwd": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p,
+                                            _c_p]),
     "vg_gat_bwd_ws_floats": (_c_i64, [_c_i32, _c_i32, _c_i32]),
     "vg_gat_bwd": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p,
                                   _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
@@ -56,6 +61,9 @@ SIGNATURES = {
     "vg_gat_jvp2_ws_floats": (_c_i64, [_c_i32, _c_i32, _c_i32]),
     "vg_gat_jvp2": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p,
                                    _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "vg_gat_jvp2_ex": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p,
+                                      _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
+                                      _c_p]),
     "vg_graphnorm_seg_ws_floats": (_c_i64, [_c_i32, _c_i32, _c_i32]),
     "vg_graphnorm_fwd_seg": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p,
                                             _c_p, _c_p, _c_p]),

@@ -156,13 +156,13 @@ class CriticEngine:
         blk = []
         for (conv, norm), keep in zip(self.blocks, keeps):
             c = conv.out_channels
-            H = _f(R, c, dev=dev)
-            self._gemm(st, ptr(x), xw, ptr(conv.lin.weight), xw, 1, ptr(H), c, R, c, xw)
-            O = _f(R, c, dev=dev)
-            alpha, a_s, a_d = _f(3 * E, dev=dev), _f(R, dev=dev), _f(R, dev=dev)
-            check(LIB.vg_gat_fwd(ptr(csr3.row_ptr), ptr(csr3.col), R, c, ptr(H), ptr(conv.att_src),
-                                 ptr(conv.att_dst), ptr(conv.bias), float(conv.negative_slope), ptr(O), ptr(alpha),
-                                 ptr(a_s), ptr(a_d), st), "vg_gat_fwd")
+            H, a_s, a_d = _f(R, c, dev=dev), _f(R, dev=dev), _f(R, dev=dev)
+            check(LIB.vg_gat_lin_att(ptr(x), xw, ptr(conv.lin.weight), R, xw, c, ptr(conv.att_src),
+                                     ptr(conv.att_dst), ptr(H), ptr(a_s), ptr(a_d), st), "vg_gat_lin_att")
+            O, alpha = _f(R, c, dev=dev), _f(3 * E, dev=dev)
+            check(LIB.vg_gat_aggregate_fwd(ptr(csr3.row_ptr), ptr(csr3.col), R, c, ptr(H), ptr(a_s), ptr(a_d),
+                                           ptr(conv.bias), float(conv.negative_slope), ptr(O), ptr(alpha), st),
+                  "vg_gat_aggregate_fwd")
             Y, stats = _f(X4, c, dev=dev), _f(3 * 2 * c, dev=dev)
             ws = _f(int(LIB.vg_graphnorm_seg_ws_floats(3, n, c)), dev=dev)
             if keep is not None and not isinstance(keep, torch.Tensor):  # DropSpec: drawn in-kernel
@@ -272,15 +272,18 @@ class CriticEngine:
         for b in range(nb):
             (conv, norm), B = self.blocks[b], blk[b]
             c, cin = B["c"], B["xw"]
-            uH = _f(n, c, dev=dev)
-            self._gemm(st, u_in, cin, ptr(conv.lin.weight), cin, 1, ptr(uH), c, n, c, cin)
+            # tangent of the projection with its attention projections in the epilogue
+            uH, up_s, up_d = _f(n, c, dev=dev), _f(n, dev=dev), _f(n, dev=dev)
+            check(LIB.vg_gat_lin_att(u_in, cin, ptr(conv.lin.weight), n, cin, c, ptr(conv.att_src),
+                                     ptr(conv.att_dst), ptr(uH), ptr(up_s), ptr(up_d), st), "vg_gat_lin_att")
             uO, hinj = _f(n, c, dev=dev), _f(n, c, dev=dev)
             ws = _f(int(LIB.vg_gat_jvp2_ws_floats(n, E, c)), dev=dev)
-            check(LIB.vg_gat_jvp2(ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot),
-                                  ptr(csr.csc_dst), n, E, c, rows(B["H"], mrow, c), ptr(uH), ptr(dO_b[b]),
-                                  ptr(conv.att_src), ptr(conv.att_dst), _off(B["a_s"], mrow), _off(B["a_d"], mrow),
-                                  _off(B["alpha"], 2 * E), float(conv.negative_slope), ptr(uO), ptr(hinj),
-                                  ptr(conv.att_src.grad), ptr(conv.att_dst.grad), ptr(ws), st), "vg_gat_jvp2")
+            check(LIB.vg_gat_jvp2_ex(ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot),
+                                     ptr(csr.csc_dst), n, E, c, rows(B["H"], mrow, c), ptr(uH), ptr(dO_b[b]),
+                                     ptr(conv.att_src), ptr(conv.att_dst), _off(B["a_s"], mrow), _off(B["a_d"], mrow),
+                                     _off(B["alpha"], 2 * E), float(conv.negative_slope), ptr(uO), ptr(hinj),
+                                     ptr(conv.att_src.grad), ptr(conv.att_dst.grad), ptr(up_s), ptr(up_d), ptr(ws),
+                                     st), "vg_gat_jvp2_ex")
             oinj = _f(n, c, dev=dev)
             ws = _f(int(LIB.vg_graphnorm_seg_ws_floats(1, n, c)), dev=dev)
             check(LIB.vg_graphnorm_jvp2(rows(B["O"], mrow, c), n, c, ptr(norm.weight), ptr(norm.bias),

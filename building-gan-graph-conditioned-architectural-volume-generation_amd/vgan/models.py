@@ -28,7 +28,7 @@ import torch.nn as nn
 
 from . import data as vdata
 from . import ops
-from .nn import MLP, Linear, linear
+from .nn import MLP, Linear, linear_att
 from .rng import RNG
 
 _CONV_TYPES = ("GCNCONV", "GRAPHCONV", "GATCONV", "GATV2CONV")
@@ -70,8 +70,10 @@ class GATConv(nn.Module):
             self.bias.zero_()
 
     def forward(self, x: torch.Tensor, csr: ops.CSR) -> torch.Tensor:
-        h = linear(x, self.lin.weight)
-        return ops.gat_conv(csr, h, self.att_src, self.att_dst, self.bias, self.negative_slope)
+        # projection + attention projections in one launch, then the edge
+        # softmax / gather-sum kernel
+        h, a_s, a_d = linear_att(x, self.lin.weight, self.att_src, self.att_dst)
+        return ops.gat_conv(csr, h, self.att_src, self.att_dst, self.bias, self.negative_slope, pre=(a_s, a_d))
 
 
 class GraphNorm(nn.Module):

@@ -76,27 +76,59 @@ class _LinearFn(Function):
 
     @staticmethod
     def backward(ctx, gy):
-        x, weight = ctx.saved_tensors
-        gx = gw = gb = None
-        if torch.is_grad_enabled():  # create_graph: differentiable MFMA matmuls
-            gy = gy.contiguous()
-            if ctx.needs_input_grad[0]:
-                gx = _MMnn.apply(gy, weight)
-            if ctx.needs_input_grad[1]:
-                gw = _MMtn.apply(gy, x)
-            if ctx.has_bias and ctx.needs_input_grad[2]:
-                gb = gy.sum(0)
-            return gx, gw, gb, None
+        return _linear_backward(ctx, gy) + (None,)
+
+
+def _linear_backward(ctx, gy):
+    """(g_x, g_weight, g_bias) of y = x W^T (+ b) for _LinearFn / _LinAttFn."""
+    x, weight = ctx.saved_tensors
+    gx = gw = gb = None
+    if torch.is_grad_enabled():  # create_graph: differentiable MFMA matmuls
         gy = gy.contiguous()
         if ctx.needs_input_grad[0]:
-            gx = ops.gemm(gy, weight, False)
-        pw, pb = ctx.params
-        if ctx.needs_input_grad[1] and ops._direct(pw, pb):  # accumulate into .grad directly
-            ops.gemm_tn_into(gy, x, pw.grad, pb.grad if ctx.has_bias else None)
-            return gx, None, None, None
-        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
-            gw, gb = ops.gemm_tn(gy, x, want_colsum=ctx.has_bias)
-        return gx, gw, (gb if ctx.has_bias else None), None
+            gx = _MMnn.apply(gy, weight)
+        if ctx.needs_input_grad[1]:
+            gw = _MMtn.apply(gy, x)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = gy.sum(0)
+        return gx, gw, gb
+    gy = gy.contiguous()
+    if ctx.needs_input_grad[0]:
+        gx = ops.gemm(gy, weight, False)
+    pw, pb = ctx.params
+    if ctx.needs_input_grad[1] and ops._direct(pw, pb):  # accumulate into .grad directly
+        ops.gemm_tn_into(gy, x, pw.grad, pb.grad if ctx.has_bias else None)
+        return gx, None, None
+    if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+        gw, gb = ops.gemm_tn(gy, x, want_colsum=ctx.has_bias)
+    return gx, gw, (gb if ctx.has_bias else None)
+
+
+class _LinAttFn(Function):
+    """GATConv.lin (no bias) with the attention projections h . att_src,
+    h . att_dst as two extra, non-differentiable outputs (their dependence on
+    h and att is differentiated inside ops.gat_conv)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, att_src, att_dst):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = False
+        ctx.params = (weight, None)
+        h, a_s, a_d = ops.lin_att(x, weight, att_src, att_dst)
+        ctx.mark_non_differentiable(a_s, a_d)
+        return h, a_s, a_d
+
+    @staticmethod
+    def backward(ctx, gh, _g_as, _g_ad):
+        gx, gw, _ = _linear_backward(ctx, gh)
+        return gx, gw, None, None
+
+
+def linear_att(x: torch.Tensor, weight: torch.Tensor, att_src: torch.Tensor, att_dst: torch.Tensor):
+    """(x W^T, projections on att_src / att_dst) -- one launch (vg_gat_lin_att)."""
+    if not x.is_cuda:
+        raise RuntimeError("vgan HIP ops require tensors on a ROCm device (no CPU fallback)")
+    return _LinAttFn.apply(x.contiguous(), weight, att_src, att_dst)
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:

@@ -356,7 +356,7 @@ def gat_conv_composed(csr, h, att_src, att_dst, bias, slope: float = NEG_SLOPE):
 
 class _GATConv(Function):
     @staticmethod
-    def forward(ctx, h, att_src, att_dst, bias, csr, slope):
+    def forward(ctx, h, att_src, att_dst, bias, csr, slope, pre=None):
         h = _f32(h)
         vs, vd, b = _f32(att_src.reshape(-1)), _f32(att_dst.reshape(-1)), _f32(bias)
         require_cuda(h, vs, vd, b)
@@ -366,10 +366,20 @@ class _GATConv(Function):
         dev = h.device
         out = torch.empty_like(h)
         alpha = torch.empty(csr.num_edges, dtype=torch.float32, device=dev)
-        a_src = torch.empty(n, dtype=torch.float32, device=dev)
-        a_dst = torch.empty(n, dtype=torch.float32, device=dev)
-        check(LIB.vg_gat_fwd(ptr(csr.row_ptr), ptr(csr.col), n, c, ptr(h), ptr(vs), ptr(vd), ptr(b), float(slope),
-                             ptr(out), ptr(alpha), ptr(a_src), ptr(a_dst), csr.stream()), "vg_gat_fwd")
+        if pre is not None:  # projections from the projection GEMM's epilogue (lin_att)
+            a_src, a_dst = pre
+            require_cuda(a_src, a_dst)
+            if a_src.numel() != n or a_dst.numel() != n:
+                raise ValueError("gat_conv: inconsistent projection shapes")
+            check(LIB.vg_gat_aggregate_fwd(ptr(csr.row_ptr), ptr(csr.col), n, c, ptr(h), ptr(a_src), ptr(a_dst),
+                                           ptr(b), float(slope), ptr(out), ptr(alpha), csr.stream()),
+                  "vg_gat_aggregate_fwd")
+        else:
+            a_src = torch.empty(n, dtype=torch.float32, device=dev)
+            a_dst = torch.empty(n, dtype=torch.float32, device=dev)
+            check(LIB.vg_gat_fwd(ptr(csr.row_ptr), ptr(csr.col), n, c, ptr(h), ptr(vs), ptr(vd), ptr(b),
+                                 float(slope), ptr(out), ptr(alpha), ptr(a_src), ptr(a_dst), csr.stream()),
+                  "vg_gat_fwd")
         ctx.csr, ctx.slope = csr, slope
         ctx.params = (att_src, att_dst, bias)
         ctx.save_for_backward(h, att_src, att_dst, bias, alpha, a_src, a_dst)
@@ -390,7 +400,7 @@ class _GATConv(Function):
             g_h = g_h + g_as.unsqueeze(1) * vs + g_ad.unsqueeze(1) * vd
             g_vs = (h * g_as.unsqueeze(1)).sum(0).view_as(att_src)
             g_vd = (h * g_ad.unsqueeze(1)).sum(0).view_as(att_dst)
-            return g_h, g_vs, g_vd, g_out.sum(0), None, None
+            return g_h, g_vs, g_vd, g_out.sum(0), None, None, None
         g_out = _f32(g_out)
         n, c = h.shape
         dev = h.device
@@ -410,14 +420,18 @@ class _GATConv(Function):
                                 float(ctx.slope), ptr(g_h), ptr(g_vs), ptr(g_vd), ptr(g_b), 1 if direct else 0, None, 0,
                                 ptr(ws), csr.stream()), "vg_gat_bwd_ex")
         if direct:
-            return g_h, None, None, None, None, None
-        return g_h, g_vs.view_as(att_src), g_vd.view_as(att_dst), g_b, None, None
+            return g_h, None, None, None, None, None, None
+        return g_h, g_vs.view_as(att_src), g_vd.view_as(att_dst), g_b, None, None, None
 
 
-def gat_conv(csr: CSR, h, att_src, att_dst, bias, slope: float = NEG_SLOPE) -> torch.Tensor:
+def gat_conv(csr: CSR, h, att_src, att_dst, bias, slope: float = NEG_SLOPE, pre=None) -> torch.Tensor:
     """GATConv (heads=1) after the projection h = x W^T: attention projections,
-    segment softmax, aggregation and bias in one kernel (see ``vg_gat_fwd``)."""
-    return _GATConv.apply(h, att_src, att_dst, bias, csr, slope)
+    segment softmax, aggregation and bias (``vg_gat_fwd``).  ``pre`` = (h .
+    att_src, h . att_dst) already computed (``lin_att``): then only the edge
+    softmax + gather-sum kernel runs (``vg_gat_aggregate_fwd``).  The
+    projections' dependence on h / att is part of this op's backward, so
+    ``pre`` carries no gradient."""
+    return _GATConv.apply(h, att_src, att_dst, bias, csr, slope, pre)
 
 
 # ------------------------------------------ GraphNorm + ReLU + Dropout
@@ -667,6 +681,25 @@ def gemm(a: torch.Tensor, b: torch.Tensor, b_trans: bool, bias: Optional[torch.T
     check(LIB.vg_gemm(ptr(a), k, ptr(b), b.shape[1], 1 if b_trans else 0, ptr(bb), int(act), None, 0, ptr(c), m, n,
                       m, k, stream_handle(a.device)), "vg_gemm")
     return c
+
+
+def lin_att(x: torch.Tensor, w: torch.Tensor, att_src: torch.Tensor, att_dst: torch.Tensor):
+    """(h = x w^T, h . att_src, h . att_dst) from one launch (vg_gat_lin_att):
+    GATConv.lin plus the attention projections, the latter in the GEMM's
+    epilogue."""
+    x, w = _f32(x), _f32(w)
+    vs, vd = _f32(att_src.reshape(-1)), _f32(att_dst.reshape(-1))
+    require_cuda(x, w, vs, vd)
+    n, k = x.shape
+    c = w.shape[0]
+    if w.shape[1] != k or vs.numel() != c or vd.numel() != c:
+        raise ValueError("lin_att: inconsistent shapes")
+    h = torch.empty(n, c, dtype=torch.float32, device=x.device)
+    a_s = torch.empty(n, dtype=torch.float32, device=x.device)
+    a_d = torch.empty(n, dtype=torch.float32, device=x.device)
+    check(LIB.vg_gat_lin_att(ptr(x), k, ptr(w), n, k, c, ptr(vs), ptr(vd), ptr(h), ptr(a_s), ptr(a_d),
+                             stream_handle(x.device)), "vg_gat_lin_att")
+    return h, a_s, a_d
 
 
 def gemm_tn(a: torch.Tensor, b: torch.Tensor, want_colsum: bool = True):

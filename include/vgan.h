@@ -68,6 +68,31 @@ int vg_gat_fwd(const int32_t* row_ptr, const int32_t* col, int32_t num_nodes, in
                const float* h, const float* att_src, const float* att_dst, const float* bias,
                float slope, float* out, float* alpha, float* a_src, float* a_dst, void* stream);
 
+/* The two halves of vg_gat_fwd, so the projection can live in a GEMM epilogue.
+ *
+ * vg_gat_att: a_src_i = <h_i, att_src>, a_dst_i = <h_i, att_dst> ([N] each) --
+ * the (x * att).sum(-1) pair of torch_geometric/nn/conv/gat_conv.py (GATConv
+ * .forward, heads=1) as called from models.py:144,242.
+ *
+ * vg_gat_lin_att: H = X W^T (X [N, Cin] row stride ldx, W [C, Cin]) AND the
+ * projections above in one launch when C <= 64 (the tile's rows are reduced
+ * against att_src / att_dst in the GEMM epilogue; C > 64 runs the GEMM then
+ * vg_gat_att) -- GATConv.lin followed by the attention projections.
+ *
+ * vg_gat_aggregate_fwd: given h and the projections, the edge softmax and the
+ * weighted CSR gather-sum (+ bias), writing out [N, C] and alpha [E'] --
+ * GATConv.edge_update (utils/_softmax.py scatter max / sum) and
+ * propagate/message/aggregate ('add' scatter) + bias.  This is the path's
+ * "scatter kernel" (SURVEY.md 8a rows A6-A7). */
+int vg_gat_att(const float* h, int32_t num_nodes, int32_t channels, const float* att_src,
+               const float* att_dst, float* a_src, float* a_dst, void* stream);
+int vg_gat_lin_att(const float* x, int32_t ldx, const float* w, int32_t num_nodes,
+                   int32_t in_channels, int32_t channels, const float* att_src,
+                   const float* att_dst, float* h, float* a_src, float* a_dst, void* stream);
+int vg_gat_aggregate_fwd(const int32_t* row_ptr, const int32_t* col, int32_t num_nodes,
+                         int32_t channels, const float* h, const float* a_src, const float* a_dst,
+                         const float* bias, float slope, float* out, float* alpha, void* stream);
+
 /* Workspace (floats) for vg_gat_bwd. */
 int64_t vg_gat_bwd_ws_floats(int32_t num_nodes, int32_t num_edges, int32_t channels);
 
@@ -108,6 +133,17 @@ int vg_gat_jvp2(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_p
                 const float* g_out, const float* att_src, const float* att_dst, const float* a_src,
                 const float* a_dst, const float* alpha, float slope, float* u_out, float* h_inj,
                 float* g_att_src, float* g_att_dst, float* workspace, void* stream);
+
+/* vg_gat_jvp2 with the tangent projections u att_src / u att_dst supplied
+ * (up_src, up_dst [N], e.g. from vg_gat_lin_att on the tangent), saving its
+ * first pass; both NULL = compute them (same as vg_gat_jvp2). */
+int vg_gat_jvp2_ex(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,
+                   const int32_t* csc_slot, const int32_t* csc_dst, int32_t num_nodes,
+                   int32_t num_edges, int32_t channels, const float* h, const float* u,
+                   const float* g_out, const float* att_src, const float* att_dst,
+                   const float* a_src, const float* a_dst, const float* alpha, float slope,
+                   float* u_out, float* h_inj, float* g_att_src, float* g_att_dst,
+                   const float* up_src, const float* up_dst, float* workspace, void* stream);
 
 /* ---- WGAN-GP critic engine helpers (trainer.py:291-332) ------------------ */
 
