@@ -116,10 +116,13 @@ class _LinAttFn(Function):
         ctx.params = (weight, None)
         h, a_s, a_d = ops.lin_att(x, weight, att_src, att_dst)
         ctx.mark_non_differentiable(a_s, a_d)
+        ctx.set_materialize_grads(False)  # no zero-filled gradients for a_s / a_d
         return h, a_s, a_d
 
     @staticmethod
     def backward(ctx, gh, _g_as, _g_ad):
+        if gh is None:
+            return None, None, None, None
         gx, gw, _ = _linear_backward(ctx, gh)
         return gx, gw, None, None
 

@@ -560,6 +560,7 @@ class _GumbelHead(Function):
                                 stream_handle(lg.device)), "vg_gumbel_fwd")
         ctx.tau = tau
         ctx.save_for_backward(soft)
+        ctx.set_materialize_grads(False)  # an unused output's gradient stays None (no zero fill launch)
         return hard, soft
 
     @staticmethod
