@@ -31,7 +31,6 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kChunks = 256;  // max row chunks per column slab (~64 rows each)
-constexpr int kFinalThreads = 1024;  // finalize: 16 waves fold the chunk partials
 
 struct Welford {
   float n, mean, m2;
@@ -60,11 +59,9 @@ __host__ __device__ inline Lay lay_for(int C) {
   return {cw, 64 / cw};
 }
 
-__device__ void stats_final_body(const float* __restrict__ part, int chunks, int C,
-                                 float* __restrict__ stats, int slab, int seg);
-
-// counter != NULL: the last block to finish also merges every segment / slab
-// (stats_final_body), saving the separate finalize launch.
+// Partials of one (chunk, 64-column slab, segment); counter is unused (the
+// former last-block fold: one workgroup folding every partial ran at a single
+// CU's bandwidth).
 __global__ void __launch_bounds__(kBlock) k_stats_partial(const float* __restrict__ x, int N, int C,
                                                           float* __restrict__ part,
                                                           float* __restrict__ stats, int* counter) {
@@ -110,42 +107,56 @@ __global__ void __launch_bounds__(kBlock) k_stats_partial(const float* __restric
     p[1] = acc.mean;
     p[2] = acc.m2;
   }
-  if (counter && vg_last_block(counter))
-    for (int sg = 0; sg < (int)gridDim.z; ++sg)
-      for (int sl = 0; sl < (int)gridDim.y; ++sl) stats_final_body(part0, gridDim.x, C, stats, sl, sg);
+  (void)counter;
+  (void)part0;
+  (void)stats;
 }
 
-// Merge the per-chunk Welford partials of one 64-column slab of one segment
-// with 256 threads: wave w merges chunks w, w+4, ... (fixed order), then the
-// 4 waves in LDS.
-__device__ void stats_final_body(const float* __restrict__ part, int chunks, int C,
-                                 float* __restrict__ stats, int slab, int seg) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = slab * 64 + lane;
-  part += (size_t)seg * chunks * C * 3;  // segment
-  stats += (size_t)seg * 2 * C;
-  const int NW = blockDim.x >> 6;
-  Welford acc = {0.f, 0.f, 0.f};
-  if (c < C)
-    for (int k = wave; k < chunks; k += NW) {
-      const float* p = part + ((size_t)k * C + c) * 3;
-      acc = merge(acc, Welford{p[0], p[1], p[2]});
-    }
-  __shared__ Welford sw[16][64];
-  sw[wave][lane] = acc;
-  __syncthreads();
-  if (wave == 0 && c < C) {
-    Welford r = sw[0][lane];
-    for (int k = 1; k < NW; ++k) r = merge(r, sw[k][lane]);
-    stats[c] = r.mean;
-    stats[C + c] = sqrtf(fmaxf(r.m2 / r.n, 0.f));
+// Fold of the chunk partials: ONE WAVE PER COLUMN, every segment; lane l takes
+// chunks l, l+64, l+128, l+192 (kChunks <= 256: four loads in flight per lane,
+// one round trip per segment), then a fixed xor-butterfly across the wave --
+// deterministic, and spread over C/4 workgroups.  A single workgroup folding
+// all partials (the first version) ran at one CU's bandwidth, ~8-10 us.
+__device__ __forceinline__ int fold_col() { return blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); }
+
+__device__ __forceinline__ Welford wave_merge(Welford w) {
+  for (int off = 1; off < 64; off <<= 1) {
+    Welford o;
+    o.n = __shfl_xor(w.n, off, 64);
+    o.mean = __shfl_xor(w.mean, off, 64);
+    o.m2 = __shfl_xor(w.m2, off, 64);
+    w = merge(w, o);
   }
-  __syncthreads();
+  return w;
 }
 
-__global__ void __launch_bounds__(kFinalThreads) k_stats_final(const float* __restrict__ part, int chunks,
-                                                     int C, float* __restrict__ stats) {
-  stats_final_body(part, chunks, C, stats, blockIdx.x, blockIdx.y);
+__device__ __forceinline__ float wave_sum(float v) {
+  for (int off = 1; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__global__ void __launch_bounds__(kBlock) k_stats_final(const float* __restrict__ part, int chunks,
+                                                        int C, int S, float* __restrict__ stats) {
+  const int c = fold_col(), lane = threadIdx.x & 63;
+  if (c >= C) return;
+  for (int sg = 0; sg < S; ++sg) {
+    const float* pp = part + (size_t)sg * chunks * C * 3;
+    float v[4][3];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = lane + 64 * u;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) v[u][q] = k < chunks ? pp[((size_t)k * C + c) * 3 + q] : 0.f;
+    }
+    Welford acc = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc = merge(acc, Welford{v[u][0], v[u][1], v[u][2]});
+    acc = wave_merge(acc);
+    if (lane == 0) {
+      stats[(size_t)sg * 2 * C + c] = acc.mean;
+      stats[(size_t)sg * 2 * C + C + c] = sqrtf(fmaxf(acc.m2 / acc.n, 0.f));
+    }
+  }
 }
 
 // keep_out != NULL: draw the dropout multiplier in-kernel (vg_keep with
@@ -176,14 +187,7 @@ __global__ void k_gn_apply(const float* __restrict__ x, long long total, int C, 
   }
 }
 
-__device__ void bwd_final_body(const float* __restrict__ part, int chunks, int C, int S,
-                               const float* __restrict__ w, const float* __restrict__ ms, float eps,
-                               const float* __restrict__ stats, float* __restrict__ sums,
-                               float* __restrict__ g_w, float* __restrict__ g_b,
-                               float* __restrict__ g_ms, int accumulate, int slab);
-
-// backward: column partial sums of gz and gz*xhat (plain sums, chunk order);
-// counter != NULL: the last block also runs the finalize (bwd_final_body).
+// backward: column partial sums of gz and gz*xhat (plain sums, chunk order)
 __global__ void __launch_bounds__(kBlock) k_gn_bwd_partial(
     const float* __restrict__ x, const float* __restrict__ gy, int N, int C,
     const float* __restrict__ w, const float* __restrict__ b, const float* __restrict__ ms,
@@ -240,64 +244,51 @@ __global__ void __launch_bounds__(kBlock) k_gn_bwd_partial(
     p[0] = a;
     p[1] = bb;
   }
-  if (counter && vg_last_block(counter))
-    for (int sl = 0; sl < (int)gridDim.y; ++sl)
-      bwd_final_body(part0, gridDim.x, C, gridDim.z, w, ms, eps, stats0, sums, g_w, g_b, g_ms,
-                     accumulate, sl);
+  (void)counter;
+  (void)part0;
+  (void)stats0;
+  (void)sums;
+  (void)g_w;
+  (void)g_b;
+  (void)g_ms;
+  (void)accumulate;
 }
 
-__device__ void bwd_final_body(const float* __restrict__ part, int chunks, int C, int S,
-                               const float* __restrict__ w, const float* __restrict__ ms, float eps,
-                               const float* __restrict__ stats, float* __restrict__ sums,
-                               float* __restrict__ g_w, float* __restrict__ g_b,
-                               float* __restrict__ g_ms, int accumulate, int slab) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = slab * 64 + lane;
-  const int NW = blockDim.x >> 6;
-  __shared__ float red[16][64][2];
-  float tw = 0.f, tb = 0.f, tm = 0.f;
-  for (int sg = 0; sg < S; ++sg) {
-    const float* pp = part + (size_t)sg * chunks * C * 2;
-    float a = 0.f, bb = 0.f;
-    if (c < C)
-      for (int k = wave; k < chunks; k += NW) {
-        a += pp[((size_t)k * C + c) * 2];
-        bb += pp[((size_t)k * C + c) * 2 + 1];
-      }
-    red[wave][lane][0] = a;
-    red[wave][lane][1] = bb;
-    __syncthreads();
-    if (wave == 0 && c < C) {
-      a = red[0][lane][0];
-      bb = red[0][lane][1];
-      for (int k = 1; k < NW; ++k) {
-        a += red[k][lane][0];
-        bb += red[k][lane][1];
-      }
-      const float* st = stats + (size_t)sg * 2 * C;
-      sums[(size_t)sg * 2 * C + c] = a;
-      sums[(size_t)sg * 2 * C + C + c] = bb;
-      tw += bb;
-      tb += a;
-      tm += -st[c] * w[c] * a / (st[C + c] + eps);
-    }
-    __syncthreads();
-  }
-  if (wave == 0 && c < C && g_w) {
-    g_w[c] = accumulate ? g_w[c] + tw : tw;
-    g_b[c] = accumulate ? g_b[c] + tb : tb;
-    g_ms[c] = accumulate ? g_ms[c] + tm : tm;
-  }
-  __syncthreads();
-}
-
-__global__ void __launch_bounds__(kFinalThreads) k_gn_bwd_final(
+// one wave per column: per-segment sums A, B (-> sums[sg][2C]) and the
+// parameter gradients summed over segments in order
+__global__ void __launch_bounds__(kBlock) k_gn_bwd_final(
     const float* __restrict__ part, int chunks, int C, int S, const float* __restrict__ w,
     const float* __restrict__ ms, float eps, const float* __restrict__ stats,
     float* __restrict__ sums, float* __restrict__ g_w, float* __restrict__ g_b,
     float* __restrict__ g_ms, int accumulate) {
-  bwd_final_body(part, chunks, C, S, w, ms, eps, stats, sums, g_w, g_b, g_ms, accumulate,
-                 blockIdx.x);
+  const int c = fold_col(), lane = threadIdx.x & 63;
+  if (c >= C) return;
+  float tw = 0.f, tb = 0.f, tm = 0.f;
+  for (int sg = 0; sg < S; ++sg) {
+    const float* pp = part + (size_t)sg * chunks * C * 2;
+    float va[4], vb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = lane + 64 * u;
+      va[u] = k < chunks ? pp[((size_t)k * C + c) * 2] : 0.f;
+      vb[u] = k < chunks ? pp[((size_t)k * C + c) * 2 + 1] : 0.f;
+    }
+    const float a = wave_sum((va[0] + va[1]) + (va[2] + va[3]));
+    const float bb = wave_sum((vb[0] + vb[1]) + (vb[2] + vb[3]));
+    const float* st = stats + (size_t)sg * 2 * C;
+    if (lane == 0) {
+      sums[(size_t)sg * 2 * C + c] = a;
+      sums[(size_t)sg * 2 * C + C + c] = bb;
+    }
+    tw += bb;
+    tb += a;
+    tm += -st[c] * w[c] * a / (st[C + c] + eps);
+  }
+  if (lane == 0 && g_w) {
+    g_w[c] = accumulate ? g_w[c] + tw : tw;
+    g_b[c] = accumulate ? g_b[c] + tb : tb;
+    g_ms[c] = accumulate ? g_ms[c] + tm : tm;
+  }
 }
 
 // g_x (+ inj for elements t >= inj_off: the second-order adjoint of the
@@ -336,12 +327,6 @@ __global__ void k_gn_bwd_apply(const float* __restrict__ x, const float* __restr
 // ---------------------------------------------------------- second order
 // column sums for the tangent / second-order pass: [sum u, sum xt u, sum p,
 // sum p u, sum p xt] per column (plain sums, chunk order)
-__device__ void jvp2_final_body(const float* __restrict__ part, int chunks, int N, int C,
-                                const float* __restrict__ w, const float* __restrict__ ms,
-                                float eps, const float* __restrict__ stats,
-                                float* __restrict__ sums, float* __restrict__ g_w,
-                                float* __restrict__ g_ms, int slab);
-
 __global__ void __launch_bounds__(kBlock) k_gn_jvp2_partial(
     const float* __restrict__ x, const float* __restrict__ u, const float* __restrict__ gy, int N,
     int C, const float* __restrict__ w, const float* __restrict__ b, const float* __restrict__ ms,
@@ -387,61 +372,46 @@ __global__ void __launch_bounds__(kBlock) k_gn_jvp2_partial(
 #pragma unroll
     for (int q = 0; q < 5; ++q) pp[q] = (s5[0][lane][q] + s5[1][lane][q]) + (s5[2][lane][q] + s5[3][lane][q]);
   }
-  if (counter && vg_last_block(counter))
-    for (int sl = 0; sl < (int)gridDim.y; ++sl)
-      jvp2_final_body(part, gridDim.x, N, C, w, ms, eps, stats, sums, g_w, g_ms, sl);
+  (void)counter;
+  (void)sums;
+  (void)g_w;
+  (void)g_ms;
 }
 
-// per column: mu' = mean u, M = mean(xt u), Sp, P1 = sum p c', P2 = sum p c;
-// g_w += P1/d - P2 M/(sigma d^2);  g_ms += w (-mu' Sp/d + mu Sp M/(sigma d^2))
-__device__ void jvp2_final_body(const float* __restrict__ part, int chunks, int N, int C,
-                                const float* __restrict__ w, const float* __restrict__ ms,
-                                float eps, const float* __restrict__ stats,
-                                float* __restrict__ sums, float* __restrict__ g_w,
-                                float* __restrict__ g_ms, int slab) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = slab * 64 + lane;
-  const int NW = blockDim.x >> 6;
-  float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-  if (c < C)
-    for (int k = wave; k < chunks; k += NW) {
-      const float* pp = part + ((size_t)k * C + c) * 5;
-#pragma unroll
-      for (int q = 0; q < 5; ++q) v[q] += pp[q];
-    }
-  __shared__ float red[16][64][5];
-#pragma unroll
-  for (int q = 0; q < 5; ++q) red[wave][lane][q] = v[q];
-  __syncthreads();
-  if (wave == 0 && c < C) {
-#pragma unroll
-    for (int q = 0; q < 5; ++q) {
-      v[q] = red[0][lane][q];
-      for (int k = 1; k < NW; ++k) v[q] += red[k][lane][q];
-    }
-    const float inv_n = 1.f / static_cast<float>(N);
-    const float mu = stats[c], sd = stats[C + c], d = sd + eps, msc = ms[c], wc = w[c];
-    const float mup = v[0] * inv_n, M = v[1] * inv_n, Sp = v[2];
-    const float P1 = v[3] - msc * mup * Sp;
-    const float P2 = v[4] + (1.f - msc) * mu * Sp;
-    const float isd = sd > 0.f ? 1.f / sd : 0.f;
-    float* sm = sums + (size_t)c * 5;
-    sm[0] = mup;
-    sm[1] = M;
-    sm[2] = Sp;
-    sm[3] = P1;
-    sm[4] = P2;
-    g_w[c] += P1 / d - P2 * M * isd / (d * d);
-    g_ms[c] += wc * (-mup * Sp / d + mu * Sp * M * isd / (d * d));
-  }
-  __syncthreads();
-}
-
-__global__ void __launch_bounds__(kFinalThreads) k_gn_jvp2_final(
+// one wave per column: mu' = mean u, M = mean(xt u), Sp, P1 = sum p c',
+// P2 = sum p c;  g_w += P1/d - P2 M/(sigma d^2);
+// g_ms += w (-mu' Sp/d + mu Sp M/(sigma d^2))
+__global__ void __launch_bounds__(kBlock) k_gn_jvp2_final(
     const float* __restrict__ part, int chunks, int N, int C, const float* __restrict__ w,
     const float* __restrict__ ms, float eps, const float* __restrict__ stats,
     float* __restrict__ sums, float* __restrict__ g_w, float* __restrict__ g_ms) {
-  jvp2_final_body(part, chunks, N, C, w, ms, eps, stats, sums, g_w, g_ms, blockIdx.x);
+  const int c = fold_col(), lane = threadIdx.x & 63;
+  if (c >= C) return;
+  float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  float t[4][5];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int k = lane + 64 * u;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) t[u][q] = k < chunks ? part[((size_t)k * C + c) * 5 + q] : 0.f;
+  }
+#pragma unroll
+  for (int q = 0; q < 5; ++q) v[q] = wave_sum((t[0][q] + t[1][q]) + (t[2][q] + t[3][q]));
+  if (lane != 0) return;
+  const float inv_n = 1.f / static_cast<float>(N);
+  const float mu = stats[c], sd = stats[C + c], d = sd + eps, msc = ms[c], wc = w[c];
+  const float mup = v[0] * inv_n, M = v[1] * inv_n, Sp = v[2];
+  const float P1 = v[3] - msc * mup * Sp;
+  const float P2 = v[4] + (1.f - msc) * mu * Sp;
+  const float isd = sd > 0.f ? 1.f / sd : 0.f;
+  float* sm = sums + (size_t)c * 5;
+  sm[0] = mup;
+  sm[1] = M;
+  sm[2] = Sp;
+  sm[3] = P1;
+  sm[4] = P2;
+  g_w[c] += P1 / d - P2 * M * isd / (d * d);
+  g_ms[c] += wc * (-mup * Sp / d + mu * Sp * M * isd / (d * d));
 }
 
 // u_out = keep [z>0] w (c'/d - c sigma'/d^2);  x_inj = dQ/dx
@@ -507,8 +477,9 @@ static int gn_fwd(const float* x, int32_t S, int32_t N, int32_t C, const float* 
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int chunks = chunks_for(N);
   dim3 grid(chunks, (C + 63) / 64, S);
-  k_stats_partial<<<grid, kBlock, 0, s>>>(x, N, C, ws, stats, sync);
-  if (!sync) k_stats_final<<<dim3(vg_blocks(C, 64), S), kFinalThreads, 0, s>>>(ws, chunks, C, stats);
+  k_stats_partial<<<grid, kBlock, 0, s>>>(x, N, C, ws, stats, nullptr);
+  (void)sync;  // former last-block-fold counter: accepted, unused
+  k_stats_final<<<vg_blocks(C, kBlock / 64), kBlock, 0, s>>>(ws, chunks, C, S, stats);
   const long long total = (long long)S * N * C;
   k_gn_apply<<<apply_blocks(total), 256, 0, s>>>(x, total, C, (long long)N * C, weight, bias,
                                                  mean_scale, keep, eps, stats, y, p_drop,
@@ -561,10 +532,10 @@ extern "C" int vg_graphnorm_bwd_seg(const float* x, int32_t S, int32_t N, int32_
   float* sums = ws + (size_t)S * kChunks * C * 5;
   dim3 grid(chunks, (C + 63) / 64, S);
   k_gn_bwd_partial<<<grid, kBlock, 0, s>>>(x, g_y, N, C, weight, bias, mean_scale, keep, eps,
-                                           stats, part, sums, g_w, g_b, g_ms, accumulate, sync);
-  if (!sync)
-    k_gn_bwd_final<<<vg_blocks(C, 64), kFinalThreads, 0, s>>>(part, chunks, C, S, weight, mean_scale, eps,
-                                                    stats, sums, g_w, g_b, g_ms, accumulate);
+                                           stats, part, sums, g_w, g_b, g_ms, accumulate, nullptr);
+  (void)sync;
+  k_gn_bwd_final<<<vg_blocks(C, kBlock / 64), kBlock, 0, s>>>(part, chunks, C, S, weight, mean_scale, eps,
+                                                              stats, sums, g_w, g_b, g_ms, accumulate);
   const long long total = (long long)S * N * C;
   k_gn_bwd_apply<<<apply_blocks(total), 256, 0, s>>>(x, g_y, total, N, C, weight, bias,
                                                      mean_scale, keep, eps, stats, sums, inj,
@@ -596,10 +567,10 @@ extern "C" int vg_graphnorm_jvp2(const float* x, int32_t N, int32_t C, const flo
   float* sums = ws + (size_t)kChunks * C * 5;
   dim3 grid(chunks, (C + 63) / 64);
   k_gn_jvp2_partial<<<grid, kBlock, 0, s>>>(x, u, g_y, N, C, weight, bias, mean_scale, keep, eps,
-                                            stats, part, sums, g_w, g_ms, sync);
-  if (!sync)
-    k_gn_jvp2_final<<<vg_blocks(C, 64), kFinalThreads, 0, s>>>(part, chunks, N, C, weight, mean_scale, eps,
-                                                     stats, sums, g_w, g_ms);
+                                            stats, part, sums, g_w, g_ms, nullptr);
+  (void)sync;
+  k_gn_jvp2_final<<<vg_blocks(C, kBlock / 64), kBlock, 0, s>>>(part, chunks, N, C, weight, mean_scale, eps,
+                                                               stats, sums, g_w, g_ms);
   const long long total = (long long)N * C;
   k_gn_jvp2_apply<<<apply_blocks(total), 256, 0, s>>>(x, u, g_y, total, N, C, weight, bias,
                                                       mean_scale, keep, eps, stats, sums, u_out,

@@ -37,8 +37,21 @@ def time_graph(g, reps: int) -> float:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--dump", default="", help="directory: write each phase graph as a DOT file (debug mode)")
+    ap.add_argument("--gaps", action="store_true",
+                    help="end with one replay of each phase 100 ms apart (split a rocprofv3 trace by phase)")
     args = ap.parse_args()
     from vgan.config import Configuration
+
+    if args.dump:  # every captured graph keeps its node list for debug_dump
+        os.makedirs(args.dump, exist_ok=True)
+        _orig_init = torch.cuda.CUDAGraph.__init__
+
+        def _init(self, *a, **k):
+            _orig_init(self, *a, **k)
+            self.enable_debug_mode()
+
+        torch.cuda.CUDAGraph.__init__ = _init
 
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -52,6 +65,10 @@ def main():
     tr.step_graphed(loc, vox)
     torch.cuda.synchronize()
     graphs = vox.derived("step_graphs")
+    if args.dump:
+        for name, g in (("labels", graphs["labels"]), ("critic", graphs["critic"][0]), ("gen", graphs["gen"])):
+            if g is not None:
+                g.debug_dump(os.path.join(args.dump, f"{name}.dot"))
     res = {}
     if graphs["labels"] is not None:
         res["labels_ms"] = time_graph(graphs["labels"], args.reps)
@@ -65,6 +82,17 @@ def main():
     en.record()
     torch.cuda.synchronize()
     res["step_ms"] = st.elapsed_time(en) / args.reps
+    if args.gaps:  # for a rocprofv3 kernel trace: one replay per phase, 100 ms apart
+        import time
+
+        for name in ("labels", "critic", "gen"):
+            g = graphs["critic"][0] if name == "critic" else graphs[name]
+            if g is None:
+                continue
+            torch.cuda.synchronize()
+            time.sleep(0.1)
+            g.replay()
+        torch.cuda.synchronize()
     print(json.dumps({k: round(v, 4) for k, v in res.items()}), flush=True)
 
 
