@@ -31,6 +31,15 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kChunks = 256;  // max row chunks per column slab (~64 rows each)
+constexpr int kFoldU = kChunks / 64;
+#ifndef VG_GN_CHUNK_ROWS
+#define VG_GN_CHUNK_ROWS 64
+#endif
+#ifndef VG_GN_APPLY_MAX
+#define VG_GN_APPLY_MAX 2048
+#endif
+constexpr int kChunkRows = VG_GN_CHUNK_ROWS;       // rows per statistics chunk
+constexpr int kApplyMaxBlocks = VG_GN_APPLY_MAX;  // elementwise grid cap  // chunk partials per lane in the one-wave folds
 
 struct Welford {
   float n, mean, m2;
@@ -141,16 +150,16 @@ __global__ void __launch_bounds__(kBlock) k_stats_final(const float* __restrict_
   if (c >= C) return;
   for (int sg = 0; sg < S; ++sg) {
     const float* pp = part + (size_t)sg * chunks * C * 3;
-    float v[4][3];
+    float v[kFoldU][3];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < kFoldU; ++u) {
       const int k = lane + 64 * u;
 #pragma unroll
       for (int q = 0; q < 3; ++q) v[u][q] = k < chunks ? pp[((size_t)k * C + c) * 3 + q] : 0.f;
     }
     Welford acc = {0.f, 0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc = merge(acc, Welford{v[u][0], v[u][1], v[u][2]});
+    for (int u = 0; u < kFoldU; ++u) acc = merge(acc, Welford{v[u][0], v[u][1], v[u][2]});
     acc = wave_merge(acc);
     if (lane == 0) {
       stats[(size_t)sg * 2 * C + c] = acc.mean;
@@ -266,15 +275,21 @@ __global__ void __launch_bounds__(kBlock) k_gn_bwd_final(
   float tw = 0.f, tb = 0.f, tm = 0.f;
   for (int sg = 0; sg < S; ++sg) {
     const float* pp = part + (size_t)sg * chunks * C * 2;
-    float va[4], vb[4];
+    float va[kFoldU], vb[kFoldU];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < kFoldU; ++u) {
       const int k = lane + 64 * u;
       va[u] = k < chunks ? pp[((size_t)k * C + c) * 2] : 0.f;
       vb[u] = k < chunks ? pp[((size_t)k * C + c) * 2 + 1] : 0.f;
     }
-    const float a = wave_sum((va[0] + va[1]) + (va[2] + va[3]));
-    const float bb = wave_sum((vb[0] + vb[1]) + (vb[2] + vb[3]));
+    float a = 0.f, bb = 0.f;
+#pragma unroll
+    for (int u = 0; u < kFoldU; ++u) {
+      a += va[u];
+      bb += vb[u];
+    }
+    a = wave_sum(a);
+    bb = wave_sum(bb);
     const float* st = stats + (size_t)sg * 2 * C;
     if (lane == 0) {
       sums[(size_t)sg * 2 * C + c] = a;
@@ -388,15 +403,19 @@ __global__ void __launch_bounds__(kBlock) k_gn_jvp2_final(
   const int c = fold_col(), lane = threadIdx.x & 63;
   if (c >= C) return;
   float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-  float t[4][5];
+  float t[kFoldU][5];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < kFoldU; ++u) {
     const int k = lane + 64 * u;
 #pragma unroll
     for (int q = 0; q < 5; ++q) t[u][q] = k < chunks ? part[((size_t)k * C + c) * 5 + q] : 0.f;
   }
 #pragma unroll
-  for (int q = 0; q < 5; ++q) v[q] = wave_sum((t[0][q] + t[1][q]) + (t[2][q] + t[3][q]));
+  for (int q = 0; q < 5; ++q) {
+#pragma unroll
+    for (int u = 0; u < kFoldU; ++u) v[q] += t[u][q];
+    v[q] = wave_sum(v[q]);
+  }
   if (lane != 0) return;
   const float inv_n = 1.f / static_cast<float>(N);
   const float mu = stats[c], sd = stats[C + c], d = sd + eps, msc = ms[c], wc = w[c];
@@ -449,13 +468,15 @@ __global__ void k_gn_jvp2_apply(const float* __restrict__ x, const float* __rest
 }  // namespace
 
 static inline int chunks_for(int N) {
-  const int c = (N + 63) / 64;
+  const int c = (N + kChunkRows - 1) / kChunkRows;
   return c < 1 ? 1 : (c > kChunks ? kChunks : c);
 }
 
+// elementwise passes: about one element per thread (every grid-stride
+// iteration is another dependent memory round trip)
 static inline int apply_blocks(long long total) {
   int blocks = vg_blocks(total, 256);
-  return blocks > 2048 ? 2048 : blocks;
+  return blocks > kApplyMaxBlocks ? kApplyMaxBlocks : blocks;
 }
 
 extern "C" int64_t vg_graphnorm_seg_ws_floats(int32_t segments, int32_t rows_per_segment,
