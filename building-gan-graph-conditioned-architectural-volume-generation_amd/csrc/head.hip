@@ -8,11 +8,16 @@ constexpr int kMaxClasses = 32;
 // models.py:150-153 -- F.gumbel_softmax(logits, tau=1.0) (hard=False):
 //   g = -log(E), E ~ Exp(1);  soft = softmax((logits + g) / tau)
 // then label_hard = onehot(argmax soft) - soft.detach() + soft.
+// tau_dev != NULL: row r uses tau_dev[r / seg_rows] (per-copy temperatures of a
+// stacked inference sweep, read from device memory so a replayed hipGraph
+// follows the schedule).
 __global__ void k_gumbel_fwd(const float* __restrict__ logits, const float* __restrict__ noise,
                              int rows, int K, float tau, float* __restrict__ soft,
-                             float* __restrict__ hard, int32_t* __restrict__ idx) {
+                             float* __restrict__ hard, int32_t* __restrict__ idx,
+                             const float* __restrict__ tau_dev = nullptr, int seg_rows = 1) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= rows) return;
+  if (tau_dev) tau = tau_dev[r / seg_rows];
   float y[kMaxClasses];
   float mx = -INFINITY;
   for (int k = 0; k < K; ++k) {
@@ -181,6 +186,18 @@ extern "C" int vg_gumbel_fwd(const float* logits, const float* noise, int32_t ro
     return VG_EINVAL;
   k_gumbel_fwd<<<vg_blocks(rows, 256), 256, 0, static_cast<hipStream_t>(stream)>>>(
       logits, noise, rows, classes, tau, soft, hard, idx);
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int vg_gumbel_fwd_dev(const float* logits, const float* noise, int32_t rows,
+                                 int32_t classes, const float* tau, int32_t seg_rows, float* soft,
+                                 float* hard, int32_t* idx, void* stream) {
+  if (rows <= 0 || classes <= 0 || classes > kMaxClasses || seg_rows <= 0 || !logits || !noise ||
+      !tau || !soft || !hard)
+    return VG_EINVAL;
+  k_gumbel_fwd<<<vg_blocks(rows, 256), 256, 0, static_cast<hipStream_t>(stream)>>>(
+      logits, noise, rows, classes, 1.f, soft, hard, idx, tau, seg_rows);
   VG_CHECK_LAUNCH();
   return 0;
 }

@@ -44,6 +44,7 @@ SIGNATURES = {
                                         _c_p, _c_p, _c_p, _c_p, _c_p]),
     "vg_type_mean": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_i32, _c_p, _c_p]),
     "vg_gumbel_fwd": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_f32, _c_p, _c_p, _c_p, _c_p]),
+    "vg_gumbel_fwd_dev": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_p, _c_p]),
     "vg_gumbel_bwd": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_i32, _c_i32, _c_f32, _c_p, _c_p]),
     "vg_far_per_graph": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32,
                                         _c_f32, _c_i32, _c_p, _c_p, _c_p]),

@@ -1,0 +1,115 @@
+"""Generator-only inference sweep (BASELINE.json configs[4]): many buildings,
+a Gumbel temperature schedule, hipGraph replay.
+
+The reference samples layouts in ``Trainer.test`` (``trainer.py:749-806``): per
+test batch one ``generator(local_graph, voxel_graph, z)`` forward in eval mode
+(``models.py:119-155``; ``F.gumbel_softmax`` at tau = 1) and argmax labels.
+``InferenceSweep`` runs that forward for a whole schedule of temperatures at
+once: one STACKED forward per batch over ``len(taus)`` copies (z [k, N, Z], each
+copy normalised on its own -- GraphNorm segments -- exactly as k separate
+forwards), and the Gumbel head reads copy c's temperature from a device
+vector (``vg_gumbel_fwd_dev``), so a captured hipGraph follows a new schedule
+without re-capture.  Per batch the result is the predicted type of every voxel
+for every temperature, [k, N] int8.
+
+``graphed=True`` captures the stacked forward of a batch on first use and
+replays it afterwards (the batch object caches its graph, as the training
+step does); a one-pass sweep over batches seen once runs eagerly.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Iterable, List, Optional, Sequence
+
+import torch
+
+from . import data as vdata
+
+
+def geometric_taus(t0: float = 1.0, t1: float = 0.1, steps: int = 10) -> List[float]:
+    """Annealing schedule tau_i = t0 (t1/t0)^(i/(steps-1)) (cfg #5)."""
+    if steps <= 1:
+        return [float(t0)]
+    r = math.log(t1 / t0) / (steps - 1)
+    return [float(t0 * math.exp(r * i)) for i in range(steps)]
+
+
+class InferenceSweep:
+    def __init__(self, generator, taus: Sequence[float], graphed: bool = False):
+        self.G = generator
+        self.taus = [float(t) for t in taus]
+        self.graphed = graphed
+        dev = next(generator.parameters()).device
+        self.tau_t = torch.tensor(self.taus, dtype=torch.float32, device=dev)
+        # one memory pool for every batch's graph: replays are sequential and
+        # only each graph's output stays referenced, so intermediates are shared
+        self._pool = torch.cuda.graph_pool_handle() if graphed else None
+
+    def set_taus(self, taus: Sequence[float]) -> None:
+        """New schedule of the same length: captured graphs keep working."""
+        if len(taus) != len(self.taus):
+            raise ValueError("a captured sweep keeps its number of temperatures")
+        self.taus = [float(t) for t in taus]
+        self.tau_t.copy_(torch.tensor(self.taus, dtype=torch.float32))
+
+    def _forward(self, local_graph, voxel_graph) -> torch.Tensor:
+        G = self.G
+        k = len(self.taus)
+        n = voxel_graph.num_nodes
+        z = G.rng.normal((k, n, G.configuration.Z_DIM), voxel_graph.x.device)
+        saved = G.tau
+        G.tau = self.tau_t
+        try:
+            _, hard, _ = G(local_graph, voxel_graph, z)
+        finally:
+            G.tau = saved
+        return hard.reshape(k, n, -1).argmax(-1).to(torch.int8)
+
+    @torch.no_grad()
+    def run_batch(self, local_graph, voxel_graph) -> torch.Tensor:
+        """[len(taus), N] int8 predicted voxel types (device tensor)."""
+        was = self.G.training
+        self.G.eval()
+        try:
+            vdata.prepared(local_graph, voxel_graph, self.G.configuration.NUM_CLASSES)
+            if not self.graphed:
+                return self._forward(local_graph, voxel_graph)
+            cached = voxel_graph.derived("sweep_graph")
+            if cached is None or cached[0] is not self:
+                dev = voxel_graph.x.device
+                side = torch.cuda.Stream(dev)
+                side.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(side):  # warm-up (lazy allocations) outside the capture
+                    self._forward(local_graph, voxel_graph)
+                torch.cuda.current_stream(dev).wait_stream(side)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self._pool):
+                    out = self._forward(local_graph, voxel_graph)
+                cached = (self, g, out)
+                voxel_graph.set_derived("sweep_graph", cached)
+            cached[1].replay()
+            return cached[2]
+        finally:
+            self.G.train(was)
+
+    def run(self, batches: Iterable, collect: bool = False) -> Dict[str, object]:
+        """Sweep every (local_graph, voxel_graph) batch; returns counts and,
+        with ``collect``, the per-batch [k, N] predictions (copied to the host
+        once at the end)."""
+        outs: List[torch.Tensor] = []
+        graphs = samples = 0
+        for local_graph, voxel_graph in batches:
+            pred = self.run_batch(local_graph, voxel_graph)
+            graphs += voxel_graph.num_graphs
+            samples += voxel_graph.num_graphs * len(self.taus)
+            if collect:
+                outs.append(pred.clone() if self.graphed else pred)
+        res: Dict[str, object] = {"graphs": graphs, "samples": samples}
+        if collect:
+            res["predictions"] = [o.cpu() for o in outs]
+        return res
+
+
+def sweep(generator, batches, taus: Optional[Sequence[float]] = None, graphed: bool = False,
+          collect: bool = False) -> Dict[str, object]:
+    return InferenceSweep(generator, taus or geometric_taus(), graphed).run(batches, collect)

@@ -556,8 +556,17 @@ class _GumbelHead(Function):
             raise ValueError("gumbel_head: logits and noise must be [N, K]")
         soft = torch.empty_like(lg)
         hard = torch.empty_like(lg)
-        check(LIB.vg_gumbel_fwd(ptr(lg), ptr(nz), lg.shape[0], lg.shape[1], float(tau), ptr(soft), ptr(hard), None,
-                                stream_handle(lg.device)), "vg_gumbel_fwd")
+        if isinstance(tau, torch.Tensor):  # per-copy temperatures on the device (inference sweep)
+            tt = _f32(tau.reshape(-1))
+            require_cuda(tt)
+            if lg.shape[0] % tt.numel():
+                raise ValueError("gumbel_head: rows must split evenly over the temperatures")
+            check(LIB.vg_gumbel_fwd_dev(ptr(lg), ptr(nz), lg.shape[0], lg.shape[1], ptr(tt), lg.shape[0] // tt.numel(),
+                                        ptr(soft), ptr(hard), None, stream_handle(lg.device)), "vg_gumbel_fwd_dev")
+            ctx.mark_non_differentiable(hard, soft)  # inference only
+        else:
+            check(LIB.vg_gumbel_fwd(ptr(lg), ptr(nz), lg.shape[0], lg.shape[1], float(tau), ptr(soft), ptr(hard),
+                                    None, stream_handle(lg.device)), "vg_gumbel_fwd")
         ctx.tau = tau
         ctx.save_for_backward(soft)
         ctx.set_materialize_grads(False)  # an unused output's gradient stays None (no zero fill launch)

@@ -271,6 +271,13 @@ int vg_type_mean(const float* local_x, const int64_t* local_type, int32_t n_loca
 int vg_gumbel_fwd(const float* logits, const float* noise, int32_t rows, int32_t classes,
                   float tau, float* soft, float* hard, int32_t* idx, void* stream);
 
+/* vg_gumbel_fwd with the temperature read from device memory: row r uses
+ * tau[r / seg_rows] (a stacked inference sweep over a tau schedule, one copy of
+ * the batch per temperature; a replayed hipGraph follows updates of tau). */
+int vg_gumbel_fwd_dev(const float* logits, const float* noise, int32_t rows, int32_t classes,
+                      const float* tau, int32_t seg_rows, float* soft, float* hard, int32_t* idx,
+                      void* stream);
+
 /* g_logits = soft * (g - sum(soft*g)) / tau with g = g_hard + g_soft (either NULL = 0). */
 int vg_gumbel_bwd(const float* soft, const float* g_hard, const float* g_soft, int32_t rows,
                   int32_t classes, float tau, float* g_logits, void* stream);

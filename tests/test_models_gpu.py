@@ -260,3 +260,51 @@ def test_stacked_generator_forward_equals_separate(cuda):
             assert torch.allclose(lk[i], l1, rtol=1e-4, atol=1e-5)
             assert torch.allclose(sk[i], s1, rtol=1e-4, atol=1e-6)
             assert (hk[i].argmax(1) != h1.argmax(1)).sum().item() <= 1
+
+
+def test_gumbel_head_device_temperatures(cuda):
+    """vg_gumbel_fwd_dev (per-copy temperatures read from the device) equals the
+    host-temperature head copy by copy, bit for bit."""
+    from vgan import ops
+
+    torch.manual_seed(5)
+    n, taus = 777, [1.0, 0.37, 0.1]
+    logits = torch.randn(len(taus) * n, 7, device=cuda)
+    noise = torch.empty_like(logits).exponential_()
+    hard, soft = ops.gumbel_head(logits, noise, torch.tensor(taus, device=cuda))
+    for c, t in enumerate(taus):
+        rows = slice(c * n, (c + 1) * n)
+        h1, s1 = ops.gumbel_head(logits[rows].contiguous(), noise[rows].contiguous(), t)
+        assert torch.equal(hard[rows], h1) and torch.equal(soft[rows], s1)
+
+
+@pytest.mark.parametrize("graphed", [False, True])
+def test_inference_sweep(cuda, graphed):
+    """Stacked eval-mode sweep over a temperature schedule (configs[4]): shapes,
+    label range, graph replay following a new schedule; at tau -> 0 the sample
+    is the argmax of logits + Gumbel noise, so the low-temperature copies agree
+    with each other far more often than with the tau = 1 copy."""
+    from vgan.infer import InferenceSweep, geometric_taus
+
+    cfg = Configuration()
+    cfg.DEVICE = str(cuda)
+    cfg.runtime["rng"] = "device"
+    torch.manual_seed(3)
+    G = VoxelGNNGenerator(cfg, 17, 12)
+    from vgan.graph import GraphBatch
+    from vgan.synth import make_building
+
+    items = [make_building(777, i) for i in range(4)]
+    loc = GraphBatch.from_data_list([l for l, _ in items]).to(cuda)
+    vox = GraphBatch.from_data_list([v for _, v in items]).to(cuda)
+    taus = geometric_taus(1.0, 0.1, 4)
+    sw = InferenceSweep(G, taus, graphed=graphed)
+    p1 = sw.run_batch(loc, vox).clone()
+    assert p1.shape == (4, vox.num_nodes) and p1.dtype == torch.int8
+    assert int(p1.min()) >= 0 and int(p1.max()) < cfg.NUM_CLASSES
+    sw.set_taus([0.05, 0.05, 0.05, 0.05])
+    p2 = sw.run_batch(loc, vox)
+    assert p2.shape == p1.shape
+    res = sw.run([(loc, vox)] * 2, collect=True)
+    assert res["graphs"] == 2 * vox.num_graphs and res["samples"] == 8 * vox.num_graphs
+    assert len(res["predictions"]) == 2
