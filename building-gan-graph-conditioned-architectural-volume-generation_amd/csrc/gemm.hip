@@ -30,6 +30,10 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int TM = 64, TN = 64, TK = 32, LDP = TK + 1;
+#ifndef VG_TN_GROUPS
+#define VG_TN_GROUPS 2
+#endif
+constexpr int kTnGroups = VG_TN_GROUPS;  // row groups (of 4 waves) per split-K workgroup
 
 template <int ACT>
 __device__ __forceinline__ float act_fn(float v, float aux) {
@@ -160,14 +164,20 @@ __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int l
 
 // part[chunk][M][K] = A[chunk rows]^T . B[chunk rows];  pdb[chunk][M] = column sums of A.
 // `rows` rows of the N reduction per chunk (a multiple of TK), pipelined like k_gemm.
-__global__ void __launch_bounds__(256) k_gemm_tn(const float* __restrict__ A, int lda,
-                                                 const float* __restrict__ B, int ldb, int N,
-                                                 int M, int K, int rows, float* __restrict__ part,
-                                                 float* __restrict__ pdb, int db_rows) {
-  __shared__ float As[2][TK][TM + 1];  // As[n][m]
-  __shared__ float Bs[2][TK][TN + 1];  // Bs[n][k]
+// G row groups of 4 waves per workgroup: group g takes the chunk's K-steps
+// g, g+G, ... into its own LDS buffers (two waves per SIMD for G = 2, so one
+// group's MFMAs cover the other's loads -- the f32 MFMA alone is 1024 cycles
+// per 32-row step), and the groups' accumulators are added in group order at
+// the end (deterministic).
+template <int G>
+__global__ void __launch_bounds__(256 * G) k_gemm_tn(const float* __restrict__ A, int lda,
+                                                     const float* __restrict__ B, int ldb, int N,
+                                                     int M, int K, int rows, float* __restrict__ part,
+                                                     float* __restrict__ pdb, int db_rows) {
+  __shared__ float As[G][2][TK][TM + 1];  // As[g][buf][n][m]
+  __shared__ float Bs[G][2][TK][TN + 1];  // Bs[g][buf][n][k]
   constexpr int PER = (TK * TM) / 256;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int grp = threadIdx.x >> 8, t = threadIdx.x & 255, lane = t & 63, wave = t >> 6;
   const int wr = wave >> 1, wc = wave & 1;
   // XCD-aware: each XCD takes a contiguous range of row chunks (tile_xy)
   const int gxy = gridDim.x * gridDim.y;
@@ -176,42 +186,61 @@ __global__ void __launch_bounds__(256) k_gemm_tn(const float* __restrict__ A, in
   const int chunk = logical / gxy, rem = logical % gxy;
   const int m0 = (rem % gridDim.x) * TM, k0 = (rem / gridDim.x) * TN;
   const int nb = chunk * rows, ne = min(N, nb + rows);
+  const int steps = ne > nb ? (ne - nb + TK - 1) / TK : 0;
+  const int iters = (steps + G - 1) / G;
   const bool do_db = pdb && k0 == 0;
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   float dbs = 0.f;
   float ra[PER], rb[PER];
-  auto load = [&](int n1) {
+  auto load = [&](int st) {
+    const int n1 = nb + st * TK;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
       const int e = t + 256 * q;
       const int r = e / TM, c = e % TM;
       const int n = n1 + r;
-      ra[q] = (n < ne && m0 + c < M) ? A[(size_t)n * lda + m0 + c] : 0.f;
-      rb[q] = (n < ne && k0 + c < K) ? B[(size_t)n * ldb + k0 + c] : 0.f;
+      const bool in = st < steps && n < ne;
+      ra[q] = (in && m0 + c < M) ? A[(size_t)n * lda + m0 + c] : 0.f;
+      rb[q] = (in && k0 + c < K) ? B[(size_t)n * ldb + k0 + c] : 0.f;
     }
   };
-  load(nb);
+  load(grp);
   int buf = 0;
-  for (int n1 = nb; n1 < ne; n1 += TK) {
+  for (int it = 0, st = grp; it < iters; ++it, st += G) {
+    const int n1 = nb + st * TK;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
       const int e = t + 256 * q;
-      As[buf][e / TM][e % TM] = ra[q];
-      Bs[buf][e / TM][e % TM] = rb[q];
-      if (do_db && n1 + e / TM < db_rows) dbs += ra[q];  // column (t & 63), rows e / TM
+      As[grp][buf][e / TM][e % TM] = ra[q];
+      Bs[grp][buf][e / TM][e % TM] = rb[q];
+      if (do_db && n1 + e / TM < db_rows) dbs += ra[q];  // column (t & 63), rows e / TM (0 past ne)
     }
     __syncthreads();
-    if (n1 + TK < ne) load(n1 + TK);
+    load(st + G);
+    if (st < steps) {
 #pragma unroll
-    for (int kk = 0; kk < TK; kk += 2) {
-      const float a = As[buf][kk + (lane >> 5)][wr * 32 + (lane & 31)];
-      const float b = Bs[buf][kk + (lane >> 5)][wc * 32 + (lane & 31)];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+      for (int kk = 0; kk < TK; kk += 2) {
+        const float a = As[grp][buf][kk + (lane >> 5)][wr * 32 + (lane & 31)];
+        const float b = Bs[grp][buf][kk + (lane >> 5)][wc * 32 + (lane & 31)];
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+      }
     }
     buf ^= 1;
   }
+  float* sh = &As[0][0][0][0];  // G * 2 * TK * (TM + 1) >= (G - 1) * 4096 floats
+  __shared__ float red[G * 4][64];
+  __syncthreads();
+  if (grp > 0)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sh[(((grp - 1) * 4 + wave) * 16 + r) * 64 + lane] = acc[r];
+  red[grp * 4 + wave][lane] = dbs;
+  __syncthreads();
+  if (grp != 0) return;
+  for (int g = 1; g < G; ++g)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] += sh[(((g - 1) * 4 + wave) * 16 + r) * 64 + lane];
   const int k = k0 + wc * 32 + (lane & 31);
   float* out = part + (size_t)chunk * M * K;
 #pragma unroll
@@ -219,12 +248,10 @@ __global__ void __launch_bounds__(256) k_gemm_tn(const float* __restrict__ A, in
     const int m = m0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
     if (m < M && k < K) out[(size_t)m * K + k] = acc[r];
   }
-  if (do_db) {
-    __shared__ float red[4][64];
-    red[t >> 6][t & 63] = dbs;
-    __syncthreads();
-    if (t < 64 && m0 + t < M)
-      pdb[(size_t)chunk * M + m0 + t] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+  if (do_db && t < 64 && m0 + t < M) {
+    float v = 0.f;
+    for (int w = 0; w < G * 4; ++w) v += red[w][t];
+    pdb[(size_t)chunk * M + m0 + t] = v;
   }
 }
 
@@ -333,7 +360,7 @@ static int gemm_tn(const float* A, int32_t lda, const float* B, int32_t ldb, int
   float* part = workspace;
   float* pdb = workspace + (size_t)chunks * M * K;
   dim3 grid((M + TM - 1) / TM, (K + TN - 1) / TN, chunks);
-  k_gemm_tn<<<grid, 256, 0, s>>>(A, lda, B, ldb, N, M, K, rows, part, db ? pdb : nullptr,
+  k_gemm_tn<kTnGroups><<<grid, 256 * kTnGroups, 0, s>>>(A, lda, B, ldb, N, M, K, rows, part, db ? pdb : nullptr,
                                  db_rows < N ? db_rows : N);
   const long long W = (long long)M * K;
   const int nb1 = (int)((W + 63) / 64), nb2 = db ? (M + 63) / 64 : 0;

@@ -12,7 +12,8 @@ from typing import Optional
 
 import torch
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvgan_hip.so")
+# VGAN_LIB: an alternative build of the same ABI (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("VGAN_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvgan_hip.so")
 VG_EINVAL = -1
 
 _c_i32, _c_i64, _c_f32, _c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
