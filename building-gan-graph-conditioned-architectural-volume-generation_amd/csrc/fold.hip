@@ -1,0 +1,87 @@
+// Deferred parameter-gradient folds: one launch for every split-K / per-block
+// partial set of a whole backward.
+//
+// The weight-gradient GEMMs (vg_gemm_tn) and the GAT backward / second-order
+// kernels (vg_gat_bwd_ex, vg_gat_jvp2_ex) reduce their parameter gradients in
+// two steps: per-workgroup partial rows, then a fold launch over those rows.
+// The folded values are needed only by the optimizer step, so the *_deferred
+// entry points skip the fold and describe it instead (vg_fold: destination,
+// shape, up to two partial sources); vg_fold_batch then runs every fold of a
+// critic iteration or of the generator backward in ONE launch -- about 24
+// launches fewer per critic iteration.  The descriptors travel by value in the
+// kernel arguments (no host-to-device copy, capturable in a hipGraph).
+//
+// Summation order is that of the immediate folds, so results are bit-identical:
+// per source, 16 waves stride the partial rows with four accumulators combined
+// as (a0 + a1) + (a2 + a3), the waves are added in order, and the destination
+// becomes (out + source 0) + source 1.
+#include "common.h"
+
+namespace {
+
+struct FoldBatch {
+  int32_t n;
+  int32_t block0[VG_FOLD_MAX + 1];  // first workgroup of fold i; block0[n] = grid size
+  vg_fold f[VG_FOLD_MAX];
+};
+
+__device__ __forceinline__ float fold_rows_sum(const float* __restrict__ part, int rows, int ld,
+                                               long long w, int wave) {
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int r = wave;
+  for (; r + 48 < rows; r += 64) {
+    a0 += part[(size_t)r * ld + w];
+    a1 += part[(size_t)(r + 16) * ld + w];
+    a2 += part[(size_t)(r + 32) * ld + w];
+    a3 += part[(size_t)(r + 48) * ld + w];
+  }
+  for (; r < rows; r += 16) a0 += part[(size_t)r * ld + w];
+  return (a0 + a1) + (a2 + a3);
+}
+
+__global__ void __launch_bounds__(1024) k_fold_batch(const FoldBatch b) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int d = 0;
+  while (d + 1 < b.n && (int)blockIdx.x >= b.block0[d + 1]) ++d;
+  const vg_fold& f = b.f[d];
+  const long long w = (long long)(blockIdx.x - b.block0[d]) * 64 + lane;
+  __shared__ float red[2][16][64];
+  for (int si = 0; si < f.nsrc; ++si)
+    red[si][wave][lane] = w < f.width ? fold_rows_sum(f.src[si].part, f.src[si].rows, f.src[si].ld, w, wave)
+                                      : 0.f;
+  __syncthreads();
+  if (wave == 0 && w < f.width) {
+    float* o = f.out + (w / f.k) * f.ldo + (w % f.k);
+    float v = f.accumulate ? *o : 0.f;
+    for (int si = 0; si < f.nsrc; ++si) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) s += red[si][k][lane];
+      v = f.accumulate || si > 0 ? v + s : s;
+    }
+    *o = v;
+  }
+}
+
+}  // namespace
+
+extern "C" int vg_fold_batch(const vg_fold* folds, int32_t n, void* stream) {
+  if (n < 0 || n > VG_FOLD_MAX || (n > 0 && !folds)) return VG_EINVAL;
+  if (n == 0) return 0;
+  FoldBatch b;
+  b.n = n;
+  int blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    const vg_fold& f = folds[i];
+    if (!f.out || f.width <= 0 || f.k <= 0 || f.ldo < f.k || f.nsrc < 1 || f.nsrc > 2) return VG_EINVAL;
+    for (int s = 0; s < f.nsrc; ++s)
+      if (!f.src[s].part || f.src[s].rows < 0 || f.src[s].ld < f.width) return VG_EINVAL;
+    b.f[i] = f;
+    b.block0[i] = blocks;
+    blocks += (f.width + 63) / 64;
+  }
+  b.block0[n] = blocks;
+  k_fold_batch<<<blocks, 1024, 0, static_cast<hipStream_t>(stream)>>>(b);
+  VG_CHECK_LAUNCH();
+  return 0;
+}

@@ -742,13 +742,14 @@ extern "C" int vg_gat_aggregate_fwd(const int32_t* row_ptr, const int32_t* col, 
   return 0;
 }
 
-extern "C" int vg_gat_bwd_ex(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,
-                             const int32_t* csc_slot, const int32_t* csc_dst, int32_t N, int32_t E,
-                             int32_t C, const float* h, const float* att_src, const float* att_dst,
-                             const float* a_src, const float* a_dst, const float* alpha,
-                             const float* g_out, float slope, float* g_h, float* g_att_src,
-                             float* g_att_dst, float* g_bias, int32_t accumulate, const float* inj,
-                             int32_t inj_row0, float* workspace, void* stream) {
+static int gat_bwd(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,
+                   const int32_t* csc_slot, const int32_t* csc_dst, int32_t N, int32_t E, int32_t C,
+                   const float* h, const float* att_src, const float* att_dst, const float* a_src,
+                   const float* a_dst, const float* alpha, const float* g_out, float slope,
+                   float* g_h, float* g_att_src, float* g_att_dst, float* g_bias,
+                   int32_t accumulate, const float* inj, int32_t inj_row0, float* workspace,
+                   void* stream, vg_fold* defer, int32_t* n_defer) {
+  if (n_defer) *n_defer = 0;
   const bool pgrads = g_att_src != nullptr;
   if (N <= 0 || E <= 0 || !row_ptr || !col || !csc_ptr || !csc_slot || !csc_dst || !h ||
       !att_src || !att_dst || !a_src || !a_dst || !alpha || !g_out || !g_h || !workspace ||
@@ -786,7 +787,12 @@ extern "C" int vg_gat_bwd_ex(const int32_t* row_ptr, const int32_t* col, const i
                              csc_ptr, csc_slot, csc_dst, N, C, h, att_src, att_dst, alpha, g_out,
                              g_pre, g_ad, inj, inj_row0, g_h, part2)));
   }
-  if (pgrads) {
+  if (pgrads && defer) {  // described for vg_fold_batch: part1 -> [g_bias | g_att_dst], part2 -> g_att_src
+    defer[0] = vg_fold{g_bias, C, C, C, accumulate, 1, {{part1, grid1, 2 * C}, {nullptr, 0, 0}}};
+    defer[1] = vg_fold{g_att_dst, C, C, C, accumulate, 1, {{part1 + C, grid1, 2 * C}, {nullptr, 0, 0}}};
+    defer[2] = vg_fold{g_att_src, C, C, C, accumulate, 1, {{part2, grid2, C}, {nullptr, 0, 0}}};
+    *n_defer = 3;
+  } else if (pgrads) {
     // fold: part1 rows -> [g_bias | g_att_dst], part2 rows -> g_att_src
     k_fold_cols<<<dim3(vg_blocks(2 * C, 64), 2), 1024, 0, s>>>(part1, grid1, 2 * C, C, accumulate,
                                                                g_bias, g_att_dst, part2, grid2, C,
@@ -794,6 +800,33 @@ extern "C" int vg_gat_bwd_ex(const int32_t* row_ptr, const int32_t* col, const i
   }
   VG_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int vg_gat_bwd_ex(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,
+                             const int32_t* csc_slot, const int32_t* csc_dst, int32_t N, int32_t E,
+                             int32_t C, const float* h, const float* att_src, const float* att_dst,
+                             const float* a_src, const float* a_dst, const float* alpha,
+                             const float* g_out, float slope, float* g_h, float* g_att_src,
+                             float* g_att_dst, float* g_bias, int32_t accumulate, const float* inj,
+                             int32_t inj_row0, float* workspace, void* stream) {
+  return gat_bwd(row_ptr, col, csc_ptr, csc_slot, csc_dst, N, E, C, h, att_src, att_dst, a_src,
+                 a_dst, alpha, g_out, slope, g_h, g_att_src, g_att_dst, g_bias, accumulate, inj,
+                 inj_row0, workspace, stream, nullptr, nullptr);
+}
+
+extern "C" int vg_gat_bwd_deferred(const int32_t* row_ptr, const int32_t* col,
+                                   const int32_t* csc_ptr, const int32_t* csc_slot,
+                                   const int32_t* csc_dst, int32_t N, int32_t E, int32_t C,
+                                   const float* h, const float* att_src, const float* att_dst,
+                                   const float* a_src, const float* a_dst, const float* alpha,
+                                   const float* g_out, float slope, float* g_h, float* g_att_src,
+                                   float* g_att_dst, float* g_bias, int32_t accumulate,
+                                   const float* inj, int32_t inj_row0, float* workspace,
+                                   vg_fold* folds_out, int32_t* n_out, void* stream) {
+  if (!folds_out || !n_out) return VG_EINVAL;
+  return gat_bwd(row_ptr, col, csc_ptr, csc_slot, csc_dst, N, E, C, h, att_src, att_dst, a_src,
+                 a_dst, alpha, g_out, slope, g_h, g_att_src, g_att_dst, g_bias, accumulate, inj,
+                 inj_row0, workspace, stream, folds_out, n_out);
 }
 
 extern "C" int vg_gat_bwd(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,

@@ -279,6 +279,25 @@ extern "C" int vg_gat_jvp2_ex(const int32_t* row_ptr, const int32_t* col, const 
                               float* h_inj, float* g_att_src, float* g_att_dst,
                               const float* up_src_in, const float* up_dst_in, float* workspace,
                               void* stream) {
+  return vg_gat_jvp2_deferred(row_ptr, col, csc_ptr, csc_slot, csc_dst, N, E, C, h, u, g_out,
+                              att_src, att_dst, a_src, a_dst, alpha, slope, u_out, h_inj, g_att_src,
+                              g_att_dst, up_src_in, up_dst_in, workspace, nullptr, nullptr, stream);
+}
+
+// folds_out == NULL: fold immediately (vg_gat_jvp2_ex); else describe the two
+// accumulating folds for vg_fold_batch.
+extern "C" int vg_gat_jvp2_deferred(const int32_t* row_ptr, const int32_t* col,
+                                    const int32_t* csc_ptr, const int32_t* csc_slot,
+                                    const int32_t* csc_dst, int32_t N, int32_t E, int32_t C,
+                                    const float* h, const float* u, const float* g_out,
+                                    const float* att_src, const float* att_dst, const float* a_src,
+                                    const float* a_dst, const float* alpha, float slope,
+                                    float* u_out, float* h_inj, float* g_att_src, float* g_att_dst,
+                                    const float* up_src_in, const float* up_dst_in,
+                                    float* workspace, vg_fold* folds_out, int32_t* n_out,
+                                    void* stream) {
+  if ((folds_out == nullptr) != (n_out == nullptr)) return VG_EINVAL;
+  if (n_out) *n_out = 0;
   Shape sh;
   if (N <= 0 || E <= 0 || !row_ptr || !col || !csc_ptr || !csc_slot || !csc_dst || !h || !u ||
       !g_out || !att_src || !att_dst || !a_src || !a_dst || !alpha || !u_out || !h_inj ||
@@ -309,8 +328,14 @@ extern "C" int vg_gat_jvp2_ex(const int32_t* row_ptr, const int32_t* col, const 
   VG_DISPATCH_JVP(C, (k_jvp_src<L_, CPL_, V_><<<grid, kBlock, 0, s>>>(
                          csc_ptr, csc_slot, csc_dst, N, C, h, u, g_out, att_src, att_dst, e_gz,
                          e_gzp, e_alp, n_gad, h_inj, part_s)));
-  k_fold_add2<<<dim3(vg_blocks(C, 64), 2), 1024, 0, s>>>(part_r, grid, part_s, grid, C, g_att_dst,
-                                                         g_att_src);
+  if (folds_out) {
+    folds_out[0] = vg_fold{g_att_dst, C, C, C, 1, 1, {{part_r, grid, C}, {nullptr, 0, 0}}};
+    folds_out[1] = vg_fold{g_att_src, C, C, C, 1, 1, {{part_s, grid, C}, {nullptr, 0, 0}}};
+    *n_out = 2;
+  } else {
+    k_fold_add2<<<dim3(vg_blocks(C, 64), 2), 1024, 0, s>>>(part_r, grid, part_s, grid, C,
+                                                           g_att_dst, g_att_src);
+  }
   VG_CHECK_LAUNCH();
   return 0;
 }

@@ -344,7 +344,9 @@ extern "C" int64_t vg_gemm_tn_ws_floats(int32_t N, int32_t M, int32_t K) {
 
 static int gemm_tn(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N, int32_t M,
                    int32_t K, float* C, int32_t ldc, float* db, int32_t db_rows,
-                   int32_t accumulate, float* workspace, void* stream) {
+                   int32_t accumulate, float* workspace, void* stream, vg_fold* defer = nullptr,
+                   int32_t* n_defer = nullptr) {
+  if (n_defer) *n_defer = 0;
   if (N < 0 || M <= 0 || K <= 0 || ldc < K || !A || !B || !C || !workspace || db_rows < 0)
     return VG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -363,10 +365,30 @@ static int gemm_tn(const float* A, int32_t lda, const float* B, int32_t ldb, int
   k_gemm_tn<kTnGroups><<<grid, 256 * kTnGroups, 0, s>>>(A, lda, B, ldb, N, M, K, rows, part, db ? pdb : nullptr,
                                  db_rows < N ? db_rows : N);
   const long long W = (long long)M * K;
+  if (defer) {  // describe the fold(s) for vg_fold_batch instead of launching them
+    defer[0] = vg_fold{C, (int32_t)W, K, ldc, accumulate, 1, {{part, chunks, (int32_t)W}, {nullptr, 0, 0}}};
+    *n_defer = 1;
+    if (db) {
+      defer[1] = vg_fold{db, M, M, M, accumulate, 1, {{pdb, chunks, M}, {nullptr, 0, 0}}};
+      *n_defer = 2;
+    }
+    VG_CHECK_LAUNCH();
+    return 0;
+  }
   const int nb1 = (int)((W + 63) / 64), nb2 = db ? (M + 63) / 64 : 0;
   k_fold_rows<<<nb1 + nb2, 1024, 0, s>>>(part, chunks, W, K, ldc, accumulate, C, nb1, pdb, M, db);
   VG_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int vg_gemm_tn_deferred(const float* A, int32_t lda, const float* B, int32_t ldb,
+                                   int32_t N, int32_t M, int32_t K, float* C, int32_t ldc,
+                                   float* db, int32_t db_rows, int32_t accumulate,
+                                   float* workspace, vg_fold* folds_out, int32_t* n_out,
+                                   void* stream) {
+  if (!folds_out || !n_out || N <= 0) return VG_EINVAL;
+  return gemm_tn(A, lda, B, ldb, N, M, K, C, ldc, db, db_rows, accumulate, workspace, stream,
+                 folds_out, n_out);
 }
 
 extern "C" int vg_gat_lin_att(const float* X, int32_t ldx, const float* W, int32_t N,

@@ -18,8 +18,32 @@ VG_EINVAL = -1
 
 _c_i32, _c_i64, _c_f32, _c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 
+
+
+class VgFoldSrc(ctypes.Structure):
+    """vg_fold_src (include/vgan.h)."""
+    _fields_ = [("part", _c_p), ("rows", _c_i32), ("ld", _c_i32)]
+
+
+class VgFold(ctypes.Structure):
+    """vg_fold (include/vgan.h): one deferred parameter-gradient fold."""
+    _fields_ = [("out", _c_p), ("width", _c_i32), ("k", _c_i32), ("ldo", _c_i32), ("accumulate", _c_i32),
+                ("nsrc", _c_i32), ("src", VgFoldSrc * 2)]
+
+
+VG_FOLD_MAX = 40
+
 # name -> (restype, argtypes); every function listed here is declared in include/vgan.h
 SIGNATURES = {
+    "vg_fold_batch": (ctypes.c_int, [_c_p, _c_i32, _c_p]),
+    "vg_gemm_tn_deferred": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_i32, _c_p,
+                                           _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p]),
+    "vg_gat_bwd_deferred": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p,
+                                           _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p,
+                                           _c_i32, _c_p, _c_p, _c_p, _c_p]),
+    "vg_gat_jvp2_deferred": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p,
+                                            _c_p, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
+                                            _c_p, _c_p, _c_p, _c_p]),
     "vg_csr_ws_ints": (_c_i64, [_c_i64, _c_i32]),
     "vg_csr_build": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "vg_gat_fwd": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p,
@@ -149,3 +173,47 @@ def require_cuda(*tensors: Optional[torch.Tensor]) -> None:
             raise RuntimeError("vgan HIP ops require tensors on a ROCm device (no CPU fallback)")
         if not t.is_contiguous():
             raise RuntimeError("vgan HIP ops require contiguous tensors")
+
+
+class FoldCollector:
+    """Collects the parameter-gradient folds of one backward (the *_deferred
+    ABI calls) and runs them in as few vg_fold_batch launches as possible.
+    Folds into the same destination merge into one two-source fold, applied
+    in call order ((out + first) + second, as the immediate folds would); the
+    partial workspaces are kept alive until the batch is enqueued."""
+
+    def __init__(self):
+        self.folds = []
+        self.keep = []
+
+    def call(self, fn, args_before_stream, stream, keep=(), name="deferred"):
+        arr = (VgFold * 3)()
+        n = ctypes.c_int32(0)
+        check(fn(*args_before_stream, arr, ctypes.byref(n), stream), name)
+        for i in range(n.value):
+            self.folds.append(VgFold.from_buffer_copy(arr[i]))
+        self.keep.extend(keep)
+
+    def flush(self, stream) -> None:
+        batches, cur, where = [], [], {}
+        for f in self.folds:
+            j = where.get(f.out)
+            if j is not None:
+                g = cur[j]
+                if (g.nsrc == 1 and f.nsrc == 1 and f.accumulate and (g.width, g.k, g.ldo) == (f.width, f.k, f.ldo)):
+                    g.src[1] = f.src[0]
+                    g.nsrc = 2
+                    continue
+                batches.append(cur)  # cannot merge: later batch, so the two never race
+                cur, where = [], {}
+            if len(cur) == VG_FOLD_MAX:
+                batches.append(cur)
+                cur, where = [], {}
+            where[f.out] = len(cur)
+            cur.append(f)
+        if cur:
+            batches.append(cur)
+        for b in batches:
+            arr = (VgFold * len(b))(*b)
+            check(LIB.vg_fold_batch(arr, len(b), stream), "vg_fold_batch")
+        self.folds, self.keep = [], []

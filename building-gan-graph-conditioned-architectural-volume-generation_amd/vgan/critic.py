@@ -37,7 +37,7 @@ import torch
 import torch.nn as nn
 
 from . import data as vdata
-from ._lib import LIB, check, ptr, stream_handle, sync_counter
+from ._lib import LIB, FoldCollector, check, ptr, stream_handle, sync_counter
 
 ACT_NONE, ACT_RELU, ACT_MASK = 0, 1, 3
 
@@ -96,10 +96,11 @@ class CriticEngine:
         check(LIB.vg_gemm(A, lda, B, ldb, bt, bias, act, aux, ldaux, C, ldc, n, m, k, st), "vg_gemm")
 
     @staticmethod
-    def _gemm_tn(st, dev, A, lda, B, ldb, n, m, k, C, ldc, db=None, db_rows=None):
+    def _gemm_tn(folds, st, dev, A, lda, B, ldb, n, m, k, C, ldc, db=None, db_rows=None):
+        """Split-K weight gradient; its fold joins the iteration's batched folds."""
         ws = _f(max(1, int(LIB.vg_gemm_tn_ws_floats(n, m, k))), dev=dev)
-        check(LIB.vg_gemm_tn_ex(A, lda, B, ldb, n, m, k, C, ldc, db, n if db_rows is None else db_rows, 1, ptr(ws),
-                                st), "vg_gemm_tn_ex")
+        folds.call(LIB.vg_gemm_tn_deferred, (A, lda, B, ldb, n, m, k, C, ldc, db, n if db_rows is None else db_rows,
+                                             1, ptr(ws)), st, keep=(ws,), name="vg_gemm_tn_deferred")
 
     # ------------------------------------------------------------ engine
     def loss_and_grad(self, local_graph, voxel_graph, label_hard, label_soft, rng) -> torch.Tensor:
@@ -136,6 +137,8 @@ class CriticEngine:
         keeps, eps = self._keeps(rng, n, dev, D.training)
         eps = eps.reshape(n).contiguous()
         nb, nd, nm = len(self.blocks), len(self.dec), len(self.mlp)
+        # parameter-gradient folds of passes C and D, run as one batch at the end
+        folds = FoldCollector()
         mrow, trow = 2 * n, 3 * n  # first row of the mix copy / of the tangent (or pass-B) rows
 
         def rows(t: torch.Tensor, r0: int, width: int):
@@ -278,12 +281,13 @@ class CriticEngine:
                                      ptr(conv.att_dst), ptr(uH), ptr(up_s), ptr(up_d), st), "vg_gat_lin_att")
             uO, hinj = _f(n, c, dev=dev), _f(n, c, dev=dev)
             ws = _f(int(LIB.vg_gat_jvp2_ws_floats(n, E, c)), dev=dev)
-            check(LIB.vg_gat_jvp2_ex(ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot),
-                                     ptr(csr.csc_dst), n, E, c, rows(B["H"], mrow, c), ptr(uH), ptr(dO_b[b]),
-                                     ptr(conv.att_src), ptr(conv.att_dst), _off(B["a_s"], mrow), _off(B["a_d"], mrow),
-                                     _off(B["alpha"], 2 * E), float(conv.negative_slope), ptr(uO), ptr(hinj),
-                                     ptr(conv.att_src.grad), ptr(conv.att_dst.grad), ptr(up_s), ptr(up_d), ptr(ws),
-                                     st), "vg_gat_jvp2_ex")
+            folds.call(LIB.vg_gat_jvp2_deferred,
+                       (ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot), ptr(csr.csc_dst), n, E,
+                        c, rows(B["H"], mrow, c), ptr(uH), ptr(dO_b[b]), ptr(conv.att_src), ptr(conv.att_dst),
+                        _off(B["a_s"], mrow), _off(B["a_d"], mrow), _off(B["alpha"], 2 * E),
+                        float(conv.negative_slope), ptr(uO), ptr(hinj), ptr(conv.att_src.grad),
+                        ptr(conv.att_dst.grad), ptr(up_s), ptr(up_d), ptr(ws)), st, keep=(ws,),
+                       name="vg_gat_jvp2_deferred")
             oinj = _f(n, c, dev=dev)
             ws = _f(int(LIB.vg_graphnorm_seg_ws_floats(1, n, c)), dev=dev)
             check(LIB.vg_graphnorm_jvp2(rows(B["O"], mrow, c), n, c, ptr(norm.weight), ptr(norm.bias),
@@ -306,7 +310,7 @@ class CriticEngine:
         for i in range(nd - 1, -1, -1):
             lin = self.dec[i]
             aw, m = lin.weight.shape
-            self._gemm_tn(st, dev, ptr(adj_dec[i]), aw, ptr(dec_in[i]), m, X4, aw, m, ptr(lin.weight.grad), m,
+            self._gemm_tn(folds, st, dev, ptr(adj_dec[i]), aw, ptr(dec_in[i]), m, X4, aw, m, ptr(lin.weight.grad), m,
                           ptr(lin.bias.grad), R)
             if i > 0:
                 self._gemm(st, ptr(adj_dec[i]), aw, ptr(lin.weight), m, 0, ptr(adj_dec[i - 1]), m, R, m, aw, None,
@@ -325,12 +329,13 @@ class CriticEngine:
                                            ptr(norm.mean_scale.grad), 1, ptr(oinj_b[b]), mrow * c, ptr(ws), sy, st),
                   "vg_graphnorm_bwd_seg")
             ws = _f(int(LIB.vg_gat_bwd_ws_floats(R, 3 * E, c)), dev=dev)
-            check(LIB.vg_gat_bwd_ex(ptr(csr3.row_ptr), ptr(csr3.col), ptr(csr3.csc_ptr), ptr(csr3.csc_slot),
-                                    ptr(csr3.csc_dst), R, 3 * E, c, ptr(B["H"]), ptr(conv.att_src), ptr(conv.att_dst),
-                                    ptr(B["a_s"]), ptr(B["a_d"]), ptr(B["alpha"]), ptr(dO), float(conv.negative_slope),
-                                    ptr(adj_H[b]), ptr(conv.att_src.grad), ptr(conv.att_dst.grad),
-                                    ptr(conv.bias.grad), 1, ptr(hinj_b[b]), mrow, ptr(ws), st), "vg_gat_bwd_ex")
-            self._gemm_tn(st, dev, ptr(adj_H[b]), c, ptr(B["X"]), cin, X4, c, cin, ptr(conv.lin.weight.grad), cin)
+            folds.call(LIB.vg_gat_bwd_deferred,
+                       (ptr(csr3.row_ptr), ptr(csr3.col), ptr(csr3.csc_ptr), ptr(csr3.csc_slot), ptr(csr3.csc_dst), R,
+                        3 * E, c, ptr(B["H"]), ptr(conv.att_src), ptr(conv.att_dst), ptr(B["a_s"]), ptr(B["a_d"]),
+                        ptr(B["alpha"]), ptr(dO), float(conv.negative_slope), ptr(adj_H[b]), ptr(conv.att_src.grad),
+                        ptr(conv.att_dst.grad), ptr(conv.bias.grad), 1, ptr(hinj_b[b]), mrow, ptr(ws)), st,
+                       keep=(ws,), name="vg_gat_bwd_deferred")
+            self._gemm_tn(folds, st, dev, ptr(adj_H[b]), c, ptr(B["X"]), cin, X4, c, cin, ptr(conv.lin.weight.grad), cin)
             if b > 0:
                 dY = _f(R, cin, dev=dev)
                 self._gemm(st, ptr(adj_H[b]), c, ptr(conv.lin.weight), cin, 0, ptr(dY), cin, R, cin, c)
@@ -341,10 +346,11 @@ class CriticEngine:
             lin = self.mlp[i]
             o, m = lin.weight.shape
             xin = X0 if i == 0 else mlp_out[i - 1]
-            self._gemm_tn(st, dev, ptr(adj_mlp[i]), o, ptr(xin), m, X4, o, m, ptr(lin.weight.grad), m,
+            self._gemm_tn(folds, st, dev, ptr(adj_mlp[i]), o, ptr(xin), m, X4, o, m, ptr(lin.weight.grad), m,
                           ptr(lin.bias.grad), R)
             if i > 0:
                 self._gemm(st, ptr(adj_mlp[i]), o, ptr(lin.weight), m, 0, ptr(adj_mlp[i - 1]), m, R, m, o, None,
                            ACT_MASK, ptr(mlp_out[i - 1]), m)
+        folds.flush(st)
         self.last_gp = out[1]
         return out[0]

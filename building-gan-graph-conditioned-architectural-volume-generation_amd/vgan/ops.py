@@ -25,7 +25,7 @@ import torch
 from torch.autograd import Function
 
 from . import _lib
-from ._lib import LIB, check, ptr, require_cuda, stream_handle, sync_counter
+from ._lib import LIB, FoldCollector, check, ptr, require_cuda, stream_handle, sync_counter
 
 NEG_SLOPE = 0.2
 SOFTMAX_EPS = 1e-16
@@ -119,6 +119,32 @@ class direct_param_grads:
     def __exit__(self, *exc):
         global _DIRECT_GRADS
         _DIRECT_GRADS = self._prev
+        return False
+
+
+_FOLDS = None  # active FoldCollector of deferred_param_folds()
+
+
+class deferred_param_folds:
+    """Within this context the direct parameter-gradient paths (``gemm_tn_into``
+    and the GATConv backward under ``direct_param_grads``) leave their partial
+    folds to ONE ``vg_fold_batch`` launch enqueued when the context exits --
+    the optimizer step is their only consumer."""
+
+    def __init__(self, device=None):
+        self.device = device
+
+    def __enter__(self):
+        global _FOLDS
+        self._prev, _FOLDS = _FOLDS, FoldCollector()
+        return self
+
+    def __exit__(self, exc_type, *exc):
+        global _FOLDS
+        col, _FOLDS = _FOLDS, self._prev
+        if exc_type is None and col.folds:
+            dev = self.device if self.device is not None else col.keep[0].device
+            col.flush(stream_handle(dev))
         return False
 
 
@@ -414,11 +440,14 @@ class _GATConv(Function):
             g_vd = torch.empty_like(g_vs)
             g_b = torch.empty_like(g_vs)
         ws = torch.empty(int(LIB.vg_gat_bwd_ws_floats(n, csr.num_edges, c)), dtype=torch.float32, device=dev)
-        check(LIB.vg_gat_bwd_ex(ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot), ptr(csr.csc_dst),
-                                n, csr.num_edges, c, ptr(h), ptr(_f32(att_src.reshape(-1))),
-                                ptr(_f32(att_dst.reshape(-1))), ptr(a_src), ptr(a_dst), ptr(alpha), ptr(g_out),
-                                float(ctx.slope), ptr(g_h), ptr(g_vs), ptr(g_vd), ptr(g_b), 1 if direct else 0, None, 0,
-                                ptr(ws), csr.stream()), "vg_gat_bwd_ex")
+        args = (ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot), ptr(csr.csc_dst), n,
+                csr.num_edges, c, ptr(h), ptr(_f32(att_src.reshape(-1))), ptr(_f32(att_dst.reshape(-1))), ptr(a_src),
+                ptr(a_dst), ptr(alpha), ptr(g_out), float(ctx.slope), ptr(g_h), ptr(g_vs), ptr(g_vd), ptr(g_b),
+                1 if direct else 0, None, 0, ptr(ws))
+        if direct and _FOLDS is not None:  # parameter-gradient fold deferred to the context's batch
+            _FOLDS.call(LIB.vg_gat_bwd_deferred, args, csr.stream(), keep=(ws,), name="vg_gat_bwd_deferred")
+        else:
+            check(LIB.vg_gat_bwd_ex(*args, csr.stream()), "vg_gat_bwd_ex")
         if direct:
             return g_h, None, None, None, None, None, None
         return g_h, g_vs.view_as(att_src), g_vd.view_as(att_dst), g_b, None, None, None
@@ -737,6 +766,11 @@ def gemm_tn_into(a: torch.Tensor, b: torch.Tensor, c_out: torch.Tensor, db_out: 
     if b.shape[0] != n or tuple(c_out.shape) != (m, k):
         raise ValueError("gemm_tn_into: inconsistent shapes")
     ws = torch.empty(max(1, int(LIB.vg_gemm_tn_ws_floats(n, m, k))), dtype=torch.float32, device=a.device)
+    if _FOLDS is not None and n > 0:  # fold deferred to the context's batch
+        _FOLDS.call(LIB.vg_gemm_tn_deferred, (ptr(a), m, ptr(b), k, n, m, k, ptr(c_out), k, ptr(db_out), n, 1,
+                                              ptr(ws)), stream_handle(a.device), keep=(ws,),
+                    name="vg_gemm_tn_deferred")
+        return
     check(LIB.vg_gemm_tn(ptr(a), m, ptr(b), k, n, m, k, ptr(c_out), k, ptr(db_out), 1, ptr(ws),
                          stream_handle(a.device)), "vg_gemm_tn")
 

@@ -182,7 +182,7 @@ class Trainer:
                 p.requires_grad_(False)
         try:
             g_loss = self._compute_generator_loss(local_graph, voxel_graph, logits, hard)
-            with ops.direct_param_grads():
+            with ops.direct_param_grads(), ops.deferred_param_folds(g_loss.device):
                 g_loss.backward()
         finally:
             if self.skip_dead_d_grads:

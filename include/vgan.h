@@ -348,6 +348,65 @@ int vg_ln_act_bwd(const float* x, int32_t N, int32_t C, const float* gamma, cons
                   float* g_gamma, float* g_beta, int32_t accumulate, float* workspace,
                   void* stream);
 
+/* ---- deferred parameter-gradient folds ------------------------------------ */
+
+/* One fold: out[(w / k) * ldo + w % k] = (accumulate ? out : 0)
+ *   + sum_r src[0].part[r * src[0].ld + w] (+ the same over src[1])   for w < width,
+ * partial rows summed in a fixed order (deterministic). */
+typedef struct {
+  const float* part;
+  int32_t rows;
+  int32_t ld;
+} vg_fold_src;
+
+typedef struct {
+  float* out;
+  int32_t width;
+  int32_t k;
+  int32_t ldo;
+  int32_t accumulate;
+  int32_t nsrc; /* 1 or 2 */
+  vg_fold_src src[2];
+} vg_fold;
+
+#define VG_FOLD_MAX 40
+
+/* Run up to VG_FOLD_MAX folds (a HOST array, passed to the kernel by value)
+ * in one launch.  The parameter gradients of a backward are needed only by
+ * the optimizer step, so the *_deferred variants below skip their own fold
+ * launch and return its descriptor(s) instead; the caller keeps their
+ * workspaces alive until vg_fold_batch is enqueued. */
+int vg_fold_batch(const vg_fold* folds, int32_t n, void* stream);
+
+/* vg_gemm_tn_ex without its fold: writes up to 2 descriptors (C, then db when
+ * non-NULL) to folds_out and their count to *n_out (host memory). */
+int vg_gemm_tn_deferred(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N,
+                        int32_t M, int32_t K, float* C, int32_t ldc, float* db, int32_t db_rows,
+                        int32_t accumulate, float* workspace, vg_fold* folds_out, int32_t* n_out,
+                        void* stream);
+
+/* vg_gat_bwd_ex without the parameter-gradient fold: up to 3 descriptors
+ * (g_bias, g_att_dst, g_att_src); none when g_att_src is NULL. */
+int vg_gat_bwd_deferred(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,
+                        const int32_t* csc_slot, const int32_t* csc_dst, int32_t num_nodes,
+                        int32_t num_edges, int32_t channels, const float* h, const float* att_src,
+                        const float* att_dst, const float* a_src, const float* a_dst,
+                        const float* alpha, const float* g_out, float slope, float* g_h,
+                        float* g_att_src, float* g_att_dst, float* g_bias, int32_t accumulate,
+                        const float* inj, int32_t inj_row0, float* workspace, vg_fold* folds_out,
+                        int32_t* n_out, void* stream);
+
+/* vg_gat_jvp2_ex without its fold: 2 descriptors (g_att_dst, g_att_src), both
+ * accumulating. */
+int vg_gat_jvp2_deferred(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,
+                         const int32_t* csc_slot, const int32_t* csc_dst, int32_t num_nodes,
+                         int32_t num_edges, int32_t channels, const float* h, const float* u,
+                         const float* g_out, const float* att_src, const float* att_dst,
+                         const float* a_src, const float* a_dst, const float* alpha, float slope,
+                         float* u_out, float* h_inj, float* g_att_src, float* g_att_dst,
+                         const float* up_src, const float* up_dst, float* workspace,
+                         vg_fold* folds_out, int32_t* n_out, void* stream);
+
 /* ---- optimiser ---------------------------------------------------------- */
 
 /* torch.optim.Adam (single-tensor semantics, weight_decay, no amsgrad) over one
