@@ -162,6 +162,141 @@ __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int l
   }
 }
 
+// Y = leaky_relu(LayerNorm(A . B^T + bias; gamma, beta, eps), slope) with the
+// LayerNorm in the epilogue: the [Linear -> LayerNorm -> LeakyReLU(0.2)]
+// blocks of the generator's MLPs (models.py:33-47, 49-66, 92-113).  A
+// workgroup owns 64 rows x 64*NT columns -- every column of the layer
+// (M <= 64 NT) -- so each row's statistics are complete in the tile: the tile
+// is staged through LDS, four threads per row take two-pass mean / biased
+// variance (as torch), then the whole workgroup normalises, activates and
+// stores with lanes along the columns (coalesced).  H (nullable) receives the
+// pre-LayerNorm activations and mean / rstd (nullable) the row statistics for
+// the backward; the no-grad forwards skip both.  Saves the separate LayerNorm
+// launch and its read of the GEMM output.
+template <int NT>
+__global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, int lda,
+                                                 const float* __restrict__ B, int ldb,
+                                                 const float* __restrict__ bias, int N, int M, int K,
+                                                 const float* __restrict__ gamma,
+                                                 const float* __restrict__ beta, float eps,
+                                                 float slope, float* __restrict__ H,
+                                                 float* __restrict__ Y, float* __restrict__ mean,
+                                                 float* __restrict__ rstd) {
+  constexpr int TNC = TN * NT;
+  constexpr int CT = TNC + 1;  // staged tile row pitch
+  __shared__ float smem[2 * TM * LDP + 2 * TNC * LDP];
+  __shared__ float s_mu[TM], s_rs[TM];
+  float(*As)[TM][LDP] = reinterpret_cast<float(*)[TM][LDP]>(smem);
+  float(*Bs)[TNC][LDP] = reinterpret_cast<float(*)[TNC][LDP]>(smem + 2 * TM * LDP);
+  constexpr int PA = (TM * TK) / 256, PB = (TNC * TK) / 256;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  int tx, ty;
+  tile_xy(tx, ty);
+  const int n0 = tx * TM;
+  f32x16 acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  float ra[PA], rb[PB];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < PA; ++q) {
+      const int e = t + 256 * q;
+      const int n = n0 + e / TK, k = k0 + e % TK;
+      ra[q] = (n < N && k < K) ? A[(size_t)n * lda + k] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < PB; ++q) {
+      const int e = t + 256 * q;
+      const int m = e / TK, k = k0 + e % TK;
+      rb[q] = (m < M && k < K) ? B[(size_t)m * ldb + k] : 0.f;
+    }
+  };
+  load(0);
+  int buf = 0;
+  for (int k0 = 0; k0 < K; k0 += TK) {
+#pragma unroll
+    for (int q = 0; q < PA; ++q) {
+      const int e = t + 256 * q;
+      As[buf][e / TK][e % TK] = ra[q];
+    }
+#pragma unroll
+    for (int q = 0; q < PB; ++q) {
+      const int e = t + 256 * q;
+      Bs[buf][e / TK][e % TK] = rb[q];
+    }
+    __syncthreads();
+    if (k0 + TK < K) load(k0 + TK);
+    const float* ar = &As[buf][wr * 32 + (lane & 31)][lane >> 5];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const float* br = &Bs[buf][j * TN + wc * 32 + (lane & 31)][lane >> 5];
+#pragma unroll
+      for (int kk = 0; kk < TK; kk += 2)
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[kk], br[kk], acc[j], 0, 0, 0);
+    }
+    buf ^= 1;
+  }
+  // stage the full-width tile (+ bias) in LDS
+  __syncthreads();
+  float* Ct = smem;
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int c = j * TN + wc * 32 + (lane & 31);
+    const float bv = (bias && c < M) ? bias[c] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      Ct[(wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * CT + c] = acc[j][r] + bv;
+  }
+  __syncthreads();
+  {  // row statistics: 4 threads per row, two-pass
+    constexpr int CPT = TNC / 4;
+    const int row = t >> 2, q = t & 3;
+    const float* cr = Ct + row * CT + q * CPT;
+    float v[CPT];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      v[i] = q * CPT + i < M ? cr[i] : 0.f;
+      s += v[i];
+    }
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    const float mu = s / static_cast<float>(M);
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i)
+      if (q * CPT + i < M) {
+        const float d = v[i] - mu;
+        ss = fmaf(d, d, ss);
+      }
+    ss += __shfl_xor(ss, 1, 64);
+    ss += __shfl_xor(ss, 2, 64);
+    const float rs = rsqrtf(ss / static_cast<float>(M) + eps);
+    if (q == 0) {
+      s_mu[row] = mu;
+      s_rs[row] = rs;
+      if (mean && n0 + row < N) {
+        mean[n0 + row] = mu;
+        rstd[n0 + row] = rs;
+      }
+    }
+  }
+  __syncthreads();
+  // normalise + activate, lanes along the columns (coalesced row stores)
+  for (int idx = t; idx < TM * TNC; idx += 256) {
+    const int row = idx / TNC, c = idx % TNC, n = n0 + row;
+    if (c < M && n < N) {
+      const float v = Ct[row * CT + c];
+      if (H) H[(size_t)n * M + c] = v;
+      const float z = fmaf((v - s_mu[row]) * s_rs[row], gamma[c], beta[c]);
+      Y[(size_t)n * M + c] = z > 0.f ? z : z * slope;
+    }
+  }
+}
+
 // part[chunk][M][K] = A[chunk rows]^T . B[chunk rows];  pdb[chunk][M] = column sums of A.
 // `rows` rows of the N reduction per chunk (a multiple of TK), pipelined like k_gemm.
 // G row groups of 4 waves per workgroup: group g takes the chunk's K-steps
@@ -389,6 +524,26 @@ extern "C" int vg_gemm_tn_deferred(const float* A, int32_t lda, const float* B, 
   if (!folds_out || !n_out || N <= 0) return VG_EINVAL;
   return gemm_tn(A, lda, B, ldb, N, M, K, C, ldc, db, db_rows, accumulate, workspace, stream,
                  folds_out, n_out);
+}
+
+extern "C" int vg_gemm_ln_act(const float* A, int32_t lda, const float* W, int32_t N, int32_t M,
+                              int32_t K, const float* bias, const float* gamma, const float* beta,
+                              float eps, float slope, float* H, float* Y, float* mean, float* rstd,
+                              void* stream) {
+  if (N < 0 || M <= 0 || M > 2 * TN || K <= 0 || lda < K || !A || !W || !gamma || !beta || !Y ||
+      ((mean == nullptr) != (rstd == nullptr)))
+    return VG_EINVAL;
+  if (N == 0) return 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 grid((N + TM - 1) / TM, 1);
+  if (M <= TN)
+    k_gemm_ln<1><<<grid, 256, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma, beta, eps, slope, H, Y, mean,
+                                      rstd);
+  else
+    k_gemm_ln<2><<<grid, 256, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma, beta, eps, slope, H, Y, mean,
+                                      rstd);
+  VG_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int vg_gat_lin_att(const float* X, int32_t ldx, const float* W, int32_t N,

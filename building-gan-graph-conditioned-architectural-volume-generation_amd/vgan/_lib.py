@@ -99,6 +99,8 @@ SIGNATURES = {
                                             _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_i64, _c_p, _c_p, _c_p]),
     "vg_graphnorm_jvp2": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p,
                                          _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "vg_gemm_ln_act": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_f32, _c_f32,
+                                      _c_p, _c_p, _c_p, _c_p, _c_p]),
     "vg_ln_act_fwd": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_f32, _c_f32, _c_p, _c_p, _c_p, _c_p]),
     "vg_ln_act_bwd_ws_floats": (_c_i64, [_c_i32]),
     "vg_ln_act_bwd": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,

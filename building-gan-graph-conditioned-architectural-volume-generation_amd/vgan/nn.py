@@ -79,27 +79,30 @@ class _LinearFn(Function):
         return _linear_backward(ctx, gy) + (None,)
 
 
-def _linear_backward(ctx, gy):
-    """(g_x, g_weight, g_bias) of y = x W^T (+ b) for _LinearFn / _LinAttFn."""
-    x, weight = ctx.saved_tensors
+def _linear_backward(ctx, gy, saved=None, needs=None):
+    """(g_x, g_weight, g_bias) of y = x W^T (+ b) for _LinearFn / _LinAttFn /
+    _LinearLNActFn (``saved`` = (x, weight) and ``needs`` = the three
+    needs-grad flags when the ctx holds more)."""
+    x, weight = saved if saved is not None else ctx.saved_tensors
+    needs = needs if needs is not None else ctx.needs_input_grad
     gx = gw = gb = None
     if torch.is_grad_enabled():  # create_graph: differentiable MFMA matmuls
         gy = gy.contiguous()
-        if ctx.needs_input_grad[0]:
+        if needs[0]:
             gx = _MMnn.apply(gy, weight)
-        if ctx.needs_input_grad[1]:
+        if needs[1]:
             gw = _MMtn.apply(gy, x)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
+        if ctx.has_bias and needs[2]:
             gb = gy.sum(0)
         return gx, gw, gb
     gy = gy.contiguous()
-    if ctx.needs_input_grad[0]:
+    if needs[0]:
         gx = ops.gemm(gy, weight, False)
     pw, pb = ctx.params
-    if ctx.needs_input_grad[1] and ops._direct(pw, pb):  # accumulate into .grad directly
+    if needs[1] and ops._direct(pw, pb):  # accumulate into .grad directly
         ops.gemm_tn_into(gy, x, pw.grad, pb.grad if ctx.has_bias else None)
         return gx, None, None
-    if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+    if needs[1] or (ctx.has_bias and needs[2]):
         gw, gb = ops.gemm_tn(gy, x, want_colsum=ctx.has_bias)
     return gx, gw, (gb if ctx.has_bias else None)
 
@@ -125,6 +128,63 @@ class _LinAttFn(Function):
             return None, None, None, None
         gx, gw, _ = _linear_backward(ctx, gh)
         return gx, gw, None, None
+
+
+class _LinearLNActFn(Function):
+    """leaky_relu(LayerNorm(x W^T + b)) with the LayerNorm in the GEMM's
+    epilogue (vg_gemm_ln_act); the backward is the LayerNorm+activation
+    backward (vg_ln_act_bwd) followed by the Linear backward."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, gamma, beta, eps, slope):
+        from ._lib import LIB, check, ptr, stream_handle
+
+        n, k = x.shape
+        m = weight.shape[0]
+        dev = x.device
+        y = torch.empty(n, m, dtype=torch.float32, device=dev)
+        save = any(ctx.needs_input_grad[:5])
+        h = torch.empty_like(y) if save else None
+        mean = torch.empty(n, dtype=torch.float32, device=dev) if save else None
+        rstd = torch.empty(n, dtype=torch.float32, device=dev) if save else None
+        check(LIB.vg_gemm_ln_act(ptr(x), k, ptr(weight), n, m, k, ptr(bias), ptr(gamma), ptr(beta), float(eps),
+                                 float(slope), ptr(h), ptr(y), ptr(mean), ptr(rstd), stream_handle(dev)),
+              "vg_gemm_ln_act")
+        ctx.eps, ctx.slope = eps, slope
+        ctx.has_bias = bias is not None
+        ctx.params = (weight, bias)
+        ctx.ln_params = (gamma, beta)
+        if save:
+            ctx.save_for_backward(x, weight, h, gamma, beta, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight, h, gamma, beta, mean, rstd = ctx.saved_tensors
+        needs = ctx.needs_input_grad
+        if torch.is_grad_enabled():  # create_graph: differentiable restatement of both halves
+            bias = ctx.params[1]
+            ins = [x, weight, bias, gamma, beta]
+            with torch.enable_grad():
+                leaves = [None if t is None else t.detach().requires_grad_(bool(nd))
+                          for t, nd in zip(ins, needs[:5])]
+                y = ops.ln_act(_LinearFn.apply(leaves[0], leaves[1], leaves[2], ops.ACT_NONE), leaves[3], leaves[4],
+                               ctx.eps, ctx.slope)
+                want = [t for t in leaves if t is not None and t.requires_grad]
+                got = iter(torch.autograd.grad(y, want, gy, create_graph=True, allow_unused=True))
+            return tuple(next(got) if t is not None and t.requires_grad else None for t in leaves) + (None, None)
+        gh, g_gamma, g_beta = ops.ln_act_backward(h, gamma, beta, ctx.eps, ctx.slope, mean, rstd, gy,
+                                                  ctx.ln_params, want_params=needs[3] or needs[4])
+        gx, gw, gb = _linear_backward(ctx, gh, saved=(x, weight), needs=needs[:3])
+        return gx, gw, gb, g_gamma, g_beta, None, None
+
+
+def linear_ln_act(x: torch.Tensor, weight: torch.Tensor, bias, gamma: torch.Tensor, beta: torch.Tensor,
+                  eps: float = 1e-5, slope: float = 0.2) -> torch.Tensor:
+    """[Linear -> LayerNorm -> LeakyReLU] in one launch (M <= 128 outputs)."""
+    if not x.is_cuda:
+        raise RuntimeError("vgan HIP ops require tensors on a ROCm device (no CPU fallback)")
+    return _LinearLNActFn.apply(x.contiguous(), weight, bias, gamma, beta, eps, slope)
 
 
 def linear_att(x: torch.Tensor, weight: torch.Tensor, att_src: torch.Tensor, att_dst: torch.Tensor):
@@ -163,7 +223,11 @@ class MLP(nn.Sequential):
                     and isinstance(mods[i + 2], nn.LeakyReLU) and len(mods[i + 1].normalized_shape) == 1
                     and mods[i + 1].elementwise_affine):
                 ln = mods[i + 1]
-                x = ops.ln_act(linear(x, m.weight, m.bias), ln.weight, ln.bias, ln.eps, mods[i + 2].negative_slope)
+                if m.out_features <= 128 and x.dim() == 2:  # LayerNorm in the GEMM epilogue
+                    x = linear_ln_act(x, m.weight, m.bias, ln.weight, ln.bias, ln.eps, mods[i + 2].negative_slope)
+                else:
+                    x = ops.ln_act(linear(x, m.weight, m.bias), ln.weight, ln.bias, ln.eps,
+                                   mods[i + 2].negative_slope)
                 i += 3
             else:
                 x = m(x)

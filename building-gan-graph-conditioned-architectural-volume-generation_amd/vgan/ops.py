@@ -701,6 +701,31 @@ class _LNAct(Function):
         return g_x, g_g, g_b, None, None
 
 
+def ln_act_backward(x, gamma, beta, eps, slope, mean, rstd, g_y, params, want_params: bool = True):
+    """First-order backward of leaky_relu(LayerNorm(x)) (vg_ln_act_bwd) from the
+    saved row statistics: (g_x, g_gamma, g_beta); the parameter gradients are
+    accumulated straight into ``params``' .grad under direct_param_grads (then
+    returned as None)."""
+    del eps  # mean / rstd already carry it
+    g_y = _f32(g_y)
+    n, c = x.shape
+    g_x = torch.empty_like(x)
+    pg, pb = params
+    direct = want_params and _direct(pg, pb)
+    if direct:
+        g_g, g_b = pg.grad, pb.grad
+    else:
+        g_g = torch.empty(c, dtype=torch.float32, device=x.device)
+        g_b = torch.empty_like(g_g)
+    ws = torch.empty(int(LIB.vg_ln_act_bwd_ws_floats(c)), dtype=torch.float32, device=x.device)
+    check(LIB.vg_ln_act_bwd(ptr(x), n, c, ptr(gamma), ptr(beta), float(slope), ptr(mean), ptr(rstd), ptr(g_y),
+                            ptr(g_x), ptr(g_g), ptr(g_b), 1 if direct else 0, ptr(ws), stream_handle(x.device)),
+          "vg_ln_act_bwd")
+    if direct or not want_params:
+        return g_x, None, None
+    return g_x, g_g, g_b
+
+
 def ln_act(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-5, slope: float = 0.2):
     """nn.LayerNorm(C) followed by nn.LeakyReLU(slope) (models.py:33-113)."""
     return _LNAct.apply(x, gamma, beta, eps, slope)

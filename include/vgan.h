@@ -332,6 +332,17 @@ int vg_gemm_tn_ex(const float* A, int32_t lda, const float* B, int32_t ldb, int3
 
 /* ---- LayerNorm + LeakyReLU ------------------------------------------------ */
 
+/* Y = leaky_relu(LayerNorm(A W^T + bias; gamma, beta, eps), slope) for M <= 128
+ * output features in ONE launch (the LayerNorm in the GEMM epilogue; A [N, K]
+ * row stride lda, W [M, K]): the [Linear -> LayerNorm -> LeakyReLU(0.2)]
+ * blocks of models.py:33-47,49-66,92-113.  H (nullable) receives A W^T + bias
+ * and mean / rstd [N] (nullable together) the row statistics, both for
+ * vg_ln_act_bwd. */
+int vg_gemm_ln_act(const float* A, int32_t lda, const float* W, int32_t N, int32_t M, int32_t K,
+                   const float* bias, const float* gamma, const float* beta, float eps, float slope,
+                   float* H, float* Y, float* mean, float* rstd, void* stream);
+
+
 /* y = leaky_relu(LayerNorm(x; gamma, beta, eps), slope) per row of x [N, C]
  * (C <= 512): the nn.LayerNorm -> nn.LeakyReLU(0.2) pairs of the generator's
  * MLPs (models.py:33-47,49-66,92-113) in one kernel.  mean / rstd [N]

@@ -424,3 +424,27 @@ def test_graphnorm_in_kernel_dropout(cuda):
     y4 = ops.graphnorm_relu_dropout(xr2, w, b, ms, k3.contiguous())
     (gx2,) = torch.autograd.grad(y4.sum(), xr2)
     assert torch.allclose(gx, gx2, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("m,k", [(16, 17), (64, 128), (100, 268), (128, 524), (128, 128)])
+def test_linear_ln_act_fused_matches_unfused(cuda, m, k):
+    """vg_gemm_ln_act (LayerNorm + LeakyReLU in the GEMM epilogue) against
+    Linear -> ln_act and torch fp64, forward and first-order gradients."""
+    from vgan.nn import linear, linear_ln_act
+
+    torch.manual_seed(m + k)
+    n = 1537
+    x = torch.randn(n, k, device=cuda)
+    w = torch.randn(m, k, device=cuda) / k ** 0.5
+    b, g, be = torch.randn(m, device=cuda), 1 + 0.1 * torch.randn(m, device=cuda), 0.1 * torch.randn(m, device=cuda)
+    p1 = [t.clone().requires_grad_(True) for t in (x, w, b, g, be)]
+    y1 = linear_ln_act(p1[0], p1[1], p1[2], p1[3], p1[4], 1e-5, 0.2)
+    p2 = [t.clone().requires_grad_(True) for t in (x, w, b, g, be)]
+    y2 = ops.ln_act(linear(p2[0], p2[1], p2[2]), p2[3], p2[4], 1e-5, 0.2)
+    xd, wd, bd, gd, bed = (t.double().cpu() for t in (x, w, b, g, be))
+    ref = torch.nn.functional.leaky_relu(torch.nn.functional.layer_norm(xd @ wd.t() + bd, (m,), gd, bed, 1e-5), 0.2)
+    assert rel_err(y1, ref) < 1e-5
+    assert rel_err(y1, y2) < 1e-5
+    gy = torch.randn(n, m, device=cuda)
+    for u, v in zip(torch.autograd.grad(y1, p1, gy), torch.autograd.grad(y2, p2, gy)):
+        assert rel_err(u, v) < 1e-5
