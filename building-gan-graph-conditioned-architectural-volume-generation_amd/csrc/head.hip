@@ -177,6 +177,112 @@ __global__ void k_adam_dev(float* __restrict__ p, const float* __restrict__ g,
   }
 }
 
+// ---------------------------------------------------------------- generator loss head
+// trainer.py:334-385 with USE_WGANGP (the FAR term has no gradient, :380):
+//   loss = (((adv + ratio) + ce) + ratio_void) + far
+//   adv = -mean(d_fake) l_adv;  ce = CE(logits, type) l_label
+//   rg = sum_n hard / N, rr = sum_n onehot / N
+//   ratio = mean_{c<K-2} (rg - rr)^2 l_ratio;  ratio_void = mean_{c>=K-2} (rg - rr)^2 l_void
+//   far = mean_g (far_gen - far_ref)^2 l_far
+// Partial row of block b: [sum d_fake | sum hard[:, c] (K) | sum onehot[:, c] (K) | sum ce_n].
+constexpr int kGLThreads = 256;
+constexpr int kGLMaxBlocks = 256;
+
+__global__ void __launch_bounds__(kGLThreads) k_gen_loss_partial(
+    const float* __restrict__ d_fake, const float* __restrict__ hard,
+    const float* __restrict__ logits, const float* __restrict__ onehot,
+    const int64_t* __restrict__ type, int N, int K, float* __restrict__ part) {
+  const int W = 2 * K + 2;
+  float acc[2 * kMaxClasses + 2];
+  for (int i = 0; i < W; ++i) acc[i] = 0.f;
+  for (int n = blockIdx.x * blockDim.x + threadIdx.x; n < N; n += gridDim.x * blockDim.x) {
+    acc[0] += d_fake[n];
+    float m = -INFINITY;
+    for (int c = 0; c < K; ++c) {
+      acc[1 + c] += hard[(size_t)n * K + c];
+      acc[1 + K + c] += onehot[(size_t)n * K + c];
+      m = fmaxf(m, logits[(size_t)n * K + c]);
+    }
+    float se = 0.f;
+    for (int c = 0; c < K; ++c) se += expf(logits[(size_t)n * K + c] - m);
+    acc[2 * K + 1] += (m + logf(se)) - logits[(size_t)n * K + type[n]];
+  }
+  __shared__ float red[kGLThreads];
+  for (int i = 0; i < W; ++i) {  // fixed-order block reduction, one value at a time
+    red[threadIdx.x] = acc[i];
+    __syncthreads();
+    for (int off = kGLThreads / 2; off > 0; off >>= 1) {
+      if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) part[(size_t)blockIdx.x * W + i] = red[0];
+    __syncthreads();
+  }
+}
+
+// out: [0] loss, [1..K] d loss / d hard[n, c], [K+1] d loss / d d_fake[n],
+// [K+2] l_label / N (the cross-entropy gradient scale)
+__global__ void __launch_bounds__(64) k_gen_loss_final(const float* __restrict__ part, int nb, int N,
+                                                       int K, const float* __restrict__ far_gen,
+                                                       const float* __restrict__ far_ref, int G,
+                                                       float l_adv, float l_label, float l_ratio,
+                                                       float l_void, float l_far,
+                                                       float* __restrict__ out) {
+  __shared__ float tot[2 * kMaxClasses + 2];
+  const int W = 2 * K + 2;
+  for (int i = threadIdx.x; i < W; i += blockDim.x) {
+    float v = 0.f;
+    for (int b = 0; b < nb; ++b) v += part[(size_t)b * W + i];
+    tot[i] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const float fn = static_cast<float>(N);
+  const float adv = -(tot[0] / fn) * l_adv;
+  float r1 = 0.f, r2 = 0.f;
+  const int k1 = K - 2;
+  for (int c = 0; c < K; ++c) {
+    const float d = tot[1 + c] / fn - tot[1 + K + c] / fn;
+    if (c < k1) r1 += d * d;
+    else r2 += d * d;
+    out[1 + c] = (c < k1 ? l_ratio * 2.f * d / k1 : l_void * 2.f * d / 2.f) / fn;
+  }
+  const float ratio = (r1 / k1) * l_ratio, ratio_void = (r2 / 2.f) * l_void;
+  const float ce = (tot[2 * K + 1] / fn) * l_label;
+  float f = 0.f;
+  for (int g = 0; g < G; ++g) {
+    const float d = far_gen[g] - far_ref[g];
+    f += d * d;
+  }
+  const float far = (f / G) * l_far;
+  out[0] = (((adv + ratio) + ce) + ratio_void) + far;
+  out[K + 1] = -l_adv / fn;
+  out[K + 2] = l_label / fn;
+}
+
+__global__ void k_gen_loss_bwd(const float* __restrict__ g_loss, const float* __restrict__ coef,
+                               const float* __restrict__ logits, const int64_t* __restrict__ type,
+                               int N, int K, float* __restrict__ g_dfake,
+                               float* __restrict__ g_hard, float* __restrict__ g_logits) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const float g = *g_loss;
+  if (g_dfake) g_dfake[n] = g * coef[K + 1];
+  if (g_hard)
+    for (int c = 0; c < K; ++c) g_hard[(size_t)n * K + c] = g * coef[1 + c];
+  if (g_logits) {
+    float m = -INFINITY;
+    for (int c = 0; c < K; ++c) m = fmaxf(m, logits[(size_t)n * K + c]);
+    float se = 0.f;
+    for (int c = 0; c < K; ++c) se += expf(logits[(size_t)n * K + c] - m);
+    const float sc = g * coef[K + 2];
+    for (int c = 0; c < K; ++c) {
+      const float p = expf(logits[(size_t)n * K + c] - m) / se;
+      g_logits[(size_t)n * K + c] = sc * (p - (c == type[n] ? 1.f : 0.f));
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int vg_gumbel_fwd(const float* logits, const float* noise, int32_t rows,
@@ -265,6 +371,40 @@ extern "C" int vg_adam_dev(float* param, const float* grad, float* exp_avg, floa
   if (blocks > 2048) blocks = 2048;
   k_adam_dev<<<blocks, 256, 0, static_cast<hipStream_t>(stream)>>>(
       param, grad, exp_avg, exp_avg_sq, n, beta1, beta2, eps, weight_decay, lr, step);
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int64_t vg_gen_loss_ws_floats(int32_t N, int32_t classes) {
+  const int nb = vg_blocks(N, kGLThreads) < kGLMaxBlocks ? vg_blocks(N, kGLThreads) : kGLMaxBlocks;
+  return (int64_t)nb * (2 * classes + 2);
+}
+
+extern "C" int vg_gen_loss_fwd(const float* d_fake, const float* hard, const float* logits,
+                               const float* onehot, const int64_t* type, int32_t N, int32_t classes,
+                               const float* far_gen, const float* far_ref, int32_t num_graphs,
+                               float l_adv, float l_label, float l_ratio, float l_void, float l_far,
+                               float* out, float* workspace, void* stream) {
+  if (N <= 0 || classes < 3 || classes > kMaxClasses || num_graphs <= 0 || !d_fake || !hard ||
+      !logits || !onehot || !type || !far_gen || !far_ref || !out || !workspace)
+    return VG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int nb = vg_blocks(N, kGLThreads) < kGLMaxBlocks ? vg_blocks(N, kGLThreads) : kGLMaxBlocks;
+  k_gen_loss_partial<<<nb, kGLThreads, 0, s>>>(d_fake, hard, logits, onehot, type, N, classes,
+                                               workspace);
+  k_gen_loss_final<<<1, 64, 0, s>>>(workspace, nb, N, classes, far_gen, far_ref, num_graphs, l_adv,
+                                    l_label, l_ratio, l_void, l_far, out);
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int vg_gen_loss_bwd(const float* g_loss, const float* out, const float* logits,
+                               const int64_t* type, int32_t N, int32_t classes, float* g_dfake,
+                               float* g_hard, float* g_logits, void* stream) {
+  if (N <= 0 || classes <= 0 || classes > kMaxClasses || !g_loss || !out || (g_logits && (!logits || !type)))
+    return VG_EINVAL;
+  k_gen_loss_bwd<<<vg_blocks(N, 256), 256, 0, static_cast<hipStream_t>(stream)>>>(
+      g_loss, out, logits, type, N, classes, g_dfake, g_hard, g_logits);
   VG_CHECK_LAUNCH();
   return 0;
 }

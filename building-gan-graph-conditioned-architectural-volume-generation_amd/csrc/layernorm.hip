@@ -193,3 +193,26 @@ extern "C" int vg_ln_act_bwd(const float* x, int32_t N, int32_t C, const float* 
   VG_CHECK_LAUNCH();
   return 0;
 }
+
+extern "C" int vg_ln_act_bwd_deferred(const float* x, int32_t N, int32_t C, const float* gamma,
+                                      const float* beta, float slope, const float* mean,
+                                      const float* rstd, const float* g_y, float* g_x,
+                                      float* g_gamma, float* g_beta, int32_t accumulate,
+                                      float* workspace, vg_fold* folds_out, int32_t* n_out,
+                                      void* stream) {
+  if (N <= 0 || !x || !gamma || !beta || !mean || !rstd || !g_y || !g_x || !g_gamma || !g_beta ||
+      !workspace || !folds_out || !n_out)
+    return VG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  int grid = 0;
+  VG_LN_DISPATCH(C, (grid = grid_for(N, L_) < kMaxBlocks ? grid_for(N, L_) : kMaxBlocks,
+                     k_ln_act_bwd<L_, CPL_><<<grid, kBlock, 0, s>>>(x, N, C, gamma, beta, slope,
+                                                                   mean, rstd, g_y, g_x,
+                                                                   workspace)));
+  // partial rows [grid][2C] = [gamma | beta]: two folds for vg_fold_batch
+  folds_out[0] = vg_fold{g_gamma, C, C, C, accumulate, 1, {{workspace, grid, 2 * C}, {nullptr, 0, 0}}};
+  folds_out[1] = vg_fold{g_beta, C, C, C, accumulate, 1, {{workspace + C, grid, 2 * C}, {nullptr, 0, 0}}};
+  *n_out = 2;
+  VG_CHECK_LAUNCH();
+  return 0;
+}

@@ -41,6 +41,8 @@ SIGNATURES = {
     "vg_gat_bwd_deferred": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p,
                                            _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p,
                                            _c_i32, _c_p, _c_p, _c_p, _c_p]),
+    "vg_ln_act_bwd_deferred": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p, _c_p,
+                                              _c_p, _c_i32, _c_p, _c_p, _c_p, _c_p]),
     "vg_gat_jvp2_deferred": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p,
                                             _c_p, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
                                             _c_p, _c_p, _c_p, _c_p]),
@@ -73,6 +75,10 @@ SIGNATURES = {
     "vg_gumbel_bwd": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_i32, _c_i32, _c_f32, _c_p, _c_p]),
     "vg_far_per_graph": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32,
                                         _c_f32, _c_i32, _c_p, _c_p, _c_p]),
+    "vg_gen_loss_ws_floats": (_c_i64, [_c_i32, _c_i32]),
+    "vg_gen_loss_fwd": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_i32, _c_f32, _c_f32,
+                                       _c_f32, _c_f32, _c_f32, _c_p, _c_p, _c_p]),
+    "vg_gen_loss_bwd": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p]),
     "vg_confusion": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_p]),
     "vg_gemm": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_i32, _c_p, _c_i32, _c_i32,
                                _c_i32, _c_i32, _c_p]),

@@ -433,8 +433,11 @@ class _GATConv(Function):
         g_h = torch.empty_like(h)
         p_s, p_d, p_b = ctx.params
         direct = _direct(p_s, p_d, p_b)
+        want_p = any(ctx.needs_input_grad[1:4])
         if direct:
             g_vs, g_vd, g_b = p_s.grad, p_d.grad, p_b.grad
+        elif not want_p:  # e.g. the frozen discriminator in the generator iteration: g_h only
+            g_vs = g_vd = g_b = None
         else:
             g_vs = torch.empty(c, dtype=torch.float32, device=dev)
             g_vd = torch.empty_like(g_vs)
@@ -448,7 +451,7 @@ class _GATConv(Function):
             _FOLDS.call(LIB.vg_gat_bwd_deferred, args, csr.stream(), keep=(ws,), name="vg_gat_bwd_deferred")
         else:
             check(LIB.vg_gat_bwd_ex(*args, csr.stream()), "vg_gat_bwd_ex")
-        if direct:
+        if direct or not want_p:
             return g_h, None, None, None, None, None, None
         return g_h, g_vs.view_as(att_src), g_vd.view_as(att_dst), g_b, None, None, None
 
@@ -631,6 +634,56 @@ def far_per_graph(x, label, ptr_, site_area, far_col=9, dy_col=4, dx_col=5, dim_
     return gen, ref
 
 
+class _GenLossHead(Function):
+    """The WGAN-GP generator loss (trainer.py:334-385) as two launches forward
+    and one backward (vg_gen_loss_fwd / _bwd) instead of ~40 small torch
+    kernels.  The FAR term enters the value only (no gradient, :380); the
+    label cross-entropy's gradient is returned only when its weight is not 0
+    (0 x a finite gradient is exactly 0)."""
+
+    @staticmethod
+    def forward(ctx, d_fake, hard, logits, onehot, vtype, far_gen, far_ref, lambdas):
+        df, hd, lg, oh = (_f32(t.reshape(t.shape[-2], -1) if t.dim() > 2 else t) for t in (d_fake, hard, logits, onehot))
+        df = df.reshape(-1).contiguous()
+        require_cuda(df, hd, lg, oh, vtype, far_gen, far_ref)
+        n, k = hd.shape
+        if df.numel() != n or lg.shape != (n, k) or oh.shape != (n, k) or vtype.numel() != n:
+            raise ValueError("gen_loss_head: inconsistent shapes")
+        dev = hd.device
+        out = torch.empty(k + 3, dtype=torch.float32, device=dev)
+        ws = torch.empty(int(LIB.vg_gen_loss_ws_floats(n, k)), dtype=torch.float32, device=dev)
+        l_adv, l_label, l_ratio, l_void, l_far = (float(v) for v in lambdas)
+        check(LIB.vg_gen_loss_fwd(ptr(df), ptr(hd), ptr(lg), ptr(oh), ptr(vtype), n, k, ptr(_f32(far_gen)),
+                                  ptr(_f32(far_ref)), far_gen.numel(), l_adv, l_label, l_ratio, l_void, l_far,
+                                  ptr(out), ptr(ws), stream_handle(dev)), "vg_gen_loss_fwd")
+        ctx.l_label = l_label
+        ctx.shapes = (d_fake.shape, hard.shape, logits.shape)
+        ctx.save_for_backward(out, lg, vtype)
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        out, lg, vtype = ctx.saved_tensors
+        n, k = lg.shape
+        dev = lg.device
+        g = _f32(g.reshape(1))
+        need_d, need_h, need_l = ctx.needs_input_grad[:3]
+        need_l = need_l and ctx.l_label != 0.0
+        g_d = torch.empty(n, dtype=torch.float32, device=dev) if need_d else None
+        g_h = torch.empty(n, k, dtype=torch.float32, device=dev) if need_h else None
+        g_l = torch.empty(n, k, dtype=torch.float32, device=dev) if need_l else None
+        check(LIB.vg_gen_loss_bwd(ptr(g), ptr(out), ptr(lg), ptr(vtype), n, k, ptr(g_d), ptr(g_h), ptr(g_l),
+                                  stream_handle(dev)), "vg_gen_loss_bwd")
+        sd, sh, sl = ctx.shapes
+        return (g_d.view(sd) if g_d is not None else None, g_h.view(sh) if g_h is not None else None,
+                g_l.view(sl) if g_l is not None else None, None, None, None, None, None)
+
+
+def gen_loss_head(d_fake, hard, logits, onehot, vtype, far_gen, far_ref, lambdas) -> torch.Tensor:
+    """WGAN-GP generator loss (device scalar); lambdas = (adv, label, ratio, ratio_void, far)."""
+    return _GenLossHead.apply(d_fake, hard, logits, onehot, vtype, far_gen, far_ref, tuple(lambdas))
+
+
 def confusion(truth, label, ptr_):
     require_cuda(truth, label, ptr_)
     g = ptr_.numel() - 1
@@ -718,9 +771,13 @@ def ln_act_backward(x, gamma, beta, eps, slope, mean, rstd, g_y, params, want_pa
         g_g = torch.empty(c, dtype=torch.float32, device=x.device)
         g_b = torch.empty_like(g_g)
     ws = torch.empty(int(LIB.vg_ln_act_bwd_ws_floats(c)), dtype=torch.float32, device=x.device)
-    check(LIB.vg_ln_act_bwd(ptr(x), n, c, ptr(gamma), ptr(beta), float(slope), ptr(mean), ptr(rstd), ptr(g_y),
-                            ptr(g_x), ptr(g_g), ptr(g_b), 1 if direct else 0, ptr(ws), stream_handle(x.device)),
-          "vg_ln_act_bwd")
+    args = (ptr(x), n, c, ptr(gamma), ptr(beta), float(slope), ptr(mean), ptr(rstd), ptr(g_y), ptr(g_x), ptr(g_g),
+            ptr(g_b), 1 if direct else 0, ptr(ws))
+    if direct and _FOLDS is not None:  # gamma / beta fold deferred to the context's batch
+        _FOLDS.call(LIB.vg_ln_act_bwd_deferred, args, stream_handle(x.device), keep=(ws,),
+                    name="vg_ln_act_bwd_deferred")
+    else:
+        check(LIB.vg_ln_act_bwd(*args, stream_handle(x.device)), "vg_ln_act_bwd")
     if direct or not want_params:
         return g_x, None, None
     return g_x, g_g, g_b

@@ -113,6 +113,15 @@ class Trainer:
         cfg = self.configuration
         prep = vdata.prepared(local_graph, voxel_graph, cfg.NUM_CLASSES)
         d_fake = self.discriminator(local_graph, voxel_graph, label_hard)
+        hard = label_hard.squeeze(0)
+        if cfg.USE_WGANGP and cfg.NUM_CLASSES > 2:  # fused loss head: same terms, same order
+            far_gen, far_ref = ops.far_per_graph(prep.voxel_x, hard, voxel_graph.ptr, voxel_graph.site_area,
+                                                 far_col=9, dy_col=4, dx_col=5,
+                                                 dim_scale=float(cfg.NORMALIZATION_FACTOR_DIMENSION),
+                                                 void_class=cfg.VOID)
+            return ops.gen_loss_head(d_fake, hard, logits, prep.onehot_f, voxel_graph.type, far_gen, far_ref,
+                                     (cfg.LAMBDA_ADV, cfg.LAMBDA_LABEL, cfg.LAMBDA_RATIO, cfg.LAMBDA_RATIO_VOID,
+                                      cfg.LAMBDA_FAR))
         if cfg.USE_WGANGP:
             adv = -d_fake.mean()
         else:
@@ -120,7 +129,6 @@ class Trainer:
         adv = adv * cfg.LAMBDA_ADV
         ce = F.cross_entropy(logits, voxel_graph.type) * cfg.LAMBDA_LABEL
         n = prep.onehot_f.shape[0]
-        hard = label_hard.squeeze(0)
         ratio_gen = hard.sum(dim=0) / n
         ratio_ref = prep.onehot_f.sum(dim=0) / n
         ratio = F.mse_loss(ratio_gen[:-2], ratio_ref[:-2]) * cfg.LAMBDA_RATIO

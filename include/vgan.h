@@ -294,6 +294,25 @@ int vg_far_per_graph(const float* x, int32_t x_stride, const float* label, int32
                      int32_t far_col, int32_t dy_col, int32_t dx_col, float dim_scale,
                      int32_t void_class, float* far_gen, float* far_ref, void* stream);
 
+/* Generator loss of the WGAN-GP step (trainer.py:334-385; the FAR term carries
+ * no gradient, :380), from the critic scores d_fake [N], label_hard / the
+ * float one-hot of the true types / logits [N, classes], the true types [N]
+ * and the per-building FAR pair [num_graphs] (vg_far_per_graph):
+ *   out[0] = (((-mean(d_fake) l_adv + ratio) + CE l_label) + ratio_void) + far
+ * and the gradient coefficients the backward needs (out has classes + 3
+ * floats).  Deterministic (block partials folded in order). */
+int64_t vg_gen_loss_ws_floats(int32_t N, int32_t classes);
+int vg_gen_loss_fwd(const float* d_fake, const float* hard, const float* logits,
+                    const float* onehot, const int64_t* type, int32_t N, int32_t classes,
+                    const float* far_gen, const float* far_ref, int32_t num_graphs, float l_adv,
+                    float l_label, float l_ratio, float l_void, float l_far, float* out,
+                    float* workspace, void* stream);
+/* d loss / d (d_fake, label_hard, logits) scaled by *g_loss (device scalar);
+ * any output may be NULL (not wanted). */
+int vg_gen_loss_bwd(const float* g_loss, const float* out, const float* logits,
+                    const int64_t* type, int32_t N, int32_t classes, float* g_dfake, float* g_hard,
+                    float* g_logits, void* stream);
+
 /* Confusion matrices for the metrics (trainer.py:387-443): conf[g][t][p] counts
  * (truth t, prediction argmax(label_row)) per building; conf_all sums them. */
 int vg_confusion(const int64_t* truth, const float* label, int32_t classes, const int64_t* ptr,
@@ -406,6 +425,13 @@ int vg_gat_bwd_deferred(const int32_t* row_ptr, const int32_t* col, const int32_
                         float* g_att_src, float* g_att_dst, float* g_bias, int32_t accumulate,
                         const float* inj, int32_t inj_row0, float* workspace, vg_fold* folds_out,
                         int32_t* n_out, void* stream);
+
+/* vg_ln_act_bwd without its fold: 2 descriptors (g_gamma, g_beta). */
+int vg_ln_act_bwd_deferred(const float* x, int32_t N, int32_t C, const float* gamma,
+                           const float* beta, float slope, const float* mean, const float* rstd,
+                           const float* g_y, float* g_x, float* g_gamma, float* g_beta,
+                           int32_t accumulate, float* workspace, vg_fold* folds_out,
+                           int32_t* n_out, void* stream);
 
 /* vg_gat_jvp2_ex without its fold: 2 descriptors (g_att_dst, g_att_src), both
  * accumulating. */

@@ -308,3 +308,35 @@ def test_inference_sweep(cuda, graphed):
     res = sw.run([(loc, vox)] * 2, collect=True)
     assert res["graphs"] == 2 * vox.num_graphs and res["samples"] == 8 * vox.num_graphs
     assert len(res["predictions"]) == 2
+
+
+@pytest.mark.parametrize("l_label", [0.0, 0.3])
+def test_generator_loss_head_matches_composite(cuda, l_label):
+    """vg_gen_loss_fwd/_bwd against the torch restatement of trainer.py:334-385
+    (adv + ratio + CE + ratio_void + FAR, FAR without gradient)."""
+    import torch.nn.functional as F
+
+    from vgan import ops
+
+    torch.manual_seed(9)
+    n, k, g = 3001, 7, 11
+    d_fake = torch.randn(n, 1, device=cuda, requires_grad=True)
+    hard = torch.rand(n, k, device=cuda).requires_grad_(True)
+    logits = torch.randn(n, k, device=cuda, requires_grad=True)
+    vtype = torch.randint(0, k, (n,), device=cuda)
+    onehot = F.one_hot(vtype, k).float()
+    far_gen, far_ref = torch.rand(g, device=cuda), torch.rand(g, device=cuda)
+    lam = (1.0, l_label, 0.1, 0.1, 0.1)
+    loss = ops.gen_loss_head(d_fake, hard, logits, onehot, vtype, far_gen, far_ref, lam)
+    rg, rr = hard.sum(0) / n, onehot.sum(0) / n
+    ref = (-d_fake.mean() * lam[0] + F.mse_loss(rg[:-2], rr[:-2]) * lam[2] + F.cross_entropy(logits, vtype) * lam[1]
+           + F.mse_loss(rg[-2:], rr[-2:]) * lam[3] + F.mse_loss(far_gen, far_ref) * lam[4])
+    assert abs(loss.item() - ref.item()) <= 1e-5 * max(1.0, abs(ref.item()))
+    got = torch.autograd.grad(loss * 1.7, (d_fake, hard, logits), allow_unused=True)
+    want = torch.autograd.grad(ref * 1.7, (d_fake, hard, logits))
+    for a, b in zip(got[:2], want[:2]):
+        assert (a - b).abs().max().item() <= 1e-5 * b.abs().max().item() + 1e-9
+    if l_label == 0.0:
+        assert got[2] is None and want[2].abs().max().item() == 0.0
+    else:
+        assert (got[2] - want[2]).abs().max().item() <= 1e-5 * want[2].abs().max().item()

@@ -15,7 +15,10 @@ def family(name: str) -> str:
     if m:
         return m.group(1)
     m = re.search(r"at::native::(?:\(anonymous namespace\)::)?(\w+)", name)
-    return ("torch:" + m.group(1)) if m else name[:40]
+    if m:
+        f = re.search(r"at::native::(?:\(anonymous namespace\)::)?\w+<[^,]*, at::native::(?:\(anonymous namespace\)::)?(\w+)", name)
+        return "torch:" + m.group(1) + (":" + f.group(1) if f else "")
+    return name[:40]
 
 
 def main():
