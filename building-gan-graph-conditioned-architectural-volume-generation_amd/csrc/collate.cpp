@@ -1,0 +1,173 @@
+// Host-side mini-batch collate of building graphs (libvgan_host.so).
+//
+// Replaces GraphDataset.collate_fn (reference data.py:156-163), i.e. two
+// torch_geometric Batch.from_data_list calls, for buildings held in a
+// GraphStore (vgan/store.py): every node-level array of the selected buildings
+// is concatenated, edge_index is shifted by the running node count, and
+// ptr / batch describe graph membership.  On top of that the collate emits the
+// int32 destination CSR (+ self loops) and its source CSC directly, so the
+// device never rebuilds them (vg_csr_build, csr.hip) and the training loop
+// takes no host sync per batch.
+//
+// Ordering is the one csr.hip produces: inside a CSR row the slots follow the
+// original edge order (remove_self_loops drops i->i), the self loop is last;
+// every CSC bucket is sorted by slot.  Buildings are independent blocks of the
+// block-diagonal graph, so each worker thread owns whole buildings and writes
+// disjoint output ranges whose offsets a serial prefix pass fixes first.
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "../../include/vgan_host.h"
+
+namespace {
+
+struct Plan {
+  std::vector<int64_t> node_off, edge_off, csr_off;  // [count + 1]
+};
+
+// Prefix sums of nodes / raw edges / CSR slots of the selected buildings.
+int plan(const int64_t* node_ptr, const int64_t* edge_ptr, const int32_t* esrc, const int32_t* edst,
+         const int64_t* index, int32_t count, int64_t num_buildings, Plan& p) {
+  p.node_off.assign(count + 1, 0);
+  p.edge_off.assign(count + 1, 0);
+  p.csr_off.assign(count + 1, 0);
+  for (int32_t b = 0; b < count; ++b) {
+    const int64_t g = index[b];
+    if (g < 0 || g >= num_buildings) return VGH_EINDEX;
+    const int64_t n = node_ptr[g + 1] - node_ptr[g];
+    const int64_t e0 = edge_ptr[g], e1 = edge_ptr[g + 1];
+    if (n <= 0 || e1 < e0) return VGH_EINVAL;
+    int64_t loops = 0;
+    if (esrc && edst)
+      for (int64_t e = e0; e < e1; ++e) loops += esrc[e] == edst[e];
+    p.node_off[b + 1] = p.node_off[b] + n;
+    p.edge_off[b + 1] = p.edge_off[b] + (e1 - e0);
+    p.csr_off[b + 1] = p.csr_off[b] + (e1 - e0) - loops + n;
+  }
+  if (p.node_off[count] > INT32_MAX || p.csr_off[count] > INT32_MAX) return VGH_ERANGE;
+  return 0;
+}
+
+// Threads pay off only past ~64k items of work each (a spawn costs ~20 us).
+constexpr int64_t kWorkPerThread = 1 << 16;
+
+template <class F>
+void parallel_buildings(int32_t count, int32_t threads, int64_t work, F&& fn) {
+  const int64_t by_work = std::max<int64_t>(1, work / kWorkPerThread);
+  const int32_t t = static_cast<int32_t>(std::max<int64_t>(1, std::min<int64_t>({threads, count, by_work})));
+  if (t == 1) {
+    for (int32_t b = 0; b < count; ++b) fn(b);
+    return;
+  }
+  std::vector<std::thread> pool;
+  pool.reserve(t);
+  for (int32_t w = 0; w < t; ++w)
+    pool.emplace_back([&, w] {
+      for (int32_t b = w; b < count; b += t) fn(b);
+    });
+  for (auto& th : pool) th.join();
+}
+
+}  // namespace
+
+extern "C" int vgh_collate_sizes(const int64_t* node_ptr, const int64_t* edge_ptr, const int32_t* esrc,
+                                 const int32_t* edst, int64_t num_buildings, const int64_t* index,
+                                 int32_t count, int64_t* sizes) {
+  if (!node_ptr || !edge_ptr || !index || !sizes || count <= 0) return VGH_EINVAL;
+  Plan p;
+  if (int rc = plan(node_ptr, edge_ptr, esrc, edst, index, count, num_buildings, p)) return rc;
+  sizes[0] = p.node_off[count];
+  sizes[1] = p.edge_off[count];
+  sizes[2] = p.csr_off[count];
+  return 0;
+}
+
+extern "C" int vgh_collate_rows(const void* src, int64_t row_bytes, const int64_t* node_ptr,
+                                int64_t num_buildings, const int64_t* index, int32_t count, void* dst,
+                                int32_t threads) {
+  if (!src || !dst || !node_ptr || !index || row_bytes <= 0 || count <= 0) return VGH_EINVAL;
+  std::vector<int64_t> off(count + 1, 0);
+  for (int32_t b = 0; b < count; ++b) {
+    const int64_t g = index[b];
+    if (g < 0 || g >= num_buildings) return VGH_EINDEX;
+    off[b + 1] = off[b] + (node_ptr[g + 1] - node_ptr[g]);
+  }
+  const char* s = static_cast<const char*>(src);
+  char* d = static_cast<char*>(dst);
+  parallel_buildings(count, threads, off[count] * row_bytes / 16, [&](int32_t b) {
+    const int64_t g = index[b];
+    std::memcpy(d + off[b] * row_bytes, s + node_ptr[g] * row_bytes, (off[b + 1] - off[b]) * row_bytes);
+  });
+  return 0;
+}
+
+extern "C" int vgh_collate_graph(const int64_t* node_ptr, const int64_t* edge_ptr, const int32_t* esrc,
+                                 const int32_t* edst, int64_t num_buildings, const int64_t* index,
+                                 int32_t count, int32_t threads, int64_t* ptr, int64_t* batch,
+                                 int64_t* edge_index, int32_t* row_ptr, int32_t* col, int32_t* csc_ptr,
+                                 int32_t* csc_slot, int32_t* csc_dst) {
+  if (!node_ptr || !edge_ptr || !esrc || !edst || !index || count <= 0) return VGH_EINVAL;
+  const bool want_csr = row_ptr && col && csc_ptr && csc_slot && csc_dst;
+  Plan p;
+  if (int rc = plan(node_ptr, edge_ptr, esrc, edst, index, count, num_buildings, p)) return rc;
+  const int64_t n_total = p.node_off[count], e_total = p.edge_off[count];
+
+  // node ids of every edge must lie inside its own building
+  for (int32_t b = 0; b < count; ++b) {
+    const int64_t g = index[b], n = node_ptr[g + 1] - node_ptr[g];
+    for (int64_t e = edge_ptr[g]; e < edge_ptr[g + 1]; ++e)
+      if (esrc[e] < 0 || esrc[e] >= n || edst[e] < 0 || edst[e] >= n) return VGH_EEDGE;
+  }
+  if (ptr)
+    for (int32_t b = 0; b <= count; ++b) ptr[b] = p.node_off[b];
+
+  parallel_buildings(count, threads, n_total + 4 * p.csr_off[count], [&](int32_t b) {
+    const int64_t g = index[b];
+    const int32_t n = static_cast<int32_t>(node_ptr[g + 1] - node_ptr[g]);
+    const int64_t e0 = edge_ptr[g], ne = edge_ptr[g + 1] - e0;
+    const int64_t no = p.node_off[b], eo = p.edge_off[b];
+    const int32_t co = static_cast<int32_t>(p.csr_off[b]);
+    if (batch)
+      for (int32_t i = 0; i < n; ++i) batch[no + i] = b;
+    if (edge_index)
+      for (int64_t e = 0; e < ne; ++e) {
+        edge_index[eo + e] = esrc[e0 + e] + no;
+        edge_index[e_total + eo + e] = edst[e0 + e] + no;
+      }
+    if (!want_csr) return;
+    // destination CSR: counting sort by destination, stable in edge order
+    std::vector<int32_t> cnt(n + 1, 0), cur(n, 0);
+    for (int64_t e = 0; e < ne; ++e)
+      if (esrc[e0 + e] != edst[e0 + e]) ++cnt[edst[e0 + e] + 1];
+    for (int32_t i = 0; i < n; ++i) cnt[i + 1] += cnt[i] + 1;  // + self loop per row
+    for (int32_t i = 0; i < n; ++i) row_ptr[no + i] = co + cnt[i];
+    for (int64_t e = 0; e < ne; ++e) {
+      const int32_t s = esrc[e0 + e], d = edst[e0 + e];
+      if (s == d) continue;
+      col[co + cnt[d] + cur[d]++] = static_cast<int32_t>(s + no);
+    }
+    for (int32_t i = 0; i < n; ++i) col[co + cnt[i + 1] - 1] = static_cast<int32_t>(i + no);
+    // source CSC: visiting slots in ascending order keeps every bucket sorted
+    std::vector<int32_t> sc(n + 1, 0);
+    const int32_t ep = cnt[n];
+    for (int32_t k = 0; k < ep; ++k) ++sc[col[co + k] - no + 1];
+    for (int32_t j = 0; j < n; ++j) sc[j + 1] += sc[j];
+    for (int32_t j = 0; j < n; ++j) csc_ptr[no + j] = co + sc[j];
+    std::fill(cur.begin(), cur.end(), 0);
+    for (int32_t i = 0; i < n; ++i)
+      for (int32_t k = cnt[i]; k < cnt[i + 1]; ++k) {
+        const int32_t j = col[co + k] - static_cast<int32_t>(no);
+        const int32_t pos = co + sc[j] + cur[j]++;
+        csc_slot[pos] = co + k;
+        csc_dst[pos] = static_cast<int32_t>(i + no);
+      }
+  });
+  if (want_csr) {
+    row_ptr[n_total] = static_cast<int32_t>(p.csr_off[count]);
+    csc_ptr[n_total] = static_cast<int32_t>(p.csr_off[count]);
+  }
+  return 0;
+}

@@ -5,7 +5,8 @@ A step runs 6 generator and 16 discriminator forwards over the SAME batch
 once here and cached on the batch object:
 
 * ``csr``              destination CSR + source CSC (``vgan.ops.CSR``), replacing
-                       GATConv's per-layer remove/add self loops;
+                       GATConv's per-layer remove/add self loops; taken as-is
+                       when the host collate (``vgan.store``) already emitted it;
 * ``matched_voxel_x``  [N, F_local + F_voxel] = [type-matched mean | voxel.x],
                        the first block of the discriminator input
                        (``models.py:230-239``) and, sliced, the generator's
@@ -45,7 +46,12 @@ def _build(local_graph, voxel_graph, n_classes: int) -> Prepared:
     lx = local_graph.x.float().contiguous()
     n, fv = vx.shape
     fl = lx.shape[1]
-    csr = ops.CSR(voxel_graph.edge_index, n)
+    getter = getattr(voxel_graph, "derived", None)
+    arrays = getter("csr_arrays") if callable(getter) else None
+    if arrays is not None and arrays[0].device == vx.device and arrays[0].numel() == n + 1:
+        csr = ops.CSR.from_arrays(*arrays)  # emitted by the host collate (vgan.store)
+    else:
+        csr = ops.CSR(voxel_graph.edge_index, n)
     mv = torch.empty(n, fl + fv, dtype=torch.float32, device=vx.device)
     ops.type_mean(lx, local_graph.type, voxel_graph.type, n_classes, out=mv, col0=0)
     mv[:, fl:].copy_(vx)

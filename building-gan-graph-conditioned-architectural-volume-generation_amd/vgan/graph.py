@@ -122,6 +122,10 @@ class GraphBatch(GraphData):
         return GraphData(**out)
 
     def to(self, device, non_blocking: bool = False) -> "GraphBatch":
+        device = torch.device(device)
+        tensors = [v for v in self._store.values() if torch.is_tensor(v)]
+        if tensors and all(_same_device(v.device, device) for v in tensors):
+            return self  # already there: keep the derived structures built on it
         moved = {
             k: (v.to(device, non_blocking=non_blocking) if torch.is_tensor(v) else v)
             for k, v in self._store.items()
@@ -129,6 +133,9 @@ class GraphBatch(GraphData):
         out = GraphBatch(**moved)
         if "ptr_host" in self._derived:
             out._derived["ptr_host"] = self._derived["ptr_host"]
+        if "csr_arrays" in self._derived:  # host-built CSR/CSC (vgan.store) travels with the batch
+            out._derived["csr_arrays"] = tuple(t.to(device, non_blocking=non_blocking)
+                                               for t in self._derived["csr_arrays"])
         return out
 
     # ------------------------------------------------------- derived, per batch
@@ -137,3 +144,11 @@ class GraphBatch(GraphData):
 
     def set_derived(self, key: str, value: Any) -> None:
         self._derived[key] = value
+
+
+def _same_device(a: torch.device, b: torch.device) -> bool:
+    if a.type != b.type:
+        return False
+    if a.type == "cpu":
+        return True
+    return b.index is None or a.index == b.index

@@ -1,0 +1,161 @@
+"""Mini-batch loaders over a ``GraphStore``: the reference's ``GraphDataLoaders``.
+
+``GraphDataLoaders`` (``data.py:166-212``) splits the dataset with
+``random_split(dataset, SPLIT_RATIOS)`` and wraps each part in a
+``DataLoader(batch_size=BATCH_SIZE, shuffle=True, drop_last=False,
+collate_fn=GraphDataset.collate_fn, num_workers=NUM_WORKERS)``.  Here:
+
+* the split and the per-epoch shuffle use the same torch machinery
+  (``random_split`` over the store's indices, a ``DataLoader`` over those
+  indices for the sampling), so they consume the global CPU RNG exactly as the
+  reference does and produce the same building order for the same seed;
+* each epoch's index batches are drawn up front on the calling thread; a
+  background thread then collates them natively (``GraphStore.collate``, the
+  GIL is released inside the C++ collate) into page-locked buffers and issues
+  their host-to-device copies on a side stream, ``prefetch`` batches ahead;
+* the consumer's stream waits on the copy's event, so a yielded
+  ``(local, voxel)`` pair is already device-resident -- the trainer's
+  ``.to(DEVICE)`` (``trainer.py:459-460``) is a no-op -- and carries the
+  host-built CSR/CSC that ``vgan.data`` adopts without a device build.
+"""
+from __future__ import annotations
+
+import queue
+import threading
+from typing import Iterator, List, Optional, Sequence, Tuple
+
+import torch
+from torch.utils.data import DataLoader, random_split
+
+from .graph import GraphBatch
+from .store import GraphStore
+
+
+class _Indices(torch.utils.data.Dataset):
+    def __init__(self, indices: Sequence[int]):
+        self.indices = list(indices)
+
+    def __len__(self) -> int:
+        return len(self.indices)
+
+    def __getitem__(self, i: int) -> int:
+        return self.indices[i]
+
+
+def _as_list(batch) -> List[int]:
+    return [int(v) for v in batch]
+
+
+class GraphLoader:
+    """Iterable of ``(local, voxel)`` GraphBatch pairs over ``indices`` of a store."""
+
+    def __init__(self, store: GraphStore, indices: Optional[Sequence[int]] = None, batch_size: int = 1,
+                 shuffle: bool = True, drop_last: bool = False, device=None, prefetch: int = 2,
+                 threads: int = 4):
+        self.store = store
+        self.indices = list(range(len(store))) if indices is None else [int(i) for i in indices]
+        self.batch_size = int(batch_size)
+        self.shuffle = shuffle
+        self.drop_last = drop_last
+        self.device = torch.device(device) if device is not None else None
+        self.prefetch = max(1, int(prefetch))
+        self.threads = threads
+
+    def __len__(self) -> int:
+        n = len(self.indices)
+        return n // self.batch_size if self.drop_last else (n + self.batch_size - 1) // self.batch_size
+
+    def batches(self) -> List[List[int]]:
+        """This epoch's building indices per batch (consumes the CPU RNG like
+        the reference's DataLoader: a base seed when the iterator is created,
+        then the RandomSampler's seed)."""
+        dl = DataLoader(_Indices(self.indices), batch_size=self.batch_size, shuffle=self.shuffle,
+                        drop_last=self.drop_last, collate_fn=_as_list, num_workers=0)
+        return list(iter(dl))
+
+    def __iter__(self) -> Iterator[Tuple[GraphBatch, GraphBatch]]:
+        plan = self.batches()
+        dev = self.device
+        if dev is None or dev.type != "cuda":
+            for idx in plan:
+                yield self.store.collate(idx, pin=False, threads=self.threads)
+            return
+        yield from _prefetched(self.store, plan, dev, self.prefetch, self.threads)
+
+
+def _prefetched(store: GraphStore, plan: List[List[int]], dev: torch.device, depth: int, threads: int):
+    copy_stream = torch.cuda.Stream(device=dev)
+    q: "queue.Queue" = queue.Queue(maxsize=depth)
+    stop = threading.Event()
+    _END = object()
+
+    def worker():
+        try:
+            for idx in plan:
+                if stop.is_set():
+                    return
+                host = store.collate(idx, pin=True, threads=threads)
+                with torch.cuda.stream(copy_stream):
+                    moved = tuple(g.to(dev, non_blocking=True) for g in host)
+                    ev = torch.cuda.Event()
+                    ev.record(copy_stream)
+                q.put((moved, host, ev))  # host buffers stay referenced until the copy is waited on
+            q.put(_END)
+        except BaseException as exc:  # surfaced on the consumer thread
+            q.put(exc)
+
+    th = threading.Thread(target=worker, name="vgan-loader", daemon=True)
+    th.start()
+    try:
+        while True:
+            item = q.get()
+            if item is _END:
+                return
+            if isinstance(item, BaseException):
+                raise item
+            moved, host, ev = item
+            torch.cuda.current_stream(dev).wait_event(ev)
+            for g in moved:  # the consumer stream now owns these allocations
+                for t in _tensors(g):
+                    t.record_stream(torch.cuda.current_stream(dev))
+            del host
+            yield moved
+    finally:
+        stop.set()
+        while th.is_alive():
+            try:
+                q.get(timeout=0.1)
+            except queue.Empty:
+                pass
+        th.join()
+
+
+def _tensors(g: GraphBatch):
+    for key in g.keys():
+        v = getattr(g, key)
+        if torch.is_tensor(v):
+            yield v
+    arrays = g.derived("csr_arrays")
+    if arrays is not None:
+        yield from arrays
+
+
+class GraphDataLoaders:
+    """``train_dataloader`` / ``validation_dataloader`` / ``test_dataloader`` of
+    the reference (``data.py:166-212``) over a GraphStore."""
+
+    def __init__(self, configuration, store: GraphStore, device=None, prefetch: int = 2):
+        self.configuration = configuration
+        self.sanity_checking = bool(getattr(configuration, "SANITY_CHECKING", False))
+        self.dataset = store
+        indices = list(range(len(store)))[: int(getattr(configuration, "DATA_SLICER", len(store)))]  # data.py:97-98
+        if self.sanity_checking:  # data.py:100-102: one building, no validation / test loaders
+            indices = [indices[int(getattr(configuration, "DATA_POINT", 0))]]
+        parts = random_split(indices, configuration.SPLIT_RATIOS)
+        kw = dict(batch_size=configuration.BATCH_SIZE, shuffle=True, drop_last=False, device=device,
+                  prefetch=prefetch)
+        self.train_dataloader = GraphLoader(store, [indices[i] for i in parts[0].indices], **kw)
+        self.validation_dataloader = None if self.sanity_checking else \
+            GraphLoader(store, [indices[i] for i in parts[1].indices], **kw)
+        self.test_dataloader = None if self.sanity_checking else \
+            GraphLoader(store, [indices[i] for i in parts[2].indices], **kw)

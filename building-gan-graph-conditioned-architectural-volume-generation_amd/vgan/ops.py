@@ -64,6 +64,25 @@ class CSR:
         self.csc_ptr, self.csc_slot, self.csc_dst = csc_ptr, csc_slot[:ep], csc_dst[:ep]
         self.device = dev
 
+    @classmethod
+    def from_arrays(cls, row_ptr: torch.Tensor, col: torch.Tensor, csc_ptr: torch.Tensor, csc_slot: torch.Tensor,
+                    csc_dst: torch.Tensor) -> "CSR":
+        """The same structure from arrays built elsewhere -- the host collate of
+        ``vgan.store`` emits them in csr.hip's order -- with no device build and
+        no host sync."""
+        for t in (row_ptr, col, csc_ptr, csc_slot, csc_dst):
+            if not t.is_cuda or t.dtype != torch.int32 or t.dim() != 1:
+                raise ValueError("CSR arrays must be int32 vectors on a ROCm device")
+        n, ep = row_ptr.numel() - 1, col.numel()
+        if csc_ptr.numel() != n + 1 or csc_slot.numel() != ep or csc_dst.numel() != ep or n <= 0:
+            raise ValueError("inconsistent CSR / CSC array sizes")
+        self = cls.__new__(cls)
+        self.num_nodes, self.num_edges = n, ep
+        self.row_ptr, self.col = row_ptr, col
+        self.csc_ptr, self.csc_slot, self.csc_dst = csc_ptr, csc_slot, csc_dst
+        self.device = row_ptr.device
+        return self
+
     def stream(self):
         return stream_handle(self.device)
 

@@ -264,3 +264,32 @@ class Dataset:
 
     def __init__(self, *args, **kwargs):
         pass
+
+
+# ------------------------------------------------- message order (index view)
+def gat_csr(edge_index: torch.Tensor, num_nodes: int):
+    """(row_ptr, col, csc_ptr, csc_slot, csc_dst) of the edge list GATConv
+    propagates over -- add_self_loops(remove_self_loops(edge_index)) -- grouped
+    by destination in the order the scatter visits the edges (original edge
+    order, the appended self loop last), and its transpose grouped by source in
+    slot order.  Pure-Python loops: small graphs only (test checker for
+    csr.hip and the host collate)."""
+    ei = add_self_loops(remove_self_loops(edge_index), num_nodes).tolist()
+    rows = [[] for _ in range(num_nodes)]
+    for s, d in zip(ei[0], ei[1]):
+        rows[d].append(s)
+    row_ptr, col = [0], []
+    for r in rows:
+        col.extend(r)
+        row_ptr.append(len(col))
+    buckets = [[] for _ in range(num_nodes)]
+    for i in range(num_nodes):
+        for k in range(row_ptr[i], row_ptr[i + 1]):
+            buckets[col[k]].append((k, i))
+    csc_ptr, csc_slot, csc_dst = [0], [], []
+    for b in buckets:
+        csc_slot.extend(k for k, _ in b)
+        csc_dst.extend(i for _, i in b)
+        csc_ptr.append(len(csc_slot))
+    as_i32 = lambda v: torch.tensor(v, dtype=torch.int32)  # noqa: E731
+    return as_i32(row_ptr), as_i32(col), as_i32(csc_ptr), as_i32(csc_slot), as_i32(csc_dst)

@@ -1,0 +1,251 @@
+"""Data path on the CPU: raw-JSON converter vs the reference, GraphStore round
+trip, native collate vs Batch.from_data_list, host CSR vs the oracle, loaders'
+split / shuffle vs the reference's torch calls, and the host library's ABI."""
+import ctypes
+import json
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+from parity_util import PKG_ROOT, ROOT
+
+GOLDEN = os.path.join(ROOT, "tests", "golden", "convert_small.pt")
+HOST_HEADER = os.path.join(ROOT, "include", "vgan_host.h")
+
+
+def _equal(a, b, what):
+    if torch.is_tensor(a):
+        assert torch.is_tensor(b), what
+        assert a.dtype == b.dtype, (what, a.dtype, b.dtype)
+        assert a.shape == b.shape, (what, a.shape, b.shape)
+        assert torch.equal(a, b), what
+    else:
+        assert a == b, what
+
+
+def _same_graph(a, b, what=""):
+    assert a.keys() == b.keys(), (what, a.keys(), b.keys())
+    for k in a.keys():
+        _equal(getattr(a, k), getattr(b, k), f"{what}.{k}")
+
+
+# ------------------------------------------------------------------ converter
+def test_converter_matches_reference_process_data():
+    from vgan import convert
+    from vgan.config import Configuration
+
+    fx = torch.load(GOLDEN, weights_only=True)
+    cfg = Configuration()
+    assert len(fx["buildings"]) == 3
+    for b in fx["buildings"]:
+        lo, vo = convert.process_building(json.loads(b["global_json"]), json.loads(b["local_json"]),
+                                          json.loads(b["voxel_json"]), cfg, b["data_number"])
+        for prefix, got in (("local.", lo), ("voxel.", vo)):
+            want = {k[len(prefix):]: v for k, v in b.items() if k.startswith(prefix)}
+            assert set(got) - {"data_number"} == set(want), (prefix, sorted(got), sorted(want))
+            for k, v in want.items():
+                _equal(got[k], v, prefix + k)
+            assert got["data_number"] == b["data_number"]
+
+
+def test_convert_directories_to_store(tmp_path):
+    from vgan import convert
+    from vgan.config import Configuration
+    from vgan.store import GraphStore
+
+    fx = torch.load(GOLDEN, weights_only=True)
+    dirs = {k: tmp_path / k for k in ("global", "local", "voxel")}
+    for d in dirs.values():
+        d.mkdir()
+    numbers = []
+    for b in fx["buildings"]:
+        n = b["data_number"]
+        numbers.append(n)
+        (dirs["global"] / f"global_graph_data_{n}.json").write_text(b["global_json"])
+        (dirs["local"] / f"local_graph_data_{n}.json").write_text(b["local_json"])
+        (dirs["voxel"] / f"voxel_data_{n}.json").write_text(b["voxel_json"])
+    cfg = Configuration()
+    st = convert.convert_directories(str(dirs["global"]), str(dirs["local"]), str(dirs["voxel"]),
+                                     str(tmp_path / "store"), cfg)
+    assert isinstance(st, GraphStore) and len(st) == 3
+    for i, b in enumerate(fx["buildings"]):
+        lg, vg = st[i]
+        m, n = lg.x.shape[0], vg.x.shape[0]
+        _equal(lg.x, b["local.x"], "local.x")
+        _equal(vg.x, b["voxel.x"], "voxel.x")
+        _equal(vg.edge_index, b["voxel.edge_index"], "voxel.edge_index")
+        _equal(lg.edge_index, b["local.edge_index"], "local.edge_index")
+        _equal(vg.type, b["voxel.voxel_graph_types"], "voxel.type")
+        _equal(vg.node_ratio, b["voxel.voxel_graph_node_ratio"], "voxel.node_ratio")
+        _equal(lg.node_ratio, b["local.local_graph_type_ratio_per_node"], "local.node_ratio")
+        # the store keeps one dtype per key (torch promotion over the dataset)
+        _equal(vg.site_area, b["voxel.site_area"].repeat(n).to(vg.site_area.dtype), "voxel.site_area")
+        assert lg.data_number == [numbers[i]] * m and vg.data_number == [numbers[i]] * n
+
+
+def test_converter_maps_void_old():
+    from vgan import convert
+    from vgan.config import Configuration
+
+    cfg = Configuration()
+    fx = torch.load(GOLDEN, weights_only=True)
+    b = fx["buildings"][0]
+    vox = json.loads(b["voxel_json"])
+    assert any(v["type"] == cfg.VOID_OLD for v in vox["voxel_node"])
+    _, vo = convert.process_building(json.loads(b["global_json"]), json.loads(b["local_json"]), vox, cfg, "1")
+    assert int(vo["voxel_graph_types"].min()) >= 0
+    assert int((vo["voxel_graph_types"] == cfg.VOID).sum()) >= sum(v["type"] == cfg.VOID_OLD for v in vox["voxel_node"])
+
+
+# ---------------------------------------------------------------- store/collate
+@pytest.fixture(scope="module")
+def synth_store(tmp_path_factory):
+    from vgan import store, synth
+
+    ds = synth.SyntheticDataset(10, seed=11)
+    path = tmp_path_factory.mktemp("store")
+    return ds, store.write_store(str(path), ds)
+
+
+def test_store_items_round_trip(synth_store):
+    ds, st = synth_store
+    assert len(st) == len(ds)
+    for i in range(len(ds)):
+        for a, b, kind in zip(st[i], ds[i], ("local", "voxel")):
+            _same_graph(a, b, f"{kind}[{i}]")
+
+
+@pytest.mark.parametrize("indices", [[0], [3, 1, 4], [9, 8, 7, 6, 5, 4, 3, 2, 1, 0], [2, 2, 5]])
+def test_native_collate_matches_from_data_list(synth_store, indices):
+    ds, st = synth_store
+    got = st.collate(indices, threads=3)
+    want = ds.collate_fn([ds[i] for i in indices])
+    for a, b, kind in zip(got, want, ("local", "voxel")):
+        _same_graph(a, b, kind)
+        assert a.num_graphs == len(indices)
+        for gi in range(len(indices)):  # batch[gi] slices the building back out
+            _same_graph(a[gi], b[gi], f"{kind}[{gi}]")
+
+
+def _random_graph(rng, n, e, loops=True):
+    src = rng.integers(0, n, e)
+    dst = rng.integers(0, n, e)
+    if loops:
+        k = rng.integers(0, n, max(1, e // 10))
+        src = np.concatenate([src, k])
+        dst = np.concatenate([dst, k])
+    return torch.from_numpy(np.stack([src, dst]).astype(np.int64))
+
+
+def test_host_csr_matches_oracle(tmp_path):
+    """Self loops in the input, duplicate edges, isolated nodes, a one-node building."""
+    from oracle import pyg
+    from vgan.graph import GraphData
+    from vgan.store import GraphStore
+
+    rng = np.random.default_rng(3)
+    items = []
+    for n, e in ((7, 20), (1, 0), (30, 90), (12, 0), (50, 400)):
+        ei = _random_graph(rng, n, e, loops=e > 0)
+        g = GraphData(x=torch.randn(n, 3), edge_index=ei, type=torch.zeros(n, dtype=torch.int64))
+        items.append((g, g))
+    st = GraphStore.write(str(tmp_path / "s"), items)
+    for order in ([0, 1, 2, 3, 4], [4, 2, 0], [1], [3, 3]):
+        _, vg = st.collate(order, threads=2)
+        want = pyg.gat_csr(vg.edge_index, vg.x.shape[0])
+        got = vg.derived("csr_arrays")
+        for name, a, b in zip(("row_ptr", "col", "csc_ptr", "csc_slot", "csc_dst"), got, want):
+            _equal(a, b, name)
+
+
+def test_store_rejects_bad_input(tmp_path, synth_store):
+    from vgan.graph import GraphData
+    from vgan.store import GraphStore
+
+    _, st = synth_store
+    with pytest.raises(ValueError):
+        st.collate([len(st)])
+    with pytest.raises(ValueError):
+        st.collate([])
+    g = GraphData(x=torch.zeros(3, 2), edge_index=torch.tensor([[0, 3], [1, 0]]))
+    with pytest.raises(ValueError):
+        GraphStore.write(str(tmp_path / "bad"), [(g, g)])
+    with pytest.raises(OSError):
+        GraphStore(str(tmp_path))  # no store there
+
+
+# -------------------------------------------------------------------- loaders
+def test_loader_shuffle_matches_reference_dataloader(synth_store):
+    """Same seed -> same building order as the reference's DataLoader(shuffle=True)."""
+    from torch.utils.data import DataLoader, Subset
+
+    from vgan.loader import GraphLoader
+
+    ds, st = synth_store
+    idx = [7, 2, 9, 0, 4, 5]
+    torch.manual_seed(123)
+    ref = DataLoader(Subset(list(range(len(ds))), idx), batch_size=4, shuffle=True, collate_fn=list)
+    want = [list(b) for b in ref] + [list(b) for b in ref]  # two epochs
+    after_ref = torch.rand(1)
+    torch.manual_seed(123)
+    loader = GraphLoader(st, idx, batch_size=4, shuffle=True)
+    got = loader.batches() + loader.batches()
+    assert got == want
+    assert torch.equal(torch.rand(1), after_ref)  # same RNG consumption
+    batches = list(loader)
+    assert len(batches) == len(loader) == 2
+    assert sum(b[1].num_graphs for b in batches) == len(idx)
+
+
+def test_graph_data_loaders_split_matches_reference(synth_store):
+    from torch.utils.data import random_split
+
+    from vgan.config import Configuration
+    from vgan.loader import GraphDataLoaders
+
+    _, st = synth_store
+    cfg = Configuration()
+    cfg.BATCH_SIZE = 3
+    torch.manual_seed(5)
+    parts = random_split(list(range(len(st))), cfg.SPLIT_RATIOS)
+    torch.manual_seed(5)
+    dl = GraphDataLoaders(cfg, st)
+    for p, loader in zip(parts, (dl.train_dataloader, dl.validation_dataloader, dl.test_dataloader)):
+        assert loader.indices == list(p.indices)
+    assert sorted(dl.train_dataloader.indices + dl.validation_dataloader.indices + dl.test_dataloader.indices) \
+        == list(range(len(st)))
+
+
+def test_graph_data_loaders_sanity_mode(synth_store):
+    from vgan.config import Configuration
+    from vgan.loader import GraphDataLoaders
+
+    _, st = synth_store
+    cfg = Configuration(sanity_checking=True)
+    cfg.DATA_POINT = 4
+    dl = GraphDataLoaders(cfg, st)
+    assert dl.train_dataloader.indices == [4]
+    assert dl.validation_dataloader is None and dl.test_dataloader is None
+
+
+# ------------------------------------------------------------------------ ABI
+def _host_header_symbols():
+    text = re.sub(r"/\*.*?\*/", "", open(HOST_HEADER).read(), flags=re.S)
+    return sorted(set(re.findall(r"\b(vgh_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_host_library_exports_header():
+    from vgan import store
+
+    lib = os.path.join(PKG_ROOT, "vgan", "libvgan_host.so")
+    assert os.path.exists(lib), "run __graft_entry__.build() first"
+    out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (vgh_[a-z0-9_]+)$", out, flags=re.M))
+    syms = _host_header_symbols()
+    assert syms and not [s for s in syms if s not in exported]
+    assert sorted(store.HOST_SIGNATURES) == syms
+    ctypes.CDLL(lib)
