@@ -71,7 +71,9 @@ __host__ __device__ inline Lay lay_for(int C) {
 // Partials of one (chunk, 64-column slab, segment); counter is unused (the
 // former last-block fold: one workgroup folding every partial ran at a single
 // CU's bandwidth).
-__global__ void __launch_bounds__(kBlock) k_stats_partial(const float* __restrict__ x, int N, int C,
+// T = float (rows of C) or _Float16 (rows of ld >= C, the f16 inference path).
+template <typename T>
+__global__ void __launch_bounds__(kBlock) k_stats_partial(const T* __restrict__ x, int N, int C, int ld,
                                                           float* __restrict__ part,
                                                           float* __restrict__ stats, int* counter) {
   float* const part0 = part;
@@ -84,13 +86,13 @@ __global__ void __launch_bounds__(kBlock) k_stats_partial(const float* __restric
   const int r0 = blockIdx.x * rows_per_chunk;
   const int r1 = min(N, r0 + rows_per_chunk);
   const bool col_ok = c < C && (lane & (ly.cw - 1)) < 64;
-  x += (size_t)blockIdx.z * N * C;  // segment
+  x += (size_t)blockIdx.z * N * ld;  // segment
   part += (size_t)blockIdx.z * gridDim.x * C * 3;
   Welford w = {0.f, 0.f, 0.f};
   if (col_ok) {
 #pragma unroll 4
     for (int r = r0 + rsub; r < r1; r += rstep) {
-      const float v = x[(size_t)r * C + c];
+      const float v = static_cast<float>(x[(size_t)r * ld + c]);
       w.n += 1.f;
       const float d = v - w.mean;
       w.mean += d / w.n;
@@ -144,27 +146,27 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// One wave per (column, segment): grid (C / 4, S).
 __global__ void __launch_bounds__(kBlock) k_stats_final(const float* __restrict__ part, int chunks,
                                                         int C, int S, float* __restrict__ stats) {
   const int c = fold_col(), lane = threadIdx.x & 63;
-  if (c >= C) return;
-  for (int sg = 0; sg < S; ++sg) {
-    const float* pp = part + (size_t)sg * chunks * C * 3;
-    float v[kFoldU][3];
+  const int sg = blockIdx.y;
+  if (c >= C || sg >= S) return;
+  const float* pp = part + (size_t)sg * chunks * C * 3;
+  float v[kFoldU][3];
 #pragma unroll
-    for (int u = 0; u < kFoldU; ++u) {
-      const int k = lane + 64 * u;
+  for (int u = 0; u < kFoldU; ++u) {
+    const int k = lane + 64 * u;
 #pragma unroll
-      for (int q = 0; q < 3; ++q) v[u][q] = k < chunks ? pp[((size_t)k * C + c) * 3 + q] : 0.f;
-    }
-    Welford acc = {0.f, 0.f, 0.f};
+    for (int q = 0; q < 3; ++q) v[u][q] = k < chunks ? pp[((size_t)k * C + c) * 3 + q] : 0.f;
+  }
+  Welford acc = {0.f, 0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < kFoldU; ++u) acc = merge(acc, Welford{v[u][0], v[u][1], v[u][2]});
-    acc = wave_merge(acc);
-    if (lane == 0) {
-      stats[(size_t)sg * 2 * C + c] = acc.mean;
-      stats[(size_t)sg * 2 * C + C + c] = sqrtf(fmaxf(acc.m2 / acc.n, 0.f));
-    }
+  for (int u = 0; u < kFoldU; ++u) acc = merge(acc, Welford{v[u][0], v[u][1], v[u][2]});
+  acc = wave_merge(acc);
+  if (lane == 0) {
+    stats[(size_t)sg * 2 * C + c] = acc.mean;
+    stats[(size_t)sg * 2 * C + C + c] = sqrtf(fmaxf(acc.m2 / acc.n, 0.f));
   }
 }
 
@@ -193,6 +195,37 @@ __global__ void k_gn_apply(const float* __restrict__ x, long long total, int C, 
       r *= keep[t];
     }
     y[t] = r;
+  }
+}
+
+// f16 rows (inference): y = relu(GraphNorm(x)) over ld-strided rows, two
+// channels per thread; columns C .. wcols-1 (wcols = C rounded up to 8) are
+// written as 0, so y may be a column slice of a wider row (ldy).
+__global__ void k_gn_apply_h(const _Float16* __restrict__ x, long long pairs, int C, int ld, int wcols,
+                             long long seg_rows, const float* __restrict__ w, const float* __restrict__ b,
+                             const float* __restrict__ ms, float eps, const float* __restrict__ stats,
+                             _Float16* __restrict__ y, int ldy) {
+  const int hp = wcols / 2;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < pairs;
+       t += (long long)gridDim.x * blockDim.x) {
+    const long long row = t / hp;
+    const int c = 2 * static_cast<int>(t % hp);
+    const float* st = stats + 2 * C * (row / seg_rows);
+    const _Float16* xp = x + row * ld + c;
+    float r[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int cc = c + q;
+      if (cc < C) {
+        const float z = ((static_cast<float>(xp[q]) - st[cc] * ms[cc]) / (st[C + cc] + eps)) * w[cc] + b[cc];
+        r[q] = z > 0.f ? z : 0.f;
+      } else {
+        r[q] = 0.f;
+      }
+    }
+    _Float16* yp = y + row * ldy + c;
+    yp[0] = static_cast<_Float16>(r[0]);
+    yp[1] = static_cast<_Float16>(r[1]);
   }
 }
 
@@ -273,31 +306,41 @@ __global__ void __launch_bounds__(kBlock) k_gn_bwd_final(
   const int c = fold_col(), lane = threadIdx.x & 63;
   if (c >= C) return;
   float tw = 0.f, tb = 0.f, tm = 0.f;
-  for (int sg = 0; sg < S; ++sg) {
-    const float* pp = part + (size_t)sg * chunks * C * 2;
-    float va[kFoldU], vb[kFoldU];
+  constexpr int kSegs = 4;  // segments whose partials are in flight together
+  for (int s0 = 0; s0 < S; s0 += kSegs) {
+    float va[kSegs][kFoldU], vb[kSegs][kFoldU];
 #pragma unroll
-    for (int u = 0; u < kFoldU; ++u) {
-      const int k = lane + 64 * u;
-      va[u] = k < chunks ? pp[((size_t)k * C + c) * 2] : 0.f;
-      vb[u] = k < chunks ? pp[((size_t)k * C + c) * 2 + 1] : 0.f;
-    }
-    float a = 0.f, bb = 0.f;
+    for (int j = 0; j < kSegs; ++j) {
+      const float* pp = part + (size_t)(s0 + j) * chunks * C * 2;
 #pragma unroll
-    for (int u = 0; u < kFoldU; ++u) {
-      a += va[u];
-      bb += vb[u];
+      for (int u = 0; u < kFoldU; ++u) {
+        const int k = lane + 64 * u;
+        const bool ok = s0 + j < S && k < chunks;
+        va[j][u] = ok ? pp[((size_t)k * C + c) * 2] : 0.f;
+        vb[j][u] = ok ? pp[((size_t)k * C + c) * 2 + 1] : 0.f;
+      }
     }
-    a = wave_sum(a);
-    bb = wave_sum(bb);
-    const float* st = stats + (size_t)sg * 2 * C;
-    if (lane == 0) {
-      sums[(size_t)sg * 2 * C + c] = a;
-      sums[(size_t)sg * 2 * C + C + c] = bb;
+#pragma unroll
+    for (int j = 0; j < kSegs; ++j) {
+      const int sg = s0 + j;
+      if (sg >= S) break;
+      float a = 0.f, bb = 0.f;
+#pragma unroll
+      for (int u = 0; u < kFoldU; ++u) {
+        a += va[j][u];
+        bb += vb[j][u];
+      }
+      a = wave_sum(a);
+      bb = wave_sum(bb);
+      const float* st = stats + (size_t)sg * 2 * C;
+      if (lane == 0) {
+        sums[(size_t)sg * 2 * C + c] = a;
+        sums[(size_t)sg * 2 * C + C + c] = bb;
+      }
+      tw += bb;
+      tb += a;
+      tm += -st[c] * w[c] * a / (st[C + c] + eps);
     }
-    tw += bb;
-    tb += a;
-    tm += -st[c] * w[c] * a / (st[C + c] + eps);
   }
   if (lane == 0 && g_w) {
     g_w[c] = accumulate ? g_w[c] + tw : tw;
@@ -498,15 +541,35 @@ static int gn_fwd(const float* x, int32_t S, int32_t N, int32_t C, const float* 
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int chunks = chunks_for(N);
   dim3 grid(chunks, (C + 63) / 64, S);
-  k_stats_partial<<<grid, kBlock, 0, s>>>(x, N, C, ws, stats, nullptr);
+  k_stats_partial<float><<<grid, kBlock, 0, s>>>(x, N, C, C, ws, stats, nullptr);
   (void)sync;  // former last-block-fold counter: accepted, unused
-  k_stats_final<<<vg_blocks(C, kBlock / 64), kBlock, 0, s>>>(ws, chunks, C, S, stats);
+  k_stats_final<<<dim3(vg_blocks(C, kBlock / 64), S), kBlock, 0, s>>>(ws, chunks, C, S, stats);
   const long long total = (long long)S * N * C;
   k_gn_apply<<<apply_blocks(total), 256, 0, s>>>(x, total, C, (long long)N * C, weight, bias,
                                                  mean_scale, keep, eps, stats, y, p_drop,
                                                  (unsigned long long)seed,
                                                  reinterpret_cast<const long long*>(iter), salt,
                                                  keep_out);
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int vg_graphnorm_fwd_h(const uint16_t* x, int32_t ld, int32_t S, int32_t N, int32_t C,
+                                  const float* weight, const float* bias, const float* mean_scale, float eps,
+                                  uint16_t* y, int32_t ldy, float* stats, float* ws, void* stream) {
+  const int wcols = (C + 7) / 8 * 8;
+  if (S <= 0 || N <= 0 || C <= 0 || ld < wcols || ld % 8 || ldy < wcols || ldy % 8 || !x || !weight || !bias ||
+      !mean_scale || !y || !stats || !ws)
+    return VG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const _Float16* X = reinterpret_cast<const _Float16*>(x);
+  const int chunks = chunks_for(N);
+  dim3 grid(chunks, (C + 63) / 64, S);
+  k_stats_partial<_Float16><<<grid, kBlock, 0, s>>>(X, N, C, ld, ws, stats, nullptr);
+  k_stats_final<<<dim3(vg_blocks(C, kBlock / 64), S), kBlock, 0, s>>>(ws, chunks, C, S, stats);
+  const long long pairs = (long long)S * N * (wcols / 2);
+  k_gn_apply_h<<<apply_blocks(pairs), 256, 0, s>>>(X, pairs, C, ld, wcols, (long long)N, weight, bias,
+                                                   mean_scale, eps, stats, reinterpret_cast<_Float16*>(y), ldy);
   VG_CHECK_LAUNCH();
   return 0;
 }

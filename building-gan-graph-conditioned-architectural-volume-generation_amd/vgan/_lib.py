@@ -46,6 +46,16 @@ SIGNATURES = {
     "vg_gat_jvp2_deferred": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p,
                                             _c_p, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
                                             _c_p, _c_p, _c_p, _c_p]),
+    "vg_hgemm": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_i32, _c_f32, _c_p,
+                                _c_i32, _c_i32, _c_p]),
+    "vg_hgemm_ln_act": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_f32,
+                                       _c_f32, _c_p, _c_i32, _c_p]),
+    "vg_hgat_lin_att": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_i32,
+                                       _c_p, _c_p, _c_p]),
+    "vg_hgat_fwd": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_i32,
+                                   _c_p]),
+    "vg_graphnorm_fwd_h": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_f32, _c_p,
+                                          _c_i32, _c_p, _c_p, _c_p]),
     "vg_csr_ws_ints": (_c_i64, [_c_i64, _c_i32]),
     "vg_csr_build": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "vg_gat_fwd": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p,

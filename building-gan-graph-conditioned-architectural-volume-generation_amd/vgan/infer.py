@@ -35,10 +35,21 @@ def geometric_taus(t0: float = 1.0, t1: float = 0.1, steps: int = 10) -> List[fl
 
 
 class InferenceSweep:
-    def __init__(self, generator, taus: Sequence[float], graphed: bool = False):
+    """``dtype="f16"`` runs the forward on the f16 kernels (``vgan.half``,
+    configs[4]'s precision); "f32" on the training path's kernels."""
+
+    def __init__(self, generator, taus: Sequence[float], graphed: bool = False, dtype: str = "f32"):
+        if dtype not in ("f32", "f16"):
+            raise ValueError(f"dtype {dtype!r}: f32 or f16")
         self.G = generator
         self.taus = [float(t) for t in taus]
         self.graphed = graphed
+        self.dtype = dtype
+        self.half = None
+        if dtype == "f16":
+            from .half import HalfGenerator
+
+            self.half = HalfGenerator(generator)
         dev = next(generator.parameters()).device
         self.tau_t = torch.tensor(self.taus, dtype=torch.float32, device=dev)
         # one memory pool for every batch's graph: replays are sequential and
@@ -57,6 +68,9 @@ class InferenceSweep:
         k = len(self.taus)
         n = voxel_graph.num_nodes
         z = G.rng.normal((k, n, G.configuration.Z_DIM), voxel_graph.x.device)
+        if self.half is not None:
+            _, hard, _ = self.half(local_graph, voxel_graph, z, tau=self.tau_t)
+            return hard.reshape(k, n, -1).argmax(-1).to(torch.int8)
         saved = G.tau
         G.tau = self.tau_t
         try:
@@ -111,5 +125,5 @@ class InferenceSweep:
 
 
 def sweep(generator, batches, taus: Optional[Sequence[float]] = None, graphed: bool = False,
-          collect: bool = False) -> Dict[str, object]:
-    return InferenceSweep(generator, taus or geometric_taus(), graphed).run(batches, collect)
+          collect: bool = False, dtype: str = "f32") -> Dict[str, object]:
+    return InferenceSweep(generator, taus or geometric_taus(), graphed, dtype).run(batches, collect)

@@ -461,6 +461,50 @@ int vg_adam_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_
                 double beta1, double beta2, float eps, float weight_decay, const double* lr,
                 const int32_t* step, void* stream);
 
+/* ---- f16 inference path (BASELINE.json configs[4]) ----------------------- */
+
+/* Generator forward in IEEE binary16 for the inference sweep.  f16 buffers are
+ * passed as uint16_t bit patterns; every row has a leading dimension (ld*) that
+ * is a multiple of 8 halves, and a buffer's columns between its width and that
+ * width rounded up to 8 hold zeros (written by the producing kernel).  K (or
+ * cin) counts the A columns read and must be a multiple of 8: the caller pads
+ * A with zero columns and W with zero columns to that width.  Accumulation is
+ * f32; biases, LayerNorm / GraphNorm parameters and attention vectors are f32.
+ * An f16 output is written over its width rounded up to 8 columns, so it may
+ * be a column slice of a wider row buffer (ldo = that buffer's stride). */
+
+/* y = act(A W^T + bias): nn.Linear (models.py:31,145 decoder head); act 0 none,
+ * 1 ReLU, 2 LeakyReLU(slope); out_f32 != 0 writes f32 rows (the logits). */
+int vg_hgemm(const uint16_t* a, int32_t lda, const uint16_t* w, int32_t ldw, int32_t n, int32_t m,
+             int32_t k, const float* bias, int32_t act, float slope, void* out, int32_t ldo,
+             int32_t out_f32, void* stream);
+
+/* y = LeakyReLU(LayerNorm(A W^T + bias)) for m <= 128 outputs: one
+ * [Linear, LayerNorm, LeakyReLU] block of the MLPs (models.py:22-31). */
+int vg_hgemm_ln_act(const uint16_t* a, int32_t lda, const uint16_t* w, int32_t ldw, int32_t n,
+                    int32_t m, int32_t k, const float* bias, const float* gamma, const float* beta,
+                    float eps, float slope, uint16_t* out, int32_t ldo, void* stream);
+
+/* GATConv.lin plus the attention projections (h . att_src, h . att_dst; f32)
+ * in the epilogue: the f16 vg_gat_lin_att (models.py:72,82). */
+int vg_hgat_lin_att(const uint16_t* x, int32_t ldx, const uint16_t* w, int32_t ldw, int32_t n,
+                    int32_t cin, int32_t cout, const float* att_src, const float* att_dst,
+                    uint16_t* h, int32_t ldh, float* a_src, float* a_dst, void* stream);
+
+/* GATConv edge softmax + CSR gather-sum + bias over f16 rows of ld = c
+ * rounded up to 8 channels (8 / 16 / 32 / 64 / 128): the f16
+ * vg_gat_aggregate_fwd (torch_geometric GATConv.propagate, models.py:144). */
+int vg_hgat_fwd(const int32_t* row_ptr, const int32_t* col, int32_t n, int32_t c, int32_t ld,
+                const uint16_t* h, const float* a_src, const float* a_dst, const float* bias,
+                float slope, uint16_t* out, int32_t ldo, void* stream);
+
+/* ReLU(GraphNorm(x)) (eval: no dropout) over S stacked segments of n f16 rows
+ * (models.py:73-75,83-85); statistics f32 ([S][2C] like vg_graphnorm_fwd_seg,
+ * workspace S * 256 * C * 3 floats). */
+int vg_graphnorm_fwd_h(const uint16_t* x, int32_t ld, int32_t S, int32_t N, int32_t C,
+                       const float* weight, const float* bias, const float* mean_scale, float eps,
+                       uint16_t* y, int32_t ldy, float* stats, float* ws, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,171 @@
+"""f16 inference path (configs[4]): every f16 kernel against an f32 reference
+of the same op on the same (f16-representable) inputs, the whole f16 generator
+forward against the f32 one, and the graphed f16 inference sweep.
+
+Tolerances: a kernel's f16 output may differ from the f32 reference by the
+final rounding to binary16 (relative 2^-11) plus f32 accumulation-order
+differences -- bounded here by 4e-3 relative to the output scale.  The whole
+forward (5 + 5 + 4 + 1 GEMM layers, 14 GAT blocks through a 1-channel
+bottleneck whose GraphNorm rescales every rounding error) compounds f16 storage
+rounding: bounded by 2e-2 RMS relative error of the logits, 5e-2 (99th
+percentile) and 0.2 (max) of their scale, and >= 97% agreement of the
+predicted types (argmax of the logits)."""
+import pytest
+import torch
+
+from vgan import data as vdata
+from vgan import ops
+from vgan._lib import LIB, check, ptr, stream_handle
+from vgan.config import Configuration
+from vgan.half import HalfGenerator, _r8
+from vgan.infer import InferenceSweep, geometric_taus
+from vgan.models import VoxelGNNGenerator
+from vgan.synth import SyntheticDataset
+
+pytestmark = pytest.mark.gpu
+
+
+def _h16(rows, cols, ld, dev, scale=1.0, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.zeros(rows, ld, dtype=torch.float16)
+    x[:, :cols] = (torch.randn(rows, cols, generator=g) * scale).half()
+    return x.to(dev)
+
+
+def _close(got, want, tol=4e-3):
+    scale = want.abs().max().clamp_min(1e-3)
+    err = (got.float() - want.float()).abs().max() / scale
+    assert err < tol, float(err)
+
+
+@pytest.mark.parametrize("n,m,k", [(1000, 128, 128), (333, 64, 528), (77, 7, 16), (4100, 16, 272), (50, 1, 8)])
+def test_hgemm_bias_act(cuda, n, m, k):
+    a = _h16(n, k, k, cuda, seed=1)
+    w = _h16(m, k, k, cuda, scale=0.1, seed=2)
+    b = torch.randn(m, device=cuda)
+    s = stream_handle(cuda)
+    ref = a.float() @ w.float().t() + b
+    for act, f in ((0, lambda v: v), (1, torch.relu), (2, lambda v: torch.nn.functional.leaky_relu(v, 0.2))):
+        out = torch.full((n, m), float("nan"), device=cuda)
+        check(LIB.vg_hgemm(ptr(a), k, ptr(w), k, n, m, k, ptr(b), act, 0.2, ptr(out), m, 1, s), "vg_hgemm")
+        _close(out, f(ref))
+        ldo = _r8(m) + 8
+        o16 = torch.full((n, ldo), float("nan"), dtype=torch.float16, device=cuda)
+        check(LIB.vg_hgemm(ptr(a), k, ptr(w), k, n, m, k, ptr(b), act, 0.2, ptr(o16), ldo, 0, s), "vg_hgemm")
+        _close(o16[:, :m], f(ref))
+        assert torch.all(o16[:, m:_r8(m)] == 0)  # pad columns written as 0
+        assert torch.isnan(o16[:, _r8(m):]).all()  # nothing beyond the padded width
+
+
+@pytest.mark.parametrize("n,m,k", [(1000, 128, 272), (513, 64, 128), (129, 16, 32)])
+def test_hgemm_ln_act(cuda, n, m, k):
+    a = _h16(n, k, k, cuda, seed=3)
+    w = _h16(m, k, k, cuda, scale=0.1, seed=4)
+    b, g, be = torch.randn(m, device=cuda), torch.rand(m, device=cuda) + 0.5, torch.randn(m, device=cuda)
+    out = torch.empty(n, m, dtype=torch.float16, device=cuda)
+    check(LIB.vg_hgemm_ln_act(ptr(a), k, ptr(w), k, n, m, k, ptr(b), ptr(g), ptr(be), 1e-5, 0.2, ptr(out), m,
+                              stream_handle(cuda)), "vg_hgemm_ln_act")
+    ref = torch.nn.functional.leaky_relu(
+        torch.nn.functional.layer_norm(a.float() @ w.float().t() + b, (m,), g, be, 1e-5), 0.2)
+    _close(out, ref)
+
+
+@pytest.mark.parametrize("cin,cout", [(128, 64), (8, 1), (16, 2), (64, 128)])
+def test_hgat_lin_att_and_aggregate(cuda, cin, cout):
+    loc, vox = SyntheticDataset(8, seed=4).batch(range(3))
+    loc, vox = loc.to(cuda), vox.to(cuda)
+    csr = vdata.prepared(loc, vox, 7).csr
+    n = vox.num_nodes
+    x = _h16(n, cin, _r8(cin), cuda, seed=5)
+    w = _h16(cout, cin, _r8(cin), cuda, scale=0.2, seed=6)
+    att_s, att_d = torch.randn(cout, device=cuda) * 0.3, torch.randn(cout, device=cuda) * 0.3
+    bias = torch.randn(cout, device=cuda)
+    s = stream_handle(cuda)
+    ldh = _r8(cout)
+    h = torch.empty(n, ldh, dtype=torch.float16, device=cuda)
+    a_s, a_d = torch.empty(n, device=cuda), torch.empty(n, device=cuda)
+    check(LIB.vg_hgat_lin_att(ptr(x), _r8(cin), ptr(w), _r8(cin), n, _r8(cin), cout, ptr(att_s), ptr(att_d), ptr(h),
+                              ldh, ptr(a_s), ptr(a_d), s), "vg_hgat_lin_att")
+    href = x.float()[:, :cin] @ w.float()[:, :cin].t()
+    _close(h[:, :cout], href)
+    assert torch.all(h[:, cout:] == 0)
+    _close(a_s, href @ att_s)
+    _close(a_d, href @ att_d)
+    # aggregation on the f16 h vs the f32 scatter kernel on the same values
+    out = torch.empty_like(h)
+    check(LIB.vg_hgat_fwd(ptr(csr.row_ptr), ptr(csr.col), n, cout, ldh, ptr(h), ptr(a_s), ptr(a_d), ptr(bias), 0.2,
+                          ptr(out), ldh, s), "vg_hgat_fwd")
+    h32 = h[:, :cout].float().contiguous()
+    ref = ops.gat_conv(csr, h32, att_s.view(1, 1, -1), att_d.view(1, 1, -1), bias, 0.2, pre=(a_s, a_d))
+    _close(out[:, :cout], ref)
+    assert torch.all(out[:, cout:] == 0)
+
+
+@pytest.mark.parametrize("c,segs", [(128, 1), (1, 3), (32, 2)])
+def test_graphnorm_fwd_h(cuda, c, segs):
+    n = 3001
+    ld = _r8(c)
+    x = _h16(segs * n, c, ld, cuda, scale=2.0, seed=7) + 0.5
+    w, b, ms = torch.rand(c, device=cuda) + 0.5, torch.randn(c, device=cuda), torch.rand(c, device=cuda)
+    s = stream_handle(cuda)
+    ldy = ld + 16  # y as a column slice of a wider row
+    y = torch.full((segs * n, ldy), float("nan"), dtype=torch.float16, device=cuda)
+    stats = torch.empty(segs * 2 * c, device=cuda)
+    ws = torch.empty(segs * 256 * c * 3, device=cuda)
+    check(LIB.vg_graphnorm_fwd_h(ptr(x), ld, segs, n, c, ptr(w), ptr(b), ptr(ms), 1e-5, ptr(y), ldy, ptr(stats),
+                                 ptr(ws), s), "vg_graphnorm_fwd_h")
+    xs = x[:, :c].float().view(segs, n, c)
+    mu = xs.mean(1, keepdim=True)
+    o = xs - mu * ms
+    sd = o.std(1, unbiased=False, keepdim=True)  # PyG GraphNorm(batch=None)
+    ref = torch.relu(o / (sd + 1e-5) * w + b).reshape(segs * n, c)
+    _close(y[:, :c], ref)
+    assert torch.all(y[:, c:ld] == 0)
+    assert torch.isnan(y[:, ld:]).all()
+
+
+@pytest.fixture(scope="module")
+def gen_batch(cuda):
+    cfg = Configuration()
+    torch.manual_seed(11)
+    G = VoxelGNNGenerator(cfg, 17, 12).to(cuda).eval()
+    loc, vox = SyntheticDataset(16, seed=9).batch(range(4))
+    return cfg, G, loc.to(cuda), vox.to(cuda)
+
+
+@pytest.mark.parametrize("k", [1, 3])
+def test_half_generator_matches_f32_forward(cuda, gen_batch, k):
+    cfg, G, loc, vox = gen_batch
+    n = vox.num_nodes
+    z = torch.randn(k, n, cfg.Z_DIM, device=cuda)
+    noise = torch.empty(k * n, 7, device=cuda).exponential_()
+    with torch.no_grad():
+        l32, _, _ = G(loc, vox, z, noise=noise.view(k, n, 7) if k > 1 else noise)
+    hg = HalfGenerator(G)
+    l16, h16, s16 = hg(loc, vox, z, noise=noise)
+    l32 = l32.reshape(-1, 7)
+    l16 = l16.reshape(-1, 7)
+    d = (l16 - l32).abs()
+    rms = float(d.pow(2).mean().sqrt() / l32.pow(2).mean().sqrt())
+    p99 = float(d.flatten().kthvalue(int(0.99 * d.numel())).values / l32.abs().max())
+    mx = float(d.max() / l32.abs().max())
+    agree = float((l16.argmax(1) == l32.argmax(1)).float().mean())
+    print(f"k={k}: logits16 vs logits32: rms rel {rms:.2e}, p99 {p99:.2e}, max {mx:.2e} (of max|logits|); "
+          f"argmax agreement {agree:.4f}")
+    assert rms < 2e-2 and p99 < 5e-2 and mx < 0.2
+    assert agree >= 0.97
+    assert torch.all(h16.sum(-1) == 1)
+
+
+def test_half_sweep_graphed(cuda, gen_batch):
+    """The f16 sweep captures and replays; replays draw fresh z / noise."""
+    cfg, G, loc, vox = gen_batch
+    taus = geometric_taus(1.0, 0.1, 4)
+    sw = InferenceSweep(G, taus, graphed=True, dtype="f16")
+    a = sw.run_batch(loc, vox).clone()
+    b = sw.run_batch(loc, vox).clone()
+    assert a.shape == (len(taus), vox.num_nodes) and a.dtype == torch.int8
+    assert int(a.min()) >= 0 and int(a.max()) < 7
+    assert not torch.equal(a, b)
+    res = InferenceSweep(G, taus, graphed=False, dtype="f16").run([(loc, vox)])
+    assert res["samples"] == vox.num_graphs * len(taus)

@@ -4,7 +4,7 @@
 
 Synthetic buildings (vgan.synth, seed 777) in batches of --batch; per batch one
 stacked eval-mode G forward over the tau schedule 1.0 -> 0.1 (geometric, --taus
-steps), f32.  Pass 1 runs eagerly (and, graphed, captures one hipGraph per
+steps), f16 (vgan.half) and/or f32.  Pass 1 runs eagerly (and, graphed, captures one hipGraph per
 batch); later passes replay.  Inputs are staged in HBM before timing.  Prints
 one JSON line: samples/s (graphs x temperatures per second) per mode."""
 from __future__ import annotations
@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--taus", type=int, default=10)
     ap.add_argument("--passes", type=int, default=2)
+    ap.add_argument("--dtype", default="f16", choices=("f16", "f32", "both"))
     args = ap.parse_args()
     from vgan.config import Configuration
     from vgan.infer import InferenceSweep, geometric_taus
@@ -47,11 +48,12 @@ def main():
         loc, vox = ds.batch(list(range(b0, min(args.graphs, b0 + args.batch))))
         batches.append((loc.to(dev), vox.to(dev)))
     taus = geometric_taus(1.0, 0.1, args.taus)
+    dtypes = ("f16", "f32") if args.dtype == "both" else (args.dtype,)
     out = {"workload": f"configs[4]: {args.graphs} synthetic buildings, batch {args.batch}, "
-                       f"{args.taus} Gumbel temperatures 1.0->0.1 (geometric), eval G forward, f32",
+                       f"{args.taus} Gumbel temperatures 1.0->0.1 (geometric), eval G forward",
            "unit": "samples/s (buildings x temperatures)"}
-    for mode in ("eager", "graphed"):
-        sw = InferenceSweep(G, taus, graphed=(mode == "graphed"))
+    for dt, mode in [(d, m) for d in dtypes for m in ("eager", "graphed")]:
+        sw = InferenceSweep(G, taus, graphed=(mode == "graphed"), dtype=dt)
         torch.cuda.synchronize()
         times = []
         for p in range(args.passes):
@@ -59,9 +61,9 @@ def main():
             res = sw.run(batches)
             torch.cuda.synchronize()
             times.append(time.perf_counter() - t0)
-            print(f"[infer] {mode} pass {p}: {times[-1]:.3f} s", file=sys.stderr, flush=True)
+            print(f"[infer] {dt} {mode} pass {p}: {times[-1]:.3f} s", file=sys.stderr, flush=True)
         best = min(times[1:]) if len(times) > 1 else times[0]
-        out[mode] = {"samples_per_s": round(res["samples"] / best, 1), "pass_s": [round(t, 4) for t in times],
+        out[f"{dt}_{mode}"] = {"samples_per_s": round(res["samples"] / best, 1), "pass_s": [round(t, 4) for t in times],
                      "samples_per_pass": res["samples"]}
     print(json.dumps(out), flush=True)
 
