@@ -30,6 +30,9 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int TM = 64, TN = 64, TK = 32, LDP = TK + 1;
+#ifndef VG_LN_TM32
+#define VG_LN_TM32 1
+#endif
 #ifndef VG_TN_GROUPS
 #define VG_TN_GROUPS 2
 #endif
@@ -173,7 +176,11 @@ __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int l
 // pre-LayerNorm activations and mean / rstd (nullable) the row statistics for
 // the backward; the no-grad forwards skip both.  Saves the separate LayerNorm
 // launch and its read of the GEMM output.
-template <int NT>
+// TMR rows per block: 64 (2 x 2 waves) or 32 (1 x 4 waves; twice the blocks,
+// for grids that would leave CUs idle or a long last round).
+// ATT: no LayerNorm -- H = A B^T and a_src / a_dst = H . att_s / att_d per row
+// (vg_gat_lin_att for 64 < C <= 128; gamma / beta unused, Y unused).
+template <int NT, int TMR = TM, bool ATT = false>
 __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, int lda,
                                                  const float* __restrict__ B, int ldb,
                                                  const float* __restrict__ bias, int N, int M, int K,
@@ -181,22 +188,29 @@ __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, in
                                                  const float* __restrict__ beta, float eps,
                                                  float slope, float* __restrict__ H,
                                                  float* __restrict__ Y, float* __restrict__ mean,
-                                                 float* __restrict__ rstd) {
+                                                 float* __restrict__ rstd,
+                                                 const float* __restrict__ att_s = nullptr,
+                                                 const float* __restrict__ att_d = nullptr,
+                                                 float* __restrict__ a_src = nullptr,
+                                                 float* __restrict__ a_dst = nullptr) {
   constexpr int TNC = TN * NT;
   constexpr int CT = TNC + 1;  // staged tile row pitch
-  __shared__ float smem[2 * TM * LDP + 2 * TNC * LDP];
-  __shared__ float s_mu[TM], s_rs[TM];
-  float(*As)[TM][LDP] = reinterpret_cast<float(*)[TM][LDP]>(smem);
-  float(*Bs)[TNC][LDP] = reinterpret_cast<float(*)[TNC][LDP]>(smem + 2 * TM * LDP);
-  constexpr int PA = (TM * TK) / 256, PB = (TNC * TK) / 256;
+  constexpr int WCOLS = 4 / (TMR / 32);       // waves across the columns
+  constexpr int NJ = TNC / (32 * WCOLS);      // 32-column MFMA tiles per wave
+  static_assert(NJ >= 1, "TMR = 32 needs 128 columns");
+  __shared__ float smem[2 * TMR * LDP + 2 * TNC * LDP];
+  __shared__ float s_mu[TMR], s_rs[TMR];
+  float(*As)[TMR][LDP] = reinterpret_cast<float(*)[TMR][LDP]>(smem);
+  float(*Bs)[TNC][LDP] = reinterpret_cast<float(*)[TNC][LDP]>(smem + 2 * TMR * LDP);
+  constexpr int PA = (TMR * TK) / 256, PB = (TNC * TK) / 256;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
+  const int wr = wave / WCOLS, wc = wave % WCOLS;
   int tx, ty;
   tile_xy(tx, ty);
-  const int n0 = tx * TM;
-  f32x16 acc[NT];
+  const int n0 = tx * TMR;
+  f32x16 acc[NJ];
 #pragma unroll
-  for (int j = 0; j < NT; ++j)
+  for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
   float ra[PA], rb[PB];
@@ -231,8 +245,8 @@ __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, in
     if (k0 + TK < K) load(k0 + TK);
     const float* ar = &As[buf][wr * 32 + (lane & 31)][lane >> 5];
 #pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      const float* br = &Bs[buf][j * TN + wc * 32 + (lane & 31)][lane >> 5];
+    for (int j = 0; j < NJ; ++j) {
+      const float* br = &Bs[buf][j * 32 * WCOLS + wc * 32 + (lane & 31)][lane >> 5];
 #pragma unroll
       for (int kk = 0; kk < TK; kk += 2)
         acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[kk], br[kk], acc[j], 0, 0, 0);
@@ -243,17 +257,47 @@ __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, in
   __syncthreads();
   float* Ct = smem;
 #pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    const int c = j * TN + wc * 32 + (lane & 31);
+  for (int j = 0; j < NJ; ++j) {
+    const int c = j * 32 * WCOLS + wc * 32 + (lane & 31);
     const float bv = (bias && c < M) ? bias[c] : 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r)
       Ct[(wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * CT + c] = acc[j][r] + bv;
   }
   __syncthreads();
-  {  // row statistics: 4 threads per row, two-pass
-    constexpr int CPT = TNC / 4;
-    const int row = t >> 2, q = t & 3;
+  if constexpr (ATT) {  // attention projections: TPR threads per row, then coalesced H stores
+    constexpr int TPR = 256 / TMR;
+    constexpr int CPT = TNC / TPR;
+    const int row = t / TPR, q = t % TPR;
+    const float* cr = Ct + row * CT + q * CPT;
+    float ss = 0.f, sd = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int c = q * CPT + i;
+      if (c < M) {
+        ss = fmaf(cr[i], att_s[c], ss);
+        sd = fmaf(cr[i], att_d[c], sd);
+      }
+    }
+#pragma unroll
+    for (int off = 1; off < TPR; off <<= 1) {
+      ss += __shfl_xor(ss, off, 64);
+      sd += __shfl_xor(sd, off, 64);
+    }
+    if (q == 0 && n0 + row < N) {
+      a_src[n0 + row] = ss;
+      a_dst[n0 + row] = sd;
+    }
+    for (int idx = t; idx < TMR * TNC; idx += 256) {
+      const int r = idx / TNC, c = idx % TNC, n = n0 + r;
+      if (c < M && n < N) H[(size_t)n * M + c] = Ct[r * CT + c];
+    }
+    return;
+  }
+  {  // row statistics: TPR threads per row, two-pass
+    constexpr int TPR = 256 / TMR;
+    constexpr int CPT = TNC / TPR;
+    const int row = t / TPR, q = t % TPR;
     const float* cr = Ct + row * CT + q * CPT;
     float v[CPT];
     float s = 0.f;
@@ -262,8 +306,8 @@ __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, in
       v[i] = q * CPT + i < M ? cr[i] : 0.f;
       s += v[i];
     }
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
+#pragma unroll
+    for (int off = 1; off < TPR; off <<= 1) s += __shfl_xor(s, off, 64);
     const float mu = s / static_cast<float>(M);
     float ss = 0.f;
 #pragma unroll
@@ -272,8 +316,8 @@ __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, in
         const float d = v[i] - mu;
         ss = fmaf(d, d, ss);
       }
-    ss += __shfl_xor(ss, 1, 64);
-    ss += __shfl_xor(ss, 2, 64);
+#pragma unroll
+    for (int off = 1; off < TPR; off <<= 1) ss += __shfl_xor(ss, off, 64);
     const float rs = rsqrtf(ss / static_cast<float>(M) + eps);
     if (q == 0) {
       s_mu[row] = mu;
@@ -286,7 +330,7 @@ __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, in
   }
   __syncthreads();
   // normalise + activate, lanes along the columns (coalesced row stores)
-  for (int idx = t; idx < TM * TNC; idx += 256) {
+  for (int idx = t; idx < TMR * TNC; idx += 256) {
     const int row = idx / TNC, c = idx % TNC, n = n0 + row;
     if (c < M && n < N) {
       const float v = Ct[row * CT + c];
@@ -539,6 +583,9 @@ extern "C" int vg_gemm_ln_act(const float* A, int32_t lda, const float* W, int32
   if (M <= TN)
     k_gemm_ln<1><<<grid, 256, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma, beta, eps, slope, H, Y, mean,
                                       rstd);
+  else if (VG_LN_TM32)
+    k_gemm_ln<2, 32><<<dim3((N + 31) / 32, 1), 256, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma, beta, eps,
+                                                            slope, H, Y, mean, rstd);
   else
     k_gemm_ln<2><<<grid, 256, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma, beta, eps, slope, H, Y, mean,
                                       rstd);
@@ -554,10 +601,17 @@ extern "C" int vg_gat_lin_att(const float* X, int32_t ldx, const float* W, int32
     return VG_EINVAL;
   if (N == 0) return 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (C > TN) {  // several column tiles: GEMM, then the per-row projection pass
+  if (C > 2 * TN) {  // several column tiles: GEMM, then the per-row projection pass
     const int rc = vg_gemm(X, ldx, W, Cin, 1, nullptr, 0, nullptr, 0, H, C, N, C, Cin, stream);
     if (rc) return rc;
     return vg_gat_att(H, N, C, att_src, att_dst, a_src, a_dst, stream);
+  }
+  if (C > TN) {  // whole 128-column rows per block, projections in the epilogue
+    k_gemm_ln<2, 32, true><<<dim3((N + 31) / 32, 1), 256, 0, s>>>(
+        X, ldx, W, Cin, nullptr, N, C, Cin, nullptr, nullptr, 0.f, 0.f, H, nullptr, nullptr, nullptr, att_src,
+        att_dst, a_src, a_dst);
+    VG_CHECK_LAUNCH();
+    return 0;
   }
   k_gemm<true, 0, true><<<dim3((N + TM - 1) / TM, 1), 256, 0, s>>>(
       X, ldx, W, Cin, nullptr, nullptr, 0, H, C, N, C, Cin, att_src, att_dst, a_src, a_dst);
