@@ -51,7 +51,14 @@ class GraphLoader:
 
     def __init__(self, store: GraphStore, indices: Optional[Sequence[int]] = None, batch_size: int = 1,
                  shuffle: bool = True, drop_last: bool = False, device=None, prefetch: int = 2,
-                 threads: int = 4):
+                 threads: int = 4, rank: int = 0, world_size: int = 1):
+        """``rank`` / ``world_size``: data-parallel sharding -- every rank draws
+        the same epoch plan (same seed) and takes batches rank, rank + world,
+        ... of it, so ranks see disjoint buildings (weak scaling, one batch
+        of ``batch_size`` per rank and step)."""
+        if not 0 <= rank < world_size:
+            raise ValueError("need 0 <= rank < world_size")
+        self.rank, self.world_size = int(rank), int(world_size)
         self.store = store
         self.indices = list(range(len(store))) if indices is None else [int(i) for i in indices]
         self.batch_size = int(batch_size)
@@ -63,7 +70,8 @@ class GraphLoader:
 
     def __len__(self) -> int:
         n = len(self.indices)
-        return n // self.batch_size if self.drop_last else (n + self.batch_size - 1) // self.batch_size
+        total = n // self.batch_size if self.drop_last else (n + self.batch_size - 1) // self.batch_size
+        return len(range(self.rank, total, self.world_size))
 
     def batches(self) -> List[List[int]]:
         """This epoch's building indices per batch (consumes the CPU RNG like
@@ -71,7 +79,7 @@ class GraphLoader:
         then the RandomSampler's seed)."""
         dl = DataLoader(_Indices(self.indices), batch_size=self.batch_size, shuffle=self.shuffle,
                         drop_last=self.drop_last, collate_fn=_as_list, num_workers=0)
-        return list(iter(dl))
+        return list(iter(dl))[self.rank::self.world_size]
 
     def __iter__(self) -> Iterator[Tuple[GraphBatch, GraphBatch]]:
         plan = self.batches()
@@ -144,7 +152,8 @@ class GraphDataLoaders:
     """``train_dataloader`` / ``validation_dataloader`` / ``test_dataloader`` of
     the reference (``data.py:166-212``) over a GraphStore."""
 
-    def __init__(self, configuration, store: GraphStore, device=None, prefetch: int = 2):
+    def __init__(self, configuration, store: GraphStore, device=None, prefetch: int = 2, rank: int = 0,
+                 world_size: int = 1):
         self.configuration = configuration
         self.sanity_checking = bool(getattr(configuration, "SANITY_CHECKING", False))
         self.dataset = store
@@ -153,7 +162,7 @@ class GraphDataLoaders:
             indices = [indices[int(getattr(configuration, "DATA_POINT", 0))]]
         parts = random_split(indices, configuration.SPLIT_RATIOS)
         kw = dict(batch_size=configuration.BATCH_SIZE, shuffle=True, drop_last=False, device=device,
-                  prefetch=prefetch)
+                  prefetch=prefetch, rank=rank, world_size=world_size)
         self.train_dataloader = GraphLoader(store, [indices[i] for i in parts[0].indices], **kw)
         self.validation_dataloader = None if self.sanity_checking else \
             GraphLoader(store, [indices[i] for i in parts[1].indices], **kw)

@@ -201,6 +201,26 @@ def test_loader_shuffle_matches_reference_dataloader(synth_store):
     assert sum(b[1].num_graphs for b in batches) == len(idx)
 
 
+def test_loader_rank_sharding(synth_store):
+    """Data-parallel ranks take disjoint interleaved batches of one epoch plan."""
+    from vgan.loader import GraphLoader
+
+    _, st = synth_store
+    plans = []
+    for rank in range(3):
+        torch.manual_seed(4)
+        loader = GraphLoader(st, list(range(len(st))), batch_size=2, shuffle=True, rank=rank, world_size=3)
+        plans.append(loader.batches())
+        assert len(loader) == len(plans[-1])
+    torch.manual_seed(4)
+    full = GraphLoader(st, list(range(len(st))), batch_size=2, shuffle=True).batches()
+    assert [b for r in range(3) for b in full[r::3]] == [b for p in plans for b in p]
+    seen = sorted(i for p in plans for b in p for i in b)
+    assert seen == list(range(len(st)))
+    with pytest.raises(ValueError):
+        GraphLoader(st, rank=2, world_size=2)
+
+
 def test_graph_data_loaders_split_matches_reference(synth_store):
     from torch.utils.data import random_split
 
