@@ -2,8 +2,9 @@
 top kernels) so the multi-MB trace itself need not be kept.
 
 usage: prof_summary.py TRACE.csv [TOP] [--after-gap] [--steps K]
-  --after-gap  keep only the kernels after the largest idle gap in the trace
-               (bench.py --profile sleeps 50 ms before its timed steps)
+  --after-gap  keep only the kernels after the LAST idle gap of >= 40 ms
+               (bench.py --profile sleeps 50 ms before its timed steps and
+               returns right after them; staging and capture gaps come earlier)
   --steps K    also report per-step dispatch counts / busy time
 """
 import csv
@@ -19,8 +20,10 @@ rows = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) f
 rows.sort()
 if after_gap and len(rows) > 1:
     gaps = [(rows[i + 1][0] - rows[i][1], i) for i in range(len(rows) - 1)]
-    g, i = max(gaps)
-    print(f"largest gap {g / 1e6:.1f} ms after dispatch {i}; keeping the {len(rows) - i - 1} dispatches after it")
+    long_gaps = [gi for gi in gaps if gi[0] >= 40_000_000]
+    g, i = long_gaps[-1] if long_gaps else max(gaps)
+    print(f"last idle gap >= 40 ms: {g / 1e6:.1f} ms after dispatch {i}; keeping the {len(rows) - i - 1} "
+          f"dispatches after it")
     rows = rows[i + 1:]
 tot = defaultdict(lambda: [0, 0.0])
 busy = 0.0
