@@ -408,3 +408,57 @@ extern "C" int vg_gen_loss_bwd(const float* g_loss, const float* out, const floa
   VG_CHECK_LAUNCH();
   return 0;
 }
+
+// ---- counter-based random draws (device RNG mode) -------------------------
+// Four draws per Philox4x32-10 call on the counter (element group, salt,
+// *iter): a captured hipGraph reads *iter at replay, so every replay draws
+// fresh numbers without torch's generator bookkeeping (two int64 fills per
+// graph replay for the registered philox seed / offset).
+namespace {
+__global__ void k_rng_fill(float* __restrict__ out, long long n, int kind, unsigned long long seed,
+                           const long long* __restrict__ iter, unsigned int salt) {
+  const long long it = *iter;
+  const uint2 key = make_uint2(static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32));
+  for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; 4 * g < n;
+       g += (long long)gridDim.x * blockDim.x) {
+    const uint4 r = vg_philox(make_uint4(static_cast<uint32_t>(g), static_cast<uint32_t>(g >> 32), salt,
+                                         static_cast<uint32_t>(it)),
+                              key);
+    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+    float v[4];
+    if (kind == 0) {  // standard normal, Box-Muller on (x, y) and (z, w)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const float u1 = (static_cast<float>(w[2 * p] >> 8) + 1.f) * (1.0f / 16777216.0f);  // (0, 1]
+        const float u2 = static_cast<float>(w[2 * p + 1] >> 8) * (1.0f / 16777216.0f);
+        const float rad = sqrtf(-2.f * logf(u1));
+        float sn, cs;
+        sincosf(6.283185307179586f * u2, &sn, &cs);
+        v[2 * p] = rad * cs;
+        v[2 * p + 1] = rad * sn;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float u = static_cast<float>(w[q] >> 8) * (1.0f / 16777216.0f);  // [0, 1)
+        v[q] = kind == 1 ? u : -logf(1.f - u);  // uniform / Exp(1)
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (4 * g + q < n) out[4 * g + q] = v[q];
+  }
+}
+}  // namespace
+
+extern "C" int vg_rng_fill(float* out, int64_t n, int32_t kind, uint64_t seed, const int64_t* iter, uint32_t salt,
+                           void* stream) {
+  if (n < 0 || !out || !iter || kind < 0 || kind > 2) return VG_EINVAL;
+  if (n == 0) return 0;
+  const long long groups = (n + 3) / 4;
+  const int blocks = static_cast<int>(groups / 256 + 1 < 2048 ? groups / 256 + 1 : 2048);
+  k_rng_fill<<<blocks, 256, 0, static_cast<hipStream_t>(stream)>>>(out, n, kind, (unsigned long long)seed,
+                                                                   reinterpret_cast<const long long*>(iter), salt);
+  VG_CHECK_LAUNCH();
+  return 0;
+}

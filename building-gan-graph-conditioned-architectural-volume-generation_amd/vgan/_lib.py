@@ -56,6 +56,7 @@ SIGNATURES = {
                                    _c_p]),
     "vg_graphnorm_fwd_h": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_f32, _c_p,
                                           _c_i32, _c_p, _c_p, _c_p]),
+    "vg_rng_fill": (ctypes.c_int, [_c_p, _c_i64, _c_i32, ctypes.c_uint64, _c_p, ctypes.c_uint32, _c_p]),
     "vg_csr_ws_ints": (_c_i64, [_c_i64, _c_i32]),
     "vg_csr_build": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "vg_gat_fwd": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p,

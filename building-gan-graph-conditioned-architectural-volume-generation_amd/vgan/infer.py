@@ -67,6 +67,7 @@ class InferenceSweep:
         G = self.G
         k = len(self.taus)
         n = voxel_graph.num_nodes
+        G.rng.reset()  # advance the device counter: every (replayed) batch draws fresh z and noise
         z = G.rng.normal((k, n, G.configuration.Z_DIM), voxel_graph.x.device)
         if self.half is not None:
             _, hard, _ = self.half(local_graph, voxel_graph, z, tau=self.tau_t)

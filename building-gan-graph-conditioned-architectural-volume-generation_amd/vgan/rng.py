@@ -10,11 +10,13 @@ penalty (``trainer.py:298``).
 * ``RNG("host")`` draws exactly those tensors, with the same ops and shapes, on
   the CPU default generator and copies them to the device -- the GPU path then
   sees bit-identical randomness to the reference CPU run (parity mode).
-* ``RNG("device")`` draws them on the GPU (fast mode; hipGraph-safe): z, eps and
-  the Gumbel noise on torch's CUDA generator; each dropout mask as a
-  ``DropSpec`` that the GraphNorm kernel materialises in-kernel from a
+* ``RNG("device")`` draws them on the GPU (fast mode; hipGraph-safe) from one
   counter-based Philox keyed by (seed, device iteration counter, call-site
-  salt) -- no extra launches.  ``reset()`` at the start of every iteration
+  salt): z, eps and the Gumbel noise through ``vg_rng_fill`` (no torch
+  generator inside the captured graphs, hence none of the two int64 seed /
+  offset fills torch adds to every replay), each dropout mask as a
+  ``DropSpec`` that the GraphNorm kernel materialises in-kernel -- no extra
+  launches.  ``reset()`` at the start of every iteration
   body advances the device counter (one tiny launch, captured in the graph),
   so hipGraph replays draw fresh masks.
 * ``RNG("fixed")`` (tests only) hands out the same seeded tensors for the k-th
@@ -24,7 +26,7 @@ penalty (``trainer.py:298``).
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Dict, Sequence
+from typing import Optional, Dict, Sequence
 
 import torch
 
@@ -40,11 +42,13 @@ class DropSpec:
 
 
 class RNG:
-    def __init__(self, mode: str = "device", seed: int = 0):
+    def __init__(self, mode: str = "device", seed: Optional[int] = None):
         if mode not in ("device", "host", "fixed"):
             raise ValueError("RNG mode must be 'device', 'host' or 'fixed'")
         self.mode = mode
-        self.seed = seed
+        # device mode: seeded from the CPU generator (torch.manual_seed(SEED + rank)
+        # in the bench / DP ranks), so ranks draw different streams
+        self.seed = (torch.initial_seed() if mode == "device" else 0) if seed is None else int(seed)
         self._k = 0
         self._fixed = {}
         self._salt = 0
@@ -80,19 +84,38 @@ class RNG:
     def _out(self, t: torch.Tensor, device) -> torch.Tensor:
         return t.to(device, non_blocking=True) if self.mode == "host" else t
 
+    def _device_draw(self, kind: int, shape, device) -> torch.Tensor:
+        """vg_rng_fill on (salt, the device iteration counter): no torch
+        generator inside captured graphs, so replays need no seed / offset
+        refills."""
+        from ._lib import LIB, check, ptr, stream_handle
+
+        device = torch.device(device)
+        out = torch.empty(*shape, dtype=torch.float32, device=device)
+        self._salt += 1
+        check(LIB.vg_rng_fill(ptr(out), out.numel(), kind, int(self.seed) & ((1 << 64) - 1), ptr(self._iter(device)),
+                              0x40000000 | self._salt, stream_handle(device)), "vg_rng_fill")
+        return out
+
     def normal(self, shape: Sequence[int], device) -> torch.Tensor:
         if self.mode == "fixed":
             return self._fixed_draw("n", shape, device, lambda g: torch.randn(*shape, generator=g))
+        if self.mode == "device" and torch.device(device).type == "cuda":
+            return self._device_draw(0, shape, device)
         return self._out(torch.randn(*shape, device=self._dev(device)), device)
 
     def uniform(self, shape: Sequence[int], device) -> torch.Tensor:
         if self.mode == "fixed":
             return self._fixed_draw("u", shape, device, lambda g: torch.rand(*shape, generator=g))
+        if self.mode == "device" and torch.device(device).type == "cuda":
+            return self._device_draw(1, shape, device)
         return self._out(torch.rand(*shape, device=self._dev(device)), device)
 
     def exponential(self, shape: Sequence[int], device) -> torch.Tensor:
         if self.mode == "fixed":
             return self._fixed_draw("e", shape, device, lambda g: torch.empty(*shape).exponential_(generator=g))
+        if self.mode == "device" and torch.device(device).type == "cuda":
+            return self._device_draw(2, shape, device)
         return self._out(torch.empty(*shape, device=self._dev(device)).exponential_(), device)
 
     def keep_mask(self, shape: Sequence[int], p: float, device):

@@ -444,6 +444,17 @@ int vg_gat_jvp2_deferred(const int32_t* row_ptr, const int32_t* col, const int32
                          const float* up_src, const float* up_dst, float* workspace,
                          vg_fold* folds_out, int32_t* n_out, void* stream);
 
+/* ---- device RNG ------------------------------------------------------------ */
+
+/* n draws into out: kind 0 standard normal (Box-Muller), 1 uniform [0, 1),
+ * 2 Exp(1) -- the z / Gumbel noise / interpolation draws of the step
+ * (trainer.py:470,484 torch.randn; models.py:150 F.gumbel_softmax; trainer.py:298
+ * torch.rand) in device-RNG mode.  Counter-based Philox4x32-10 on (element
+ * group, salt, *iter) with key seed, so a captured graph replays fresh draws
+ * as *iter advances. */
+int vg_rng_fill(float* out, int64_t n, int32_t kind, uint64_t seed, const int64_t* iter, uint32_t salt,
+                void* stream);
+
 /* ---- optimiser ---------------------------------------------------------- */
 
 /* torch.optim.Adam (single-tensor semantics, weight_decay, no amsgrad) over one
