@@ -67,15 +67,33 @@ class _MMtn(Function):
 
 
 class _LinearFn(Function):
+    """y = act(x W^T + b) on vg_gemm; act is ACT_NONE or ACT_RELU (the
+    [Linear, ReLU] blocks of the discriminator's MLPs, models.py:166-175, with
+    the ReLU in the GEMM epilogue)."""
+
     @staticmethod
     def forward(ctx, x, weight, bias, act):
-        ctx.save_for_backward(x, weight)
+        if act not in (ops.ACT_NONE, ops.ACT_RELU):
+            raise ValueError("_LinearFn: act must be ACT_NONE or ACT_RELU")
+        y = ops.gemm(x, weight, True, bias, act)
+        ctx.act = act
+        if act == ops.ACT_RELU:
+            ctx.save_for_backward(x, weight, y)
+        else:
+            ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
         ctx.params = (weight, bias)
-        return ops.gemm(x, weight, True, bias, act)
+        return y
 
     @staticmethod
     def backward(ctx, gy):
+        if ctx.act == ops.ACT_RELU:
+            x, weight, y = ctx.saved_tensors
+            if torch.is_grad_enabled():
+                gy = gy * (y > 0).to(gy.dtype)  # differentiable in gy (create_graph)
+            else:
+                gy = torch.ops.aten.threshold_backward(gy, y, 0)
+            return _linear_backward(ctx, gy, saved=(x, weight)) + (None,)
         return _linear_backward(ctx, gy) + (None,)
 
 
@@ -211,14 +229,20 @@ class Linear(nn.Linear):
 class MLP(nn.Sequential):
     """nn.Sequential of the reference's [Linear, (LayerNorm,) activation]
     blocks (same children, same state_dict keys); every Linear -> LayerNorm
-    -> LeakyReLU triple runs as one GEMM plus one fused LayerNorm+activation
-    kernel (vg_ln_act_fwd)."""
+    -> LeakyReLU triple runs as one GEMM with the LayerNorm in its epilogue
+    (or GEMM + vg_ln_act_fwd past 128 outputs), every Linear -> ReLU pair as
+    one GEMM with the ReLU in its epilogue."""
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         mods = list(self)
         i = 0
         while i < len(mods):
             m = mods[i]
+            if (isinstance(m, nn.Linear) and i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU)
+                    and x.dim() == 2):  # ReLU in the GEMM epilogue
+                x = _LinearFn.apply(x.contiguous(), m.weight, m.bias, ops.ACT_RELU)
+                i += 2
+                continue
             if (isinstance(m, nn.Linear) and i + 2 < len(mods) and isinstance(mods[i + 1], nn.LayerNorm)
                     and isinstance(mods[i + 2], nn.LeakyReLU) and len(mods[i + 1].normalized_shape) == 1
                     and mods[i + 1].elementwise_affine):
