@@ -30,10 +30,13 @@
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kChunks = 256;  // max row chunks per column slab (~64 rows each)
+#ifndef VG_GN_CHUNKS
+#define VG_GN_CHUNKS 256
+#endif
+constexpr int kChunks = VG_GN_CHUNKS;  // max row chunks per column slab
 constexpr int kFoldU = kChunks / 64;
 #ifndef VG_GN_CHUNK_ROWS
-#define VG_GN_CHUNK_ROWS 64
+#define VG_GN_CHUNK_ROWS 32
 #endif
 #ifndef VG_GN_APPLY_MAX
 #define VG_GN_APPLY_MAX 2048

@@ -170,7 +170,7 @@ class HalfGenerator:
             else:
                 y, ldy = torch.empty_like(h), ldh
             stats = torch.empty(kk * 2 * cout, dtype=torch.float32, device=dev)
-            ws = torch.empty(kk * 256 * cout * 3, dtype=torch.float32, device=dev)
+            ws = torch.empty(int(LIB.vg_graphnorm_seg_ws_floats(kk, n, cout)), dtype=torch.float32, device=dev)
             check(LIB.vg_graphnorm_fwd_h(ptr(agg), ldh, kk, n, cout, ptr(gw), ptr(gb), ptr(gms), eps, ptr(y), ldy,
                                          ptr(stats), ptr(ws), s), "vg_graphnorm_fwd_h")
             x, ldx = y, ldy

@@ -511,7 +511,7 @@ int vg_hgat_fwd(const int32_t* row_ptr, const int32_t* col, int32_t n, int32_t c
 
 /* ReLU(GraphNorm(x)) (eval: no dropout) over S stacked segments of n f16 rows
  * (models.py:73-75,83-85); statistics f32 ([S][2C] like vg_graphnorm_fwd_seg,
- * workspace S * 256 * C * 3 floats). */
+ * workspace vg_graphnorm_seg_ws_floats(S, N, C) floats). */
 int vg_graphnorm_fwd_h(const uint16_t* x, int32_t ld, int32_t S, int32_t N, int32_t C,
                        const float* weight, const float* bias, const float* mean_scale, float eps,
                        uint16_t* y, int32_t ldy, float* stats, float* ws, void* stream);

@@ -111,7 +111,7 @@ def test_graphnorm_fwd_h(cuda, c, segs):
     ldy = ld + 16  # y as a column slice of a wider row
     y = torch.full((segs * n, ldy), float("nan"), dtype=torch.float16, device=cuda)
     stats = torch.empty(segs * 2 * c, device=cuda)
-    ws = torch.empty(segs * 256 * c * 3, device=cuda)
+    ws = torch.empty(int(LIB.vg_graphnorm_seg_ws_floats(segs, n, c)), device=cuda)
     check(LIB.vg_graphnorm_fwd_h(ptr(x), ld, segs, n, c, ptr(w), ptr(b), ptr(ms), 1e-5, ptr(y), ldy, ptr(stats),
                                  ptr(ws), s), "vg_graphnorm_fwd_h")
     xs = x[:, :c].float().view(segs, n, c)
