@@ -39,7 +39,10 @@ namespace {
 
 using namespace vg;
 
-constexpr int kMaxBwdBlocks = 512;    // grid cap of the backward row passes (partials count)
+#ifndef VG_BWD_MAX_BLOCKS
+#define VG_BWD_MAX_BLOCKS 4096
+#endif
+constexpr int kMaxBwdBlocks = VG_BWD_MAX_BLOCKS;  // grid cap of the backward row passes (partials count)
 constexpr int kEP = 3;                // edge slots per lane in the edge-parallel kernels
 
 template <int CPL>

@@ -27,7 +27,10 @@ namespace {
 
 using namespace vg;
 
-constexpr int kMaxBlocks = 512;
+#ifndef VG_BWD_MAX_BLOCKS
+#define VG_BWD_MAX_BLOCKS 4096
+#endif
+constexpr int kMaxBlocks = VG_BWD_MAX_BLOCKS;
 
 template <int L, int CPL, bool VEC>
 __global__ void __launch_bounds__(kBlock) k_jvp_att(const float* __restrict__ u, int N, int C,

@@ -19,7 +19,10 @@ namespace {
 
 using namespace vg;
 
-constexpr int kMaxBlocks = 512;
+#ifndef VG_LN_MAX_BLOCKS
+#define VG_LN_MAX_BLOCKS 512
+#endif
+constexpr int kMaxBlocks = VG_LN_MAX_BLOCKS;
 
 template <int L, int CPL>
 __global__ void __launch_bounds__(kBlock) k_ln_act_fwd(const float* __restrict__ x, int N, int C,
