@@ -180,7 +180,21 @@ __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int l
 // for grids that would leave CUs idle or a long last round).
 // ATT: no LayerNorm -- H = A B^T and a_src / a_dst = H . att_s / att_d per row
 // (vg_gat_lin_att for 64 < C <= 128; gamma / beta unused, Y unused).
-template <int NT, int TMR = TM, bool ATT = false>
+// Multi-source A for k_gemm_ln (vg_gemm_ln_act_ms): the K columns are the
+// concatenation of up to kMaxSrc row-major sources, each with its own stride,
+// its first column in W, and optionally rows taken modulo rows_mod (a source
+// shared by stacked copies); `add` (rows modulo add_rows) is added before the
+// LayerNorm.  Passed by value in kernarg.
+constexpr int kMaxSrc = 4;
+struct MsDesc {
+  const float* p[kMaxSrc];
+  int ld[kMaxSrc], kend[kMaxSrc], wcol[kMaxSrc], rmod[kMaxSrc];
+  int nsrc;
+  const float* add;
+  int ld_add, add_rows;
+};
+
+template <int NT, int TMR = TM, bool ATT = false, bool MS = false>
 __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, int lda,
                                                  const float* __restrict__ B, int ldb,
                                                  const float* __restrict__ bias, int N, int M, int K,
@@ -192,7 +206,9 @@ __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, in
                                                  const float* __restrict__ att_s = nullptr,
                                                  const float* __restrict__ att_d = nullptr,
                                                  float* __restrict__ a_src = nullptr,
-                                                 float* __restrict__ a_dst = nullptr) {
+                                                 float* __restrict__ a_dst = nullptr, int ldy = 0,
+                                                 const MsDesc ms = MsDesc{}) {
+  if (ldy == 0) ldy = M;
   constexpr int TNC = TN * NT;
   constexpr int CT = TNC + 1;  // staged tile row pitch
   constexpr int WCOLS = 4 / (TMR / 32);       // waves across the columns
@@ -215,17 +231,31 @@ __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, in
     for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
   float ra[PA], rb[PB];
   auto load = [&](int k0) {
+    // MS: sources are TK-aligned column blocks, so one source serves the chunk
+    const float* asrc = A;
+    int ald = lda, acol = k0, wcol = k0;
+    if constexpr (MS) {
+      int sidx = 0;
+#pragma unroll
+      for (int i = 0; i < kMaxSrc - 1; ++i)
+        if (i < ms.nsrc - 1 && k0 >= ms.kend[i]) sidx = i + 1;
+      const int kb = sidx > 0 ? ms.kend[sidx - 1] : 0;
+      asrc = ms.p[sidx];
+      ald = ms.ld[sidx];
+      acol = k0 - kb;
+      wcol = ms.wcol[sidx] + (k0 - kb);
+    }
 #pragma unroll
     for (int q = 0; q < PA; ++q) {
       const int e = t + 256 * q;
-      const int n = n0 + e / TK, k = k0 + e % TK;
-      ra[q] = (n < N && k < K) ? A[(size_t)n * lda + k] : 0.f;
+      const int n = n0 + e / TK, kc = e % TK;
+      ra[q] = (n < N && k0 + kc < K) ? asrc[(size_t)n * ald + acol + kc] : 0.f;
     }
 #pragma unroll
     for (int q = 0; q < PB; ++q) {
       const int e = t + 256 * q;
-      const int m = e / TK, k = k0 + e % TK;
-      rb[q] = (m < M && k < K) ? B[(size_t)m * ldb + k] : 0.f;
+      const int m = e / TK, kc = e % TK;
+      rb[q] = (m < M && k0 + kc < K) ? B[(size_t)m * ldb + wcol + kc] : 0.f;
     }
   };
   load(0);
@@ -256,13 +286,24 @@ __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, in
   // stage the full-width tile (+ bias) in LDS
   __syncthreads();
   float* Ct = smem;
+  const int add0 = MS && ms.add ? n0 % ms.add_rows : 0;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int c = j * 32 * WCOLS + wc * 32 + (lane & 31);
     const float bv = (bias && c < M) ? bias[c] : 0.f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r)
-      Ct[(wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * CT + c] = acc[j][r] + bv;
+    for (int r = 0; r < 16; ++r) {
+      const int rl = wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      float v = acc[j][r] + bv;
+      if constexpr (MS) {  // addend row (n0 + rl) mod add_rows; rl < TMR <= add_rows
+        if (ms.add && n0 + rl < N && c < M) {
+          int ar = add0 + rl;
+          if (ar >= ms.add_rows) ar -= ms.add_rows;
+          v += ms.add[(size_t)ar * ms.ld_add + c];
+        }
+      }
+      Ct[rl * CT + c] = v;
+    }
   }
   __syncthreads();
   if constexpr (ATT) {  // attention projections: TPR threads per row, then coalesced H stores
@@ -336,7 +377,7 @@ __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, in
       const float v = Ct[row * CT + c];
       if (H) H[(size_t)n * M + c] = v;
       const float z = fmaf((v - s_mu[row]) * s_rs[row], gamma[c], beta[c]);
-      Y[(size_t)n * M + c] = z > 0.f ? z : z * slope;
+      Y[(size_t)n * ldy + c] = z > 0.f ? z : z * slope;
     }
   }
 }
@@ -589,6 +630,39 @@ extern "C" int vg_gemm_ln_act(const float* A, int32_t lda, const float* W, int32
   else
     k_gemm_ln<2><<<grid, 256, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma, beta, eps, slope, H, Y, mean,
                                       rstd);
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int vg_gemm_ln_act_ms(const vg_asrc* src, int32_t nsrc, const float* W, int32_t ldw, int32_t N,
+                                 int32_t M, const float* bias, const float* addend, int32_t ld_add,
+                                 int32_t add_rows, const float* gamma, const float* beta, float eps, float slope,
+                                 float* Y, int32_t ldy, void* stream) {
+  if (!src || nsrc <= 0 || nsrc > kMaxSrc || !W || N < 0 || M <= TN || M > 2 * TN || !gamma || !beta || !Y ||
+      ldy < M || (addend && (ld_add < M || add_rows < 32)))
+    return VG_EINVAL;
+  MsDesc d{};
+  int K = 0;
+  for (int i = 0; i < nsrc; ++i) {
+    if (!src[i].ptr || src[i].cols <= 0 || src[i].cols % TK || src[i].ld < src[i].cols || src[i].w_col0 < 0 ||
+        src[i].w_col0 + src[i].cols > ldw || src[i].rows_mod != 0)
+      return VG_EINVAL;
+    K += src[i].cols;
+    d.p[i] = src[i].ptr;
+    d.ld[i] = src[i].ld;
+    d.kend[i] = K;
+    d.wcol[i] = src[i].w_col0;
+    d.rmod[i] = src[i].rows_mod;
+  }
+  d.nsrc = nsrc;
+  d.add = addend;
+  d.ld_add = ld_add;
+  d.add_rows = add_rows;
+  if (N == 0) return 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  k_gemm_ln<2, 32, false, true><<<dim3((N + 31) / 32, 1), 256, 0, s>>>(
+      nullptr, 0, W, ldw, bias, N, M, K, gamma, beta, eps, slope, nullptr, Y, nullptr, nullptr, nullptr, nullptr,
+      nullptr, nullptr, ldy, d);
   VG_CHECK_LAUNCH();
   return 0;
 }

@@ -33,6 +33,11 @@ class VgFold(ctypes.Structure):
 
 VG_FOLD_MAX = 40
 
+
+class VgASrc(ctypes.Structure):
+    """vg_asrc (include/vgan.h): one column block of vg_gemm_ln_act_ms's A."""
+    _fields_ = [("ptr", _c_p), ("ld", _c_i32), ("cols", _c_i32), ("w_col0", _c_i32), ("rows_mod", _c_i32)]
+
 # name -> (restype, argtypes); every function listed here is declared in include/vgan.h
 SIGNATURES = {
     "vg_fold_batch": (ctypes.c_int, [_c_p, _c_i32, _c_p]),
@@ -57,6 +62,8 @@ SIGNATURES = {
     "vg_graphnorm_fwd_h": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_f32, _c_p,
                                           _c_i32, _c_p, _c_p, _c_p]),
     "vg_rng_fill": (ctypes.c_int, [_c_p, _c_i64, _c_i32, ctypes.c_uint64, _c_p, ctypes.c_uint32, _c_p]),
+    "vg_gemm_ln_act_ms": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_i32, _c_i32, _c_p,
+                                         _c_p, _c_f32, _c_f32, _c_p, _c_i32, _c_p]),
     "vg_csr_ws_ints": (_c_i64, [_c_i64, _c_i32]),
     "vg_csr_build": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "vg_gat_fwd": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p,

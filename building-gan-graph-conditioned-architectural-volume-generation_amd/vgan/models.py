@@ -20,6 +20,7 @@ per-batch data and are computed once per mini-batch (``vgan.data``).
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from typing import List, Optional
 
@@ -28,7 +29,7 @@ import torch.nn as nn
 
 from . import data as vdata
 from . import ops
-from .nn import MLP, Linear, linear_att
+from .nn import MLP, Linear, linear_att, linear_ln_act, run_blocks
 from .rng import RNG
 
 _CONV_TYPES = ("GCNCONV", "GRAPHCONV", "GATCONV", "GATV2CONV")
@@ -163,6 +164,64 @@ class VoxelGNNGenerator(nn.Module):
         self.tau = 1.0
         self.to(cfg.DEVICE)
 
+    def _mlp_blocks(self, mlp: nn.Module):
+        mods = list(mlp.children())
+        return [tuple(mods[i:i + 3]) for i in range(0, len(mods) - 2, 3)
+                if isinstance(mods[i], nn.Linear) and isinstance(mods[i + 1], nn.LayerNorm)
+                and isinstance(mods[i + 2], nn.LeakyReLU)]
+
+    def _first_block_ms(self, block, srcs, emvx, emvx_w0, rows, n):
+        """First [Linear, LayerNorm, LeakyReLU] block over stacked copies:
+        the copy-invariant columns [em | voxel.x] once on N rows (vg_gemm into
+        the addend, bias included), the per-copy columns read in place from
+        their own tensors (vg_gemm_ln_act_ms) -- no torch.cat, no repeat."""
+        from ._lib import LIB, VgASrc, check, ptr, stream_handle
+
+        lin, ln, act = block
+        w = lin.weight
+        m, ktot = w.shape
+        dev = w.device
+        st = stream_handle(dev)
+        add = torch.empty(n, m, dtype=torch.float32, device=dev)
+        check(LIB.vg_gemm(ptr(emvx), emvx.shape[1], ctypes.c_void_p(w.data_ptr() + 4 * emvx_w0), ktot, 1, ptr(lin.bias),
+                          0, None, 0, ptr(add), m, n, m, emvx.shape[1], st), "vg_gemm")
+        arr = (VgASrc * len(srcs))(*[VgASrc(t.data_ptr(), t.stride(0), cols, w0, 0) for t, cols, w0 in srcs])
+        y = torch.empty(rows, m, dtype=torch.float32, device=dev)
+        check(LIB.vg_gemm_ln_act_ms(arr, len(srcs), ptr(w), ktot, rows, m, None, ptr(add), m, n, ptr(ln.weight),
+                                    ptr(ln.bias), float(ln.eps), float(act.negative_slope), ptr(y), m, st),
+              "vg_gemm_ln_act_ms")
+        return y
+
+    def _forward_stacked_nograd(self, prep, z, k: int):
+        """The no-grad forward over k stacked copies (critic labels, inference
+        sweep): models.py:119-145 with both concatenations replaced by
+        multi-source GEMMs and the copy-invariant [em | voxel.x] products
+        formed once per building batch.  None when a layer shape falls outside
+        the fused kernels (then the generic path runs)."""
+        mlp_b, dec_b = self._mlp_blocks(self.mlp_encoder), self._mlp_blocks(self.decoder)
+        if not mlp_b or not dec_b or not all(64 < b[0].out_features <= 128 for b in (mlp_b[0], dec_b[0])):
+            return None
+        em = self.matched_features_encoder(prep.matched_x)
+        vx = prep.voxel_x
+        n = vx.shape[0]
+        rows = k * n
+        hl, vd = em.shape[1], vx.shape[1]
+        zz = z.reshape(rows, -1).contiguous()
+        zd = zz.shape[1]
+        emvx = torch.cat([em, vx], dim=-1).contiguous()  # N rows only
+        # MLP encoder input [em | voxel.x | z] (models.py:131)
+        x = self._first_block_ms(mlp_b[0], [(zz, zd, hl + vd)], emvx, 0, rows, n)
+        for lin, ln, act in mlp_b[1:]:
+            x = linear_ln_act(x, lin.weight, lin.bias, ln.weight, ln.bias, ln.eps, act.negative_slope)
+        csr = prep.csr.stacked(k)
+        enc = self.encoder(x, csr, self.rng, segments=k)
+        ec, hg = enc.shape[1], x.shape[1]
+        # decoder input [enc | x | em | voxel.x | z] (models.py:145)
+        d = self._first_block_ms(dec_b[0], [(enc, ec, 0), (x, hg, ec), (zz, zd, ec + hg + hl + vd)], emvx, ec + hg,
+                                 rows, n)
+        mods = list(self.decoder.children())[3:]
+        return run_blocks(mods, d)
+
     def forward(self, local_graph, voxel_graph, z, noise: Optional[torch.Tensor] = None):
         """z [1, N, Z] (the reference's shape) -> ([N, 7] x 3).  z [k, N, Z]
         with k > 1 draws k independent samples in ONE stacked forward (the
@@ -170,6 +229,14 @@ class VoxelGNNGenerator(nn.Module):
         returns [k, N, 7] tensors; the program-feature encoder runs once."""
         prep = vdata.prepared(local_graph, voxel_graph, self.configuration.NUM_CLASSES)
         k = z.shape[0] if z.dim() == 3 else 1
+        if k > 1 and not torch.is_grad_enabled() and prep.voxel_x.is_cuda:
+            logits = self._forward_stacked_nograd(prep, z, k)
+            if logits is not None:
+                n = prep.voxel_x.shape[0]
+                if noise is None:
+                    noise = self.rng.exponential(logits.shape, logits.device)
+                label_hard, label_soft = ops.gumbel_head(logits, noise.reshape(logits.shape), self.tau)
+                return logits.view(k, n, -1), label_hard.view(k, n, -1), label_soft.view(k, n, -1)
         em = self.matched_features_encoder(prep.matched_x)
         vx = prep.voxel_x
         n = vx.shape[0]

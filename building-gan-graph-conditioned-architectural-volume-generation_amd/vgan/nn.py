@@ -234,26 +234,30 @@ class MLP(nn.Sequential):
     one GEMM with the ReLU in its epilogue."""
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        mods = list(self)
-        i = 0
-        while i < len(mods):
-            m = mods[i]
-            if (isinstance(m, nn.Linear) and i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU)
-                    and x.dim() == 2):  # ReLU in the GEMM epilogue
-                x = _LinearFn.apply(x.contiguous(), m.weight, m.bias, ops.ACT_RELU)
-                i += 2
-                continue
-            if (isinstance(m, nn.Linear) and i + 2 < len(mods) and isinstance(mods[i + 1], nn.LayerNorm)
-                    and isinstance(mods[i + 2], nn.LeakyReLU) and len(mods[i + 1].normalized_shape) == 1
-                    and mods[i + 1].elementwise_affine):
-                ln = mods[i + 1]
-                if m.out_features <= 128 and x.dim() == 2:  # LayerNorm in the GEMM epilogue
-                    x = linear_ln_act(x, m.weight, m.bias, ln.weight, ln.bias, ln.eps, mods[i + 2].negative_slope)
-                else:
-                    x = ops.ln_act(linear(x, m.weight, m.bias), ln.weight, ln.bias, ln.eps,
-                                   mods[i + 2].negative_slope)
-                i += 3
+        return run_blocks(list(self), x)
+
+
+def run_blocks(mods, x: torch.Tensor) -> torch.Tensor:
+    """MLP.forward over a list of children (also used for an MLP's tail)."""
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        if (isinstance(m, nn.Linear) and i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU)
+                and x.dim() == 2):  # ReLU in the GEMM epilogue
+            x = _LinearFn.apply(x.contiguous(), m.weight, m.bias, ops.ACT_RELU)
+            i += 2
+            continue
+        if (isinstance(m, nn.Linear) and i + 2 < len(mods) and isinstance(mods[i + 1], nn.LayerNorm)
+                and isinstance(mods[i + 2], nn.LeakyReLU) and len(mods[i + 1].normalized_shape) == 1
+                and mods[i + 1].elementwise_affine):
+            ln = mods[i + 1]
+            if m.out_features <= 128 and x.dim() == 2:  # LayerNorm in the GEMM epilogue
+                x = linear_ln_act(x, m.weight, m.bias, ln.weight, ln.bias, ln.eps, mods[i + 2].negative_slope)
             else:
-                x = m(x)
-                i += 1
-        return x
+                x = ops.ln_act(linear(x, m.weight, m.bias), ln.weight, ln.bias, ln.eps,
+                               mods[i + 2].negative_slope)
+            i += 3
+        else:
+            x = m(x)
+            i += 1
+    return x

@@ -455,6 +455,29 @@ int vg_gat_jvp2_deferred(const int32_t* row_ptr, const int32_t* col, const int32
 int vg_rng_fill(float* out, int64_t n, int32_t kind, uint64_t seed, const int64_t* iter, uint32_t salt,
                 void* stream);
 
+/* ---- multi-source LayerNorm GEMM (no-grad stacked generator forward) ------- */
+
+/* One source of vg_gemm_ln_act_ms's A: `cols` columns (a multiple of 32) of
+ * a row-major matrix with row stride `ld`, multiplied by W's columns
+ * [w_col0, w_col0 + cols).  rows_mod: reserved, must be 0. */
+typedef struct vg_asrc {
+  const float* ptr;
+  int32_t ld;
+  int32_t cols;
+  int32_t w_col0;
+  int32_t rows_mod;
+} vg_asrc;
+
+/* Y = LeakyReLU(LayerNorm([A_0 | A_1 | ...] W_sel^T + bias + addend[n mod
+ * add_rows])), 64 < M <= 128: the first [Linear, LayerNorm, LeakyReLU] block of
+ * the generator's MLP encoder and decoder over stacked copies without
+ * materialising torch.cat (models.py:131,145); the copy-invariant columns are
+ * folded into `addend` (nullable, add_rows >= 32).  Y row stride ldy. */
+int vg_gemm_ln_act_ms(const vg_asrc* src, int32_t nsrc, const float* W, int32_t ldw, int32_t N,
+                      int32_t M, const float* bias, const float* addend, int32_t ld_add,
+                      int32_t add_rows, const float* gamma, const float* beta, float eps, float slope,
+                      float* Y, int32_t ldy, void* stream);
+
 /* ---- optimiser ---------------------------------------------------------- */
 
 /* torch.optim.Adam (single-tensor semantics, weight_decay, no amsgrad) over one

@@ -257,9 +257,14 @@ def test_stacked_generator_forward_equals_separate(cuda):
         lk, hk, sk = G(loc, vox, z, noise=noise)
         for i in range(k):
             l1, h1, s1 = G(loc, vox, z[i:i + 1], noise=noise[i])
-            assert torch.allclose(lk[i], l1, rtol=1e-4, atol=1e-5)
-            assert torch.allclose(sk[i], s1, rtol=1e-4, atol=1e-6)
-            assert (hk[i].argmax(1) != h1.argmax(1)).sum().item() <= 1
+            # the stacked no-grad path sums the first MLP / decoder layers in
+            # another order (copy-invariant columns folded once, multi-source
+            # GEMM); f32 rounding then grows through the 14 GAT blocks
+            err = float((lk[i] - l1).abs().max() / l1.abs().max())
+            print(f"copy {i}: max |stacked - separate| / max|logits| = {err:.2e}")
+            assert err < 1e-3
+            assert torch.allclose(sk[i], s1, rtol=1e-3, atol=1e-4)
+            assert (hk[i].argmax(1) != h1.argmax(1)).float().mean().item() <= 2e-3
 
 
 def test_gumbel_head_device_temperatures(cuda):
