@@ -11,10 +11,9 @@
 // launches fewer per critic iteration.  The descriptors travel by value in the
 // kernel arguments (no host-to-device copy, capturable in a hipGraph).
 //
-// Summation order is that of the immediate folds, so results are bit-identical:
-// per source, 16 waves stride the partial rows with four accumulators combined
-// as (a0 + a1) + (a2 + a3), the waves are added in order, and the destination
-// becomes (out + source 0) + source 1.
+// Summation order is fixed (deterministic): per source, 16 waves stride the
+// partial rows with sixteen accumulators combined pairwise, the waves are added
+// in order, and the destination becomes (out + source 0) + source 1.
 #include "common.h"
 
 namespace {
@@ -25,18 +24,26 @@ struct FoldBatch {
   vg_fold f[VG_FOLD_MAX];
 };
 
+// Sixteen rows in flight per wave and iteration (the GAT / LayerNorm partial
+// sets have up to a few thousand rows: a short dependent loop, not one round
+// trip per four rows); fixed combination order.
 __device__ __forceinline__ float fold_rows_sum(const float* __restrict__ part, int rows, int ld,
                                                long long w, int wave) {
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  constexpr int U = 16;
+  float a[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) a[u] = 0.f;
   int r = wave;
-  for (; r + 48 < rows; r += 64) {
-    a0 += part[(size_t)r * ld + w];
-    a1 += part[(size_t)(r + 16) * ld + w];
-    a2 += part[(size_t)(r + 32) * ld + w];
-    a3 += part[(size_t)(r + 48) * ld + w];
+  for (; r + 16 * (U - 1) < rows; r += 16 * U) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) a[u] += part[(size_t)(r + 16 * u) * ld + w];
   }
-  for (; r < rows; r += 16) a0 += part[(size_t)r * ld + w];
-  return (a0 + a1) + (a2 + a3);
+  for (; r < rows; r += 16) a[0] += part[(size_t)r * ld + w];
+#pragma unroll
+  for (int h = U / 2; h > 0; h >>= 1)
+#pragma unroll
+    for (int u = 0; u < h; ++u) a[u] += a[u + h];
+  return a[0];
 }
 
 __global__ void __launch_bounds__(1024) k_fold_batch(const FoldBatch b) {
