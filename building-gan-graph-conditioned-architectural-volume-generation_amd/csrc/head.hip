@@ -188,41 +188,61 @@ __global__ void k_adam_dev(float* __restrict__ p, const float* __restrict__ g,
 constexpr int kGLThreads = 256;
 constexpr int kGLMaxBlocks = 256;
 
+template <int KM>  // KM >= K: class-count bound the loops unroll to (8 or kMaxClasses)
 __global__ void __launch_bounds__(kGLThreads) k_gen_loss_partial(
     const float* __restrict__ d_fake, const float* __restrict__ hard,
     const float* __restrict__ logits, const float* __restrict__ onehot,
     const int64_t* __restrict__ type, int N, int K, float* __restrict__ part) {
+  constexpr int WM = 2 * KM + 2;
   const int W = 2 * K + 2;
-  float acc[2 * kMaxClasses + 2];
-  for (int i = 0; i < W; ++i) acc[i] = 0.f;
+  // acc slots: [0] d_fake, [1 + c] hard, [1 + KM + c] onehot, [WM - 1] ce
+  float acc[WM];
+#pragma unroll
+  for (int i = 0; i < WM; ++i) acc[i] = 0.f;
   for (int n = blockIdx.x * blockDim.x + threadIdx.x; n < N; n += gridDim.x * blockDim.x) {
     acc[0] += d_fake[n];
+    float lg[KM];
     float m = -INFINITY;
-    for (int c = 0; c < K; ++c) {
-      acc[1 + c] += hard[(size_t)n * K + c];
-      acc[1 + K + c] += onehot[(size_t)n * K + c];
-      m = fmaxf(m, logits[(size_t)n * K + c]);
-    }
-    float se = 0.f;
-    for (int c = 0; c < K; ++c) se += expf(logits[(size_t)n * K + c] - m);
-    acc[2 * K + 1] += (m + logf(se)) - logits[(size_t)n * K + type[n]];
+#pragma unroll
+    for (int c = 0; c < KM; ++c)
+      if (c < K) {
+        acc[1 + c] += hard[(size_t)n * K + c];
+        acc[1 + KM + c] += onehot[(size_t)n * K + c];
+        lg[c] = logits[(size_t)n * K + c];
+        m = fmaxf(m, lg[c]);
+      }
+    float se = 0.f, lt = 0.f;
+    const int64_t ty = type[n];
+#pragma unroll
+    for (int c = 0; c < KM; ++c)
+      if (c < K) {
+        se += expf(lg[c] - m);
+        if (c == ty) lt = lg[c];
+      }
+    acc[WM - 1] += (m + logf(se)) - lt;
   }
-  __shared__ float red[kGLThreads];
-  for (int i = 0; i < W; ++i) {  // fixed-order block reduction, one value at a time
-    red[threadIdx.x] = acc[i];
-    __syncthreads();
-    for (int off = kGLThreads / 2; off > 0; off >>= 1) {
-      if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) part[(size_t)blockIdx.x * W + i] = red[0];
-    __syncthreads();
+  // fixed-order reduction: xor tree inside each wave, then the waves in order
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+    for (int off = 32; off > 0; off >>= 1) acc[i] += __shfl_xor(acc[i], off, 64);
+  __shared__ float red[kGLThreads / 64][WM];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < WM; ++i) red[wave][i] = acc[i];
+  __syncthreads();
+  if ((int)threadIdx.x < W) {  // output slot -> acc slot
+    const int i = threadIdx.x;
+    const int slot = i == 0 ? 0 : i <= K ? i : i <= 2 * K ? 1 + KM + (i - 1 - K) : WM - 1;
+    float v = 0.f;
+    for (int w = 0; w < kGLThreads / 64; ++w) v += red[w][slot];
+    part[(size_t)blockIdx.x * W + i] = v;
   }
 }
 
 // out: [0] loss, [1..K] d loss / d hard[n, c], [K+1] d loss / d d_fake[n],
 // [K+2] l_label / N (the cross-entropy gradient scale)
-__global__ void __launch_bounds__(64) k_gen_loss_final(const float* __restrict__ part, int nb, int N,
+__global__ void __launch_bounds__(1024) k_gen_loss_final(const float* __restrict__ part, int nb, int N,
                                                        int K, const float* __restrict__ far_gen,
                                                        const float* __restrict__ far_ref, int G,
                                                        float l_adv, float l_label, float l_ratio,
@@ -230,10 +250,14 @@ __global__ void __launch_bounds__(64) k_gen_loss_final(const float* __restrict__
                                                        float* __restrict__ out) {
   __shared__ float tot[2 * kMaxClasses + 2];
   const int W = 2 * K + 2;
-  for (int i = threadIdx.x; i < W; i += blockDim.x) {
-    float v = 0.f;
-    for (int b = 0; b < nb; ++b) v += part[(size_t)b * W + i];
-    tot[i] = v;
+  {  // one wave per value, lanes over the partial rows, fixed xor tree
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int i = wave; i < W; i += blockDim.x / 64) {
+      float v = 0.f;
+      for (int b = lane; b < nb; b += 64) v += part[(size_t)b * W + i];
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+      if (lane == 0) tot[i] = v;
+    }
   }
   __syncthreads();
   if (threadIdx.x != 0) return;
@@ -390,9 +414,12 @@ extern "C" int vg_gen_loss_fwd(const float* d_fake, const float* hard, const flo
     return VG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int nb = vg_blocks(N, kGLThreads) < kGLMaxBlocks ? vg_blocks(N, kGLThreads) : kGLMaxBlocks;
-  k_gen_loss_partial<<<nb, kGLThreads, 0, s>>>(d_fake, hard, logits, onehot, type, N, classes,
-                                               workspace);
-  k_gen_loss_final<<<1, 64, 0, s>>>(workspace, nb, N, classes, far_gen, far_ref, num_graphs, l_adv,
+  if (classes <= 8)
+    k_gen_loss_partial<8><<<nb, kGLThreads, 0, s>>>(d_fake, hard, logits, onehot, type, N, classes, workspace);
+  else
+    k_gen_loss_partial<kMaxClasses><<<nb, kGLThreads, 0, s>>>(d_fake, hard, logits, onehot, type, N, classes,
+                                                              workspace);
+  k_gen_loss_final<<<1, 1024, 0, s>>>(workspace, nb, N, classes, far_gen, far_ref, num_graphs, l_adv,
                                     l_label, l_ratio, l_void, l_far, out);
   VG_CHECK_LAUNCH();
   return 0;
