@@ -280,10 +280,22 @@ def main():
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a ROCm GPU")
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    # VGAN_DIST_BACKEND=gloo rehearses the N>1 path (barriers, rank sharding,
+    # eager all-reduce + Adam between replays, max-over-ranks timing) with
+    # several ranks sharing the GPUs of a smaller box; RCCL ("nccl") is the
+    # product backend and refuses two ranks on one GPU.
+    backend = os.environ.get("VGAN_DIST_BACKEND", "nccl")
+    n_dev = torch.cuda.device_count()
+    if local >= n_dev and backend == "nccl":
+        raise SystemExit(f"LOCAL_RANK {local} but only {n_dev} GPU(s) visible")
+    local_dev = local % n_dev
+    torch.cuda.set_device(local_dev)
+    device = torch.device("cuda", local_dev)
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
 
     from vgan.config import Configuration
 
