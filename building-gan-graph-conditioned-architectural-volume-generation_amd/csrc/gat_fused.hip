@@ -44,6 +44,10 @@ using namespace vg;
 #endif
 constexpr int kMaxBwdBlocks = VG_BWD_MAX_BLOCKS;  // grid cap of the backward row passes (partials count)
 constexpr int kEP = 3;                // edge slots per lane in the edge-parallel kernels
+#ifndef VG_FWD_ROWS
+#define VG_FWD_ROWS 4
+#endif
+constexpr int kFwdRows = VG_FWD_ROWS;  // neighbour rows in flight per step of the forward gather-sum
 
 template <int CPL>
 __device__ __forceinline__ void load_param(Vec<CPL>& r, const float* __restrict__ p, int c0, int C) {
@@ -134,12 +138,12 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_cp(
 #pragma unroll
   for (int q = 0; q < CPL; ++q) acc.v[q] = 0.f;
   const int dreg = deg < T * L ? deg : T * L;
-  for (int j0 = 0; j0 < dreg; j0 += 4) {
-    const int nj = dreg - j0 < 4 ? dreg - j0 : 4;
-    Vec<CPL> hv[4];
-    float a[4];
+  for (int j0 = 0; j0 < dreg; j0 += kFwdRows) {
+    const int nj = dreg - j0 < kFwdRows ? dreg - j0 : kFwdRows;
+    Vec<CPL> hv[kFwdRows];
+    float a[kFwdRows];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < kFwdRows; ++u)
       if (u < nj) {
         const int j = j0 + u;
         const int t = j / L;
@@ -150,7 +154,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_cp(
         load_row<CPL, VEC>(hv[u], h + (size_t)s * C, c0, C);
       }
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < kFwdRows; ++u)
       if (u < nj)
 #pragma unroll
         for (int q = 0; q < CPL; ++q) acc.v[q] = fmaf(a[u], hv[u].v[q], acc.v[q]);
