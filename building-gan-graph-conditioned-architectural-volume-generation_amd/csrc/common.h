@@ -60,15 +60,32 @@ __device__ __forceinline__ uint4 vg_philox(uint4 c, uint2 k) {
   return c;
 }
 
-// Dropout multiplier of element t: Bernoulli(1 - p) / (1 - p) from the
-// counter (t, salt, iteration) under key = seed.
+// Dropout multiplier of element t: Bernoulli(1 - p) / (1 - p) from lane t % 4
+// of the Philox block at counter (t / 4, salt, iteration) under key = seed --
+// one Philox call serves four consecutive elements (vg_keep4, the quad
+// elementwise kernels); vg_keep draws the same value for a single element.
+__device__ __forceinline__ float vg_keep_of(uint32_t r, float p) {
+  const float u = static_cast<float>(r >> 8) * (1.0f / 16777216.0f);
+  return u < 1.f - p ? 1.f / (1.f - p) : 0.f;
+}
+
+__device__ __forceinline__ uint4 vg_keep_block(long long q, uint32_t salt, long long iter, uint64_t seed) {
+  return vg_philox(make_uint4(static_cast<uint32_t>(q), static_cast<uint32_t>(q >> 32), salt,
+                              static_cast<uint32_t>(iter)),
+                   make_uint2(static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32)));
+}
+
+__device__ __forceinline__ float4 vg_keep4_raw(long long q, uint32_t salt, long long iter, uint64_t seed,
+                                               float p) {
+  const uint4 r = vg_keep_block(q, salt, iter, seed);
+  return make_float4(vg_keep_of(r.x, p), vg_keep_of(r.y, p), vg_keep_of(r.z, p), vg_keep_of(r.w, p));
+}
+
 __device__ __forceinline__ float vg_keep(long long t, uint32_t salt, long long iter, uint64_t seed,
                                          float p) {
-  const uint4 r = vg_philox(make_uint4(static_cast<uint32_t>(t), static_cast<uint32_t>(t >> 32), salt,
-                                       static_cast<uint32_t>(iter)),
-                            make_uint2(static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32)));
-  const float u = static_cast<float>(r.x >> 8) * (1.0f / 16777216.0f);
-  return u < 1.f - p ? 1.f / (1.f - p) : 0.f;
+  const uint4 r = vg_keep_block(t >> 2, salt, iter, seed);
+  const int l = static_cast<int>(t & 3);
+  return vg_keep_of(l == 0 ? r.x : l == 1 ? r.y : l == 2 ? r.z : r.w, p);
 }
 
 // "Last block folds": every block calls this after writing its partials; it
