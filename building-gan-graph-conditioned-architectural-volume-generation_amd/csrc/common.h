@@ -90,22 +90,31 @@ __device__ __forceinline__ float vg_keep(long long t, uint32_t salt, long long i
 
 // "Last block folds": every block calls this after writing its partials; it
 // returns true in exactly one block -- the last to arrive -- which then sees
-// all partials (release/acquire fences) and folds them in a fixed order, so
-// the result is deterministic and no separate fold launch is needed.
+// all partials and folds them in a fixed order, so the result is
+// deterministic and no separate fold launch is needed.  Hand-off in the
+// single-lane form of MI355X_MICROARCH.md (inter-workgroup visibility):
+// every wave waits for its stores, a barrier, then ONE lane releases at agent
+// scope, waits, and adds to the counter; the block whose add came last
+// acquires at agent scope, waits, and the barrier releases its waves to read.
 // `counter` is a caller-owned int32 that is 0 on entry and reset to 0 by the
 // last block (launches that share a counter must be stream-ordered).
 __device__ __forceinline__ bool vg_last_block(int* counter) {
   __shared__ int last;
-  __threadfence();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int nblocks = static_cast<int>(gridDim.x * gridDim.y * gridDim.z);
-    const int prev = atomicAdd(counter, 1);
+    const int prev = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = prev == nblocks - 1;
-    if (last) atomicExch(counter, 0);
+    if (last) {
+      __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }
   __syncthreads();
-  if (last) __threadfence();
   return last != 0;
 }
 
