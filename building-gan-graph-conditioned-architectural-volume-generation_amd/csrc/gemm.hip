@@ -546,9 +546,12 @@ extern "C" int vg_gemm(const float* A, int32_t lda, const float* B, int32_t ldb,
 // rows per split-K chunk: aim at ~768 workgroups in total but at most
 // 256 chunks per output tile (the fold reads chunks x M x K partials; more chunks
 // made the fold, not the product, the long pole), multiples of TK
+#ifndef VG_TN_TARGET
+#define VG_TN_TARGET 768
+#endif
 static inline int tn_rows(int N, int M, int K) {
   const int tiles = ((M + TM - 1) / TM) * ((K + TN - 1) / TN);
-  int target = 768 / tiles;
+  int target = VG_TN_TARGET / tiles;
   if (target > 256) target = 256;
   if (target < 1) target = 1;
   int rows = (N + target - 1) / target;
