@@ -448,3 +448,89 @@ def test_linear_ln_act_fused_matches_unfused(cuda, m, k):
     gy = torch.randn(n, m, device=cuda)
     for u, v in zip(torch.autograd.grad(y1, p1, gy), torch.autograd.grad(y2, p2, gy)):
         assert rel_err(u, v) < 1e-5
+
+
+@pytest.mark.parametrize("C", [1, 8, 64])
+@pytest.mark.parametrize("case", ["edgeless", "single_node", "self_loops_only"])
+def test_gat_conv_degenerate_graphs(cuda, C, case):
+    """Graphs with no edges besides GATConv's own self loops: E = 0, a single
+    node, and an edge_index holding only self loops (removed, then re-added,
+    as torch_geometric's GATConv does).  Every row then has exactly one
+    neighbour, itself: alpha = 1 and out = h + bias."""
+    torch.manual_seed(100 + C)
+    n = {"edgeless": 7, "single_node": 1, "self_loops_only": 9}[case]
+    if case == "self_loops_only":
+        ei = torch.arange(n).repeat(2, 1)
+    else:
+        ei = torch.zeros(2, 0, dtype=torch.long)
+    csr = ops.CSR(ei.to(cuda), n)
+    assert csr.num_edges == n
+    h = torch.randn(n, C, dtype=torch.float64, requires_grad=True)
+    att_s = (torch.randn(C, dtype=torch.float64) / C ** 0.5).requires_grad_(True)
+    att_d = (torch.randn(C, dtype=torch.float64) / C ** 0.5).requires_grad_(True)
+    b = torch.randn(C, dtype=torch.float64, requires_grad=True)
+    ref = _oracle_gat(h, att_s, att_d, b, ei)
+    assert torch.allclose(ref, h + b)
+    g_out = torch.randn(n, C, dtype=torch.float64)
+    ref_grads = torch.autograd.grad(ref, (h, att_s, att_d, b), g_out)
+    gt = [t.detach().float().to(cuda).requires_grad_(True) for t in (h, att_s, att_d, b)]
+    out = ops.gat_conv(csr, *gt)
+    assert rel_err(out, ref) < 1e-6
+    grads = torch.autograd.grad(out, gt, g_out.float().to(cuda))
+    for got, want in zip(grads, ref_grads):
+        if want.norm() == 0:  # att_src / att_dst: softmax over one edge has no gradient
+            assert got.abs().max().item() < 1e-6
+        else:
+            assert rel_err(got, want) < 1e-5
+
+
+@pytest.mark.parametrize("n", [1, 2, 5])
+@pytest.mark.parametrize("C", [4, 16])
+def test_graphnorm_tiny_row_counts(cuda, n, C):
+    """GraphNorm over 1-5 rows (a zero-variance column at n = 1: torch's std
+    backward mask) through the quad apply passes."""
+    torch.manual_seed(n * 31 + C)
+    x = torch.randn(n, C, dtype=torch.float64) * 2 + 0.5
+    w = torch.rand(C, dtype=torch.float64) + 0.5
+    b = torch.randn(C, dtype=torch.float64) * 0.3
+    ms = torch.rand(C, dtype=torch.float64)
+    ts = [t.clone().requires_grad_(True) for t in (x, w, b, ms)]
+    ref = ops.graphnorm_relu_dropout_torch(ts[0], ts[1], ts[2], ts[3], None, 1e-5)
+    gy = torch.randn(n, C, dtype=torch.float64)
+    ref_g = torch.autograd.grad(ref, ts, gy)
+    gt = [t.float().to(cuda).requires_grad_(True) for t in (x, w, b, ms)]
+    out = ops.graphnorm_relu_dropout(gt[0], gt[1], gt[2], gt[3], None)
+    # sigma = 0 at n = 1: (1 - mean_scale) x / eps, large but exact up to f32 rounding
+    assert rel_err(out, ref) < 1e-5
+    got_g = torch.autograd.grad(out, gt, gy.float().to(cuda))
+    for a, r in zip(got_g, ref_g):
+        assert rel_err(a, r) < 1e-4 or (a.double().cpu() - r).abs().max().item() < 1e-6
+
+
+def test_graphnorm_quad_and_scalar_paths_agree(cuda):
+    """The quad apply passes (16-B aligned rows) and the scalar ones (the same
+    rows read through a 4-byte-offset view) give the same forward and
+    backward, and draw the same in-kernel dropout mask."""
+    from vgan.rng import RNG
+
+    torch.manual_seed(5)
+    n, c = 513, 32
+    base = torch.randn(n * c + 1, device=cuda)
+    x_al = base[: n * c].view(n, c).clone()  # aligned copy
+    x_mis = base[1:].view(n, c)  # misaligned storage -> scalar kernels
+    x_mis.copy_(x_al)
+    assert x_mis.data_ptr() % 16 != 0
+    w, b, ms = torch.rand(c, device=cuda) + 0.5, torch.randn(c, device=cuda), torch.rand(c, device=cuda)
+    rng = RNG("device", seed=99)
+    rng.reset()
+    spec = rng.keep_mask((n, c), 0.2, cuda)
+    xa = x_al.clone().requires_grad_(True)
+    ya = ops.graphnorm_relu_dropout(xa, w, b, ms, spec)
+    xm = x_mis.detach().requires_grad_(True)
+    ym = ops.graphnorm_relu_dropout(xm, w, b, ms, spec)
+    assert torch.equal(ya == 0, ym == 0)  # the same dropout mask (and ReLU pattern)
+    assert torch.allclose(ya, ym, rtol=1e-6, atol=1e-6)
+    gy = torch.randn(n, c, device=cuda)
+    (ga,) = torch.autograd.grad(ya, xa, gy)
+    (gm,) = torch.autograd.grad(ym, xm, gy)
+    assert torch.allclose(ga, gm, rtol=1e-5, atol=1e-6)
