@@ -6,6 +6,9 @@ usage: prof_summary.py TRACE.csv [TOP] [--after-gap] [--steps K]
                (bench.py --profile sleeps 50 ms before its timed steps and
                returns right after them; staging and capture gaps come earlier)
   --steps K    also report per-step dispatch counts / busy time
+  --gaps       also report the idle gaps between consecutive dispatches of
+               the kept region: total per size bucket and the largest ones
+               with the kernels on either side
 """
 import csv
 import sys
@@ -36,5 +39,32 @@ print(f"dispatches {len(rows)}  kernel-busy {busy / 1e3:.2f} ms  span {(t1 - t0)
 if steps:
     print(f"per step: {len(rows) / steps:.0f} dispatches, {busy / 1e3 / steps:.3f} ms busy, "
           f"{(t1 - t0) / 1e6 / steps:.3f} ms span")
+if "--gaps" in sys.argv:
+    import re
+
+    def short(n):
+        m = re.search(r"::(k_\w+)", n)
+        return m.group(1) if m else n[:40]
+
+    buckets = [(1, "<1 us"), (5, "1-5 us"), (20, "5-20 us"), (100, "20-100 us"), (float("inf"), ">=100 us")]
+    acc = {b: [0, 0.0] for _, b in buckets}
+    big = []
+    end = rows[0][1]
+    for i in range(1, len(rows)):
+        g = (rows[i][0] - end) / 1e3
+        end = max(end, rows[i][1])
+        if g <= 0:
+            continue
+        for lim, b in buckets:
+            if g < lim:
+                acc[b][0] += 1
+                acc[b][1] += g
+                break
+        big.append((g, short(rows[i - 1][2]), short(rows[i][2])))
+    div = steps or 1
+    print("idle gaps per step: " + ", ".join(f"{b}: {acc[b][0] / div:.0f} x, {acc[b][1] / div:.1f} us"
+                                              for _, b in buckets))
+    for g, a, b in sorted(big, reverse=True)[:12]:
+        print(f"  gap {g:8.1f} us  {a} -> {b}")
 for name, (n, us) in sorted(tot.items(), key=lambda kv: -kv[1][1])[:top]:
     print(f"{us / 1e3:9.3f} ms {n:7d} x {us / n:8.2f} us  {name[:110]}")
