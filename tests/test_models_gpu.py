@@ -238,10 +238,12 @@ def test_direct_param_grads_match_autograd(cuda):
     assert torch.allclose(grads[0], grads[1], rtol=1e-5, atol=1e-6)
 
 
-def test_stacked_generator_forward_equals_separate(cuda):
+@pytest.mark.parametrize("k", [3, 24])
+def test_stacked_generator_forward_equals_separate(cuda, k):
     """G(z [k, N, Z]) -- k samples in one stacked forward (block-diagonal CSR,
     per-copy GraphNorm statistics) -- equals k separate forwards (eval mode,
-    same z and Gumbel noise)."""
+    same z and Gumbel noise).  k = 24 stacks > 32k rows (more than the
+    step's five critic-label copies)."""
     from vgan.synth import SyntheticDataset
 
     cfg = Configuration()
@@ -250,12 +252,13 @@ def test_stacked_generator_forward_equals_separate(cuda):
     G = VoxelGNNGenerator(cfg, 17, 12).eval()
     loc, vox = SyntheticDataset(16, seed=6).batch(range(4))
     loc, vox = loc.to(cuda), vox.to(cuda)
-    k, n = 3, vox.num_nodes
+    n = vox.num_nodes
+    assert k < 24 or k * n >= 32768
     z = torch.randn(k, n, cfg.Z_DIM, device=cuda)
     noise = torch.empty(k, n, 7, device=cuda).exponential_()
     with torch.no_grad():
         lk, hk, sk = G(loc, vox, z, noise=noise)
-        for i in range(k):
+        for i in sorted({0, k // 2, k - 1}):
             l1, h1, s1 = G(loc, vox, z[i:i + 1], noise=noise[i])
             # the stacked no-grad path sums the first MLP / decoder layers in
             # another order (copy-invariant columns folded once, multi-source

@@ -426,14 +426,14 @@ def test_graphnorm_in_kernel_dropout(cuda):
     assert torch.allclose(gx, gx2, rtol=1e-4, atol=1e-6)
 
 
-@pytest.mark.parametrize("m,k", [(16, 17), (64, 128), (100, 268), (128, 524), (128, 128)])
-def test_linear_ln_act_fused_matches_unfused(cuda, m, k):
+@pytest.mark.parametrize("m,k,n", [(16, 17, 1537), (64, 128, 1537), (100, 268, 1537), (128, 524, 1537),
+                                   (128, 128, 1537), (128, 268, 33001)])
+def test_linear_ln_act_fused_matches_unfused(cuda, m, k, n):
     """vg_gemm_ln_act (LayerNorm + LeakyReLU in the GEMM epilogue) against
     Linear -> ln_act and torch fp64, forward and first-order gradients."""
     from vgan.nn import linear, linear_ln_act
 
     torch.manual_seed(m + k)
-    n = 1537
     x = torch.randn(n, k, device=cuda)
     w = torch.randn(m, k, device=cuda) / k ** 0.5
     b, g, be = torch.randn(m, device=cuda), 1 + 0.1 * torch.randn(m, device=cuda), 0.1 * torch.randn(m, device=cuda)
