@@ -101,8 +101,8 @@ def test_gat_conv_forward_backward(cuda, C, graph):
     assert rel_err(comp, out) < 1e-5
 
 
-@pytest.mark.parametrize("C", [1, 3, 8, 9, 32, 64, 100, 128])
-@pytest.mark.parametrize("cin", [7, 64])
+@pytest.mark.parametrize("C", [1, 3, 8, 9, 16, 32, 64, 100, 128])
+@pytest.mark.parametrize("cin", [1, 7, 16, 64])
 def test_lin_att_and_aggregate_match_oracle(cuda, C, cin):
     """vg_gat_lin_att (projection GEMM + attention projections in its
     epilogue) and vg_gat_aggregate_fwd (edge softmax + gather-sum) against the
