@@ -98,16 +98,17 @@ __device__ __forceinline__ float vg_keep(long long t, uint32_t salt, long long i
 // acquires at agent scope, waits, and the barrier releases its waves to read.
 // `counter` is a caller-owned int32 that is 0 on entry and reset to 0 by the
 // last block (launches that share a counter must be stream-ordered).
-__device__ __forceinline__ bool vg_last_block(int* counter) {
+// vg_last_arrival: the same over a group of `arrivals` blocks sharing a
+// counter (called uniformly by every thread of each block).
+__device__ __forceinline__ bool vg_last_arrival(int* counter, int arrivals) {
   __shared__ int last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int nblocks = static_cast<int>(gridDim.x * gridDim.y * gridDim.z);
     const int prev = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = prev == nblocks - 1;
+    last = prev == arrivals - 1;
     if (last) {
       __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -116,6 +117,11 @@ __device__ __forceinline__ bool vg_last_block(int* counter) {
   }
   __syncthreads();
   return last != 0;
+}
+
+// the whole grid arrives on one counter
+__device__ __forceinline__ bool vg_last_block(int* counter) {
+  return vg_last_arrival(counter, static_cast<int>(gridDim.x * gridDim.y * gridDim.z));
 }
 
 static inline int vg_blocks(long long work, int per_block) {
