@@ -47,7 +47,10 @@ constexpr int kEP = 3;                // edge slots per lane in the edge-paralle
 #ifndef VG_FWD_ROWS
 #define VG_FWD_ROWS 4
 #endif
-constexpr int kFwdRows = VG_FWD_ROWS;  // neighbour rows in flight per step of the forward gather-sum
+constexpr int kFwdRows = VG_FWD_ROWS;
+#ifndef VG_FWD_C64_L8
+#define VG_FWD_C64_L8 0  // 33..64 channels: 8 lanes x 8 channels per row (A/B knob)
+#endif  // neighbour rows in flight per step of the forward gather-sum
 
 template <int CPL>
 __device__ __forceinline__ void load_param(Vec<CPL>& r, const float* __restrict__ p, int c0, int C) {
@@ -741,6 +744,9 @@ extern "C" int vg_gat_aggregate_fwd(const int32_t* row_ptr, const int32_t* col, 
     else
       k_gat_fwd_ep<8, true><<<grid, kBlock, 0, s>>>(row_ptr, col, N, C, h, nullptr, nullptr, bias,
                                                      slope, out, alpha, as, ad);
+  } else if (VG_FWD_C64_L8 && C > 32 && C <= 64 && C % 8 == 0) {
+    k_gat_fwd_cp<8, 8, true><<<grid_for(N, 8), kBlock, 0, s>>>(row_ptr, col, N, C, h, a_src, a_dst, bias,
+                                                                slope, out, alpha);
   } else {
     VG_DISPATCH_FUSED(C, (k_gat_fwd_cp<L_, CPL_, V_><<<grid_for(N, L_), kBlock, 0, s>>>(
                              row_ptr, col, N, C, h, a_src, a_dst, bias, slope, out, alpha)));
