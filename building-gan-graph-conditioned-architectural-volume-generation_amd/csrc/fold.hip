@@ -18,27 +18,34 @@
 
 namespace {
 
+#ifndef VG_FOLD_SHORT_ROWS
+#define VG_FOLD_SHORT_ROWS 256
+#endif
+constexpr int kShortRows = VG_FOLD_SHORT_ROWS;
+
 struct FoldBatch {
   int32_t n;
   int32_t block0[VG_FOLD_MAX + 1];  // first workgroup of fold i; block0[n] = grid size
+  int32_t waves[VG_FOLD_MAX];       // waves per 64-column group: 16, or 4 for short folds
   vg_fold f[VG_FOLD_MAX];
 };
 
 // Sixteen rows in flight per wave and iteration (the GAT / LayerNorm partial
 // sets have up to a few thousand rows: a short dependent loop, not one round
-// trip per four rows); fixed combination order.
+// trip per four rows); fixed combination order.  `stride` = waves per column
+// group.
 __device__ __forceinline__ float fold_rows_sum(const float* __restrict__ part, int rows, int ld,
-                                               long long w, int wave) {
+                                               long long w, int sub, int stride) {
   constexpr int U = 16;
   float a[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) a[u] = 0.f;
-  int r = wave;
-  for (; r + 16 * (U - 1) < rows; r += 16 * U) {
+  int r = sub;
+  for (; r + stride * (U - 1) < rows; r += stride * U) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) a[u] += part[(size_t)(r + 16 * u) * ld + w];
+    for (int u = 0; u < U; ++u) a[u] += part[(size_t)(r + stride * u) * ld + w];
   }
-  for (; r < rows; r += 16) a[0] += part[(size_t)r * ld + w];
+  for (; r < rows; r += stride) a[0] += part[(size_t)r * ld + w];
 #pragma unroll
   for (int h = U / 2; h > 0; h >>= 1)
 #pragma unroll
@@ -46,24 +53,30 @@ __device__ __forceinline__ float fold_rows_sum(const float* __restrict__ part, i
   return a[0];
 }
 
+// A workgroup (16 waves) folds 64 columns with 16 waves striding the rows, or
+// -- short folds (<= kShortRows partial rows: the split-K weight-gradient
+// partials, ~40-256 chunks) -- 256 columns, four waves per 64-column group.
+// The generator backward folds ~274k columns: at 16 waves per 64 columns its
+// grid ran 8+ rounds of 1024-thread workgroups, each one round trip long.
 __global__ void __launch_bounds__(1024) k_fold_batch(const FoldBatch b) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int d = 0;
   while (d + 1 < b.n && (int)blockIdx.x >= b.block0[d + 1]) ++d;
   const vg_fold& f = b.f[d];
-  const long long w = (long long)(blockIdx.x - b.block0[d]) * 64 + lane;
+  const int wpg = b.waves[d];               // waves per column group
+  const int grp = wave / wpg, sub = wave % wpg;
+  const long long w = ((long long)(blockIdx.x - b.block0[d]) * (16 / wpg) + grp) * 64 + lane;
   __shared__ float red[2][16][64];
   for (int si = 0; si < f.nsrc; ++si)
-    red[si][wave][lane] = w < f.width ? fold_rows_sum(f.src[si].part, f.src[si].rows, f.src[si].ld, w, wave)
+    red[si][wave][lane] = w < f.width ? fold_rows_sum(f.src[si].part, f.src[si].rows, f.src[si].ld, w, sub, wpg)
                                       : 0.f;
   __syncthreads();
-  if (wave == 0 && w < f.width) {
+  if (sub == 0 && w < f.width) {
     float* o = f.out + (w / f.k) * f.ldo + (w % f.k);
     float v = f.accumulate ? *o : 0.f;
     for (int si = 0; si < f.nsrc; ++si) {
       float s = 0.f;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) s += red[si][k][lane];
+      for (int k = 0; k < wpg; ++k) s += red[si][wave + k][lane];
       v = f.accumulate || si > 0 ? v + s : s;
     }
     *o = v;
@@ -83,9 +96,12 @@ extern "C" int vg_fold_batch(const vg_fold* folds, int32_t n, void* stream) {
     if (!f.out || f.width <= 0 || f.k <= 0 || f.ldo < f.k || f.nsrc < 1 || f.nsrc > 2) return VG_EINVAL;
     for (int s = 0; s < f.nsrc; ++s)
       if (!f.src[s].part || f.src[s].rows < 0 || f.src[s].ld < f.width) return VG_EINVAL;
+    int rows = 0;
+    for (int s = 0; s < f.nsrc; ++s) rows = f.src[s].rows > rows ? f.src[s].rows : rows;
     b.f[i] = f;
+    b.waves[i] = rows <= kShortRows ? 4 : 16;
     b.block0[i] = blocks;
-    blocks += (f.width + 63) / 64;
+    blocks += (f.width + 64 * (16 / b.waves[i]) - 1) / (64 * (16 / b.waves[i]));
   }
   b.block0[n] = blocks;
   k_fold_batch<<<blocks, 1024, 0, static_cast<hipStream_t>(stream)>>>(b);
