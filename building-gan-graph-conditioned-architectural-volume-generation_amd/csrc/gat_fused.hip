@@ -48,6 +48,15 @@ constexpr int kEP = 3;                // edge slots per lane in the edge-paralle
 #define VG_FWD_ROWS 4
 #endif
 constexpr int kFwdRows = VG_FWD_ROWS;
+#ifndef VG_FWD_SLICE_ROWS
+#define VG_FWD_SLICE_ROWS 100000
+#endif
+constexpr int kSliceRows = VG_FWD_SLICE_ROWS;  // aggregate in 64-channel slices from this many rows
+#ifndef VG_FWD_SLICE
+#define VG_FWD_SLICE 64
+#endif
+constexpr int kSlice = VG_FWD_SLICE;  // channels per slice: 64 (L 16 x 4) or 32 (L 8 x 4)
+static_assert(kSlice == 64 || kSlice == 32, "slice width");
 #ifndef VG_FWD_C64_L8
 #define VG_FWD_C64_L8 0  // 33..64 channels: 8 lanes x 8 channels per row (A/B knob)
 #endif  // neighbour rows in flight per step of the forward gather-sum
@@ -89,7 +98,19 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_cp(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, int N, int C,
     const float* __restrict__ h, const float* __restrict__ a_src, const float* __restrict__ a_dst,
     const float* __restrict__ bias, float slope, float* __restrict__ out,
-    float* __restrict__ alpha) {
+    float* __restrict__ alpha, int ld = 0) {
+  // ld > 0: a channel slice -- h / out / bias point at the slice's first
+  // channel, rows are ld floats apart, and only the slice at blockIdx.y == 0
+  // writes alpha (every slice recomputes the row's softmax)
+  const bool wr_alpha = blockIdx.y == 0;
+  if (ld == 0) {
+    ld = C;
+  } else {
+    const int cb = blockIdx.y * C;
+    h += cb;
+    out += cb;
+    bias += cb;
+  }
   constexpr int T = 4;  // edges per lane kept in registers (rows up to 4L edges)
   const GroupIdx g = group_index<L>();
   if (g.row >= N) return;
@@ -129,11 +150,12 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_cp(
     const int k = beg + g.lane + t * L;
     if (k < end) {
       e_t[t] = e_t[t] / denom;  // alpha
-      alpha[k] = e_t[t];
+      if (wr_alpha) alpha[k] = e_t[t];
     }
   }
-  for (int k = beg + g.lane + T * L; k < end; k += L)
-    alpha[k] = expf(lrelu(a_src[col[k]] + ad, slope) - m) / denom;
+  if (wr_alpha)
+    for (int k = beg + g.lane + T * L; k < end; k += L)
+      alpha[k] = expf(lrelu(a_src[col[k]] + ad, slope) - m) / denom;
 
   // channel-parallel gather-sum, 4 neighbour rows in flight
   const int c0 = g.lane * CPL;
@@ -154,7 +176,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_cp(
         const float av = t == 0 ? e_t[0] : t == 1 ? e_t[1] : t == 2 ? e_t[2] : e_t[3];
         const int s = __shfl(sv, g.base + (j & (L - 1)), 64);
         a[u] = __shfl(av, g.base + (j & (L - 1)), 64);
-        load_row<CPL, VEC>(hv[u], h + (size_t)s * C, c0, C);
+        load_row<CPL, VEC>(hv[u], h + (size_t)s * ld, c0, C);
       }
 #pragma unroll
     for (int u = 0; u < kFwdRows; ++u)
@@ -166,7 +188,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_cp(
     const int s = col[beg + j];
     const float a = expf(lrelu(a_src[s] + ad, slope) - m) / denom;
     Vec<CPL> hv;
-    load_row<CPL, VEC>(hv, h + (size_t)s * C, c0, C);
+    load_row<CPL, VEC>(hv, h + (size_t)s * ld, c0, C);
 #pragma unroll
     for (int q = 0; q < CPL; ++q) acc.v[q] = fmaf(a, hv.v[q], acc.v[q]);
   }
@@ -174,7 +196,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_cp(
   load_param<CPL>(b, bias, c0, C);
 #pragma unroll
   for (int q = 0; q < CPL; ++q) acc.v[q] += b.v[q];
-  store_row<CPL, VEC>(acc, out + (size_t)i * C, c0, C);
+  store_row<CPL, VEC>(acc, out + (size_t)i * ld, c0, C);
 }
 
 // C <= 8: 8 lanes per destination row, one edge per lane.
@@ -744,6 +766,13 @@ extern "C" int vg_gat_aggregate_fwd(const int32_t* row_ptr, const int32_t* col, 
     else
       k_gat_fwd_ep<8, true><<<grid, kBlock, 0, s>>>(row_ptr, col, N, C, h, nullptr, nullptr, bias,
                                                      slope, out, alpha, as, ad);
+  } else if (N >= kSliceRows && C % kSlice == 0 && C > kSlice) {
+    // large graphs: 64-channel slices, slice-major in dispatch order, so the
+    // rows an XCD gathers at a time (a window of ~2 lattice floors) are half
+    // or less of the full-width footprint in its 4 MiB L2
+    constexpr int Ls = kSlice / 4;
+    k_gat_fwd_cp<Ls, 4, true><<<dim3(grid_for(N, Ls), C / kSlice), kBlock, 0, s>>>(
+        row_ptr, col, N, kSlice, h, a_src, a_dst, bias, slope, out, alpha, C);
   } else if (VG_FWD_C64_L8 && C > 32 && C <= 64 && C % 8 == 0) {
     k_gat_fwd_cp<8, 8, true><<<grid_for(N, 8), kBlock, 0, s>>>(row_ptr, col, N, C, h, a_src, a_dst, bias,
                                                                 slope, out, alpha);

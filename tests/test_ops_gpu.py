@@ -534,3 +534,39 @@ def test_graphnorm_quad_and_scalar_paths_agree(cuda):
     (ga,) = torch.autograd.grad(ya, xa, gy)
     (gm,) = torch.autograd.grad(ym, xm, gy)
     assert torch.allclose(ga, gm, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("C", [128, 256])
+def test_aggregate_channel_slices_equal_full_width(cuda, C):
+    """Graphs of >= 100k rows aggregate in 64-channel slices (gat_fused.hip
+    kSliceRows): every slice recomputes the row softmax and gathers its own
+    channels.  The result equals, bit for bit, 64-channel calls on the
+    column blocks (the same kernel shape and summation order), and alpha is
+    written once."""
+    from vgan._lib import LIB, check, ptr, stream_handle
+
+    items = [synth.make_stress_building(777, i, F=20, Y=50, X=50)[1] for i in (1, 2)]
+    from vgan.graph import GraphBatch
+
+    vox = GraphBatch.from_data_list(items)
+    n = vox.num_nodes
+    assert n >= 100000
+    csr = ops.CSR(vox.edge_index.to(cuda), n)
+    torch.manual_seed(C)
+    h = torch.randn(n, C, device=cuda)
+    a_s, a_d = torch.randn(n, device=cuda), torch.randn(n, device=cuda)
+    bias = torch.randn(C, device=cuda)
+    st = stream_handle(cuda)
+    out = torch.empty(n, C, device=cuda)
+    alpha = torch.full((csr.num_edges,), -1.0, device=cuda)
+    check(LIB.vg_gat_aggregate_fwd(ptr(csr.row_ptr), ptr(csr.col), n, C, ptr(h), ptr(a_s), ptr(a_d), ptr(bias),
+                                   0.2, ptr(out), ptr(alpha), st), "vg_gat_aggregate_fwd")
+    for j in range(C // 64):
+        hj = h[:, 64 * j:64 * (j + 1)].contiguous()
+        bj = bias[64 * j:64 * (j + 1)].contiguous()
+        oj = torch.empty(n, 64, device=cuda)
+        aj = torch.empty(csr.num_edges, device=cuda)
+        check(LIB.vg_gat_aggregate_fwd(ptr(csr.row_ptr), ptr(csr.col), n, 64, ptr(hj), ptr(a_s), ptr(a_d), ptr(bj),
+                                       0.2, ptr(oj), ptr(aj), st), "vg_gat_aggregate_fwd")
+        assert torch.equal(out[:, 64 * j:64 * (j + 1)], oj)
+        assert torch.equal(alpha, aj)
