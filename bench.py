@@ -302,6 +302,7 @@ def main():
     cfg = Configuration()
     cfg.DEVICE = str(device)
     cfg.runtime["rng"] = "device"
+    cfg.runtime["rank"], cfg.runtime["world_size"] = rank, world  # per-rank device RNG streams
     torch.manual_seed(cfg.SEED + rank)
     torch.cuda.manual_seed(cfg.SEED + rank)
     log(f"rank {rank}/{world}: staging {args.pool} batches of {args.batch} buildings")

@@ -136,9 +136,17 @@ extern "C" int vg_gp_head(const float* g, int32_t N, int32_t K, const float* sco
   if (N <= 0 || K <= 0 || ldu < K || !g || !scores || !u0 || !out || !workspace || !sync)
     return VG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (K > 8) return VG_EINVAL;  // the path's K is NUM_CLASSES = 7
-  k_gp_head<8><<<vg_blocks(N, 256), 256, 0, s>>>(g, N, K, scores, lambda, u0, ldu, workspace, sync,
-                                                 out);
+  // classes live in registers: instantiations for K <= 8 (the path's
+  // NUM_CLASSES = 7), 16 and 32; wider rows are refused (vgan.h)
+  const int blocks = vg_blocks(N, 256);
+  if (K <= 8)
+    k_gp_head<8><<<blocks, 256, 0, s>>>(g, N, K, scores, lambda, u0, ldu, workspace, sync, out);
+  else if (K <= 16)
+    k_gp_head<16><<<blocks, 256, 0, s>>>(g, N, K, scores, lambda, u0, ldu, workspace, sync, out);
+  else if (K <= 32)
+    k_gp_head<32><<<blocks, 256, 0, s>>>(g, N, K, scores, lambda, u0, ldu, workspace, sync, out);
+  else
+    return VG_EINVAL;
   VG_CHECK_LAUNCH();
   return 0;
 }

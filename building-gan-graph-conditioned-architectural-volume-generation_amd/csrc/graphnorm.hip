@@ -767,7 +767,9 @@ extern "C" int vg_graphnorm_bwd_seg(const float* x, int32_t S, int32_t N, int32_
                                                               stats, sums, g_w, g_b, g_ms, accumulate);
   const long long total = (long long)S * N * C;
   const int lds_f = 3 * C + 4 * C * S;
-  if (quad_ok(total, C, lds_f, {x, g_y, keep, g_x, inj}) && (!inj || inj_offset % 4 == 0))
+  // the quad form narrows inj_offset to int: only when it fits (as total does)
+  if (quad_ok(total, C, lds_f, {x, g_y, keep, g_x, inj}) &&
+      (!inj || (inj_offset % 4 == 0 && inj_offset < (1LL << 31))))
     k_gn_bwd_apply4<<<apply_blocks(total / 4), 256, lds_f * 4, s>>>(
         x, g_y, static_cast<int>(total / 4), N, C, S, weight, bias, mean_scale, keep, eps, stats, sums,
         inj, inj ? static_cast<int>(inj_offset) : 0, g_x);

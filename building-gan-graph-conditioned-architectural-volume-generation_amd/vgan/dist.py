@@ -28,13 +28,20 @@ def env_world() -> tuple:
     return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("LOCAL_RANK", 0))
 
 
-def init(backend: Optional[str] = None) -> tuple:
-    """Initialise the default process group from torchrun env vars (no-op at 1 rank)."""
+def init(backend: Optional[str] = None, configuration=None) -> tuple:
+    """Initialise the default process group from torchrun env vars (no-op at 1
+    rank) and record the layout in ``configuration.runtime`` (``rank``,
+    ``world_size``), which the Trainer's per-rank RNG seed reads."""
     rank, world, local = env_world()
     if world > 1 and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         dist.init_process_group(backend=backend, rank=rank, world_size=world)
+    if configuration is not None:
+        runtime = getattr(configuration, "runtime", None)
+        if runtime is None:
+            runtime = configuration.runtime = {}
+        runtime["rank"], runtime["world_size"] = rank, world
     return rank, world, local
 
 

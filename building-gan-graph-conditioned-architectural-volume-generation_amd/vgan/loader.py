@@ -51,14 +51,25 @@ class GraphLoader:
 
     def __init__(self, store: GraphStore, indices: Optional[Sequence[int]] = None, batch_size: int = 1,
                  shuffle: bool = True, drop_last: bool = False, device=None, prefetch: int = 2,
-                 threads: int = 4, rank: int = 0, world_size: int = 1):
+                 threads: int = 4, rank: int = 0, world_size: int = 1, seed: Optional[int] = None):
         """``rank`` / ``world_size``: data-parallel sharding -- every rank draws
-        the same epoch plan (same seed) and takes batches rank, rank + world,
-        ... of it, so ranks see disjoint buildings (weak scaling, one batch
-        of ``batch_size`` per rank and step)."""
+        the same epoch plan and takes batches rank, rank + world, ... of it, so
+        ranks see disjoint buildings (weak scaling, one batch of
+        ``batch_size`` per rank and step).
+
+        With ``world_size > 1`` the plan is cut to a multiple of
+        ``world_size`` batches (every rank runs the same number of steps, so
+        the per-step gradient all-reduces pair up) and the shuffle draws from
+        its own generator seeded with ``seed + epoch`` -- not the global CPU
+        RNG, which ranks seed differently (``SEED + rank``).  One rank keeps
+        the reference's global-RNG shuffle (``data.py:177-184``)."""
         if not 0 <= rank < world_size:
             raise ValueError("need 0 <= rank < world_size")
+        if world_size > 1 and seed is None:
+            raise ValueError("data-parallel sharding needs a seed shared by all ranks")
         self.rank, self.world_size = int(rank), int(world_size)
+        self.seed = None if seed is None else int(seed)
+        self.epoch = 0
         self.store = store
         self.indices = list(range(len(store))) if indices is None else [int(i) for i in indices]
         self.batch_size = int(batch_size)
@@ -71,18 +82,29 @@ class GraphLoader:
     def __len__(self) -> int:
         n = len(self.indices)
         total = n // self.batch_size if self.drop_last else (n + self.batch_size - 1) // self.batch_size
-        return len(range(self.rank, total, self.world_size))
+        return total // self.world_size
 
-    def batches(self) -> List[List[int]]:
-        """This epoch's building indices per batch (consumes the CPU RNG like
-        the reference's DataLoader: a base seed when the iterator is created,
-        then the RandomSampler's seed)."""
+    def batches(self, epoch: Optional[int] = None) -> List[List[int]]:
+        """This rank's building indices per batch for ``epoch`` (default: the
+        loader's epoch counter).  One rank: consumes the CPU RNG like the
+        reference's DataLoader (a base seed when the iterator is created, then
+        the RandomSampler's seed).  Several ranks: a generator seeded with
+        ``seed + epoch``, identical on every rank."""
+        gen = None
+        if self.seed is not None:
+            gen = torch.Generator().manual_seed(self.seed + (self.epoch if epoch is None else int(epoch)))
         dl = DataLoader(_Indices(self.indices), batch_size=self.batch_size, shuffle=self.shuffle,
-                        drop_last=self.drop_last, collate_fn=_as_list, num_workers=0)
-        return list(iter(dl))[self.rank::self.world_size]
+                        drop_last=self.drop_last, collate_fn=_as_list, num_workers=0, generator=gen)
+        plan = list(iter(dl))
+        plan = plan[:len(plan) - len(plan) % self.world_size]
+        return plan[self.rank::self.world_size]
+
+    def set_epoch(self, epoch: int) -> None:
+        self.epoch = int(epoch)
 
     def __iter__(self) -> Iterator[Tuple[GraphBatch, GraphBatch]]:
         plan = self.batches()
+        self.epoch += 1
         dev = self.device
         if dev is None or dev.type != "cuda":
             for idx in plan:
@@ -160,9 +182,13 @@ class GraphDataLoaders:
         indices = list(range(len(store)))[: int(getattr(configuration, "DATA_SLICER", len(store)))]  # data.py:97-98
         if self.sanity_checking:  # data.py:100-102: one building, no validation / test loaders
             indices = [indices[int(getattr(configuration, "DATA_POINT", 0))]]
-        parts = random_split(indices, configuration.SPLIT_RATIOS)
+        # one rank: the reference's split on the global CPU RNG; several ranks:
+        # the same split on every rank from a generator seeded with SEED
+        seed = int(configuration.SEED) if world_size > 1 else None
+        split_gen = torch.Generator().manual_seed(seed) if seed is not None else torch.default_generator
+        parts = random_split(indices, configuration.SPLIT_RATIOS, generator=split_gen)
         kw = dict(batch_size=configuration.BATCH_SIZE, shuffle=True, drop_last=False, device=device,
-                  prefetch=prefetch, rank=rank, world_size=world_size)
+                  prefetch=prefetch, rank=rank, world_size=world_size, seed=seed)
         self.train_dataloader = GraphLoader(store, [indices[i] for i in parts[0].indices], **kw)
         self.validation_dataloader = None if self.sanity_checking else \
             GraphLoader(store, [indices[i] for i in parts[1].indices], **kw)

@@ -59,8 +59,14 @@ class Trainer:
         self.log_dir = log_dir or os.path.join(configuration.LOG_DIR,
                                                datetime.datetime.now().strftime("%m-%d-%Y__%H-%M-%S"))
         runtime = getattr(configuration, "runtime", {})
-        self.rng = RNG(runtime.get("rng", "device"),
-                       seed=torch.initial_seed() + 7919 * int(runtime.get("rank", 0)))
+        # data-parallel rank: the process group's when one is initialised (every
+        # rank builds its models after the same torch.manual_seed, so the rank
+        # term is what gives ranks different z / dropout / Gumbel / eps draws)
+        rank = int(runtime.get("rank", 0))
+        if torch.distributed.is_available() and torch.distributed.is_initialized():
+            rank = torch.distributed.get_rank()
+        self.rank = rank
+        self.rng = RNG(runtime.get("rng", "device"), seed=torch.initial_seed() + 7919 * rank)
         generator.rng = self.rng
         discriminator.rng = self.rng
         self.flat_g = FlatParams(generator)
@@ -73,7 +79,9 @@ class Trainer:
         self.skip_dead_d_grads = runtime.get("skip_dead_d_grads", True)
         # critic iterations: the explicit four-pass engine (vgan/critic.py) or
         # autograd double backward through the differentiable HIP ops
-        use_engine = runtime.get("critic", "engine") == "engine" and getattr(configuration, "USE_WGANGP", True)
+        # (vg_gp_head holds a row's classes in registers: K <= 32)
+        use_engine = (runtime.get("critic", "engine") == "engine" and getattr(configuration, "USE_WGANGP", True)
+                      and int(configuration.NUM_CLASSES) <= 32)
         self.critic = CriticEngine(discriminator, configuration) if use_engine else None
         self.states = {"epoch_start": 1, "best_f1_score": 0.0}
 
@@ -331,8 +339,10 @@ class Trainer:
             precs.append(prec)
             recs.append(rec)
             accs.append(acc)
-        g_mean = torch.stack(g_losses).mean().item()
-        d_mean = torch.cat(d_losses).mean().item()
+        # epoch means of the losses averaged over the data-parallel ranks (one
+        # collective per epoch); the F1 / precision / recall are this rank's
+        means = self.sync.all_reduce_scalars(torch.stack([torch.stack(g_losses).mean(), torch.cat(d_losses).mean()]))
+        g_mean, d_mean = (float(v) for v in means.tolist())
         print(f"The function _train_each_epoch took {time.time() - start} seconds to run.")
         return (g_mean, d_mean, float(np.mean(f1s)), min(f1_graphs), float(np.mean(precs)), float(np.mean(recs)),
                 float(np.mean(accs)))

@@ -158,7 +158,8 @@ int vg_critic_input(const float* mvx, int32_t N, int32_t F, const float* real, c
  * out[1] = gp = lambda mean_n (|g_n|-1)^2, out[0] = mean(fake) - mean(real) + gp,
  * u0 [N,K] (row stride ldu) = dgp/dg.  Deterministic (per-block sums folded in
  * order by the last block).  workspace: vg_gp_head_ws_floats(N); sync: a
- * caller-owned int32 device counter, 0 on entry (left at 0). */
+ * caller-owned int32 device counter, 0 on entry (left at 0).  A row's classes
+ * are held in registers: K <= 32 (VG_EINVAL above; the path's K is 7). */
 int64_t vg_gp_head_ws_floats(int32_t N);
 int vg_gp_head(const float* g, int32_t N, int32_t K, const float* scores, float lambda, float* u0,
                int32_t ldu, float* out, float* workspace, int32_t* sync, void* stream);

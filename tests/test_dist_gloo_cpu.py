@@ -44,18 +44,92 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_gloo_two_ranks_average_and_broadcast():
-    world = 2
+def _run(target, world=2):
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda t: t[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (_, p0, g0, m0), (_, p1, g1, _) = res
+    return res
+
+
+def test_gloo_two_ranks_average_and_broadcast():
+    (_, p0, g0, m0), (_, p1, g1, _) = _run(_worker)
     assert torch.equal(p0, p1)  # parameters broadcast from rank 0
     assert torch.allclose(g0, g1) and torch.allclose(g0, m0, atol=1e-6)  # averaged gradient
+
+
+def _trainer_worker(rank, world, port, q):
+    """bench.py's order: per-rank CPU seed, then the models after the SAME
+    torch.manual_seed(SEED) -- the rank must still reach the Trainer's RNG."""
+    import sys
+
+    from parity_util import PKG_ROOT
+    sys.path.insert(0, PKG_ROOT)
+    from vgan import dist as vdist
+    from vgan.config import Configuration
+    from vgan.models import VoxelGNNDiscriminator, VoxelGNNGenerator
+    from vgan.trainer import Trainer
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    cfg = Configuration()
+    cfg.DEVICE = "cpu"
+    vdist.init("gloo", configuration=cfg)
+    assert cfg.runtime["rank"] == rank and cfg.runtime["world_size"] == world
+    cfg.runtime["rank"] = 0  # the process group, not a stale runtime entry, decides
+    torch.manual_seed(cfg.SEED + rank)
+    torch.manual_seed(cfg.SEED)
+    G, D = VoxelGNNGenerator(cfg, 17, 12), VoxelGNNDiscriminator(cfg, 17, 12)
+    og = torch.optim.Adam(G.parameters(), lr=cfg.LEARNING_RATE_GENERATOR, betas=cfg.BETAS)
+    od = torch.optim.Adam(D.parameters(), lr=cfg.LEARNING_RATE_DISCRIMINATOR, betas=cfg.BETAS)
+    tr = Trainer(G, D, None, og, od, None, cfg)
+    means = tr.sync.all_reduce_scalars(torch.tensor([float(rank), 2.0 * rank]))
+    q.put((rank, tr.rank, tr.rng.seed, means.tolist()))  # plain data: the worker exits before the parent reads
+    dist.destroy_process_group()
+
+
+def test_gloo_ranks_draw_different_streams():
+    (_, r0, s0, m0), (_, r1, s1, m1) = _run(_trainer_worker)
+    assert (r0, r1) == (0, 1)
+    assert s0 != s1  # per-rank z / dropout / Gumbel / eps streams
+    assert m0 == m1 == [0.5, 1.0]  # logged losses averaged
+
+
+def test_sharded_loader_equal_steps_shared_shuffle():
+    """Uneven batch count (11 batches, 2 ranks): every rank gets the same
+    number of batches, ranks are disjoint, and the plan does not depend on the
+    global CPU RNG (ranks seed it differently)."""
+    import sys
+
+    from parity_util import PKG_ROOT
+    if PKG_ROOT not in sys.path:
+        sys.path.insert(0, PKG_ROOT)
+    from vgan.loader import GraphLoader
+
+    indices = list(range(100, 141))  # 41 buildings -> 11 batches of 4 (drop_last=False)
+    plans = []
+    for rank in range(2):
+        torch.manual_seed(777 + rank)
+        ld = GraphLoader(None, indices, batch_size=4, rank=rank, world_size=2, seed=777)
+        plans.append(ld.batches())
+        assert len(ld) == len(plans[-1]) == 5
+    flat0 = [i for b in plans[0] for i in b]
+    flat1 = [i for b in plans[1] for i in b]
+    assert not set(flat0) & set(flat1)
+    assert len(flat0) + len(flat1) == 40  # the tail batch is cut, never split unevenly
+    # next epoch reshuffles identically on both ranks
+    a = GraphLoader(None, indices, batch_size=4, rank=0, world_size=2, seed=777)
+    b = GraphLoader(None, indices, batch_size=4, rank=1, world_size=2, seed=777)
+    torch.manual_seed(1)
+    e1a = a.batches(epoch=1)
+    torch.manual_seed(2)
+    e1b = b.batches(epoch=1)
+    assert e1a != plans[0] and not set(sum(e1a, [])) & set(sum(e1b, []))
+    import pytest
+    with pytest.raises(ValueError):
+        GraphLoader(None, indices, batch_size=4, rank=0, world_size=2)  # no shared seed

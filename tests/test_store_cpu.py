@@ -208,15 +208,16 @@ def test_loader_rank_sharding(synth_store):
     _, st = synth_store
     plans = []
     for rank in range(3):
-        torch.manual_seed(4)
-        loader = GraphLoader(st, list(range(len(st))), batch_size=2, shuffle=True, rank=rank, world_size=3)
+        torch.manual_seed(4 + rank)  # the global RNG differs per rank; the plan must not
+        loader = GraphLoader(st, list(range(len(st))), batch_size=2, shuffle=True, rank=rank, world_size=3, seed=4)
         plans.append(loader.batches())
         assert len(loader) == len(plans[-1])
-    torch.manual_seed(4)
-    full = GraphLoader(st, list(range(len(st))), batch_size=2, shuffle=True).batches()
+    full = GraphLoader(st, list(range(len(st))), batch_size=2, shuffle=True, seed=4).batches()
+    full = full[:len(full) - len(full) % 3]  # every rank takes the same number of batches
     assert [b for r in range(3) for b in full[r::3]] == [b for p in plans for b in p]
     seen = sorted(i for p in plans for b in p for i in b)
-    assert seen == list(range(len(st)))
+    assert seen == sorted(i for b in full for i in b)
+    assert len({len(p) for p in plans}) == 1
     with pytest.raises(ValueError):
         GraphLoader(st, rank=2, world_size=2)
 
