@@ -144,7 +144,7 @@ def make_pool(cfg, rank: int, world: int, pool: int, batch: int, device):
     return out
 
 
-def build_trainer(cfg):
+def build_trainer(cfg, precision: str = "f32"):
     from vgan.models import VoxelGNNDiscriminator, VoxelGNNGenerator
     from vgan.trainer import Trainer
 
@@ -154,6 +154,7 @@ def build_trainer(cfg):
     og = torch.optim.Adam(G.parameters(), lr=cfg.LEARNING_RATE_GENERATOR, betas=cfg.BETAS)
     od = torch.optim.Adam(D.parameters(), lr=cfg.LEARNING_RATE_DISCRIMINATOR, betas=cfg.BETAS)
     sched = torch.optim.lr_scheduler.CosineAnnealingLR(og, T_max=cfg.EPOCHS)
+    cfg.runtime["precision"] = precision
     return Trainer(G, D, None, og, od, sched, cfg)
 
 
@@ -166,6 +167,35 @@ def run_steps(tr, pool, k: int, offset: int = 0):
         loc, vox = pool[(offset + s) % len(pool)]
         out = tr.step_graphed(loc, vox) if GRAPHED else tr.step(loc, vox)
     return out
+
+
+def timed_steps(tr, pool, steps: int, warmup: int, world: int, device, profile: bool = False):
+    """Warm-up (every pooled batch once: its CSR / type-mean / graphs), then
+    ``steps`` timed steps between barrier + synchronize on both sides; the
+    max over ranks.  Returns seconds."""
+    for (loc, vox) in pool:
+        run_steps(tr, [(loc, vox)], 1)
+    run_steps(tr, pool, warmup)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    if profile:
+        time.sleep(0.05)  # idle gap that tools/prof_summary.py --after-gap keys on
+    t0 = time.perf_counter()
+    for s in range(steps):
+        run_steps(tr, pool, 1, offset=s)
+        if (s + 1) % 10 == 0:
+            log(f"step {s + 1}/{steps}")
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
 
 
 def stress_roofline(device, channels=(128, 64, 1), reps: int = 20):
@@ -265,6 +295,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-stress", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture of the step")
+    ap.add_argument("--precision", choices=("f32", "bf16"), default="f32",
+                    help="dense-product precision of the main measurement (f32 = configs[1]); the default run adds "
+                         "a bf16 line (configs[2]) after it")
+    ap.add_argument("--no-bf16", action="store_true", help="skip the extra bf16 (configs[2]) measurement")
     ap.add_argument("--profile", action="store_true",
                     help="for rocprofv3: only warm-up + timed steps (50 ms idle gap before the timed region), "
                          "no instrumented / stress / CPU passes")
@@ -307,7 +341,7 @@ def main():
     torch.cuda.manual_seed(cfg.SEED + rank)
     log(f"rank {rank}/{world}: staging {args.pool} batches of {args.batch} buildings")
     pool = make_pool(cfg, rank, world, args.pool, args.batch, device)
-    tr = build_trainer(cfg)
+    tr = build_trainer(cfg, args.precision)
     n_nodes = sum(v.num_nodes for _, v in pool) / len(pool)
     if args.roofline_only:  # for rocprofv3 --pmc passes: only the scatter-kernel roofline replays
         from vgan import data as vdata
@@ -318,41 +352,35 @@ def main():
         return
 
     # warm-up (also builds every batch's CSR / type-mean once, as the first step of a batch would)
-    for (loc, vox) in pool:
-        run_steps(tr, [(loc, vox)], 1)
-    run_steps(tr, pool, args.warmup)
-    torch.cuda.synchronize()
-    log("warm-up done")
-
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    if args.profile:
-        time.sleep(0.05)  # idle gap that tools/prof_summary.py --after-gap keys on
-    t0 = time.perf_counter()
-    for s in range(args.steps):
-        run_steps(tr, pool, 1, offset=s)
-        if (s + 1) % 10 == 0:
-            log(f"step {s + 1}/{args.steps}")
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = timed_steps(tr, pool, args.steps, args.warmup, world, device, profile=args.profile)
     value = args.batch * world * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
-    log(f"timed ({'hipGraph' if GRAPHED else 'eager'}): {ms_per_step:.2f} ms/step, {value:.1f} graphs/s")
+    log(f"timed ({'hipGraph' if GRAPHED else 'eager'}, {args.precision}): {ms_per_step:.2f} ms/step, "
+        f"{value:.1f} graphs/s")
 
     if args.profile:
         if rank == 0:
-            print(json.dumps({"profile": True, "value": round(value, 3), "ms_per_step": round(ms_per_step, 3),
-                              "steps": args.steps}), flush=True)
+            print(json.dumps({"profile": True, "precision": args.precision, "value": round(value, 3),
+                              "ms_per_step": round(ms_per_step, 3), "steps": args.steps}), flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
+
+    # configs[2]: the same step with bf16 dense products (fresh models, same seed)
+    bf16 = None
+    if args.precision == "f32" and not args.no_bf16:
+        del tr
+        torch.manual_seed(cfg.SEED + rank)
+        tr16 = build_trainer(cfg, "bf16")
+        el16 = timed_steps(tr16, pool, args.steps, args.warmup, world, device)
+        bf16 = {"value": round(args.batch * world * args.steps / el16, 3), "unit": "graphs/s",
+                "ms_per_step": round(el16 / args.steps * 1e3, 3), "dtype": "bf16 operands, f32 accumulate",
+                "workload": f"configs[2]: the configs[1] step with every dense product (nn.Linear / GATConv.lin: "
+                            f"forward, input and weight gradients) on bf16 operands, f32 accumulation; "
+                            f"aggregation, GraphNorm, losses, Adam f32; dp{world}"}
+        log(f"timed bf16: {bf16['ms_per_step']:.2f} ms/step, {bf16['value']:.1f} graphs/s")
+        tr = tr16
+        cfg.runtime["precision"] = "f32"
 
     # the dominant message-passing kernel's roofline: the step's own mix of
     # vg_gat_aggregate_fwd launches, graph-replayed between HIP events
@@ -384,11 +412,14 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": args.precision,
             "data": "synthetic (seeded 6-type buildings in the reference tensor layout; random-init weights)",
             "config": {
-                "workload": "configs[1]: 6-type dataset, batch=32 voxel graphs per GPU, fp32, full G+D step "
-                            "(5 critic WGAN-GP + 1 generator iteration, Adam), HIP message passing",
+                "workload": ("configs[1]: 6-type dataset, batch=32 voxel graphs per GPU, fp32, full G+D step "
+                             "(5 critic WGAN-GP + 1 generator iteration, Adam), HIP message passing")
+                if args.precision == "f32" else
+                ("configs[2]: 6-type dataset, batch=32 voxel graphs per GPU, bf16 dense products (f32 accumulate), "
+                 "full G+D step (5 critic WGAN-GP + 1 generator iteration, Adam), HIP message passing"),
                 "global_batch": args.batch * world,
                 "avg_voxel_nodes_per_batch": round(n_nodes, 1),
                 "parallelism": f"dp{world}",
@@ -413,6 +444,8 @@ def main():
             },
             "cpu_baseline": cpu,
         }
+        if bf16:
+            result["bf16"] = bf16
         if stress:
             c128 = stress["per_channels"][128]
             result["roofline_stress"] = {

@@ -19,6 +19,17 @@
 // f32 in, f32 accumulate: the MFMA is an exact fmaf chain (no TF32 on gfx950),
 // so results differ from a CPU GEMM only by summation order.
 //
+// bf16 mode (the *_bf16 entry points; BASELINE configs[2]): the same kernels
+// with template flag BF round both operands to bf16 (round-to-nearest-even,
+// v_cvt_pk_bf16_f32) as they are staged into LDS and multiply them on
+// v_mfma_f32_32x32x16_bf16 with f32 accumulation -- torch.autocast's
+// treatment of a matmul, except that outputs, epilogues (bias, activation,
+// LayerNorm, attention projections) and bias gradients stay f32.  A K-tile of
+// 32 is 2 MFMAs of 32 cycles instead of 16 f32 MFMAs of 64.  LDS rows hold 32
+// bf16 padded to 40 (80 B: the 8-element fragment of a lane is one aligned
+// 16-byte read); global loads take 4 consecutive k per thread (one 8-byte LDS
+// store).
+//
 // Tiling: 256-thread workgroup = 4 waves, 64 x 64 output tile, each wave one
 // 32 x 32 MFMA tile; K staged through LDS 32 at a time.  LDS rows are padded
 // to 33 floats so the MFMA operand reads (32 lanes down a column) and the
@@ -28,8 +39,25 @@
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int TM = 64, TN = 64, TK = 32, LDP = TK + 1;
+constexpr int LDH = TK + 8;  // bf16 LDS row pitch (elements)
+
+__device__ __forceinline__ bf16x4 to_bf4(const float (&v)[4]) {
+  bf16x4 r;
+  r[0] = static_cast<__bf16>(v[0]);
+  r[1] = static_cast<__bf16>(v[1]);
+  r[2] = static_cast<__bf16>(v[2]);
+  r[3] = static_cast<__bf16>(v[3]);
+  return r;
+}
+
+__device__ __forceinline__ f32x16 mfma_bf(const __bf16* a, const __bf16* b, f32x16 acc) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(a),
+                                                 *reinterpret_cast<const bf16x8*>(b), acc, 0, 0, 0);
+}
 #ifndef VG_LN_TM32
 #define VG_LN_TM32 1
 #endif
@@ -66,7 +94,7 @@ __device__ __forceinline__ void tile_xy(int& tx, int& ty) {
 // ATT (BT, ACT 0, M <= 64): also a_src[n] = <C[n,:], att_s>, a_dst[n] =
 // <C[n,:], att_d> -- GATConv's attention projections as the epilogue of its
 // own projection GEMM (the output tile is staged through LDS once).
-template <bool BT, int ACT, bool ATT = false>
+template <bool BT, int ACT, bool ATT = false, bool BF = false>
 __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int lda,
                                               const float* __restrict__ B, int ldb,
                                               const float* __restrict__ bias,
@@ -76,8 +104,9 @@ __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int l
                                               const float* __restrict__ att_d = nullptr,
                                               float* __restrict__ a_src = nullptr,
                                               float* __restrict__ a_dst = nullptr) {
-  __shared__ float As[2][TM][LDP];
-  __shared__ float Bs[2][TN][LDP];  // Bs[j][k] = op(B)[k][j]
+  __shared__ __attribute__((aligned(16))) float smem[2 * TM * LDP + 2 * TN * LDP];
+  float(*As)[TM][LDP] = reinterpret_cast<float(*)[TM][LDP]>(smem);
+  float(*Bs)[TN][LDP] = reinterpret_cast<float(*)[TN][LDP]>(smem + 2 * TM * LDP);  // Bs[j][k] = op(B)[k][j]
   constexpr int PER = (TM * TK) / 256;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wr = wave >> 1, wc = wave & 1;
@@ -87,6 +116,51 @@ __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int l
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  if constexpr (BF) {
+    // Ah[buf][n][k], Bh[buf][m][k] = op(B)[k][m], bf16; quads of 4 k per thread
+    __bf16(*Ah)[TM][LDH] = reinterpret_cast<__bf16(*)[TM][LDH]>(smem);
+    __bf16(*Bh)[TN][LDH] = reinterpret_cast<__bf16(*)[TN][LDH]>(smem + 2 * TM * LDP);
+    constexpr int QG = (TM * TK / 4) / 256;
+    float qa[QG][4], qb[QG][4];
+    auto load_bf = [&](int k0) {
+#pragma unroll
+      for (int q = 0; q < QG; ++q) {
+        const int g = t + 256 * q;
+        const int row = g >> 3, kq = (g & 7) * 4;
+        const int n = n0 + row;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int k = k0 + kq + i;
+          qa[q][i] = (n < N && k < K) ? A[(size_t)n * lda + k] : 0.f;
+          if (BT) {
+            const int m = m0 + row;
+            qb[q][i] = (m < M && k < K) ? B[(size_t)m * ldb + k] : 0.f;
+          } else {
+            const int m = m0 + (g & 63), kk = k0 + (g >> 6) * 4 + i;
+            qb[q][i] = (m < M && kk < K) ? B[(size_t)kk * ldb + m] : 0.f;
+          }
+        }
+      }
+    };
+    load_bf(0);
+    int buf = 0;
+    for (int k0 = 0; k0 < K; k0 += TK) {
+#pragma unroll
+      for (int q = 0; q < QG; ++q) {
+        const int g = t + 256 * q;
+        *reinterpret_cast<bf16x4*>(&Ah[buf][g >> 3][(g & 7) * 4]) = to_bf4(qa[q]);
+        if (BT) *reinterpret_cast<bf16x4*>(&Bh[buf][g >> 3][(g & 7) * 4]) = to_bf4(qb[q]);
+        else *reinterpret_cast<bf16x4*>(&Bh[buf][g & 63][(g >> 6) * 4]) = to_bf4(qb[q]);
+      }
+      __syncthreads();
+      if (k0 + TK < K) load_bf(k0 + TK);
+      const int h8 = 8 * (lane >> 5);
+#pragma unroll
+      for (int s16 = 0; s16 < TK; s16 += 16)
+        acc = mfma_bf(&Ah[buf][wr * 32 + (lane & 31)][s16 + h8], &Bh[buf][wc * 32 + (lane & 31)][s16 + h8], acc);
+      buf ^= 1;
+    }
+  } else {
   float ra[PER], rb[PER];
   auto load = [&](int k0) {
 #pragma unroll
@@ -124,6 +198,7 @@ __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int l
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[kk], br[kk], acc, 0, 0, 0);
     buf ^= 1;
   }
+  }  // f32 operands
   const int m = m0 + wc * 32 + (lane & 31);
   const float bv = (bias && m < M) ? bias[m] : 0.f;
 #pragma unroll
@@ -194,7 +269,7 @@ struct MsDesc {
   int ld_add, add_rows;
 };
 
-template <int NT, int TMR = TM, bool ATT = false, bool MS = false>
+template <int NT, int TMR = TM, bool ATT = false, bool MS = false, bool BF = false>
 __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, int lda,
                                                  const float* __restrict__ B, int ldb,
                                                  const float* __restrict__ bias, int N, int M, int K,
@@ -214,7 +289,7 @@ __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, in
   constexpr int WCOLS = 4 / (TMR / 32);       // waves across the columns
   constexpr int NJ = TNC / (32 * WCOLS);      // 32-column MFMA tiles per wave
   static_assert(NJ >= 1, "TMR = 32 needs 128 columns");
-  __shared__ float smem[2 * TMR * LDP + 2 * TNC * LDP];
+  __shared__ __attribute__((aligned(16))) float smem[2 * TMR * LDP + 2 * TNC * LDP];
   __shared__ float s_mu[TMR], s_rs[TMR];
   float(*As)[TMR][LDP] = reinterpret_cast<float(*)[TMR][LDP]>(smem);
   float(*Bs)[TNC][LDP] = reinterpret_cast<float(*)[TNC][LDP]>(smem + 2 * TMR * LDP);
@@ -229,11 +304,12 @@ __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, in
   for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-  float ra[PA], rb[PB];
-  auto load = [&](int k0) {
-    // MS: sources are TK-aligned column blocks, so one source serves the chunk
-    const float* asrc = A;
-    int ald = lda, acol = k0, wcol = k0;
+  // MS: sources are TK-aligned column blocks, so one source serves the chunk
+  auto chunk_src = [&](int k0, const float*& asrc, int& ald, int& acol, int& wcol) {
+    asrc = A;
+    ald = lda;
+    acol = k0;
+    wcol = k0;
     if constexpr (MS) {
       int sidx = 0;
 #pragma unroll
@@ -245,6 +321,63 @@ __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, in
       acol = k0 - kb;
       wcol = ms.wcol[sidx] + (k0 - kb);
     }
+  };
+  if constexpr (BF) {
+    __bf16(*Ah)[TMR][LDH] = reinterpret_cast<__bf16(*)[TMR][LDH]>(smem);
+    __bf16(*Bh)[TNC][LDH] = reinterpret_cast<__bf16(*)[TNC][LDH]>(smem + 2 * TMR * LDP);
+    constexpr int QA = (TMR * TK / 4) / 256, QB = (TNC * TK / 4) / 256;
+    float qa[QA][4], qb[QB][4];
+    auto load_bf = [&](int k0) {
+      const float* asrc;
+      int ald, acol, wcol;
+      chunk_src(k0, asrc, ald, acol, wcol);
+#pragma unroll
+      for (int q = 0; q < QA; ++q) {
+        const int g = t + 256 * q;
+        const int n = n0 + (g >> 3), kq = (g & 7) * 4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          qa[q][i] = (n < N && k0 + kq + i < K) ? asrc[(size_t)n * ald + acol + kq + i] : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < QB; ++q) {
+        const int g = t + 256 * q;
+        const int m = g >> 3, kq = (g & 7) * 4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          qb[q][i] = (m < M && k0 + kq + i < K) ? B[(size_t)m * ldb + wcol + kq + i] : 0.f;
+      }
+    };
+    load_bf(0);
+    int buf = 0;
+    for (int k0 = 0; k0 < K; k0 += TK) {
+#pragma unroll
+      for (int q = 0; q < QA; ++q) {
+        const int g = t + 256 * q;
+        *reinterpret_cast<bf16x4*>(&Ah[buf][g >> 3][(g & 7) * 4]) = to_bf4(qa[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < QB; ++q) {
+        const int g = t + 256 * q;
+        *reinterpret_cast<bf16x4*>(&Bh[buf][g >> 3][(g & 7) * 4]) = to_bf4(qb[q]);
+      }
+      __syncthreads();
+      if (k0 + TK < K) load_bf(k0 + TK);
+      const int h8 = 8 * (lane >> 5);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int s16 = 0; s16 < TK; s16 += 16)
+          acc[j] = mfma_bf(&Ah[buf][wr * 32 + (lane & 31)][s16 + h8],
+                           &Bh[buf][j * 32 * WCOLS + wc * 32 + (lane & 31)][s16 + h8], acc[j]);
+      buf ^= 1;
+    }
+  } else {
+  float ra[PA], rb[PB];
+  auto load = [&](int k0) {
+    const float* asrc;
+    int ald, acol, wcol;
+    chunk_src(k0, asrc, ald, acol, wcol);
 #pragma unroll
     for (int q = 0; q < PA; ++q) {
       const int e = t + 256 * q;
@@ -283,6 +416,7 @@ __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, in
     }
     buf ^= 1;
   }
+  }  // f32 operands
   // stage the full-width tile (+ bias) in LDS
   __syncthreads();
   float* Ct = smem;
@@ -389,13 +523,14 @@ __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, in
 // group's MFMAs cover the other's loads -- the f32 MFMA alone is 1024 cycles
 // per 32-row step), and the groups' accumulators are added in group order at
 // the end (deterministic).
-template <int G>
+template <int G, bool BF = false>
 __global__ void __launch_bounds__(256 * G) k_gemm_tn(const float* __restrict__ A, int lda,
                                                      const float* __restrict__ B, int ldb, int N,
                                                      int M, int K, int rows, float* __restrict__ part,
                                                      float* __restrict__ pdb, int db_rows) {
-  __shared__ float As[G][2][TK][TM + 1];  // As[g][buf][n][m]
-  __shared__ float Bs[G][2][TK][TN + 1];  // Bs[g][buf][n][k]
+  __shared__ __attribute__((aligned(16))) float smem[G * 2 * TK * (TM + 1) + G * 2 * TK * (TN + 1)];
+  float(*As)[2][TK][TM + 1] = reinterpret_cast<float(*)[2][TK][TM + 1]>(smem);  // As[g][buf][n][m]
+  float(*Bs)[2][TK][TN + 1] = reinterpret_cast<float(*)[2][TK][TN + 1]>(smem + G * 2 * TK * (TM + 1));  // [n][k]
   constexpr int PER = (TK * TM) / 256;
   const int grp = threadIdx.x >> 8, t = threadIdx.x & 255, lane = t & 63, wave = t >> 6;
   const int wr = wave >> 1, wc = wave & 1;
@@ -413,6 +548,55 @@ __global__ void __launch_bounds__(256 * G) k_gemm_tn(const float* __restrict__ A
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   float dbs = 0.f;
+  if constexpr (BF) {
+    // Ah[g][buf][m][n], Bh[g][buf][k][n] (the reduction index n contiguous):
+    // quads of 4 rows n of one column per thread
+    __bf16(*Ah)[2][TM][LDH] = reinterpret_cast<__bf16(*)[2][TM][LDH]>(smem);
+    __bf16(*Bh)[2][TN][LDH] = reinterpret_cast<__bf16(*)[2][TN][LDH]>(smem + G * 2 * TK * (TM + 1));
+    constexpr int QG = (TK * TM / 4) / 256;
+    float qa[QG][4], qb[QG][4];
+    auto load_bf = [&](int st) {
+      const int n1 = nb + st * TK;
+#pragma unroll
+      for (int q = 0; q < QG; ++q) {
+        const int g = t + 256 * q;
+        const int c = g & 63, nq = (g >> 6) * 4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int n = n1 + nq + i;
+          const bool in = st < steps && n < ne;
+          qa[q][i] = (in && m0 + c < M) ? A[(size_t)n * lda + m0 + c] : 0.f;
+          qb[q][i] = (in && k0 + c < K) ? B[(size_t)n * ldb + k0 + c] : 0.f;
+        }
+      }
+    };
+    load_bf(grp);
+    int buf = 0;
+    for (int it = 0, st = grp; it < iters; ++it, st += G) {
+      const int n1 = nb + st * TK;
+#pragma unroll
+      for (int q = 0; q < QG; ++q) {
+        const int g = t + 256 * q;
+        const int c = g & 63, nq = (g >> 6) * 4;
+        *reinterpret_cast<bf16x4*>(&Ah[grp][buf][c][nq]) = to_bf4(qa[q]);
+        *reinterpret_cast<bf16x4*>(&Bh[grp][buf][c][nq]) = to_bf4(qb[q]);
+        if (do_db)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (n1 + nq + i < db_rows) dbs += qa[q][i];  // f32 column sums (0 past ne)
+      }
+      __syncthreads();
+      load_bf(st + G);
+      if (st < steps) {
+        const int h8 = 8 * (lane >> 5);
+#pragma unroll
+        for (int s16 = 0; s16 < TK; s16 += 16)
+          acc = mfma_bf(&Ah[grp][buf][wr * 32 + (lane & 31)][s16 + h8],
+                        &Bh[grp][buf][wc * 32 + (lane & 31)][s16 + h8], acc);
+      }
+      buf ^= 1;
+    }
+  } else {
   float ra[PER], rb[PER];
   auto load = [&](int st) {
     const int n1 = nb + st * TK;
@@ -449,7 +633,8 @@ __global__ void __launch_bounds__(256 * G) k_gemm_tn(const float* __restrict__ A
     }
     buf ^= 1;
   }
-  float* sh = &As[0][0][0][0];  // G * 2 * TK * (TM + 1) >= (G - 1) * 4096 floats
+  }  // f32 operands
+  float* sh = smem;  // G * 2 * TK * (TM + 1) >= (G - 1) * 4096 floats
   __shared__ float red[G * 4][64];
   __syncthreads();
   if (grp > 0)
@@ -521,16 +706,17 @@ __global__ void __launch_bounds__(1024) k_fold_rows(const float* __restrict__ pa
 
 }  // namespace
 
-extern "C" int vg_gemm(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t b_trans,
-                       const float* bias, int32_t act, const float* aux, int32_t ldaux, float* C,
-                       int32_t ldc, int32_t N, int32_t M, int32_t K, void* stream) {
+template <bool BF>
+static int gemm(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t b_trans, const float* bias,
+                int32_t act, const float* aux, int32_t ldaux, float* C, int32_t ldc, int32_t N, int32_t M,
+                int32_t K, void* stream) {
   if (N < 0 || M <= 0 || K <= 0 || !A || !B || !C || act < 0 || act > 3) return VG_EINVAL;
   if (act == 3 && !aux) return VG_EINVAL;
   if (N == 0) return 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
   dim3 grid((N + TM - 1) / TM, (M + TN - 1) / TN);
 #define VG_G(BT, ACT) \
-  k_gemm<BT, ACT><<<grid, 256, 0, s>>>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, N, M, K)
+  k_gemm<BT, ACT, false, BF><<<grid, 256, 0, s>>>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, N, M, K)
   if (b_trans) {
     if (act == 0) VG_G(true, 0); else if (act == 1) VG_G(true, 1);
     else if (act == 2) VG_G(true, 2); else VG_G(true, 3);
@@ -541,6 +727,18 @@ extern "C" int vg_gemm(const float* A, int32_t lda, const float* B, int32_t ldb,
 #undef VG_G
   VG_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int vg_gemm(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t b_trans,
+                       const float* bias, int32_t act, const float* aux, int32_t ldaux, float* C,
+                       int32_t ldc, int32_t N, int32_t M, int32_t K, void* stream) {
+  return gemm<false>(A, lda, B, ldb, b_trans, bias, act, aux, ldaux, C, ldc, N, M, K, stream);
+}
+
+extern "C" int vg_gemm_bf16(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t b_trans,
+                            const float* bias, int32_t act, const float* aux, int32_t ldaux, float* C,
+                            int32_t ldc, int32_t N, int32_t M, int32_t K, void* stream) {
+  return gemm<true>(A, lda, B, ldb, b_trans, bias, act, aux, ldaux, C, ldc, N, M, K, stream);
 }
 
 // rows per split-K chunk: aim at ~768 workgroups in total but at most
@@ -565,6 +763,7 @@ extern "C" int64_t vg_gemm_tn_ws_floats(int32_t N, int32_t M, int32_t K) {
   return chunks * ((int64_t)M * K + M);
 }
 
+template <bool BF = false>
 static int gemm_tn(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N, int32_t M,
                    int32_t K, float* C, int32_t ldc, float* db, int32_t db_rows,
                    int32_t accumulate, float* workspace, void* stream, vg_fold* defer = nullptr,
@@ -585,7 +784,7 @@ static int gemm_tn(const float* A, int32_t lda, const float* B, int32_t ldb, int
   float* part = workspace;
   float* pdb = workspace + (size_t)chunks * M * K;
   dim3 grid((M + TM - 1) / TM, (K + TN - 1) / TN, chunks);
-  k_gemm_tn<kTnGroups><<<grid, 256 * kTnGroups, 0, s>>>(A, lda, B, ldb, N, M, K, rows, part, db ? pdb : nullptr,
+  k_gemm_tn<kTnGroups, BF><<<grid, 256 * kTnGroups, 0, s>>>(A, lda, B, ldb, N, M, K, rows, part, db ? pdb : nullptr,
                                  db_rows < N ? db_rows : N);
   const long long W = (long long)M * K;
   if (defer) {  // describe the fold(s) for vg_fold_batch instead of launching them
@@ -614,10 +813,21 @@ extern "C" int vg_gemm_tn_deferred(const float* A, int32_t lda, const float* B, 
                  folds_out, n_out);
 }
 
-extern "C" int vg_gemm_ln_act(const float* A, int32_t lda, const float* W, int32_t N, int32_t M,
-                              int32_t K, const float* bias, const float* gamma, const float* beta,
-                              float eps, float slope, float* H, float* Y, float* mean, float* rstd,
-                              void* stream) {
+extern "C" int vg_gemm_tn_deferred_bf16(const float* A, int32_t lda, const float* B, int32_t ldb,
+                                        int32_t N, int32_t M, int32_t K, float* C, int32_t ldc,
+                                        float* db, int32_t db_rows, int32_t accumulate,
+                                        float* workspace, vg_fold* folds_out, int32_t* n_out,
+                                        void* stream) {
+  if (!folds_out || !n_out || N <= 0) return VG_EINVAL;
+  return gemm_tn<true>(A, lda, B, ldb, N, M, K, C, ldc, db, db_rows, accumulate, workspace, stream,
+                       folds_out, n_out);
+}
+
+template <bool BF>
+static int gemm_ln_act(const float* A, int32_t lda, const float* W, int32_t N, int32_t M,
+                       int32_t K, const float* bias, const float* gamma, const float* beta,
+                       float eps, float slope, float* H, float* Y, float* mean, float* rstd,
+                       void* stream) {
   if (N < 0 || M <= 0 || M > 2 * TN || K <= 0 || lda < K || !A || !W || !gamma || !beta || !Y ||
       ((mean == nullptr) != (rstd == nullptr)))
     return VG_EINVAL;
@@ -625,22 +835,37 @@ extern "C" int vg_gemm_ln_act(const float* A, int32_t lda, const float* W, int32
   hipStream_t s = static_cast<hipStream_t>(stream);
   const dim3 grid((N + TM - 1) / TM, 1);
   if (M <= TN)
-    k_gemm_ln<1><<<grid, 256, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma, beta, eps, slope, H, Y, mean,
-                                      rstd);
+    k_gemm_ln<1, TM, false, false, BF><<<grid, 256, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma, beta, eps, slope,
+                                                             H, Y, mean, rstd);
   else if (VG_LN_TM32)
-    k_gemm_ln<2, 32><<<dim3((N + 31) / 32, 1), 256, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma, beta, eps,
-                                                            slope, H, Y, mean, rstd);
+    k_gemm_ln<2, 32, false, false, BF><<<dim3((N + 31) / 32, 1), 256, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma,
+                                                                              beta, eps, slope, H, Y, mean, rstd);
   else
-    k_gemm_ln<2><<<grid, 256, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma, beta, eps, slope, H, Y, mean,
-                                      rstd);
+    k_gemm_ln<2, TM, false, false, BF><<<grid, 256, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma, beta, eps, slope,
+                                                             H, Y, mean, rstd);
   VG_CHECK_LAUNCH();
   return 0;
 }
 
-extern "C" int vg_gemm_ln_act_ms(const vg_asrc* src, int32_t nsrc, const float* W, int32_t ldw, int32_t N,
-                                 int32_t M, const float* bias, const float* addend, int32_t ld_add,
-                                 int32_t add_rows, const float* gamma, const float* beta, float eps, float slope,
-                                 float* Y, int32_t ldy, void* stream) {
+extern "C" int vg_gemm_ln_act(const float* A, int32_t lda, const float* W, int32_t N, int32_t M,
+                              int32_t K, const float* bias, const float* gamma, const float* beta,
+                              float eps, float slope, float* H, float* Y, float* mean, float* rstd,
+                              void* stream) {
+  return gemm_ln_act<false>(A, lda, W, N, M, K, bias, gamma, beta, eps, slope, H, Y, mean, rstd, stream);
+}
+
+extern "C" int vg_gemm_ln_act_bf16(const float* A, int32_t lda, const float* W, int32_t N, int32_t M,
+                                   int32_t K, const float* bias, const float* gamma, const float* beta,
+                                   float eps, float slope, float* H, float* Y, float* mean, float* rstd,
+                                   void* stream) {
+  return gemm_ln_act<true>(A, lda, W, N, M, K, bias, gamma, beta, eps, slope, H, Y, mean, rstd, stream);
+}
+
+template <bool BF>
+static int gemm_ln_act_ms(const vg_asrc* src, int32_t nsrc, const float* W, int32_t ldw, int32_t N,
+                          int32_t M, const float* bias, const float* addend, int32_t ld_add,
+                          int32_t add_rows, const float* gamma, const float* beta, float eps, float slope,
+                          float* Y, int32_t ldy, void* stream) {
   if (!src || nsrc <= 0 || nsrc > kMaxSrc || !W || N < 0 || M <= TN || M > 2 * TN || !gamma || !beta || !Y ||
       ldy < M || (addend && (ld_add < M || add_rows < 32)))
     return VG_EINVAL;
@@ -663,9 +888,52 @@ extern "C" int vg_gemm_ln_act_ms(const vg_asrc* src, int32_t nsrc, const float* 
   d.add_rows = add_rows;
   if (N == 0) return 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  k_gemm_ln<2, 32, false, true><<<dim3((N + 31) / 32, 1), 256, 0, s>>>(
+  k_gemm_ln<2, 32, false, true, BF><<<dim3((N + 31) / 32, 1), 256, 0, s>>>(
       nullptr, 0, W, ldw, bias, N, M, K, gamma, beta, eps, slope, nullptr, Y, nullptr, nullptr, nullptr, nullptr,
       nullptr, nullptr, ldy, d);
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int vg_gemm_ln_act_ms(const vg_asrc* src, int32_t nsrc, const float* W, int32_t ldw, int32_t N,
+                                 int32_t M, const float* bias, const float* addend, int32_t ld_add,
+                                 int32_t add_rows, const float* gamma, const float* beta, float eps, float slope,
+                                 float* Y, int32_t ldy, void* stream) {
+  return gemm_ln_act_ms<false>(src, nsrc, W, ldw, N, M, bias, addend, ld_add, add_rows, gamma, beta, eps, slope,
+                               Y, ldy, stream);
+}
+
+extern "C" int vg_gemm_ln_act_ms_bf16(const vg_asrc* src, int32_t nsrc, const float* W, int32_t ldw, int32_t N,
+                                      int32_t M, const float* bias, const float* addend, int32_t ld_add,
+                                      int32_t add_rows, const float* gamma, const float* beta, float eps,
+                                      float slope, float* Y, int32_t ldy, void* stream) {
+  return gemm_ln_act_ms<true>(src, nsrc, W, ldw, N, M, bias, addend, ld_add, add_rows, gamma, beta, eps, slope,
+                              Y, ldy, stream);
+}
+
+template <bool BF>
+static int gat_lin_att(const float* X, int32_t ldx, const float* W, int32_t N,
+                       int32_t Cin, int32_t C, const float* att_src, const float* att_dst,
+                       float* H, float* a_src, float* a_dst, void* stream) {
+  if (N < 0 || Cin <= 0 || C <= 0 || ldx < Cin || !X || !W || !att_src || !att_dst || !H ||
+      !a_src || !a_dst)
+    return VG_EINVAL;
+  if (N == 0) return 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (C > 2 * TN) {  // several column tiles: GEMM, then the per-row projection pass
+    const int rc = gemm<BF>(X, ldx, W, Cin, 1, nullptr, 0, nullptr, 0, H, C, N, C, Cin, stream);
+    if (rc) return rc;
+    return vg_gat_att(H, N, C, att_src, att_dst, a_src, a_dst, stream);
+  }
+  if (C > TN) {  // whole 128-column rows per block, projections in the epilogue
+    k_gemm_ln<2, 32, true, false, BF><<<dim3((N + 31) / 32, 1), 256, 0, s>>>(
+        X, ldx, W, Cin, nullptr, N, C, Cin, nullptr, nullptr, 0.f, 0.f, H, nullptr, nullptr, nullptr, att_src,
+        att_dst, a_src, a_dst);
+    VG_CHECK_LAUNCH();
+    return 0;
+  }
+  k_gemm<true, 0, true, BF><<<dim3((N + TM - 1) / TM, 1), 256, 0, s>>>(
+      X, ldx, W, Cin, nullptr, nullptr, 0, H, C, N, C, Cin, att_src, att_dst, a_src, a_dst);
   VG_CHECK_LAUNCH();
   return 0;
 }
@@ -673,33 +941,25 @@ extern "C" int vg_gemm_ln_act_ms(const vg_asrc* src, int32_t nsrc, const float* 
 extern "C" int vg_gat_lin_att(const float* X, int32_t ldx, const float* W, int32_t N,
                               int32_t Cin, int32_t C, const float* att_src, const float* att_dst,
                               float* H, float* a_src, float* a_dst, void* stream) {
-  if (N < 0 || Cin <= 0 || C <= 0 || ldx < Cin || !X || !W || !att_src || !att_dst || !H ||
-      !a_src || !a_dst)
-    return VG_EINVAL;
-  if (N == 0) return 0;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  if (C > 2 * TN) {  // several column tiles: GEMM, then the per-row projection pass
-    const int rc = vg_gemm(X, ldx, W, Cin, 1, nullptr, 0, nullptr, 0, H, C, N, C, Cin, stream);
-    if (rc) return rc;
-    return vg_gat_att(H, N, C, att_src, att_dst, a_src, a_dst, stream);
-  }
-  if (C > TN) {  // whole 128-column rows per block, projections in the epilogue
-    k_gemm_ln<2, 32, true><<<dim3((N + 31) / 32, 1), 256, 0, s>>>(
-        X, ldx, W, Cin, nullptr, N, C, Cin, nullptr, nullptr, 0.f, 0.f, H, nullptr, nullptr, nullptr, att_src,
-        att_dst, a_src, a_dst);
-    VG_CHECK_LAUNCH();
-    return 0;
-  }
-  k_gemm<true, 0, true><<<dim3((N + TM - 1) / TM, 1), 256, 0, s>>>(
-      X, ldx, W, Cin, nullptr, nullptr, 0, H, C, N, C, Cin, att_src, att_dst, a_src, a_dst);
-  VG_CHECK_LAUNCH();
-  return 0;
+  return gat_lin_att<false>(X, ldx, W, N, Cin, C, att_src, att_dst, H, a_src, a_dst, stream);
+}
+
+extern "C" int vg_gat_lin_att_bf16(const float* X, int32_t ldx, const float* W, int32_t N,
+                                   int32_t Cin, int32_t C, const float* att_src, const float* att_dst,
+                                   float* H, float* a_src, float* a_dst, void* stream) {
+  return gat_lin_att<true>(X, ldx, W, N, Cin, C, att_src, att_dst, H, a_src, a_dst, stream);
 }
 
 extern "C" int vg_gemm_tn(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N,
                           int32_t M, int32_t K, float* C, int32_t ldc, float* db, int32_t accumulate,
                           float* workspace, void* stream) {
   return gemm_tn(A, lda, B, ldb, N, M, K, C, ldc, db, N, accumulate, workspace, stream);
+}
+
+extern "C" int vg_gemm_tn_bf16(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N,
+                               int32_t M, int32_t K, float* C, int32_t ldc, float* db, int32_t accumulate,
+                               float* workspace, void* stream) {
+  return gemm_tn<true>(A, lda, B, ldb, N, M, K, C, ldc, db, N, accumulate, workspace, stream);
 }
 
 extern "C" int vg_gemm_tn_ex(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N,

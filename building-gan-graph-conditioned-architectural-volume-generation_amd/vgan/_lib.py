@@ -138,6 +138,12 @@ SIGNATURES = {
                                _c_f32, _c_p]),
 }
 
+# the dense products of the path, each also exported with bf16 operands
+# (include/vgan.h, "bf16 training"); same signatures
+DENSE = ("vg_gemm", "vg_gemm_tn", "vg_gemm_tn_deferred", "vg_gemm_ln_act", "vg_gemm_ln_act_ms", "vg_gat_lin_att")
+for _name in DENSE:
+    SIGNATURES[_name + "_bf16"] = SIGNATURES[_name]
+
 
 def _load() -> ctypes.CDLL:
     if not os.path.exists(LIB_PATH):
@@ -154,6 +160,46 @@ def _load() -> ctypes.CDLL:
 
 
 LIB = _load()
+
+
+# Operand precision of the dense products: "f32" (the reference's) or "bf16"
+# (configs[2]: bf16 operands, f32 accumulation and outputs).  A process-wide
+# setting rather than a thread-local one: autograd runs the backward of the
+# HIP ops on its own device thread, which must see the same precision.
+PRECISIONS = ("f32", "bf16")
+_precision = "f32"
+
+
+def gemm_precision() -> str:
+    return _precision
+
+
+def set_gemm_precision(p: str) -> None:
+    global _precision
+    if p not in PRECISIONS:
+        raise ValueError(f"gemm precision must be one of {PRECISIONS}, not {p!r}")
+    _precision = p
+
+
+class gemm_precision_scope:
+    """``with gemm_precision_scope("bf16"): ...`` -- set, then restore."""
+
+    def __init__(self, p: str):
+        self.p = p
+
+    def __enter__(self):
+        self.prev = _precision
+        set_gemm_precision(self.p)
+        return self
+
+    def __exit__(self, *exc):
+        set_gemm_precision(self.prev)
+        return False
+
+
+def dense(name: str):
+    """Entry point of the dense product ``name`` (one of DENSE) in the current precision."""
+    return getattr(LIB, name + "_bf16" if _precision == "bf16" else name)
 
 
 def ptr(t: Optional[torch.Tensor]):

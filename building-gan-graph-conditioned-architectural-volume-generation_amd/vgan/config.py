@@ -103,6 +103,10 @@ class Configuration(ProgramMap):
     * ``skip_dead_d_grads``: skip D's parameter gradients in the generator
       iteration (the next critic iteration zeroes them, ``trainer.py:475``).
     * ``world_size`` / ``rank``: data-parallel layout (set by ``vgan.dist``).
+    * ``precision``: ``"f32"`` (default; the reference's arithmetic) or
+      ``"bf16"`` (BASELINE configs[2]: every dense product -- nn.Linear and
+      GATConv.lin, forward, input and weight gradients -- with bf16 operands
+      and f32 accumulation; everything else f32).
     """
 
     _DATA_ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", "data"))
@@ -116,7 +120,7 @@ class Configuration(ProgramMap):
 
     def __init__(self, sanity_checking: bool = False):
         self.SANITY_CHECKING = sanity_checking
-        self.runtime = {"rng": "device", "world_size": 1, "rank": 0}
+        self.runtime = {"rng": "device", "world_size": 1, "rank": 0, "precision": "f32"}
         if sanity_checking:
             self.BATCH_SIZE = 1
             self.DATA_SLICER = int(1e10)

@@ -37,7 +37,7 @@ import torch
 import torch.nn as nn
 
 from . import data as vdata
-from ._lib import LIB, FoldCollector, check, ptr, stream_handle, sync_counter
+from ._lib import LIB, FoldCollector, check, dense, ptr, stream_handle, sync_counter
 
 ACT_NONE, ACT_RELU, ACT_MASK = 0, 1, 3
 
@@ -93,13 +93,13 @@ class CriticEngine:
 
     @staticmethod
     def _gemm(st, A, lda, B, ldb, bt, C, ldc, n, m, k, bias=None, act=ACT_NONE, aux=None, ldaux=0):
-        check(LIB.vg_gemm(A, lda, B, ldb, bt, bias, act, aux, ldaux, C, ldc, n, m, k, st), "vg_gemm")
+        check(dense("vg_gemm")(A, lda, B, ldb, bt, bias, act, aux, ldaux, C, ldc, n, m, k, st), "vg_gemm")
 
     @staticmethod
     def _gemm_tn(folds, st, dev, A, lda, B, ldb, n, m, k, C, ldc, db=None, db_rows=None):
         """Split-K weight gradient; its fold joins the iteration's batched folds."""
         ws = _f(max(1, int(LIB.vg_gemm_tn_ws_floats(n, m, k))), dev=dev)
-        folds.call(LIB.vg_gemm_tn_deferred, (A, lda, B, ldb, n, m, k, C, ldc, db, n if db_rows is None else db_rows,
+        folds.call(dense("vg_gemm_tn_deferred"), (A, lda, B, ldb, n, m, k, C, ldc, db, n if db_rows is None else db_rows,
                                              1, ptr(ws)), st, keep=(ws,), name="vg_gemm_tn_deferred")
 
     # ------------------------------------------------------------ engine
@@ -160,7 +160,7 @@ class CriticEngine:
         for (conv, norm), keep in zip(self.blocks, keeps):
             c = conv.out_channels
             H, a_s, a_d = _f(R, c, dev=dev), _f(R, dev=dev), _f(R, dev=dev)
-            check(LIB.vg_gat_lin_att(ptr(x), xw, ptr(conv.lin.weight), R, xw, c, ptr(conv.att_src),
+            check(dense("vg_gat_lin_att")(ptr(x), xw, ptr(conv.lin.weight), R, xw, c, ptr(conv.att_src),
                                      ptr(conv.att_dst), ptr(H), ptr(a_s), ptr(a_d), st), "vg_gat_lin_att")
             O, alpha = _f(R, c, dev=dev), _f(3 * E, dev=dev)
             check(LIB.vg_gat_aggregate_fwd(ptr(csr3.row_ptr), ptr(csr3.col), R, c, ptr(H), ptr(a_s), ptr(a_d),
@@ -277,7 +277,7 @@ class CriticEngine:
             c, cin = B["c"], B["xw"]
             # tangent of the projection with its attention projections in the epilogue
             uH, up_s, up_d = _f(n, c, dev=dev), _f(n, dev=dev), _f(n, dev=dev)
-            check(LIB.vg_gat_lin_att(u_in, cin, ptr(conv.lin.weight), n, cin, c, ptr(conv.att_src),
+            check(dense("vg_gat_lin_att")(u_in, cin, ptr(conv.lin.weight), n, cin, c, ptr(conv.att_src),
                                      ptr(conv.att_dst), ptr(uH), ptr(up_s), ptr(up_d), st), "vg_gat_lin_att")
             uO, hinj = _f(n, c, dev=dev), _f(n, c, dev=dev)
             ws = _f(int(LIB.vg_gat_jvp2_ws_floats(n, E, c)), dev=dev)

@@ -175,7 +175,7 @@ class VoxelGNNGenerator(nn.Module):
         the copy-invariant columns [em | voxel.x] once on N rows (vg_gemm into
         the addend, bias included), the per-copy columns read in place from
         their own tensors (vg_gemm_ln_act_ms) -- no torch.cat, no repeat."""
-        from ._lib import LIB, VgASrc, check, ptr, stream_handle
+        from ._lib import LIB, VgASrc, check, dense, ptr, stream_handle
 
         lin, ln, act = block
         w = lin.weight
@@ -183,11 +183,11 @@ class VoxelGNNGenerator(nn.Module):
         dev = w.device
         st = stream_handle(dev)
         add = torch.empty(n, m, dtype=torch.float32, device=dev)
-        check(LIB.vg_gemm(ptr(emvx), emvx.shape[1], ctypes.c_void_p(w.data_ptr() + 4 * emvx_w0), ktot, 1, ptr(lin.bias),
+        check(dense("vg_gemm")(ptr(emvx), emvx.shape[1], ctypes.c_void_p(w.data_ptr() + 4 * emvx_w0), ktot, 1, ptr(lin.bias),
                           0, None, 0, ptr(add), m, n, m, emvx.shape[1], st), "vg_gemm")
         arr = (VgASrc * len(srcs))(*[VgASrc(t.data_ptr(), t.stride(0), cols, w0, 0) for t, cols, w0 in srcs])
         y = torch.empty(rows, m, dtype=torch.float32, device=dev)
-        check(LIB.vg_gemm_ln_act_ms(arr, len(srcs), ptr(w), ktot, rows, m, None, ptr(add), m, n, ptr(ln.weight),
+        check(dense("vg_gemm_ln_act_ms")(arr, len(srcs), ptr(w), ktot, rows, m, None, ptr(add), m, n, ptr(ln.weight),
                                     ptr(ln.bias), float(ln.eps), float(act.negative_slope), ptr(y), m, st),
               "vg_gemm_ln_act_ms")
         return y

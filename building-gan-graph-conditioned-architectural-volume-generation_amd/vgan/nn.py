@@ -155,7 +155,7 @@ class _LinearLNActFn(Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, gamma, beta, eps, slope):
-        from ._lib import LIB, check, ptr, stream_handle
+        from ._lib import LIB, check, dense, ptr, stream_handle
 
         n, k = x.shape
         m = weight.shape[0]
@@ -165,7 +165,7 @@ class _LinearLNActFn(Function):
         h = torch.empty_like(y) if save else None
         mean = torch.empty(n, dtype=torch.float32, device=dev) if save else None
         rstd = torch.empty(n, dtype=torch.float32, device=dev) if save else None
-        check(LIB.vg_gemm_ln_act(ptr(x), k, ptr(weight), n, m, k, ptr(bias), ptr(gamma), ptr(beta), float(eps),
+        check(dense("vg_gemm_ln_act")(ptr(x), k, ptr(weight), n, m, k, ptr(bias), ptr(gamma), ptr(beta), float(eps),
                                  float(slope), ptr(h), ptr(y), ptr(mean), ptr(rstd), stream_handle(dev)),
               "vg_gemm_ln_act")
         ctx.eps, ctx.slope = eps, slope

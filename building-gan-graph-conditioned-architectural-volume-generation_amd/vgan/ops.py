@@ -25,7 +25,7 @@ import torch
 from torch.autograd import Function
 
 from . import _lib
-from ._lib import LIB, FoldCollector, check, ptr, require_cuda, stream_handle, sync_counter
+from ._lib import LIB, FoldCollector, dense, check, ptr, require_cuda, stream_handle, sync_counter
 
 NEG_SLOPE = 0.2
 SOFTMAX_EPS = 1e-16
@@ -818,7 +818,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, b_trans: bool, bias: Optional[torch.T
     if (b.shape[1] if b_trans else b.shape[0]) != k:
         raise ValueError("gemm: inner dimensions differ")
     c = torch.empty(n, m, dtype=torch.float32, device=a.device)
-    check(LIB.vg_gemm(ptr(a), k, ptr(b), b.shape[1], 1 if b_trans else 0, ptr(bb), int(act), None, 0, ptr(c), m, n,
+    check(dense("vg_gemm")(ptr(a), k, ptr(b), b.shape[1], 1 if b_trans else 0, ptr(bb), int(act), None, 0, ptr(c), m, n,
                       m, k, stream_handle(a.device)), "vg_gemm")
     return c
 
@@ -837,7 +837,7 @@ def lin_att(x: torch.Tensor, w: torch.Tensor, att_src: torch.Tensor, att_dst: to
     h = torch.empty(n, c, dtype=torch.float32, device=x.device)
     a_s = torch.empty(n, dtype=torch.float32, device=x.device)
     a_d = torch.empty(n, dtype=torch.float32, device=x.device)
-    check(LIB.vg_gat_lin_att(ptr(x), k, ptr(w), n, k, c, ptr(vs), ptr(vd), ptr(h), ptr(a_s), ptr(a_d),
+    check(dense("vg_gat_lin_att")(ptr(x), k, ptr(w), n, k, c, ptr(vs), ptr(vd), ptr(h), ptr(a_s), ptr(a_d),
                              stream_handle(x.device)), "vg_gat_lin_att")
     return h, a_s, a_d
 
@@ -853,7 +853,7 @@ def gemm_tn(a: torch.Tensor, b: torch.Tensor, want_colsum: bool = True):
     c = torch.empty(m, k, dtype=torch.float32, device=a.device)
     db = torch.empty(m, dtype=torch.float32, device=a.device) if want_colsum else None
     ws = torch.empty(max(1, int(LIB.vg_gemm_tn_ws_floats(n, m, k))), dtype=torch.float32, device=a.device)
-    check(LIB.vg_gemm_tn(ptr(a), m, ptr(b), k, n, m, k, ptr(c), k, ptr(db), 0, ptr(ws), stream_handle(a.device)),
+    check(dense("vg_gemm_tn")(ptr(a), m, ptr(b), k, n, m, k, ptr(c), k, ptr(db), 0, ptr(ws), stream_handle(a.device)),
           "vg_gemm_tn")
     return c, db
 
@@ -868,11 +868,11 @@ def gemm_tn_into(a: torch.Tensor, b: torch.Tensor, c_out: torch.Tensor, db_out: 
         raise ValueError("gemm_tn_into: inconsistent shapes")
     ws = torch.empty(max(1, int(LIB.vg_gemm_tn_ws_floats(n, m, k))), dtype=torch.float32, device=a.device)
     if _FOLDS is not None and n > 0:  # fold deferred to the context's batch
-        _FOLDS.call(LIB.vg_gemm_tn_deferred, (ptr(a), m, ptr(b), k, n, m, k, ptr(c_out), k, ptr(db_out), n, 1,
+        _FOLDS.call(dense("vg_gemm_tn_deferred"), (ptr(a), m, ptr(b), k, n, m, k, ptr(c_out), k, ptr(db_out), n, 1,
                                               ptr(ws)), stream_handle(a.device), keep=(ws,),
                     name="vg_gemm_tn_deferred")
         return
-    check(LIB.vg_gemm_tn(ptr(a), m, ptr(b), k, n, m, k, ptr(c_out), k, ptr(db_out), 1, ptr(ws),
+    check(dense("vg_gemm_tn")(ptr(a), m, ptr(b), k, n, m, k, ptr(c_out), k, ptr(db_out), 1, ptr(ws),
                          stream_handle(a.device)), "vg_gemm_tn")
 
 

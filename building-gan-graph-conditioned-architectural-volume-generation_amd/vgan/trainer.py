@@ -28,6 +28,7 @@ Differences that do not change results:
 from __future__ import annotations
 
 import datetime
+import itertools
 import os
 import time
 from typing import Dict, List, Optional
@@ -39,10 +40,13 @@ import torch.nn.functional as F
 from . import data as vdata
 from . import metrics as vmetrics
 from . import ops
+from ._lib import gemm_precision_scope
 from .critic import CriticEngine
 from .dist import GradSync
 from .flat import FlatAdam, FlatParams
 from .rng import RNG
+
+_TRAINER_IDS = itertools.count()
 
 
 class Trainer:
@@ -84,6 +88,14 @@ class Trainer:
                       and int(configuration.NUM_CLASSES) <= 32)
         self.critic = CriticEngine(discriminator, configuration) if use_engine else None
         self.states = {"epoch_start": 1, "best_f1_score": 0.0}
+        # captured step graphs are cached on the batch, per trainer (two
+        # trainers -- e.g. f32 and bf16 -- may step the same batch)
+        self._graph_key = f"step_graphs:{next(_TRAINER_IDS)}"
+        # operand precision of the dense products: "f32" (configs[1], the
+        # reference's) or "bf16" (configs[2]: bf16 operands, f32 accumulate)
+        self.precision = runtime.get("precision", "f32")
+        if self.precision not in ("f32", "bf16"):
+            raise ValueError(f"runtime['precision'] must be 'f32' or 'bf16', not {self.precision!r}")
 
     def _critic_loss_backward(self, local_graph, voxel_graph, label_hard, label_soft) -> torch.Tensor:
         """d_loss of trainer.py:476-479 with D's gradients accumulated into .grad."""
@@ -208,6 +220,10 @@ class Trainer:
 
     def step(self, local_graph, voxel_graph) -> Dict[str, torch.Tensor]:
         """One full G+D step (trainer.py:466-495); returns device tensors."""
+        with gemm_precision_scope(self.precision):
+            return self._step(local_graph, voxel_graph)
+
+    def _step(self, local_graph, voxel_graph) -> Dict[str, torch.Tensor]:
         cfg = self.configuration
         labels = self._critic_labels(local_graph, voxel_graph) if self._stacked_labels() else None
         d_losses: List[torch.Tensor] = []
@@ -247,6 +263,10 @@ class Trainer:
             d.copy_(s_)
 
     def capture(self, local_graph, voxel_graph):
+        with gemm_precision_scope(self.precision):
+            return self._capture(local_graph, voxel_graph)
+
+    def _capture(self, local_graph, voxel_graph):
         """Record the step of this (static) batch as hipGraphs.
 
         * stacked labels (device RNG): one graph for the stacked critic-label
@@ -296,12 +316,12 @@ class Trainer:
         self._restore(snap)
         graphs = {"labels": g_labels, "label_tensors": labels, "critic": critic, "gen": g_gen, "acc": acc,
                   "hard": hard, "with_adam": with_adam}
-        voxel_graph.set_derived("step_graphs", graphs)
+        voxel_graph.set_derived(self._graph_key, graphs)
         return graphs
 
     def step_graphed(self, local_graph, voxel_graph) -> Dict[str, torch.Tensor]:
         """``step`` replayed from hipGraphs (captured on first use per batch)."""
-        graphs = voxel_graph.derived("step_graphs") if callable(getattr(voxel_graph, "derived", None)) else None
+        graphs = voxel_graph.derived(self._graph_key) if callable(getattr(voxel_graph, "derived", None)) else None
         if graphs is None:
             graphs = self.capture(local_graph, voxel_graph)
         self.adam_g.sync_lr()
@@ -357,7 +377,8 @@ class Trainer:
         for local_graph, voxel_graph in self.dataloaders.validation_dataloader:
             local_graph = local_graph.to(self.configuration.DEVICE)
             voxel_graph = voxel_graph.to(self.configuration.DEVICE)
-            logits, hard, _ = self._generate(local_graph, voxel_graph)
+            with gemm_precision_scope(self.precision):
+                logits, hard, _ = self._generate(local_graph, voxel_graph)
             g_losses.append(self._compute_generator_loss(local_graph, voxel_graph, logits, hard))
             f1, per_graph, prec, rec, acc = self._compute_metrics(voxel_graph, hard)
             f1s.append(f1)
@@ -410,7 +431,8 @@ class Trainer:
         for local_graph, voxel_graph in self.dataloaders.test_dataloader:
             local_graph = local_graph.to(self.configuration.DEVICE)
             voxel_graph = voxel_graph.to(self.configuration.DEVICE)
-            _, hard, _ = self._generate(local_graph, voxel_graph)
+            with gemm_precision_scope(self.precision):
+                _, hard, _ = self._generate(local_graph, voxel_graph)
             f1, per_graph, prec, rec, acc = self._compute_metrics(voxel_graph, hard)
             f1s.append(f1)
             f1_graphs.extend(per_graph)

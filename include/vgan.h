@@ -479,6 +479,38 @@ int vg_gemm_ln_act_ms(const vg_asrc* src, int32_t nsrc, const float* W, int32_t 
                       int32_t add_rows, const float* gamma, const float* beta, float eps, float slope,
                       float* Y, int32_t ldy, void* stream);
 
+/* ---- bf16 training (BASELINE.json configs[2]) ---------------------------- */
+
+/* The dense products of the training step with bf16 operands: the same
+ * arguments, buffers (f32) and results as the functions without the suffix,
+ * except that both operands of every product are rounded to bf16 (round to
+ * nearest even) and multiplied on v_mfma_f32_32x32x16_bf16 with f32
+ * accumulation -- what torch.autocast(dtype=torch.bfloat16) does to the
+ * nn.Linear / GATConv.lin matmuls of models.py (forward, input gradient and
+ * weight gradient).  Outputs, epilogues (bias, activation, LayerNorm,
+ * attention projections) and bias gradients stay f32, as does every other
+ * kernel of the path (aggregation, softmax, GraphNorm, losses, Adam). */
+int vg_gemm_bf16(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t b_trans,
+                 const float* bias, int32_t act, const float* aux, int32_t ldaux, float* C,
+                 int32_t ldc, int32_t N, int32_t M, int32_t K, void* stream);
+int vg_gemm_tn_bf16(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N, int32_t M,
+                    int32_t K, float* C, int32_t ldc, float* db, int32_t accumulate,
+                    float* workspace, void* stream);
+int vg_gemm_tn_deferred_bf16(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N,
+                             int32_t M, int32_t K, float* C, int32_t ldc, float* db,
+                             int32_t db_rows, int32_t accumulate, float* workspace,
+                             vg_fold* folds_out, int32_t* n_out, void* stream);
+int vg_gemm_ln_act_bf16(const float* A, int32_t lda, const float* W, int32_t N, int32_t M, int32_t K,
+                        const float* bias, const float* gamma, const float* beta, float eps,
+                        float slope, float* H, float* Y, float* mean, float* rstd, void* stream);
+int vg_gemm_ln_act_ms_bf16(const vg_asrc* src, int32_t nsrc, const float* W, int32_t ldw, int32_t N,
+                           int32_t M, const float* bias, const float* addend, int32_t ld_add,
+                           int32_t add_rows, const float* gamma, const float* beta, float eps,
+                           float slope, float* Y, int32_t ldy, void* stream);
+int vg_gat_lin_att_bf16(const float* x, int32_t ldx, const float* w, int32_t num_nodes,
+                        int32_t c_in, int32_t c_out, const float* att_src, const float* att_dst,
+                        float* h, float* a_src, float* a_dst, void* stream);
+
 /* ---- optimiser ---------------------------------------------------------- */
 
 /* torch.optim.Adam (single-tensor semantics, weight_decay, no amsgrad) over one

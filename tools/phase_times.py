@@ -64,7 +64,7 @@ def main():
     loc, vox = pool[0]
     tr.step_graphed(loc, vox)
     torch.cuda.synchronize()
-    graphs = vox.derived("step_graphs")
+    graphs = vox.derived(tr._graph_key)
     if args.dump:
         for name, g in (("labels", graphs["labels"]), ("critic", graphs["critic"][0]), ("gen", graphs["gen"])):
             if g is not None:
