@@ -25,10 +25,10 @@
 // v_mfma_f32_32x32x16_bf16 with f32 accumulation -- torch.autocast's
 // treatment of a matmul, except that outputs, epilogues (bias, activation,
 // LayerNorm, attention projections) and bias gradients stay f32.  A K-tile of
-// 32 is 2 MFMAs of 32 cycles instead of 16 f32 MFMAs of 64.  LDS rows hold 32
-// bf16 padded to 40 (80 B: the 8-element fragment of a lane is one aligned
-// 16-byte read); global loads take 4 consecutive k per thread (one 8-byte LDS
-// store).
+// 32 is 2 bf16 MFMAs instead of 16 f32 MFMAs.  The global loads are the f32
+// path's (coalesced, one float per thread and step); the values are rounded
+// as they are written to LDS, whose rows hold 32 bf16 padded to 40 (80 B: the
+// 8-element fragment of a lane is one aligned 16-byte read).
 //
 // Tiling: 256-thread workgroup = 4 waves, 64 x 64 output tile, each wave one
 // 32 x 32 MFMA tile; K staged through LDS 32 at a time.  LDS rows are padded
@@ -116,52 +116,11 @@ __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int l
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  if constexpr (BF) {
-    // Ah[buf][n][k], Bh[buf][m][k] = op(B)[k][m], bf16; quads of 4 k per thread
-    __bf16(*Ah)[TM][LDH] = reinterpret_cast<__bf16(*)[TM][LDH]>(smem);
-    __bf16(*Bh)[TN][LDH] = reinterpret_cast<__bf16(*)[TN][LDH]>(smem + 2 * TM * LDP);
-    constexpr int QG = (TM * TK / 4) / 256;
-    float qa[QG][4], qb[QG][4];
-    auto load_bf = [&](int k0) {
-#pragma unroll
-      for (int q = 0; q < QG; ++q) {
-        const int g = t + 256 * q;
-        const int row = g >> 3, kq = (g & 7) * 4;
-        const int n = n0 + row;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int k = k0 + kq + i;
-          qa[q][i] = (n < N && k < K) ? A[(size_t)n * lda + k] : 0.f;
-          if (BT) {
-            const int m = m0 + row;
-            qb[q][i] = (m < M && k < K) ? B[(size_t)m * ldb + k] : 0.f;
-          } else {
-            const int m = m0 + (g & 63), kk = k0 + (g >> 6) * 4 + i;
-            qb[q][i] = (m < M && kk < K) ? B[(size_t)kk * ldb + m] : 0.f;
-          }
-        }
-      }
-    };
-    load_bf(0);
-    int buf = 0;
-    for (int k0 = 0; k0 < K; k0 += TK) {
-#pragma unroll
-      for (int q = 0; q < QG; ++q) {
-        const int g = t + 256 * q;
-        *reinterpret_cast<bf16x4*>(&Ah[buf][g >> 3][(g & 7) * 4]) = to_bf4(qa[q]);
-        if (BT) *reinterpret_cast<bf16x4*>(&Bh[buf][g >> 3][(g & 7) * 4]) = to_bf4(qb[q]);
-        else *reinterpret_cast<bf16x4*>(&Bh[buf][g & 63][(g >> 6) * 4]) = to_bf4(qb[q]);
-      }
-      __syncthreads();
-      if (k0 + TK < K) load_bf(k0 + TK);
-      const int h8 = 8 * (lane >> 5);
-#pragma unroll
-      for (int s16 = 0; s16 < TK; s16 += 16)
-        acc = mfma_bf(&Ah[buf][wr * 32 + (lane & 31)][s16 + h8], &Bh[buf][wc * 32 + (lane & 31)][s16 + h8], acc);
-      buf ^= 1;
-    }
-  } else {
   float ra[PER], rb[PER];
+  // BF && !BT: B in quads of 4 k per thread (lanes along m: coalesced), one
+  // 8-byte LDS store per quad instead of four transposing 2-byte stores
+  constexpr int QB = (TN * TK / 4) / 256;
+  float qb[QB][4];
   auto load = [&](int k0) {
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
@@ -172,33 +131,67 @@ __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int l
       if (BT) {
         const int m = m0 + row;
         rb[q] = (m < M && k < K) ? B[(size_t)m * ldb + k] : 0.f;
-      } else {
+      } else if (!BF) {
         const int kr = e / TN, j = e % TN;
         const int m = m0 + j, kk = k0 + kr;
         rb[q] = (m < M && kk < K) ? B[(size_t)kk * ldb + m] : 0.f;
       }
     }
+    if constexpr (BF && !BT) {
+#pragma unroll
+      for (int q = 0; q < QB; ++q) {
+        const int g = t + 256 * q;
+        const int m = m0 + (g & 63), kq = (g >> 6) * 4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int kk = k0 + kq + i;
+          qb[q][i] = (m < M && kk < K) ? B[(size_t)kk * ldb + m] : 0.f;
+        }
+      }
+    }
   };
+  // BF: the same coalesced global loads, staged as bf16 -- Ah[buf][n][k],
+  // Bh[buf][m][k] = op(B)[k][m] -- and multiplied 16 k at a time
+  __bf16(*Ah)[TM][LDH] = reinterpret_cast<__bf16(*)[TM][LDH]>(smem);
+  __bf16(*Bh)[TN][LDH] = reinterpret_cast<__bf16(*)[TN][LDH]>(smem + 2 * TM * LDP);
   load(0);
   int buf = 0;
   for (int k0 = 0; k0 < K; k0 += TK) {
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
       const int e = t + 256 * q;
-      As[buf][e / TK][e % TK] = ra[q];
-      if (BT) Bs[buf][e / TK][e % TK] = rb[q];
-      else Bs[buf][e % TN][e / TN] = rb[q];
+      if constexpr (BF) {
+        Ah[buf][e / TK][e % TK] = static_cast<__bf16>(ra[q]);
+        if (BT) Bh[buf][e / TK][e % TK] = static_cast<__bf16>(rb[q]);
+      } else {
+        As[buf][e / TK][e % TK] = ra[q];
+        if (BT) Bs[buf][e / TK][e % TK] = rb[q];
+        else Bs[buf][e % TN][e / TN] = rb[q];
+      }
+    }
+    if constexpr (BF && !BT) {
+#pragma unroll
+      for (int q = 0; q < QB; ++q) {
+        const int g = t + 256 * q;
+        *reinterpret_cast<bf16x4*>(&Bh[buf][g & 63][(g >> 6) * 4]) = to_bf4(qb[q]);
+      }
     }
     __syncthreads();
     if (k0 + TK < K) load(k0 + TK);
-    const float* ar = &As[buf][wr * 32 + (lane & 31)][lane >> 5];
-    const float* br = &Bs[buf][wc * 32 + (lane & 31)][lane >> 5];
+    if constexpr (BF) {
+      const int h8 = 8 * (lane >> 5);
 #pragma unroll
-    for (int kk = 0; kk < TK; kk += 2)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[kk], br[kk], acc, 0, 0, 0);
+      for (int s16 = 0; s16 < TK; s16 += 16)
+        acc = mfma_bf(&Ah[buf][wr * 32 + (lane & 31)][s16 + h8], &Bh[buf][wc * 32 + (lane & 31)][s16 + h8], acc);
+    } else {
+      const float* ar = &As[buf][wr * 32 + (lane & 31)][lane >> 5];
+      const float* br = &Bs[buf][wc * 32 + (lane & 31)][lane >> 5];
+#pragma unroll
+      for (int kk = 0; kk < TK; kk += 2)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[kk], br[kk], acc, 0, 0, 0);
+    }
     buf ^= 1;
   }
-  }  // f32 operands
   const int m = m0 + wc * 32 + (lane & 31);
   const float bv = (bias && m < M) ? bias[m] : 0.f;
 #pragma unroll
@@ -322,57 +315,9 @@ __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, in
       wcol = ms.wcol[sidx] + (k0 - kb);
     }
   };
-  if constexpr (BF) {
-    __bf16(*Ah)[TMR][LDH] = reinterpret_cast<__bf16(*)[TMR][LDH]>(smem);
-    __bf16(*Bh)[TNC][LDH] = reinterpret_cast<__bf16(*)[TNC][LDH]>(smem + 2 * TMR * LDP);
-    constexpr int QA = (TMR * TK / 4) / 256, QB = (TNC * TK / 4) / 256;
-    float qa[QA][4], qb[QB][4];
-    auto load_bf = [&](int k0) {
-      const float* asrc;
-      int ald, acol, wcol;
-      chunk_src(k0, asrc, ald, acol, wcol);
-#pragma unroll
-      for (int q = 0; q < QA; ++q) {
-        const int g = t + 256 * q;
-        const int n = n0 + (g >> 3), kq = (g & 7) * 4;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          qa[q][i] = (n < N && k0 + kq + i < K) ? asrc[(size_t)n * ald + acol + kq + i] : 0.f;
-      }
-#pragma unroll
-      for (int q = 0; q < QB; ++q) {
-        const int g = t + 256 * q;
-        const int m = g >> 3, kq = (g & 7) * 4;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          qb[q][i] = (m < M && k0 + kq + i < K) ? B[(size_t)m * ldb + wcol + kq + i] : 0.f;
-      }
-    };
-    load_bf(0);
-    int buf = 0;
-    for (int k0 = 0; k0 < K; k0 += TK) {
-#pragma unroll
-      for (int q = 0; q < QA; ++q) {
-        const int g = t + 256 * q;
-        *reinterpret_cast<bf16x4*>(&Ah[buf][g >> 3][(g & 7) * 4]) = to_bf4(qa[q]);
-      }
-#pragma unroll
-      for (int q = 0; q < QB; ++q) {
-        const int g = t + 256 * q;
-        *reinterpret_cast<bf16x4*>(&Bh[buf][g >> 3][(g & 7) * 4]) = to_bf4(qb[q]);
-      }
-      __syncthreads();
-      if (k0 + TK < K) load_bf(k0 + TK);
-      const int h8 = 8 * (lane >> 5);
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int s16 = 0; s16 < TK; s16 += 16)
-          acc[j] = mfma_bf(&Ah[buf][wr * 32 + (lane & 31)][s16 + h8],
-                           &Bh[buf][j * 32 * WCOLS + wc * 32 + (lane & 31)][s16 + h8], acc[j]);
-      buf ^= 1;
-    }
-  } else {
+  // BF: the same coalesced global loads, staged as bf16 (Ah[buf][n][k], Bh[buf][m][k])
+  __bf16(*Ah)[TMR][LDH] = reinterpret_cast<__bf16(*)[TMR][LDH]>(smem);
+  __bf16(*Bh)[TNC][LDH] = reinterpret_cast<__bf16(*)[TNC][LDH]>(smem + 2 * TMR * LDP);
   float ra[PA], rb[PB];
   auto load = [&](int k0) {
     const float* asrc;
@@ -397,26 +342,37 @@ __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, in
 #pragma unroll
     for (int q = 0; q < PA; ++q) {
       const int e = t + 256 * q;
-      As[buf][e / TK][e % TK] = ra[q];
+      if constexpr (BF) Ah[buf][e / TK][e % TK] = static_cast<__bf16>(ra[q]);
+      else As[buf][e / TK][e % TK] = ra[q];
     }
 #pragma unroll
     for (int q = 0; q < PB; ++q) {
       const int e = t + 256 * q;
-      Bs[buf][e / TK][e % TK] = rb[q];
+      if constexpr (BF) Bh[buf][e / TK][e % TK] = static_cast<__bf16>(rb[q]);
+      else Bs[buf][e / TK][e % TK] = rb[q];
     }
     __syncthreads();
     if (k0 + TK < K) load(k0 + TK);
-    const float* ar = &As[buf][wr * 32 + (lane & 31)][lane >> 5];
+    if constexpr (BF) {
+      const int h8 = 8 * (lane >> 5);
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const float* br = &Bs[buf][j * 32 * WCOLS + wc * 32 + (lane & 31)][lane >> 5];
+      for (int j = 0; j < NJ; ++j)
 #pragma unroll
-      for (int kk = 0; kk < TK; kk += 2)
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[kk], br[kk], acc[j], 0, 0, 0);
+        for (int s16 = 0; s16 < TK; s16 += 16)
+          acc[j] = mfma_bf(&Ah[buf][wr * 32 + (lane & 31)][s16 + h8],
+                           &Bh[buf][j * 32 * WCOLS + wc * 32 + (lane & 31)][s16 + h8], acc[j]);
+    } else {
+      const float* ar = &As[buf][wr * 32 + (lane & 31)][lane >> 5];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const float* br = &Bs[buf][j * 32 * WCOLS + wc * 32 + (lane & 31)][lane >> 5];
+#pragma unroll
+        for (int kk = 0; kk < TK; kk += 2)
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[kk], br[kk], acc[j], 0, 0, 0);
+      }
     }
     buf ^= 1;
   }
-  }  // f32 operands
   // stage the full-width tile (+ bias) in LDS
   __syncthreads();
   float* Ct = smem;
@@ -548,62 +504,22 @@ __global__ void __launch_bounds__(256 * G) k_gemm_tn(const float* __restrict__ A
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   float dbs = 0.f;
-  if constexpr (BF) {
-    // Ah[g][buf][m][n], Bh[g][buf][k][n] (the reduction index n contiguous):
-    // quads of 4 rows n of one column per thread
-    __bf16(*Ah)[2][TM][LDH] = reinterpret_cast<__bf16(*)[2][TM][LDH]>(smem);
-    __bf16(*Bh)[2][TN][LDH] = reinterpret_cast<__bf16(*)[2][TN][LDH]>(smem + G * 2 * TK * (TM + 1));
-    constexpr int QG = (TK * TM / 4) / 256;
-    float qa[QG][4], qb[QG][4];
-    auto load_bf = [&](int st) {
-      const int n1 = nb + st * TK;
-#pragma unroll
-      for (int q = 0; q < QG; ++q) {
-        const int g = t + 256 * q;
-        const int c = g & 63, nq = (g >> 6) * 4;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int n = n1 + nq + i;
-          const bool in = st < steps && n < ne;
-          qa[q][i] = (in && m0 + c < M) ? A[(size_t)n * lda + m0 + c] : 0.f;
-          qb[q][i] = (in && k0 + c < K) ? B[(size_t)n * ldb + k0 + c] : 0.f;
-        }
-      }
-    };
-    load_bf(grp);
-    int buf = 0;
-    for (int it = 0, st = grp; it < iters; ++it, st += G) {
-      const int n1 = nb + st * TK;
-#pragma unroll
-      for (int q = 0; q < QG; ++q) {
-        const int g = t + 256 * q;
-        const int c = g & 63, nq = (g >> 6) * 4;
-        *reinterpret_cast<bf16x4*>(&Ah[grp][buf][c][nq]) = to_bf4(qa[q]);
-        *reinterpret_cast<bf16x4*>(&Bh[grp][buf][c][nq]) = to_bf4(qb[q]);
-        if (do_db)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (n1 + nq + i < db_rows) dbs += qa[q][i];  // f32 column sums (0 past ne)
-      }
-      __syncthreads();
-      load_bf(st + G);
-      if (st < steps) {
-        const int h8 = 8 * (lane >> 5);
-#pragma unroll
-        for (int s16 = 0; s16 < TK; s16 += 16)
-          acc = mfma_bf(&Ah[grp][buf][wr * 32 + (lane & 31)][s16 + h8],
-                        &Bh[grp][buf][wc * 32 + (lane & 31)][s16 + h8], acc);
-      }
-      buf ^= 1;
-    }
-  } else {
+  // BF: the same coalesced global loads, staged as bf16 and transposed --
+  // Ah[g][buf][m][n], Bh[g][buf][k][n] -- so a lane's 8 consecutive n are one read
+  __bf16(*Ah)[2][TM][LDH] = reinterpret_cast<__bf16(*)[2][TM][LDH]>(smem);
+  __bf16(*Bh)[2][TN][LDH] = reinterpret_cast<__bf16(*)[2][TN][LDH]>(smem + G * 2 * TK * (TM + 1));
+  // BF: thread t takes column t & 63 and a quad of 4 rows n per q (each
+  // load coalesced along the columns), so element (q, i) is row
+  // 4 * (e / TM) + i of the f32 mapping's row e / TM -- one 8-byte store into
+  // the transposed image per quad
   float ra[PER], rb[PER];
   auto load = [&](int st) {
     const int n1 = nb + st * TK;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
       const int e = t + 256 * q;
-      const int r = e / TM, c = e % TM;
+      const int c = e % TM;
+      const int r = BF ? 4 * ((t >> 6) + 4 * (q >> 2)) + (q & 3) : e / TM;
       const int n = n1 + r;
       const bool in = st < steps && n < ne;
       ra[q] = (in && m0 + c < M) ? A[(size_t)n * lda + m0 + c] : 0.f;
@@ -617,23 +533,43 @@ __global__ void __launch_bounds__(256 * G) k_gemm_tn(const float* __restrict__ A
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
       const int e = t + 256 * q;
-      As[grp][buf][e / TM][e % TM] = ra[q];
-      Bs[grp][buf][e / TM][e % TM] = rb[q];
-      if (do_db && n1 + e / TM < db_rows) dbs += ra[q];  // column (t & 63), rows e / TM (0 past ne)
+      const int r = BF ? 4 * ((t >> 6) + 4 * (q >> 2)) + (q & 3) : e / TM;
+      if constexpr (!BF) {
+        As[grp][buf][r][e % TM] = ra[q];
+        Bs[grp][buf][r][e % TM] = rb[q];
+      }
+      if (do_db && n1 + r < db_rows) dbs += ra[q];  // column (t & 63), row r (0 past ne)
+    }
+    if constexpr (BF) {  // transposed images: the reduction index n contiguous
+#pragma unroll
+      for (int q4 = 0; q4 < PER / 4; ++q4) {
+        const int c = t & 63, r0 = 4 * ((t >> 6) + 4 * q4);
+        const float va[4] = {ra[4 * q4], ra[4 * q4 + 1], ra[4 * q4 + 2], ra[4 * q4 + 3]};
+        const float vb[4] = {rb[4 * q4], rb[4 * q4 + 1], rb[4 * q4 + 2], rb[4 * q4 + 3]};
+        *reinterpret_cast<bf16x4*>(&Ah[grp][buf][c][r0]) = to_bf4(va);
+        *reinterpret_cast<bf16x4*>(&Bh[grp][buf][c][r0]) = to_bf4(vb);
+      }
     }
     __syncthreads();
     load(st + G);
     if (st < steps) {
+      if constexpr (BF) {
+        const int h8 = 8 * (lane >> 5);
 #pragma unroll
-      for (int kk = 0; kk < TK; kk += 2) {
-        const float a = As[grp][buf][kk + (lane >> 5)][wr * 32 + (lane & 31)];
-        const float b = Bs[grp][buf][kk + (lane >> 5)][wc * 32 + (lane & 31)];
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+        for (int s16 = 0; s16 < TK; s16 += 16)
+          acc = mfma_bf(&Ah[grp][buf][wr * 32 + (lane & 31)][s16 + h8],
+                        &Bh[grp][buf][wc * 32 + (lane & 31)][s16 + h8], acc);
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < TK; kk += 2) {
+          const float a = As[grp][buf][kk + (lane >> 5)][wr * 32 + (lane & 31)];
+          const float b = Bs[grp][buf][kk + (lane >> 5)][wc * 32 + (lane & 31)];
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+        }
       }
     }
     buf ^= 1;
   }
-  }  // f32 operands
   float* sh = smem;  // G * 2 * TK * (TM + 1) >= (G - 1) * 4096 floats
   __shared__ float red[G * 4][64];
   __syncthreads();
