@@ -479,23 +479,18 @@ __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, in
 // group's MFMAs cover the other's loads -- the f32 MFMA alone is 1024 cycles
 // per 32-row step), and the groups' accumulators are added in group order at
 // the end (deterministic).
-template <int G, bool BF = false>
-__global__ void __launch_bounds__(256 * G) k_gemm_tn(const float* __restrict__ A, int lda,
-                                                     const float* __restrict__ B, int ldb, int N,
-                                                     int M, int K, int rows, float* __restrict__ part,
-                                                     float* __restrict__ pdb, int db_rows) {
+// One (row chunk, 64 x 64 output tile) of a split-K product: the body of
+// k_gemm_tn (one product per launch) and k_gemm_tn_group (many).
+template <int G, bool BF>
+__device__ __forceinline__ void tn_tile(const float* __restrict__ A, int lda, const float* __restrict__ B,
+                                        int ldb, int N, int M, int K, int rows, int chunk, int m0, int k0,
+                                        float* __restrict__ part, float* __restrict__ pdb, int db_rows) {
   __shared__ __attribute__((aligned(16))) float smem[G * 2 * TK * (TM + 1) + G * 2 * TK * (TN + 1)];
   float(*As)[2][TK][TM + 1] = reinterpret_cast<float(*)[2][TK][TM + 1]>(smem);  // As[g][buf][n][m]
   float(*Bs)[2][TK][TN + 1] = reinterpret_cast<float(*)[2][TK][TN + 1]>(smem + G * 2 * TK * (TM + 1));  // [n][k]
   constexpr int PER = (TK * TM) / 256;
   const int grp = threadIdx.x >> 8, t = threadIdx.x & 255, lane = t & 63, wave = t >> 6;
   const int wr = wave >> 1, wc = wave & 1;
-  // XCD-aware: each XCD takes a contiguous range of row chunks (tile_xy)
-  const int gxy = gridDim.x * gridDim.y;
-  const int logical = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
-                                gxy * gridDim.z);
-  const int chunk = logical / gxy, rem = logical % gxy;
-  const int m0 = (rem % gridDim.x) * TM, k0 = (rem / gridDim.x) * TN;
   const int nb = chunk * rows, ne = min(N, nb + rows);
   const int steps = ne > nb ? (ne - nb + TK - 1) / TK : 0;
   const int iters = (steps + G - 1) / G;
@@ -594,6 +589,45 @@ __global__ void __launch_bounds__(256 * G) k_gemm_tn(const float* __restrict__ A
     for (int w = 0; w < G * 4; ++w) v += red[w][t];
     pdb[(size_t)chunk * M + m0 + t] = v;
   }
+}
+
+template <int G, bool BF = false>
+__global__ void __launch_bounds__(256 * G) k_gemm_tn(const float* __restrict__ A, int lda,
+                                                     const float* __restrict__ B, int ldb, int N,
+                                                     int M, int K, int rows, float* __restrict__ part,
+                                                     float* __restrict__ pdb, int db_rows) {
+  // XCD-aware: each XCD takes a contiguous range of row chunks (tile_xy)
+  const int gxy = gridDim.x * gridDim.y;
+  const int logical = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
+                                gxy * gridDim.z);
+  const int chunk = logical / gxy, rem = logical % gxy;
+  tn_tile<G, BF>(A, lda, B, ldb, N, M, K, rows, chunk, (rem % gridDim.x) * TM, (rem / gridDim.x) * TN, part, pdb,
+                 db_rows);
+}
+
+// Up to VG_TN_GROUP_MAX planned products in one launch (vg_gemm_tn_group):
+// the weight gradients of a whole backward are only read by the optimizer,
+// so they need not run where the backward produces their operands.  Blocks
+// [block0[p], block0[p + 1]) belong to product p, chunk-major as in
+// k_gemm_tn; the XCD remap spans the whole grid, so each XCD takes a
+// contiguous range of (product, chunk) blocks.
+struct TnGroup {
+  vg_tn p[VG_TN_GROUP_MAX];
+  int block0[VG_TN_GROUP_MAX + 1];
+  int n;
+};
+
+template <int G, bool BF>
+__global__ void __launch_bounds__(256 * G) k_gemm_tn_group(const TnGroup g) {
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  int p = 0;
+  while (p + 1 < g.n && lb >= g.block0[p + 1]) ++p;
+  const vg_tn& d = g.p[p];
+  const int local = lb - g.block0[p];
+  const int gx = (d.M + TM - 1) / TM, gxy = gx * ((d.K + TN - 1) / TN);
+  const int chunk = local / gxy, rem = local % gxy;
+  tn_tile<G, BF>(d.A, d.lda, d.B, d.ldb, d.N, d.M, d.K, d.rows, chunk, (rem % gx) * TM, (rem / gx) * TN, d.part,
+                 d.pdb, d.db_rows);
 }
 
 // out[w / K][w % K] (row stride ldo) = sum_c part[c][w], fixed order (+= when acc);
@@ -757,6 +791,72 @@ extern "C" int vg_gemm_tn_deferred_bf16(const float* A, int32_t lda, const float
   if (!folds_out || !n_out || N <= 0) return VG_EINVAL;
   return gemm_tn<true>(A, lda, B, ldb, N, M, K, C, ldc, db, db_rows, accumulate, workspace, stream,
                        folds_out, n_out);
+}
+
+template <bool BF>
+static int gemm_tn_plan(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N, int32_t M, int32_t K,
+                        float* C, int32_t ldc, float* db, int32_t db_rows, int32_t accumulate, float* workspace,
+                        vg_tn* prod_out, vg_fold* folds_out, int32_t* n_out) {
+  if (n_out) *n_out = 0;
+  if (!prod_out || !folds_out || !n_out || N <= 0 || M <= 0 || K <= 0 || ldc < K || !A || !B || !C ||
+      !workspace || db_rows < 0)
+    return VG_EINVAL;
+  const int rows = tn_rows(N, M, K);
+  const int chunks = (N + rows - 1) / rows;
+  float* part = workspace;
+  float* pdb = workspace + (size_t)chunks * M * K;
+  *prod_out = vg_tn{A, B, part, db ? pdb : nullptr, lda, ldb, N, M, K, rows, chunks, db_rows < N ? db_rows : N,
+                    BF ? 1 : 0};
+  const int32_t W = M * K;
+  folds_out[0] = vg_fold{C, W, K, ldc, accumulate, 1, {{part, chunks, W}, {nullptr, 0, 0}}};
+  *n_out = 1;
+  if (db) {
+    folds_out[1] = vg_fold{db, M, M, M, accumulate, 1, {{pdb, chunks, M}, {nullptr, 0, 0}}};
+    *n_out = 2;
+  }
+  return 0;
+}
+
+extern "C" int vg_gemm_tn_plan(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N, int32_t M,
+                               int32_t K, float* C, int32_t ldc, float* db, int32_t db_rows, int32_t accumulate,
+                               float* workspace, vg_tn* prod_out, vg_fold* folds_out, int32_t* n_out) {
+  return gemm_tn_plan<false>(A, lda, B, ldb, N, M, K, C, ldc, db, db_rows, accumulate, workspace, prod_out,
+                             folds_out, n_out);
+}
+
+extern "C" int vg_gemm_tn_plan_bf16(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N,
+                                    int32_t M, int32_t K, float* C, int32_t ldc, float* db, int32_t db_rows,
+                                    int32_t accumulate, float* workspace, vg_tn* prod_out, vg_fold* folds_out,
+                                    int32_t* n_out) {
+  return gemm_tn_plan<true>(A, lda, B, ldb, N, M, K, C, ldc, db, db_rows, accumulate, workspace, prod_out,
+                            folds_out, n_out);
+}
+
+extern "C" int vg_gemm_tn_group(const vg_tn* prods, int32_t n, void* stream) {
+  if (n < 0 || n > VG_TN_GROUP_MAX || (n > 0 && !prods)) return VG_EINVAL;
+  if (n == 0) return 0;
+  TnGroup g{};
+  long long blocks = 0;
+  const int bf = prods[0].bf16;
+  for (int i = 0; i < n; ++i) {
+    const vg_tn& d = prods[i];
+    if (d.bf16 != bf || !d.A || !d.B || !d.part || d.N <= 0 || d.M <= 0 || d.K <= 0 || d.rows <= 0 ||
+        d.rows % TK || d.chunks != (d.N + d.rows - 1) / d.rows || d.db_rows < 0 || d.db_rows > d.N)
+      return VG_EINVAL;
+    g.p[i] = d;
+    g.block0[i] = static_cast<int>(blocks);
+    blocks += (long long)d.chunks * ((d.M + TM - 1) / TM) * ((d.K + TN - 1) / TN);
+  }
+  if (blocks > (1LL << 30)) return VG_EINVAL;
+  g.block0[n] = static_cast<int>(blocks);
+  g.n = n;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (bf)
+    k_gemm_tn_group<kTnGroups, true><<<static_cast<int>(blocks), 256 * kTnGroups, 0, s>>>(g);
+  else
+    k_gemm_tn_group<kTnGroups, false><<<static_cast<int>(blocks), 256 * kTnGroups, 0, s>>>(g);
+  VG_CHECK_LAUNCH();
+  return 0;
 }
 
 template <bool BF>

@@ -34,6 +34,19 @@ class VgFold(ctypes.Structure):
 VG_FOLD_MAX = 40
 
 
+class VgTn(ctypes.Structure):
+    """vg_tn (include/vgan.h): one planned weight-gradient product."""
+    _fields_ = [("A", _c_p), ("B", _c_p), ("part", _c_p), ("pdb", _c_p), ("lda", _c_i32), ("ldb", _c_i32),
+                ("N", _c_i32), ("M", _c_i32), ("K", _c_i32), ("rows", _c_i32), ("chunks", _c_i32),
+                ("db_rows", _c_i32), ("bf16", _c_i32)]
+
+
+VG_TN_GROUP_MAX = 32
+# VGAN_TN_GROUP=0: launch every weight-gradient product where the backward
+# forms it (one launch per layer) instead of grouping them (A/B knob)
+_TN_GROUP = os.environ.get("VGAN_TN_GROUP", "1") == "1"
+
+
 class VgASrc(ctypes.Structure):
     """vg_asrc (include/vgan.h): one column block of vg_gemm_ln_act_ms's A."""
     _fields_ = [("ptr", _c_p), ("ld", _c_i32), ("cols", _c_i32), ("w_col0", _c_i32), ("rows_mod", _c_i32)]
@@ -41,6 +54,9 @@ class VgASrc(ctypes.Structure):
 # name -> (restype, argtypes); every function listed here is declared in include/vgan.h
 SIGNATURES = {
     "vg_fold_batch": (ctypes.c_int, [_c_p, _c_i32, _c_p]),
+    "vg_gemm_tn_plan": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_i32, _c_p,
+                                       _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p]),
+    "vg_gemm_tn_group": (ctypes.c_int, [_c_p, _c_i32, _c_p]),
     "vg_gemm_tn_deferred": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_i32, _c_p,
                                            _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p]),
     "vg_gat_bwd_deferred": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p,
@@ -140,7 +156,8 @@ SIGNATURES = {
 
 # the dense products of the path, each also exported with bf16 operands
 # (include/vgan.h, "bf16 training"); same signatures
-DENSE = ("vg_gemm", "vg_gemm_tn", "vg_gemm_tn_deferred", "vg_gemm_ln_act", "vg_gemm_ln_act_ms", "vg_gat_lin_att")
+DENSE = ("vg_gemm", "vg_gemm_tn", "vg_gemm_tn_deferred", "vg_gemm_tn_plan", "vg_gemm_ln_act", "vg_gemm_ln_act_ms",
+         "vg_gat_lin_att")
 for _name in DENSE:
     SIGNATURES[_name + "_bf16"] = SIGNATURES[_name]
 
@@ -257,6 +274,7 @@ class FoldCollector:
     def __init__(self):
         self.folds = []
         self.keep = []
+        self.products = []
 
     def call(self, fn, args_before_stream, stream, keep=(), name="deferred"):
         arr = (VgFold * 3)()
@@ -266,7 +284,33 @@ class FoldCollector:
             self.folds.append(VgFold.from_buffer_copy(arr[i]))
         self.keep.extend(keep)
 
+    def tn(self, args_before_outputs, stream, keep=()):
+        """A weight-gradient product (vg_gemm_tn_plan's arguments up to the
+        workspace; accumulate into C / db).  It runs at flush() in one
+        vg_gemm_tn_group launch with the backward's other products, before
+        the folds; ``keep`` holds A, B and the workspace until then."""
+        if not _TN_GROUP:
+            self.call(dense("vg_gemm_tn_deferred"), args_before_outputs, stream, keep=keep, name="vg_gemm_tn_deferred")
+            return
+        prod = VgTn()
+        arr = (VgFold * 2)()
+        n = ctypes.c_int32(0)
+        check(dense("vg_gemm_tn_plan")(*args_before_outputs, ctypes.byref(prod), arr, ctypes.byref(n)),
+              "vg_gemm_tn_plan")
+        self.products.append(prod)
+        for i in range(n.value):
+            self.folds.append(VgFold.from_buffer_copy(arr[i]))
+        self.keep.extend(keep)
+
     def flush(self, stream) -> None:
+        # the grouped products first: their partials feed the folds
+        for bf in (0, 1):
+            prods = [p for p in self.products if p.bf16 == bf]
+            for i in range(0, len(prods), VG_TN_GROUP_MAX):
+                part = prods[i:i + VG_TN_GROUP_MAX]
+                arr = (VgTn * len(part))(*part)
+                check(LIB.vg_gemm_tn_group(arr, len(part), stream), "vg_gemm_tn_group")
+        self.products = []
         batches, cur, where = [], [], {}
         for f in self.folds:
             j = where.get(f.out)

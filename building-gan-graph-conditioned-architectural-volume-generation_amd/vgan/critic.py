@@ -99,8 +99,9 @@ class CriticEngine:
     def _gemm_tn(folds, st, dev, A, lda, B, ldb, n, m, k, C, ldc, db=None, db_rows=None):
         """Split-K weight gradient; its fold joins the iteration's batched folds."""
         ws = _f(max(1, int(LIB.vg_gemm_tn_ws_floats(n, m, k))), dev=dev)
-        folds.call(dense("vg_gemm_tn_deferred"), (A, lda, B, ldb, n, m, k, C, ldc, db, n if db_rows is None else db_rows,
-                                             1, ptr(ws)), st, keep=(ws,), name="vg_gemm_tn_deferred")
+        # A / B are buffers of loss_and_grad, alive until its folds.flush()
+        folds.tn((A, lda, B, ldb, n, m, k, C, ldc, db, n if db_rows is None else db_rows, 1, ptr(ws)), st,
+                 keep=(ws,))
 
     # ------------------------------------------------------------ engine
     def loss_and_grad(self, local_graph, voxel_graph, label_hard, label_soft, rng) -> torch.Tensor:

@@ -868,9 +868,8 @@ def gemm_tn_into(a: torch.Tensor, b: torch.Tensor, c_out: torch.Tensor, db_out: 
         raise ValueError("gemm_tn_into: inconsistent shapes")
     ws = torch.empty(max(1, int(LIB.vg_gemm_tn_ws_floats(n, m, k))), dtype=torch.float32, device=a.device)
     if _FOLDS is not None and n > 0:  # fold deferred to the context's batch
-        _FOLDS.call(dense("vg_gemm_tn_deferred"), (ptr(a), m, ptr(b), k, n, m, k, ptr(c_out), k, ptr(db_out), n, 1,
-                                              ptr(ws)), stream_handle(a.device), keep=(ws,),
-                    name="vg_gemm_tn_deferred")
+        _FOLDS.tn((ptr(a), m, ptr(b), k, n, m, k, ptr(c_out), k, ptr(db_out), n, 1, ptr(ws)),
+                  stream_handle(a.device), keep=(ws, a, b))
         return
     check(dense("vg_gemm_tn")(ptr(a), m, ptr(b), k, n, m, k, ptr(c_out), k, ptr(db_out), 1, ptr(ws),
                          stream_handle(a.device)), "vg_gemm_tn")

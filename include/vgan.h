@@ -416,6 +416,40 @@ int vg_gemm_tn_deferred(const float* A, int32_t lda, const float* B, int32_t ldb
                         int32_t accumulate, float* workspace, vg_fold* folds_out, int32_t* n_out,
                         void* stream);
 
+/* One planned weight-gradient product (split-K over N): part[chunk][M][K] =
+ * A[chunk rows]^T B[chunk rows] (A [N,M] row stride lda, B [N,K] stride ldb)
+ * and pdb[chunk][M] = column sums of A over rows < db_rows (pdb NULL: none);
+ * rows per chunk a multiple of 32; bf16 != 0: bf16 operands (vg_gemm_bf16). */
+typedef struct {
+  const float* A;
+  const float* B;
+  float* part;
+  float* pdb;
+  int32_t lda, ldb, N, M, K, rows, chunks, db_rows, bf16;
+} vg_tn;
+
+#define VG_TN_GROUP_MAX 32
+
+/* vg_gemm_tn_deferred that launches nothing: the product itself is described
+ * in *prod_out (host memory) for vg_gemm_tn_group, its folds (C, then db when
+ * non-NULL) in folds_out / *n_out.  The weight gradients of a backward are
+ * read only by the optimizer step, so the trainer runs all products of one
+ * backward in a single vg_gemm_tn_group launch (nn.Linear / GATConv.lin
+ * weight gradients of models.py, replacing one launch per layer), then their
+ * folds in vg_fold_batch.  The caller keeps A, B and workspace alive and
+ * unmodified until then. */
+int vg_gemm_tn_plan(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N, int32_t M,
+                    int32_t K, float* C, int32_t ldc, float* db, int32_t db_rows, int32_t accumulate,
+                    float* workspace, vg_tn* prod_out, vg_fold* folds_out, int32_t* n_out);
+int vg_gemm_tn_plan_bf16(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N, int32_t M,
+                         int32_t K, float* C, int32_t ldc, float* db, int32_t db_rows, int32_t accumulate,
+                         float* workspace, vg_tn* prod_out, vg_fold* folds_out, int32_t* n_out);
+
+/* Run up to VG_TN_GROUP_MAX planned products (a HOST array, passed to the
+ * kernel by value) in one launch; all of one precision.  Each writes only its
+ * own part / pdb. */
+int vg_gemm_tn_group(const vg_tn* prods, int32_t n, void* stream);
+
 /* vg_gat_bwd_ex without the parameter-gradient fold: up to 3 descriptors
  * (g_bias, g_att_dst, g_att_src); none when g_att_src is NULL. */
 int vg_gat_bwd_deferred(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,

@@ -376,3 +376,39 @@ def test_engine_matches_autograd_path_on_gpu(cuda):
     assert abs(l_eng.item() - l_ag.item()) <= 1e-5 * max(1.0, abs(l_ag.item()))
     ok, worst, total = grads_close(g_eng, g_ag, rtol=1e-3)
     assert ok, (worst, total)
+
+
+@pytest.mark.parametrize("precision", ["f32", "bf16"])
+def test_grouped_weight_gradients_bit_identical(cuda, precision, monkeypatch):
+    """The weight-gradient products of a backward run as ONE vg_gemm_tn_group
+    launch at its end (FoldCollector.tn) instead of one launch per layer: the
+    same tiles and chunks, so the critic engine's D gradient and the
+    generator backward's G gradient are bit-identical either way."""
+    from vgan import _lib, ops
+    from vgan._lib import gemm_precision_scope
+    from vgan.models import VoxelGNNGenerator
+
+    cfg, D, flat, loc, vox, prep, hard, soft, eng = _engine_setup(cuda, numbers=(5, 6), seed=4)
+    torch.manual_seed(9)
+    G = VoxelGNNGenerator(cfg, 17, 12).to(cuda).eval()
+    from vgan.flat import FlatParams
+    flat_g = FlatParams(G)
+    z = torch.randn(1, vox.num_nodes, cfg.Z_DIM, device=cuda)
+    noise = torch.empty(vox.num_nodes, 7, device=cuda).exponential_()
+    w = torch.randn(vox.num_nodes, 7, device=cuda)
+    hd, sd = hard.to(cuda).unsqueeze(0), soft.to(cuda).unsqueeze(0)
+    out = {}
+    for grouped in (True, False):
+        monkeypatch.setattr(_lib, "_TN_GROUP", grouped)
+        with gemm_precision_scope(precision):
+            flat.zero_grad()
+            loss = eng.loss_and_grad(loc, vox, hd, sd, _RecRNG(3))
+            flat_g.zero_grad()
+            logits, _, soft_g = G(loc, vox, z, noise=noise)
+            with ops.direct_param_grads(), ops.deferred_param_folds(cuda):
+                ((logits * w).sum() + (soft_g * w).sum()).backward()
+        torch.cuda.synchronize()
+        out[grouped] = (loss.item(), flat.grad.clone(), flat_g.grad.clone())
+    assert out[True][0] == out[False][0]
+    assert torch.equal(out[True][1], out[False][1])
+    assert torch.equal(out[True][2], out[False][2])
