@@ -717,9 +717,14 @@ extern "C" int vg_gemm_bf16(const float* A, int32_t lda, const float* B, int32_t
 #ifndef VG_TN_TARGET
 #define VG_TN_TARGET 768
 #endif
-static inline int tn_rows(int N, int M, int K) {
+#ifndef VG_TN_GROUP_TARGET
+#define VG_TN_GROUP_TARGET 192
+#endif
+// (a product planned for vg_gemm_tn_group shares the grid with the other
+// products of its backward: VG_TN_GROUP_TARGET workgroups each)
+static inline int tn_rows(int N, int M, int K, int wg_target = VG_TN_TARGET) {
   const int tiles = ((M + TM - 1) / TM) * ((K + TN - 1) / TN);
-  int target = VG_TN_TARGET / tiles;
+  int target = wg_target / tiles;
   if (target > 256) target = 256;
   if (target < 1) target = 1;
   int rows = (N + target - 1) / target;
@@ -729,7 +734,9 @@ static inline int tn_rows(int N, int M, int K) {
 
 extern "C" int64_t vg_gemm_tn_ws_floats(int32_t N, int32_t M, int32_t K) {
   if (N <= 0) return 1;
-  const int64_t chunks = (N + tn_rows(N, M, K) - 1) / tn_rows(N, M, K);
+  // enough for either plan: one launch per product or a grouped product
+  const int r = min(tn_rows(N, M, K), tn_rows(N, M, K, VG_TN_GROUP_TARGET));
+  const int64_t chunks = (N + r - 1) / r;
   return chunks * ((int64_t)M * K + M);
 }
 
@@ -801,7 +808,7 @@ static int gemm_tn_plan(const float* A, int32_t lda, const float* B, int32_t ldb
   if (!prod_out || !folds_out || !n_out || N <= 0 || M <= 0 || K <= 0 || ldc < K || !A || !B || !C ||
       !workspace || db_rows < 0)
     return VG_EINVAL;
-  const int rows = tn_rows(N, M, K);
+  const int rows = tn_rows(N, M, K, VG_TN_GROUP_TARGET);
   const int chunks = (N + rows - 1) / rows;
   float* part = workspace;
   float* pdb = workspace + (size_t)chunks * M * K;
