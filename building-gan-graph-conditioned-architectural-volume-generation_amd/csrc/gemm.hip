@@ -88,13 +88,29 @@ __device__ __forceinline__ void tile_xy(int& tx, int& ty) {
   ty = logical % gy;
 }
 
+// GraphNorm-backward partials in the epilogue of the GEMM that produces the
+// layer's output gradient g_y (vg_gemm_gn_bwd): x, keep [rows, M] (the
+// GraphNorm input and dropout multiplier), stats [S][2M] of segments of
+// seg_rows rows, tpart [row tile][2 slots][M][2] (sum gz, sum gz * xhat).
+struct GnpDesc {
+  const float* x;
+  const float* keep;
+  const float* stats;
+  const float* w;
+  const float* b;
+  const float* ms;
+  float eps;
+  int seg_rows;
+  float* tpart;
+};
+
 // C = A . op(B) (+bias) (+act).  BT: B is [M, K] (op = B^T); else B is [K, M].
 // Software pipelined: the next K-tile is loaded into registers while the MFMAs
 // of the current one run; LDS is double-buffered (one barrier per K-tile).
 // ATT (BT, ACT 0, M <= 64): also a_src[n] = <C[n,:], att_s>, a_dst[n] =
 // <C[n,:], att_d> -- GATConv's attention projections as the epilogue of its
 // own projection GEMM (the output tile is staged through LDS once).
-template <bool BT, int ACT, bool ATT = false, bool BF = false>
+template <bool BT, int ACT, bool ATT = false, bool BF = false, bool GNP = false>
 __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int lda,
                                               const float* __restrict__ B, int ldb,
                                               const float* __restrict__ bias,
@@ -103,7 +119,8 @@ __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int l
                                               const float* __restrict__ att_s = nullptr,
                                               const float* __restrict__ att_d = nullptr,
                                               float* __restrict__ a_src = nullptr,
-                                              float* __restrict__ a_dst = nullptr) {
+                                              float* __restrict__ a_dst = nullptr,
+                                              const GnpDesc gn = GnpDesc{}) {
   __shared__ __attribute__((aligned(16))) float smem[2 * TM * LDP + 2 * TN * LDP];
   float(*As)[TM][LDP] = reinterpret_cast<float(*)[TM][LDP]>(smem);
   float(*Bs)[TN][LDP] = reinterpret_cast<float(*)[TN][LDP]>(smem + 2 * TM * LDP);  // Bs[j][k] = op(B)[k][j]
@@ -116,6 +133,36 @@ __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int l
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  // GNP: the epilogue's GraphNorm operands are loaded here, so their latency
+  // hides behind the K loop: the tile's 16 rows of x / keep per lane, the two
+  // segments' statistics and the column's parameters
+  float gx_[GNP ? 16 : 1], gk_[GNP ? 16 : 1];
+  float gmu[2] = {0.f, 0.f}, gsd[2] = {1.f, 1.f}, gw_ = 0.f, gb_ = 0.f, gms_ = 0.f;
+  int gbound = 0;
+  if constexpr (GNP) {
+    const int mc = m0 + wc * 32 + (lane & 31);
+    const int seg0 = n0 / gn.seg_rows;
+    gbound = (seg0 + 1) * gn.seg_rows;  // first row of the next segment
+    if (mc < M) {
+      gw_ = gn.w[mc];
+      gb_ = gn.b[mc];
+      gms_ = gn.ms[mc];
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        if (q == 0 || gbound < N) {
+          const float* st = gn.stats + (size_t)(seg0 + q) * 2 * M;
+          gmu[q] = st[mc];
+          gsd[q] = st[M + mc] + gn.eps;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int n = n0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const bool ok = n < N && mc < M;
+      gx_[r] = ok ? gn.x[(size_t)n * M + mc] : 0.f;
+      gk_[r] = ok && gn.keep ? gn.keep[(size_t)n * M + mc] : 1.f;
+    }
+  }
   float ra[PER], rb[PER];
   // BF && !BT: B in quads of 4 k per thread (lanes along m: coalesced), one
   // 8-byte LDS store per quad instead of four transposing 2-byte stores
@@ -200,6 +247,55 @@ __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int l
     if (n < N && m < M) {
       const float av = ACT == 3 ? aux[(size_t)n * ldaux + m] : 0.f;
       C[(size_t)n * ldc + m] = act_fn<ACT>(acc[r] + bv, av);
+    }
+  }
+  if constexpr (GNP) {
+    // column partials of gz = g_y [z > 0] keep and gz * xhat over the tile's
+    // rows, per segment slot (0: the segment of row n0, 1: the next one);
+    // g_y = acc (ACT 0, no bias).  Row order in-lane, then the lane pair
+    // holding the other 16 rows, then the two row waves: deterministic.
+    float pa[2] = {0.f, 0.f}, pb[2] = {0.f, 0.f};
+    if (m < M) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = n0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (n < N) {
+          const int sl = n >= gbound;
+          const float xh = (gx_[r] - (sl ? gmu[1] : gmu[0]) * gms_) / (sl ? gsd[1] : gsd[0]);
+          const float gz = xh * gw_ + gb_ > 0.f ? acc[r] * gk_[r] : 0.f;
+          if (sl) {
+            pa[1] += gz;
+            pb[1] = fmaf(gz, xh, pb[1]);
+          } else {
+            pa[0] += gz;
+            pb[0] = fmaf(gz, xh, pb[0]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      pa[q] += __shfl_xor(pa[q], 32, 64);
+      pb[q] += __shfl_xor(pb[q], 32, 64);
+    }
+    __syncthreads();  // every wave is done with the last K-tile's LDS images
+    float* red = smem;  // [wr][64 columns][4]
+    if (lane < 32) {
+      float* rp = red + ((wr * 64) + wc * 32 + lane) * 4;
+      rp[0] = pa[0];
+      rp[1] = pb[0];
+      rp[2] = pa[1];
+      rp[3] = pb[1];
+    }
+    __syncthreads();
+    if (wr == 0 && lane < 32 && m < M) {
+      const float* r0p = red + (wc * 32 + lane) * 4;
+      const float* r1p = red + (64 + wc * 32 + lane) * 4;
+      float* tp = gn.tpart + (size_t)tx * 2 * M * 2;
+      tp[(size_t)m * 2] = r0p[0] + r1p[0];
+      tp[(size_t)m * 2 + 1] = r0p[1] + r1p[1];
+      tp[(size_t)(M + m) * 2] = r0p[2] + r1p[2];
+      tp[(size_t)(M + m) * 2 + 1] = r0p[3] + r1p[3];
     }
   }
   if constexpr (ATT) {
@@ -481,11 +577,14 @@ __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, in
 // the end (deterministic).
 // One (row chunk, 64 x 64 output tile) of a split-K product: the body of
 // k_gemm_tn (one product per launch) and k_gemm_tn_group (many).
+// smem: the kernel's tn_smem_floats<G>() floats (shared by both tile kinds)
+template <int G>
+constexpr int tn_smem_floats() { return G * 2 * TK * (TM + 1) + G * 2 * TK * (TN + 1); }
+
 template <int G, bool BF>
-__device__ __forceinline__ void tn_tile(const float* __restrict__ A, int lda, const float* __restrict__ B,
+__device__ __forceinline__ void tn_tile(float* smem, const float* __restrict__ A, int lda, const float* __restrict__ B,
                                         int ldb, int N, int M, int K, int rows, int chunk, int m0, int k0,
                                         float* __restrict__ part, float* __restrict__ pdb, int db_rows) {
-  __shared__ __attribute__((aligned(16))) float smem[G * 2 * TK * (TM + 1) + G * 2 * TK * (TN + 1)];
   float(*As)[2][TK][TM + 1] = reinterpret_cast<float(*)[2][TK][TM + 1]>(smem);  // As[g][buf][n][m]
   float(*Bs)[2][TK][TN + 1] = reinterpret_cast<float(*)[2][TK][TN + 1]>(smem + G * 2 * TK * (TM + 1));  // [n][k]
   constexpr int PER = (TK * TM) / 256;
@@ -591,6 +690,85 @@ __device__ __forceinline__ void tn_tile(const float* __restrict__ A, int lda, co
   }
 }
 
+// Narrow products (M, K <= 32, f32 operands): one 32 x 32 output tile per row
+// group, whose four waves split each 32-row K-step (8 rows = 4 MFMAs each)
+// instead of padding the product to a 64 x 64 tile, which quadrupled the f32
+// MFMA work of the narrow GAT / decoder layers (widths 1..32).  The waves'
+// accumulators are added in a fixed order at the end (deterministic).
+constexpr int TSN = 32;
+
+template <int G>
+__device__ __forceinline__ void tn_tile_narrow(float* smem, const float* __restrict__ A, int lda,
+                                               const float* __restrict__ B, int ldb, int N, int M, int K, int rows,
+                                               int chunk, float* __restrict__ part, float* __restrict__ pdb,
+                                               int db_rows) {
+  constexpr int PERN = (TK * TSN) / 256;
+  float(*As)[2][TK][TSN + 1] = reinterpret_cast<float(*)[2][TK][TSN + 1]>(smem);  // [g][buf][n][m]
+  float(*Bs)[2][TK][TSN + 1] = reinterpret_cast<float(*)[2][TK][TSN + 1]>(smem + G * 2 * TK * (TSN + 1));
+  const int grp = threadIdx.x >> 8, t = threadIdx.x & 255, lane = t & 63, wave = t >> 6;
+  const int nb = chunk * rows, ne = min(N, nb + rows);
+  const int steps = ne > nb ? (ne - nb + TK - 1) / TK : 0;
+  const int iters = (steps + G - 1) / G;
+  const int c = t & (TSN - 1);  // this thread's column in every load
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  float dbs = 0.f;
+  float ra[PERN], rb[PERN];
+  auto load = [&](int st) {
+    const int n1 = nb + st * TK;
+#pragma unroll
+    for (int q = 0; q < PERN; ++q) {
+      const int n = n1 + (t + 256 * q) / TSN;
+      const bool in = st < steps && n < ne;
+      ra[q] = (in && c < M) ? A[(size_t)n * lda + c] : 0.f;
+      rb[q] = (in && c < K) ? B[(size_t)n * ldb + c] : 0.f;
+    }
+  };
+  load(grp);
+  int buf = 0;
+  for (int it = 0, st = grp; it < iters; ++it, st += G) {
+    const int n1 = nb + st * TK;
+#pragma unroll
+    for (int q = 0; q < PERN; ++q) {
+      const int r = (t + 256 * q) / TSN;
+      As[grp][buf][r][c] = ra[q];
+      Bs[grp][buf][r][c] = rb[q];
+      if (pdb && n1 + r < db_rows) dbs += ra[q];
+    }
+    __syncthreads();
+    load(st + G);
+    if (st < steps) {
+#pragma unroll
+      for (int kk = 0; kk < 8; kk += 2) {
+        const int r = wave * 8 + kk + (lane >> 5);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[grp][buf][r][lane & 31], Bs[grp][buf][r][lane & 31], acc, 0,
+                                                   0, 0);
+      }
+    }
+    buf ^= 1;
+  }
+  __shared__ float redn[G * 8][TSN];
+  __syncthreads();  // every wave is done with the last K-step's images
+#pragma unroll
+  for (int r = 0; r < 16; ++r) smem[((grp * 4 + wave) * 16 + r) * 64 + lane] = acc[r];
+  redn[t >> 5 | grp << 3][c] = dbs;
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    float v = 0.f;
+    for (int w = 0; w < G * 4; ++w) v += smem[(w * 16 + r) * 64 + lane];
+    const int m = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), k = lane & 31;
+    if (m < M && k < K) part[(size_t)chunk * M * K + (size_t)m * K + k] = v;
+  }
+  if (pdb && lane < M) {
+    float v = 0.f;
+    for (int w = 0; w < G * 8; ++w) v += redn[w][lane];
+    pdb[(size_t)chunk * M + lane] = v;
+  }
+}
+
 template <int G, bool BF = false>
 __global__ void __launch_bounds__(256 * G) k_gemm_tn(const float* __restrict__ A, int lda,
                                                      const float* __restrict__ B, int ldb, int N,
@@ -601,8 +779,12 @@ __global__ void __launch_bounds__(256 * G) k_gemm_tn(const float* __restrict__ A
   const int logical = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
                                 gxy * gridDim.z);
   const int chunk = logical / gxy, rem = logical % gxy;
-  tn_tile<G, BF>(A, lda, B, ldb, N, M, K, rows, chunk, (rem % gridDim.x) * TM, (rem / gridDim.x) * TN, part, pdb,
-                 db_rows);
+  __shared__ __attribute__((aligned(16))) float smem[tn_smem_floats<G>()];
+  if (!BF && M <= TSN && K <= TSN)
+    tn_tile_narrow<G>(smem, A, lda, B, ldb, N, M, K, rows, chunk, part, pdb, db_rows);
+  else
+    tn_tile<G, BF>(smem, A, lda, B, ldb, N, M, K, rows, chunk, (rem % gridDim.x) * TM, (rem / gridDim.x) * TN, part,
+                   pdb, db_rows);
 }
 
 // Up to VG_TN_GROUP_MAX planned products in one launch (vg_gemm_tn_group):
@@ -626,8 +808,12 @@ __global__ void __launch_bounds__(256 * G) k_gemm_tn_group(const TnGroup g) {
   const int local = lb - g.block0[p];
   const int gx = (d.M + TM - 1) / TM, gxy = gx * ((d.K + TN - 1) / TN);
   const int chunk = local / gxy, rem = local % gxy;
-  tn_tile<G, BF>(d.A, d.lda, d.B, d.ldb, d.N, d.M, d.K, d.rows, chunk, (rem % gx) * TM, (rem / gx) * TN, d.part,
-                 d.pdb, d.db_rows);
+  __shared__ __attribute__((aligned(16))) float smem[tn_smem_floats<G>()];
+  if (!BF && d.M <= TSN && d.K <= TSN)
+    tn_tile_narrow<G>(smem, d.A, d.lda, d.B, d.ldb, d.N, d.M, d.K, d.rows, chunk, d.part, d.pdb, d.db_rows);
+  else
+    tn_tile<G, BF>(smem, d.A, d.lda, d.B, d.ldb, d.N, d.M, d.K, d.rows, chunk, (rem % gx) * TM, (rem / gx) * TN,
+                   d.part, d.pdb, d.db_rows);
 }
 
 // out[w / K][w % K] (row stride ldo) = sum_c part[c][w], fixed order (+= when acc);
@@ -697,6 +883,40 @@ static int gemm(const float* A, int32_t lda, const float* B, int32_t ldb, int32_
 #undef VG_G
   VG_CHECK_LAUNCH();
   return 0;
+}
+
+template <bool BF>
+static int gemm_gn_bwd(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N, int32_t M, int32_t K,
+                       float* C, int32_t ldc, const float* gn_x, const float* keep, int32_t seg_rows,
+                       const float* weight, const float* bias, const float* mean_scale, float eps,
+                       const float* stats, float* tpart, void* stream) {
+  if (N <= 0 || M <= 0 || K <= 0 || ldc < M || !A || !B || !C || !gn_x || !weight || !bias || !mean_scale ||
+      !stats || !tpart || seg_rows < TM || N % seg_rows)
+    return VG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  dim3 grid((N + TM - 1) / TM, (M + TN - 1) / TN);
+  const GnpDesc gn{gn_x, keep, stats, weight, bias, mean_scale, eps, seg_rows, tpart};
+  k_gemm<false, 0, false, BF, true><<<grid, 256, 0, s>>>(A, lda, B, ldb, nullptr, nullptr, 0, C, ldc, N, M, K,
+                                                         nullptr, nullptr, nullptr, nullptr, gn);
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int vg_gemm_gn_bwd(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N, int32_t M,
+                              int32_t K, float* C, int32_t ldc, const float* gn_x, const float* keep,
+                              int32_t seg_rows, const float* weight, const float* bias, const float* mean_scale,
+                              float eps, const float* stats, float* tpart, void* stream) {
+  return gemm_gn_bwd<false>(A, lda, B, ldb, N, M, K, C, ldc, gn_x, keep, seg_rows, weight, bias, mean_scale, eps,
+                            stats, tpart, stream);
+}
+
+extern "C" int vg_gemm_gn_bwd_bf16(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N, int32_t M,
+                                   int32_t K, float* C, int32_t ldc, const float* gn_x, const float* keep,
+                                   int32_t seg_rows, const float* weight, const float* bias,
+                                   const float* mean_scale, float eps, const float* stats, float* tpart,
+                                   void* stream) {
+  return gemm_gn_bwd<true>(A, lda, B, ldb, N, M, K, C, ldc, gn_x, keep, seg_rows, weight, bias, mean_scale, eps,
+                           stats, tpart, stream);
 }
 
 extern "C" int vg_gemm(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t b_trans,

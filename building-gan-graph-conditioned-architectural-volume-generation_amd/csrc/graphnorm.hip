@@ -354,6 +354,48 @@ __global__ void __launch_bounds__(kBlock) k_gn_bwd_final(
   }
 }
 
+// The same fold over the partials that the producing GEMM wrote in its
+// epilogue (vg_gemm_gn_bwd): tpart[tile][slot][C][2] for 64-row tiles of the
+// S * N stacked rows, slot 0 = the segment of the tile's first row, slot 1 =
+// the next segment (a tile straddles at most two: N >= 64).  One wave per
+// column; segment sg sums its tiles in tile order (deterministic).
+__global__ void __launch_bounds__(kBlock) k_gn_bwd_final_tiles(
+    const float* __restrict__ tpart, int N, int C, int S, const float* __restrict__ w,
+    const float* __restrict__ ms, float eps, const float* __restrict__ stats, float* __restrict__ sums,
+    float* __restrict__ g_w, float* __restrict__ g_b, float* __restrict__ g_ms, int accumulate) {
+  constexpr int kTile = 64;
+  const int c = fold_col(), lane = threadIdx.x & 63;
+  if (c >= C) return;
+  float tw = 0.f, tb = 0.f, tm = 0.f;
+  for (int sg = 0; sg < S; ++sg) {
+    const long long r0 = (long long)sg * N, r1 = r0 + N - 1;
+    const int t0 = static_cast<int>(r0 / kTile), t1 = static_cast<int>(r1 / kTile);
+    float a = 0.f, bb = 0.f;
+#pragma unroll 4
+    for (int t = t0 + lane; t <= t1; t += 64) {
+      const int slot = (long long)t * kTile >= r0 ? 0 : 1;  // first row in sg, or in sg - 1
+      const float* p = tpart + ((size_t)(2 * t + slot) * C + c) * 2;
+      a += p[0];
+      bb += p[1];
+    }
+    a = wave_sum(a);
+    bb = wave_sum(bb);
+    const float* st = stats + (size_t)sg * 2 * C;
+    if (lane == 0) {
+      sums[(size_t)sg * 2 * C + c] = a;
+      sums[(size_t)sg * 2 * C + C + c] = bb;
+    }
+    tw += bb;
+    tb += a;
+    tm += -st[c] * w[c] * a / (st[C + c] + eps);
+  }
+  if (lane == 0 && g_w) {
+    g_w[c] = accumulate ? g_w[c] + tw : tw;
+    g_b[c] = accumulate ? g_b[c] + tb : tb;
+    g_ms[c] = accumulate ? g_ms[c] + tm : tm;
+  }
+}
+
 // g_x (+ inj for elements t >= inj_off: the second-order adjoint of the
 // critic engine's mix copy)
 __global__ void k_gn_bwd_apply(const float* __restrict__ x, const float* __restrict__ gy,
@@ -746,6 +788,11 @@ extern "C" int vg_graphnorm_fwd(const float* x, int32_t N, int32_t C, const floa
                               nullptr, stream);
 }
 
+static void gn_bwd_apply_launch(const float* x, int32_t S, int32_t N, int32_t C, const float* weight,
+                                const float* bias, const float* mean_scale, const float* keep, float eps,
+                                const float* stats, const float* sums, const float* g_y, float* g_x,
+                                const float* inj, int64_t inj_offset, hipStream_t s);
+
 extern "C" int vg_graphnorm_bwd_seg(const float* x, int32_t S, int32_t N, int32_t C,
                                     const float* weight, const float* bias,
                                     const float* mean_scale, const float* keep, float eps,
@@ -765,6 +812,38 @@ extern "C" int vg_graphnorm_bwd_seg(const float* x, int32_t S, int32_t N, int32_
   (void)sync;
   k_gn_bwd_final<<<vg_blocks(C, kBlock / 64), kBlock, 0, s>>>(part, chunks, C, S, weight, mean_scale, eps,
                                                               stats, sums, g_w, g_b, g_ms, accumulate);
+  gn_bwd_apply_launch(x, S, N, C, weight, bias, mean_scale, keep, eps, stats, sums, g_y, g_x, inj, inj_offset, s);
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int64_t vg_gemm_gn_tpart_floats(int32_t rows, int32_t channels) {
+  return ((int64_t)rows + 63) / 64 * 2 * 2 * (int64_t)(channels > 0 ? channels : 1);
+}
+
+extern "C" int vg_graphnorm_bwd_seg_tiles(const float* x, int32_t S, int32_t N, int32_t C,
+                                          const float* weight, const float* bias,
+                                          const float* mean_scale, const float* keep, float eps,
+                                          const float* stats, const float* g_y, const float* tpart,
+                                          float* g_x, float* g_w, float* g_b, float* g_ms,
+                                          int32_t accumulate, const float* inj, int64_t inj_offset,
+                                          float* ws, void* stream) {
+  if (S <= 0 || N < 64 || C <= 0 || !x || !weight || !bias || !mean_scale || !stats || !g_y || !tpart ||
+      !g_x || !ws || (g_w && (!g_b || !g_ms)) || inj_offset < 0)
+    return VG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  float* sums = ws + (size_t)S * kChunks * C * 5;
+  k_gn_bwd_final_tiles<<<vg_blocks(C, kBlock / 64), kBlock, 0, s>>>(tpart, N, C, S, weight, mean_scale, eps,
+                                                                    stats, sums, g_w, g_b, g_ms, accumulate);
+  gn_bwd_apply_launch(x, S, N, C, weight, bias, mean_scale, keep, eps, stats, sums, g_y, g_x, inj, inj_offset, s);
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+static void gn_bwd_apply_launch(const float* x, int32_t S, int32_t N, int32_t C, const float* weight,
+                                const float* bias, const float* mean_scale, const float* keep, float eps,
+                                const float* stats, const float* sums, const float* g_y, float* g_x,
+                                const float* inj, int64_t inj_offset, hipStream_t s) {
   const long long total = (long long)S * N * C;
   const int lds_f = 3 * C + 4 * C * S;
   // the quad form narrows inj_offset to int: only when it fits (as total does)
@@ -777,8 +856,6 @@ extern "C" int vg_graphnorm_bwd_seg(const float* x, int32_t S, int32_t N, int32_
     k_gn_bwd_apply<<<apply_blocks(total), 256, 0, s>>>(x, g_y, total, N, C, weight, bias,
                                                        mean_scale, keep, eps, stats, sums, inj,
                                                        (long long)inj_offset, g_x);
-  VG_CHECK_LAUNCH();
-  return 0;
 }
 
 extern "C" int vg_graphnorm_bwd(const float* x, int32_t N, int32_t C, const float* weight,

@@ -57,6 +57,12 @@ SIGNATURES = {
     "vg_gemm_tn_plan": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_i32, _c_p,
                                        _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p]),
     "vg_gemm_tn_group": (ctypes.c_int, [_c_p, _c_i32, _c_p]),
+    "vg_gemm_gn_tpart_floats": (_c_i64, [_c_i32, _c_i32]),
+    "vg_gemm_gn_bwd": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p,
+                                      _c_i32, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p]),
+    "vg_graphnorm_bwd_seg_tiles": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p,
+                                                  _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_i64, _c_p,
+                                                  _c_p]),
     "vg_gemm_tn_deferred": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_i32, _c_p,
                                            _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p]),
     "vg_gat_bwd_deferred": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p,
@@ -157,7 +163,7 @@ SIGNATURES = {
 # the dense products of the path, each also exported with bf16 operands
 # (include/vgan.h, "bf16 training"); same signatures
 DENSE = ("vg_gemm", "vg_gemm_tn", "vg_gemm_tn_deferred", "vg_gemm_tn_plan", "vg_gemm_ln_act", "vg_gemm_ln_act_ms",
-         "vg_gat_lin_att")
+         "vg_gat_lin_att", "vg_gemm_gn_bwd")
 for _name in DENSE:
     SIGNATURES[_name + "_bf16"] = SIGNATURES[_name]
 

@@ -33,6 +33,8 @@ from __future__ import annotations
 
 from typing import List, Optional
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -40,6 +42,9 @@ from . import data as vdata
 from ._lib import LIB, FoldCollector, check, dense, ptr, stream_handle, sync_counter
 
 ACT_NONE, ACT_RELU, ACT_MASK = 0, 1, 3
+# VGAN_GN_FUSE=0: the GraphNorm backward's column partials in their own pass
+# instead of the epilogue of the GEMM producing its g_y (A/B knob)
+_GN_FUSE = os.environ.get("VGAN_GN_FUSE", "1") == "1"
 
 
 def _f(*shape, dev):
@@ -145,6 +150,51 @@ class CriticEngine:
         def rows(t: torch.Tensor, r0: int, width: int):
             return _off(t, r0 * width)
 
+        # a tile straddles at most two stacked copies: n >= 64 rows per copy
+        fuse_gn = _GN_FUSE and n >= 64
+
+        def gn_inputs(b: int, mix: bool):
+            """block b's GraphNorm input, keep and statistics: the mix copy's
+            rows (pass B) or all three copies (pass D)"""
+            B, c = blk[b], blk[b]["c"]
+            x = rows(B["O"], mrow, c) if mix else ptr(B["O"])
+            keep = None if B["keep"] is None else (rows(B["keep"], mrow, c) if mix else ptr(B["keep"]))
+            stats = _off(B["stats"], 2 * 2 * c) if mix else ptr(B["stats"])
+            return x, keep, stats
+
+        def gemm_dy(A, lda, Wt, ldw, out, nrows: int, m: int, k: int, b: int, mix: bool):
+            """out [nrows, m] = A Wt, the output gradient of block b's GraphNorm;
+            with fuse_gn that backward's column partials come from this GEMM's
+            epilogue (returned, for gn_bwd), else None."""
+            if not fuse_gn:
+                self._gemm(st, A, lda, Wt, ldw, 0, out, m, nrows, m, k)
+                return None
+            norm = self.blocks[b][1]
+            tp = _f(int(LIB.vg_gemm_gn_tpart_floats(nrows, m)), dev=dev)
+            x, keep, stats = gn_inputs(b, mix)
+            check(dense("vg_gemm_gn_bwd")(A, lda, Wt, ldw, nrows, m, k, out, m, x, keep, n, ptr(norm.weight),
+                                          ptr(norm.bias), ptr(norm.mean_scale), float(norm.eps), stats, ptr(tp), st),
+                  "vg_gemm_gn_bwd")
+            return tp
+
+        def gn_bwd(b: int, mix: bool, tp, g_y, g_x, pgrads: bool, inj=None, inj_off: int = 0):
+            """block b's GraphNorm(+ReLU+Dropout) backward: g_x from g_y"""
+            norm, c = self.blocks[b][1], blk[b]["c"]
+            S = 1 if mix else 3
+            x, keep, stats = gn_inputs(b, mix)
+            ws = _f(int(LIB.vg_graphnorm_seg_ws_floats(S, n, c)), dev=dev)
+            pg = (ptr(norm.weight.grad), ptr(norm.bias.grad), ptr(norm.mean_scale.grad)) if pgrads else (None,) * 3
+            if tp is not None:
+                check(LIB.vg_graphnorm_bwd_seg_tiles(x, S, n, c, ptr(norm.weight), ptr(norm.bias), ptr(norm.mean_scale),
+                                                     keep, float(norm.eps), stats, ptr(g_y), ptr(tp), ptr(g_x), *pg,
+                                                     1 if pgrads else 0, inj, inj_off, ptr(ws), st),
+                      "vg_graphnorm_bwd_seg_tiles")
+            else:
+                check(LIB.vg_graphnorm_bwd_seg(x, S, n, c, ptr(norm.weight), ptr(norm.bias), ptr(norm.mean_scale),
+                                               keep, float(norm.eps), stats, ptr(g_y), ptr(g_x), *pg,
+                                               1 if pgrads else 0, inj, inj_off, ptr(ws), sy, st),
+                      "vg_graphnorm_bwd_seg")
+
         # ---------------------------------------------------------- pass A
         X0 = _f(X4, W0, dev=dev)
         check(LIB.vg_critic_input(ptr(mvx), n, F, ptr(real), ptr(hard), ptr(soft), ptr(eps), K, 4, ptr(X0), st),
@@ -215,20 +265,15 @@ class CriticEngine:
                        None, ACT_MASK, rows(dec_out[i - 1], mrow, m), m)
         W = self.dec[0].weight
         dY = _f(n, W.shape[1], dev=dev)
-        self._gemm(st, rows(adj_dec[0], trow, W.shape[0]), W.shape[0], ptr(W), W.shape[1], 0, ptr(dY), W.shape[1], n,
-                   W.shape[1], W.shape[0])
+        tp = gemm_dy(rows(adj_dec[0], trow, W.shape[0]), W.shape[0], ptr(W), W.shape[1], ptr(dY), n, W.shape[1],
+                     W.shape[0], nb - 1, True)
         dY_b, dO_b = [None] * nb, [None] * nb
         for b in range(nb - 1, -1, -1):
             (conv, norm), B = self.blocks[b], blk[b]
             c = B["c"]
             dY_b[b] = dY
             dO = _f(n, c, dev=dev)
-            ws = _f(int(LIB.vg_graphnorm_seg_ws_floats(1, n, c)), dev=dev)
-            check(LIB.vg_graphnorm_bwd_seg(rows(B["O"], mrow, c), 1, n, c, ptr(norm.weight), ptr(norm.bias),
-                                           ptr(norm.mean_scale),
-                                           rows(B["keep"], mrow, c) if B["keep"] is not None else None,
-                                           float(norm.eps), _off(B["stats"], 2 * 2 * c), ptr(dY), ptr(dO), None, None,
-                                           None, 0, None, 0, ptr(ws), sy, st), "vg_graphnorm_bwd_seg")
+            gn_bwd(b, True, tp, dY, dO, False)
             dH = rows(adj_H[b], trow, c)
             ws = _f(int(LIB.vg_gat_bwd_ws_floats(n, E, c)), dev=dev)
             check(LIB.vg_gat_bwd_ex(ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot),
@@ -240,7 +285,7 @@ class CriticEngine:
             cin = B["xw"]
             if b > 0:
                 dX = _f(n, cin, dev=dev)
-                self._gemm(st, dH, c, ptr(conv.lin.weight), cin, 0, ptr(dX), cin, n, cin, c)
+                tp = gemm_dy(dH, c, ptr(conv.lin.weight), cin, ptr(dX), n, cin, c, b - 1, True)
                 dY = dX
             else:
                 self._gemm(st, dH, c, ptr(conv.lin.weight), cin, 0, rows(adj_mlp[-1], trow, cin), cin, n, cin, c,
@@ -318,17 +363,12 @@ class CriticEngine:
                            ACT_MASK, ptr(dec_out[i - 1]), m)
             else:
                 dY = _f(R, m, dev=dev)
-                self._gemm(st, ptr(adj_dec[0]), aw, ptr(lin.weight), m, 0, ptr(dY), m, R, m, aw)
+                tp = gemm_dy(ptr(adj_dec[0]), aw, ptr(lin.weight), m, ptr(dY), R, m, aw, nb - 1, False)
         for b in range(nb - 1, -1, -1):
             (conv, norm), B = self.blocks[b], blk[b]
             c, cin = B["c"], B["xw"]
             dO = _f(R, c, dev=dev)
-            ws = _f(int(LIB.vg_graphnorm_seg_ws_floats(3, n, c)), dev=dev)
-            check(LIB.vg_graphnorm_bwd_seg(ptr(B["O"]), 3, n, c, ptr(norm.weight), ptr(norm.bias),
-                                           ptr(norm.mean_scale), ptr(B["keep"]), float(norm.eps), ptr(B["stats"]),
-                                           ptr(dY), ptr(dO), ptr(norm.weight.grad), ptr(norm.bias.grad),
-                                           ptr(norm.mean_scale.grad), 1, ptr(oinj_b[b]), mrow * c, ptr(ws), sy, st),
-                  "vg_graphnorm_bwd_seg")
+            gn_bwd(b, False, tp, dY, dO, True, ptr(oinj_b[b]), mrow * c)
             ws = _f(int(LIB.vg_gat_bwd_ws_floats(R, 3 * E, c)), dev=dev)
             folds.call(LIB.vg_gat_bwd_deferred,
                        (ptr(csr3.row_ptr), ptr(csr3.col), ptr(csr3.csc_ptr), ptr(csr3.csc_slot), ptr(csr3.csc_dst), R,
@@ -339,7 +379,7 @@ class CriticEngine:
             self._gemm_tn(folds, st, dev, ptr(adj_H[b]), c, ptr(B["X"]), cin, X4, c, cin, ptr(conv.lin.weight.grad), cin)
             if b > 0:
                 dY = _f(R, cin, dev=dev)
-                self._gemm(st, ptr(adj_H[b]), c, ptr(conv.lin.weight), cin, 0, ptr(dY), cin, R, cin, c)
+                tp = gemm_dy(ptr(adj_H[b]), c, ptr(conv.lin.weight), cin, ptr(dY), R, cin, c, b - 1, False)
             else:
                 self._gemm(st, ptr(adj_H[b]), c, ptr(conv.lin.weight), cin, 0, ptr(adj_mlp[-1]), cin, R, cin, c,
                            None, ACT_MASK, ptr(mlp_out[-1]), cin)

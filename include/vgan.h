@@ -513,6 +513,36 @@ int vg_gemm_ln_act_ms(const vg_asrc* src, int32_t nsrc, const float* W, int32_t 
                       int32_t add_rows, const float* gamma, const float* beta, float eps, float slope,
                       float* Y, int32_t ldy, void* stream);
 
+/* ---- GraphNorm backward partials in the producing GEMM -------------------- */
+
+/* C[N,M] = A[N,K] B[K,M] (vg_gemm, b_trans 0, no bias / activation) is the
+ * output gradient g_y of a GraphNorm(+ReLU+Dropout) over S = N / seg_rows
+ * stacked segments (the critic engine's dX products, vgan/critic.py); the
+ * epilogue also forms that backward's column partials -- sum gz and
+ * sum gz * xhat, gz = g_y [z > 0] keep -- per 64-row tile and segment slot
+ * into tpart (vg_gemm_gn_tpart_floats(N, M) floats), from gn_x / keep
+ * [N, M] (keep nullable), stats [S][2M] and the GraphNorm parameters.  This
+ * replaces vg_graphnorm_bwd_seg's partial pass (one launch and its re-read of
+ * g_y).  seg_rows >= 64 and N a multiple of it (VG_EINVAL otherwise). */
+int64_t vg_gemm_gn_tpart_floats(int32_t rows, int32_t channels);
+int vg_gemm_gn_bwd(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N, int32_t M,
+                   int32_t K, float* C, int32_t ldc, const float* gn_x, const float* keep,
+                   int32_t seg_rows, const float* weight, const float* bias, const float* mean_scale,
+                   float eps, const float* stats, float* tpart, void* stream);
+int vg_gemm_gn_bwd_bf16(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N,
+                        int32_t M, int32_t K, float* C, int32_t ldc, const float* gn_x,
+                        const float* keep, int32_t seg_rows, const float* weight,
+                        const float* bias, const float* mean_scale, float eps, const float* stats,
+                        float* tpart, void* stream);
+
+/* vg_graphnorm_bwd_seg from the partials vg_gemm_gn_bwd left in tpart (its
+ * fold and apply passes only); N = seg_rows >= 64. */
+int vg_graphnorm_bwd_seg_tiles(const float* x, int32_t S, int32_t N, int32_t C, const float* weight,
+                               const float* bias, const float* mean_scale, const float* keep,
+                               float eps, const float* stats, const float* g_y, const float* tpart,
+                               float* g_x, float* g_w, float* g_b, float* g_ms, int32_t accumulate,
+                               const float* inj, int64_t inj_offset, float* ws, void* stream);
+
 /* ---- bf16 training (BASELINE.json configs[2]) ---------------------------- */
 
 /* The dense products of the training step with bf16 operands: the same

@@ -13,7 +13,7 @@ import torch
 import critic_ref as CR
 from oracle import pyg
 from oracle import reference as R
-from parity_util import grads_close
+from parity_util import grads_close, rel_err
 from vgan import ops, synth
 from vgan._lib import LIB, check, ptr, stream_handle, sync_counter
 from vgan.config import Configuration
@@ -381,9 +381,10 @@ def test_engine_matches_autograd_path_on_gpu(cuda):
 @pytest.mark.parametrize("precision", ["f32", "bf16"])
 def test_grouped_weight_gradients_bit_identical(cuda, precision, monkeypatch):
     """The weight-gradient products of a backward run as ONE vg_gemm_tn_group
-    launch at its end (FoldCollector.tn) instead of one launch per layer: the
-    same tiles and chunks, so the critic engine's D gradient and the
-    generator backward's G gradient are bit-identical either way."""
+    launch at its end (FoldCollector.tn) instead of one launch per layer.  The
+    grouped plan splits each product over fewer row chunks (192 instead of
+    768 workgroups), so the f32 sums differ only in order: the critic loss is
+    identical and the D and G gradients agree to 1e-6 relative."""
     from vgan import _lib, ops
     from vgan._lib import gemm_precision_scope
     from vgan.models import VoxelGNNGenerator
@@ -410,5 +411,28 @@ def test_grouped_weight_gradients_bit_identical(cuda, precision, monkeypatch):
         torch.cuda.synchronize()
         out[grouped] = (loss.item(), flat.grad.clone(), flat_g.grad.clone())
     assert out[True][0] == out[False][0]
-    assert torch.equal(out[True][1], out[False][1])
-    assert torch.equal(out[True][2], out[False][2])
+    assert rel_err(out[True][1], out[False][1]) < 1e-6
+    assert rel_err(out[True][2], out[False][2]) < 1e-6
+
+
+@pytest.mark.parametrize("training", [True, False])
+def test_gemm_fused_graphnorm_backward_partials(cuda, training, monkeypatch):
+    """The critic engine's GraphNorm backward with its column partials formed
+    in the epilogue of the GEMM that produces g_y (vg_gemm_gn_bwd + the tile
+    fold) against the separate partial pass: the same sums in another order,
+    so loss and D gradient agree to f32 rounding."""
+    from vgan import critic as vcritic
+
+    cfg, D, flat, loc, vox, prep, hard, soft, eng = _engine_setup(cuda, numbers=(5, 6, 7), seed=8)
+    D.train(training)
+    hd, sd = hard.to(cuda).unsqueeze(0), soft.to(cuda).unsqueeze(0)
+    out = {}
+    for fuse in (True, False):
+        monkeypatch.setattr(vcritic, "_GN_FUSE", fuse)
+        flat.zero_grad()
+        loss = eng.loss_and_grad(loc, vox, hd, sd, _RecRNG(21))
+        torch.cuda.synchronize()
+        out[fuse] = (loss.item(), flat.grad.clone())
+    assert vox.num_nodes >= 64
+    assert abs(out[True][0] - out[False][0]) <= 1e-6 * max(1.0, abs(out[False][0]))
+    assert rel_err(out[True][1], out[False][1]) < 1e-5

@@ -9,6 +9,8 @@ usage: prof_summary.py TRACE.csv [TOP] [--after-gap] [--steps K]
   --gaps       also report the idle gaps between consecutive dispatches of
                the kept region: total per size bucket and the largest ones
                with the kernels on either side
+  --seq PAT    per-launch durations, in order, of the kernels whose name
+               contains PAT (the first step's)
 """
 import csv
 import sys
@@ -66,5 +68,10 @@ if "--gaps" in sys.argv:
                                               for _, b in buckets))
     for g, a, b in sorted(big, reverse=True)[:12]:
         print(f"  gap {g:8.1f} us  {a} -> {b}")
+if "--seq" in sys.argv:  # per-launch durations (in order) of kernels whose name contains the pattern
+    pat = sys.argv[sys.argv.index("--seq") + 1]
+    seq = [(e - s) / 1e3 for s, e, name in rows if pat in name]
+    per = len(seq) // steps if steps else len(seq)
+    print(f"{pat}: {len(seq)} launches; first step: " + " ".join(f"{v:.1f}" for v in seq[:per]))
 for name, (n, us) in sorted(tot.items(), key=lambda kv: -kv[1][1])[:top]:
     print(f"{us / 1e3:9.3f} ms {n:7d} x {us / n:8.2f} us  {name[:110]}")
