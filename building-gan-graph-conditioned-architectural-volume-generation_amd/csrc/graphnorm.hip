@@ -363,31 +363,56 @@ __global__ void __launch_bounds__(kBlock) k_gn_bwd_final_tiles(
     const float* __restrict__ tpart, int N, int C, int S, const float* __restrict__ w,
     const float* __restrict__ ms, float eps, const float* __restrict__ stats, float* __restrict__ sums,
     float* __restrict__ g_w, float* __restrict__ g_b, float* __restrict__ g_ms, int accumulate) {
-  constexpr int kTile = 64;
+  constexpr int kTile = 64, kSegs = 4, kU = 4;  // segments in flight together, tiles per lane and segment
   const int c = fold_col(), lane = threadIdx.x & 63;
   if (c >= C) return;
   float tw = 0.f, tb = 0.f, tm = 0.f;
-  for (int sg = 0; sg < S; ++sg) {
-    const long long r0 = (long long)sg * N, r1 = r0 + N - 1;
-    const int t0 = static_cast<int>(r0 / kTile), t1 = static_cast<int>(r1 / kTile);
-    float a = 0.f, bb = 0.f;
-#pragma unroll 4
-    for (int t = t0 + lane; t <= t1; t += 64) {
-      const int slot = (long long)t * kTile >= r0 ? 0 : 1;  // first row in sg, or in sg - 1
-      const float* p = tpart + ((size_t)(2 * t + slot) * C + c) * 2;
-      a += p[0];
-      bb += p[1];
+  for (int s0 = 0; s0 < S; s0 += kSegs) {
+    float va[kSegs][kU], vb[kSegs][kU];
+    int t0[kSegs], t1[kSegs];
+#pragma unroll
+    for (int j = 0; j < kSegs; ++j) {
+      const long long r0 = (long long)(s0 + j) * N;
+      t0[j] = static_cast<int>(r0 / kTile);
+      t1[j] = static_cast<int>((r0 + N - 1) / kTile);
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int t = t0[j] + lane + 64 * u;
+        const bool ok = s0 + j < S && t <= t1[j];
+        const int slot = (long long)t * kTile >= r0 ? 0 : 1;  // first row in this segment, or in the previous one
+        const float* p = tpart + ((size_t)(2 * t + slot) * C + c) * 2;
+        va[j][u] = ok ? p[0] : 0.f;
+        vb[j][u] = ok ? p[1] : 0.f;
+      }
     }
-    a = wave_sum(a);
-    bb = wave_sum(bb);
-    const float* st = stats + (size_t)sg * 2 * C;
-    if (lane == 0) {
-      sums[(size_t)sg * 2 * C + c] = a;
-      sums[(size_t)sg * 2 * C + C + c] = bb;
+#pragma unroll
+    for (int j = 0; j < kSegs; ++j) {
+      const int sg = s0 + j;
+      if (sg >= S) break;
+      float a = 0.f, bb = 0.f;
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        a += va[j][u];
+        bb += vb[j][u];
+      }
+      const long long r0 = (long long)sg * N;
+      for (int t = t0[j] + lane + 64 * kU; t <= t1[j]; t += 64) {  // segments of more than 16k rows
+        const int slot = (long long)t * kTile >= r0 ? 0 : 1;
+        const float* p = tpart + ((size_t)(2 * t + slot) * C + c) * 2;
+        a += p[0];
+        bb += p[1];
+      }
+      a = wave_sum(a);
+      bb = wave_sum(bb);
+      const float* st = stats + (size_t)sg * 2 * C;
+      if (lane == 0) {
+        sums[(size_t)sg * 2 * C + c] = a;
+        sums[(size_t)sg * 2 * C + C + c] = bb;
+      }
+      tw += bb;
+      tb += a;
+      tm += -st[c] * w[c] * a / (st[C + c] + eps);
     }
-    tw += bb;
-    tb += a;
-    tm += -st[c] * w[c] * a / (st[C + c] + eps);
   }
   if (lane == 0 && g_w) {
     g_w[c] = accumulate ? g_w[c] + tw : tw;

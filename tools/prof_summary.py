@@ -68,6 +68,24 @@ if "--gaps" in sys.argv:
                                               for _, b in buckets))
     for g, a, b in sorted(big, reverse=True)[:12]:
         print(f"  gap {g:8.1f} us  {a} -> {b}")
+if "--dump-step" in sys.argv and steps:  # the first timed step's kernels in order, runs of one name folded
+    import re
+
+    per = len(rows) // steps
+    out, prev, cnt, t = [], None, 0, 0.0
+    for s_, e_, name in rows[:per] + [(0, 0, None)]:
+        m = re.search(r"::(k_\w+)", name) if name else None
+        short = (m.group(1) if m else name[:60]) if name else None
+        if short == prev:
+            cnt += 1
+            t += (e_ - s_) / 1e3
+            continue
+        if prev is not None:
+            out.append(f"{prev} x{cnt} {t:.1f}us" if cnt > 1 else f"{prev} {t:.1f}us")
+        prev, cnt, t = short, 1, (e_ - s_) / 1e3
+    print("first step, in order:")
+    for line in out:
+        print("   ", line)
 if "--seq" in sys.argv:  # per-launch durations (in order) of kernels whose name contains the pattern
     pat = sys.argv[sys.argv.index("--seq") + 1]
     seq = [(e - s) / 1e3 for s, e, name in rows if pat in name]
