@@ -124,12 +124,14 @@ def aggregate_roofline(tr, csr, device, reps: int = 20):
 def load_pmc_traffic():
     """Per-launch HBM-side bytes of the scatter kernel from the committed
     rocprofv3 PMC summary (tools/pmc_roofline.sh), or None."""
-    path = os.path.join(ROOT, "profiles", "r01_pmc_aggregate.json")
+    path = os.path.join(ROOT, "profiles", "r02_pmc_aggregate.json")
+    if not os.path.exists(path):
+        path = os.path.join(ROOT, "profiles", "r01_pmc_aggregate.json")
     if not os.path.exists(path):
         return None, None
     with open(path) as f:
         d = json.load(f)
-    return d.get("traffic_bytes_per_launch"), "profiles/r01_pmc_aggregate.json"
+    return d.get("traffic_bytes_per_launch"), os.path.relpath(path, ROOT)
 
 
 def make_pool(cfg, rank: int, world: int, pool: int, batch: int, device):
