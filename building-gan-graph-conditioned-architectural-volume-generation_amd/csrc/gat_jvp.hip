@@ -145,9 +145,11 @@ __global__ void __launch_bounds__(kBlock) k_jvp_rows(
   block_partials<L, CPL>(&pd, 1, C, part);
 }
 
+// The source pass as a block body: logical block lb of nb (one launch of
+// k_jvp_src, or one item of a grouped launch).
 template <int L, int CPL, bool VEC>
-__global__ void __launch_bounds__(kBlock) k_jvp_src(
-    const int32_t* __restrict__ csc_ptr, const int32_t* __restrict__ csc_slot,
+__device__ __forceinline__ void jvp_src_body(
+    int lb, int nb, const int32_t* __restrict__ csc_ptr, const int32_t* __restrict__ csc_slot,
     const int32_t* __restrict__ csc_dst, int N, int C, const float* __restrict__ h,
     const float* __restrict__ u, const float* __restrict__ gv, const float* __restrict__ att_s,
     const float* __restrict__ att_d, const float* __restrict__ e_gz,
@@ -161,8 +163,7 @@ __global__ void __launch_bounds__(kBlock) k_jvp_src(
   load_row<CPL, false>(vd, att_d, c0, C);
 #pragma unroll
   for (int q = 0; q < CPL; ++q) ps.v[q] = 0.f;
-  const int lb = xcd_remap(blockIdx.x, gridDim.x);
-  for (int j = lb * G + grp; j < N; j += gridDim.x * G) {
+  for (int j = lb * G + grp; j < N; j += nb * G) {
     const int beg = csc_ptr[j], end = csc_ptr[j + 1];
     float gas = 0.f, gps = 0.f;
     for (int p = beg + lane; p < end; p += L) {
@@ -203,7 +204,59 @@ __global__ void __launch_bounds__(kBlock) k_jvp_src(
     }
     store_row<CPL, VEC>(acc, h_inj + (size_t)j * C, c0, C);
   }
-  block_partials<L, CPL>(&ps, 1, C, part);
+  block_partials<L, CPL>(&ps, 1, C, part, lb);
+}
+
+template <int L, int CPL, bool VEC>
+__global__ void __launch_bounds__(kBlock) k_jvp_src(
+    const int32_t* __restrict__ csc_ptr, const int32_t* __restrict__ csc_slot,
+    const int32_t* __restrict__ csc_dst, int N, int C, const float* __restrict__ h,
+    const float* __restrict__ u, const float* __restrict__ gv, const float* __restrict__ att_s,
+    const float* __restrict__ att_d, const float* __restrict__ e_gz,
+    const float* __restrict__ e_gzp, const float* __restrict__ e_alp,
+    const float* __restrict__ n_gad, float* __restrict__ h_inj, float* __restrict__ part) {
+  jvp_src_body<L, CPL, VEC>(xcd_remap(blockIdx.x, gridDim.x), gridDim.x, csc_ptr, csc_slot, csc_dst, N, C, h, u, gv,
+                            att_s, att_d, e_gz, e_gzp, e_alp, n_gad, h_inj, part);
+}
+
+// Grouped source passes (vg_gat_jvp_src_group): the tangent sweep's dQ/dh
+// injections and att_src partials are read only by the later VJP pass and the
+// gradient folds, so the critic engine runs every layer's source pass in one
+// launch at the end of the sweep.  Blocks [block0[i], block0[i+1]) are item
+// i's; shape ids (VEC layouts only): 0 = L8 x 1 (C <= 8), 1 = L8 x 2,
+// 2 = L8 x 4, 3 = L16 x 4, 4 = L16 x 8, 5 = L32 x 8.
+struct JvpSrcGroup {
+  vg_jvp_src d[VG_JVP_GROUP_MAX];
+  int block0[VG_JVP_GROUP_MAX + 1];
+  int n;
+};
+
+__global__ void __launch_bounds__(kBlock) k_jvp_src_group(const JvpSrcGroup g) {
+  const int lbg = xcd_remap(blockIdx.x, gridDim.x);
+  int i = 0;
+  while (i + 1 < g.n && lbg >= g.block0[i + 1]) ++i;
+  const vg_jvp_src& d = g.d[i];
+  const int lb = lbg - g.block0[i], nb = g.block0[i + 1] - g.block0[i];
+#define VG_JS(L_, CPL_)                                                                                   \
+  jvp_src_body<L_, CPL_, true>(lb, nb, d.csc_ptr, d.csc_slot, d.csc_dst, d.N, d.C, d.h, d.u, d.g_out,      \
+                               d.att_src, d.att_dst, d.e_gz, d.e_gzp, d.e_alp, d.n_gad, d.h_inj, d.part)
+  switch (d.shape) {
+    case 0: VG_JS(8, 1); break;
+    case 1: VG_JS(8, 2); break;
+    case 2: VG_JS(8, 4); break;
+    case 3: VG_JS(16, 4); break;
+    case 4: VG_JS(16, 8); break;
+    default: VG_JS(32, 8); break;
+  }
+#undef VG_JS
+}
+
+inline int jvp_shape_id(int C, const Shape& sh) {
+  if (C <= 8) return 0;
+  if (!sh.vec) return -1;
+  if (sh.L == 8) return sh.CPL == 2 ? 1 : 2;
+  if (sh.L == 16) return sh.CPL == 4 ? 3 : 4;
+  return 5;
 }
 
 // g_a[c] += sum_b part_a[b][c] (blockIdx.y == 0), g_b[c] += sum_b part_b[b][c] (== 1)
@@ -289,6 +342,13 @@ extern "C" int vg_gat_jvp2_ex(const int32_t* row_ptr, const int32_t* col, const 
 
 // folds_out == NULL: fold immediately (vg_gat_jvp2_ex); else describe the two
 // accumulating folds for vg_fold_batch.
+static int jvp2(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr, const int32_t* csc_slot,
+                const int32_t* csc_dst, int32_t N, int32_t E, int32_t C, const float* h, const float* u,
+                const float* g_out, const float* att_src, const float* att_dst, const float* a_src,
+                const float* a_dst, const float* alpha, float slope, float* u_out, float* h_inj,
+                float* g_att_src, float* g_att_dst, const float* up_src_in, const float* up_dst_in,
+                float* workspace, vg_fold* folds_out, int32_t* n_out, vg_jvp_src* src_out, void* stream);
+
 extern "C" int vg_gat_jvp2_deferred(const int32_t* row_ptr, const int32_t* col,
                                     const int32_t* csc_ptr, const int32_t* csc_slot,
                                     const int32_t* csc_dst, int32_t N, int32_t E, int32_t C,
@@ -299,6 +359,52 @@ extern "C" int vg_gat_jvp2_deferred(const int32_t* row_ptr, const int32_t* col,
                                     const float* up_src_in, const float* up_dst_in,
                                     float* workspace, vg_fold* folds_out, int32_t* n_out,
                                     void* stream) {
+  return jvp2(row_ptr, col, csc_ptr, csc_slot, csc_dst, N, E, C, h, u, g_out, att_src, att_dst, a_src, a_dst,
+              alpha, slope, u_out, h_inj, g_att_src, g_att_dst, up_src_in, up_dst_in, workspace, folds_out, n_out,
+              nullptr, stream);
+}
+
+extern "C" int vg_gat_jvp2_plan(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,
+                                const int32_t* csc_slot, const int32_t* csc_dst, int32_t N, int32_t E, int32_t C,
+                                const float* h, const float* u, const float* g_out, const float* att_src,
+                                const float* att_dst, const float* a_src, const float* a_dst, const float* alpha,
+                                float slope, float* u_out, float* h_inj, float* g_att_src, float* g_att_dst,
+                                const float* up_src_in, const float* up_dst_in, float* workspace,
+                                vg_fold* folds_out, int32_t* n_out, vg_jvp_src* src_out, void* stream) {
+  if (!folds_out || !n_out || !src_out) return VG_EINVAL;
+  return jvp2(row_ptr, col, csc_ptr, csc_slot, csc_dst, N, E, C, h, u, g_out, att_src, att_dst, a_src, a_dst,
+              alpha, slope, u_out, h_inj, g_att_src, g_att_dst, up_src_in, up_dst_in, workspace, folds_out, n_out,
+              src_out, stream);
+}
+
+extern "C" int vg_gat_jvp_src_group(const vg_jvp_src* items, int32_t n, void* stream) {
+  if (n < 0 || n > VG_JVP_GROUP_MAX || (n > 0 && !items)) return VG_EINVAL;
+  if (n == 0) return 0;
+  JvpSrcGroup g{};
+  long long blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    const vg_jvp_src& d = items[i];
+    if (d.shape < 0 || d.shape > 5 || d.blocks <= 0 || d.blocks > kMaxBlocks || d.N <= 0 || d.C <= 0 || !d.csc_ptr ||
+        !d.csc_slot || !d.csc_dst || !d.h || !d.u || !d.g_out || !d.att_src || !d.att_dst || !d.e_gz || !d.e_gzp ||
+        !d.e_alp || !d.n_gad || !d.h_inj || !d.part)
+      return VG_EINVAL;
+    g.d[i] = d;
+    g.block0[i] = static_cast<int>(blocks);
+    blocks += d.blocks;
+  }
+  g.block0[n] = static_cast<int>(blocks);
+  g.n = n;
+  k_jvp_src_group<<<static_cast<int>(blocks), kBlock, 0, static_cast<hipStream_t>(stream)>>>(g);
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+static int jvp2(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr, const int32_t* csc_slot,
+                const int32_t* csc_dst, int32_t N, int32_t E, int32_t C, const float* h, const float* u,
+                const float* g_out, const float* att_src, const float* att_dst, const float* a_src,
+                const float* a_dst, const float* alpha, float slope, float* u_out, float* h_inj,
+                float* g_att_src, float* g_att_dst, const float* up_src_in, const float* up_dst_in,
+                float* workspace, vg_fold* folds_out, int32_t* n_out, vg_jvp_src* src_out, void* stream) {
   if ((folds_out == nullptr) != (n_out == nullptr)) return VG_EINVAL;
   if (n_out) *n_out = 0;
   Shape sh;
@@ -328,9 +434,16 @@ extern "C" int vg_gat_jvp2_deferred(const int32_t* row_ptr, const int32_t* col,
   VG_DISPATCH_JVP(C, (k_jvp_rows<L_, CPL_, V_><<<grid, kBlock, 0, s>>>(
                          row_ptr, col, N, C, h, u, g_out, a_src, a_dst, up_src, up_dst, alpha,
                          slope, u_out, e_u, e_h, e_gz, e_gzp, e_alp, n_gad, part_r)));
-  VG_DISPATCH_JVP(C, (k_jvp_src<L_, CPL_, V_><<<grid, kBlock, 0, s>>>(
-                         csc_ptr, csc_slot, csc_dst, N, C, h, u, g_out, att_src, att_dst, e_gz,
-                         e_gzp, e_alp, n_gad, h_inj, part_s)));
+  const int shape_id = jvp_shape_id(C, sh);
+  if (src_out && shape_id >= 0) {  // described for vg_gat_jvp_src_group
+    *src_out = vg_jvp_src{csc_ptr, csc_slot, csc_dst, h, u, g_out, att_src, att_dst, e_gz, e_gzp, e_alp,
+                          n_gad, h_inj, part_s, N, C, grid, shape_id};
+  } else {
+    if (src_out) src_out->shape = -1;  // ran here
+    VG_DISPATCH_JVP(C, (k_jvp_src<L_, CPL_, V_><<<grid, kBlock, 0, s>>>(
+                           csc_ptr, csc_slot, csc_dst, N, C, h, u, g_out, att_src, att_dst, e_gz,
+                           e_gzp, e_alp, n_gad, h_inj, part_s)));
+  }
   if (folds_out) {
     folds_out[0] = vg_fold{g_att_dst, C, C, C, 1, 1, {{part_r, grid, C}, {nullptr, 0, 0}}};
     folds_out[1] = vg_fold{g_att_src, C, C, C, 1, 1, {{part_s, grid, C}, {nullptr, 0, 0}}};

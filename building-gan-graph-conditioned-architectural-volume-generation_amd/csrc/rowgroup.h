@@ -170,7 +170,9 @@ inline bool pick_fused_shape(int C, Shape& sh) {
 // visits (grid-stride); the block folds its groups through LDS and writes one
 // row of `part` ([gridDim.x][W]).  W <= 3 * 256.
 template <int L, int CPL>
-__device__ void block_partials(const Vec<CPL>* vals, int nvec, int C, float* __restrict__ part) {
+__device__ void block_partials(const Vec<CPL>* vals, int nvec, int C, float* __restrict__ part,
+                               int bid = -1) {
+  if (bid < 0) bid = blockIdx.x;  // the partial row (grouped launches pass their own block index)
   constexpr int G = kBlock / L;
   __shared__ float red[kBlock * 8 * 2];  // (256/L) groups x L*CPL channels (CPL <= 8) x up to 2 vectors
   const int grp = threadIdx.x / L, lane = threadIdx.x & (L - 1);
@@ -183,7 +185,7 @@ __device__ void block_partials(const Vec<CPL>* vals, int nvec, int C, float* __r
     const int v = w / Wg, c = w % Wg;
     float s = 0.f;
     for (int k = 0; k < G; ++k) s += red[(k * nvec + v) * Wg + c];
-    if (c < C) part[(size_t)blockIdx.x * nvec * C + v * C + c] = s;
+    if (c < C) part[(size_t)bid * nvec * C + v * C + c] = s;
   }
 }
 

@@ -47,6 +47,20 @@ VG_TN_GROUP_MAX = 32
 _TN_GROUP = os.environ.get("VGAN_TN_GROUP", "1") == "1"
 
 
+class VgJvpSrc(ctypes.Structure):
+    """vg_jvp_src (include/vgan.h): one described source pass of vg_gat_jvp2."""
+    _fields_ = [(k, _c_p) for k in ("csc_ptr", "csc_slot", "csc_dst", "h", "u", "g_out", "att_src", "att_dst",
+                                     "e_gz", "e_gzp", "e_alp", "n_gad", "h_inj", "part")] + \
+               [("N", _c_i32), ("C", _c_i32), ("blocks", _c_i32), ("shape", _c_i32)]
+
+
+VG_JVP_GROUP_MAX = 16
+# VGAN_JVP_GROUP=1: the tangent sweep's source passes as one grouped launch
+# before pass D.  Off: measured 0.07 ms per step slower than one launch per
+# block right after its destination-row pass (DESIGN.md 4.9)
+_JVP_GROUP = os.environ.get("VGAN_JVP_GROUP", "0") == "1"
+
+
 class VgASrc(ctypes.Structure):
     """vg_asrc (include/vgan.h): one column block of vg_gemm_ln_act_ms's A."""
     _fields_ = [("ptr", _c_p), ("ld", _c_i32), ("cols", _c_i32), ("w_col0", _c_i32), ("rows_mod", _c_i32)]
@@ -57,6 +71,8 @@ SIGNATURES = {
     "vg_gemm_tn_plan": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_i32, _c_p,
                                        _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p]),
     "vg_gemm_tn_group": (ctypes.c_int, [_c_p, _c_i32, _c_p]),
+    "vg_gat_jvp2_plan": (ctypes.c_int, [_c_p] * 5 + [_c_i32] * 3 + [_c_p] * 8 + [_c_f32] + [_c_p] * 7 + [_c_p] * 4),
+    "vg_gat_jvp_src_group": (ctypes.c_int, [_c_p, _c_i32, _c_p]),
     "vg_gemm_gn_tpart_floats": (_c_i64, [_c_i32, _c_i32]),
     "vg_gemm_gn_bwd": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p,
                                       _c_i32, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p]),
@@ -281,6 +297,7 @@ class FoldCollector:
         self.folds = []
         self.keep = []
         self.products = []
+        self.jvp_src = []
 
     def call(self, fn, args_before_stream, stream, keep=(), name="deferred"):
         arr = (VgFold * 3)()
@@ -308,7 +325,34 @@ class FoldCollector:
             self.folds.append(VgFold.from_buffer_copy(arr[i]))
         self.keep.extend(keep)
 
+    def jvp(self, args_before_outputs, stream, keep=()):
+        """vg_gat_jvp2 with its folds deferred and its source pass (dQ/dh
+        injections) described for ONE grouped launch by run_jvp_src();
+        ``keep`` holds h, u, g_out and the workspace until then."""
+        arr = (VgFold * 2)()
+        n = ctypes.c_int32(0)
+        if not _JVP_GROUP:
+            check(LIB.vg_gat_jvp2_deferred(*args_before_outputs, arr, ctypes.byref(n), stream), "vg_gat_jvp2_deferred")
+        else:
+            src = VgJvpSrc()
+            check(LIB.vg_gat_jvp2_plan(*args_before_outputs, arr, ctypes.byref(n), ctypes.byref(src), stream),
+                  "vg_gat_jvp2_plan")
+            if src.shape >= 0:
+                self.jvp_src.append(src)
+        for i in range(n.value):
+            self.folds.append(VgFold.from_buffer_copy(arr[i]))
+        self.keep.extend(keep)
+
+    def run_jvp_src(self, stream) -> None:
+        """The described source passes, in one launch per VG_JVP_GROUP_MAX."""
+        for i in range(0, len(self.jvp_src), VG_JVP_GROUP_MAX):
+            part = self.jvp_src[i:i + VG_JVP_GROUP_MAX]
+            arr = (VgJvpSrc * len(part))(*part)
+            check(LIB.vg_gat_jvp_src_group(arr, len(part), stream), "vg_gat_jvp_src_group")
+        self.jvp_src = []
+
     def flush(self, stream) -> None:
+        self.run_jvp_src(stream)  # (their att_src partials feed folds)
         # the grouped products first: their partials feed the folds
         for bf in (0, 1):
             prods = [p for p in self.products if p.bf16 == bf]

@@ -327,13 +327,12 @@ class CriticEngine:
                                      ptr(conv.att_dst), ptr(uH), ptr(up_s), ptr(up_d), st), "vg_gat_lin_att")
             uO, hinj = _f(n, c, dev=dev), _f(n, c, dev=dev)
             ws = _f(int(LIB.vg_gat_jvp2_ws_floats(n, E, c)), dev=dev)
-            folds.call(LIB.vg_gat_jvp2_deferred,
-                       (ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot), ptr(csr.csc_dst), n, E,
-                        c, rows(B["H"], mrow, c), ptr(uH), ptr(dO_b[b]), ptr(conv.att_src), ptr(conv.att_dst),
-                        _off(B["a_s"], mrow), _off(B["a_d"], mrow), _off(B["alpha"], 2 * E),
-                        float(conv.negative_slope), ptr(uO), ptr(hinj), ptr(conv.att_src.grad),
-                        ptr(conv.att_dst.grad), ptr(up_s), ptr(up_d), ptr(ws)), st, keep=(ws,),
-                       name="vg_gat_jvp2_deferred")
+            # the source pass (hinj, read in pass D) joins one grouped launch after the sweep
+            folds.jvp((ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot), ptr(csr.csc_dst), n, E,
+                       c, rows(B["H"], mrow, c), ptr(uH), ptr(dO_b[b]), ptr(conv.att_src), ptr(conv.att_dst),
+                       _off(B["a_s"], mrow), _off(B["a_d"], mrow), _off(B["alpha"], 2 * E),
+                       float(conv.negative_slope), ptr(uO), ptr(hinj), ptr(conv.att_src.grad),
+                       ptr(conv.att_dst.grad), ptr(up_s), ptr(up_d), ptr(ws)), st, keep=(ws, uH))
             oinj = _f(n, c, dev=dev)
             ws = _f(int(LIB.vg_graphnorm_seg_ws_floats(1, n, c)), dev=dev)
             check(LIB.vg_graphnorm_jvp2(rows(B["O"], mrow, c), n, c, ptr(norm.weight), ptr(norm.bias),
@@ -349,6 +348,8 @@ class CriticEngine:
             self._gemm(st, u_in, uw, ptr(lin.weight), uw, 1, rows(dec_out[i], trow, o), o, n, o, uw, None, ACT_MASK,
                        rows(dec_out[i], mrow, o), o)
             u_in, uw = rows(dec_out[i], trow, o), o
+
+        folds.run_jvp_src(st)  # every block's dQ/dh injection, one launch
 
         # ---------------------------------------------------------- pass D
         # weight gradients over 4N rows: [pass-D adjoint ; pass-B adjoint]^T [activation ; tangent]

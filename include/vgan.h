@@ -479,6 +479,49 @@ int vg_gat_jvp2_deferred(const int32_t* row_ptr, const int32_t* col, const int32
                          const float* up_src, const float* up_dst, float* workspace,
                          vg_fold* folds_out, int32_t* n_out, void* stream);
 
+/* The source-node pass of vg_gat_jvp2 (dQ/dh injections h_inj and the
+ * att_src partials), described for a grouped launch.  shape: the pass's lane
+ * layout (0-5), or -1 when vg_gat_jvp2_plan ran it already (non-vector
+ * layouts). */
+typedef struct {
+  const int32_t* csc_ptr;
+  const int32_t* csc_slot;
+  const int32_t* csc_dst;
+  const float* h;
+  const float* u;
+  const float* g_out;
+  const float* att_src;
+  const float* att_dst;
+  const float* e_gz;
+  const float* e_gzp;
+  const float* e_alp;
+  const float* n_gad;
+  float* h_inj;
+  float* part;
+  int32_t N, C, blocks, shape;
+} vg_jvp_src;
+
+#define VG_JVP_GROUP_MAX 16
+
+/* vg_gat_jvp2_deferred that launches only the destination-row pass: the
+ * source pass goes to *src_out for vg_gat_jvp_src_group.  The tangent sweep
+ * of the critic engine (trainer.py:306-316's double backward) reads h_inj only
+ * in its later VJP pass, so the engine runs every layer's source pass in one
+ * launch at the end of the sweep.  The caller keeps h, u, g_out and the
+ * workspace alive and unmodified until then. */
+int vg_gat_jvp2_plan(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,
+                     const int32_t* csc_slot, const int32_t* csc_dst, int32_t num_nodes,
+                     int32_t num_edges, int32_t channels, const float* h, const float* u,
+                     const float* g_out, const float* att_src, const float* att_dst,
+                     const float* a_src, const float* a_dst, const float* alpha, float slope,
+                     float* u_out, float* h_inj, float* g_att_src, float* g_att_dst,
+                     const float* up_src, const float* up_dst, float* workspace,
+                     vg_fold* folds_out, int32_t* n_out, vg_jvp_src* src_out, void* stream);
+
+/* Run up to VG_JVP_GROUP_MAX described source passes (a HOST array, by value)
+ * in one launch; items with shape -1 are skipped by the caller. */
+int vg_gat_jvp_src_group(const vg_jvp_src* items, int32_t n, void* stream);
+
 /* ---- device RNG ------------------------------------------------------------ */
 
 /* n draws into out: kind 0 standard normal (Box-Muller), 1 uniform [0, 1),

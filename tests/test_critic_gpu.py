@@ -436,3 +436,23 @@ def test_gemm_fused_graphnorm_backward_partials(cuda, training, monkeypatch):
     assert vox.num_nodes >= 64
     assert abs(out[True][0] - out[False][0]) <= 1e-6 * max(1.0, abs(out[False][0]))
     assert rel_err(out[True][1], out[False][1]) < 1e-5
+
+
+def test_grouped_jvp_source_passes_bit_identical(cuda, monkeypatch):
+    """The tangent sweep's source passes (dQ/dh injections, att_src partials)
+    run as one vg_gat_jvp_src_group launch before pass D instead of one
+    launch per block: the same block bodies and partial rows, so the loss and
+    the D gradient are bit-identical."""
+    from vgan import _lib
+
+    cfg, D, flat, loc, vox, prep, hard, soft, eng = _engine_setup(cuda, numbers=(5, 6), seed=12)
+    hd, sd = hard.to(cuda).unsqueeze(0), soft.to(cuda).unsqueeze(0)
+    out = {}
+    for grouped in (True, False):
+        monkeypatch.setattr(_lib, "_JVP_GROUP", grouped)
+        flat.zero_grad()
+        loss = eng.loss_and_grad(loc, vox, hd, sd, _RecRNG(5))
+        torch.cuda.synchronize()
+        out[grouped] = (loss.item(), flat.grad.clone())
+    assert out[True][0] == out[False][0]
+    assert torch.equal(out[True][1], out[False][1])
