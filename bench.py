@@ -201,7 +201,9 @@ def timed_steps(tr, pool, steps: int, warmup: int, world: int, device, profile: 
 
 
 def stress_roofline(device, channels=(128, 64, 1), reps: int = 20):
-    """vg_gat_aggregate_fwd on config #4 (8 x 50k-node buildings), cold MALL."""
+    """vg_gat_aggregate_fwd on config #4 (8 x 50k-node buildings), cold MALL;
+    for C a multiple of 64 also vg_gat_aggregate_fwd_lds (the tile plan's
+    distinct source rows staged through LDS, bit-identical output)."""
     from vgan import ops
     from vgan._lib import LIB, check, ptr, stream_handle
     from vgan.synth import make_stress_building
@@ -211,8 +213,13 @@ def stress_roofline(device, channels=(128, 64, 1), reps: int = 20):
     vox = GraphBatch.from_data_list([v for _, v in items]).to(device)
     csr = ops.CSR(vox.edge_index, vox.num_nodes)
     n, e = csr.num_nodes, csr.num_edges
+    plan = csr.tile_plan()
+    tiles = (n + 15) // 16
+    uniq = plan[:tiles].clamp_min(0).sum().item()
+    log(f"tile plan: {uniq / tiles:.1f} distinct sources for {e / tiles:.1f} edges per tile, "
+        f"largest {csr._tile_umax}, unplanned tiles {int((plan[:tiles] < 0).sum().item())}")
     scratch = torch.empty(512 * 1024 * 1024 // 4, device=device)  # flush the 256 MB MALL between reps
-    res = {}
+    res, res_lds = {}, {}
     for c in channels:
         h = torch.randn(n, c, device=device)
         a_s, a_d = 0.3 * torch.randn(n, device=device), 0.3 * torch.randn(n, device=device)
@@ -224,22 +231,35 @@ def stress_roofline(device, channels=(128, 64, 1), reps: int = 20):
                                            ptr(bias), 0.2, ptr(out), ptr(alpha), stream_handle(device)),
                   "vg_gat_aggregate_fwd")
 
-        for _ in range(3):
-            run()
-        times = []
-        for _ in range(reps):
-            scratch.fill_(1.0)
-            st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            st.record()
-            run()
-            en.record()
-            torch.cuda.synchronize()
-            times.append(st.elapsed_time(en))
-        avg = sum(times) / len(times)
+        def run_lds():
+            check(LIB.vg_gat_aggregate_fwd_lds(ptr(csr.row_ptr), ptr(csr.col), n, c, ptr(h), ptr(a_s), ptr(a_d),
+                                               ptr(bias), 0.2, ptr(out), ptr(alpha), ptr(plan), csr._tile_umax,
+                                               stream_handle(device)),
+                  "vg_gat_aggregate_fwd_lds")
+
+        def timed(fn):
+            for _ in range(3):
+                fn()
+            times = []
+            for _ in range(reps):
+                scratch.fill_(1.0)
+                st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                st.record()
+                fn()
+                en.record()
+                torch.cuda.synchronize()
+                times.append(st.elapsed_time(en))
+            return sum(times) / len(times)
+
         b = agg_bytes(n, e, c)
+        avg = timed(run)
         res[c] = {"avg_us": avg * 1e3, "bytes": b, "achieved_gbs": b / (avg * 1e-3) / 1e9}
+        if c % 64 == 0:
+            avg = timed(run_lds)
+            res_lds[c] = {"avg_us": avg * 1e3, "bytes": b, "achieved_gbs": b / (avg * 1e-3) / 1e9}
     del scratch
-    return {"nodes": n, "edges": e, "per_channels": res}
+    return {"nodes": n, "edges": e, "per_channels": res, "per_channels_lds": res_lds,
+            "distinct_sources_per_tile": round(uniq / tiles, 1), "edges_per_tile": round(e / tiles, 1)}
 
 
 def cpu_baseline(cfg_batch: int, seconds_budget: float):
@@ -400,6 +420,8 @@ def main():
         if stress:
             for c, r in stress["per_channels"].items():
                 log(f"stress C={c}: {r['avg_us']:.1f} us, {r['achieved_gbs']:.0f} GB/s")
+            for c, r in stress["per_channels_lds"].items():
+                log(f"stress C={c} (LDS-staged): {r['avg_us']:.1f} us, {r['achieved_gbs']:.0f} GB/s")
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args.batch, args.cpu_seconds)
@@ -449,14 +471,27 @@ def main():
         if bf16:
             result["bf16"] = bf16
         if stress:
-            c128 = stress["per_channels"][128]
+            # configs[3]: the faster of the two large-graph aggregations -- the
+            # register gather (k_gat_fwd_cp) or the LDS-staged tile plan
+            # (k_gat_fwd_lds); both are reported, DESIGN.md 4.10 explains the pick
+            reg, lds = stress["per_channels"][128], stress["per_channels_lds"].get(128)
+            use_lds = lds is not None and lds["avg_us"] < reg["avg_us"]
+            c128 = lds if use_lds else reg
+            kname = ("vg_gat_aggregate_fwd_lds (tile plan: each 16-row tile's distinct source rows staged "
+                     "through LDS)" if use_lds else
+                     "vg_gat_aggregate_fwd (register gather: 16-lane rows, 4 source rows in flight per lane group)")
             result["roofline_stress"] = {
                 "workload": f"configs[3]: 8 x 50k-node buildings, N={stress['nodes']}, E'={stress['edges']}, "
                             "C=128 fp32, cold MALL",
+                "kernel": kname,
+                "tile_plan": f"{stress['distinct_sources_per_tile']} distinct source rows for "
+                             f"{stress['edges_per_tile']} edges per 16-row tile",
                 "bound": "hbm", "achieved": round(c128["achieved_gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(c128["achieved_gbs"] / HBM_PEAK_GBS, 4), "avg_launch_us": round(c128["avg_us"], 2),
-                "per_channels": {str(c): {k: round(v, 2) for k, v in r.items()}
-                                 for c, r in stress["per_channels"].items()},
+                "per_channels_register_gather": {str(c): {k: round(v, 2) for k, v in r.items()}
+                                                 for c, r in stress["per_channels"].items()},
+                "per_channels_lds": {str(c): {k: round(v, 2) for k, v in r.items()}
+                                     for c, r in stress["per_channels_lds"].items()},
             }
     if world > 1:
         dist.barrier()

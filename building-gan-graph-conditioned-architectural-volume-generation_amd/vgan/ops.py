@@ -111,6 +111,41 @@ class CSR:
         cache[copies] = out
         return out
 
+    def tile_plan(self) -> torch.Tensor:
+        """The LDS tile plan of this graph (vg_gat_tile_plan: per 16-row tile
+        the distinct sources and every edge's slot among them), built once and
+        cached; consumed by aggregate_lds."""
+        plan = self.__dict__.get("_tile_plan")
+        if plan is None:
+            n_ints = int(LIB.vg_gat_tile_plan_ints(self.num_nodes, self.num_edges))
+            plan = torch.empty(n_ints, dtype=torch.int32, device=self.device)
+            check(LIB.vg_gat_tile_plan(ptr(self.row_ptr), ptr(self.col), self.num_nodes, self.num_edges, ptr(plan),
+                                       self.stream()), "vg_gat_tile_plan")
+            tiles = (self.num_nodes + 15) // 16
+            # the LDS image is sized to the largest tile (one host sync, once per graph)
+            self._tile_umax = max(1, int(plan[:tiles].max().item()))
+            self._tile_plan = plan
+        return plan
+
+
+def aggregate_lds(csr: "CSR", h: torch.Tensor, a_src: torch.Tensor, a_dst: torch.Tensor, bias: torch.Tensor,
+                  slope: float = 0.2):
+    """(out, alpha) of vg_gat_aggregate_fwd_lds: GATConv's edge softmax and
+    gather-sum with every 16-row tile's distinct source rows staged in LDS
+    (large graphs; C a multiple of 64).  Bit-identical to the register-gather
+    kernel."""
+    h = _f32(h)
+    require_cuda(h, a_src, a_dst, bias)
+    n, c = h.shape
+    if n != csr.num_nodes or c % 64:
+        raise ValueError("aggregate_lds: h must be [num_nodes, 64k]")
+    out = torch.empty_like(h)
+    alpha = torch.empty(csr.num_edges, dtype=torch.float32, device=h.device)
+    check(LIB.vg_gat_aggregate_fwd_lds(ptr(csr.row_ptr), ptr(csr.col), n, c, ptr(h), ptr(_f32(a_src)),
+                                       ptr(_f32(a_dst)), ptr(_f32(bias)), float(slope), ptr(out), ptr(alpha),
+                                       ptr(csr.tile_plan()), csr._tile_umax, csr.stream()), "vg_gat_aggregate_fwd_lds")
+    return out, alpha
+
 
 def _f32(t: torch.Tensor) -> torch.Tensor:
     if t.dtype != torch.float32:

@@ -40,7 +40,8 @@ def _worker(rank, world, port, q):
     sync.all_reduce_grad(flat)
     gathered = [torch.zeros_like(local) for _ in range(world)]
     dist.all_gather(gathered, local)
-    q.put((rank, flat.param.clone(), flat.grad.clone(), torch.stack(gathered).mean(0)))
+    # plain data: a tensor travels as a file descriptor that dies with this process
+    q.put((rank, flat.param.tolist(), flat.grad.tolist(), torch.stack(gathered).mean(0).tolist()))
     dist.destroy_process_group()
 
 
@@ -60,6 +61,7 @@ def _run(target, world=2):
 
 def test_gloo_two_ranks_average_and_broadcast():
     (_, p0, g0, m0), (_, p1, g1, _) = _run(_worker)
+    p0, g0, m0, p1, g1 = (torch.tensor(v) for v in (p0, g0, m0, p1, g1))
     assert torch.equal(p0, p1)  # parameters broadcast from rank 0
     assert torch.allclose(g0, g1) and torch.allclose(g0, m0, atol=1e-6)  # averaged gradient
 
