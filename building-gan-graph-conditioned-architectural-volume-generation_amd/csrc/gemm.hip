@@ -799,6 +799,188 @@ struct TnGroup {
   int n;
 };
 
+// f32 products without LDS staging: the 32x32x2 f32 MFMA takes lane l's A
+// operand as A[n + l / 32][m + l % 32] and its B operand as B[n + l / 32]
+// [k + l % 32] -- for a weight gradient (reduction over rows n) both are
+// plain coalesced row loads, so every wave feeds its MFMAs straight from
+// global memory: no LDS images, no barrier per K-step.  Each of the 4 waves
+// takes the whole (up to) 64 x 64 tile (2 x 2 accumulators) over every 4th
+// 16-row block of the chunk; the waves' sums are added through LDS once at
+// the end in a fixed order ((w0 + w2) + (w1 + w3): deterministic).
+#ifndef VG_TN_DIRECT
+#define VG_TN_DIRECT 1  // f32 grouped products: 1 tn_tile_direct, 0 the LDS-staged tn_tile (A/B)
+#endif
+#ifndef VG_TN_DU
+#define VG_TN_DU 8
+#endif
+constexpr int kTnDU = VG_TN_DU;  // row pairs (MFMA K-steps) per wave per block of 2 * kTnDU rows
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const float* p, int bytes) {
+  // descriptor words provably wave-uniform, or hipcc wraps every buffer op in a waterfall loop
+  const unsigned long long a = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(a));
+  const unsigned hi = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(a >> 32));
+  void* base = reinterpret_cast<void*>((static_cast<unsigned long long>(hi) << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(base, 0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+// M1 / K1: the tile's second 32-column halves (of M / K) are live.
+// BF: bf16 operands, f32 accumulation (v_mfma_f32_32x32x16_bf16 takes lane
+// l's A operand as A[n + 8 (l / 32) + j][m + l % 32], j < 8: the same
+// coalesced row loads, eight rows per lane, rounded to bf16 in registers).
+template <bool M1, bool K1, bool BF>
+__device__ __forceinline__ void tn_tile_direct(float* red, const float* __restrict__ A, int lda,
+                                               const float* __restrict__ B, int ldb, int N, int M, int K, int rows,
+                                               int chunk, int m0, int k0, float* __restrict__ part,
+                                               float* __restrict__ pdb, int db_rows) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int nb = chunk * rows, ne = min(N, nb + rows);
+  const int col = lane & 31, half = lane >> 5;
+  const bool do_db = pdb && k0 == 0;
+  static_assert(!BF || kTnDU == 8, "a bf16 block is one 16-row MFMA step");
+  // row of load p within the block: f32 pairs (2p + half), bf16 eights (8 half + p)
+  const int hrow = BF ? 8 * half : half, prow = BF ? 1 : 2;
+  f32x16 c00, c01, c10, c11;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) c00[r] = c01[r] = c10[r] = c11[r] = 0.f;
+  float db0 = 0.f, db1 = 0.f;
+  // Buffer loads: a 32-bit per-lane offset (the row pair's step in the
+  // scalar soffset) and a hardware range check -- rows >= N (the last
+  // chunk's tail; a chunk's 16-row blocks never cross into the next chunk,
+  // rows % 32 == 0) read as 0 with no mask; a column past M / K gets an
+  // offset beyond the buffer (the host keeps N * ld * 4 < 2^30).
+  constexpr unsigned kOob = 1u << 30;
+  const auto ra = uniform_rsrc(A, N * lda * 4);
+  const auto rb = uniform_rsrc(B, N * ldb * 4);
+  const unsigned oa0 = m0 + col < M ? (m0 + col) * 4u : kOob, oa1 = m0 + 32 + col < M ? (m0 + 32 + col) * 4u : kOob;
+  const unsigned ob0 = k0 + col < K ? (k0 + col) * 4u : kOob, ob1 = k0 + 32 + col < K ? (k0 + 32 + col) * 4u : kOob;
+#pragma nounroll
+  for (int n16 = nb + 2 * kTnDU * wave; n16 < ne; n16 += 8 * kTnDU) {
+    float a0[kTnDU], a1[kTnDU], b0[kTnDU], b1[kTnDU];
+    const unsigned ra_n = (unsigned)(n16 + hrow) * lda * 4u, rb_n = (unsigned)(n16 + hrow) * ldb * 4u;
+#pragma unroll
+    for (int p = 0; p < kTnDU; ++p) {
+      const int sa = prow * p * lda * 4, sb = prow * p * ldb * 4;
+      a0[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra, ra_n + oa0, sa, 0));
+      b0[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, rb_n + ob0, sb, 0));
+      if constexpr (M1) a1[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra, ra_n + oa1, sa, 0));
+      else a1[p] = 0.f;
+      if constexpr (K1) b1[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, rb_n + ob1, sb, 0));
+      else b1[p] = 0.f;
+    }
+    if constexpr (BF) {
+      bf16x8 ha0, ha1, hb0, hb1;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        ha0[j] = static_cast<__bf16>(a0[j]);
+        hb0[j] = static_cast<__bf16>(b0[j]);
+        ha1[j] = static_cast<__bf16>(a1[j]);
+        hb1[j] = static_cast<__bf16>(b1[j]);
+      }
+      c00 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha0, hb0, c00, 0, 0, 0);
+      if constexpr (K1) c01 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha0, hb1, c01, 0, 0, 0);
+      if constexpr (M1) c10 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha1, hb0, c10, 0, 0, 0);
+      if constexpr (M1 && K1) c11 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha1, hb1, c11, 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int p = 0; p < kTnDU; ++p) {
+        c00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[p], b0[p], c00, 0, 0, 0);
+        if constexpr (K1) c01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[p], b1[p], c01, 0, 0, 0);
+        if constexpr (M1) c10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[p], b0[p], c10, 0, 0, 0);
+        if constexpr (M1 && K1) c11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[p], b1[p], c11, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < kTnDU; ++p)
+      if (do_db && n16 + hrow + prow * p < db_rows) {  // the f32 values (as tn_tile)
+        db0 += a0[p];
+        db1 += a1[p];
+      }
+  }
+  // Cross-wave sum, one accumulator at a time (so the epilogue never holds
+  // all 64 accumulators in VGPRs): ((w0 + w2) + (w1 + w3)), deterministic;
+  // red holds 2 slots x 16 floats per lane.  Wave 0 writes the partial.
+  const int half4 = 4 * half;
+  float* out = part + (size_t)chunk * M * K;
+  auto reduce_store = [&](f32x16& c, int mo, int ko) {
+    if (wave >= 2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[((wave - 2) * 16 + r) * 64 + lane] = c[r];
+    __syncthreads();
+    if (wave < 2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) c[r] += red[(wave * 16 + r) * 64 + lane];
+    __syncthreads();
+    if (wave == 1)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[r * 64 + lane] = c[r];
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + mo + (r & 3) + 8 * (r >> 2) + half4, k = k0 + ko + col;
+        if (m < M && k < K) out[(size_t)m * K + k] = c[r] + red[r * 64 + lane];
+      }
+    }
+    __syncthreads();  // red is free for the next accumulator
+  };
+  reduce_store(c00, 0, 0);
+  if constexpr (K1) reduce_store(c01, 0, 32);
+  if constexpr (M1) reduce_store(c10, 32, 0);
+  if constexpr (M1 && K1) reduce_store(c11, 32, 32);
+  if (do_db) {  // lanes l and l + 32 hold the same column's other rows
+    db0 += __shfl_xor(db0, 32, 64);
+    db1 += __shfl_xor(db1, 32, 64);
+    if (wave >= 2) {
+      red[(wave - 2) * 64 + lane] = db0;
+      red[(2 + wave - 2) * 64 + lane] = db1;
+    }
+    __syncthreads();
+    if (wave < 2) {
+      db0 += red[wave * 64 + lane];
+      db1 += red[(2 + wave) * 64 + lane];
+    }
+    __syncthreads();
+    if (wave == 1) {
+      red[lane] = db0;
+      red[64 + lane] = db1;
+    }
+    __syncthreads();
+    if (wave == 0 && half == 0) {
+      if (m0 + col < M) pdb[(size_t)chunk * M + m0 + col] = db0 + red[lane];
+      if (m0 + 32 + col < M) pdb[(size_t)chunk * M + m0 + 32 + col] = db1 + red[64 + lane];
+    }
+  }
+}
+
+constexpr int kTnDirectRed = 2 * 16 * 64;  // floats of the cross-wave buffer (8 KB)
+
+template <bool BF>
+__global__ void __launch_bounds__(256) k_gemm_tn_group_direct(const TnGroup g) {
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  int p = 0;
+  while (p + 1 < g.n && lb >= g.block0[p + 1]) ++p;
+  const vg_tn& d = g.p[p];
+  const int local = lb - g.block0[p];
+  const int gx = (d.M + TM - 1) / TM, gxy = gx * ((d.K + TN - 1) / TN);
+  const int chunk = local / gxy, rem = local % gxy;
+  __shared__ float red[kTnDirectRed];
+  const int m0 = (rem % gx) * TM, k0 = (rem / gx) * TN;
+  const bool m1 = m0 + 32 < d.M, k1 = k0 + 32 < d.K;
+  if (m1 && k1)
+    tn_tile_direct<true, true, BF>(red, d.A, d.lda, d.B, d.ldb, d.N, d.M, d.K, d.rows, chunk, m0, k0, d.part, d.pdb,
+                               d.db_rows);
+  else if (m1)
+    tn_tile_direct<true, false, BF>(red, d.A, d.lda, d.B, d.ldb, d.N, d.M, d.K, d.rows, chunk, m0, k0, d.part, d.pdb,
+                                d.db_rows);
+  else if (k1)
+    tn_tile_direct<false, true, BF>(red, d.A, d.lda, d.B, d.ldb, d.N, d.M, d.K, d.rows, chunk, m0, k0, d.part, d.pdb,
+                                d.db_rows);
+  else
+    tn_tile_direct<false, false, BF>(red, d.A, d.lda, d.B, d.ldb, d.N, d.M, d.K, d.rows, chunk, m0, k0, d.part, d.pdb,
+                                 d.db_rows);
+}
+
 template <int G, bool BF>
 __global__ void __launch_bounds__(256 * G) k_gemm_tn_group(const TnGroup g) {
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
@@ -1078,7 +1260,17 @@ extern "C" int vg_gemm_tn_group(const vg_tn* prods, int32_t n, void* stream) {
   g.block0[n] = static_cast<int>(blocks);
   g.n = n;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (bf)
+#ifndef VG_TN_DIRECT_BF
+#define VG_TN_DIRECT_BF 1  // bf16 grouped products: 1 tn_tile_direct<.., true>, 0 the LDS-staged tn_tile (A/B)
+#endif
+  bool direct = bf ? VG_TN_DIRECT_BF : VG_TN_DIRECT;  // buffer offsets: every operand under 2^30 bytes
+  for (int i = 0; direct && i < n; ++i)
+    direct = (long long)prods[i].N * prods[i].lda * 4 < (1LL << 30) && (long long)prods[i].N * prods[i].ldb * 4 < (1LL << 30);
+  if (direct && bf)
+    k_gemm_tn_group_direct<true><<<static_cast<int>(blocks), 256, 0, s>>>(g);
+  else if (direct)
+    k_gemm_tn_group_direct<false><<<static_cast<int>(blocks), 256, 0, s>>>(g);
+  else if (bf)
     k_gemm_tn_group<kTnGroups, true><<<static_cast<int>(blocks), 256 * kTnGroups, 0, s>>>(g);
   else
     k_gemm_tn_group<kTnGroups, false><<<static_cast<int>(blocks), 256 * kTnGroups, 0, s>>>(g);
