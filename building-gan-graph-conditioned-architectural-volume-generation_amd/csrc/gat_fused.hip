@@ -33,6 +33,7 @@
 //                          + g_a_src_j att_src + g_a_dst_j att_dst;
 //                          block partials of sum_j g_a_src_j h_j (att_src)
 //   B3 (columns)           fold the block partials into g_bias, g_att_src, g_att_dst.
+#include "gnbwd.h"
 #include "rowgroup.h"
 
 namespace {
@@ -321,12 +322,15 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_ep(
 }
 
 // ================================================== backward B1 (destination)
-template <int L, int CPL, bool VEC>
+// GN: g_out is not read but formed here -- the GraphNorm(+ReLU+Dropout)
+// backward of the layer's output (gnbwd.h, vg_gat_bwd_gn) -- and written to
+// gn.g_out for the source pass (one launch and one pass over g_out fewer).
+template <int L, int CPL, bool VEC, bool GN = false>
 __global__ void __launch_bounds__(kBlock) k_gat_bwd_rows_cp(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, int N, int C,
     const float* __restrict__ h, const float* __restrict__ a_src, const float* __restrict__ a_dst,
     const float* __restrict__ alpha, const float* __restrict__ g_out, float slope,
-    float* __restrict__ g_pre, float* __restrict__ g_ad, float* __restrict__ part) {
+    float* __restrict__ g_pre, float* __restrict__ g_ad, float* __restrict__ part, const GnRows gn = GnRows{}) {
   constexpr int G = kBlock / L;
   const int grp = threadIdx.x / L, lane = threadIdx.x & (L - 1);
   const int base = (threadIdx.x & 63) & ~(L - 1);
@@ -339,7 +343,14 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_rows_cp(
     const int beg = row_ptr[i], end = row_ptr[i + 1];
     const int deg = end - beg;
     Vec<CPL> go, hi;
-    load_row<CPL, VEC>(go, g_out + (size_t)i * C, c0, C);
+    if constexpr (GN) {
+      // every operand of the row's g_out in one round of loads (the column
+      // parameters are L2 hits); the store waits for the end of the row, so
+      // the neighbour gathers below are not ordered behind it
+      gn_row<CPL, VEC>(gn, C, i, c0, go);
+    } else {
+      load_row<CPL, VEC>(go, g_out + (size_t)i * C, c0, C);
+    }
     load_row<CPL, VEC>(hi, h + (size_t)i * C, c0, C);
     const int s_own = lane < deg ? col[beg + lane] : 0;
     const float al_own = lane < deg ? alpha[beg + lane] : 0.f;
@@ -398,6 +409,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_rows_cp(
     }
     gad = group_sum<L>(gad);
     if (lane == 0) g_ad[i] = gad;
+    if constexpr (GN) store_row<CPL, VEC>(go, gn.g_out + (size_t)i * C, c0, C);
 #pragma unroll
     for (int q = 0; q < CPL; ++q) {
       pb.v[q] += go.v[q];
@@ -408,12 +420,12 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_rows_cp(
   block_partials<L, CPL>(vals, 2, C, part);
 }
 
-template <int CMAX>
+template <int CMAX, bool GN = false>
 __global__ void __launch_bounds__(kBlock) k_gat_bwd_rows_ep(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, int N, int C,
     const float* __restrict__ h, const float* __restrict__ a_src, const float* __restrict__ a_dst,
     const float* __restrict__ alpha, const float* __restrict__ g_out, float slope,
-    float* __restrict__ g_pre, float* __restrict__ g_ad, float* __restrict__ part) {
+    float* __restrict__ g_pre, float* __restrict__ g_ad, float* __restrict__ part, const GnRows gn = GnRows{}) {
   constexpr int L = 8, G = kBlock / L;
   const int grp = threadIdx.x / L, lane = threadIdx.x & (L - 1);
   float pb[CMAX], pd[CMAX];
@@ -423,8 +435,15 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_rows_ep(
   for (int i = lb * G + grp; i < N; i += gridDim.x * G) {
     const int beg = row_ptr[i], end = row_ptr[i + 1];
     float go[CMAX];
+    if constexpr (GN) {  // every lane forms the whole (<= 8-channel) row; lane c stores it at the end
+      Vec<CMAX> gv;
+      gn_row<CMAX, false>(gn, C, i, 0, gv);
 #pragma unroll
-    for (int c = 0; c < CMAX; ++c) go[c] = c < C ? g_out[(size_t)i * C + c] : 0.f;
+      for (int c = 0; c < CMAX; ++c) go[c] = gv.v[c];
+    } else {
+#pragma unroll
+      for (int c = 0; c < CMAX; ++c) go[c] = c < C ? g_out[(size_t)i * C + c] : 0.f;
+    }
     float ga[kEP], al[kEP];
     float t = 0.f;
 #pragma unroll
@@ -474,6 +493,10 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_rows_ep(
       gad += gp;
     }
     gad = group_sum<L>(gad);
+    if constexpr (GN)
+#pragma unroll
+      for (int c = 0; c < CMAX; ++c)
+        if (c < C && lane == c) gn.g_out[(size_t)i * C + c] = go[c];
     if (lane == 0) {
       g_ad[i] = gad;
 #pragma unroll
@@ -790,12 +813,17 @@ static int gat_bwd(const int32_t* row_ptr, const int32_t* col, const int32_t* cs
                    const float* a_dst, const float* alpha, const float* g_out, float slope,
                    float* g_h, float* g_att_src, float* g_att_dst, float* g_bias,
                    int32_t accumulate, const float* inj, int32_t inj_row0, float* workspace,
-                   void* stream, vg_fold* defer, int32_t* n_defer) {
+                   void* stream, vg_fold* defer, int32_t* n_defer, const GnRows* gn = nullptr) {
   if (n_defer) *n_defer = 0;
   const bool pgrads = g_att_src != nullptr;
   if (N <= 0 || E <= 0 || !row_ptr || !col || !csc_ptr || !csc_slot || !csc_dst || !h ||
       !att_src || !att_dst || !a_src || !a_dst || !alpha || !g_out || !g_h || !workspace ||
       (pgrads && (!g_att_dst || !g_bias)) || inj_row0 < 0)
+    return VG_EINVAL;
+  const size_t gn_lds = 0;
+  if (gn && (gn->S <= 0 || gn->seg_rows <= 0 || (long long)gn->S * gn->seg_rows != N ||
+             !gn->x || !gn->g_y || !gn->weight || !gn->bias || !gn->mean_scale || !gn->stats || !gn->sums ||
+             gn->g_out != g_out || gn->inj_row0 < 0))
     return VG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
   float* g_pre = workspace;
@@ -807,8 +835,13 @@ static int gat_bwd(const int32_t* row_ptr, const int32_t* col, const int32_t* cs
     grid1 = grid2 = bwd_grid(N, 8);
 #define VG_EP(CM)                                                                                 \
   do {                                                                                            \
-    k_gat_bwd_rows_ep<CM><<<grid1, kBlock, 0, s>>>(row_ptr, col, N, C, h, a_src, a_dst, alpha,     \
-                                                   g_out, slope, g_pre, g_ad, part1);             \
+    if (gn)                                                                                       \
+      k_gat_bwd_rows_ep<CM, true><<<grid1, kBlock, gn_lds, s>>>(row_ptr, col, N, C, h, a_src, a_dst, \
+                                                                alpha, g_out, slope, g_pre, g_ad,  \
+                                                                part1, *gn);                       \
+    else                                                                                          \
+      k_gat_bwd_rows_ep<CM><<<grid1, kBlock, 0, s>>>(row_ptr, col, N, C, h, a_src, a_dst, alpha,   \
+                                                     g_out, slope, g_pre, g_ad, part1);           \
     k_gat_bwd_src_ep<CM><<<grid2, kBlock, 0, s>>>(csc_ptr, csc_slot, csc_dst, N, C, h, att_src,    \
                                                   att_dst, alpha, g_out, g_pre, g_ad, inj,         \
                                                   inj_row0, g_h, part2);                           \
@@ -822,9 +855,14 @@ static int gat_bwd(const int32_t* row_ptr, const int32_t* col, const int32_t* cs
     Shape sh;
     if (!pick_fused_shape(C, sh)) return VG_EINVAL;
     grid1 = grid2 = bwd_grid(N, sh.L);
-    VG_DISPATCH_FUSED(C, (k_gat_bwd_rows_cp<L_, CPL_, V_><<<grid1, kBlock, 0, s>>>(
-                             row_ptr, col, N, C, h, a_src, a_dst, alpha, g_out, slope, g_pre,
-                             g_ad, part1)));
+    if (gn)
+      VG_DISPATCH_FUSED(C, (k_gat_bwd_rows_cp<L_, CPL_, V_, true><<<grid1, kBlock, gn_lds, s>>>(
+                               row_ptr, col, N, C, h, a_src, a_dst, alpha, g_out, slope, g_pre,
+                               g_ad, part1, *gn)));
+    else
+      VG_DISPATCH_FUSED(C, (k_gat_bwd_rows_cp<L_, CPL_, V_><<<grid1, kBlock, 0, s>>>(
+                               row_ptr, col, N, C, h, a_src, a_dst, alpha, g_out, slope, g_pre,
+                               g_ad, part1)));
     VG_DISPATCH_FUSED(C, (k_gat_bwd_src_cp<L_, CPL_, V_><<<grid2, kBlock, 0, s>>>(
                              csc_ptr, csc_slot, csc_dst, N, C, h, att_src, att_dst, alpha, g_out,
                              g_pre, g_ad, inj, inj_row0, g_h, part2)));
@@ -869,6 +907,24 @@ extern "C" int vg_gat_bwd_deferred(const int32_t* row_ptr, const int32_t* col,
   return gat_bwd(row_ptr, col, csc_ptr, csc_slot, csc_dst, N, E, C, h, att_src, att_dst, a_src,
                  a_dst, alpha, g_out, slope, g_h, g_att_src, g_att_dst, g_bias, accumulate, inj,
                  inj_row0, workspace, stream, folds_out, n_out);
+}
+
+extern "C" int vg_gat_bwd_gn(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,
+                             const int32_t* csc_slot, const int32_t* csc_dst, int32_t N, int32_t E, int32_t C,
+                             const float* h, const float* att_src, const float* att_dst, const float* a_src,
+                             const float* a_dst, const float* alpha, const vg_gn_bwd_in* gn, float* g_out,
+                             float slope, float* g_h, float* g_att_src, float* g_att_dst, float* g_bias,
+                             int32_t accumulate, const float* inj, int32_t inj_row0, float* workspace,
+                             vg_fold* folds_out, int32_t* n_out, void* stream) {
+  if (!gn || !g_out || (folds_out != nullptr) != (n_out != nullptr) || gn->inj_offset < 0 ||
+      (gn->inj && (gn->inj_offset % (C > 0 ? C : 1) != 0 || gn->inj_offset / (C > 0 ? C : 1) >= (1LL << 31))))
+    return VG_EINVAL;
+  const GnRows g{gn->x, gn->keep, gn->g_y, gn->inj, gn->weight, gn->bias, gn->mean_scale, gn->stats, gn->sums,
+                 g_out, gn->eps, gn->segments, gn->seg_rows,
+                 gn->inj ? static_cast<int>(gn->inj_offset / C) : 0};
+  return gat_bwd(row_ptr, col, csc_ptr, csc_slot, csc_dst, N, E, C, h, att_src, att_dst, a_src, a_dst, alpha, g_out,
+                 slope, g_h, g_att_src, g_att_dst, g_bias, accumulate, inj, inj_row0, workspace, stream, folds_out,
+                 n_out, &g);
 }
 
 extern "C" int vg_gat_bwd(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,

@@ -26,6 +26,7 @@
 // elementwise kernel applies.  Lanes are packed (col, row-sub) so narrow layers
 // (C = 1..32) still use every lane of the wave.
 #include "common.h"
+#include "gnbwd.h"
 
 #include <initializer_list>
 
@@ -438,16 +439,8 @@ __global__ void k_gn_bwd_apply(const float* __restrict__ x, const float* __restr
     const long long sg = t / seg_elems;
     const float* st = stats + 2 * C * sg;
     const float* sm = sums + 2 * C * sg;
-    const float mu = st[c], sd = st[C + c], s = sd + eps;
-    const float wc = w[c], msc = ms[c];
-    const float xv = x[t];
-    const float xh = (xv - mu * msc) / s;
-    const float z = xh * wc + b[c];
-    float gz = z > 0.f ? gy[t] : 0.f;
-    if (keep) gz *= keep[t];
-    const float A = sm[c], B = sm[C + c];
-    float g = (wc / s) * (gz - msc * A * inv_n);
-    if (sd > 0.f) g -= (wc * B * inv_n / (s * sd)) * (xv - mu);
+    float g = vg::gn_bwd_elem(x[t], gy[t], keep ? keep[t] : 1.f, keep != nullptr, st[c], st[C + c], w[c], b[c],
+                              ms[c], sm[c], sm[C + c], eps, inv_n);
     if (inj && t >= inj_off) g += inj[t - inj_off];
     gx[t] = g;
   }
@@ -687,15 +680,8 @@ __global__ void k_gn_bwd_apply4(const float* __restrict__ x, const float* __rest
     F4 out;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float mu = muv.v[j], sd = sdv.v[j], s = sd + eps;
-      const float wc = wv.v[j], msc = mv.v[j];
-      const float xh = (xv.v[j] - mu * msc) / s;
-      const float z = xh * wc + bv.v[j];
-      float gz = z > 0.f ? gv.v[j] : 0.f;
-      if (keep) gz *= kv.v[j];
-      const float A = Av.v[j], B = Bv.v[j];
-      float g = (wc / s) * (gz - msc * A * inv_n);
-      if (sd > 0.f) g -= (wc * B * inv_n / (s * sd)) * (xv.v[j] - mu);
+      float g = vg::gn_bwd_elem(xv.v[j], gv.v[j], kv.v[j], keep != nullptr, muv.v[j], sdv.v[j], wv.v[j], bv.v[j],
+                                mv.v[j], Av.v[j], Bv.v[j], eps, inv_n);
       if (has_inj) g += iv.v[j];
       out.v[j] = g;
     }
@@ -825,7 +811,7 @@ extern "C" int vg_graphnorm_bwd_seg(const float* x, int32_t S, int32_t N, int32_
                                     float* g_b, float* g_ms, int32_t accumulate, const float* inj,
                                     int64_t inj_offset, float* ws, int32_t* sync, void* stream) {
   if (S <= 0 || N <= 0 || C <= 0 || !x || !weight || !bias || !mean_scale || !stats || !g_y ||
-      !g_x || !ws || (g_w && (!g_b || !g_ms)) || inj_offset < 0)
+      !ws || (g_w && (!g_b || !g_ms)) || inj_offset < 0)
     return VG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int chunks = chunks_for(N);
@@ -837,9 +823,14 @@ extern "C" int vg_graphnorm_bwd_seg(const float* x, int32_t S, int32_t N, int32_
   (void)sync;
   k_gn_bwd_final<<<vg_blocks(C, kBlock / 64), kBlock, 0, s>>>(part, chunks, C, S, weight, mean_scale, eps,
                                                               stats, sums, g_w, g_b, g_ms, accumulate);
-  gn_bwd_apply_launch(x, S, N, C, weight, bias, mean_scale, keep, eps, stats, sums, g_y, g_x, inj, inj_offset, s);
+  if (g_x)  // g_x NULL: the column sums only (vg_gat_bwd_gn applies them)
+    gn_bwd_apply_launch(x, S, N, C, weight, bias, mean_scale, keep, eps, stats, sums, g_y, g_x, inj, inj_offset, s);
   VG_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int64_t vg_graphnorm_bwd_sums_offset(int32_t segments, int32_t channels) {
+  return (int64_t)segments * kChunks * channels * 5;
 }
 
 extern "C" int64_t vg_gemm_gn_tpart_floats(int32_t rows, int32_t channels) {
@@ -854,13 +845,14 @@ extern "C" int vg_graphnorm_bwd_seg_tiles(const float* x, int32_t S, int32_t N, 
                                           int32_t accumulate, const float* inj, int64_t inj_offset,
                                           float* ws, void* stream) {
   if (S <= 0 || N < 64 || C <= 0 || !x || !weight || !bias || !mean_scale || !stats || !g_y || !tpart ||
-      !g_x || !ws || (g_w && (!g_b || !g_ms)) || inj_offset < 0)
+      !ws || (g_w && (!g_b || !g_ms)) || inj_offset < 0)
     return VG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
   float* sums = ws + (size_t)S * kChunks * C * 5;
   k_gn_bwd_final_tiles<<<vg_blocks(C, kBlock / 64), kBlock, 0, s>>>(tpart, N, C, S, weight, mean_scale, eps,
                                                                     stats, sums, g_w, g_b, g_ms, accumulate);
-  gn_bwd_apply_launch(x, S, N, C, weight, bias, mean_scale, keep, eps, stats, sums, g_y, g_x, inj, inj_offset, s);
+  if (g_x)
+    gn_bwd_apply_launch(x, S, N, C, weight, bias, mean_scale, keep, eps, stats, sums, g_y, g_x, inj, inj_offset, s);
   VG_CHECK_LAUNCH();
   return 0;
 }

@@ -61,6 +61,18 @@ VG_JVP_GROUP_MAX = 16
 _JVP_GROUP = os.environ.get("VGAN_JVP_GROUP", "0") == "1"
 
 
+class VgGnBwdIn(ctypes.Structure):
+    """vg_gn_bwd_in (include/vgan.h): the GraphNorm backward a GAT backward
+    row pass forms in its prologue (vg_gat_bwd_gn)."""
+    _fields_ = [(k, _c_p) for k in ("x", "keep", "g_y", "inj", "weight", "bias", "mean_scale", "stats", "sums")] + \
+               [("eps", _c_f32), ("segments", _c_i32), ("seg_rows", _c_i32), ("inj_offset", _c_i64)]
+
+
+# VGAN_GN_ROWS=0: the GraphNorm backward's elementwise pass as its own launch
+# instead of in the GAT backward's destination-row pass (A/B knob)
+_GN_ROWS = os.environ.get("VGAN_GN_ROWS", "1") == "1"
+
+
 class VgASrc(ctypes.Structure):
     """vg_asrc (include/vgan.h): one column block of vg_gemm_ln_act_ms's A."""
     _fields_ = [("ptr", _c_p), ("ld", _c_i32), ("cols", _c_i32), ("w_col0", _c_i32), ("rows_mod", _c_i32)]
@@ -83,6 +95,10 @@ SIGNATURES = {
     "vg_graphnorm_bwd_seg_tiles": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p,
                                                   _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_i64, _c_p,
                                                   _c_p]),
+    "vg_graphnorm_bwd_sums_offset": (_c_i64, [_c_i32, _c_i32]),
+    "vg_gat_bwd_gn": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p,
+                                     _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_i32, _c_p, _c_p,
+                                     _c_p, _c_p]),
     "vg_gemm_tn_deferred": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_i32, _c_p,
                                            _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p]),
     "vg_gat_bwd_deferred": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p,

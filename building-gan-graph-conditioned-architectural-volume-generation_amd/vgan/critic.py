@@ -33,13 +33,14 @@ from __future__ import annotations
 
 from typing import List, Optional
 
+import ctypes
 import os
 
 import torch
 import torch.nn as nn
 
 from . import data as vdata
-from ._lib import LIB, FoldCollector, check, dense, ptr, stream_handle, sync_counter
+from ._lib import _GN_ROWS, LIB, FoldCollector, VgGnBwdIn, check, dense, ptr, stream_handle, sync_counter
 
 ACT_NONE, ACT_RELU, ACT_MASK = 0, 1, 3
 # VGAN_GN_FUSE=0: the GraphNorm backward's column partials in their own pass
@@ -178,22 +179,33 @@ class CriticEngine:
             return tp
 
         def gn_bwd(b: int, mix: bool, tp, g_y, g_x, pgrads: bool, inj=None, inj_off: int = 0):
-            """block b's GraphNorm(+ReLU+Dropout) backward: g_x from g_y"""
+            """block b's GraphNorm(+ReLU+Dropout) backward: g_x from g_y.
+            g_x None: the column sums only -- returns the descriptor with which
+            vg_gat_bwd_gn forms g_x in its destination-row pass (and the
+            workspace holding the sums)."""
             norm, c = self.blocks[b][1], blk[b]["c"]
             S = 1 if mix else 3
             x, keep, stats = gn_inputs(b, mix)
             ws = _f(int(LIB.vg_graphnorm_seg_ws_floats(S, n, c)), dev=dev)
             pg = (ptr(norm.weight.grad), ptr(norm.bias.grad), ptr(norm.mean_scale.grad)) if pgrads else (None,) * 3
+            gx = None if g_x is None else ptr(g_x)
             if tp is not None:
                 check(LIB.vg_graphnorm_bwd_seg_tiles(x, S, n, c, ptr(norm.weight), ptr(norm.bias), ptr(norm.mean_scale),
-                                                     keep, float(norm.eps), stats, ptr(g_y), ptr(tp), ptr(g_x), *pg,
+                                                     keep, float(norm.eps), stats, ptr(g_y), ptr(tp), gx, *pg,
                                                      1 if pgrads else 0, inj, inj_off, ptr(ws), st),
                       "vg_graphnorm_bwd_seg_tiles")
             else:
                 check(LIB.vg_graphnorm_bwd_seg(x, S, n, c, ptr(norm.weight), ptr(norm.bias), ptr(norm.mean_scale),
-                                               keep, float(norm.eps), stats, ptr(g_y), ptr(g_x), *pg,
+                                               keep, float(norm.eps), stats, ptr(g_y), gx, *pg,
                                                1 if pgrads else 0, inj, inj_off, ptr(ws), sy, st),
                       "vg_graphnorm_bwd_seg")
+            if g_x is not None:
+                return None
+            gn = VgGnBwdIn(x=x, keep=keep, g_y=ptr(g_y), inj=inj, weight=ptr(norm.weight), bias=ptr(norm.bias),
+                           mean_scale=ptr(norm.mean_scale), stats=stats,
+                           sums=_off(ws, int(LIB.vg_graphnorm_bwd_sums_offset(S, c))), eps=float(norm.eps),
+                           segments=S, seg_rows=n, inj_offset=inj_off if inj else 0)
+            return gn, ws
 
         # ---------------------------------------------------------- pass A
         X0 = _f(X4, W0, dev=dev)
@@ -273,14 +285,23 @@ class CriticEngine:
             c = B["c"]
             dY_b[b] = dY
             dO = _f(n, c, dev=dev)
-            gn_bwd(b, True, tp, dY, dO, False)
             dH = rows(adj_H[b], trow, c)
             ws = _f(int(LIB.vg_gat_bwd_ws_floats(n, E, c)), dev=dev)
-            check(LIB.vg_gat_bwd_ex(ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot),
-                                    ptr(csr.csc_dst), n, E, c, rows(B["H"], mrow, c), ptr(conv.att_src),
-                                    ptr(conv.att_dst), _off(B["a_s"], mrow), _off(B["a_d"], mrow),
-                                    _off(B["alpha"], 2 * E), ptr(dO), float(conv.negative_slope), dH, None, None, None,
-                                    0, None, 0, ptr(ws), st), "vg_gat_bwd_ex")
+            if _GN_ROWS:  # g_x (= dO) formed in the GAT backward's destination-row pass
+                gn, gws = gn_bwd(b, True, tp, dY, None, False)
+                check(LIB.vg_gat_bwd_gn(ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot),
+                                        ptr(csr.csc_dst), n, E, c, rows(B["H"], mrow, c), ptr(conv.att_src),
+                                        ptr(conv.att_dst), _off(B["a_s"], mrow), _off(B["a_d"], mrow),
+                                        _off(B["alpha"], 2 * E), ctypes.byref(gn), ptr(dO),
+                                        float(conv.negative_slope), dH, None, None, None, 0, None, 0, ptr(ws), None,
+                                        None, st), "vg_gat_bwd_gn")
+            else:
+                gn_bwd(b, True, tp, dY, dO, False)
+                check(LIB.vg_gat_bwd_ex(ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot),
+                                        ptr(csr.csc_dst), n, E, c, rows(B["H"], mrow, c), ptr(conv.att_src),
+                                        ptr(conv.att_dst), _off(B["a_s"], mrow), _off(B["a_d"], mrow),
+                                        _off(B["alpha"], 2 * E), ptr(dO), float(conv.negative_slope), dH, None, None,
+                                        None, 0, None, 0, ptr(ws), st), "vg_gat_bwd_ex")
             dO_b[b] = dO
             cin = B["xw"]
             if b > 0:
@@ -369,14 +390,20 @@ class CriticEngine:
             (conv, norm), B = self.blocks[b], blk[b]
             c, cin = B["c"], B["xw"]
             dO = _f(R, c, dev=dev)
-            gn_bwd(b, False, tp, dY, dO, True, ptr(oinj_b[b]), mrow * c)
             ws = _f(int(LIB.vg_gat_bwd_ws_floats(R, 3 * E, c)), dev=dev)
-            folds.call(LIB.vg_gat_bwd_deferred,
-                       (ptr(csr3.row_ptr), ptr(csr3.col), ptr(csr3.csc_ptr), ptr(csr3.csc_slot), ptr(csr3.csc_dst), R,
+            gat_args = (ptr(csr3.row_ptr), ptr(csr3.col), ptr(csr3.csc_ptr), ptr(csr3.csc_slot), ptr(csr3.csc_dst), R,
                         3 * E, c, ptr(B["H"]), ptr(conv.att_src), ptr(conv.att_dst), ptr(B["a_s"]), ptr(B["a_d"]),
-                        ptr(B["alpha"]), ptr(dO), float(conv.negative_slope), ptr(adj_H[b]), ptr(conv.att_src.grad),
-                        ptr(conv.att_dst.grad), ptr(conv.bias.grad), 1, ptr(hinj_b[b]), mrow, ptr(ws)), st,
-                       keep=(ws,), name="vg_gat_bwd_deferred")
+                        ptr(B["alpha"]))
+            gat_tail = (float(conv.negative_slope), ptr(adj_H[b]), ptr(conv.att_src.grad), ptr(conv.att_dst.grad),
+                        ptr(conv.bias.grad), 1, ptr(hinj_b[b]), mrow, ptr(ws))
+            if _GN_ROWS:
+                gn, gws = gn_bwd(b, False, tp, dY, None, True, ptr(oinj_b[b]), mrow * c)
+                folds.call(LIB.vg_gat_bwd_gn, gat_args + (ctypes.byref(gn), ptr(dO)) + gat_tail, st,
+                           keep=(ws, gws), name="vg_gat_bwd_gn")
+            else:
+                gn_bwd(b, False, tp, dY, dO, True, ptr(oinj_b[b]), mrow * c)
+                folds.call(LIB.vg_gat_bwd_deferred, gat_args + (ptr(dO),) + gat_tail, st, keep=(ws,),
+                           name="vg_gat_bwd_deferred")
             self._gemm_tn(folds, st, dev, ptr(adj_H[b]), c, ptr(B["X"]), cin, X4, c, cin, ptr(conv.lin.weight.grad), cin)
             if b > 0:
                 dY = _f(R, cin, dev=dev)

@@ -597,12 +597,50 @@ int vg_gemm_gn_bwd_bf16(const float* A, int32_t lda, const float* B, int32_t ldb
                         float* tpart, void* stream);
 
 /* vg_graphnorm_bwd_seg from the partials vg_gemm_gn_bwd left in tpart (its
- * fold and apply passes only); N = seg_rows >= 64. */
+ * fold and apply passes only); N = seg_rows >= 64.  g_x NULL (here and in
+ * vg_graphnorm_bwd_seg): the column sums only, left in the workspace at
+ * vg_graphnorm_bwd_sums_offset floats ([S][2C]: sum gz | sum gz xhat) for
+ * vg_gat_bwd_gn, which applies them. */
 int vg_graphnorm_bwd_seg_tiles(const float* x, int32_t S, int32_t N, int32_t C, const float* weight,
                                const float* bias, const float* mean_scale, const float* keep,
                                float eps, const float* stats, const float* g_y, const float* tpart,
                                float* g_x, float* g_w, float* g_b, float* g_ms, int32_t accumulate,
                                const float* inj, int64_t inj_offset, float* ws, void* stream);
+int64_t vg_graphnorm_bwd_sums_offset(int32_t segments, int32_t channels);
+
+/* The GraphNorm(+ReLU+Dropout) backward whose output g_x is the g_out of the
+ * GATConv below it (models.py:72-75 / 192-195: conv -> norm -> relu ->
+ * dropout): x, keep, g_y, stats of the S stacked segments of seg_rows rows,
+ * sums = the column sums of vg_graphnorm_bwd_seg(_tiles) called with g_x
+ * NULL; inj (nullable) is added from flat element inj_offset on (a multiple
+ * of the channel count). */
+typedef struct {
+  const float* x;
+  const float* keep;
+  const float* g_y;
+  const float* inj;
+  const float* weight;
+  const float* bias;
+  const float* mean_scale;
+  const float* stats;
+  const float* sums;
+  float eps;
+  int32_t segments, seg_rows;
+  int64_t inj_offset;
+} vg_gn_bwd_in;
+
+/* vg_gat_bwd_ex / vg_gat_bwd_deferred (folds_out, n_out both NULL: folded
+ * here) with g_out formed in the destination-row pass from *gn and written
+ * to g_out (for the source pass and the caller): the GraphNorm backward's
+ * elementwise launch and its pass over g_x disappear.  num_nodes =
+ * segments * seg_rows. */
+int vg_gat_bwd_gn(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr, const int32_t* csc_slot,
+                  const int32_t* csc_dst, int32_t num_nodes, int32_t num_edges, int32_t channels,
+                  const float* h, const float* att_src, const float* att_dst, const float* a_src,
+                  const float* a_dst, const float* alpha, const vg_gn_bwd_in* gn, float* g_out, float slope,
+                  float* g_h, float* g_att_src, float* g_att_dst, float* g_bias, int32_t accumulate,
+                  const float* inj, int32_t inj_row0, float* workspace, vg_fold* folds_out, int32_t* n_out,
+                  void* stream);
 
 /* ---- bf16 training (BASELINE.json configs[2]) ---------------------------- */
 

@@ -456,3 +456,27 @@ def test_grouped_jvp_source_passes_bit_identical(cuda, monkeypatch):
         out[grouped] = (loss.item(), flat.grad.clone())
     assert out[True][0] == out[False][0]
     assert torch.equal(out[True][1], out[False][1])
+
+
+@pytest.mark.parametrize("training,fuse", [(True, True), (False, True), (True, False)])
+def test_gat_backward_forms_graphnorm_backward(cuda, training, fuse, monkeypatch):
+    """The GraphNorm backward's elementwise pass formed in the GAT backward's
+    destination-row pass (vg_gat_bwd_gn, gnbwd.h) against its own launch: one
+    formula over the same column sums, so the loss and the D gradient are the
+    same up to f32 contraction (dropout masks, the pass-D injection, both
+    sum folds: GEMM tiles and the separate partial pass)."""
+    from vgan import critic as vcritic
+
+    cfg, D, flat, loc, vox, prep, hard, soft, eng = _engine_setup(cuda, numbers=(5, 6, 7), seed=31)
+    D.train(training)
+    monkeypatch.setattr(vcritic, "_GN_FUSE", fuse)
+    hd, sd = hard.to(cuda).unsqueeze(0), soft.to(cuda).unsqueeze(0)
+    out = {}
+    for rows in (True, False):
+        monkeypatch.setattr(vcritic, "_GN_ROWS", rows)
+        flat.zero_grad()
+        loss = eng.loss_and_grad(loc, vox, hd, sd, _RecRNG(22))
+        torch.cuda.synchronize()
+        out[rows] = (loss.item(), flat.grad.clone())
+    assert out[True][0] == out[False][0]
+    assert rel_err(out[True][1], out[False][1]) < 1e-6
