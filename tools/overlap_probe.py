@@ -1,89 +1,76 @@
-"""Do two captured step graphs overlap when replayed on two streams?
+"""Host time of each replay call of the overlapped critic-label schedule
+(label 1 on the main stream, labels 2.. on the label stream, critic 1 on the
+main stream): does launching a graph on one stream hold the host (or the
+device) until another stream's graph is done?  One JSON line."""
+from __future__ import annotations
 
-    python tools/overlap_probe.py
-
-Captures the stacked critic-label G forward and one critic iteration as two
-hipGraphs with SEPARATE memory pools, then times (HIP events, R replays)
-  serial      labels; critic        on one stream
-  concurrent  labels || critic      on two streams, joined per replay
-Values are meaningless (the critic reads labels while they are rewritten);
-only the device time is of interest.  Prints one JSON line (us per pair)."""
 import json
 import os
 import sys
+import time
 
-import torch
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "building-gan-graph-conditioned-architectural-volume-generation_amd"))
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
 import bench  # noqa: E402
 
 
-def timed(fn, reps):
-    torch.cuda.synchronize()
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record()
-    for _ in range(reps):
-        fn()
-    b.record()
-    torch.cuda.synchronize()
-    return a.elapsed_time(b) * 1e3 / reps
-
-
 def main():
-    dev = torch.device("cuda", 0)
-    torch.cuda.set_device(dev)
     from vgan.config import Configuration
 
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
     cfg = Configuration()
     cfg.DEVICE = str(dev)
     cfg.runtime["rng"] = "device"
+    torch.manual_seed(cfg.SEED)
     pool = bench.make_pool(cfg, 0, 1, 1, 32, dev)
-    tr = bench.build_trainer(cfg)
+    tr = bench.build_trainer(cfg, "f32")
     loc, vox = pool[0]
-    bench.run_steps(tr, pool, 2)  # lazy init + the trainer's own capture
+    for _ in range(3):
+        tr.step_graphed(loc, vox)
     torch.cuda.synchronize()
-    acc = torch.zeros(2, dtype=torch.float32, device=dev)
-    pa, pb, pc = (torch.cuda.graph_pool_handle() for _ in range(3))
-    gl = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(gl, pool=pa):
-        labels = tr._critic_labels(loc, vox)
-    gc = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(gc, pool=pb):
-        tr._critic_body(loc, vox, acc, True, labels, 0)
-    gc2 = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(gc2, pool=pc):
-        tr._critic_body(loc, vox, acc, True, labels, 1)
-    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
-    main_s = torch.cuda.current_stream(dev)
-    reps = 20
-
-    def serial():
-        gl.replay()
-        gc.replay()
-
-    def conc(ga, gb):
-        def f():
-            s1.wait_stream(main_s)
-            s2.wait_stream(main_s)
-            with torch.cuda.stream(s1):
-                ga.replay()
-            with torch.cuda.stream(s2):
-                gb.replay()
-            main_s.wait_stream(s1)
-            main_s.wait_stream(s2)
-        return f
-
+    g = vox.derived(tr._graph_key)
+    main = torch.cuda.current_stream()
+    side = torch.cuda.Stream(dev)
     res = {}
-    for _ in range(2):  # second round is the reported one
-        res = {
-            "labels_us": timed(gl.replay, reps),
-            "critic_us": timed(gc.replay, reps),
-            "serial_labels_critic_us": timed(serial, reps),
-            "concurrent_labels_critic_us": timed(conc(gl, gc), reps),
-            "serial_critic_critic_us": timed(lambda: (gc.replay(), gc2.replay()), reps),
-            "concurrent_critic_critic_us": timed(conc(gc, gc2), reps),
-        }
-    print(json.dumps({k: round(v, 1) for k, v in res.items()}), flush=True)
+    for rep in range(3):
+        torch.cuda.synchronize()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        t = [time.perf_counter()]
+        ev[0].record(main)
+        g["labels"].replay()
+        t.append(time.perf_counter())
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            g["labels_rest"].replay()
+            ev[1].record(side)
+        t.append(time.perf_counter())
+        g["critic"][0].replay()
+        ev[2].record(main)
+        t.append(time.perf_counter())
+        torch.cuda.synchronize()
+        t.append(time.perf_counter())
+        res[rep] = {"host_label1_ms": (t[1] - t[0]) * 1e3, "host_rest_ms": (t[2] - t[1]) * 1e3,
+                    "host_critic_ms": (t[3] - t[2]) * 1e3, "wall_ms": (t[4] - t[0]) * 1e3,
+                    "dev_rest_end_ms": ev[0].elapsed_time(ev[1]), "dev_critic_end_ms": ev[0].elapsed_time(ev[2])}
+    # alone: label graph replays serially
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    g["labels_rest"].replay()
+    b.record()
+    torch.cuda.synchronize()
+    res["rest_alone_ms"] = a.elapsed_time(b)
+    a.record()
+    g["critic"][0].replay()
+    b.record()
+    torch.cuda.synchronize()
+    res["critic_alone_ms"] = a.elapsed_time(b)
+    print(json.dumps(res))
 
 
 if __name__ == "__main__":
