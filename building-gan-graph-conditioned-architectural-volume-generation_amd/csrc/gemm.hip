@@ -1120,7 +1120,7 @@ extern "C" int vg_gemm_bf16(const float* A, int32_t lda, const float* B, int32_t
 #define VG_TN_TARGET 768
 #endif
 #ifndef VG_TN_GROUP_TARGET
-#define VG_TN_GROUP_TARGET 192
+#define VG_TN_GROUP_TARGET 64  // with tn_tile_direct; step A/B over 16..192: profiles/r02_ab_tn_direct.txt
 #endif
 // (a product planned for vg_gemm_tn_group shares the grid with the other
 // products of its backward: VG_TN_GROUP_TARGET workgroups each)

@@ -96,13 +96,24 @@ __global__ void __launch_bounds__(kBlock) k_stats_partial(const T* __restrict__ 
   part += (size_t)blockIdx.z * gridDim.x * C * 3;
   Welford w = {0.f, 0.f, 0.f};
   if (col_ok) {
-#pragma unroll 4
-    for (int r = r0 + rsub; r < r1; r += rstep) {
-      const float v = static_cast<float>(x[(size_t)r * ld + c]);
-      w.n += 1.f;
-      const float d = v - w.mean;
-      w.mean += d / w.n;
-      w.m2 += d * (v - w.mean);
+    // kB rows per lane in flight at once (a chunk is ~13 rows per lane at
+    // batch 32), then the Welford updates in row order (as one row at a time)
+    constexpr int kB = 16;
+    for (int rb = r0 + rsub; rb < r1; rb += kB * rstep) {
+      float v[kB];
+#pragma unroll
+      for (int j = 0; j < kB; ++j) {
+        const int r = rb + j * rstep;
+        v[j] = r < r1 ? static_cast<float>(x[(size_t)r * ld + c]) : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < kB; ++j) {
+        if (rb + j * rstep >= r1) break;
+        w.n += 1.f;
+        const float d = v[j] - w.mean;
+        w.mean += d / w.n;
+        w.m2 += d * (v[j] - w.mean);
+      }
     }
   }
   // merge lanes of the same column inside the wave (xor over the row-sub bits)
@@ -623,21 +634,30 @@ __global__ void k_gn_apply4(const float* __restrict__ x, int quads, int N, int C
                             unsigned int salt, float* __restrict__ keep_out) {
   extern __shared__ float4 sh4[];
   float* sh = reinterpret_cast<float*>(sh4);
-  stage_cols(sh, w, b, ms, C, stats, 2 * C * S, nullptr, 0);
+  // the first quad's x / keep are in flight while the column operands are
+  // staged (one memory round trip instead of two: the usual single pass)
+  const int q0 = blockIdx.x * blockDim.x + threadIdx.x;
+  F4 xp = {{0.f, 0.f, 0.f, 0.f}}, kp = {{1.f, 1.f, 1.f, 1.f}};
+  if (q0 < quads) {
+    xp = ld4(x + 4 * q0);
+    if (!keep_out && keep) kp = ld4(keep + 4 * q0);
+  }
   const long long it = keep_out ? *iter : 0;
-  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < quads; q += gridDim.x * blockDim.x) {
+  stage_cols(sh, w, b, ms, C, stats, 2 * C * S, nullptr, 0);
+  for (int q = q0; q < quads; q += gridDim.x * blockDim.x) {
     const int t0 = q * 4;
     const int row = t0 / C;
     const int c0 = t0 - row * C;
     const float* st = sh + 3 * C + 2 * C * (row / N);
-    const F4 xv = ld4(x + t0);
+    const bool first = q == q0;
+    const F4 xv = first ? xp : ld4(x + t0);
     F4 k4 = {{1.f, 1.f, 1.f, 1.f}};
     if (keep_out) {
       const float4 k = vg_keep4_raw(q, salt, it, seed, p_drop);
       k4 = F4{{k.x, k.y, k.z, k.w}};
       st4(keep_out + t0, k4);
     } else if (keep) {
-      k4 = ld4(keep + t0);
+      k4 = first ? kp : ld4(keep + t0);
     }
     const F4 wv = ld4(sh + c0), bv = ld4(sh + C + c0), mv = ld4(sh + 2 * C + c0);
     const F4 muv = ld4(st + c0), sdv = ld4(st + C + c0);
@@ -662,19 +682,31 @@ __global__ void k_gn_bwd_apply4(const float* __restrict__ x, const float* __rest
                                 float* __restrict__ gx) {
   extern __shared__ float4 sh4[];
   float* sh = reinterpret_cast<float*>(sh4);
+  const F4 one = {{1.f, 1.f, 1.f, 1.f}}, zero = {{0.f, 0.f, 0.f, 0.f}};
+  // the first quad's operands in flight while the column operands are staged
+  const int q0 = blockIdx.x * blockDim.x + threadIdx.x;
+  F4 xp = zero, gp = zero, kp = one, ip = zero;
+  if (q0 < quads) {
+    const int t0 = 4 * q0;
+    xp = ld4(x + t0);
+    gp = ld4(gy + t0);
+    if (keep) kp = ld4(keep + t0);
+    if (inj && t0 >= inj_off) ip = ld4(inj + (t0 - inj_off));
+  }
   stage_cols(sh, w, b, ms, C, stats, 2 * C * S, sums, 2 * C * S);
   const float inv_n = 1.f / static_cast<float>(N);
-  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < quads; q += gridDim.x * blockDim.x) {
+  for (int q = q0; q < quads; q += gridDim.x * blockDim.x) {
     const int t0 = q * 4;
     const int row = t0 / C;
     const int c0 = t0 - row * C;
     const int sg = row / N;
     const float* st = sh + 3 * C + 2 * C * sg;
     const float* sm = sh + 3 * C + 2 * C * S + 2 * C * sg;
-    const F4 xv = ld4(x + t0), gv = ld4(gy + t0);
-    const F4 kv = keep ? ld4(keep + t0) : F4{{1.f, 1.f, 1.f, 1.f}};
+    const bool first = q == q0;
+    const F4 xv = first ? xp : ld4(x + t0), gv = first ? gp : ld4(gy + t0);
+    const F4 kv = first ? kp : (keep ? ld4(keep + t0) : one);
     const bool has_inj = inj && t0 >= inj_off;
-    const F4 iv = has_inj ? ld4(inj + (t0 - inj_off)) : F4{{0.f, 0.f, 0.f, 0.f}};
+    const F4 iv = first ? ip : (has_inj ? ld4(inj + (t0 - inj_off)) : zero);
     const F4 wv = ld4(sh + c0), bv = ld4(sh + C + c0), mv = ld4(sh + 2 * C + c0);
     const F4 muv = ld4(st + c0), sdv = ld4(st + C + c0), Av = ld4(sm + c0), Bv = ld4(sm + C + c0);
     F4 out;

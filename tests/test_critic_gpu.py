@@ -382,8 +382,8 @@ def test_engine_matches_autograd_path_on_gpu(cuda):
 def test_grouped_weight_gradients_bit_identical(cuda, precision, monkeypatch):
     """The weight-gradient products of a backward run as ONE vg_gemm_tn_group
     launch at its end (FoldCollector.tn) instead of one launch per layer.  The
-    grouped plan splits each product over fewer row chunks (192 instead of
-    768 workgroups), so the f32 sums differ only in order: the critic loss is
+    grouped plan splits each product over fewer row chunks (64 instead of
+    768 workgroups per output tile), so the f32 sums differ only in order: the critic loss is
     identical and the D and G gradients agree to 1e-6 relative."""
     from vgan import _lib, ops
     from vgan._lib import gemm_precision_scope
