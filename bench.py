@@ -74,7 +74,8 @@ def aggregate_roofline(tr, csr, device, reps: int = 20):
     step's CSRs and channel counts, captured in a hipGraph and replayed
     ``reps`` times between HIP events on the replay stream (back-to-back
     launches, as inside the step's own graphs)."""
-    from vgan._lib import LIB, check, ptr, stream_handle
+    from vgan import ops
+    from vgan._lib import ptr, stream_handle
 
     calls = step_aggregate_calls(tr, csr)
     gen = torch.Generator(device=device)
@@ -95,8 +96,7 @@ def aggregate_roofline(tr, csr, device, reps: int = 20):
         st = stream_handle(device)
         for c_csr, c in calls:
             h, a_s, a_d, b, out, alpha = bufs[(c_csr.num_nodes, c)]
-            check(LIB.vg_gat_aggregate_fwd(ptr(c_csr.row_ptr), ptr(c_csr.col), c_csr.num_nodes, c, ptr(h), ptr(a_s),
-                                           ptr(a_d), ptr(b), 0.2, ptr(out), ptr(alpha), st), "vg_gat_aggregate_fwd")
+            ops.aggregate_fwd_raw(c_csr, c, ptr(h), ptr(a_s), ptr(a_d), ptr(b), 0.2, ptr(out), ptr(alpha), st)
 
     side = torch.cuda.Stream(device)
     side.wait_stream(torch.cuda.current_stream(device))
@@ -227,9 +227,8 @@ def stress_roofline(device, channels=(128, 64, 1), reps: int = 20):
         out, alpha = torch.empty(n, c, device=device), torch.empty(e, device=device)
 
         def run():
-            check(LIB.vg_gat_aggregate_fwd(ptr(csr.row_ptr), ptr(csr.col), n, c, ptr(h), ptr(a_s), ptr(a_d),
-                                           ptr(bias), 0.2, ptr(out), ptr(alpha), stream_handle(device)),
-                  "vg_gat_aggregate_fwd")
+            ops.aggregate_fwd_raw(csr, c, ptr(h), ptr(a_s), ptr(a_d), ptr(bias), 0.2, ptr(out), ptr(alpha),
+                                  stream_handle(device))
 
         def run_lds():
             check(LIB.vg_gat_aggregate_fwd_lds(ptr(csr.row_ptr), ptr(csr.col), n, c, ptr(h), ptr(a_s), ptr(a_d),

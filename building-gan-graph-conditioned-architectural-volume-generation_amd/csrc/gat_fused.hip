@@ -94,12 +94,16 @@ __global__ void __launch_bounds__(kBlock) k_gat_att(const float* __restrict__ h,
 // C >= 9, pass B: logits + exact two-pass segment softmax edge-parallel over
 // the group's lanes, then the channel-parallel weighted gather-sum (4 rows
 // gathered per step, independent loads in flight).
-template <int L, int CPL, bool VEC>
+// ELL: the row's sources come from the padded column array ell [N][ew]
+// (-1 past the degree, ew <= 4L, vg_csr_ell) at a fixed offset, so their
+// loads -- and the a_src gathers behind them -- need not wait for row_ptr,
+// which is still read (in parallel) for the degree and the alpha offsets.
+template <int L, int CPL, bool VEC, bool ELL = false>
 __global__ void __launch_bounds__(kBlock) k_gat_fwd_cp(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, int N, int C,
     const float* __restrict__ h, const float* __restrict__ a_src, const float* __restrict__ a_dst,
     const float* __restrict__ bias, float slope, float* __restrict__ out,
-    float* __restrict__ alpha, int ld = 0) {
+    float* __restrict__ alpha, int ld = 0, const int32_t* __restrict__ ell = nullptr, int ew = 0) {
   // ld > 0: a channel slice -- h / out / bias point at the slice's first
   // channel, rows are ld floats apart, and only the slice at blockIdx.y == 0
   // writes alpha (every slice recomputes the row's softmax)
@@ -123,38 +127,46 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_cp(
   // edge-parallel logits, kept per lane: edge j lives in lane j % L, slot j / L
   int s_t[T];
   float e_t[T];
+  bool v_t[T];
   float m = -INFINITY;
 #pragma unroll
   for (int t = 0; t < T; ++t) {
-    const int k = beg + g.lane + t * L;
-    s_t[t] = 0;
+    const int j = g.lane + t * L;
+    if constexpr (ELL) {
+      const int sr = j < ew ? ell[(size_t)i * ew + j] : -1;
+      v_t[t] = sr >= 0;
+      s_t[t] = v_t[t] ? sr : 0;
+    } else {
+      v_t[t] = beg + j < end;
+      s_t[t] = v_t[t] ? col[beg + j] : 0;
+    }
     e_t[t] = -INFINITY;
-    if (k < end) {
-      s_t[t] = col[k];
+    if (v_t[t]) {
       e_t[t] = lrelu(a_src[s_t[t]] + ad, slope);
       m = fmaxf(m, e_t[t]);
     }
   }
-  for (int k = beg + g.lane + T * L; k < end; k += L) m = fmaxf(m, lrelu(a_src[col[k]] + ad, slope));
+  if constexpr (!ELL)
+    for (int k = beg + g.lane + T * L; k < end; k += L) m = fmaxf(m, lrelu(a_src[col[k]] + ad, slope));
   m = group_max<L>(m);
   float ssum = 0.f;
 #pragma unroll
   for (int t = 0; t < T; ++t)
-    if (beg + g.lane + t * L < end) {
+    if (v_t[t]) {
       e_t[t] = expf(e_t[t] - m);  // now holds p = exp(e - max)
       ssum += e_t[t];
     }
-  for (int k = beg + g.lane + T * L; k < end; k += L) ssum += expf(lrelu(a_src[col[k]] + ad, slope) - m);
+  if constexpr (!ELL)
+    for (int k = beg + g.lane + T * L; k < end; k += L) ssum += expf(lrelu(a_src[col[k]] + ad, slope) - m);
   const float denom = group_sum<L>(ssum) + kSoftmaxEps;
 #pragma unroll
   for (int t = 0; t < T; ++t) {
-    const int k = beg + g.lane + t * L;
-    if (k < end) {
+    if (v_t[t]) {
       e_t[t] = e_t[t] / denom;  // alpha
-      if (wr_alpha) alpha[k] = e_t[t];
+      if (wr_alpha) alpha[beg + g.lane + t * L] = e_t[t];
     }
   }
-  if (wr_alpha)
+  if (!ELL && wr_alpha)
     for (int k = beg + g.lane + T * L; k < end; k += L)
       alpha[k] = expf(lrelu(a_src[col[k]] + ad, slope) - m) / denom;
 
@@ -185,7 +197,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_cp(
 #pragma unroll
         for (int q = 0; q < CPL; ++q) acc.v[q] = fmaf(a[u], hv[u].v[q], acc.v[q]);
   }
-  for (int j = T * L; j < deg; ++j) {  // very long rows: alpha from memory (written above by this group)
+  for (int j = T * L; !ELL && j < deg; ++j) {  // very long rows: alpha from memory (written above by this group)
     const int s = col[beg + j];
     const float a = expf(lrelu(a_src[s] + ad, slope) - m) / denom;
     Vec<CPL> hv;
@@ -203,12 +215,14 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_cp(
 // C <= 8: 8 lanes per destination row, one edge per lane.
 // PRE: a_src / a_dst are inputs (vg_gat_lin_att computed them in the
 // projection GEMM's epilogue); otherwise they are formed here and written.
-template <int CMAX, bool PRE = false>
+// ELL as in k_gat_fwd_cp (ew <= 8 kEP).
+template <int CMAX, bool PRE = false, bool ELL = false>
 __global__ void __launch_bounds__(kBlock) k_gat_fwd_ep(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, int N, int C,
     const float* __restrict__ h, const float* __restrict__ att_s, const float* __restrict__ att_d,
     const float* __restrict__ bias, float slope, float* __restrict__ out, float* __restrict__ alpha,
-    float* __restrict__ a_src_io, float* __restrict__ a_dst_io) {
+    float* __restrict__ a_src_io, float* __restrict__ a_dst_io, const int32_t* __restrict__ ell = nullptr,
+    int ew = 0) {
   constexpr int L = 8;
   const GroupIdx g = group_index<L>();
   if (g.row >= N) return;
@@ -237,13 +251,26 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_ep(
   const int beg = row_ptr[i], end = row_ptr[i + 1];
   float hv[kEP][CMAX];
   float e[kEP];
+  bool v[kEP];
+  int sv[kEP];
+#pragma unroll
+  for (int t = 0; t < kEP; ++t) {
+    const int j = g.lane + t * L;
+    if constexpr (ELL) {
+      const int sr = j < ew ? ell[(size_t)i * ew + j] : -1;
+      v[t] = sr >= 0;
+      sv[t] = v[t] ? sr : 0;
+    } else {
+      v[t] = beg + j < end;
+      sv[t] = v[t] ? col[beg + j] : 0;
+    }
+  }
   float m = -INFINITY;
 #pragma unroll
   for (int t = 0; t < kEP; ++t) {
-    const int k = beg + g.lane + t * L;
     e[t] = -INFINITY;
-    if (k < end) {
-      const int s = col[k];
+    if (v[t]) {
+      const int s = sv[t];
       float a = PRE ? a_src_io[s] : 0.f;
 #pragma unroll
       for (int c = 0; c < CMAX; ++c) {
@@ -258,7 +285,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_ep(
     }
   }
   // rows longer than 8*kEP: stream the rest (logits only for the max)
-  for (int k = beg + g.lane + kEP * L; k < end; k += L) {
+  for (int k = beg + g.lane + kEP * L; !ELL && k < end; k += L) {
     const int s = col[k];
     float a = PRE ? a_src_io[s] : 0.f;
     if (!PRE)
@@ -274,7 +301,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_ep(
   for (int c = 0; c < CMAX; ++c) acc[c] = 0.f;
 #pragma unroll
   for (int t = 0; t < kEP; ++t) {
-    if (beg + g.lane + t * L < end) {
+    if (v[t]) {
       const float p = expf(e[t] - m);
       e[t] = p;
       ssum += p;
@@ -282,7 +309,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_ep(
       for (int c = 0; c < CMAX; ++c) acc[c] = fmaf(p, hv[t][c], acc[c]);
     }
   }
-  for (int k = beg + g.lane + kEP * L; k < end; k += L) {
+  for (int k = beg + g.lane + kEP * L; !ELL && k < end; k += L) {
     const int s = col[k];
     float a = PRE ? a_src_io[s] : 0.f, hv2[CMAX];
 #pragma unroll
@@ -306,11 +333,9 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_ep(
     out[(size_t)i * C + g.lane] = v / denom + bias[g.lane];
   }
 #pragma unroll
-  for (int t = 0; t < kEP; ++t) {
-    const int k = beg + g.lane + t * L;
-    if (k < end) alpha[k] = e[t] / denom;
-  }
-  for (int k = beg + g.lane + kEP * L; k < end; k += L) {
+  for (int t = 0; t < kEP; ++t)
+    if (v[t]) alpha[beg + g.lane + t * L] = e[t] / denom;
+  for (int k = beg + g.lane + kEP * L; !ELL && k < end; k += L) {
     const int s = col[k];
     float a = PRE ? a_src_io[s] : 0.f;
     if (!PRE)
@@ -765,44 +790,94 @@ extern "C" int vg_gat_att(const float* h, int32_t N, int32_t C, const float* att
   return 0;
 }
 
-extern "C" int vg_gat_aggregate_fwd(const int32_t* row_ptr, const int32_t* col, int32_t N,
-                                    int32_t C, const float* h, const float* a_src,
-                                    const float* a_dst, const float* bias, float slope, float* out,
-                                    float* alpha, void* stream) {
+// the aggregation with (ell != NULL) or without the padded column array; a
+// kernel shape takes the ELL path when ew fits its edge slots (4L, or 8 kEP)
+static int aggregate_fwd(const int32_t* row_ptr, const int32_t* col, const int32_t* ell, int32_t ew, int32_t N,
+                         int32_t C, const float* h, const float* a_src, const float* a_dst, const float* bias,
+                         float slope, float* out, float* alpha, void* stream) {
   if (N <= 0 || C <= 0 || C > 256 || !row_ptr || !col || !h || !a_src || !a_dst || !bias ||
-      !out || !alpha)
+      !out || !alpha || (ell && ew <= 0))
     return VG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
   float* as = const_cast<float*>(a_src);  // read-only under PRE
   float* ad = const_cast<float*>(a_dst);
   if (C <= 8) {
     const int grid = grid_for(N, 8);
-    if (C <= 1)
-      k_gat_fwd_ep<1, true><<<grid, kBlock, 0, s>>>(row_ptr, col, N, C, h, nullptr, nullptr, bias,
-                                                     slope, out, alpha, as, ad);
-    else if (C <= 2)
-      k_gat_fwd_ep<2, true><<<grid, kBlock, 0, s>>>(row_ptr, col, N, C, h, nullptr, nullptr, bias,
-                                                     slope, out, alpha, as, ad);
-    else if (C <= 4)
-      k_gat_fwd_ep<4, true><<<grid, kBlock, 0, s>>>(row_ptr, col, N, C, h, nullptr, nullptr, bias,
-                                                     slope, out, alpha, as, ad);
-    else
-      k_gat_fwd_ep<8, true><<<grid, kBlock, 0, s>>>(row_ptr, col, N, C, h, nullptr, nullptr, bias,
-                                                     slope, out, alpha, as, ad);
+    const bool e = ell && ew <= 8 * kEP;
+#define VG_EPF(CM)                                                                                           \
+  do {                                                                                                       \
+    if (e)                                                                                                   \
+      k_gat_fwd_ep<CM, true, true><<<grid, kBlock, 0, s>>>(row_ptr, col, N, C, h, nullptr, nullptr, bias,    \
+                                                           slope, out, alpha, as, ad, ell, ew);              \
+    else                                                                                                     \
+      k_gat_fwd_ep<CM, true><<<grid, kBlock, 0, s>>>(row_ptr, col, N, C, h, nullptr, nullptr, bias, slope,   \
+                                                     out, alpha, as, ad);                                    \
+  } while (0)
+    if (C <= 1) VG_EPF(1);
+    else if (C <= 2) VG_EPF(2);
+    else if (C <= 4) VG_EPF(4);
+    else VG_EPF(8);
+#undef VG_EPF
   } else if (N >= kSliceRows && C % kSlice == 0 && C > kSlice) {
     // large graphs: 64-channel slices, slice-major in dispatch order, so the
     // rows an XCD gathers at a time (a window of ~2 lattice floors) are half
     // or less of the full-width footprint in its 4 MiB L2
     constexpr int Ls = kSlice / 4;
-    k_gat_fwd_cp<Ls, 4, true><<<dim3(grid_for(N, Ls), C / kSlice), kBlock, 0, s>>>(
-        row_ptr, col, N, kSlice, h, a_src, a_dst, bias, slope, out, alpha, C);
+    if (ell && ew <= 4 * Ls)
+      k_gat_fwd_cp<Ls, 4, true, true><<<dim3(grid_for(N, Ls), C / kSlice), kBlock, 0, s>>>(
+          row_ptr, col, N, kSlice, h, a_src, a_dst, bias, slope, out, alpha, C, ell, ew);
+    else
+      k_gat_fwd_cp<Ls, 4, true><<<dim3(grid_for(N, Ls), C / kSlice), kBlock, 0, s>>>(
+          row_ptr, col, N, kSlice, h, a_src, a_dst, bias, slope, out, alpha, C);
   } else if (VG_FWD_C64_L8 && C > 32 && C <= 64 && C % 8 == 0) {
     k_gat_fwd_cp<8, 8, true><<<grid_for(N, 8), kBlock, 0, s>>>(row_ptr, col, N, C, h, a_src, a_dst, bias,
                                                                 slope, out, alpha);
   } else {
-    VG_DISPATCH_FUSED(C, (k_gat_fwd_cp<L_, CPL_, V_><<<grid_for(N, L_), kBlock, 0, s>>>(
-                             row_ptr, col, N, C, h, a_src, a_dst, bias, slope, out, alpha)));
+    Shape sh;
+    if (!pick_fused_shape(C, sh)) return VG_EINVAL;
+    if (ell && ew <= 4 * sh.L)
+      VG_DISPATCH_FUSED(C, (k_gat_fwd_cp<L_, CPL_, V_, true><<<grid_for(N, L_), kBlock, 0, s>>>(
+                               row_ptr, col, N, C, h, a_src, a_dst, bias, slope, out, alpha, 0, ell, ew)));
+    else
+      VG_DISPATCH_FUSED(C, (k_gat_fwd_cp<L_, CPL_, V_><<<grid_for(N, L_), kBlock, 0, s>>>(
+                               row_ptr, col, N, C, h, a_src, a_dst, bias, slope, out, alpha)));
   }
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int vg_gat_aggregate_fwd(const int32_t* row_ptr, const int32_t* col, int32_t N,
+                                    int32_t C, const float* h, const float* a_src,
+                                    const float* a_dst, const float* bias, float slope, float* out,
+                                    float* alpha, void* stream) {
+  return aggregate_fwd(row_ptr, col, nullptr, 0, N, C, h, a_src, a_dst, bias, slope, out, alpha, stream);
+}
+
+extern "C" int vg_gat_aggregate_fwd_ell(const int32_t* row_ptr, const int32_t* col, const int32_t* ell,
+                                        int32_t ell_width, int32_t N, int32_t C, const float* h,
+                                        const float* a_src, const float* a_dst, const float* bias, float slope,
+                                        float* out, float* alpha, void* stream) {
+  if (!ell) return VG_EINVAL;
+  return aggregate_fwd(row_ptr, col, ell, ell_width, N, C, h, a_src, a_dst, bias, slope, out, alpha, stream);
+}
+
+// ell [N][width] = the row's CSR columns in order, -1 past its degree (the
+// caller guarantees width >= the largest degree)
+__global__ void k_csr_ell(const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, int N, int width,
+                          int32_t* __restrict__ ell) {
+  const long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (t >= (long long)N * width) return;
+  const int i = static_cast<int>(t / width), j = static_cast<int>(t % width);
+  const int beg = row_ptr[i], deg = row_ptr[i + 1] - beg;
+  ell[t] = j < deg ? col[beg + j] : -1;
+}
+
+extern "C" int vg_csr_ell(const int32_t* row_ptr, const int32_t* col, int32_t N, int32_t width, int32_t* ell,
+                          void* stream) {
+  if (N <= 0 || width <= 0 || !row_ptr || !col || !ell) return VG_EINVAL;
+  const long long total = (long long)N * width;
+  k_csr_ell<<<static_cast<int>((total + 255) / 256), 256, 0, static_cast<hipStream_t>(stream)>>>(row_ptr, col, N,
+                                                                                                  width, ell);
   VG_CHECK_LAUNCH();
   return 0;
 }

@@ -129,6 +129,9 @@ SIGNATURES = {
     "vg_gat_att": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "vg_gat_lin_att": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p,
                                       _c_p]),
+    "vg_csr_ell": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p]),
+    "vg_gat_aggregate_fwd_ell": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p,
+                                                _c_f32, _c_p, _c_p, _c_p]),
     "vg_gat_aggregate_fwd": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p,
                                             _c_p]),
     "vg_gat_bwd_ws_floats": (_c_i64, [_c_i32, _c_i32, _c_i32]),

@@ -40,6 +40,7 @@ import torch
 import torch.nn as nn
 
 from . import data as vdata
+from . import ops
 from ._lib import _GN_ROWS, LIB, FoldCollector, VgGnBwdIn, check, dense, ptr, stream_handle, sync_counter
 
 ACT_NONE, ACT_RELU, ACT_MASK = 0, 1, 3
@@ -226,9 +227,8 @@ class CriticEngine:
             check(dense("vg_gat_lin_att")(ptr(x), xw, ptr(conv.lin.weight), R, xw, c, ptr(conv.att_src),
                                      ptr(conv.att_dst), ptr(H), ptr(a_s), ptr(a_d), st), "vg_gat_lin_att")
             O, alpha = _f(R, c, dev=dev), _f(3 * E, dev=dev)
-            check(LIB.vg_gat_aggregate_fwd(ptr(csr3.row_ptr), ptr(csr3.col), R, c, ptr(H), ptr(a_s), ptr(a_d),
-                                           ptr(conv.bias), float(conv.negative_slope), ptr(O), ptr(alpha), st),
-                  "vg_gat_aggregate_fwd")
+            ops.aggregate_fwd_raw(csr3, c, ptr(H), ptr(a_s), ptr(a_d), ptr(conv.bias), float(conv.negative_slope),
+                                  ptr(O), ptr(alpha), st)
             Y, stats = _f(X4, c, dev=dev), _f(3 * 2 * c, dev=dev)
             ws = _f(int(LIB.vg_graphnorm_seg_ws_floats(3, n, c)), dev=dev)
             if keep is not None and not isinstance(keep, torch.Tensor):  # DropSpec: drawn in-kernel

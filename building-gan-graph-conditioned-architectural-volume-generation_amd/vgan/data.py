@@ -52,6 +52,7 @@ def _build(local_graph, voxel_graph, n_classes: int) -> Prepared:
         csr = ops.CSR.from_arrays(*arrays)  # emitted by the host collate (vgan.store)
     else:
         csr = ops.CSR(voxel_graph.edge_index, n)
+    csr.ell()  # the padded column array (one host sync) before any graph capture
     mv = torch.empty(n, fl + fv, dtype=torch.float32, device=vx.device)
     ops.type_mean(lx, local_graph.type, voxel_graph.type, n_classes, out=mv, col0=0)
     mv[:, fl:].copy_(vx)

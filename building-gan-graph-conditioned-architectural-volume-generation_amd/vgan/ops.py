@@ -19,6 +19,7 @@ available and every derivative runs through the same C ABI.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -29,6 +30,10 @@ from ._lib import LIB, FoldCollector, dense, check, ptr, require_cuda, stream_ha
 
 NEG_SLOPE = 0.2
 SOFTMAX_EPS = 1e-16
+# VGAN_ELL=0: the aggregation reads its sources through row_ptr -> col only
+# (A/B knob for the padded column array, CSR.ell)
+_ELL = os.environ.get("VGAN_ELL", "1") == "1"
+ELL_WIDTHS = (8, 16, 32)
 
 
 # --------------------------------------------------------------------- CSR
@@ -108,8 +113,37 @@ class CSR:
         out.col = tile(self.col, n)
         out.csc_slot = tile(self.csc_slot, e)
         out.csc_dst = tile(self.csc_dst, n)
+        if "_ell_w" in self.__dict__:  # same degrees: no host sync for the copies' width
+            out._ell_w = self._ell_w
         cache[copies] = out
         return out
+
+    def ell(self):
+        """(ell, width): the destination rows' sources padded to a fixed width
+        (vg_csr_ell: [N][width] int32, -1 past the degree; width the smallest
+        of 8 / 16 / 32 that holds the largest degree), so the aggregation
+        loads a row's sources without waiting for row_ptr.  (None, 0) when
+        the largest degree exceeds 32 or VGAN_ELL=0.  Built once and cached;
+        the width costs one host sync per graph (inherited by stacked()
+        copies), taken by data.prepared before any capture."""
+        cached = self.__dict__.get("_ell")
+        if cached is not None:
+            return cached
+        if not _ELL:
+            return None, 0
+        w = self.__dict__.get("_ell_w")
+        if w is None:
+            maxdeg = int((self.row_ptr[1:] - self.row_ptr[:-1]).max().item()) if self.num_nodes else 0
+            w = next((x for x in ELL_WIDTHS if maxdeg <= x), 0)
+            self._ell_w = w
+        if w == 0:
+            self._ell = (None, 0)
+            return self._ell
+        t = torch.empty(self.num_nodes * w, dtype=torch.int32, device=self.device)
+        check(LIB.vg_csr_ell(ptr(self.row_ptr), ptr(self.col), self.num_nodes, w, ptr(t), self.stream()),
+              "vg_csr_ell")
+        self._ell = (t, w)
+        return self._ell
 
     def tile_plan(self) -> torch.Tensor:
         """The LDS tile plan of this graph (vg_gat_tile_plan: per 16-row tile
@@ -126,6 +160,19 @@ class CSR:
             self._tile_umax = max(1, int(plan[:tiles].max().item()))
             self._tile_plan = plan
         return plan
+
+
+def aggregate_fwd_raw(csr: "CSR", c: int, h, a_src, a_dst, bias, slope: float, out, alpha, stream) -> None:
+    """vg_gat_aggregate_fwd over raw device pointers (ctypes), through the
+    padded column array when the graph has one (vg_gat_aggregate_fwd_ell);
+    bit-identical either way."""
+    ell, w = csr.ell()
+    if ell is not None:
+        check(LIB.vg_gat_aggregate_fwd_ell(ptr(csr.row_ptr), ptr(csr.col), ptr(ell), w, csr.num_nodes, c, h, a_src,
+                                           a_dst, bias, float(slope), out, alpha, stream), "vg_gat_aggregate_fwd_ell")
+    else:
+        check(LIB.vg_gat_aggregate_fwd(ptr(csr.row_ptr), ptr(csr.col), csr.num_nodes, c, h, a_src, a_dst, bias,
+                                       float(slope), out, alpha, stream), "vg_gat_aggregate_fwd")
 
 
 def aggregate_lds(csr: "CSR", h: torch.Tensor, a_src: torch.Tensor, a_dst: torch.Tensor, bias: torch.Tensor,
@@ -451,9 +498,8 @@ class _GATConv(Function):
             require_cuda(a_src, a_dst)
             if a_src.numel() != n or a_dst.numel() != n:
                 raise ValueError("gat_conv: inconsistent projection shapes")
-            check(LIB.vg_gat_aggregate_fwd(ptr(csr.row_ptr), ptr(csr.col), n, c, ptr(h), ptr(a_src), ptr(a_dst),
-                                           ptr(b), float(slope), ptr(out), ptr(alpha), csr.stream()),
-                  "vg_gat_aggregate_fwd")
+            aggregate_fwd_raw(csr, c, ptr(h), ptr(a_src), ptr(a_dst), ptr(b), slope, ptr(out), ptr(alpha),
+                              csr.stream())
         else:
             a_src = torch.empty(n, dtype=torch.float32, device=dev)
             a_dst = torch.empty(n, dtype=torch.float32, device=dev)

@@ -558,6 +558,21 @@ int vg_gemm_ln_act_ms(const vg_asrc* src, int32_t nsrc, const float* W, int32_t 
 
 /* ---- LDS-staged aggregation (large graphs, BASELINE configs[3]) ----------- */
 
+/* The destination CSR's sources padded to a fixed width: ell [N][width] =
+ * row i's columns in CSR order, -1 past its degree (width >= the largest
+ * degree).  Built once per graph (the critic's stacked copies: the same
+ * width). */
+int vg_csr_ell(const int32_t* row_ptr, const int32_t* col, int32_t num_nodes, int32_t width, int32_t* ell,
+               void* stream);
+/* vg_gat_aggregate_fwd reading each row's sources from ell (vg_csr_ell), so
+ * they load without waiting for row_ptr (still read for the degree and the
+ * alpha offsets); kernel shapes whose edge slots cannot hold ell_width fall
+ * back to row_ptr -> col.  Bit-identical to vg_gat_aggregate_fwd. */
+int vg_gat_aggregate_fwd_ell(const int32_t* row_ptr, const int32_t* col, const int32_t* ell, int32_t ell_width,
+                             int32_t num_nodes, int32_t channels, const float* h, const float* a_src,
+                             const float* a_dst, const float* bias, float slope, float* out, float* alpha,
+                             void* stream);
+
 /* Tile plan of a destination CSR (vg_csr_build's arrays), once per graph: for
  * every tile of 16 destination rows the sorted distinct sources of its edges
  * and each edge's slot among them.  plan: vg_gat_tile_plan_ints(N, E') int32s. */

@@ -623,3 +623,53 @@ def test_aggregate_lds_bit_identical(cuda, graph, C):
     hd = h.double().cpu()
     ref = pyg.gat_propagate(hd, a_s.double().cpu(), a_d.double().cpu(), ei) + b.double().cpu()
     assert rel_err(out, ref) < 1e-5
+
+
+@pytest.mark.parametrize("graph", ["lattice", "stress", "star", "stress_big", "stacked"])
+@pytest.mark.parametrize("C", [1, 3, 8, 12, 32, 64, 128, 192])
+def test_aggregate_ell_bit_identical(cuda, graph, C):
+    """vg_gat_aggregate_fwd_ell (each row's sources from the padded column
+    array, vg_csr_ell) equals vg_gat_aggregate_fwd bit for bit -- same edges,
+    order and arithmetic -- on the lattice (width 8), the stress lattice
+    (width 32, the 64-channel slice path at >= 100k rows is covered by
+    stress_big's size class in bench.py), a stacked CSR (the critic's three
+    copies: the width is inherited) and a star whose hub exceeds 32 edges
+    (no ELL: the same kernel as before)."""
+    from vgan.graph import GraphBatch
+
+    torch.manual_seed(C)
+    if graph == "star":
+        ei, n = _star_graph(600)
+    elif graph == "stress_big":
+        items = [synth.make_stress_building(777, i, F=6, Y=20, X=20) for i in range(2)]
+        vox = GraphBatch.from_data_list([v for _, v in items])
+        ei, n = vox.edge_index, vox.num_nodes
+    else:
+        _, vox = _graph(stress=(graph == "stress"))
+        ei, n = vox.edge_index, vox.num_nodes
+    csr = ops.CSR(ei.to(cuda), n)
+    ell, w = csr.ell()
+    if graph == "stacked":
+        csr = csr.stacked(3)
+        n = csr.num_nodes
+        ell, w2 = csr.ell()
+        assert w2 == w
+    if graph == "star":
+        assert ell is None and w == 0
+    else:
+        assert ell is not None and w in ops.ELL_WIDTHS
+        deg = (csr.row_ptr[1:] - csr.row_ptr[:-1]).cpu()
+        e2 = ell.view(n, w).cpu()
+        assert torch.equal((e2 >= 0).sum(1).int(), deg.int())
+        for i in range(0, n, max(1, n // 17)):  # the rows' sources in CSR order
+            b0, b1 = int(csr.row_ptr[i]), int(csr.row_ptr[i + 1])
+            assert torch.equal(e2[i, :b1 - b0], csr.col[b0:b1].cpu())
+    h = torch.randn(n, C, device=cuda)
+    a_s, a_d = 0.5 * torch.randn(n, device=cuda), 0.5 * torch.randn(n, device=cuda)
+    b = torch.randn(C, device=cuda)
+    from vgan._lib import ptr
+
+    out, alpha = torch.empty_like(h), torch.empty(csr.num_edges, device=cuda)
+    ops.aggregate_fwd_raw(csr, C, ptr(h), ptr(a_s), ptr(a_d), ptr(b), 0.2, ptr(out), ptr(alpha), csr.stream())
+    ref_out, ref_alpha = _aggregate_ref_kernel(csr, h, a_s, a_d, b)
+    assert torch.equal(out, ref_out) and torch.equal(alpha, ref_alpha)
