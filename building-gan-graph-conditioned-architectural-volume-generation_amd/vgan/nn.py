@@ -115,7 +115,8 @@ def _linear_backward(ctx, gy, saved=None, needs=None):
         return gx, gw, gb
     gy = gy.contiguous()
     if needs[0]:
-        gx = ops.gemm(gy, weight, False)
+        hint = ops.gn_hint_for(x)  # x is a GraphNorm output: its backward's partials from this GEMM
+        gx = ops.gemm_gn_bwd(gy, weight, hint) if hint is not None else ops.gemm(gy, weight, False)
     pw, pb = ctx.params
     if needs[1] and ops._direct(pw, pb):  # accumulate into .grad directly
         ops.gemm_tn_into(gy, x, pw.grad, pb.grad if ctx.has_bias else None)

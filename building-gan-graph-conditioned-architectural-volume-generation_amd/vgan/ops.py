@@ -576,12 +576,56 @@ def graphnorm_relu_dropout_torch(x, weight, bias, mean_scale, keep, eps):
     return y * keep if keep is not None else y
 
 
+# The GraphNorm backward's column partials from the epilogue of the GEMM that
+# produces its g_y (vg_gemm_gn_bwd, as the critic engine does): a GraphNorm
+# forward whose output feeds a linear layer leaves a hint keyed by that output
+# (address, shape); the linear backward finds it for its input and forms
+# g_x = g_h W with the partials; the GraphNorm backward folds them
+# (vg_graphnorm_bwd_seg_tiles) when its g_y IS that GEMM output -- a second
+# consumer of y would make autograd sum into a new tensor, and the hint holds
+# the GEMM output, so the sum cannot land in place.  VGAN_GN_EPI=0: off.
+_GN_EPI = os.environ.get("VGAN_GN_EPI", "1") == "1"
+_GN_HINTS = {}
+
+
+class _GnHint:
+    __slots__ = ("x", "keep", "stats", "weight", "bias", "mean_scale", "eps", "segments", "seg_rows", "tp", "gx")
+
+    def __init__(self, **kw):
+        for k in self.__slots__:
+            setattr(self, k, kw.get(k))
+
+
+def gn_hint_for(x: torch.Tensor):
+    """The GraphNorm hint of a linear layer's input, or None."""
+    if not _GN_HINTS:
+        return None
+    return _GN_HINTS.get((x.data_ptr(), tuple(x.shape)))
+
+
+def gemm_gn_bwd(gy: torch.Tensor, weight: torch.Tensor, hint: "_GnHint") -> torch.Tensor:
+    """g_x = g_y W (the linear backward's input gradient, = g_y of the
+    GraphNorm in ``hint``) with that GraphNorm backward's column partials
+    left on the hint."""
+    gy, w = _f32(gy), _f32(weight)
+    n, k = gy.shape
+    m = w.shape[1]
+    gx = torch.empty(n, m, dtype=torch.float32, device=gy.device)
+    tp = torch.empty(int(LIB.vg_gemm_gn_tpart_floats(n, m)), dtype=torch.float32, device=gy.device)
+    check(dense("vg_gemm_gn_bwd")(ptr(gy), k, ptr(w), m, n, m, k, ptr(gx), m, ptr(hint.x), ptr(hint.keep),
+                                  hint.seg_rows, ptr(hint.weight), ptr(hint.bias), ptr(hint.mean_scale),
+                                  float(hint.eps), ptr(hint.stats), ptr(tp), stream_handle(gy.device)),
+          "vg_gemm_gn_bwd")
+    hint.tp, hint.gx = tp, gx
+    return gx
+
+
 class _GraphNormReLUDropout(Function):
     """GraphNorm(batch=None) + ReLU + Dropout; ``segments`` > 1 normalises that
     many equal row blocks independently (stacked forwards of one batch)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, mean_scale, keep, eps, spec, segments):
+    def forward(ctx, x, weight, bias, mean_scale, keep, eps, spec, segments, hint=False):
         x = _f32(x)
         w, b, ms = _f32(weight), _f32(bias), _f32(mean_scale)
         kp = _f32(keep) if keep is not None else None
@@ -611,6 +655,13 @@ class _GraphNormReLUDropout(Function):
         ctx.eps, ctx.has_keep, ctx.segments = eps, kp is not None, S
         ctx.params = (weight, bias, mean_scale)
         ctx.save_for_backward(x, weight, bias, mean_scale, kp if kp is not None else x.new_empty(0), stats)
+        ctx.hint_key = None
+        if hint and n >= 64 and c % 4 == 0 and any(ctx.needs_input_grad[:4]):
+            if len(_GN_HINTS) > 256:  # forwards whose backward never ran
+                _GN_HINTS.clear()
+            ctx.hint_key = (y.data_ptr(), tuple(y.shape))
+            _GN_HINTS[ctx.hint_key] = _GnHint(x=x, keep=kp, stats=stats, weight=w, bias=b, mean_scale=ms, eps=eps,
+                                              segments=S, seg_rows=n)
         return y
 
     @staticmethod
@@ -627,7 +678,7 @@ class _GraphNormReLUDropout(Function):
                 grads = torch.autograd.grad(y, need, g_y, create_graph=True, allow_unused=True)
             it = iter(grads)
             res = [next(it) if t.requires_grad else None for t in ins]
-            return res[0], res[1], res[2], res[3], None, None, None, None
+            return res[0], res[1], res[2], res[3], None, None, None, None, None
         g_y = _f32(g_y)
         rows, c = x.shape
         n = rows // S
@@ -641,20 +692,31 @@ class _GraphNormReLUDropout(Function):
             g_b = torch.empty_like(g_w)
             g_ms = torch.empty_like(g_w)
         ws = torch.empty(int(LIB.vg_graphnorm_seg_ws_floats(S, n, c)), dtype=torch.float32, device=x.device)
-        check(LIB.vg_graphnorm_bwd_seg(ptr(x), S, n, c, ptr(w), ptr(b), ptr(ms), ptr(kp), float(ctx.eps), ptr(stats),
-                                       ptr(g_y), ptr(g_x), ptr(g_w), ptr(g_b), ptr(g_ms), 1 if direct else 0, None, 0,
-                                       ptr(ws), sync_counter(x.device), stream_handle(x.device)),
-              "vg_graphnorm_bwd_seg")
+        hint = _GN_HINTS.pop(ctx.hint_key, None) if ctx.hint_key is not None else None
+        if hint is not None and hint.tp is not None and hint.gx is not None and \
+                g_y.data_ptr() == hint.gx.data_ptr() and g_y.shape == hint.gx.shape:
+            check(LIB.vg_graphnorm_bwd_seg_tiles(ptr(x), S, n, c, ptr(w), ptr(b), ptr(ms), ptr(kp), float(ctx.eps),
+                                                 ptr(stats), ptr(g_y), ptr(hint.tp), ptr(g_x), ptr(g_w), ptr(g_b),
+                                                 ptr(g_ms), 1 if direct else 0, None, 0, ptr(ws),
+                                                 stream_handle(x.device)), "vg_graphnorm_bwd_seg_tiles")
+        else:
+            check(LIB.vg_graphnorm_bwd_seg(ptr(x), S, n, c, ptr(w), ptr(b), ptr(ms), ptr(kp), float(ctx.eps),
+                                           ptr(stats), ptr(g_y), ptr(g_x), ptr(g_w), ptr(g_b), ptr(g_ms),
+                                           1 if direct else 0, None, 0, ptr(ws), sync_counter(x.device),
+                                           stream_handle(x.device)), "vg_graphnorm_bwd_seg")
+        if hint is not None:
+            hint.tp = hint.gx = None
         if direct:
-            return g_x, None, None, None, None, None, None, None
-        return g_x, g_w, g_b, g_ms, None, None, None, None
+            return g_x, None, None, None, None, None, None, None, None
+        return g_x, g_w, g_b, g_ms, None, None, None, None, None
 
 
 def graphnorm_relu_dropout(x, weight, bias, mean_scale, keep, eps: float = 1e-5, segments: int = 1):
     """keep: dropout multipliers [N, C], a ``vgan.rng.DropSpec`` (drawn in-kernel) or None."""
+    hint = _GN_EPI and torch.is_grad_enabled()  # a backward will run: leave the GEMM-epilogue hint
     if keep is not None and not isinstance(keep, torch.Tensor):
-        return _GraphNormReLUDropout.apply(x, weight, bias, mean_scale, None, eps, keep, segments)
-    return _GraphNormReLUDropout.apply(x, weight, bias, mean_scale, keep, eps, None, segments)
+        return _GraphNormReLUDropout.apply(x, weight, bias, mean_scale, None, eps, keep, segments, hint)
+    return _GraphNormReLUDropout.apply(x, weight, bias, mean_scale, keep, eps, None, segments, hint)
 
 
 # ------------------------------------------------------ type-matched mean

@@ -480,3 +480,45 @@ def test_gat_backward_forms_graphnorm_backward(cuda, training, fuse, monkeypatch
         out[rows] = (loss.item(), flat.grad.clone())
     assert out[True][0] == out[False][0]
     assert rel_err(out[True][1], out[False][1]) < 1e-6
+
+
+@pytest.mark.parametrize("precision", ["f32", "bf16"])
+def test_autograd_graphnorm_partials_from_next_gemm(cuda, precision, monkeypatch):
+    """Autograd path (the generator iteration): a GraphNorm whose output feeds
+    a linear layer takes its backward's column partials from that layer's dX
+    GEMM epilogue (ops.gemm_gn_bwd + vg_graphnorm_bwd_seg_tiles) instead of a
+    partial pass; the encoder's last GraphNorm (its output also goes to the
+    decoder concat) keeps the separate pass.  Gradients agree to f32 rounding."""
+    from vgan import ops
+    from vgan._lib import gemm_precision_scope
+    from vgan.flat import FlatParams
+    from vgan.models import VoxelGNNGenerator
+    from vgan.rng import RNG
+
+    cfg, D, flat, loc, vox, prep, hard, soft, eng = _engine_setup(cuda, numbers=(5, 6, 7), seed=6)
+    torch.manual_seed(13)
+    G = VoxelGNNGenerator(cfg, 17, 12).to(cuda).train()
+    flat_g = FlatParams(G)
+    z = torch.randn(1, vox.num_nodes, cfg.Z_DIM, device=cuda)
+    noise = torch.empty(vox.num_nodes, 7, device=cuda).exponential_()
+    w = torch.randn(vox.num_nodes, 7, device=cuda)
+    calls = []
+    orig = ops.gemm_gn_bwd
+    monkeypatch.setattr(ops, "gemm_gn_bwd", lambda *a: calls.append(1) or orig(*a))
+    out = {}
+    ops._GN_HINTS.clear()  # hints of earlier tests' forwards whose backward never ran
+    for epi in (True, False):
+        monkeypatch.setattr(ops, "_GN_EPI", epi)
+        G.rng = RNG("fixed", seed=3)
+        flat_g.zero_grad()
+        with gemm_precision_scope(precision):
+            logits, _, soft_g = G(loc, vox, z, noise=noise)
+            with ops.direct_param_grads(), ops.deferred_param_folds(cuda):
+                ((logits * w).sum() + (soft_g * w).sum()).backward()
+        torch.cuda.synchronize()
+        out[epi] = flat_g.grad.clone()
+        assert not ops._GN_HINTS
+    assert vox.num_nodes >= 64 and len(calls) >= 10
+    # bf16: the f32 sums differ in order only (~1e-7), but a downstream operand
+    # rounded to bf16 turns such a difference into a bf16 ulp (2^-8)
+    assert rel_err(out[True], out[False]) < (1e-5 if precision == "f32" else 2e-2)
