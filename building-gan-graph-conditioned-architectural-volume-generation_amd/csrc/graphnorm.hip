@@ -187,15 +187,17 @@ __global__ void __launch_bounds__(kBlock) k_stats_final(const float* __restrict_
   }
 }
 
-// keep_out != NULL: draw the dropout multiplier in-kernel (vg_keep with
-// p_drop, seed, *iter, salt), apply it and store it for the backward.
+// iter != NULL: draw the dropout multiplier in-kernel (vg_keep with p_drop,
+// seed, *iter, salt) and apply it; keep_out != NULL also stores it for the
+// backward (a no-grad forward -- the critic labels -- skips the store).
 __global__ void k_gn_apply(const float* __restrict__ x, long long total, int C, long long seg_elems,
                            const float* __restrict__ w, const float* __restrict__ b,
                            const float* __restrict__ ms, const float* __restrict__ keep,
                            float eps, const float* __restrict__ stats, float* __restrict__ y,
                            float p_drop, unsigned long long seed, const long long* __restrict__ iter,
                            unsigned int salt, float* __restrict__ keep_out) {
-  const long long it = keep_out ? *iter : 0;
+  const bool draw = iter != nullptr;
+  const long long it = draw ? *iter : 0;
   for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
        t += (long long)gridDim.x * blockDim.x) {
     const int c = static_cast<int>(t % C);
@@ -204,9 +206,9 @@ __global__ void k_gn_apply(const float* __restrict__ x, long long total, int C, 
     const float o = x[t] - mu * ms[c];
     const float z = (o / (sd + eps)) * w[c] + b[c];
     float r = z > 0.f ? z : 0.f;
-    if (keep_out) {
+    if (draw) {
       const float k = vg_keep(t, salt, it, seed, p_drop);
-      keep_out[t] = k;
+      if (keep_out) keep_out[t] = k;
       r *= k;
     } else if (keep) {
       r *= keep[t];
@@ -640,9 +642,10 @@ __global__ void k_gn_apply4(const float* __restrict__ x, int quads, int N, int C
   F4 xp = {{0.f, 0.f, 0.f, 0.f}}, kp = {{1.f, 1.f, 1.f, 1.f}};
   if (q0 < quads) {
     xp = ld4(x + 4 * q0);
-    if (!keep_out && keep) kp = ld4(keep + 4 * q0);
+    if (!iter && keep) kp = ld4(keep + 4 * q0);
   }
-  const long long it = keep_out ? *iter : 0;
+  const bool draw = iter != nullptr;
+  const long long it = draw ? *iter : 0;
   stage_cols(sh, w, b, ms, C, stats, 2 * C * S, nullptr, 0);
   for (int q = q0; q < quads; q += gridDim.x * blockDim.x) {
     const int t0 = q * 4;
@@ -652,10 +655,10 @@ __global__ void k_gn_apply4(const float* __restrict__ x, int quads, int N, int C
     const bool first = q == q0;
     const F4 xv = first ? xp : ld4(x + t0);
     F4 k4 = {{1.f, 1.f, 1.f, 1.f}};
-    if (keep_out) {
+    if (draw) {
       const float4 k = vg_keep4_raw(q, salt, it, seed, p_drop);
       k4 = F4{{k.x, k.y, k.z, k.w}};
-      st4(keep_out + t0, k4);
+      if (keep_out) st4(keep_out + t0, k4);
     } else if (keep) {
       k4 = first ? kp : ld4(keep + t0);
     }
@@ -667,7 +670,7 @@ __global__ void k_gn_apply4(const float* __restrict__ x, int quads, int N, int C
       const float o = xv.v[j] - muv.v[j] * mv.v[j];
       const float z = (o / (sdv.v[j] + eps)) * wv.v[j] + bv.v[j];
       r.v[j] = z > 0.f ? z : 0.f;
-      if (keep_out || keep) r.v[j] *= k4.v[j];
+      if (draw || keep) r.v[j] *= k4.v[j];
     }
     st4(y + t0, r);
   }
@@ -819,7 +822,7 @@ extern "C" int vg_graphnorm_fwd_drop(const float* x, int32_t S, int32_t N, int32
                                      const int64_t* iter, uint32_t salt, float eps, float* y,
                                      float* keep_out, float* stats, float* ws, int32_t* sync,
                                      void* stream) {
-  if (!iter || !keep_out || !(p_drop >= 0.f && p_drop < 1.f)) return VG_EINVAL;
+  if (!iter || !(p_drop >= 0.f && p_drop < 1.f)) return VG_EINVAL;  // keep_out NULL: apply, do not store
   return gn_fwd(x, S, N, C, weight, bias, mean_scale, nullptr, eps, y, stats, ws, p_drop, seed,
                 iter, salt, keep_out, sync, stream);
 }

@@ -586,6 +586,7 @@ def graphnorm_relu_dropout_torch(x, weight, bias, mean_scale, keep, eps):
 # the GEMM output, so the sum cannot land in place.  VGAN_GN_EPI=0: off.
 _GN_EPI = os.environ.get("VGAN_GN_EPI", "1") == "1"
 _GN_HINTS = {}
+_STORE_NOGRAD_KEEP = os.environ.get("VGAN_STORE_NOGRAD_KEEP", "0") == "1"
 
 
 class _GnHint:
@@ -625,7 +626,9 @@ class _GraphNormReLUDropout(Function):
     many equal row blocks independently (stacked forwards of one batch)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, mean_scale, keep, eps, spec, segments, hint=False):
+    def forward(ctx, x, weight, bias, mean_scale, keep, eps, spec, segments, grad=True):
+        # grad: grad mode at the call (a backward will follow): leave the
+        # GEMM-epilogue hint; store a dropout mask drawn in-kernel
         x = _f32(x)
         w, b, ms = _f32(weight), _f32(bias), _f32(mean_scale)
         kp = _f32(keep) if keep is not None else None
@@ -643,7 +646,8 @@ class _GraphNormReLUDropout(Function):
         if spec is not None:  # dropout drawn in-kernel (device RNG)
             if tuple(spec.shape) != tuple(x.shape):
                 raise ValueError("graphnorm: dropout spec shape differs from x")
-            kp = torch.empty_like(x)
+            # no backward: apply the mask, do not store it (VGAN_STORE_NOGRAD_KEEP=1: store, A/B knob)
+            kp = torch.empty_like(x) if grad or _STORE_NOGRAD_KEEP else None
             check(LIB.vg_graphnorm_fwd_drop(ptr(x), S, n, c, ptr(w), ptr(b), ptr(ms), float(spec.p), int(spec.seed),
                                             ptr(spec.iter), int(spec.salt) & 0xFFFFFFFF, float(eps), ptr(y), ptr(kp),
                                             ptr(stats), ptr(ws), sync_counter(x.device), stream_handle(x.device)),
@@ -656,7 +660,7 @@ class _GraphNormReLUDropout(Function):
         ctx.params = (weight, bias, mean_scale)
         ctx.save_for_backward(x, weight, bias, mean_scale, kp if kp is not None else x.new_empty(0), stats)
         ctx.hint_key = None
-        if hint and n >= 64 and c % 4 == 0 and any(ctx.needs_input_grad[:4]):
+        if _GN_EPI and grad and n >= 64 and c % 4 == 0 and any(ctx.needs_input_grad[:4]):
             if len(_GN_HINTS) > 256:  # forwards whose backward never ran
                 _GN_HINTS.clear()
             ctx.hint_key = (y.data_ptr(), tuple(y.shape))
@@ -713,10 +717,10 @@ class _GraphNormReLUDropout(Function):
 
 def graphnorm_relu_dropout(x, weight, bias, mean_scale, keep, eps: float = 1e-5, segments: int = 1):
     """keep: dropout multipliers [N, C], a ``vgan.rng.DropSpec`` (drawn in-kernel) or None."""
-    hint = _GN_EPI and torch.is_grad_enabled()  # a backward will run: leave the GEMM-epilogue hint
+    grad = torch.is_grad_enabled()  # a backward may follow (the GEMM-epilogue hint, the stored mask)
     if keep is not None and not isinstance(keep, torch.Tensor):
-        return _GraphNormReLUDropout.apply(x, weight, bias, mean_scale, None, eps, keep, segments, hint)
-    return _GraphNormReLUDropout.apply(x, weight, bias, mean_scale, keep, eps, None, segments, hint)
+        return _GraphNormReLUDropout.apply(x, weight, bias, mean_scale, None, eps, keep, segments, grad)
+    return _GraphNormReLUDropout.apply(x, weight, bias, mean_scale, keep, eps, None, segments, grad)
 
 
 # ------------------------------------------------------ type-matched mean

@@ -223,7 +223,8 @@ int vg_graphnorm_fwd_seg(const float* x, int32_t segments, int32_t rows, int32_t
  * / (1-p) from a counter-based Philox4x32-10 keyed by seed on the counter
  * (element, salt, *iter) -- *iter is read from device memory, so a hipGraph
  * replay draws fresh masks once the caller advances it.  keep_out [S*N, C]
- * receives the multipliers for the backward.  Replaces nn.Dropout(0.2)'s two
+ * receives the multipliers for the backward (NULL: applied, not stored -- a
+ * forward with no backward).  Replaces nn.Dropout(0.2)'s two
  * launches (bernoulli_, div_) at models.py:75,85,195,205. */
 int vg_graphnorm_fwd_drop(const float* x, int32_t segments, int32_t rows, int32_t channels,
                           const float* weight, const float* bias, const float* mean_scale,

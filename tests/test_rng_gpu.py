@@ -34,3 +34,28 @@ def test_counter_and_seed(cuda):
     c = RNG("device", seed=6)
     c.reset()
     assert not torch.equal(c.normal((1000,), cuda), x1)  # another seed
+
+
+@pytest.mark.parametrize("C", [1, 6, 64])
+def test_inkernel_dropout_without_store(cuda, C):
+    """GraphNorm + ReLU + in-kernel dropout (DropSpec) in a no-grad forward
+    applies the same mask without storing it (vg_graphnorm_fwd_drop with
+    keep_out NULL): y is bitwise the grad-mode y, whose stored mask has the
+    Bernoulli(0.8) / 0.8 values."""
+    from vgan import ops
+
+    torch.manual_seed(C)
+    n = 300
+    x = torch.randn(n, C, device=cuda)
+    w, b, ms = torch.rand(C, device=cuda) + 0.5, torch.randn(C, device=cuda), torch.rand(C, device=cuda)
+    r = RNG("device", seed=9)
+    r.reset()
+    spec = r.keep_mask((n, C), 0.2, cuda)
+    xg = x.clone().requires_grad_(True)
+    y_grad = ops.graphnorm_relu_dropout(xg, w, b, ms, spec, 1e-5)
+    with torch.no_grad():
+        y_nograd = ops.graphnorm_relu_dropout(x, w, b, ms, spec, 1e-5)
+    assert torch.equal(y_grad.detach(), y_nograd)
+    keep = y_grad.grad_fn.saved_tensors[4]
+    vals = set(torch.unique(keep).tolist())
+    assert vals <= {0.0, 1.25} and 0.0 in vals and abs(float((keep > 0).float().mean()) - 0.8) < 0.08
