@@ -329,6 +329,79 @@ __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int l
   }
 }
 
+// The plain f32 products (no ATT / GNP epilogue) with 16 waves per 64 x 64
+// tile, one 16 x 16 v_mfma_f32_16x16x4_f32 sub-tile each, instead of 4 waves
+// with a 32 x 32 tile.  The step's products are skinny (K, M <= 128 over
+// 13k-66k rows): k_gemm put 1.5-2.4 waves on a SIMD and its waves spent
+// 50-67 % of their cycles parked on loads (rocprofv3 SQ_WAIT_ANY); the same
+// work in 4x the waves hides that latency.  Same LDS images, double
+// buffering and XCD-aware tile order as k_gemm; same f32 MFMA rate.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <bool BT, int ACT>
+__global__ void __launch_bounds__(1024) k_gemm16(const float* __restrict__ A, int lda,
+                                                 const float* __restrict__ B, int ldb,
+                                                 const float* __restrict__ bias,
+                                                 const float* __restrict__ aux, int ldaux,
+                                                 float* __restrict__ C, int ldc, int N, int M, int K) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * TM * LDP + 2 * TN * LDP];
+  float(*As)[TM][LDP] = reinterpret_cast<float(*)[TM][LDP]>(smem);
+  float(*Bs)[TN][LDP] = reinterpret_cast<float(*)[TN][LDP]>(smem + 2 * TM * LDP);  // Bs[j][k] = op(B)[k][j]
+  constexpr int PER = (TM * TK) / 1024;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wr = wave >> 2, wc = wave & 3;  // 4 x 4 sub-tiles of 16 x 16
+  int tx, ty;
+  tile_xy(tx, ty);
+  const int n0 = tx * TM, m0 = ty * TN;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float ra[PER], rb[PER];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int e = t + 1024 * q;
+      const int row = e / TK, kc = e % TK;
+      const int n = n0 + row, k = k0 + kc;
+      ra[q] = (n < N && k < K) ? A[(size_t)n * lda + k] : 0.f;
+      if (BT) {
+        const int m = m0 + row;
+        rb[q] = (m < M && k < K) ? B[(size_t)m * ldb + k] : 0.f;
+      } else {
+        const int kr = e / TN, j = e % TN;
+        const int m = m0 + j, kk = k0 + kr;
+        rb[q] = (m < M && kk < K) ? B[(size_t)kk * ldb + m] : 0.f;
+      }
+    }
+  };
+  load(0);
+  int buf = 0;
+  for (int k0 = 0; k0 < K; k0 += TK) {
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int e = t + 1024 * q;
+      As[buf][e / TK][e % TK] = ra[q];
+      if (BT) Bs[buf][e / TK][e % TK] = rb[q];
+      else Bs[buf][e % TN][e / TN] = rb[q];
+    }
+    __syncthreads();
+    if (k0 + TK < K) load(k0 + TK);
+    const float* ar = &As[buf][wr * 16 + (lane & 15)][lane >> 4];
+    const float* br = &Bs[buf][wc * 16 + (lane & 15)][lane >> 4];
+#pragma unroll
+    for (int kk = 0; kk < TK; kk += 4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ar[kk], br[kk], acc, 0, 0, 0);
+    buf ^= 1;
+  }
+  const int m = m0 + wc * 16 + (lane & 15);
+  const float bv = (bias && m < M) ? bias[m] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int n = n0 + wr * 16 + 4 * (lane >> 4) + r;
+    if (n < N && m < M) {
+      const float av = ACT == 3 ? aux[(size_t)n * ldaux + m] : 0.f;
+      C[(size_t)n * ldc + m] = act_fn<ACT>(acc[r] + bv, av);
+    }
+  }
+}
+
 // Y = leaky_relu(LayerNorm(A . B^T + bias; gamma, beta, eps), slope) with the
 // LayerNorm in the epilogue: the [Linear -> LayerNorm -> LeakyReLU(0.2)]
 // blocks of the generator's MLPs (models.py:33-47, 49-66, 92-113).  A
@@ -1053,8 +1126,16 @@ static int gemm(const float* A, int32_t lda, const float* B, int32_t ldb, int32_
   if (N == 0) return 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
   dim3 grid((N + TM - 1) / TM, (M + TN - 1) / TN);
-#define VG_G(BT, ACT) \
-  k_gemm<BT, ACT, false, BF><<<grid, 256, 0, s>>>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, N, M, K)
+#ifndef VG_GEMM16
+#define VG_GEMM16 1  // f32: k_gemm16 (16 waves of 16 x 16 MFMA tiles); 0: k_gemm (A/B)
+#endif
+#define VG_G(BT, ACT)                                                                                      \
+  do {                                                                                                     \
+    if (!BF && VG_GEMM16)                                                                                  \
+      k_gemm16<BT, ACT><<<grid, 1024, 0, s>>>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, N, M, K);         \
+    else                                                                                                   \
+      k_gemm<BT, ACT, false, BF><<<grid, 256, 0, s>>>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, N, M, K); \
+  } while (0)
   if (b_trans) {
     if (act == 0) VG_G(true, 0); else if (act == 1) VG_G(true, 1);
     else if (act == 2) VG_G(true, 2); else VG_G(true, 3);
