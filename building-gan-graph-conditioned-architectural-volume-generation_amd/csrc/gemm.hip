@@ -338,22 +338,61 @@ __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int l
 // buffering and XCD-aware tile order as k_gemm; same f32 MFMA rate.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-template <bool BT, int ACT>
+// ATT, GNP as in k_gemm (the attention projections / the GraphNorm-backward
+// tile partials in the epilogue).  BF: bf16 operands through
+// v_mfma_f32_16x16x32_bf16 -- the f32 LDS images are converted when read
+// (lane l: row l & 15, k = 8 (l >> 4) + j).
+template <bool BT, int ACT, bool ATT = false, bool BF = false, bool GNP = false>
 __global__ void __launch_bounds__(1024) k_gemm16(const float* __restrict__ A, int lda,
                                                  const float* __restrict__ B, int ldb,
                                                  const float* __restrict__ bias,
                                                  const float* __restrict__ aux, int ldaux,
-                                                 float* __restrict__ C, int ldc, int N, int M, int K) {
-  __shared__ __attribute__((aligned(16))) float smem[2 * TM * LDP + 2 * TN * LDP];
-  float(*As)[TM][LDP] = reinterpret_cast<float(*)[TM][LDP]>(smem);
-  float(*Bs)[TN][LDP] = reinterpret_cast<float(*)[TN][LDP]>(smem + 2 * TM * LDP);  // Bs[j][k] = op(B)[k][j]
+                                                 float* __restrict__ C, int ldc, int N, int M, int K,
+                                                 const float* __restrict__ att_s = nullptr,
+                                                 const float* __restrict__ att_d = nullptr,
+                                                 float* __restrict__ a_src = nullptr,
+                                                 float* __restrict__ a_dst = nullptr,
+                                                 const GnpDesc gn = GnpDesc{}) {
+  constexpr int LDQ = BF ? TK + 4 : LDP;  // BF: 16-B aligned rows for the 8-float reads
+  __shared__ __attribute__((aligned(16))) float smem[2 * TM * LDQ + 2 * TN * LDQ];
+  float(*As)[TM][LDQ] = reinterpret_cast<float(*)[TM][LDQ]>(smem);
+  float(*Bs)[TN][LDQ] = reinterpret_cast<float(*)[TN][LDQ]>(smem + 2 * TM * LDQ);  // Bs[j][k] = op(B)[k][j]
   constexpr int PER = (TM * TK) / 1024;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wr = wave >> 2, wc = wave & 3;  // 4 x 4 sub-tiles of 16 x 16
   int tx, ty;
   tile_xy(tx, ty);
   const int n0 = tx * TM, m0 = ty * TN;
+  const int mc = m0 + wc * 16 + (lane & 15);  // this lane's output column
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  // GNP: the epilogue's GraphNorm operands (the lane's 4 rows of x / keep, the
+  // two segments' statistics, the column's parameters) loaded before the K loop
+  float gx_[GNP ? 4 : 1], gk_[GNP ? 4 : 1];
+  float gmu[2] = {0.f, 0.f}, gsd[2] = {1.f, 1.f}, gw_ = 0.f, gb_ = 0.f, gms_ = 0.f;
+  int gbound = 0;
+  if constexpr (GNP) {
+    const int seg0 = n0 / gn.seg_rows;
+    gbound = (seg0 + 1) * gn.seg_rows;
+    if (mc < M) {
+      gw_ = gn.w[mc];
+      gb_ = gn.b[mc];
+      gms_ = gn.ms[mc];
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        if (q == 0 || gbound < N) {
+          const float* st = gn.stats + (size_t)(seg0 + q) * 2 * M;
+          gmu[q] = st[mc];
+          gsd[q] = st[M + mc] + gn.eps;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + wr * 16 + 4 * (lane >> 4) + r;
+      const bool ok = n < N && mc < M;
+      gx_[r] = ok ? gn.x[(size_t)n * M + mc] : 0.f;
+      gk_[r] = ok && gn.keep ? gn.keep[(size_t)n * M + mc] : 1.f;
+    }
+  }
   float ra[PER], rb[PER];
   auto load = [&](int k0) {
 #pragma unroll
@@ -384,20 +423,118 @@ __global__ void __launch_bounds__(1024) k_gemm16(const float* __restrict__ A, in
     }
     __syncthreads();
     if (k0 + TK < K) load(k0 + TK);
-    const float* ar = &As[buf][wr * 16 + (lane & 15)][lane >> 4];
-    const float* br = &Bs[buf][wc * 16 + (lane & 15)][lane >> 4];
+    if constexpr (BF) {
+      const float4* ap = reinterpret_cast<const float4*>(&As[buf][wr * 16 + (lane & 15)][8 * (lane >> 4)]);
+      const float4* bp = reinterpret_cast<const float4*>(&Bs[buf][wc * 16 + (lane & 15)][8 * (lane >> 4)]);
+      const float4 a0 = ap[0], a1 = ap[1], b0 = bp[0], b1 = bp[1];
+      bf16x8 ha, hb;
+      ha[0] = static_cast<__bf16>(a0.x); ha[1] = static_cast<__bf16>(a0.y);
+      ha[2] = static_cast<__bf16>(a0.z); ha[3] = static_cast<__bf16>(a0.w);
+      ha[4] = static_cast<__bf16>(a1.x); ha[5] = static_cast<__bf16>(a1.y);
+      ha[6] = static_cast<__bf16>(a1.z); ha[7] = static_cast<__bf16>(a1.w);
+      hb[0] = static_cast<__bf16>(b0.x); hb[1] = static_cast<__bf16>(b0.y);
+      hb[2] = static_cast<__bf16>(b0.z); hb[3] = static_cast<__bf16>(b0.w);
+      hb[4] = static_cast<__bf16>(b1.x); hb[5] = static_cast<__bf16>(b1.y);
+      hb[6] = static_cast<__bf16>(b1.z); hb[7] = static_cast<__bf16>(b1.w);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ha, hb, acc, 0, 0, 0);
+    } else {
+      const float* ar = &As[buf][wr * 16 + (lane & 15)][lane >> 4];
+      const float* br = &Bs[buf][wc * 16 + (lane & 15)][lane >> 4];
 #pragma unroll
-    for (int kk = 0; kk < TK; kk += 4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ar[kk], br[kk], acc, 0, 0, 0);
+      for (int kk = 0; kk < TK; kk += 4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ar[kk], br[kk], acc, 0, 0, 0);
+    }
     buf ^= 1;
   }
-  const int m = m0 + wc * 16 + (lane & 15);
-  const float bv = (bias && m < M) ? bias[m] : 0.f;
+  const float bv = (bias && mc < M) ? bias[mc] : 0.f;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int n = n0 + wr * 16 + 4 * (lane >> 4) + r;
-    if (n < N && m < M) {
-      const float av = ACT == 3 ? aux[(size_t)n * ldaux + m] : 0.f;
-      C[(size_t)n * ldc + m] = act_fn<ACT>(acc[r] + bv, av);
+    if (n < N && mc < M) {
+      const float av = ACT == 3 ? aux[(size_t)n * ldaux + mc] : 0.f;
+      C[(size_t)n * ldc + mc] = act_fn<ACT>(acc[r] + bv, av);
+    }
+  }
+  if constexpr (GNP) {
+    // column partials of gz = g_y [z > 0] keep and gz * xhat per segment slot:
+    // the lane's 4 rows in order, the 4 lanes of the column (xor 16, 32),
+    // then the 4 row waves of the column through LDS in order: deterministic
+    float pa[2] = {0.f, 0.f}, pb[2] = {0.f, 0.f};
+    if (mc < M) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wr * 16 + 4 * (lane >> 4) + r;
+        if (n < N) {
+          const int sl = n >= gbound;
+          const float xh = (gx_[r] - (sl ? gmu[1] : gmu[0]) * gms_) / (sl ? gsd[1] : gsd[0]);
+          const float gz = xh * gw_ + gb_ > 0.f ? acc[r] * gk_[r] : 0.f;
+          if (sl) {
+            pa[1] += gz;
+            pb[1] = fmaf(gz, xh, pb[1]);
+          } else {
+            pa[0] += gz;
+            pb[0] = fmaf(gz, xh, pb[0]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      pa[q] += __shfl_xor(pa[q], 16, 64);
+      pb[q] += __shfl_xor(pb[q], 16, 64);
+      pa[q] += __shfl_xor(pa[q], 32, 64);
+      pb[q] += __shfl_xor(pb[q], 32, 64);
+    }
+    __syncthreads();  // every wave is done with the last K-tile's LDS images
+    float* red = smem;  // [wr][64 columns][4]
+    if (lane < 16) {
+      float* rp = red + ((wr * 64) + wc * 16 + lane) * 4;
+      rp[0] = pa[0];
+      rp[1] = pb[0];
+      rp[2] = pa[1];
+      rp[3] = pb[1];
+    }
+    __syncthreads();
+    if (wr == 0 && lane < 16 && mc < M) {
+      float s[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int w = 0; w < 4; ++w) {
+        const float* rp = red + ((w * 64) + wc * 16 + lane) * 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s[q] += rp[q];
+      }
+      float* tp = gn.tpart + (size_t)tx * 2 * M * 2;
+      tp[(size_t)mc * 2] = s[0];
+      tp[(size_t)mc * 2 + 1] = s[1];
+      tp[(size_t)(M + mc) * 2] = s[2];
+      tp[(size_t)(M + mc) * 2 + 1] = s[3];
+    }
+  }
+  if constexpr (ATT) {
+    // the 64 x 64 tile staged in LDS, then 16 threads per row dot 4 columns
+    // each with att_s / att_d and combine over the 16 lanes
+    float(*Ct)[TN + 1] = reinterpret_cast<float(*)[TN + 1]>(smem);
+    __syncthreads();  // every wave is done with the last K-tile's images
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Ct[wr * 16 + 4 * (lane >> 4) + r][wc * 16 + (lane & 15)] = acc[r] + bv;
+    __syncthreads();
+    const int row = t >> 4, q = t & 15;
+    float ss = 0.f, sd = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = q * 4 + j;
+      if (c < M) {
+        const float v = Ct[row][c];
+        ss = fmaf(v, att_s[c], ss);
+        sd = fmaf(v, att_d[c], sd);
+      }
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      ss += __shfl_xor(ss, o, 64);
+      sd += __shfl_xor(sd, o, 64);
+    }
+    if (q == 0 && n0 + row < N) {
+      a_src[n0 + row] = ss;
+      a_dst[n0 + row] = sd;
     }
   }
 }
@@ -1127,12 +1264,17 @@ static int gemm(const float* A, int32_t lda, const float* B, int32_t ldb, int32_
   hipStream_t s = static_cast<hipStream_t>(stream);
   dim3 grid((N + TM - 1) / TM, (M + TN - 1) / TN);
 #ifndef VG_GEMM16
-#define VG_GEMM16 1  // f32: k_gemm16 (16 waves of 16 x 16 MFMA tiles); 0: k_gemm (A/B)
+// k_gemm16 (16 waves of 16 x 16 MFMA tiles) instead of k_gemm, per product
+// kind (A/B bits): 1 plain f32, 2 the attention projections, 4 the
+// GraphNorm-backward partials, 8 bf16 operands.  Bit 8 is off: converting the
+// f32 LDS images to bf16 at read time measured slower than k_gemm's bf16
+// staging (bf16 step 8.46 vs 8.31 ms, profiles/r02_ab_gemm16_att_gnp.txt)
+#define VG_GEMM16 7
 #endif
 #define VG_G(BT, ACT)                                                                                      \
   do {                                                                                                     \
-    if (!BF && VG_GEMM16)                                                                                  \
-      k_gemm16<BT, ACT><<<grid, 1024, 0, s>>>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, N, M, K);         \
+    if ((VG_GEMM16 & (BF ? 8 : 1)) != 0)                                                                   \
+      k_gemm16<BT, ACT, false, BF><<<grid, 1024, 0, s>>>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, N, M, K); \
     else                                                                                                   \
       k_gemm<BT, ACT, false, BF><<<grid, 256, 0, s>>>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, N, M, K); \
   } while (0)
@@ -1159,8 +1301,12 @@ static int gemm_gn_bwd(const float* A, int32_t lda, const float* B, int32_t ldb,
   hipStream_t s = static_cast<hipStream_t>(stream);
   dim3 grid((N + TM - 1) / TM, (M + TN - 1) / TN);
   const GnpDesc gn{gn_x, keep, stats, weight, bias, mean_scale, eps, seg_rows, tpart};
-  k_gemm<false, 0, false, BF, true><<<grid, 256, 0, s>>>(A, lda, B, ldb, nullptr, nullptr, 0, C, ldc, N, M, K,
-                                                         nullptr, nullptr, nullptr, nullptr, gn);
+  if ((VG_GEMM16 & 4) && (!BF || (VG_GEMM16 & 8)))
+    k_gemm16<false, 0, false, BF, true><<<grid, 1024, 0, s>>>(A, lda, B, ldb, nullptr, nullptr, 0, C, ldc, N, M, K,
+                                                             nullptr, nullptr, nullptr, nullptr, gn);
+  else
+    k_gemm<false, 0, false, BF, true><<<grid, 256, 0, s>>>(A, lda, B, ldb, nullptr, nullptr, 0, C, ldc, N, M, K,
+                                                           nullptr, nullptr, nullptr, nullptr, gn);
   VG_CHECK_LAUNCH();
   return 0;
 }
@@ -1468,8 +1614,12 @@ static int gat_lin_att(const float* X, int32_t ldx, const float* W, int32_t N,
     VG_CHECK_LAUNCH();
     return 0;
   }
-  k_gemm<true, 0, true, BF><<<dim3((N + TM - 1) / TM, 1), 256, 0, s>>>(
-      X, ldx, W, Cin, nullptr, nullptr, 0, H, C, N, C, Cin, att_src, att_dst, a_src, a_dst);
+  if ((VG_GEMM16 & 2) && (!BF || (VG_GEMM16 & 8)))
+    k_gemm16<true, 0, true, BF><<<dim3((N + TM - 1) / TM, 1), 1024, 0, s>>>(
+        X, ldx, W, Cin, nullptr, nullptr, 0, H, C, N, C, Cin, att_src, att_dst, a_src, a_dst);
+  else
+    k_gemm<true, 0, true, BF><<<dim3((N + TM - 1) / TM, 1), 256, 0, s>>>(
+        X, ldx, W, Cin, nullptr, nullptr, 0, H, C, N, C, Cin, att_src, att_dst, a_src, a_dst);
   VG_CHECK_LAUNCH();
   return 0;
 }
