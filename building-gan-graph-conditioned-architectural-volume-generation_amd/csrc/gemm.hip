@@ -58,6 +58,9 @@ __device__ __forceinline__ f32x16 mfma_bf(const __bf16* a, const __bf16* b, f32x
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(a),
                                                  *reinterpret_cast<const bf16x8*>(b), acc, 0, 0, 0);
 }
+#ifndef VG_LN16
+#define VG_LN16 1  // f32 k_gemm_ln16 (16 waves of 16 x 16 MFMA tiles); 0: k_gemm_ln (A/B)
+#endif
 #ifndef VG_LN_TM32
 #define VG_LN_TM32 1
 #endif
@@ -539,6 +542,95 @@ __global__ void __launch_bounds__(1024) k_gemm16(const float* __restrict__ A, in
   }
 }
 
+// k_gemm_ln's epilogue over the staged tile Ct [TMR][TN * NT + 1] (bias and
+// addend included): the attention projections (ATT) or the row statistics,
+// then the normalised, activated rows stored coalesced.  NTH threads.
+template <int NT, int TMR, bool ATT, int NTH>
+__device__ __forceinline__ void ln_tile_epilogue(const float* Ct, float* s_mu, float* s_rs, int t, int n0, int N,
+                                                 int M, const float* __restrict__ gamma,
+                                                 const float* __restrict__ beta, float eps, float slope,
+                                                 float* __restrict__ H, float* __restrict__ Y,
+                                                 float* __restrict__ mean, float* __restrict__ rstd,
+                                                 const float* __restrict__ att_s, const float* __restrict__ att_d,
+                                                 float* __restrict__ a_src, float* __restrict__ a_dst, int ldy) {
+  constexpr int TNC = TN * NT;
+  constexpr int CT = TNC + 1;
+  if constexpr (ATT) {  // attention projections: TPR threads per row, then coalesced H stores
+    constexpr int TPR = NTH / TMR;
+    constexpr int CPT = TNC / TPR;
+    const int row = t / TPR, q = t % TPR;
+    const float* cr = Ct + row * CT + q * CPT;
+    float ss = 0.f, sd = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int c = q * CPT + i;
+      if (c < M) {
+        ss = fmaf(cr[i], att_s[c], ss);
+        sd = fmaf(cr[i], att_d[c], sd);
+      }
+    }
+#pragma unroll
+    for (int off = 1; off < TPR; off <<= 1) {
+      ss += __shfl_xor(ss, off, 64);
+      sd += __shfl_xor(sd, off, 64);
+    }
+    if (q == 0 && n0 + row < N) {
+      a_src[n0 + row] = ss;
+      a_dst[n0 + row] = sd;
+    }
+    for (int idx = t; idx < TMR * TNC; idx += NTH) {
+      const int r = idx / TNC, c = idx % TNC, n = n0 + r;
+      if (c < M && n < N) H[(size_t)n * M + c] = Ct[r * CT + c];
+    }
+    return;
+  }
+  {  // row statistics: TPR threads per row, two-pass
+    constexpr int TPR = NTH / TMR;
+    constexpr int CPT = TNC / TPR;
+    const int row = t / TPR, q = t % TPR;
+    const float* cr = Ct + row * CT + q * CPT;
+    float v[CPT];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      v[i] = q * CPT + i < M ? cr[i] : 0.f;
+      s += v[i];
+    }
+#pragma unroll
+    for (int off = 1; off < TPR; off <<= 1) s += __shfl_xor(s, off, 64);
+    const float mu = s / static_cast<float>(M);
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i)
+      if (q * CPT + i < M) {
+        const float d = v[i] - mu;
+        ss = fmaf(d, d, ss);
+      }
+#pragma unroll
+    for (int off = 1; off < TPR; off <<= 1) ss += __shfl_xor(ss, off, 64);
+    const float rs = rsqrtf(ss / static_cast<float>(M) + eps);
+    if (q == 0) {
+      s_mu[row] = mu;
+      s_rs[row] = rs;
+      if (mean && n0 + row < N) {
+        mean[n0 + row] = mu;
+        rstd[n0 + row] = rs;
+      }
+    }
+  }
+  __syncthreads();
+  // normalise + activate, lanes along the columns (coalesced row stores)
+  for (int idx = t; idx < TMR * TNC; idx += NTH) {
+    const int row = idx / TNC, c = idx % TNC, n = n0 + row;
+    if (c < M && n < N) {
+      const float v = Ct[row * CT + c];
+      if (H) H[(size_t)n * M + c] = v;
+      const float z = fmaf((v - s_mu[row]) * s_rs[row], gamma[c], beta[c]);
+      Y[(size_t)n * ldy + c] = z > 0.f ? z : z * slope;
+    }
+  }
+}
+
 // Y = leaky_relu(LayerNorm(A . B^T + bias; gamma, beta, eps), slope) with the
 // LayerNorm in the epilogue: the [Linear -> LayerNorm -> LeakyReLU(0.2)]
 // blocks of the generator's MLPs (models.py:33-47, 49-66, 92-113).  A
@@ -702,80 +794,132 @@ __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, in
     }
   }
   __syncthreads();
-  if constexpr (ATT) {  // attention projections: TPR threads per row, then coalesced H stores
-    constexpr int TPR = 256 / TMR;
-    constexpr int CPT = TNC / TPR;
-    const int row = t / TPR, q = t % TPR;
-    const float* cr = Ct + row * CT + q * CPT;
-    float ss = 0.f, sd = 0.f;
+  ln_tile_epilogue<NT, TMR, ATT, 256>(Ct, s_mu, s_rs, t, n0, N, M, gamma, beta, eps, slope, H, Y, mean, rstd, att_s,
+                                      att_d, a_src, a_dst, ldy);
+}
+
+// k_gemm_ln with 16 waves (f32): 16 x 16 v_mfma_f32_16x16x4f32 sub-tiles,
+// TMR / 16 row waves x 16 / (TMR / 16) column waves, NJ sub-tiles per wave
+// (as k_gemm16 against k_gemm: 4x the waves to cover the global -> LDS
+// latency of these K <= 128 products).  Same arguments and epilogue.
+template <int NT, int TMR = TM, bool ATT = false, bool MS = false>
+__global__ void __launch_bounds__(1024) k_gemm_ln16(const float* __restrict__ A, int lda,
+                                                    const float* __restrict__ B, int ldb,
+                                                    const float* __restrict__ bias, int N, int M, int K,
+                                                    const float* __restrict__ gamma,
+                                                    const float* __restrict__ beta, float eps,
+                                                    float slope, float* __restrict__ H,
+                                                    float* __restrict__ Y, float* __restrict__ mean,
+                                                    float* __restrict__ rstd,
+                                                    const float* __restrict__ att_s = nullptr,
+                                                    const float* __restrict__ att_d = nullptr,
+                                                    float* __restrict__ a_src = nullptr,
+                                                    float* __restrict__ a_dst = nullptr, int ldy = 0,
+                                                    const MsDesc ms = MsDesc{}) {
+  if (ldy == 0) ldy = M;
+  constexpr int TNC = TN * NT;
+  constexpr int CT = TNC + 1;
+  constexpr int WRW = TMR / 16, WCW = 16 / WRW;  // row / column waves
+  constexpr int NJ = TNC / (16 * WCW);           // 16-column sub-tiles per wave
+  static_assert(NJ >= 1 && WRW * WCW == 16, "tile shape");
+  __shared__ __attribute__((aligned(16))) float smem[2 * TMR * LDP + 2 * TNC * LDP];
+  __shared__ float s_mu[TMR], s_rs[TMR];
+  float(*As)[TMR][LDP] = reinterpret_cast<float(*)[TMR][LDP]>(smem);
+  float(*Bs)[TNC][LDP] = reinterpret_cast<float(*)[TNC][LDP]>(smem + 2 * TMR * LDP);
+  constexpr int PA = (TMR * TK) / 1024, PB = (TNC * TK) / 1024;
+  static_assert(PA >= 1 && PB >= 1, "tile shape");
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wr = wave / WCW, wc = wave % WCW;
+  int tx, ty;
+  tile_xy(tx, ty);
+  const int n0 = tx * TMR;
+  f32x4 acc[NJ];
 #pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int c = q * CPT + i;
-      if (c < M) {
-        ss = fmaf(cr[i], att_s[c], ss);
-        sd = fmaf(cr[i], att_d[c], sd);
-      }
+  for (int j = 0; j < NJ; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto chunk_src = [&](int k0, const float*& asrc, int& ald, int& acol, int& wcol) {
+    asrc = A;
+    ald = lda;
+    acol = k0;
+    wcol = k0;
+    if constexpr (MS) {
+      int sidx = 0;
+#pragma unroll
+      for (int i = 0; i < kMaxSrc - 1; ++i)
+        if (i < ms.nsrc - 1 && k0 >= ms.kend[i]) sidx = i + 1;
+      const int kb = sidx > 0 ? ms.kend[sidx - 1] : 0;
+      asrc = ms.p[sidx];
+      ald = ms.ld[sidx];
+      acol = k0 - kb;
+      wcol = ms.wcol[sidx] + (k0 - kb);
+    }
+  };
+  float ra[PA], rb[PB];
+  auto load = [&](int k0) {
+    const float* asrc;
+    int ald, acol, wcol;
+    chunk_src(k0, asrc, ald, acol, wcol);
+#pragma unroll
+    for (int q = 0; q < PA; ++q) {
+      const int e = t + 1024 * q;
+      const int n = n0 + e / TK, kc = e % TK;
+      ra[q] = (n < N && k0 + kc < K) ? asrc[(size_t)n * ald + acol + kc] : 0.f;
     }
 #pragma unroll
-    for (int off = 1; off < TPR; off <<= 1) {
-      ss += __shfl_xor(ss, off, 64);
-      sd += __shfl_xor(sd, off, 64);
+    for (int q = 0; q < PB; ++q) {
+      const int e = t + 1024 * q;
+      const int m = e / TK, kc = e % TK;
+      rb[q] = (m < M && k0 + kc < K) ? B[(size_t)m * ldb + wcol + kc] : 0.f;
     }
-    if (q == 0 && n0 + row < N) {
-      a_src[n0 + row] = ss;
-      a_dst[n0 + row] = sd;
+  };
+  load(0);
+  int buf = 0;
+  for (int k0 = 0; k0 < K; k0 += TK) {
+#pragma unroll
+    for (int q = 0; q < PA; ++q) {
+      const int e = t + 1024 * q;
+      As[buf][e / TK][e % TK] = ra[q];
     }
-    for (int idx = t; idx < TMR * TNC; idx += 256) {
-      const int r = idx / TNC, c = idx % TNC, n = n0 + r;
-      if (c < M && n < N) H[(size_t)n * M + c] = Ct[r * CT + c];
+#pragma unroll
+    for (int q = 0; q < PB; ++q) {
+      const int e = t + 1024 * q;
+      Bs[buf][e / TK][e % TK] = rb[q];
     }
-    return;
+    __syncthreads();
+    if (k0 + TK < K) load(k0 + TK);
+    const float* ar = &As[buf][wr * 16 + (lane & 15)][lane >> 4];
+#pragma unroll
+    for (int kk = 0; kk < TK; kk += 4)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+            ar[kk], Bs[buf][j * 16 * WCW + wc * 16 + (lane & 15)][(lane >> 4) + kk], acc[j], 0, 0, 0);
+    buf ^= 1;
   }
-  {  // row statistics: TPR threads per row, two-pass
-    constexpr int TPR = 256 / TMR;
-    constexpr int CPT = TNC / TPR;
-    const int row = t / TPR, q = t % TPR;
-    const float* cr = Ct + row * CT + q * CPT;
-    float v[CPT];
-    float s = 0.f;
+  // stage the full-width tile (+ bias, + addend) in LDS
+  __syncthreads();
+  float* Ct = smem;
+  const int add0 = MS && ms.add ? n0 % ms.add_rows : 0;
 #pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      v[i] = q * CPT + i < M ? cr[i] : 0.f;
-      s += v[i];
-    }
+  for (int j = 0; j < NJ; ++j) {
+    const int c = j * 16 * WCW + wc * 16 + (lane & 15);
+    const float bv = (bias && c < M) ? bias[c] : 0.f;
 #pragma unroll
-    for (int off = 1; off < TPR; off <<= 1) s += __shfl_xor(s, off, 64);
-    const float mu = s / static_cast<float>(M);
-    float ss = 0.f;
-#pragma unroll
-    for (int i = 0; i < CPT; ++i)
-      if (q * CPT + i < M) {
-        const float d = v[i] - mu;
-        ss = fmaf(d, d, ss);
+    for (int r = 0; r < 4; ++r) {
+      const int rl = wr * 16 + 4 * (lane >> 4) + r;
+      float v = acc[j][r] + bv;
+      if constexpr (MS) {  // addend row (n0 + rl) mod add_rows; rl < TMR <= add_rows
+        if (ms.add && n0 + rl < N && c < M) {
+          int ar2 = add0 + rl;
+          if (ar2 >= ms.add_rows) ar2 -= ms.add_rows;
+          v += ms.add[(size_t)ar2 * ms.ld_add + c];
+        }
       }
-#pragma unroll
-    for (int off = 1; off < TPR; off <<= 1) ss += __shfl_xor(ss, off, 64);
-    const float rs = rsqrtf(ss / static_cast<float>(M) + eps);
-    if (q == 0) {
-      s_mu[row] = mu;
-      s_rs[row] = rs;
-      if (mean && n0 + row < N) {
-        mean[n0 + row] = mu;
-        rstd[n0 + row] = rs;
-      }
+      Ct[rl * CT + c] = v;
     }
   }
   __syncthreads();
-  // normalise + activate, lanes along the columns (coalesced row stores)
-  for (int idx = t; idx < TMR * TNC; idx += 256) {
-    const int row = idx / TNC, c = idx % TNC, n = n0 + row;
-    if (c < M && n < N) {
-      const float v = Ct[row * CT + c];
-      if (H) H[(size_t)n * M + c] = v;
-      const float z = fmaf((v - s_mu[row]) * s_rs[row], gamma[c], beta[c]);
-      Y[(size_t)n * ldy + c] = z > 0.f ? z : z * slope;
-    }
-  }
+  ln_tile_epilogue<NT, TMR, ATT, 1024>(Ct, s_mu, s_rs, t, n0, N, M, gamma, beta, eps, slope, H, Y, mean, rstd, att_s,
+                                       att_d, a_src, a_dst, ldy);
 }
 
 // part[chunk][M][K] = A[chunk rows]^T . B[chunk rows];  pdb[chunk][M] = column sums of A.
@@ -1516,7 +1660,17 @@ static int gemm_ln_act(const float* A, int32_t lda, const float* W, int32_t N, i
   if (N == 0) return 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const dim3 grid((N + TM - 1) / TM, 1);
-  if (M <= TN)
+  if (!BF && VG_LN16) {
+    if (M <= TN)
+      k_gemm_ln16<1, TM><<<grid, 1024, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma, beta, eps, slope, H, Y, mean,
+                                              rstd);
+    else if (VG_LN_TM32)
+      k_gemm_ln16<2, 32><<<dim3((N + 31) / 32, 1), 1024, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma, beta, eps,
+                                                                slope, H, Y, mean, rstd);
+    else
+      k_gemm_ln16<2, TM><<<grid, 1024, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma, beta, eps, slope, H, Y, mean,
+                                              rstd);
+  } else if (M <= TN)
     k_gemm_ln<1, TM, false, false, BF><<<grid, 256, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma, beta, eps, slope,
                                                              H, Y, mean, rstd);
   else if (VG_LN_TM32)
@@ -1570,9 +1724,14 @@ static int gemm_ln_act_ms(const vg_asrc* src, int32_t nsrc, const float* W, int3
   d.add_rows = add_rows;
   if (N == 0) return 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  k_gemm_ln<2, 32, false, true, BF><<<dim3((N + 31) / 32, 1), 256, 0, s>>>(
-      nullptr, 0, W, ldw, bias, N, M, K, gamma, beta, eps, slope, nullptr, Y, nullptr, nullptr, nullptr, nullptr,
-      nullptr, nullptr, ldy, d);
+  if (!BF && VG_LN16)
+    k_gemm_ln16<2, 32, false, true><<<dim3((N + 31) / 32, 1), 1024, 0, s>>>(
+        nullptr, 0, W, ldw, bias, N, M, K, gamma, beta, eps, slope, nullptr, Y, nullptr, nullptr, nullptr, nullptr,
+        nullptr, nullptr, ldy, d);
+  else
+    k_gemm_ln<2, 32, false, true, BF><<<dim3((N + 31) / 32, 1), 256, 0, s>>>(
+        nullptr, 0, W, ldw, bias, N, M, K, gamma, beta, eps, slope, nullptr, Y, nullptr, nullptr, nullptr, nullptr,
+        nullptr, nullptr, ldy, d);
   VG_CHECK_LAUNCH();
   return 0;
 }
@@ -1608,9 +1767,14 @@ static int gat_lin_att(const float* X, int32_t ldx, const float* W, int32_t N,
     return vg_gat_att(H, N, C, att_src, att_dst, a_src, a_dst, stream);
   }
   if (C > TN) {  // whole 128-column rows per block, projections in the epilogue
-    k_gemm_ln<2, 32, true, false, BF><<<dim3((N + 31) / 32, 1), 256, 0, s>>>(
-        X, ldx, W, Cin, nullptr, N, C, Cin, nullptr, nullptr, 0.f, 0.f, H, nullptr, nullptr, nullptr, att_src,
-        att_dst, a_src, a_dst);
+    if (!BF && VG_LN16)
+      k_gemm_ln16<2, 32, true><<<dim3((N + 31) / 32, 1), 1024, 0, s>>>(
+          X, ldx, W, Cin, nullptr, N, C, Cin, nullptr, nullptr, 0.f, 0.f, H, nullptr, nullptr, nullptr, att_src,
+          att_dst, a_src, a_dst);
+    else
+      k_gemm_ln<2, 32, true, false, BF><<<dim3((N + 31) / 32, 1), 256, 0, s>>>(
+          X, ldx, W, Cin, nullptr, N, C, Cin, nullptr, nullptr, 0.f, 0.f, H, nullptr, nullptr, nullptr, att_src,
+          att_dst, a_src, a_dst);
     VG_CHECK_LAUNCH();
     return 0;
   }
