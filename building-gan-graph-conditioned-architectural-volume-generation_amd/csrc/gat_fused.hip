@@ -67,6 +67,98 @@ __device__ __forceinline__ void load_param(Vec<CPL>& r, const float* __restrict_
   load_row<CPL, false>(r, p, c0, C);  // parameters live at arbitrary offsets of the flat buffer
 }
 
+// GraphNorm column partials of the rows a workgroup aggregated: the forward
+// statistics of the GraphNorm that follows every GATConv (models.py:73-75,
+// 193-195; graphnorm.hip's k_stats_partial re-read the whole output for them).
+// Per column (count, mean, M2) of the block's rows, two passes over the row
+// values still in registers: sums by xor-shuffles across the wave's L-lane row
+// groups then across the 4 waves in order through LDS, the mean, then the
+// squared deviations the same way (deterministic).  Slot 0 is the segment of
+// the block's first row, slot 1 the next one (reduced and written only when the
+// block straddles one: seg_rows >= the block's rows, vg_gat_gnp_rows).
+// gnp [blocks][2][ldc][3], column cb + c.  v: this lane's CPL columns c0.. of
+// its row (lanes past C hold anything: their columns are not written).
+// (A first form folded each column serially over the block's rows with
+// Welford updates in one wave: +4 us per launch, slower than the separate
+// statistics pass it replaced.)
+template <int L, int CPL>
+__device__ __forceinline__ void gnp_block(const float (&v)[CPL], int row, int lb, int N, int seg_rows, int C,
+                                          int c0, int cb, int ldc, float* __restrict__ gnp) {
+  constexpr int G = kBlock / L, W = L * CPL;
+  __shared__ float red[kBlock / 64][2][W];
+  __shared__ float mv[2][W];
+  const int row0 = lb * G;
+  const int bound = (row0 / seg_rows + 1) * seg_rows;
+  const bool straddle = row0 + G > bound && bound < N;  // block-uniform
+  const int n0 = min(min(bound, N), row0 + G) - row0;
+  const int n1 = straddle ? min(N, row0 + G) - bound : 0;
+  const bool in0 = row < N && row < bound, in1 = row < N && row >= bound;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float s0[CPL], s1[CPL];
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) {
+      float x0 = v[q], x1 = v[q];
+      if (pass == 1) {
+        x0 -= mv[0][c0 + q];
+        x0 *= x0;
+        if (straddle) {
+          x1 -= mv[1][c0 + q];
+          x1 *= x1;
+        }
+      }
+      s0[q] = in0 ? x0 : 0.f;
+      s1[q] = in1 ? x1 : 0.f;
+    }
+#pragma unroll
+    for (int off = L; off < 64; off <<= 1)
+#pragma unroll
+      for (int q = 0; q < CPL; ++q) {
+        s0[q] += __shfl_xor(s0[q], off, 64);
+        if (straddle) s1[q] += __shfl_xor(s1[q], off, 64);
+      }
+    if (lane < L)
+#pragma unroll
+      for (int q = 0; q < CPL; ++q) {
+        red[wave][0][c0 + q] = s0[q];
+        red[wave][1][c0 + q] = s1[q];
+      }
+    __syncthreads();
+    const int c = threadIdx.x;
+    if (pass == 0) {
+      if (c < W) {
+        float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+        for (int w = 0; w < kBlock / 64; ++w) {
+          a0 += red[w][0][c];
+          a1 += red[w][1][c];
+        }
+        mv[0][c] = n0 > 0 ? a0 / static_cast<float>(n0) : 0.f;
+        mv[1][c] = n1 > 0 ? a1 / static_cast<float>(n1) : 0.f;
+      }
+      __syncthreads();
+    } else if (c < C) {
+      float m0 = 0.f, m1 = 0.f;
+#pragma unroll
+      for (int w = 0; w < kBlock / 64; ++w) {
+        m0 += red[w][0][c];
+        m1 += red[w][1][c];
+      }
+      float* p = gnp + ((size_t)lb * 2 * ldc + cb + c) * 3;
+      p[0] = static_cast<float>(n0);
+      p[1] = mv[0][c];
+      p[2] = m0;
+      if (straddle) {
+        p += (size_t)ldc * 3;
+        p[0] = static_cast<float>(n1);
+        p[1] = mv[1][c];
+        p[2] = m1;
+      }
+    }
+  }
+}
+
 // ===================================================================== forward
 // C >= 9, pass A: per-row attention projections a_src_i = <h_i, att_src>,
 // a_dst_i = <h_i, att_dst> (two group reductions per ROW, not per edge).
@@ -98,16 +190,20 @@ __global__ void __launch_bounds__(kBlock) k_gat_att(const float* __restrict__ h,
 // (-1 past the degree, ew <= 4L, vg_csr_ell) at a fixed offset, so their
 // loads -- and the a_src gathers behind them -- need not wait for row_ptr,
 // which is still read (in parallel) for the degree and the alpha offsets.
-template <int L, int CPL, bool VEC, bool ELL = false>
+// GNP: also the GraphNorm column partials of the output rows (gnp_fold).
+template <int L, int CPL, bool VEC, bool ELL = false, bool GNP = false>
 __global__ void __launch_bounds__(kBlock) k_gat_fwd_cp(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, int N, int C,
     const float* __restrict__ h, const float* __restrict__ a_src, const float* __restrict__ a_dst,
     const float* __restrict__ bias, float slope, float* __restrict__ out,
-    float* __restrict__ alpha, int ld = 0, const int32_t* __restrict__ ell = nullptr, int ew = 0) {
+    float* __restrict__ alpha, int ld = 0, const int32_t* __restrict__ ell = nullptr, int ew = 0,
+    float* __restrict__ gnp = nullptr, int seg_rows = 0) {
   // ld > 0: a channel slice -- h / out / bias point at the slice's first
   // channel, rows are ld floats apart, and only the slice at blockIdx.y == 0
   // writes alpha (every slice recomputes the row's softmax)
   const bool wr_alpha = blockIdx.y == 0;
+  const int ldc = ld == 0 ? C : ld;  // total columns (the GraphNorm partials' row)
+  const int cbase = ld == 0 ? 0 : blockIdx.y * C;
   if (ld == 0) {
     ld = C;
   } else {
@@ -118,8 +214,11 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_cp(
   }
   constexpr int T = 4;  // edges per lane kept in registers (rows up to 4L edges)
   const GroupIdx g = group_index<L>();
-  if (g.row >= N) return;
-  const int i = g.row;
+  // GNP keeps every wave to the block barrier: a group past N recomputes row
+  // N - 1 and stores nothing
+  const bool live = g.row < N;
+  if (!GNP && !live) return;
+  const int i = live ? g.row : N - 1;
   const int beg = row_ptr[i], end = row_ptr[i + 1];
   const int deg = end - beg;
   const float ad = a_dst[i];
@@ -163,10 +262,10 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_cp(
   for (int t = 0; t < T; ++t) {
     if (v_t[t]) {
       e_t[t] = e_t[t] / denom;  // alpha
-      if (wr_alpha) alpha[beg + g.lane + t * L] = e_t[t];
+      if (wr_alpha && live) alpha[beg + g.lane + t * L] = e_t[t];
     }
   }
-  if (!ELL && wr_alpha)
+  if (!ELL && wr_alpha && live)
     for (int k = beg + g.lane + T * L; k < end; k += L)
       alpha[k] = expf(lrelu(a_src[col[k]] + ad, slope) - m) / denom;
 
@@ -209,24 +308,29 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_cp(
   load_param<CPL>(b, bias, c0, C);
 #pragma unroll
   for (int q = 0; q < CPL; ++q) acc.v[q] += b.v[q];
-  store_row<CPL, VEC>(acc, out + (size_t)i * ld, c0, C);
+  if (live) store_row<CPL, VEC>(acc, out + (size_t)i * ld, c0, C);
+  if constexpr (GNP)
+    gnp_block<L, CPL>(acc.v, g.row, xcd_remap(blockIdx.x, gridDim.x), N, seg_rows, C, c0, cbase, ldc, gnp);
 }
 
 // C <= 8: 8 lanes per destination row, one edge per lane.
 // PRE: a_src / a_dst are inputs (vg_gat_lin_att computed them in the
 // projection GEMM's epilogue); otherwise they are formed here and written.
 // ELL as in k_gat_fwd_cp (ew <= 8 kEP).
-template <int CMAX, bool PRE = false, bool ELL = false>
+// GNP as in k_gat_fwd_cp (with PRE: the attention projections are inputs).
+template <int CMAX, bool PRE = false, bool ELL = false, bool GNP = false>
 __global__ void __launch_bounds__(kBlock) k_gat_fwd_ep(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, int N, int C,
     const float* __restrict__ h, const float* __restrict__ att_s, const float* __restrict__ att_d,
     const float* __restrict__ bias, float slope, float* __restrict__ out, float* __restrict__ alpha,
     float* __restrict__ a_src_io, float* __restrict__ a_dst_io, const int32_t* __restrict__ ell = nullptr,
-    int ew = 0) {
+    int ew = 0, float* __restrict__ gnp = nullptr, int seg_rows = 0) {
+  static_assert(!GNP || PRE, "GraphNorm partials with precomputed projections only");
   constexpr int L = 8;
   const GroupIdx g = group_index<L>();
-  if (g.row >= N) return;
-  const int i = g.row;
+  const bool live = g.row < N;
+  if (!GNP && !live) return;
+  const int i = live ? g.row : N - 1;
   float vs[CMAX];
   float ad = 0.f;
   if constexpr (PRE) {
@@ -325,17 +429,19 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_ep(
   const float denom = group_sum<L>(ssum) + kSoftmaxEps;
 #pragma unroll
   for (int c = 0; c < CMAX; ++c) acc[c] = group_sum<L>(acc[c]);
+  float o = 0.f;
   if (g.lane < C) {
     float v = 0.f;
 #pragma unroll
     for (int c = 0; c < CMAX; ++c)
       if (c == g.lane) v = acc[c];
-    out[(size_t)i * C + g.lane] = v / denom + bias[g.lane];
+    o = v / denom + bias[g.lane];
+    if (live) out[(size_t)i * C + g.lane] = o;
   }
 #pragma unroll
   for (int t = 0; t < kEP; ++t)
-    if (v[t]) alpha[beg + g.lane + t * L] = e[t] / denom;
-  for (int k = beg + g.lane + kEP * L; !ELL && k < end; k += L) {
+    if (v[t] && live) alpha[beg + g.lane + t * L] = e[t] / denom;
+  for (int k = beg + g.lane + kEP * L; !ELL && live && k < end; k += L) {
     const int s = col[k];
     float a = PRE ? a_src_io[s] : 0.f;
     if (!PRE)
@@ -343,6 +449,10 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_ep(
       for (int c = 0; c < CMAX; ++c)
         if (c < C) a = fmaf(h[(size_t)s * C + c], vs[c], a);
     alpha[k] = expf(lrelu(a + ad, slope) - m) / denom;
+  }
+  if constexpr (GNP) {
+    const float ov[1] = {o};
+    gnp_block<L, 1>(ov, g.row, xcd_remap(blockIdx.x, gridDim.x), N, seg_rows, C, g.lane, 0, C, gnp);
   }
 }
 
@@ -792,13 +902,22 @@ extern "C" int vg_gat_att(const float* h, int32_t N, int32_t C, const float* att
 
 // the aggregation with (ell != NULL) or without the padded column array; a
 // kernel shape takes the ELL path when ew fits its edge slots (4L, or 8 kEP)
-static int aggregate_fwd(const int32_t* row_ptr, const int32_t* col, const int32_t* ell, int32_t ew, int32_t N,
-                         int32_t C, const float* h, const float* a_src, const float* a_dst, const float* bias,
-                         float slope, float* out, float* alpha, void* stream) {
-  if (N <= 0 || C <= 0 || C > 256 || !row_ptr || !col || !h || !a_src || !a_dst || !bias ||
-      !out || !alpha || (ell && ew <= 0))
-    return VG_EINVAL;
-  hipStream_t s = static_cast<hipStream_t>(stream);
+// rows per workgroup of the aggregation kernel aggregate_fwd picks for (N, C):
+// the granularity of its GraphNorm partials
+static int agg_rows_per_block(int32_t N, int32_t C) {
+  if (C <= 8) return kBlock / 8;
+  if (N >= kSliceRows && C % kSlice == 0 && C > kSlice) return kBlock / (kSlice / 4);
+  if (VG_FWD_C64_L8 && C > 32 && C <= 64 && C % 8 == 0) return kBlock / 8;
+  Shape sh;
+  if (!pick_fused_shape(C, sh)) return 0;
+  return kBlock / sh.L;
+}
+
+template <bool GNP>
+static int aggregate_fwd_launch(const int32_t* row_ptr, const int32_t* col, const int32_t* ell, int32_t ew,
+                                 int32_t N, int32_t C, const float* h, const float* a_src, const float* a_dst,
+                                 const float* bias, float slope, float* out, float* alpha, float* gnp,
+                                 int32_t seg_rows, hipStream_t s) {
   float* as = const_cast<float*>(a_src);  // read-only under PRE
   float* ad = const_cast<float*>(a_dst);
   if (C <= 8) {
@@ -807,11 +926,13 @@ static int aggregate_fwd(const int32_t* row_ptr, const int32_t* col, const int32
 #define VG_EPF(CM)                                                                                           \
   do {                                                                                                       \
     if (e)                                                                                                   \
-      k_gat_fwd_ep<CM, true, true><<<grid, kBlock, 0, s>>>(row_ptr, col, N, C, h, nullptr, nullptr, bias,    \
-                                                           slope, out, alpha, as, ad, ell, ew);              \
+      k_gat_fwd_ep<CM, true, true, GNP><<<grid, kBlock, 0, s>>>(row_ptr, col, N, C, h, nullptr, nullptr,     \
+                                                                bias, slope, out, alpha, as, ad, ell, ew,    \
+                                                                gnp, seg_rows);                              \
     else                                                                                                     \
-      k_gat_fwd_ep<CM, true><<<grid, kBlock, 0, s>>>(row_ptr, col, N, C, h, nullptr, nullptr, bias, slope,   \
-                                                     out, alpha, as, ad);                                    \
+      k_gat_fwd_ep<CM, true, false, GNP><<<grid, kBlock, 0, s>>>(row_ptr, col, N, C, h, nullptr, nullptr,    \
+                                                                 bias, slope, out, alpha, as, ad, nullptr,   \
+                                                                 0, gnp, seg_rows);                          \
   } while (0)
     if (C <= 1) VG_EPF(1);
     else if (C <= 2) VG_EPF(2);
@@ -824,24 +945,44 @@ static int aggregate_fwd(const int32_t* row_ptr, const int32_t* col, const int32
     // or less of the full-width footprint in its 4 MiB L2
     constexpr int Ls = kSlice / 4;
     if (ell && ew <= 4 * Ls)
-      k_gat_fwd_cp<Ls, 4, true, true><<<dim3(grid_for(N, Ls), C / kSlice), kBlock, 0, s>>>(
-          row_ptr, col, N, kSlice, h, a_src, a_dst, bias, slope, out, alpha, C, ell, ew);
+      k_gat_fwd_cp<Ls, 4, true, true, GNP><<<dim3(grid_for(N, Ls), C / kSlice), kBlock, 0, s>>>(
+          row_ptr, col, N, kSlice, h, a_src, a_dst, bias, slope, out, alpha, C, ell, ew, gnp, seg_rows);
     else
-      k_gat_fwd_cp<Ls, 4, true><<<dim3(grid_for(N, Ls), C / kSlice), kBlock, 0, s>>>(
-          row_ptr, col, N, kSlice, h, a_src, a_dst, bias, slope, out, alpha, C);
+      k_gat_fwd_cp<Ls, 4, true, false, GNP><<<dim3(grid_for(N, Ls), C / kSlice), kBlock, 0, s>>>(
+          row_ptr, col, N, kSlice, h, a_src, a_dst, bias, slope, out, alpha, C, nullptr, 0, gnp, seg_rows);
   } else if (VG_FWD_C64_L8 && C > 32 && C <= 64 && C % 8 == 0) {
-    k_gat_fwd_cp<8, 8, true><<<grid_for(N, 8), kBlock, 0, s>>>(row_ptr, col, N, C, h, a_src, a_dst, bias,
-                                                                slope, out, alpha);
+    k_gat_fwd_cp<8, 8, true, false, GNP><<<grid_for(N, 8), kBlock, 0, s>>>(
+        row_ptr, col, N, C, h, a_src, a_dst, bias, slope, out, alpha, 0, nullptr, 0, gnp, seg_rows);
   } else {
     Shape sh;
-    if (!pick_fused_shape(C, sh)) return VG_EINVAL;
+    pick_fused_shape(C, sh);
     if (ell && ew <= 4 * sh.L)
-      VG_DISPATCH_FUSED(C, (k_gat_fwd_cp<L_, CPL_, V_, true><<<grid_for(N, L_), kBlock, 0, s>>>(
-                               row_ptr, col, N, C, h, a_src, a_dst, bias, slope, out, alpha, 0, ell, ew)));
+      VG_DISPATCH_FUSED(C, (k_gat_fwd_cp<L_, CPL_, V_, true, GNP><<<grid_for(N, L_), kBlock, 0, s>>>(
+                               row_ptr, col, N, C, h, a_src, a_dst, bias, slope, out, alpha, 0, ell, ew, gnp,
+                               seg_rows)));
     else
-      VG_DISPATCH_FUSED(C, (k_gat_fwd_cp<L_, CPL_, V_><<<grid_for(N, L_), kBlock, 0, s>>>(
-                               row_ptr, col, N, C, h, a_src, a_dst, bias, slope, out, alpha)));
+      VG_DISPATCH_FUSED(C, (k_gat_fwd_cp<L_, CPL_, V_, false, GNP><<<grid_for(N, L_), kBlock, 0, s>>>(
+                               row_ptr, col, N, C, h, a_src, a_dst, bias, slope, out, alpha, 0, nullptr, 0, gnp,
+                               seg_rows)));
   }
+  return 0;
+}
+
+static int aggregate_fwd(const int32_t* row_ptr, const int32_t* col, const int32_t* ell, int32_t ew, int32_t N,
+                         int32_t C, const float* h, const float* a_src, const float* a_dst, const float* bias,
+                         float slope, float* out, float* alpha, void* stream, float* gnp = nullptr,
+                         int32_t seg_rows = 0) {
+  if (N <= 0 || C <= 0 || C > 256 || !row_ptr || !col || !h || !a_src || !a_dst || !bias ||
+      !out || !alpha || (ell && ew <= 0) || agg_rows_per_block(N, C) == 0)
+    return VG_EINVAL;
+  // a workgroup's rows span at most two GraphNorm segments
+  if (gnp && (seg_rows < agg_rows_per_block(N, C) || N % seg_rows != 0)) return VG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int rc = gnp ? aggregate_fwd_launch<true>(row_ptr, col, ell, ew, N, C, h, a_src, a_dst, bias, slope, out,
+                                                  alpha, gnp, seg_rows, s)
+                     : aggregate_fwd_launch<false>(row_ptr, col, ell, ew, N, C, h, a_src, a_dst, bias, slope,
+                                                   out, alpha, nullptr, 0, s);
+  if (rc) return rc;
   VG_CHECK_LAUNCH();
   return 0;
 }
@@ -859,6 +1000,23 @@ extern "C" int vg_gat_aggregate_fwd_ell(const int32_t* row_ptr, const int32_t* c
                                         float* out, float* alpha, void* stream) {
   if (!ell) return VG_EINVAL;
   return aggregate_fwd(row_ptr, col, ell, ell_width, N, C, h, a_src, a_dst, bias, slope, out, alpha, stream);
+}
+
+extern "C" int32_t vg_gat_gnp_rows(int32_t N, int32_t C) { return N > 0 ? agg_rows_per_block(N, C) : 0; }
+
+extern "C" int64_t vg_gat_gnp_floats(int32_t N, int32_t C) {
+  const int g = N > 0 ? agg_rows_per_block(N, C) : 0;
+  if (g == 0) return 0;
+  return (((int64_t)N + g - 1) / g) * 2 * C * 3;
+}
+
+extern "C" int vg_gat_aggregate_fwd_gnp(const int32_t* row_ptr, const int32_t* col, const int32_t* ell,
+                                        int32_t ell_width, int32_t N, int32_t C, const float* h,
+                                        const float* a_src, const float* a_dst, const float* bias, float slope,
+                                        float* out, float* alpha, int32_t seg_rows, float* gnp, void* stream) {
+  if (!gnp) return VG_EINVAL;
+  return aggregate_fwd(row_ptr, col, ell, ell ? ell_width : 0, N, C, h, a_src, a_dst, bias, slope, out, alpha,
+                       stream, gnp, seg_rows);
 }
 
 // ell [N][width] = the row's CSR columns in order, -1 past its degree (the

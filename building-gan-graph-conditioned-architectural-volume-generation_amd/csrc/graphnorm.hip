@@ -187,6 +187,46 @@ __global__ void __launch_bounds__(kBlock) k_stats_final(const float* __restrict_
   }
 }
 
+// The same fold over the block partials the GAT aggregation wrote in its
+// epilogue (vg_gat_aggregate_fwd_gnp): gnp [blocks][2][C][3] for blocks of G
+// rows of the S * N stacked rows, slot 0 = the segment of the block's first
+// row, slot 1 = the next one.  One wave per (column, segment); lane l merges
+// the segment's blocks l, l + 64, ... in order (16 in flight: one round trip
+// at batch 32), then the xor butterfly: deterministic.
+__global__ void __launch_bounds__(kBlock) k_stats_final_gnp(const float* __restrict__ gnp, int G, int N, int C,
+                                                            int S, float* __restrict__ stats) {
+  const int c = fold_col(), lane = threadIdx.x & 63;
+  const int sg = blockIdx.y;
+  if (c >= C || sg >= S) return;
+  const int r0 = sg * N;
+  const int b0 = r0 / G, b1 = (r0 + N - 1) / G;  // inclusive
+  constexpr int U = 16;
+  Welford acc = {0.f, 0.f, 0.f};
+  for (int bb = b0 + lane; bb <= b1; bb += 64 * U) {
+    float v[U][3];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int b = bb + 64 * u;
+      if (b <= b1) {
+        const int slot = b * G < r0 ? 1 : 0;
+        const float* p = gnp + (((size_t)b * 2 + slot) * C + c) * 3;
+        v[u][0] = p[0];
+        v[u][1] = p[1];
+        v[u][2] = p[2];
+      } else {
+        v[u][0] = v[u][1] = v[u][2] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc = merge(acc, Welford{v[u][0], v[u][1], v[u][2]});
+  }
+  acc = wave_merge(acc);
+  if (lane == 0) {
+    stats[(size_t)sg * 2 * C + c] = acc.mean;
+    stats[(size_t)sg * 2 * C + C + c] = sqrtf(fmaxf(acc.m2 / acc.n, 0.f));
+  }
+}
+
 // iter != NULL: draw the dropout multiplier in-kernel (vg_keep with p_drop,
 // seed, *iter, salt) and apply it; keep_out != NULL also stores it for the
 // backward (a no-grad forward -- the critic labels -- skips the store).
@@ -759,18 +799,26 @@ extern "C" int64_t vg_graphnorm_ws_floats(int32_t num_nodes, int32_t channels) {
   return vg_graphnorm_seg_ws_floats(1, num_nodes, channels);
 }
 
+// gnp != NULL: the column statistics from the GAT aggregation's block
+// partials (G rows per block) instead of a pass over x
 static int gn_fwd(const float* x, int32_t S, int32_t N, int32_t C, const float* weight,
                   const float* bias, const float* mean_scale, const float* keep, float eps, float* y,
                   float* stats, float* ws, float p_drop, uint64_t seed, const int64_t* iter,
-                  uint32_t salt, float* keep_out, int32_t* sync, void* stream) {
-  if (S <= 0 || N <= 0 || C <= 0 || !x || !weight || !bias || !mean_scale || !y || !stats || !ws)
+                  uint32_t salt, float* keep_out, int32_t* sync, void* stream, const float* gnp = nullptr,
+                  int32_t gnp_rows = 0) {
+  if (S <= 0 || N <= 0 || C <= 0 || !x || !weight || !bias || !mean_scale || !y || !stats || (!ws && !gnp) ||
+      (gnp && (gnp_rows <= 0 || gnp_rows > N)))
     return VG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const int chunks = chunks_for(N);
-  dim3 grid(chunks, (C + 63) / 64, S);
-  k_stats_partial<float><<<grid, kBlock, 0, s>>>(x, N, C, C, ws, stats, nullptr);
+  if (gnp) {
+    k_stats_final_gnp<<<dim3(vg_blocks(C, kBlock / 64), S), kBlock, 0, s>>>(gnp, gnp_rows, N, C, S, stats);
+  } else {
+    const int chunks = chunks_for(N);
+    dim3 grid(chunks, (C + 63) / 64, S);
+    k_stats_partial<float><<<grid, kBlock, 0, s>>>(x, N, C, C, ws, stats, nullptr);
+    k_stats_final<<<dim3(vg_blocks(C, kBlock / 64), S), kBlock, 0, s>>>(ws, chunks, C, S, stats);
+  }
   (void)sync;  // former last-block-fold counter: accepted, unused
-  k_stats_final<<<dim3(vg_blocks(C, kBlock / 64), S), kBlock, 0, s>>>(ws, chunks, C, S, stats);
   const long long total = (long long)S * N * C;
   const int lds_f = 3 * C + 2 * C * S;
   if (quad_ok(total, C, lds_f, {x, keep, y, keep_out}))
@@ -825,6 +873,16 @@ extern "C" int vg_graphnorm_fwd_drop(const float* x, int32_t S, int32_t N, int32
   if (!iter || !(p_drop >= 0.f && p_drop < 1.f)) return VG_EINVAL;  // keep_out NULL: apply, do not store
   return gn_fwd(x, S, N, C, weight, bias, mean_scale, nullptr, eps, y, stats, ws, p_drop, seed,
                 iter, salt, keep_out, sync, stream);
+}
+
+extern "C" int vg_graphnorm_fwd_gnp(const float* x, int32_t S, int32_t N, int32_t C, const float* weight,
+                                    const float* bias, const float* mean_scale, const float* keep, float p_drop,
+                                    uint64_t seed, const int64_t* iter, uint32_t salt, float eps, float* y,
+                                    float* keep_out, float* stats, const float* gnp, int32_t gnp_rows,
+                                    void* stream) {
+  if (!gnp || (iter && !(p_drop >= 0.f && p_drop < 1.f)) || (iter && keep)) return VG_EINVAL;
+  return gn_fwd(x, S, N, C, weight, bias, mean_scale, keep, eps, y, stats, nullptr, iter ? p_drop : 0.f,
+                iter ? seed : 0, iter, iter ? salt : 0, iter ? keep_out : nullptr, nullptr, stream, gnp, gnp_rows);
 }
 
 extern "C" int vg_graphnorm_fwd(const float* x, int32_t N, int32_t C, const float* weight,

@@ -132,6 +132,13 @@ SIGNATURES = {
     "vg_csr_ell": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p]),
     "vg_gat_aggregate_fwd_ell": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p,
                                                 _c_f32, _c_p, _c_p, _c_p]),
+    "vg_gat_gnp_rows": (_c_i32, [_c_i32, _c_i32]),
+    "vg_gat_gnp_floats": (_c_i64, [_c_i32, _c_i32]),
+    "vg_gat_aggregate_fwd_gnp": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p,
+                                                _c_f32, _c_p, _c_p, _c_i32, _c_p, _c_p]),
+    "vg_graphnorm_fwd_gnp": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32,
+                                            ctypes.c_uint64, _c_p, ctypes.c_uint32, _c_f32, _c_p, _c_p, _c_p, _c_p,
+                                            _c_i32, _c_p]),
     "vg_gat_aggregate_fwd": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p,
                                             _c_p]),
     "vg_gat_bwd_ws_floats": (_c_i64, [_c_i32, _c_i32, _c_i32]),

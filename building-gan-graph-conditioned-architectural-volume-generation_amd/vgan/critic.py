@@ -227,9 +227,25 @@ class CriticEngine:
             check(dense("vg_gat_lin_att")(ptr(x), xw, ptr(conv.lin.weight), R, xw, c, ptr(conv.att_src),
                                      ptr(conv.att_dst), ptr(H), ptr(a_s), ptr(a_d), st), "vg_gat_lin_att")
             O, alpha = _f(R, c, dev=dev), _f(3 * E, dev=dev)
+            gnp, g = ops.gnp_buffer(csr3, c, dev)  # the GraphNorm's column partials from the aggregation
             ops.aggregate_fwd_raw(csr3, c, ptr(H), ptr(a_s), ptr(a_d), ptr(conv.bias), float(conv.negative_slope),
-                                  ptr(O), ptr(alpha), st)
+                                  ptr(O), ptr(alpha), st, gnp)
             Y, stats = _f(X4, c, dev=dev), _f(3 * 2 * c, dev=dev)
+            if gnp is not None:
+                spec = keep if keep is not None and not isinstance(keep, torch.Tensor) else None
+                if spec is not None:
+                    keep = _f(R, c, dev=dev)
+                    args = (None, float(spec.p), int(spec.seed), ptr(spec.iter), int(spec.salt) & 0xFFFFFFFF)
+                else:
+                    args = (ptr(keep), 0.0, 0, None, 0)
+                check(LIB.vg_graphnorm_fwd_gnp(ptr(O), 3, n, c, ptr(norm.weight), ptr(norm.bias),
+                                               ptr(norm.mean_scale), *args, float(norm.eps), ptr(Y),
+                                               ptr(keep) if spec is not None else None, ptr(stats), ptr(gnp), g, st),
+                      "vg_graphnorm_fwd_gnp")
+                blk.append(dict(X=x, xw=xw, H=H, O=O, alpha=alpha, a_s=a_s, a_d=a_d, Y=Y, stats=stats, keep=keep,
+                                c=c))
+                x, xw = Y, c
+                continue
             ws = _f(int(LIB.vg_graphnorm_seg_ws_floats(3, n, c)), dev=dev)
             if keep is not None and not isinstance(keep, torch.Tensor):  # DropSpec: drawn in-kernel
                 spec, keep = keep, _f(R, c, dev=dev)

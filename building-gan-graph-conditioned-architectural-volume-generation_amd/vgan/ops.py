@@ -20,6 +20,7 @@ available and every derivative runs through the same C ABI.
 from __future__ import annotations
 
 import os
+import weakref
 from typing import Optional, Tuple
 
 import torch
@@ -115,8 +116,15 @@ class CSR:
         out.csc_dst = tile(self.csc_dst, n)
         if "_ell_w" in self.__dict__:  # same degrees: no host sync for the copies' width
             out._ell_w = self._ell_w
+        out._seg_rows = n
         cache[copies] = out
         return out
+
+    @property
+    def seg_rows(self) -> int:
+        """Rows per stacked copy (``stacked``): the GraphNorm segment a
+        forward over this graph normalises separately."""
+        return self.__dict__.get("_seg_rows", self.num_nodes)
 
     def ell(self):
         """(ell, width): the destination rows' sources padded to a fixed width
@@ -162,17 +170,67 @@ class CSR:
         return plan
 
 
-def aggregate_fwd_raw(csr: "CSR", c: int, h, a_src, a_dst, bias, slope: float, out, alpha, stream) -> None:
+def aggregate_fwd_raw(csr: "CSR", c: int, h, a_src, a_dst, bias, slope: float, out, alpha, stream,
+                      gnp=None) -> None:
     """vg_gat_aggregate_fwd over raw device pointers (ctypes), through the
     padded column array when the graph has one (vg_gat_aggregate_fwd_ell);
-    bit-identical either way."""
+    bit-identical either way.  gnp (``gnp_buffer``): also the following
+    GraphNorm's column partials (vg_gat_aggregate_fwd_gnp)."""
     ell, w = csr.ell()
-    if ell is not None:
+    if gnp is not None:
+        check(LIB.vg_gat_aggregate_fwd_gnp(ptr(csr.row_ptr), ptr(csr.col), ptr(ell) if ell is not None else None,
+                                           w if ell is not None else 0, csr.num_nodes, c, h, a_src, a_dst, bias,
+                                           float(slope), out, alpha, csr.seg_rows, ptr(gnp), stream),
+              "vg_gat_aggregate_fwd_gnp")
+    elif ell is not None:
         check(LIB.vg_gat_aggregate_fwd_ell(ptr(csr.row_ptr), ptr(csr.col), ptr(ell), w, csr.num_nodes, c, h, a_src,
                                            a_dst, bias, float(slope), out, alpha, stream), "vg_gat_aggregate_fwd_ell")
     else:
         check(LIB.vg_gat_aggregate_fwd(ptr(csr.row_ptr), ptr(csr.col), csr.num_nodes, c, h, a_src, a_dst, bias,
                                        float(slope), out, alpha, stream), "vg_gat_aggregate_fwd")
+
+
+# GraphNorm statistics from the GAT aggregation's epilogue: every GATConv is
+# followed by a GraphNorm (models.py:73-75,193-195), whose column statistics
+# pass (k_stats_partial) re-read the aggregation's output.  The aggregation
+# writes per-workgroup Welford partials instead (vg_gat_aggregate_fwd_gnp) and
+# the GraphNorm folds them (vg_graphnorm_fwd_gnp): one launch and one pass over
+# the layer's output fewer per GraphNorm.  VGAN_GN_FWD_FUSE=0: off.
+_GN_FWD_FUSE = os.environ.get("VGAN_GN_FWD_FUSE", "1") == "1"
+
+
+def gnp_buffer(csr: "CSR", c: int, device):
+    """(gnp, rows per partial) for an aggregation over ``csr`` at ``c``
+    channels, or (None, 0) when its workgroups would span more than two
+    GraphNorm segments."""
+    if not _GN_FWD_FUSE:
+        return None, 0
+    g = int(LIB.vg_gat_gnp_rows(csr.num_nodes, c))
+    if g <= 0 or csr.seg_rows < g or csr.num_nodes % csr.seg_rows:
+        return None, 0
+    return torch.empty(int(LIB.vg_gat_gnp_floats(csr.num_nodes, c)), dtype=torch.float32, device=device), g
+
+
+class _GnpHint:
+    """The partials of the last GAT aggregation, for the GraphNorm that
+    consumes exactly its output tensor (same object, not modified since)."""
+    __slots__ = ("ref", "version", "gnp", "rows", "seg_rows")
+
+    def __init__(self, out, gnp, rows, seg_rows):
+        self.ref, self.version = weakref.ref(out), out._version
+        self.gnp, self.rows, self.seg_rows = gnp, rows, seg_rows
+
+
+_GNP_LAST: Optional[_GnpHint] = None
+
+
+def _take_gnp(x: torch.Tensor, seg_rows: int):
+    """(gnp, rows) left by the aggregation that produced ``x``, or (None, 0)."""
+    global _GNP_LAST
+    h, _GNP_LAST = _GNP_LAST, None
+    if h is None or h.ref() is not x or x._version != h.version or h.seg_rows != seg_rows:
+        return None, 0
+    return h.gnp, h.rows
 
 
 def aggregate_lds(csr: "CSR", h: torch.Tensor, a_src: torch.Tensor, a_dst: torch.Tensor, bias: torch.Tensor,
@@ -498,8 +556,12 @@ class _GATConv(Function):
             require_cuda(a_src, a_dst)
             if a_src.numel() != n or a_dst.numel() != n:
                 raise ValueError("gat_conv: inconsistent projection shapes")
+            gnp, g = gnp_buffer(csr, c, dev)
             aggregate_fwd_raw(csr, c, ptr(h), ptr(a_src), ptr(a_dst), ptr(b), slope, ptr(out), ptr(alpha),
-                              csr.stream())
+                              csr.stream(), gnp)
+            if gnp is not None:
+                global _GNP_LAST
+                _GNP_LAST = _GnpHint(out, gnp, g, csr.seg_rows)
         else:
             a_src = torch.empty(n, dtype=torch.float32, device=dev)
             a_dst = torch.empty(n, dtype=torch.float32, device=dev)
@@ -642,10 +704,21 @@ class _GraphNormReLUDropout(Function):
             raise ValueError("graphnorm: inconsistent shapes")
         y = torch.empty_like(x)
         stats = torch.empty(S * 2 * c, dtype=torch.float32, device=x.device)
-        ws = torch.empty(int(LIB.vg_graphnorm_seg_ws_floats(S, n, c)), dtype=torch.float32, device=x.device)
-        if spec is not None:  # dropout drawn in-kernel (device RNG)
-            if tuple(spec.shape) != tuple(x.shape):
-                raise ValueError("graphnorm: dropout spec shape differs from x")
+        gnp, g = _take_gnp(x, n)
+        ws = None if gnp is not None else \
+            torch.empty(int(LIB.vg_graphnorm_seg_ws_floats(S, n, c)), dtype=torch.float32, device=x.device)
+        if spec is not None and tuple(spec.shape) != tuple(x.shape):
+            raise ValueError("graphnorm: dropout spec shape differs from x")
+        if gnp is not None:  # column statistics from the aggregation's partials
+            if spec is not None:
+                kp = torch.empty_like(x) if grad or _STORE_NOGRAD_KEEP else None
+                args = (None, float(spec.p), int(spec.seed), ptr(spec.iter), int(spec.salt) & 0xFFFFFFFF)
+            else:
+                args = (ptr(kp), 0.0, 0, None, 0)
+            check(LIB.vg_graphnorm_fwd_gnp(ptr(x), S, n, c, ptr(w), ptr(b), ptr(ms), *args, float(eps), ptr(y),
+                                           ptr(kp) if spec is not None else None, ptr(stats), ptr(gnp), g,
+                                           stream_handle(x.device)), "vg_graphnorm_fwd_gnp")
+        elif spec is not None:  # dropout drawn in-kernel (device RNG)
             # no backward: apply the mask, do not store it (VGAN_STORE_NOGRAD_KEEP=1: store, A/B knob)
             kp = torch.empty_like(x) if grad or _STORE_NOGRAD_KEEP else None
             check(LIB.vg_graphnorm_fwd_drop(ptr(x), S, n, c, ptr(w), ptr(b), ptr(ms), float(spec.p), int(spec.seed),

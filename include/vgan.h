@@ -231,6 +231,16 @@ int vg_graphnorm_fwd_drop(const float* x, int32_t segments, int32_t rows, int32_
                           float p_drop, uint64_t seed, const int64_t* iter, uint32_t salt,
                           float eps, float* y, float* keep_out, float* stats, float* workspace,
                           int32_t* sync, void* stream);
+/* vg_graphnorm_fwd_seg (iter == NULL: keep multipliers or none) or
+ * vg_graphnorm_fwd_drop (iter != NULL, keep NULL) with the column statistics
+ * folded from the aggregation's partials (vg_gat_aggregate_fwd_gnp over the
+ * segments * rows rows with seg_rows = rows; gnp_rows = vg_gat_gnp_rows of
+ * that call) instead of a pass over x: one launch fewer, x read once.  The
+ * statistics differ from the chunked fold only in f32 rounding. */
+int vg_graphnorm_fwd_gnp(const float* x, int32_t segments, int32_t rows, int32_t channels, const float* weight,
+                         const float* bias, const float* mean_scale, const float* keep, float p_drop, uint64_t seed,
+                         const int64_t* iter, uint32_t salt, float eps, float* y, float* keep_out, float* stats,
+                         const float* gnp, int32_t gnp_rows, void* stream);
 /* Backward over the segments; parameter gradients sum over segments and are
  * written (accumulate = 0) or added (1); g_w may be NULL (no parameter
  * gradients: g_b, g_ms are then ignored).  inj (nullable) is added to g_x
@@ -573,6 +583,20 @@ int vg_gat_aggregate_fwd_ell(const int32_t* row_ptr, const int32_t* col, const i
                              int32_t num_nodes, int32_t channels, const float* h, const float* a_src,
                              const float* a_dst, const float* bias, float slope, float* out, float* alpha,
                              void* stream);
+/* GraphNorm statistics fused into the aggregation (the GraphNorm after every
+ * GATConv, models.py:73-75,193-195; it re-read `out` for its column
+ * statistics).  vg_gat_aggregate_fwd(_ell) (ell may be NULL) that also writes
+ * per-workgroup Welford partials (count, mean, M2) of the output columns to
+ * gnp [vg_gat_gnp_floats(N, C)]: one per workgroup of vg_gat_gnp_rows(N, C)
+ * rows and segment slot, segments being seg_rows-row blocks of the N rows
+ * (N % seg_rows == 0, seg_rows >= vg_gat_gnp_rows).  vg_graphnorm_fwd_gnp
+ * folds them.  out and alpha are bit-identical to vg_gat_aggregate_fwd. */
+int32_t vg_gat_gnp_rows(int32_t num_nodes, int32_t channels);
+int64_t vg_gat_gnp_floats(int32_t num_nodes, int32_t channels);
+int vg_gat_aggregate_fwd_gnp(const int32_t* row_ptr, const int32_t* col, const int32_t* ell, int32_t ell_width,
+                             int32_t num_nodes, int32_t channels, const float* h, const float* a_src,
+                             const float* a_dst, const float* bias, float slope, float* out, float* alpha,
+                             int32_t seg_rows, float* gnp, void* stream);
 
 /* Tile plan of a destination CSR (vg_csr_build's arrays), once per graph: for
  * every tile of 16 destination rows the sorted distinct sources of its edges

@@ -1,0 +1,185 @@
+"""GraphNorm column statistics from the GAT aggregation's epilogue
+(vg_gat_aggregate_fwd_gnp + vg_graphnorm_fwd_gnp, ops.gnp_buffer) against
+the separate statistics pass (vg_graphnorm_fwd_seg / _drop) and a torch fp32
+GraphNorm (torch_geometric GraphNorm, batch=None: models.py:73-75,193-195).
+
+The aggregation's out / alpha must stay bit-identical to vg_gat_aggregate_fwd;
+the statistics are the same Welford sums grouped by workgroup instead of by
+row chunk, so they agree with the chunked fold to f32 rounding (tolerances
+below), and dropout masks drawn in-kernel are bit-identical."""
+from __future__ import annotations
+
+import pytest
+import torch
+
+from parity_util import rel_err
+from test_critic_gpu import _RecRNG, _engine_setup
+from test_ops_gpu import _aggregate_ref_kernel, _graph, _star_graph
+from vgan import ops
+from vgan._lib import LIB, check, ptr
+
+pytestmark = pytest.mark.gpu
+
+EPS = 1e-5
+
+
+def _csr(cuda, graph: str, copies: int):
+    if graph == "star":
+        ei, n = _star_graph(600)
+    else:
+        _, vox = _graph(stress=(graph == "stress"))
+        ei, n = vox.edge_index, vox.num_nodes
+    csr = ops.CSR(ei.to(cuda), n)
+    csr.ell()
+    if graph == "big":  # >= 100k rows: the 64-channel slice path of the aggregation
+        copies = -(-100_000 // n)
+    return csr.stacked(copies) if copies > 1 else csr
+
+
+def _gn_torch(x, S, w, b, ms, keep=None):
+    """fp32 GraphNorm + ReLU (+ dropout multipliers) per segment."""
+    ys, stats = [], []
+    for xs in x.chunk(S):
+        mu = xs.mean(0)
+        c = xs - mu * ms
+        sd = c.std(0, unbiased=False)
+        ys.append(torch.relu(c / (sd + EPS) * w + b))
+        stats.append(torch.cat([mu, sd]))
+    y = torch.cat(ys)
+    return (y * keep if keep is not None else y), torch.cat(stats)
+
+
+@pytest.mark.parametrize("graph,copies", [("lattice", 1), ("lattice", 3), ("stress", 1), ("stress", 5),
+                                          ("star", 1), ("star", 3), ("big", 0)])
+@pytest.mark.parametrize("C", [1, 3, 8, 12, 32, 64, 128])
+def test_aggregate_gnp_matches_statistics_pass(cuda, graph, copies, C):
+    if graph == "big" and C < 128:
+        pytest.skip("the slice path needs C > 64")
+    torch.manual_seed(C + 7 * copies)
+    csr = _csr(cuda, graph, copies)
+    n, seg = csr.num_nodes, csr.seg_rows
+    S = n // seg
+    gnp, g = ops.gnp_buffer(csr, C, cuda)
+    assert gnp is not None and g in (8, 16, 32) and seg >= g
+    h = torch.randn(n, C, device=cuda)
+    a_s, a_d = 0.5 * torch.randn(n, device=cuda), 0.5 * torch.randn(n, device=cuda)
+    b = torch.randn(C, device=cuda)
+    out, alpha = torch.empty_like(h), torch.empty(csr.num_edges, device=cuda)
+    gnp.fill_(float("nan"))  # every partial the fold reads must be written
+    ops.aggregate_fwd_raw(csr, C, ptr(h), ptr(a_s), ptr(a_d), ptr(b), 0.2, ptr(out), ptr(alpha), csr.stream(), gnp)
+    ref_out, ref_alpha = _aggregate_ref_kernel(csr, h, a_s, a_d, b)
+    assert torch.equal(out, ref_out) and torch.equal(alpha, ref_alpha)
+
+    w = 1 + 0.2 * torch.randn(C, device=cuda)
+    bb = 0.2 * torch.randn(C, device=cuda)
+    ms = 1 + 0.2 * torch.randn(C, device=cuda)
+    st = ops.stream_handle(cuda)
+    y1, st1 = torch.empty_like(out), torch.empty(S * 2 * C, device=cuda)
+    check(LIB.vg_graphnorm_fwd_gnp(ptr(out), S, seg, C, ptr(w), ptr(bb), ptr(ms), None, 0.0, 0, None, 0, EPS,
+                                   ptr(y1), None, ptr(st1), ptr(gnp), g, st), "vg_graphnorm_fwd_gnp")
+    y2, st2 = torch.empty_like(out), torch.empty(S * 2 * C, device=cuda)
+    ws = torch.empty(int(LIB.vg_graphnorm_seg_ws_floats(S, seg, C)), device=cuda)
+    check(LIB.vg_graphnorm_fwd_seg(ptr(out), S, seg, C, ptr(w), ptr(bb), ptr(ms), None, EPS, ptr(y2), ptr(st2),
+                                   ptr(ws), None, st), "vg_graphnorm_fwd_seg")
+    y_ref, st_ref = _gn_torch(out.double(), S, w.double(), bb.double(), ms.double())
+    torch.cuda.synchronize()
+    assert torch.isfinite(st1).all()
+    # column statistics: f32 Welford in another grouping, 1e-5 of the f64 values
+    assert (st1.double() - st_ref).abs().max().item() <= 1e-5 * max(1.0, st_ref.abs().max().item())
+    assert (st1 - st2).abs().max().item() <= 1e-5 * max(1.0, st2.abs().max().item())
+    assert rel_err(y1.double(), y_ref) < 1e-5
+    assert rel_err(y1, y2) < 1e-5
+
+
+@pytest.mark.parametrize("C", [4, 64])
+def test_gnp_dropout_mask_bit_identical(cuda, C):
+    """In-kernel dropout through the partials path draws the same multipliers
+    (counter-based Philox on the element index) as vg_graphnorm_fwd_drop."""
+    torch.manual_seed(C)
+    csr = _csr(cuda, "lattice", 3)
+    n, seg = csr.num_nodes, csr.seg_rows
+    gnp, g = ops.gnp_buffer(csr, C, cuda)
+    h = torch.randn(n, C, device=cuda)
+    a_s, a_d = 0.5 * torch.randn(n, device=cuda), 0.5 * torch.randn(n, device=cuda)
+    b = torch.randn(C, device=cuda)
+    out, alpha = torch.empty_like(h), torch.empty(csr.num_edges, device=cuda)
+    ops.aggregate_fwd_raw(csr, C, ptr(h), ptr(a_s), ptr(a_d), ptr(b), 0.2, ptr(out), ptr(alpha), csr.stream(), gnp)
+    w, bb, ms = torch.ones(C, device=cuda), torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    it = torch.tensor([5], dtype=torch.int64, device=cuda)
+    st = ops.stream_handle(cuda)
+    y1, k1, s1 = torch.empty_like(out), torch.empty_like(out), torch.empty(6 * C, device=cuda)
+    check(LIB.vg_graphnorm_fwd_gnp(ptr(out), 3, seg, C, ptr(w), ptr(bb), ptr(ms), None, 0.2, 1234, ptr(it), 77, EPS,
+                                   ptr(y1), ptr(k1), ptr(s1), ptr(gnp), g, st), "vg_graphnorm_fwd_gnp")
+    y2, k2, s2 = torch.empty_like(out), torch.empty_like(out), torch.empty(6 * C, device=cuda)
+    ws = torch.empty(int(LIB.vg_graphnorm_seg_ws_floats(3, seg, C)), device=cuda)
+    check(LIB.vg_graphnorm_fwd_drop(ptr(out), 3, seg, C, ptr(w), ptr(bb), ptr(ms), 0.2, 1234, ptr(it), 77, EPS,
+                                    ptr(y2), ptr(k2), ptr(s2), ptr(ws), None, st), "vg_graphnorm_fwd_drop")
+    torch.cuda.synchronize()
+    assert torch.equal(k1, k2)
+    assert 0.1 < (k1 == 0).float().mean().item() < 0.3
+    assert rel_err(y1, y2) < 1e-5
+
+
+def test_gnp_abi_rejects_bad_segments(cuda):
+    """Segments shorter than a workgroup's rows, or not dividing N: VG_EINVAL."""
+    csr = _csr(cuda, "lattice", 1)
+    n, C = csr.num_nodes, 64
+    g = int(LIB.vg_gat_gnp_rows(n, C))
+    assert g == 16 and int(LIB.vg_gat_gnp_rows(n, 8)) == 32
+    assert int(LIB.vg_gat_gnp_floats(n, C)) == -(-n // g) * 2 * C * 3
+    h = torch.zeros(n, C, device=cuda)
+    v = torch.zeros(n, device=cuda)
+    out, alpha = torch.empty_like(h), torch.empty(csr.num_edges, device=cuda)
+    gnp = torch.empty(int(LIB.vg_gat_gnp_floats(n, C)), device=cuda)
+    for seg in (g - 1, n - 1):
+        rc = LIB.vg_gat_aggregate_fwd_gnp(ptr(csr.row_ptr), ptr(csr.col), None, 0, n, C, ptr(h), ptr(v), ptr(v),
+                                          ptr(v[:C]), 0.2, ptr(out), ptr(alpha), seg, ptr(gnp), csr.stream())
+        assert rc != 0
+
+
+@pytest.mark.parametrize("training", [True, False])
+def test_critic_engine_and_generator_with_gnp(cuda, training, monkeypatch):
+    """The critic engine and the generator's autograd path with the GraphNorm
+    statistics from the aggregation against the separate statistics pass:
+    the same loss and gradients to f32 rounding, and the fused path runs for
+    every GraphNorm of both networks."""
+    from vgan.flat import FlatParams
+    from vgan.models import VoxelGNNGenerator
+    from vgan.rng import RNG
+
+    cfg, D, flat, loc, vox, prep, hard, soft, eng = _engine_setup(cuda, numbers=(5, 6, 7), seed=17)
+    D.train(training)
+    torch.manual_seed(19)
+    G = VoxelGNNGenerator(cfg, 17, 12).to(cuda).train(training)
+    flat_g = FlatParams(G)
+    z = torch.randn(1, vox.num_nodes, cfg.Z_DIM, device=cuda)
+    noise = torch.empty(vox.num_nodes, 7, device=cuda).exponential_()
+    wgt = torch.randn(vox.num_nodes, 7, device=cuda)
+    hd, sd = hard.to(cuda).unsqueeze(0), soft.to(cuda).unsqueeze(0)
+    calls = []
+    orig = LIB.vg_graphnorm_fwd_gnp
+
+    def counted(*a):
+        calls.append(1)
+        return orig(*a)
+
+    out = {}
+    for fuse in (True, False):
+        monkeypatch.setattr(ops, "_GN_FWD_FUSE", fuse)
+        monkeypatch.setattr(LIB, "vg_graphnorm_fwd_gnp", counted)
+        calls.clear()
+        flat.zero_grad()
+        loss = eng.loss_and_grad(loc, vox, hd, sd, _RecRNG(4))
+        G.rng = RNG("fixed", seed=3)
+        flat_g.zero_grad()
+        logits, _, soft_g = G(loc, vox, z, noise=noise)
+        with ops.direct_param_grads(), ops.deferred_param_folds(cuda):
+            ((logits * wgt).sum() + (soft_g * wgt).sum()).backward()
+        torch.cuda.synchronize()
+        out[fuse] = (loss.item(), flat.grad.clone(), logits.detach().clone(), flat_g.grad.clone(), len(calls))
+    n_gn = len(eng.blocks) + G.encoder.num_blocks
+    assert out[True][4] == n_gn and out[False][4] == 0
+    assert abs(out[True][0] - out[False][0]) <= 1e-5 * max(1.0, abs(out[False][0]))
+    assert rel_err(out[True][1], out[False][1]) < 1e-4
+    assert rel_err(out[True][2], out[False][2]) < 1e-5
+    assert rel_err(out[True][3], out[False][3]) < 1e-4
