@@ -68,12 +68,24 @@ def step_aggregate_calls(tr, csr):
     return calls
 
 
-def aggregate_roofline(tr, csr, device, reps: int = 20):
+def gnp_bytes(csr, c: int) -> int:
+    """Bytes of the GraphNorm block partials vg_gat_aggregate_fwd_gnp writes
+    (count, mean, M2 per column and workgroup; slot 1 of a straddling block is
+    not counted)."""
+    from vgan._lib import LIB
+
+    g = int(LIB.vg_gat_gnp_rows(csr.num_nodes, c))
+    return 4 * 3 * c * (-(-csr.num_nodes // g))
+
+
+def aggregate_roofline(tr, csr, device, reps: int = 20, gnp: bool = False):
     """Average device duration of the scatter kernel (vg_gat_aggregate_fwd)
     over the step's own mix of launches: one launch per call of a step, on the
     step's CSRs and channel counts, captured in a hipGraph and replayed
     ``reps`` times between HIP events on the replay stream (back-to-back
-    launches, as inside the step's own graphs)."""
+    launches, as inside the step's own graphs).  gnp: the variant the step
+    runs (vg_gat_aggregate_fwd_gnp: the following GraphNorm's column partials
+    in the epilogue; its bytes add the partials written)."""
     from vgan import ops
     from vgan._lib import ptr, stream_handle
 
@@ -90,13 +102,16 @@ def aggregate_roofline(tr, csr, device, reps: int = 20):
                          0.3 * torch.randn(n, device=device, generator=gen),
                          torch.randn(c, device=device, generator=gen),
                          torch.empty(n, c, device=device),
-                         torch.empty(c_csr.num_edges, device=device)]
+                         torch.empty(c_csr.num_edges, device=device),
+                         ops.gnp_buffer(c_csr, c, device)[0] if gnp else None]
+    if gnp and any(b[-1] is None for b in bufs.values()):
+        return None
 
     def launch_all():
         st = stream_handle(device)
         for c_csr, c in calls:
-            h, a_s, a_d, b, out, alpha = bufs[(c_csr.num_nodes, c)]
-            ops.aggregate_fwd_raw(c_csr, c, ptr(h), ptr(a_s), ptr(a_d), ptr(b), 0.2, ptr(out), ptr(alpha), st)
+            h, a_s, a_d, b, out, alpha, part = bufs[(c_csr.num_nodes, c)]
+            ops.aggregate_fwd_raw(c_csr, c, ptr(h), ptr(a_s), ptr(a_d), ptr(b), 0.2, ptr(out), ptr(alpha), st, part)
 
     side = torch.cuda.Stream(device)
     side.wait_stream(torch.cuda.current_stream(device))
@@ -116,7 +131,8 @@ def aggregate_roofline(tr, csr, device, reps: int = 20):
     torch.cuda.synchronize()
     total_ms = st.elapsed_time(en)
     launches = reps * len(calls)
-    nbytes = reps * sum(agg_bytes(c_csr.num_nodes, c_csr.num_edges, c) for c_csr, c in calls)
+    nbytes = reps * sum(agg_bytes(c_csr.num_nodes, c_csr.num_edges, c) + (gnp_bytes(c_csr, c) if gnp else 0)
+                        for c_csr, c in calls)
     return {"launches": launches, "launches_per_step": len(calls), "avg_us": total_ms * 1e3 / launches,
             "avg_bytes": nbytes / launches, "achieved_gbs": nbytes / (total_ms * 1e-3) / 1e9}
 
@@ -411,6 +427,9 @@ def main():
     kern = aggregate_roofline(tr, csr0, device, reps=max(args.steps, 10))
     log(f"vg_gat_aggregate_fwd: {kern['launches']} launches, avg {kern['avg_us']:.2f} us, "
         f"{kern['achieved_gbs']:.1f} GB/s")
+    kern_gnp = aggregate_roofline(tr, csr0, device, reps=max(args.steps, 10), gnp=True)
+    if kern_gnp:
+        log(f"vg_gat_aggregate_fwd_gnp: avg {kern_gnp['avg_us']:.2f} us, {kern_gnp['achieved_gbs']:.1f} GB/s")
     traffic, traffic_src = load_pmc_traffic()
 
     result = None
@@ -464,6 +483,14 @@ def main():
                 "launches_per_step": kern["launches_per_step"],
                 "timing": "the step's own mix of launches (CSRs, channel counts), hipGraph-replayed between HIP "
                           "events on the replay stream",
+                "step_variant": None if not kern_gnp else {
+                    "kernel": "vg_gat_aggregate_fwd_gnp (the variant the step runs: the following GraphNorm's "
+                              "column partials in the epilogue, replacing that GraphNorm's statistics pass)",
+                    "achieved": round(kern_gnp["achieved_gbs"], 2),
+                    "frac": round(kern_gnp["achieved_gbs"] / HBM_PEAK_GBS, 5),
+                    "avg_launch_us": round(kern_gnp["avg_us"], 3),
+                    "avg_algorithmic_bytes": int(kern_gnp["avg_bytes"]),
+                },
             },
             "cpu_baseline": cpu,
         }

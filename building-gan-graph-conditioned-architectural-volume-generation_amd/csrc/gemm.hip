@@ -107,6 +107,51 @@ struct GnpDesc {
   float* tpart;
 };
 
+// GraphNorm + ReLU + Dropout applied to the A operand as it is loaded
+// (vg_gat_lin_att_gn: the GraphNorm that ends a GATConv block feeding the next
+// block's projection, models.py:73-77): A holds the GraphNorm INPUT x [rows, K]
+// (lda = K); every element becomes y = keep * relu(w (x - ms mu)/(sd + eps) + b)
+// with the statistics of its row's segment -- the formula and operation order
+// of k_gn_apply4 -- and y (and a drawn keep) are stored for the backward when
+// y != NULL.  keep: multipliers read (iter == NULL) or drawn in-kernel
+// (iter != NULL: vg_keep, the same draws as vg_graphnorm_fwd_drop).
+struct GnaDesc {
+  const float* stats;  // [S][2K]
+  const float* w;
+  const float* b;
+  const float* ms;
+  const float* keep;   // multipliers [rows, K] or NULL (iter == NULL)
+  float eps, p_drop;
+  int seg_rows;
+  unsigned int salt;
+  unsigned long long seed;
+  const long long* iter;
+  float* y;         // [rows, K] or NULL
+  float* keep_out;  // [rows, K] or NULL (drawn multipliers)
+};
+
+constexpr int kGnaMaxK = 128;  // GraphNorm channels the operand transform stages in LDS
+
+// one element: gp = the block's staged column operands [w | b | ms | mu0 | sd0 + eps | mu1 | sd1 + eps]
+// (segment slots 0 / 1: the tile's first row's segment and the next)
+__device__ __forceinline__ float gna_elem(const GnaDesc& ga, const float* gp, float x, int n, int k, int K,
+                                          int bound, long long it) {
+  const int sl = n >= bound ? 5 * K : 3 * K;
+  const float o = x - gp[sl + k] * gp[2 * K + k];
+  const float z = (o / gp[sl + K + k]) * gp[k] + gp[K + k];
+  float r = z > 0.f ? z : 0.f;
+  const size_t t = (size_t)n * K + k;
+  if (ga.iter) {
+    const float kv = vg_keep((long long)t, ga.salt, it, ga.seed, ga.p_drop);
+    if (ga.keep_out) ga.keep_out[t] = kv;
+    r *= kv;
+  } else if (ga.keep) {
+    r *= ga.keep[t];
+  }
+  if (ga.y) ga.y[t] = r;
+  return r;
+}
+
 // C = A . op(B) (+bias) (+act).  BT: B is [M, K] (op = B^T); else B is [K, M].
 // Software pipelined: the next K-tile is loaded into registers while the MFMAs
 // of the current one run; LDS is double-buffered (one barrier per K-tile).
@@ -345,8 +390,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // tile partials in the epilogue).  BF: bf16 operands through
 // v_mfma_f32_16x16x32_bf16 -- the f32 LDS images are converted when read
 // (lane l: row l & 15, k = 8 (l >> 4) + j).
-template <bool BT, int ACT, bool ATT = false, bool BF = false, bool GNP = false>
-__global__ void __launch_bounds__(1024) k_gemm16(const float* __restrict__ A, int lda,
+// GNA: GraphNorm + ReLU + Dropout applied to A as it loads (GnaDesc; one
+// column tile: every A element is loaded, transformed and stored once).
+template <bool BT, int ACT, bool ATT = false, bool BF = false, bool GNP = false, bool GNA = false>
+__device__ __forceinline__ void gemm16_body(const float* __restrict__ A, int lda,
                                                  const float* __restrict__ B, int ldb,
                                                  const float* __restrict__ bias,
                                                  const float* __restrict__ aux, int ldaux,
@@ -355,7 +402,7 @@ __global__ void __launch_bounds__(1024) k_gemm16(const float* __restrict__ A, in
                                                  const float* __restrict__ att_d = nullptr,
                                                  float* __restrict__ a_src = nullptr,
                                                  float* __restrict__ a_dst = nullptr,
-                                                 const GnpDesc gn = GnpDesc{}) {
+                                                 const GnpDesc gn = GnpDesc{}, const GnaDesc ga = GnaDesc{}) {
   constexpr int LDQ = BF ? TK + 4 : LDP;  // BF: 16-B aligned rows for the 8-float reads
   __shared__ __attribute__((aligned(16))) float smem[2 * TM * LDQ + 2 * TN * LDQ];
   float(*As)[TM][LDQ] = reinterpret_cast<float(*)[TM][LDQ]>(smem);
@@ -397,6 +444,24 @@ __global__ void __launch_bounds__(1024) k_gemm16(const float* __restrict__ A, in
     }
   }
   float ra[PER], rb[PER];
+  const long long g_it = (GNA && ga.iter) ? *ga.iter : 0;
+  __shared__ float gpar[GNA ? 7 * kGnaMaxK : 1];
+  int gbnd = 0;
+  if constexpr (GNA) {
+    const int seg0 = n0 / ga.seg_rows;
+    gbnd = (seg0 + 1) * ga.seg_rows;
+    const bool two = gbnd < N;
+    for (int k = t; k < K; k += 1024) {
+      gpar[k] = ga.w[k];
+      gpar[K + k] = ga.b[k];
+      gpar[2 * K + k] = ga.ms[k];
+      const float* st = ga.stats + (size_t)seg0 * 2 * K;
+      gpar[3 * K + k] = st[k];
+      gpar[4 * K + k] = st[K + k] + ga.eps;
+      gpar[5 * K + k] = two ? st[2 * K + k] : 0.f;
+      gpar[6 * K + k] = two ? st[3 * K + k] + ga.eps : 1.f;
+    }
+  }
   auto load = [&](int k0) {
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
@@ -415,8 +480,17 @@ __global__ void __launch_bounds__(1024) k_gemm16(const float* __restrict__ A, in
     }
   };
   load(0);
+  if constexpr (GNA) __syncthreads();  // the staged column operands
   int buf = 0;
   for (int k0 = 0; k0 < K; k0 += TK) {
+    if constexpr (GNA) {  // the loaded x of this K-tile -> y (stored once: one column tile)
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int e = t + 1024 * q;
+        const int n = n0 + e / TK, k = k0 + e % TK;
+        if (n < N && k < K) ra[q] = gna_elem(ga, gpar, ra[q], n, k, K, gbnd, g_it);
+      }
+    }
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
       const int e = t + 1024 * q;
@@ -540,6 +614,30 @@ __global__ void __launch_bounds__(1024) k_gemm16(const float* __restrict__ A, in
       a_dst[n0 + row] = sd;
     }
   }
+}
+
+template <bool BT, int ACT, bool ATT = false, bool BF = false, bool GNP = false>
+__global__ void __launch_bounds__(1024) k_gemm16(const float* __restrict__ A, int lda, const float* __restrict__ B,
+                                                 int ldb, const float* __restrict__ bias,
+                                                 const float* __restrict__ aux, int ldaux, float* __restrict__ C,
+                                                 int ldc, int N, int M, int K,
+                                                 const float* __restrict__ att_s = nullptr,
+                                                 const float* __restrict__ att_d = nullptr,
+                                                 float* __restrict__ a_src = nullptr,
+                                                 float* __restrict__ a_dst = nullptr, const GnpDesc gn = GnpDesc{}) {
+  gemm16_body<BT, ACT, ATT, BF, GNP, false>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, N, M, K, att_s, att_d, a_src,
+                                            a_dst, gn);
+}
+
+// the projection GEMM with the GraphNorm applied to its operand (vg_gat_lin_att_gn):
+// held to 64 VGPRs so two 16-wave workgroups share a CU (78 unconstrained:
+// the per-element GraphNorm operands and the dropout draw)
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8)))
+k_gemm16_gna(const float* __restrict__ A, const float* __restrict__ B, float* __restrict__ C, int N, int M, int K,
+             const float* __restrict__ att_s, const float* __restrict__ att_d, float* __restrict__ a_src,
+             float* __restrict__ a_dst, const GnaDesc ga) {
+  gemm16_body<true, 0, true, false, false, true>(A, K, B, K, nullptr, nullptr, 0, C, M, N, M, K, att_s, att_d,
+                                                 a_src, a_dst, GnpDesc{}, ga);
 }
 
 // k_gemm_ln's epilogue over the staged tile Ct [TMR][TN * NT + 1] (bias and
@@ -1784,6 +1882,36 @@ static int gat_lin_att(const float* X, int32_t ldx, const float* W, int32_t N,
   else
     k_gemm<true, 0, true, BF><<<dim3((N + TM - 1) / TM, 1), 256, 0, s>>>(
         X, ldx, W, Cin, nullptr, nullptr, 0, H, C, N, C, Cin, att_src, att_dst, a_src, a_dst);
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int vg_gat_lin_att_gn(const float* X, const float* W, int32_t N, int32_t Cin, int32_t C,
+                                 const float* att_src, const float* att_dst, float* H, float* a_src, float* a_dst,
+                                 const vg_gn_apply* gn, void* stream) {
+  // one column tile (C <= 64) on the 16-wave f32 tile; otherwise VG_EINVAL and
+  // the caller applies the GraphNorm itself (vg_graphnorm_fwd_gnp)
+  if (N <= 0 || Cin <= 0 || C <= 0 || C > TN || !(VG_GEMM16 & 2) || !X || !W || !att_src || !att_dst || !H ||
+      !a_src || !a_dst || !gn || !gn->stats || !gn->weight || !gn->bias || !gn->mean_scale || gn->seg_rows <= 0 ||
+      N % gn->seg_rows != 0 || gn->seg_rows < TM || Cin > kGnaMaxK || (gn->iter && gn->keep) ||
+      (gn->iter && !(gn->p_drop >= 0.f && gn->p_drop < 1.f)))
+    return VG_EINVAL;
+  GnaDesc ga;
+  ga.stats = gn->stats;
+  ga.w = gn->weight;
+  ga.b = gn->bias;
+  ga.ms = gn->mean_scale;
+  ga.keep = gn->keep;
+  ga.eps = gn->eps;
+  ga.p_drop = gn->p_drop;
+  ga.seg_rows = gn->seg_rows;
+  ga.salt = gn->salt;
+  ga.seed = gn->seed;
+  ga.iter = reinterpret_cast<const long long*>(gn->iter);
+  ga.y = gn->y;
+  ga.keep_out = gn->iter ? gn->keep_out : nullptr;
+  k_gemm16_gna<<<dim3((N + TM - 1) / TM, 1), 1024, 0, static_cast<hipStream_t>(stream)>>>(
+      X, W, H, N, C, Cin, att_src, att_dst, a_src, a_dst, ga);
   VG_CHECK_LAUNCH();
   return 0;
 }

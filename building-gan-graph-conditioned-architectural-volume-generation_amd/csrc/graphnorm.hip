@@ -885,6 +885,15 @@ extern "C" int vg_graphnorm_fwd_gnp(const float* x, int32_t S, int32_t N, int32_
                 iter ? seed : 0, iter, iter ? salt : 0, iter ? keep_out : nullptr, nullptr, stream, gnp, gnp_rows);
 }
 
+extern "C" int vg_graphnorm_stats_gnp(int32_t S, int32_t N, int32_t C, const float* gnp, int32_t gnp_rows,
+                                      float* stats, void* stream) {
+  if (S <= 0 || N <= 0 || C <= 0 || !gnp || !stats || gnp_rows <= 0 || gnp_rows > N) return VG_EINVAL;
+  k_stats_final_gnp<<<dim3(vg_blocks(C, kBlock / 64), S), kBlock, 0, static_cast<hipStream_t>(stream)>>>(
+      gnp, gnp_rows, N, C, S, stats);
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int vg_graphnorm_fwd(const float* x, int32_t N, int32_t C, const float* weight,
                                 const float* bias, const float* mean_scale, const float* keep,
                                 float eps, float* y, float* stats, float* ws, void* stream) {

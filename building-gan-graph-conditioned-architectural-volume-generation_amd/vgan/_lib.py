@@ -73,6 +73,20 @@ class VgGnBwdIn(ctypes.Structure):
 _GN_ROWS = os.environ.get("VGAN_GN_ROWS", "1") == "1"
 
 
+class VgGnApply(ctypes.Structure):
+    """vg_gn_apply (include/vgan.h): the GraphNorm + ReLU + Dropout that
+    vg_gat_lin_att_gn applies to its operand as it loads."""
+    _fields_ = [(k, _c_p) for k in ("stats", "weight", "bias", "mean_scale", "keep")] + \
+               [("eps", _c_f32), ("p_drop", _c_f32), ("seg_rows", _c_i32), ("salt", ctypes.c_uint32),
+                ("seed", ctypes.c_uint64), ("iter", _c_p), ("y", _c_p), ("keep_out", _c_p)]
+
+
+# VGAN_GN_APPLY_GEMM=1: the GraphNorm that ends a critic-engine block applied
+# in the next block's projection GEMM (vg_gat_lin_att_gn) instead of by its own
+# launch.  Off: measured slower (profiles/r02_ab_gn_apply_gemm.txt).
+_GN_APPLY_GEMM = os.environ.get("VGAN_GN_APPLY_GEMM", "0") == "1"
+
+
 class VgASrc(ctypes.Structure):
     """vg_asrc (include/vgan.h): one column block of vg_gemm_ln_act_ms's A."""
     _fields_ = [("ptr", _c_p), ("ld", _c_i32), ("cols", _c_i32), ("w_col0", _c_i32), ("rows_mod", _c_i32)]
@@ -132,6 +146,9 @@ SIGNATURES = {
     "vg_csr_ell": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p]),
     "vg_gat_aggregate_fwd_ell": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p,
                                                 _c_f32, _c_p, _c_p, _c_p]),
+    "vg_gat_lin_att_gn": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p,
+                                         ctypes.POINTER(VgGnApply), _c_p]),
+    "vg_graphnorm_stats_gnp": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p]),
     "vg_gat_gnp_rows": (_c_i32, [_c_i32, _c_i32]),
     "vg_gat_gnp_floats": (_c_i64, [_c_i32, _c_i32]),
     "vg_gat_aggregate_fwd_gnp": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p,

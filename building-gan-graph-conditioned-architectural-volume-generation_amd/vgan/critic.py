@@ -41,7 +41,9 @@ import torch.nn as nn
 
 from . import data as vdata
 from . import ops
-from ._lib import _GN_ROWS, LIB, FoldCollector, VgGnBwdIn, check, dense, ptr, stream_handle, sync_counter
+from ._lib import (_GN_ROWS, LIB, FoldCollector, VgGnApply, VgGnBwdIn, check, dense, gemm_precision, ptr,
+                   stream_handle, sync_counter)
+from . import _lib
 
 ACT_NONE, ACT_RELU, ACT_MASK = 0, 1, 3
 # VGAN_GN_FUSE=0: the GraphNorm backward's column partials in their own pass
@@ -221,11 +223,19 @@ class CriticEngine:
             mlp_out.append(y)
             x, xw = y, o
         blk = []
-        for (conv, norm), keep in zip(self.blocks, keeps):
+        pend = None  # the previous block's GraphNorm, applied in this block's projection GEMM
+        nb = len(self.blocks)
+        for bi, ((conv, norm), keep) in enumerate(zip(self.blocks, keeps)):
             c = conv.out_channels
             H, a_s, a_d = _f(R, c, dev=dev), _f(R, dev=dev), _f(R, dev=dev)
-            check(dense("vg_gat_lin_att")(ptr(x), xw, ptr(conv.lin.weight), R, xw, c, ptr(conv.att_src),
-                                     ptr(conv.att_dst), ptr(H), ptr(a_s), ptr(a_d), st), "vg_gat_lin_att")
+            if pend is not None:  # x = the previous GraphNorm's INPUT; its y / keep written by this GEMM
+                check(LIB.vg_gat_lin_att_gn(ptr(pend["O"]), ptr(conv.lin.weight), R, xw, c, ptr(conv.att_src),
+                                            ptr(conv.att_dst), ptr(H), ptr(a_s), ptr(a_d), ctypes.byref(pend["desc"]),
+                                            st), "vg_gat_lin_att_gn")
+                pend = None
+            else:
+                check(dense("vg_gat_lin_att")(ptr(x), xw, ptr(conv.lin.weight), R, xw, c, ptr(conv.att_src),
+                                              ptr(conv.att_dst), ptr(H), ptr(a_s), ptr(a_d), st), "vg_gat_lin_att")
             O, alpha = _f(R, c, dev=dev), _f(3 * E, dev=dev)
             gnp, g = ops.gnp_buffer(csr3, c, dev)  # the GraphNorm's column partials from the aggregation
             ops.aggregate_fwd_raw(csr3, c, ptr(H), ptr(a_s), ptr(a_d), ptr(conv.bias), float(conv.negative_slope),
@@ -238,12 +248,25 @@ class CriticEngine:
                     args = (None, float(spec.p), int(spec.seed), ptr(spec.iter), int(spec.salt) & 0xFFFFFFFF)
                 else:
                     args = (ptr(keep), 0.0, 0, None, 0)
-                check(LIB.vg_graphnorm_fwd_gnp(ptr(O), 3, n, c, ptr(norm.weight), ptr(norm.bias),
-                                               ptr(norm.mean_scale), *args, float(norm.eps), ptr(Y),
-                                               ptr(keep) if spec is not None else None, ptr(stats), ptr(gnp), g, st),
-                      "vg_graphnorm_fwd_gnp")
                 blk.append(dict(X=x, xw=xw, H=H, O=O, alpha=alpha, a_s=a_s, a_d=a_d, Y=Y, stats=stats, keep=keep,
                                 c=c))
+                nxt = self.blocks[bi + 1][0].out_channels if bi + 1 < nb else 0
+                if _lib._GN_APPLY_GEMM and 0 < nxt <= 64 and c <= 128 and n >= 64 and gemm_precision() == "f32":
+                    check(LIB.vg_graphnorm_stats_gnp(3, n, c, ptr(gnp), g, ptr(stats), st), "vg_graphnorm_stats_gnp")
+                    desc = VgGnApply(stats=stats.data_ptr(), weight=norm.weight.data_ptr(),
+                                     bias=norm.bias.data_ptr(), mean_scale=norm.mean_scale.data_ptr(),
+                                     keep=None if spec is not None or keep is None else keep.data_ptr(),
+                                     eps=float(norm.eps), p_drop=float(spec.p) if spec is not None else 0.0, seg_rows=n,
+                                     salt=(int(spec.salt) & 0xFFFFFFFF) if spec is not None else 0,
+                                     seed=int(spec.seed) if spec is not None else 0,
+                                     iter=spec.iter.data_ptr() if spec is not None else None, y=Y.data_ptr(),
+                                     keep_out=keep.data_ptr() if spec is not None else None)
+                    pend = dict(O=O, desc=desc)
+                else:
+                    check(LIB.vg_graphnorm_fwd_gnp(ptr(O), 3, n, c, ptr(norm.weight), ptr(norm.bias),
+                                                   ptr(norm.mean_scale), *args, float(norm.eps), ptr(Y),
+                                                   ptr(keep) if spec is not None else None, ptr(stats), ptr(gnp), g,
+                                                   st), "vg_graphnorm_fwd_gnp")
                 x, xw = Y, c
                 continue
             ws = _f(int(LIB.vg_graphnorm_seg_ws_floats(3, n, c)), dev=dev)

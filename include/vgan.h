@@ -544,6 +544,44 @@ int vg_gat_jvp_src_group(const vg_jvp_src* items, int32_t n, void* stream);
 int vg_rng_fill(float* out, int64_t n, int32_t kind, uint64_t seed, const int64_t* iter, uint32_t salt,
                 void* stream);
 
+/* ---- GraphNorm applied in the next projection's operand load --------------- */
+
+/* The GraphNorm(+ReLU+Dropout) that ends a GATConv block, applied to the next
+ * block's projection GEMM operand as it loads (models.py:73-77: module_{4b+1..3}
+ * then module_{4(b+1)}.lin): stats [segments][2C] from vg_graphnorm_stats_gnp
+ * (or any GraphNorm statistics pass), segments of seg_rows rows.  keep: dropout
+ * multipliers [rows, C] read (iter == NULL; NULL = eval, no dropout) or drawn
+ * in-kernel (iter != NULL: vg_graphnorm_fwd_drop's draws, stored to keep_out
+ * when not NULL).  y != NULL receives the GraphNorm output for the backward. */
+typedef struct vg_gn_apply {
+  const float* stats;
+  const float* weight;
+  const float* bias;
+  const float* mean_scale;
+  const float* keep;
+  float eps;
+  float p_drop;
+  int32_t seg_rows;
+  uint32_t salt;
+  uint64_t seed;
+  const int64_t* iter;
+  float* y;
+  float* keep_out;
+} vg_gn_apply;
+
+/* vg_gat_lin_att(X = GraphNorm INPUT [N, Cin], ldx = Cin) with gn applied to
+ * every element of X first: one launch and one pass over the activations
+ * fewer than vg_graphnorm_fwd_gnp + vg_gat_lin_att.  H, a_src, a_dst and y are
+ * bit-identical to that pair.  C <= 64 (one column tile), f32 products; other
+ * shapes return VG_EINVAL (apply the GraphNorm separately). */
+int vg_gat_lin_att_gn(const float* X, const float* W, int32_t N, int32_t Cin, int32_t C, const float* att_src,
+                      const float* att_dst, float* H, float* a_src, float* a_dst, const vg_gn_apply* gn,
+                      void* stream);
+/* Only the column statistics of vg_graphnorm_fwd_gnp (the fold of the
+ * aggregation's partials), for vg_gat_lin_att_gn. */
+int vg_graphnorm_stats_gnp(int32_t segments, int32_t rows, int32_t channels, const float* gnp, int32_t gnp_rows,
+                           float* stats, void* stream);
+
 /* ---- multi-source LayerNorm GEMM (no-grad stacked generator forward) ------- */
 
 /* One source of vg_gemm_ln_act_ms's A: `cols` columns (a multiple of 32) of

@@ -143,10 +143,12 @@ def test_critic_engine_and_generator_with_gnp(cuda, training, monkeypatch):
     statistics from the aggregation against the separate statistics pass:
     the same loss and gradients to f32 rounding, and the fused path runs for
     every GraphNorm of both networks."""
+    from vgan import _lib
     from vgan.flat import FlatParams
     from vgan.models import VoxelGNNGenerator
     from vgan.rng import RNG
 
+    monkeypatch.setattr(_lib, "_GN_APPLY_GEMM", False)  # every GraphNorm applies itself (counted below)
     cfg, D, flat, loc, vox, prep, hard, soft, eng = _engine_setup(cuda, numbers=(5, 6, 7), seed=17)
     D.train(training)
     torch.manual_seed(19)
@@ -183,3 +185,116 @@ def test_critic_engine_and_generator_with_gnp(cuda, training, monkeypatch):
     assert rel_err(out[True][1], out[False][1]) < 1e-4
     assert rel_err(out[True][2], out[False][2]) < 1e-5
     assert rel_err(out[True][3], out[False][3]) < 1e-4
+
+
+def _lin_att_gn_case(cuda, S, n, cin, cout, mode, seed=0):
+    """vg_gat_lin_att_gn against vg_graphnorm_fwd_gnp + vg_gat_lin_att on the
+    same GraphNorm input / statistics (keep: none, multipliers, drawn)."""
+    import ctypes
+
+    from vgan._lib import VgGnApply
+
+    g = torch.Generator(device=cuda).manual_seed(seed)
+    R = S * n
+    x = torch.randn(R, cin, device=cuda, generator=g) * 1.5 + 0.3
+    w = 1 + 0.2 * torch.randn(cin, device=cuda, generator=g)
+    b = 0.2 * torch.randn(cin, device=cuda, generator=g)
+    ms = 1 + 0.2 * torch.randn(cin, device=cuda, generator=g)
+    W = torch.randn(cout, cin, device=cuda, generator=g) / cin ** 0.5
+    att_s, att_d = torch.randn(cout, device=cuda, generator=g), torch.randn(cout, device=cuda, generator=g)
+    stats = torch.empty(S * 2 * cin, device=cuda)
+    ws = torch.empty(int(LIB.vg_graphnorm_seg_ws_floats(S, n, cin)), device=cuda)
+    st = ops.stream_handle(cuda)
+    keep_in = (torch.rand(R, cin, device=cuda, generator=g) > 0.2).float() / 0.8 if mode == "keep" else None
+    it = torch.tensor([3], dtype=torch.int64, device=cuda)
+    # reference: GraphNorm (statistics + apply), then the projection
+    y_ref, k_ref = torch.empty_like(x), torch.empty_like(x)
+    if mode == "drop":
+        check(LIB.vg_graphnorm_fwd_drop(ptr(x), S, n, cin, ptr(w), ptr(b), ptr(ms), 0.2, 99, ptr(it), 5, EPS,
+                                        ptr(y_ref), ptr(k_ref), ptr(stats), ptr(ws), None, st), "fwd_drop")
+    else:
+        check(LIB.vg_graphnorm_fwd_seg(ptr(x), S, n, cin, ptr(w), ptr(b), ptr(ms), ptr(keep_in), EPS, ptr(y_ref),
+                                       ptr(stats), ptr(ws), None, st), "fwd_seg")
+    H0, s0, d0 = torch.empty(R, cout, device=cuda), torch.empty(R, device=cuda), torch.empty(R, device=cuda)
+    check(LIB.vg_gat_lin_att(ptr(y_ref), cin, ptr(W), R, cin, cout, ptr(att_s), ptr(att_d), ptr(H0), ptr(s0),
+                             ptr(d0), st), "lin_att")
+    # fused: the same statistics, the GraphNorm applied in the operand load
+    y, kp = torch.full_like(x, float("nan")), torch.full_like(x, float("nan"))
+    H1, s1, d1 = torch.empty(R, cout, device=cuda), torch.empty(R, device=cuda), torch.empty(R, device=cuda)
+    desc = VgGnApply(stats=stats.data_ptr(), weight=w.data_ptr(), bias=b.data_ptr(), mean_scale=ms.data_ptr(),
+                     keep=keep_in.data_ptr() if keep_in is not None else None, eps=EPS,
+                     p_drop=0.2 if mode == "drop" else 0.0, seg_rows=n, salt=5 if mode == "drop" else 0,
+                     seed=99 if mode == "drop" else 0, iter=it.data_ptr() if mode == "drop" else None,
+                     y=y.data_ptr(), keep_out=kp.data_ptr() if mode == "drop" else None)
+    check(LIB.vg_gat_lin_att_gn(ptr(x), ptr(W), R, cin, cout, ptr(att_s), ptr(att_d), ptr(H1), ptr(s1), ptr(d1),
+                                ctypes.byref(desc), st), "lin_att_gn")
+    torch.cuda.synchronize()
+    return (y_ref, k_ref, H0, s0, d0), (y, kp, H1, s1, d1)
+
+
+@pytest.mark.parametrize("mode", ["none", "keep", "drop"])
+@pytest.mark.parametrize("S,n", [(1, 700), (3, 1001), (5, 130)])
+@pytest.mark.parametrize("cin,cout", [(64, 32), (32, 16), (8, 16), (16, 64), (128, 64)])
+def test_lin_att_gn_matches_separate_apply(cuda, mode, S, n, cin, cout):
+    """The GraphNorm output y, the drawn dropout multipliers and the projection
+    (H, a_src, a_dst) equal the separate GraphNorm apply + projection; the
+    tiles that straddle a segment boundary use the next segment's statistics."""
+    ref, got = _lin_att_gn_case(cuda, S, n, cin, cout, mode, seed=cin + cout + S)
+    y_ref, k_ref, H0, s0, d0 = ref
+    y, kp, H1, s1, d1 = got
+    if mode == "drop":
+        assert torch.equal(kp, k_ref)
+    # same formula and operation order as k_gn_apply4: equal up to FMA contraction
+    assert (y - y_ref).abs().max().item() <= 1e-6 * max(1.0, y_ref.abs().max().item())
+    assert rel_err(H1, H0) < 1e-6 and rel_err(s1, s0) < 1e-6 and rel_err(d1, d0) < 1e-6
+
+
+def test_lin_att_gn_rejects_unsupported(cuda):
+    """C > 64 (several column tiles), Cin > 128 or segments shorter than a
+    64-row tile: VG_EINVAL (the caller applies the GraphNorm itself)."""
+    import ctypes
+
+    from vgan._lib import VgGnApply
+
+    z = torch.zeros(256 * 256, device=cuda)
+    desc = VgGnApply(stats=z.data_ptr(), weight=z.data_ptr(), bias=z.data_ptr(), mean_scale=z.data_ptr(), eps=EPS,
+                     seg_rows=128, y=None)
+    st = ops.stream_handle(cuda)
+    for N, cin, c, seg in ((256, 32, 128, 128), (256, 256, 32, 128), (256, 32, 32, 32)):
+        desc.seg_rows = seg
+        rc = LIB.vg_gat_lin_att_gn(ptr(z), ptr(z), N, cin, c, ptr(z), ptr(z), ptr(z), ptr(z), ptr(z),
+                                   ctypes.byref(desc), st)
+        assert rc != 0
+
+
+@pytest.mark.parametrize("training", [True, False])
+def test_critic_engine_gn_apply_in_gemm(cuda, training, monkeypatch):
+    """The critic engine with each block's GraphNorm applied in the next
+    block's projection GEMM (vg_gat_lin_att_gn) against the separate apply:
+    the same loss and D gradient to f32 rounding, and the fused GEMM runs for
+    every block whose successor projects to <= 64 channels."""
+    from vgan import _lib
+
+    cfg, D, flat, loc, vox, prep, hard, soft, eng = _engine_setup(cuda, numbers=(5, 6, 7), seed=23)
+    D.train(training)
+    hd, sd = hard.to(cuda).unsqueeze(0), soft.to(cuda).unsqueeze(0)
+    calls = []
+    orig = LIB.vg_gat_lin_att_gn
+
+    def counted(*a):
+        calls.append(1)
+        return orig(*a)
+
+    monkeypatch.setattr(LIB, "vg_gat_lin_att_gn", counted)
+    out = {}
+    for fuse in (True, False):
+        monkeypatch.setattr(_lib, "_GN_APPLY_GEMM", fuse)
+        calls.clear()
+        flat.zero_grad()
+        loss = eng.loss_and_grad(loc, vox, hd, sd, _RecRNG(8))
+        torch.cuda.synchronize()
+        out[fuse] = (loss.item(), flat.grad.clone(), len(calls))
+    widths = [conv.out_channels for conv, _ in eng.blocks]
+    assert out[True][2] == sum(1 for c in widths[1:] if c <= 64) and out[False][2] == 0
+    assert abs(out[True][0] - out[False][0]) <= 1e-6 * max(1.0, abs(out[False][0]))
+    assert rel_err(out[True][1], out[False][1]) < 1e-5
