@@ -132,24 +132,34 @@ struct GnaDesc {
 
 constexpr int kGnaMaxK = 128;  // GraphNorm channels the operand transform stages in LDS
 
-// one element: gp = the block's staged column operands [w | b | ms | mu0 | sd0 + eps | mu1 | sd1 + eps]
+// gp = the block's staged column operands [w | b | ms | mu0 | sd0 + eps | mu1 | sd1 + eps]
 // (segment slots 0 / 1: the tile's first row's segment and the next)
-__device__ __forceinline__ float gna_elem(const GnaDesc& ga, const float* gp, float x, int n, int k, int K,
-                                          int bound, long long it) {
+// four consecutive columns k .. k+3 of row n (k % 4 == 0, K % 4 == 0): one
+// Philox block draws all four multipliers (vg_keep4_raw: the values vg_keep
+// gives each element), float4 stores of y / keep
+__device__ __forceinline__ float4 gna_quad(const GnaDesc& ga, const float* gp, float4 x, int n, int k, int K,
+                                           int bound, long long it) {
   const int sl = n >= bound ? 5 * K : 3 * K;
-  const float o = x - gp[sl + k] * gp[2 * K + k];
-  const float z = (o / gp[sl + K + k]) * gp[k] + gp[K + k];
-  float r = z > 0.f ? z : 0.f;
   const size_t t = (size_t)n * K + k;
+  float4 kv = make_float4(1.f, 1.f, 1.f, 1.f);
   if (ga.iter) {
-    const float kv = vg_keep((long long)t, ga.salt, it, ga.seed, ga.p_drop);
-    if (ga.keep_out) ga.keep_out[t] = kv;
-    r *= kv;
+    kv = vg_keep4_raw((long long)(t >> 2), ga.salt, it, ga.seed, ga.p_drop);
+    if (ga.keep_out) *reinterpret_cast<float4*>(ga.keep_out + t) = kv;
   } else if (ga.keep) {
-    r *= ga.keep[t];
+    kv = *reinterpret_cast<const float4*>(ga.keep + t);
   }
-  if (ga.y) ga.y[t] = r;
-  return r;
+  const bool mul = ga.iter || ga.keep;
+  float xv[4] = {x.x, x.y, x.z, x.w}, kk[4] = {kv.x, kv.y, kv.z, kv.w}, r[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float o = xv[j] - gp[sl + k + j] * gp[2 * K + k + j];
+    const float z = (o / gp[sl + K + k + j]) * gp[k + j] + gp[K + k + j];
+    r[j] = z > 0.f ? z : 0.f;
+    if (mul) r[j] *= kk[j];
+  }
+  const float4 y = make_float4(r[0], r[1], r[2], r[3]);
+  if (ga.y) *reinterpret_cast<float4*>(ga.y + t) = y;
+  return y;
 }
 
 // C = A . op(B) (+bias) (+act).  BT: B is [M, K] (op = B^T); else B is [K, M].
@@ -462,13 +472,23 @@ __device__ __forceinline__ void gemm16_body(const float* __restrict__ A, int lda
       gpar[6 * K + k] = two ? st[3 * K + k] + ga.eps : 1.f;
     }
   }
+  // GNA: A as float4 quads, threads 0..511 (one row quad each per K-tile)
+  float4 rq = make_float4(0.f, 0.f, 0.f, 0.f);
+  constexpr int QPR = TK / 4;  // quads per tile row
   auto load = [&](int k0) {
+    if constexpr (GNA) {
+      if (t < TM * QPR) {
+        const int n = n0 + t / QPR, k = k0 + 4 * (t % QPR);
+        rq = (n < N && k < K) ? *reinterpret_cast<const float4*>(A + (size_t)n * lda + k)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
       const int e = t + 1024 * q;
       const int row = e / TK, kc = e % TK;
       const int n = n0 + row, k = k0 + kc;
-      ra[q] = (n < N && k < K) ? A[(size_t)n * lda + k] : 0.f;
+      if constexpr (!GNA) ra[q] = (n < N && k < K) ? A[(size_t)n * lda + k] : 0.f;
       if (BT) {
         const int m = m0 + row;
         rb[q] = (m < M && k < K) ? B[(size_t)m * ldb + k] : 0.f;
@@ -483,18 +503,21 @@ __device__ __forceinline__ void gemm16_body(const float* __restrict__ A, int lda
   if constexpr (GNA) __syncthreads();  // the staged column operands
   int buf = 0;
   for (int k0 = 0; k0 < K; k0 += TK) {
-    if constexpr (GNA) {  // the loaded x of this K-tile -> y (stored once: one column tile)
-#pragma unroll
-      for (int q = 0; q < PER; ++q) {
-        const int e = t + 1024 * q;
-        const int n = n0 + e / TK, k = k0 + e % TK;
-        if (n < N && k < K) ra[q] = gna_elem(ga, gpar, ra[q], n, k, K, gbnd, g_it);
+    if constexpr (GNA) {  // the loaded x quad of this K-tile -> y (stored once: one column tile)
+      if (t < TM * QPR) {
+        const int row = t / QPR, kq = 4 * (t % QPR);
+        const int n = n0 + row, k = k0 + kq;
+        if (n < N && k < K) rq = gna_quad(ga, gpar, rq, n, k, K, gbnd, g_it);
+        As[buf][row][kq] = rq.x;
+        As[buf][row][kq + 1] = rq.y;
+        As[buf][row][kq + 2] = rq.z;
+        As[buf][row][kq + 3] = rq.w;
       }
     }
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
       const int e = t + 1024 * q;
-      As[buf][e / TK][e % TK] = ra[q];
+      if constexpr (!GNA) As[buf][e / TK][e % TK] = ra[q];
       if (BT) Bs[buf][e / TK][e % TK] = rb[q];
       else Bs[buf][e % TN][e / TN] = rb[q];
     }
@@ -1893,7 +1916,10 @@ extern "C" int vg_gat_lin_att_gn(const float* X, const float* W, int32_t N, int3
   // the caller applies the GraphNorm itself (vg_graphnorm_fwd_gnp)
   if (N <= 0 || Cin <= 0 || C <= 0 || C > TN || !(VG_GEMM16 & 2) || !X || !W || !att_src || !att_dst || !H ||
       !a_src || !a_dst || !gn || !gn->stats || !gn->weight || !gn->bias || !gn->mean_scale || gn->seg_rows <= 0 ||
-      N % gn->seg_rows != 0 || gn->seg_rows < TM || Cin > kGnaMaxK || (gn->iter && gn->keep) ||
+      N % gn->seg_rows != 0 || gn->seg_rows < TM || Cin > kGnaMaxK || Cin % 4 != 0 ||
+      (reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(gn->y) & 15) ||
+      (reinterpret_cast<uintptr_t>(gn->keep) & 15) || (reinterpret_cast<uintptr_t>(gn->keep_out) & 15) ||
+      (gn->iter && gn->keep) ||
       (gn->iter && !(gn->p_drop >= 0.f && gn->p_drop < 1.f)))
     return VG_EINVAL;
   GnaDesc ga;
