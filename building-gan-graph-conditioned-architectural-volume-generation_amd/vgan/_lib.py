@@ -87,6 +87,32 @@ class VgGnApply(ctypes.Structure):
 _GN_APPLY_GEMM = os.environ.get("VGAN_GN_APPLY_GEMM", "0") == "1"
 
 
+class VgChainLayer(ctypes.Structure):
+    """vg_chain_layer (include/vgan.h): one layer of vg_linear_chain."""
+    _fields_ = [(k, _c_p) for k in ("weight", "bias", "aux", "out")] + \
+               [(k, _c_i32) for k in ("ld_aux", "ld_out", "w_trans", "act")]
+
+
+# VGAN_CHAIN=0: the critic's decoder chains as one vg_gemm launch per layer
+# instead of one vg_linear_chain launch per pass (A/B knob)
+_CHAIN = os.environ.get("VGAN_CHAIN", "1") == "1"
+
+
+def linear_chain(x, ldx: int, rows: int, widths, layers, stream) -> bool:
+    """vg_linear_chain over ``layers`` (dicts of VgChainLayer fields; device
+    pointers as ints / c_void_p); False when the width chain has no kernel
+    (the caller runs its per-layer GEMMs)."""
+    if not _CHAIN or _precision != "f32":
+        return False
+    n = len(layers)
+    arr = (VgChainLayer * n)()
+    for i, l in enumerate(layers):
+        for k, v in l.items():
+            setattr(arr[i], k, v.value if isinstance(v, ctypes.c_void_p) else v)
+    w = (ctypes.c_int32 * (n + 1))(*widths)
+    return LIB.vg_linear_chain(x, ldx, rows, w, n, arr, stream) == 0
+
+
 class VgASrc(ctypes.Structure):
     """vg_asrc (include/vgan.h): one column block of vg_gemm_ln_act_ms's A."""
     _fields_ = [("ptr", _c_p), ("ld", _c_i32), ("cols", _c_i32), ("w_col0", _c_i32), ("rows_mod", _c_i32)]
@@ -149,6 +175,7 @@ SIGNATURES = {
     "vg_gat_lin_att_gn": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p,
                                          ctypes.POINTER(VgGnApply), _c_p]),
     "vg_graphnorm_stats_gnp": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p]),
+    "vg_linear_chain": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p]),
     "vg_gat_gnp_rows": (_c_i32, [_c_i32, _c_i32]),
     "vg_gat_gnp_floats": (_c_i64, [_c_i32, _c_i32]),
     "vg_gat_aggregate_fwd_gnp": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p,

@@ -41,11 +41,12 @@ import torch.nn as nn
 
 from . import data as vdata
 from . import ops
-from ._lib import (_GN_ROWS, LIB, FoldCollector, VgGnApply, VgGnBwdIn, check, dense, gemm_precision, ptr,
-                   stream_handle, sync_counter)
+from ._lib import (_GN_ROWS, LIB, FoldCollector, VgGnApply, VgGnBwdIn, check, dense, gemm_precision,
+                   linear_chain, ptr, stream_handle, sync_counter)
 from . import _lib
 
 ACT_NONE, ACT_RELU, ACT_MASK = 0, 1, 3
+_CHAIN_TANGENT = os.environ.get("VGAN_CHAIN_TANGENT", "0") == "1"
 # VGAN_GN_FUSE=0: the GraphNorm backward's column partials in their own pass
 # instead of the epilogue of the GEMM producing its g_y (A/B knob)
 _GN_FUSE = os.environ.get("VGAN_GN_FUSE", "1") == "1"
@@ -282,15 +283,17 @@ class CriticEngine:
                                                ptr(ws), sy, st), "vg_graphnorm_fwd_seg")
             blk.append(dict(X=x, xw=xw, H=H, O=O, alpha=alpha, a_s=a_s, a_d=a_d, Y=Y, stats=stats, keep=keep, c=c))
             x, xw = Y, c
-        dec_out = []
-        for i, lin in enumerate(self.dec):
-            o = lin.out_features
-            last = i == nd - 1
-            z = _f(R if last else X4, o, dev=dev)
-            self._gemm(st, ptr(x), xw, ptr(lin.weight), xw, 1, ptr(z), o, R, o, xw, ptr(lin.bias),
-                       ACT_NONE if last else ACT_RELU)
-            dec_out.append(z)
-            x, xw = z, o
+        dec_out = [_f(R if i == nd - 1 else X4, lin.out_features, dev=dev) for i, lin in enumerate(self.dec)]
+        dec_w = [xw] + [lin.out_features for lin in self.dec]
+        if not linear_chain(ptr(x), xw, R, dec_w,
+                            [dict(weight=lin.weight.data_ptr(), bias=lin.bias.data_ptr(), out=z.data_ptr(),
+                                  ld_out=lin.out_features, act=ACT_NONE if i == nd - 1 else ACT_RELU)
+                             for i, (lin, z) in enumerate(zip(self.dec, dec_out))], st):
+            for i, lin in enumerate(self.dec):
+                o = lin.out_features
+                self._gemm(st, ptr(x), xw, ptr(lin.weight), xw, 1, ptr(dec_out[i]), o, R, o, xw, ptr(lin.bias),
+                           ACT_NONE if i == nd - 1 else ACT_RELU)
+                x, xw = dec_out[i], o
         scores = dec_out[-1]
         if scores.shape[1] != 1:
             raise ValueError("the critic must output one score per node")
@@ -308,12 +311,25 @@ class CriticEngine:
         adj_H = [_f(X4, B["c"], dev=dev) for B in blk]
         adj_mlp = [_f(X4, l.out_features, dev=dev) for l in self.mlp]
 
+        def adj_chain(r0: int, nrows: int, r_aux: int) -> bool:
+            """the decoder's adjoint chain adj_dec[nd-1] -> ... -> adj_dec[0]
+            (rows r0.. of the adjoint buffers, masks from rows r_aux.. of the
+            forward outputs) as one vg_linear_chain launch"""
+            ws = [self.dec[i].weight.shape[0] for i in range(nd - 1, 0, -1)] + [self.dec[0].weight.shape[0]]
+            return linear_chain(rows(adj_dec[nd - 1], r0, ws[0]), ws[0], nrows, ws,
+                                [dict(weight=self.dec[i].weight.data_ptr(), w_trans=1, act=ACT_MASK,
+                                      aux=rows(dec_out[i - 1], r_aux, self.dec[i].weight.shape[1]),
+                                      ld_aux=self.dec[i].weight.shape[1],
+                                      out=rows(adj_dec[i - 1], r0, self.dec[i].weight.shape[1]),
+                                      ld_out=self.dec[i].weight.shape[1]) for i in range(nd - 1, 0, -1)], st)
+
         # ---------------------------------------------------------- pass B
-        for i in range(nd - 1, 0, -1):
-            Wt = self.dec[i].weight
-            aw, m = Wt.shape
-            self._gemm(st, rows(adj_dec[i], trow, aw), aw, ptr(Wt), m, 0, rows(adj_dec[i - 1], trow, m), m, n, m, aw,
-                       None, ACT_MASK, rows(dec_out[i - 1], mrow, m), m)
+        if not adj_chain(trow, n, mrow):
+            for i in range(nd - 1, 0, -1):
+                Wt = self.dec[i].weight
+                aw, m = Wt.shape
+                self._gemm(st, rows(adj_dec[i], trow, aw), aw, ptr(Wt), m, 0, rows(adj_dec[i - 1], trow, m), m, n, m,
+                           aw, None, ACT_MASK, rows(dec_out[i - 1], mrow, m), m)
         W = self.dec[0].weight
         dY = _f(n, W.shape[1], dev=dev)
         tp = gemm_dy(rows(adj_dec[0], trow, W.shape[0]), W.shape[0], ptr(W), W.shape[1], ptr(dY), n, W.shape[1],
@@ -403,25 +419,37 @@ class CriticEngine:
                   "vg_graphnorm_jvp2")
             hinj_b[b], oinj_b[b] = hinj, oinj
             u_in, uw = rows(B["Y"], trow, c), c
-        for i, lin in enumerate(self.dec[:-1]):
-            o = lin.out_features
-            self._gemm(st, u_in, uw, ptr(lin.weight), uw, 1, rows(dec_out[i], trow, o), o, n, o, uw, None, ACT_MASK,
-                       rows(dec_out[i], mrow, o), o)
-            u_in, uw = rows(dec_out[i], trow, o), o
+        # the tangent chain stays per-layer GEMMs: one thread per row through
+        # 64-32-16-8 measured 25.8 us against 16.9 us for the three GEMMs at
+        # 12.7k rows (profiles/r02_chain_probe.json; forward 29.6 vs 31.2 us,
+        # adjoint 15.3 vs 24.1 us at 38k rows)
+        tan_w = [uw] + [lin.out_features for lin in self.dec[:-1]]
+        if not _CHAIN_TANGENT or not linear_chain(u_in, uw, n, tan_w,
+                            [dict(weight=lin.weight.data_ptr(), act=ACT_MASK,
+                                  aux=rows(dec_out[i], mrow, lin.out_features), ld_aux=lin.out_features,
+                                  out=rows(dec_out[i], trow, lin.out_features), ld_out=lin.out_features)
+                             for i, lin in enumerate(self.dec[:-1])], st):
+            for i, lin in enumerate(self.dec[:-1]):
+                o = lin.out_features
+                self._gemm(st, u_in, uw, ptr(lin.weight), uw, 1, rows(dec_out[i], trow, o), o, n, o, uw, None,
+                           ACT_MASK, rows(dec_out[i], mrow, o), o)
+                u_in, uw = rows(dec_out[i], trow, o), o
 
         folds.run_jvp_src(st)  # every block's dQ/dh injection, one launch
 
         # ---------------------------------------------------------- pass D
         # weight gradients over 4N rows: [pass-D adjoint ; pass-B adjoint]^T [activation ; tangent]
         dec_in = [blk[-1]["Y"] if blk else mlp_out[-1]] + dec_out[:-1]
+        chained = adj_chain(0, R, 0)  # the adjoint chain first; the weight-gradient products are deferred
         for i in range(nd - 1, -1, -1):
             lin = self.dec[i]
             aw, m = lin.weight.shape
             self._gemm_tn(folds, st, dev, ptr(adj_dec[i]), aw, ptr(dec_in[i]), m, X4, aw, m, ptr(lin.weight.grad), m,
                           ptr(lin.bias.grad), R)
             if i > 0:
-                self._gemm(st, ptr(adj_dec[i]), aw, ptr(lin.weight), m, 0, ptr(adj_dec[i - 1]), m, R, m, aw, None,
-                           ACT_MASK, ptr(dec_out[i - 1]), m)
+                if not chained:
+                    self._gemm(st, ptr(adj_dec[i]), aw, ptr(lin.weight), m, 0, ptr(adj_dec[i - 1]), m, R, m, aw, None,
+                               ACT_MASK, ptr(dec_out[i - 1]), m)
             else:
                 dY = _f(R, m, dev=dev)
                 tp = gemm_dy(ptr(adj_dec[0]), aw, ptr(lin.weight), m, ptr(dY), R, m, aw, nb - 1, False)

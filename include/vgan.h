@@ -582,6 +582,33 @@ int vg_gat_lin_att_gn(const float* X, const float* W, int32_t N, int32_t Cin, in
 int vg_graphnorm_stats_gnp(int32_t segments, int32_t rows, int32_t channels, const float* gnp, int32_t gnp_rows,
                            float* stats, void* stream);
 
+/* ---- row-local chains of narrow linear layers ------------------------------ */
+
+/* One layer of vg_linear_chain: y = x W^T (w_trans 0, weight [out][in], an
+ * nn.Linear forward) or y = x W (w_trans 1, weight [in][out]: the adjoint of
+ * an nn.Linear of weight [in][out]), + bias (NULL: none), then act 0 none,
+ * 1 ReLU, 3 mask (y = aux[row][j] > 0 ? y : 0, aux [rows][ld_aux]: ReLU's
+ * derivative taken from the layer's forward output); out [rows][ld_out]
+ * receives y (NULL: not stored). */
+typedef struct vg_chain_layer {
+  const float* weight;
+  const float* bias;
+  const float* aux;
+  float* out;
+  int32_t ld_aux;
+  int32_t ld_out;
+  int32_t w_trans;
+  int32_t act;
+} vg_chain_layer;
+
+/* nlayers (2-4) narrow linear layers applied row by row in ONE launch: the
+ * critic's decoder (models.py:273-279) forward 64-32-16-8-1, its tangent
+ * 64-32-16-8 and its adjoint 1-8-16-32 (vgan/critic.py passes A-D), each
+ * formerly one vg_gemm launch per layer.  widths [nlayers + 1]; rows of x
+ * ldx floats apart.  Other width chains return VG_EINVAL (use vg_gemm). */
+int vg_linear_chain(const float* x, int32_t ldx, int32_t rows, const int32_t* widths, int32_t nlayers,
+                    const vg_chain_layer* layers, void* stream);
+
 /* ---- multi-source LayerNorm GEMM (no-grad stacked generator forward) ------- */
 
 /* One source of vg_gemm_ln_act_ms's A: `cols` columns (a multiple of 32) of
