@@ -419,10 +419,9 @@ class CriticEngine:
                   "vg_graphnorm_jvp2")
             hinj_b[b], oinj_b[b] = hinj, oinj
             u_in, uw = rows(B["Y"], trow, c), c
-        # the tangent chain stays per-layer GEMMs: one thread per row through
-        # 64-32-16-8 measured 25.8 us against 16.9 us for the three GEMMs at
-        # 12.7k rows (profiles/r02_chain_probe.json; forward 29.6 vs 31.2 us,
-        # adjoint 15.3 vs 24.1 us at 38k rows)
+        # the tangent chain stays per-layer GEMMs (VGAN_CHAIN_TANGENT=1: the
+        # chain): 16.0 vs 16.6 us at 12.7k rows and the step flat
+        # (profiles/r02_chain_probe_p4.json, profiles/r02_ab_chain.txt)
         tan_w = [uw] + [lin.out_features for lin in self.dec[:-1]]
         if not _CHAIN_TANGENT or not linear_chain(u_in, uw, n, tan_w,
                             [dict(weight=lin.weight.data_ptr(), act=ACT_MASK,
