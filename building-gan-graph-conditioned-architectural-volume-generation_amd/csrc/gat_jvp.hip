@@ -53,8 +53,45 @@ __global__ void __launch_bounds__(kBlock) k_jvp_att(const float* __restrict__ u,
   }
 }
 
+// The tangent sweep's GraphNorm column sums formed where the GraphNorm's
+// input tangent u is produced (GNJ; vg_gat_jvp2_gn_deferred): per column
+// [sum u, sum xt u, sum p, sum p u, sum p xt] with xt = x - mu,
+// p = g_y [z > 0] keep -- the sums of graphnorm.hip's k_gn_jvp2_partial, which
+// re-read x, u, g_y and keep in a launch of its own -- as one row of partials
+// per workgroup, part [blocks][5][C] (groups in order: deterministic).
+struct GnJvp {
+  const float* x;
+  const float* keep;
+  const float* gy;
+  const float* stats;
+  const float* w;
+  const float* b;
+  const float* ms;
+  float eps;
+  float* part;
+};
+
+template <int L, int CPL>
+__device__ __forceinline__ void gnj_block_sums(const Vec<CPL> (&v)[5], int C, float* __restrict__ part) {
+  constexpr int G = kBlock / L, Wg = L * CPL;
+  __shared__ float red[kBlock * CPL];  // G groups x Wg channels
+  const int grp = threadIdx.x / L, lane = threadIdx.x & (L - 1);
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    __syncthreads();  // the previous sum (or the att_dst partials) is done with red
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) red[grp * Wg + lane * CPL + q] = v[k].v[q];
+    __syncthreads();
+    for (int c = threadIdx.x; c < Wg; c += kBlock) {
+      float s = 0.f;
+      for (int g = 0; g < G; ++g) s += red[g * Wg + c];
+      if (c < C) part[((size_t)blockIdx.x * 5 + k) * C + c] = s;
+    }
+  }
+}
+
 // e_u / e_h: per-edge U, H written by the lane that reads them back (no restrict).
-template <int L, int CPL, bool VEC>
+template <int L, int CPL, bool VEC, bool GNJ = false>
 __global__ void __launch_bounds__(kBlock) k_jvp_rows(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, int N, int C,
     const float* __restrict__ h, const float* __restrict__ u, const float* __restrict__ gv,
@@ -62,13 +99,31 @@ __global__ void __launch_bounds__(kBlock) k_jvp_rows(
     const float* __restrict__ up_src, const float* __restrict__ up_dst,
     const float* __restrict__ alpha, float slope, float* __restrict__ u_out, float* e_u,
     float* e_h, float* __restrict__ e_gz, float* __restrict__ e_gzp, float* __restrict__ e_alp,
-    float* __restrict__ n_gad, float* __restrict__ part) {
+    float* __restrict__ n_gad, float* __restrict__ part, const GnJvp gj = GnJvp{}) {
   constexpr int G = kBlock / L;
   const int grp = threadIdx.x / L, lane = threadIdx.x & (L - 1);
   const int c0 = lane * CPL;
   Vec<CPL> pd;
 #pragma unroll
   for (int q = 0; q < CPL; ++q) pd.v[q] = 0.f;
+  // GNJ: the lane's columns' GraphNorm operands and its five running sums
+  Vec<CPL> gmu, gs, gw, gb, gms, gsum[5];
+  if constexpr (GNJ) {
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) {
+      const int c = c0 + q;
+      const bool ok = c < C;
+      gmu.v[q] = ok ? gj.stats[c] : 0.f;
+      gs.v[q] = ok ? gj.stats[C + c] + gj.eps : 1.f;
+      gw.v[q] = ok ? gj.w[c] : 0.f;
+      gb.v[q] = ok ? gj.b[c] : 0.f;
+      gms.v[q] = ok ? gj.ms[c] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+#pragma unroll
+      for (int q = 0; q < CPL; ++q) gsum[k].v[q] = 0.f;
+  }
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
   for (int i = lb * G + grp; i < N; i += gridDim.x * G) {
     const int beg = row_ptr[i], end = row_ptr[i + 1];
@@ -117,6 +172,25 @@ __global__ void __launch_bounds__(kBlock) k_jvp_rows(
         }
     }
     store_row<CPL, VEC>(acc, u_out + (size_t)i * C, c0, C);
+    if constexpr (GNJ) {  // this row's terms of the GraphNorm tangent sums (k_gn_jvp2_partial's formulas)
+      Vec<CPL> xv, gyv, kv;
+      load_row<CPL, VEC>(xv, gj.x + (size_t)i * C, c0, C);
+      load_row<CPL, VEC>(gyv, gj.gy + (size_t)i * C, c0, C);
+      if (gj.keep) load_row<CPL, VEC>(kv, gj.keep + (size_t)i * C, c0, C);
+#pragma unroll
+      for (int q = 0; q < CPL; ++q) {
+        const float uv = acc.v[q];
+        const float xt = xv.v[q] - gmu.v[q];
+        const float z = ((xv.v[q] - gmu.v[q] * gms.v[q]) / gs.v[q]) * gw.v[q] + gb.v[q];
+        float pv = z > 0.f ? gyv.v[q] : 0.f;
+        if (gj.keep) pv *= kv.v[q];
+        gsum[0].v[q] += uv;
+        gsum[1].v[q] = fmaf(xt, uv, gsum[1].v[q]);
+        gsum[2].v[q] += pv;
+        gsum[3].v[q] = fmaf(pv, uv, gsum[3].v[q]);
+        gsum[4].v[q] = fmaf(pv, xt, gsum[4].v[q]);
+      }
+    }
     float gad = 0.f, gpd = 0.f;
     for (int k = beg + lane; k < end; k += L) {
       const int j = col[k];
@@ -143,6 +217,7 @@ __global__ void __launch_bounds__(kBlock) k_jvp_rows(
     for (int q = 0; q < CPL; ++q) pd.v[q] = fmaf(gad, hi.v[q], fmaf(gpd, ui.v[q], pd.v[q]));
   }
   block_partials<L, CPL>(&pd, 1, C, part);
+  if constexpr (GNJ) gnj_block_sums<L, CPL>(gsum, C, gj.part);
 }
 
 // The source pass as a block body: logical block lb of nb (one launch of
@@ -347,7 +422,29 @@ static int jvp2(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_p
                 const float* g_out, const float* att_src, const float* att_dst, const float* a_src,
                 const float* a_dst, const float* alpha, float slope, float* u_out, float* h_inj,
                 float* g_att_src, float* g_att_dst, const float* up_src_in, const float* up_dst_in,
-                float* workspace, vg_fold* folds_out, int32_t* n_out, vg_jvp_src* src_out, void* stream);
+                float* workspace, vg_fold* folds_out, int32_t* n_out, vg_jvp_src* src_out, void* stream,
+                const vg_gn_jvp* gn = nullptr);
+
+extern "C" int32_t vg_gat_jvp2_blocks(int32_t N, int32_t C) {
+  Shape sh;
+  if (N <= 0 || !jvp_shape(C, sh)) return 0;
+  const int grid = grid_for(N, sh.L);
+  return grid > kMaxBlocks ? kMaxBlocks : grid;
+}
+
+extern "C" int vg_gat_jvp2_gn_deferred(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,
+                                       const int32_t* csc_slot, const int32_t* csc_dst, int32_t N, int32_t E,
+                                       int32_t C, const float* h, const float* u, const float* g_out,
+                                       const float* att_src, const float* att_dst, const float* a_src,
+                                       const float* a_dst, const float* alpha, float slope, float* u_out,
+                                       float* h_inj, float* g_att_src, float* g_att_dst, const float* up_src_in,
+                                       const float* up_dst_in, float* workspace, const vg_gn_jvp* gn,
+                                       vg_fold* folds_out, int32_t* n_out, void* stream) {
+  if (!gn || !folds_out || !n_out) return VG_EINVAL;
+  return jvp2(row_ptr, col, csc_ptr, csc_slot, csc_dst, N, E, C, h, u, g_out, att_src, att_dst, a_src, a_dst,
+              alpha, slope, u_out, h_inj, g_att_src, g_att_dst, up_src_in, up_dst_in, workspace, folds_out, n_out,
+              nullptr, stream, gn);
+}
 
 extern "C" int vg_gat_jvp2_deferred(const int32_t* row_ptr, const int32_t* col,
                                     const int32_t* csc_ptr, const int32_t* csc_slot,
@@ -404,8 +501,11 @@ static int jvp2(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_p
                 const float* g_out, const float* att_src, const float* att_dst, const float* a_src,
                 const float* a_dst, const float* alpha, float slope, float* u_out, float* h_inj,
                 float* g_att_src, float* g_att_dst, const float* up_src_in, const float* up_dst_in,
-                float* workspace, vg_fold* folds_out, int32_t* n_out, vg_jvp_src* src_out, void* stream) {
+                float* workspace, vg_fold* folds_out, int32_t* n_out, vg_jvp_src* src_out, void* stream,
+                const vg_gn_jvp* gn) {
   if ((folds_out == nullptr) != (n_out == nullptr)) return VG_EINVAL;
+  if (gn && (!gn->x || !gn->g_y || !gn->stats || !gn->weight || !gn->bias || !gn->mean_scale || !gn->part))
+    return VG_EINVAL;
   if (n_out) *n_out = 0;
   Shape sh;
   if (N <= 0 || E <= 0 || !row_ptr || !col || !csc_ptr || !csc_slot || !csc_dst || !h || !u ||
@@ -431,9 +531,16 @@ static int jvp2(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_p
   if (!up_src_in)  // tangent projections not supplied by the tangent GEMM's epilogue
     VG_DISPATCH_JVP(C, (k_jvp_att<L_, CPL_, V_><<<grid_for(N, L_), kBlock, 0, s>>>(
                            u, N, C, att_src, att_dst, up_src_ws, up_dst_ws)));
-  VG_DISPATCH_JVP(C, (k_jvp_rows<L_, CPL_, V_><<<grid, kBlock, 0, s>>>(
-                         row_ptr, col, N, C, h, u, g_out, a_src, a_dst, up_src, up_dst, alpha,
-                         slope, u_out, e_u, e_h, e_gz, e_gzp, e_alp, n_gad, part_r)));
+  if (gn) {
+    const GnJvp gj{gn->x, gn->keep, gn->g_y, gn->stats, gn->weight, gn->bias, gn->mean_scale, gn->eps, gn->part};
+    VG_DISPATCH_JVP(C, (k_jvp_rows<L_, CPL_, V_, true><<<grid, kBlock, 0, s>>>(
+                           row_ptr, col, N, C, h, u, g_out, a_src, a_dst, up_src, up_dst, alpha,
+                           slope, u_out, e_u, e_h, e_gz, e_gzp, e_alp, n_gad, part_r, gj)));
+  } else {
+    VG_DISPATCH_JVP(C, (k_jvp_rows<L_, CPL_, V_><<<grid, kBlock, 0, s>>>(
+                           row_ptr, col, N, C, h, u, g_out, a_src, a_dst, up_src, up_dst, alpha,
+                           slope, u_out, e_u, e_h, e_gz, e_gzp, e_alp, n_gad, part_r)));
+  }
   const int shape_id = jvp_shape_id(C, sh);
   if (src_out && shape_id >= 0) {  // described for vg_gat_jvp_src_group
     *src_out = vg_jvp_src{csc_ptr, csc_slot, csc_dst, h, u, g_out, att_src, att_dst, e_gz, e_gzp, e_alp,

@@ -594,6 +594,49 @@ __global__ void __launch_bounds__(kBlock) k_gn_jvp2_final(
   g_ms[c] += wc * (-mup * Sp / d + mu * Sp * M * isd / (d * d));
 }
 
+// The same fold over the rows of partials the GAT tangent pass wrote
+// (vg_gat_jvp2_gn_deferred: part [blocks][5][C]); one wave per column, lane l
+// sums blocks l, l + 64, ... in order (16 in flight), then the butterfly.
+__global__ void __launch_bounds__(kBlock) k_gn_jvp2_final_blk(
+    const float* __restrict__ part, int blocks, int N, int C, const float* __restrict__ w,
+    const float* __restrict__ ms, float eps, const float* __restrict__ stats,
+    float* __restrict__ sums, float* __restrict__ g_w, float* __restrict__ g_ms) {
+  const int c = fold_col(), lane = threadIdx.x & 63;
+  if (c >= C) return;
+  constexpr int U = 16;
+  float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int b0 = lane; b0 < blocks; b0 += 64 * U) {
+    float t[U][5];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int b = b0 + 64 * u;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) t[u][q] = b < blocks ? part[((size_t)b * 5 + q) * C + c] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int q = 0; q < 5; ++q) v[q] += t[u][q];
+  }
+#pragma unroll
+  for (int q = 0; q < 5; ++q) v[q] = wave_sum(v[q]);
+  if (lane != 0) return;
+  const float inv_n = 1.f / static_cast<float>(N);
+  const float mu = stats[c], sd = stats[C + c], d = sd + eps, msc = ms[c], wc = w[c];
+  const float mup = v[0] * inv_n, M = v[1] * inv_n, Sp = v[2];
+  const float P1 = v[3] - msc * mup * Sp;
+  const float P2 = v[4] + (1.f - msc) * mu * Sp;
+  const float isd = sd > 0.f ? 1.f / sd : 0.f;
+  float* sm = sums + (size_t)c * 5;
+  sm[0] = mup;
+  sm[1] = M;
+  sm[2] = Sp;
+  sm[3] = P1;
+  sm[4] = P2;
+  g_w[c] += P1 / d - P2 * M * isd / (d * d);
+  g_ms[c] += wc * (-mup * Sp / d + mu * Sp * M * isd / (d * d));
+}
+
 // u_out = keep [z>0] w (c'/d - c sigma'/d^2);  x_inj = dQ/dx
 __global__ void k_gn_jvp2_apply(const float* __restrict__ x, const float* __restrict__ u,
                                 const float* __restrict__ gy, long long total, int N, int C,
@@ -984,6 +1027,25 @@ extern "C" int vg_graphnorm_bwd(const float* x, int32_t N, int32_t C, const floa
   if (!g_w || !g_b || !g_ms) return VG_EINVAL;
   return vg_graphnorm_bwd_seg(x, 1, N, C, weight, bias, mean_scale, keep, eps, stats, g_y, g_x,
                               g_w, g_b, g_ms, 0, nullptr, 0, ws, nullptr, stream);
+}
+
+extern "C" int vg_graphnorm_jvp2_part(const float* x, int32_t N, int32_t C, const float* weight,
+                                      const float* bias, const float* mean_scale, const float* keep, float eps,
+                                      const float* stats, const float* u, const float* g_y, float* u_out,
+                                      float* x_inj, float* g_w, float* g_ms, const float* part, int32_t blocks,
+                                      float* ws, void* stream) {
+  if (N <= 0 || C <= 0 || !x || !weight || !bias || !mean_scale || !stats || !u || !g_y || !u_out || !x_inj ||
+      !g_w || !g_ms || !part || blocks <= 0 || !ws)
+    return VG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  float* sums = ws + (size_t)kChunks * C * 5;  // the same workspace layout as vg_graphnorm_jvp2
+  k_gn_jvp2_final_blk<<<vg_blocks(C, kBlock / 64), kBlock, 0, s>>>(part, blocks, N, C, weight, mean_scale, eps,
+                                                                   stats, sums, g_w, g_ms);
+  const long long total = (long long)N * C;
+  k_gn_jvp2_apply<<<apply_blocks(total), 256, 0, s>>>(x, u, g_y, total, N, C, weight, bias, mean_scale, keep, eps,
+                                                      stats, sums, u_out, x_inj);
+  VG_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int vg_graphnorm_jvp2(const float* x, int32_t N, int32_t C, const float* weight,

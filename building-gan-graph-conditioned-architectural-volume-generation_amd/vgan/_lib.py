@@ -87,6 +87,19 @@ class VgGnApply(ctypes.Structure):
 _GN_APPLY_GEMM = os.environ.get("VGAN_GN_APPLY_GEMM", "0") == "1"
 
 
+class VgGnJvp(ctypes.Structure):
+    """vg_gn_jvp (include/vgan.h): the GraphNorm whose tangent sums the GAT
+    tangent pass forms (vg_gat_jvp2_gn_deferred)."""
+    _fields_ = [(k, _c_p) for k in ("x", "keep", "g_y", "stats", "weight", "bias", "mean_scale")] + \
+               [("eps", _c_f32), ("part", _c_p)]
+
+
+# VGAN_GN_JVP_FUSE=1: the tangent sweep's GraphNorm sums formed in the GAT
+# tangent pass (vg_gat_jvp2_gn_deferred) instead of their own pass.  Off:
+# measured slower (k_jvp_rows 94 -> 154 VGPRs; profiles/r02_rejected_gn_jvp_fuse.txt)
+_GN_JVP_FUSE = os.environ.get("VGAN_GN_JVP_FUSE", "0") == "1"
+
+
 class VgChainLayer(ctypes.Structure):
     """vg_chain_layer (include/vgan.h): one layer of vg_linear_chain."""
     _fields_ = [(k, _c_p) for k in ("weight", "bias", "aux", "out")] + \
@@ -175,6 +188,11 @@ SIGNATURES = {
     "vg_gat_lin_att_gn": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p,
                                          ctypes.POINTER(VgGnApply), _c_p]),
     "vg_graphnorm_stats_gnp": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p]),
+    "vg_gat_jvp2_blocks": (_c_i32, [_c_i32, _c_i32]),
+    "vg_gat_jvp2_gn_deferred": (ctypes.c_int, [_c_p] * 5 + [_c_i32] * 3 + [_c_p] * 8 + [_c_f32] + [_c_p] * 7 +
+                                [ctypes.POINTER(VgGnJvp), _c_p, _c_p, _c_p]),
+    "vg_graphnorm_jvp2_part": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p,
+                                              _c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_p]),
     "vg_linear_chain": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p]),
     "vg_gat_gnp_rows": (_c_i32, [_c_i32, _c_i32]),
     "vg_gat_gnp_floats": (_c_i64, [_c_i32, _c_i32]),
@@ -413,6 +431,17 @@ class FoldCollector:
                   "vg_gat_jvp2_plan")
             if src.shape >= 0:
                 self.jvp_src.append(src)
+        for i in range(n.value):
+            self.folds.append(VgFold.from_buffer_copy(arr[i]))
+        self.keep.extend(keep)
+
+    def jvp_gn(self, args_before_outputs, gn: "VgGnJvp", stream, keep=()):
+        """vg_gat_jvp2_gn_deferred: ``jvp`` (source pass run here) that also
+        writes the GraphNorm tangent sums of ``gn`` into gn.part."""
+        arr = (VgFold * 2)()
+        n = ctypes.c_int32(0)
+        check(LIB.vg_gat_jvp2_gn_deferred(*args_before_outputs, ctypes.byref(gn), arr, ctypes.byref(n), stream),
+              "vg_gat_jvp2_gn_deferred")
         for i in range(n.value):
             self.folds.append(VgFold.from_buffer_copy(arr[i]))
         self.keep.extend(keep)

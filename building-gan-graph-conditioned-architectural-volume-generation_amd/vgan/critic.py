@@ -41,7 +41,7 @@ import torch.nn as nn
 
 from . import data as vdata
 from . import ops
-from ._lib import (_GN_ROWS, LIB, FoldCollector, VgGnApply, VgGnBwdIn, check, dense, gemm_precision,
+from ._lib import (_GN_ROWS, LIB, FoldCollector, VgGnApply, VgGnBwdIn, VgGnJvp, check, dense, gemm_precision,
                    linear_chain, ptr, stream_handle, sync_counter)
 from . import _lib
 
@@ -404,19 +404,33 @@ class CriticEngine:
             uO, hinj = _f(n, c, dev=dev), _f(n, c, dev=dev)
             ws = _f(int(LIB.vg_gat_jvp2_ws_floats(n, E, c)), dev=dev)
             # the source pass (hinj, read in pass D) joins one grouped launch after the sweep
-            folds.jvp((ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot), ptr(csr.csc_dst), n, E,
-                       c, rows(B["H"], mrow, c), ptr(uH), ptr(dO_b[b]), ptr(conv.att_src), ptr(conv.att_dst),
-                       _off(B["a_s"], mrow), _off(B["a_d"], mrow), _off(B["alpha"], 2 * E),
-                       float(conv.negative_slope), ptr(uO), ptr(hinj), ptr(conv.att_src.grad),
-                       ptr(conv.att_dst.grad), ptr(up_s), ptr(up_d), ptr(ws)), st, keep=(ws, uH))
+            jargs = (ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot), ptr(csr.csc_dst), n, E,
+                     c, rows(B["H"], mrow, c), ptr(uH), ptr(dO_b[b]), ptr(conv.att_src), ptr(conv.att_dst),
+                     _off(B["a_s"], mrow), _off(B["a_d"], mrow), _off(B["alpha"], 2 * E),
+                     float(conv.negative_slope), ptr(uO), ptr(hinj), ptr(conv.att_src.grad),
+                     ptr(conv.att_dst.grad), ptr(up_s), ptr(up_d), ptr(ws))
+            gx, gkeep = rows(B["O"], mrow, c), rows(B["keep"], mrow, c) if B["keep"] is not None else None
+            gstats = _off(B["stats"], 2 * 2 * c)
             oinj = _f(n, c, dev=dev)
-            ws = _f(int(LIB.vg_graphnorm_seg_ws_floats(1, n, c)), dev=dev)
-            check(LIB.vg_graphnorm_jvp2(rows(B["O"], mrow, c), n, c, ptr(norm.weight), ptr(norm.bias),
-                                        ptr(norm.mean_scale),
-                                        rows(B["keep"], mrow, c) if B["keep"] is not None else None, float(norm.eps),
-                                        _off(B["stats"], 2 * 2 * c), ptr(uO), ptr(dY_b[b]), rows(B["Y"], trow, c),
-                                        ptr(oinj), ptr(norm.weight.grad), ptr(norm.mean_scale.grad), ptr(ws), sy, st),
-                  "vg_graphnorm_jvp2")
+            gws = _f(int(LIB.vg_graphnorm_seg_ws_floats(1, n, c)), dev=dev)
+            if _lib._GN_JVP_FUSE:  # the GraphNorm tangent sums from the GAT tangent pass
+                nblk = int(LIB.vg_gat_jvp2_blocks(n, c))
+                gpart = _f(nblk * 5 * c, dev=dev)
+                gn = VgGnJvp(x=gx.value, keep=gkeep.value if gkeep is not None else None, g_y=dY_b[b].data_ptr(),
+                             stats=gstats.value, weight=norm.weight.data_ptr(), bias=norm.bias.data_ptr(),
+                             mean_scale=norm.mean_scale.data_ptr(), eps=float(norm.eps), part=gpart.data_ptr())
+                folds.jvp_gn(jargs, gn, st, keep=(ws, uH, gpart))
+                check(LIB.vg_graphnorm_jvp2_part(gx, n, c, ptr(norm.weight), ptr(norm.bias), ptr(norm.mean_scale),
+                                                 gkeep, float(norm.eps), gstats, ptr(uO), ptr(dY_b[b]),
+                                                 rows(B["Y"], trow, c), ptr(oinj), ptr(norm.weight.grad),
+                                                 ptr(norm.mean_scale.grad), ptr(gpart), nblk, ptr(gws), st),
+                      "vg_graphnorm_jvp2_part")
+            else:
+                folds.jvp(jargs, st, keep=(ws, uH))
+                check(LIB.vg_graphnorm_jvp2(gx, n, c, ptr(norm.weight), ptr(norm.bias), ptr(norm.mean_scale), gkeep,
+                                            float(norm.eps), gstats, ptr(uO), ptr(dY_b[b]), rows(B["Y"], trow, c),
+                                            ptr(oinj), ptr(norm.weight.grad), ptr(norm.mean_scale.grad), ptr(gws), sy,
+                                            st), "vg_graphnorm_jvp2")
             hinj_b[b], oinj_b[b] = hinj, oinj
             u_in, uw = rows(B["Y"], trow, c), c
         # the tangent chain stays per-layer GEMMs (VGAN_CHAIN_TANGENT=1: the

@@ -582,6 +582,42 @@ int vg_gat_lin_att_gn(const float* X, const float* W, int32_t N, int32_t Cin, in
 int vg_graphnorm_stats_gnp(int32_t segments, int32_t rows, int32_t channels, const float* gnp, int32_t gnp_rows,
                            float* stats, void* stream);
 
+/* ---- the tangent sweep's GraphNorm sums in the GAT tangent pass ------------ */
+
+/* The GraphNorm (+ReLU+Dropout) whose input tangent the GAT tangent pass
+ * produces (critic engine pass C): x / keep / g_y [N, C] (keep may be NULL),
+ * stats [2C], parameters; part [vg_gat_jvp2_blocks(N, C)][5][C] receives the
+ * per-workgroup column sums that vg_graphnorm_jvp2's first pass formed by
+ * re-reading x, u, g_y and keep. */
+typedef struct vg_gn_jvp {
+  const float* x;
+  const float* keep;
+  const float* g_y;
+  const float* stats;
+  const float* weight;
+  const float* bias;
+  const float* mean_scale;
+  float eps;
+  float* part;
+} vg_gn_jvp;
+
+int32_t vg_gat_jvp2_blocks(int32_t num_nodes, int32_t channels);
+/* vg_gat_jvp2_deferred that also writes gn->part from the tangent rows it
+ * produces (u_out = the GraphNorm input tangent). */
+int vg_gat_jvp2_gn_deferred(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,
+                            const int32_t* csc_slot, const int32_t* csc_dst, int32_t num_nodes, int32_t num_edges,
+                            int32_t channels, const float* h, const float* u, const float* g_out,
+                            const float* att_src, const float* att_dst, const float* a_src, const float* a_dst,
+                            const float* alpha, float slope, float* u_out, float* h_inj, float* g_att_src,
+                            float* g_att_dst, const float* up_src_in, const float* up_dst_in, float* workspace,
+                            const vg_gn_jvp* gn, vg_fold* folds_out, int32_t* n_out, void* stream);
+/* vg_graphnorm_jvp2 (segments 1) from those partials: the fold and the
+ * elementwise pass only.  workspace as for vg_graphnorm_jvp2. */
+int vg_graphnorm_jvp2_part(const float* x, int32_t rows, int32_t channels, const float* weight, const float* bias,
+                           const float* mean_scale, const float* keep, float eps, const float* stats, const float* u,
+                           const float* g_y, float* u_out, float* x_inj, float* g_w, float* g_ms, const float* part,
+                           int32_t blocks, float* workspace, void* stream);
+
 /* ---- row-local chains of narrow linear layers ------------------------------ */
 
 /* One layer of vg_linear_chain: y = x W^T (w_trans 0, weight [out][in], an

@@ -298,3 +298,37 @@ def test_critic_engine_gn_apply_in_gemm(cuda, training, monkeypatch):
     assert out[True][2] == sum(1 for c in widths[1:] if c <= 64) and out[False][2] == 0
     assert abs(out[True][0] - out[False][0]) <= 1e-6 * max(1.0, abs(out[False][0]))
     assert rel_err(out[True][1], out[False][1]) < 1e-5
+
+
+@pytest.mark.parametrize("training", [True, False])
+def test_critic_tangent_graphnorm_sums_from_gat_pass(cuda, training, monkeypatch):
+    """Pass C with each GraphNorm's tangent sums (sum u, sum xt u, sum p,
+    sum p u, sum p xt) formed in the GAT tangent pass that produces u
+    (vg_gat_jvp2_gn_deferred + vg_graphnorm_jvp2_part) against the separate
+    sums pass (vg_graphnorm_jvp2): pass C feeds only the gradient, so the loss
+    is identical and the D gradient agrees to f32 rounding (sums in another
+    order); the fused path runs for every block."""
+    from vgan import _lib
+
+    cfg, D, flat, loc, vox, prep, hard, soft, eng = _engine_setup(cuda, numbers=(5, 6, 7), seed=41)
+    D.train(training)
+    hd, sd = hard.to(cuda).unsqueeze(0), soft.to(cuda).unsqueeze(0)
+    calls = []
+    orig = LIB.vg_gat_jvp2_gn_deferred
+
+    def counted(*a):
+        calls.append(1)
+        return orig(*a)
+
+    monkeypatch.setattr(LIB, "vg_gat_jvp2_gn_deferred", counted)
+    out = {}
+    for fuse in (True, False):
+        monkeypatch.setattr(_lib, "_GN_JVP_FUSE", fuse)
+        calls.clear()
+        flat.zero_grad()
+        loss = eng.loss_and_grad(loc, vox, hd, sd, _RecRNG(12))
+        torch.cuda.synchronize()
+        out[fuse] = (loss.item(), flat.grad.clone(), len(calls))
+    assert out[True][2] == len(eng.blocks) and out[False][2] == 0
+    assert out[True][0] == out[False][0]
+    assert rel_err(out[True][1], out[False][1]) < 1e-5
