@@ -95,11 +95,23 @@ __device__ __forceinline__ void chain_layer_p(const float* xs, float* ys, const 
   (void)y;
 }
 
+// Staging loads all issue before the first LDS store (a compile-time count per
+// thread, in registers): a load -> wait -> store loop runs its loads one after
+// another.
 template <int IN, int OUT>
 __device__ __forceinline__ void stage_layer(float* Ws, const ChainLayer& L) {
-  for (int e = threadIdx.x; e < IN * OUT; e += blockDim.x) {
+  constexpr int NE = (IN * OUT + 255) / 256;
+  float r[NE];
+#pragma unroll
+  for (int u = 0; u < NE; ++u) {
+    const int e = threadIdx.x + 256 * u;
     const int j = e / IN, k = e - j * IN;
-    Ws[e] = L.wt ? L.w[(size_t)k * OUT + j] : L.w[(size_t)j * IN + k];
+    r[u] = e < IN * OUT ? (L.wt ? L.w[(size_t)k * OUT + j] : L.w[(size_t)j * IN + k]) : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < NE; ++u) {
+    const int e = threadIdx.x + 256 * u;
+    if (e < IN * OUT) Ws[e] = r[u];
   }
 }
 
@@ -118,11 +130,23 @@ __global__ void __launch_bounds__(256) k_chain(const ChainDesc d) {
   if constexpr (W3 > 0) stage_layer<W2, W3>(Ws + S0 + S1, d.l[2]);
   if constexpr (W4 > 0) stage_layer<W3, W4>(Ws + S0 + S1 + S2, d.l[3]);
   const int row0 = blockIdx.x * kRowsPerBlock;
-  // the block's input rows, coalesced, into the image
-  for (int e = threadIdx.x; e < kRowsPerBlock * W0; e += blockDim.x) {
-    const int r = e / W0, k = e - r * W0;
-    const int row = min(row0 + r, d.rows - 1);
-    img[0][r * img_pitch(W0) + k] = d.x[(size_t)row * d.ldx + k];
+  // the block's input rows, coalesced, into the image (loads first, as above)
+  {
+    constexpr int NX = (kRowsPerBlock * W0 + 255) / 256;
+    float r[NX];
+#pragma unroll
+    for (int u = 0; u < NX; ++u) {
+      const int e = threadIdx.x + 256 * u;
+      const int rr = e / W0, k = e - rr * W0;
+      const int row = min(row0 + rr, d.rows - 1);
+      r[u] = e < kRowsPerBlock * W0 ? d.x[(size_t)row * d.ldx + k] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < NX; ++u) {
+      const int e = threadIdx.x + 256 * u;
+      const int rr = e / W0, k = e - rr * W0;
+      if (e < kRowsPerBlock * W0) img[0][rr * img_pitch(W0) + k] = r[u];
+    }
   }
   __syncthreads();
   const int p = threadIdx.x % kP;

@@ -46,7 +46,7 @@ from ._lib import (_GN_ROWS, LIB, FoldCollector, VgGnApply, VgGnBwdIn, VgGnJvp, 
 from . import _lib
 
 ACT_NONE, ACT_RELU, ACT_MASK = 0, 1, 3
-_CHAIN_TANGENT = os.environ.get("VGAN_CHAIN_TANGENT", "0") == "1"
+_CHAIN_TANGENT = os.environ.get("VGAN_CHAIN_TANGENT", "1") == "1"
 # VGAN_GN_FUSE=0: the GraphNorm backward's column partials in their own pass
 # instead of the epilogue of the GEMM producing its g_y (A/B knob)
 _GN_FUSE = os.environ.get("VGAN_GN_FUSE", "1") == "1"
@@ -433,9 +433,9 @@ class CriticEngine:
                                             st), "vg_graphnorm_jvp2")
             hinj_b[b], oinj_b[b] = hinj, oinj
             u_in, uw = rows(B["Y"], trow, c), c
-        # the tangent chain stays per-layer GEMMs (VGAN_CHAIN_TANGENT=1: the
-        # chain): 16.0 vs 16.6 us at 12.7k rows and the step flat
-        # (profiles/r02_chain_probe_p4.json, profiles/r02_ab_chain.txt)
+        # the tangent chain (VGAN_CHAIN_TANGENT=0: per-layer GEMMs): 14.3 vs
+        # 16.7 us at 12.7k rows (profiles/r02_chain_probe_v3.json,
+        # profiles/r02_ab_chain.txt)
         tan_w = [uw] + [lin.out_features for lin in self.dec[:-1]]
         if not _CHAIN_TANGENT or not linear_chain(u_in, uw, n, tan_w,
                             [dict(weight=lin.weight.data_ptr(), act=ACT_MASK,

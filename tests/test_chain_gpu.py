@@ -88,6 +88,6 @@ def test_critic_engine_with_decoder_chains(cuda, training, monkeypatch):
         loss = eng.loss_and_grad(loc, vox, hd, sd, _RecRNG(6))
         torch.cuda.synchronize()
         out[chain] = (loss.item(), flat.grad.clone(), len(calls))
-    assert out[True][2] == 3 and out[False][2] == 0  # passes A, B, D (pass C: per-layer GEMMs, faster)
+    assert out[True][2] == 4 and out[False][2] == 0  # passes A, B, C, D
     assert abs(out[True][0] - out[False][0]) <= 1e-5 * max(1.0, abs(out[False][0]))
     assert rel_err(out[True][1], out[False][1]) < 1e-4
