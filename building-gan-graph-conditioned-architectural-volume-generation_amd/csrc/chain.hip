@@ -27,7 +27,10 @@ struct ChainDesc {
   ChainLayer l[kChainMax];
   const float* x;
   int ldx, rows;
+  int bf16;  // products on bf16-rounded operands (the *_bf16 GEMMs' arithmetic: exact products, f32 sums)
 };
+
+__device__ __forceinline__ float bf16_round(float v) { return static_cast<float>(static_cast<__bf16>(v)); }
 
 // P lanes per row (consecutive threads of one wave): lane p computes outputs
 // j = p, p + P, ... of every layer from the whole input row, read from the
@@ -45,7 +48,7 @@ constexpr int img_pitch(int w) { return w % 4 == 0 ? w + 4 : w + 1; }
 
 template <int IN, int OUT>
 __device__ __forceinline__ void chain_layer_p(const float* xs, float* ys, const float* Ws, const ChainLayer& L,
-                                              int row, bool live, int p) {
+                                              int row, bool live, int p, bool bf16) {
   constexpr int PITCH_IN = img_pitch(IN), PITCH_OUT = img_pitch(OUT);
   constexpr int J = (OUT + kP - 1) / kP;  // outputs per lane
   const int rl = threadIdx.x / kP;
@@ -64,6 +67,9 @@ __device__ __forceinline__ void chain_layer_p(const float* xs, float* ys, const 
 #pragma unroll
     for (int k = 0; k < IN; ++k) x[k] = xs[rl * PITCH_IN + k];
   }
+  if (bf16)
+#pragma unroll
+    for (int k = 0; k < IN; ++k) x[k] = bf16_round(x[k]);
   float y[J];
 #pragma unroll
   for (int jj = 0; jj < J; ++jj) {
@@ -99,7 +105,7 @@ __device__ __forceinline__ void chain_layer_p(const float* xs, float* ys, const 
 // thread, in registers): a load -> wait -> store loop runs its loads one after
 // another.
 template <int IN, int OUT>
-__device__ __forceinline__ void stage_layer(float* Ws, const ChainLayer& L) {
+__device__ __forceinline__ void stage_layer(float* Ws, const ChainLayer& L, bool bf16) {
   constexpr int NE = (IN * OUT + 255) / 256;
   float r[NE];
 #pragma unroll
@@ -111,7 +117,7 @@ __device__ __forceinline__ void stage_layer(float* Ws, const ChainLayer& L) {
 #pragma unroll
   for (int u = 0; u < NE; ++u) {
     const int e = threadIdx.x + 256 * u;
-    if (e < IN * OUT) Ws[e] = r[u];
+    if (e < IN * OUT) Ws[e] = bf16 ? bf16_round(r[u]) : r[u];
   }
 }
 
@@ -125,10 +131,11 @@ __global__ void __launch_bounds__(256) k_chain(const ChainDesc d) {
   constexpr int WMAX = cmaxw(cmaxw(W0, W1), cmaxw(cmaxw(W2, W3), W4));
   __shared__ __attribute__((aligned(16))) float Ws[cmax1(S0 + S1 + S2 + S3)];
   __shared__ __attribute__((aligned(16))) float img[2][kRowsPerBlock * (WMAX + 4)];  // row images: in / out
-  stage_layer<W0, W1>(Ws, d.l[0]);
-  if constexpr (W2 > 0) stage_layer<W1, W2>(Ws + S0, d.l[1]);
-  if constexpr (W3 > 0) stage_layer<W2, W3>(Ws + S0 + S1, d.l[2]);
-  if constexpr (W4 > 0) stage_layer<W3, W4>(Ws + S0 + S1 + S2, d.l[3]);
+  const bool bf = d.bf16 != 0;
+  stage_layer<W0, W1>(Ws, d.l[0], bf);
+  if constexpr (W2 > 0) stage_layer<W1, W2>(Ws + S0, d.l[1], bf);
+  if constexpr (W3 > 0) stage_layer<W2, W3>(Ws + S0 + S1, d.l[2], bf);
+  if constexpr (W4 > 0) stage_layer<W3, W4>(Ws + S0 + S1 + S2, d.l[3], bf);
   const int row0 = blockIdx.x * kRowsPerBlock;
   // the block's input rows, coalesced, into the image (loads first, as above)
   {
@@ -153,16 +160,16 @@ __global__ void __launch_bounds__(256) k_chain(const ChainDesc d) {
   const int rowr = row0 + threadIdx.x / kP;
   const bool live = rowr < d.rows;
   const int row = live ? rowr : d.rows - 1;
-  chain_layer_p<W0, W1>(img[0], img[1], Ws, d.l[0], row, live, p);
+  chain_layer_p<W0, W1>(img[0], img[1], Ws, d.l[0], row, live, p, bf);
   if constexpr (W2 > 0) {
     __syncthreads();
-    chain_layer_p<W1, W2>(img[1], img[0], Ws + S0, d.l[1], row, live, p);
+    chain_layer_p<W1, W2>(img[1], img[0], Ws + S0, d.l[1], row, live, p, bf);
     if constexpr (W3 > 0) {
       __syncthreads();
-      chain_layer_p<W2, W3>(img[0], img[1], Ws + S0 + S1, d.l[2], row, live, p);
+      chain_layer_p<W2, W3>(img[0], img[1], Ws + S0 + S1, d.l[2], row, live, p, bf);
       if constexpr (W4 > 0) {
         __syncthreads();
-        chain_layer_p<W3, W4>(img[1], img[0], Ws + S0 + S1 + S2, d.l[3], row, live, p);
+        chain_layer_p<W3, W4>(img[1], img[0], Ws + S0 + S1 + S2, d.l[3], row, live, p, bf);
       }
     }
   }
@@ -172,10 +179,11 @@ __global__ void __launch_bounds__(256) k_chain(const ChainDesc d) {
 
 // The width chains instantiated: the critic's decoder at DISCRIMINATOR_HIDDEN_DIM
 // 64 (forward, tangent, adjoint); other widths return VG_EINVAL (per-layer GEMMs).
-extern "C" int vg_linear_chain(const float* x, int32_t ldx, int32_t rows, const int32_t* widths, int32_t nlayers,
-                               const vg_chain_layer* layers, void* stream) {
+static int linear_chain(const float* x, int32_t ldx, int32_t rows, const int32_t* widths, int32_t nlayers,
+                        const vg_chain_layer* layers, void* stream, int bf16) {
   if (rows <= 0 || !x || !widths || !layers || nlayers < 2 || nlayers > kChainMax) return VG_EINVAL;
   ChainDesc d{};
+  d.bf16 = bf16;
   d.x = x;
   d.ldx = ldx;
   d.rows = rows;
@@ -206,4 +214,14 @@ extern "C" int vg_linear_chain(const float* x, int32_t ldx, int32_t rows, const 
     return VG_EINVAL;
   VG_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int vg_linear_chain(const float* x, int32_t ldx, int32_t rows, const int32_t* widths, int32_t nlayers,
+                               const vg_chain_layer* layers, void* stream) {
+  return linear_chain(x, ldx, rows, widths, nlayers, layers, stream, 0);
+}
+
+extern "C" int vg_linear_chain_bf16(const float* x, int32_t ldx, int32_t rows, const int32_t* widths,
+                                    int32_t nlayers, const vg_chain_layer* layers, void* stream) {
+  return linear_chain(x, ldx, rows, widths, nlayers, layers, stream, 1);
 }

@@ -115,7 +115,7 @@ def linear_chain(x, ldx: int, rows: int, widths, layers, stream) -> bool:
     """vg_linear_chain over ``layers`` (dicts of VgChainLayer fields; device
     pointers as ints / c_void_p); False when the width chain has no kernel
     (the caller runs its per-layer GEMMs)."""
-    if not _CHAIN or _precision != "f32":
+    if not _CHAIN:
         return False
     n = len(layers)
     arr = (VgChainLayer * n)()
@@ -123,7 +123,8 @@ def linear_chain(x, ldx: int, rows: int, widths, layers, stream) -> bool:
         for k, v in l.items():
             setattr(arr[i], k, v.value if isinstance(v, ctypes.c_void_p) else v)
     w = (ctypes.c_int32 * (n + 1))(*widths)
-    return LIB.vg_linear_chain(x, ldx, rows, w, n, arr, stream) == 0
+    fn = LIB.vg_linear_chain_bf16 if _precision == "bf16" else LIB.vg_linear_chain
+    return fn(x, ldx, rows, w, n, arr, stream) == 0
 
 
 class VgASrc(ctypes.Structure):
@@ -194,6 +195,7 @@ SIGNATURES = {
     "vg_graphnorm_jvp2_part": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p,
                                               _c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_p]),
     "vg_linear_chain": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p]),
+    "vg_linear_chain_bf16": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p]),
     "vg_gat_gnp_rows": (_c_i32, [_c_i32, _c_i32]),
     "vg_gat_gnp_floats": (_c_i64, [_c_i32, _c_i32]),
     "vg_gat_aggregate_fwd_gnp": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p,

@@ -644,6 +644,11 @@ typedef struct vg_chain_layer {
  * ldx floats apart.  Other width chains return VG_EINVAL (use vg_gemm). */
 int vg_linear_chain(const float* x, int32_t ldx, int32_t rows, const int32_t* widths, int32_t nlayers,
                     const vg_chain_layer* layers, void* stream);
+/* The same with every product on bf16-rounded operands (inputs and weights
+ * rounded to nearest-even, exact products, f32 sums): the arithmetic of the
+ * *_bf16 GEMMs it replaces in bf16 mode (configs[2]). */
+int vg_linear_chain_bf16(const float* x, int32_t ldx, int32_t rows, const int32_t* widths, int32_t nlayers,
+                         const vg_chain_layer* layers, void* stream);
 
 /* ---- multi-source LayerNorm GEMM (no-grad stacked generator forward) ------- */
 
