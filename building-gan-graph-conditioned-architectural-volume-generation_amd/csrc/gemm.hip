@@ -132,11 +132,11 @@ struct GnaDesc {
 
 constexpr int kGnaMaxK = 128;  // GraphNorm channels the operand transform stages in LDS
 
-// gp = the block's staged column operands [w | b | ms | mu0 | sd0 + eps | mu1 | sd1 + eps]
-// (segment slots 0 / 1: the tile's first row's segment and the next)
-// four consecutive columns k .. k+3 of row n (k % 4 == 0, K % 4 == 0): one
+// Four consecutive columns k .. k+3 of row n (k % 4 == 0, K % 4 == 0): one
 // Philox block draws all four multipliers (vg_keep4_raw: the values vg_keep
-// gives each element), float4 stores of y / keep
+// gives each element), float4 stores of y / keep.  gp = the block's staged
+// column operands [w | b | ms | mu0 | sd0 + eps | mu1 | sd1 + eps] (segment
+// slots 0 / 1: the tile's first row's segment and the next).
 __device__ __forceinline__ float4 gna_quad(const GnaDesc& ga, const float* gp, float4 x, int n, int k, int K,
                                            int bound, long long it) {
   const int sl = n >= bound ? 5 * K : 3 * K;
