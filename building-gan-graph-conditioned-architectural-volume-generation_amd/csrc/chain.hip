@@ -70,7 +70,6 @@ __device__ __forceinline__ void chain_layer_p(const float* xs, float* ys, const 
   if (bf16)
 #pragma unroll
     for (int k = 0; k < IN; ++k) x[k] = bf16_round(x[k]);
-  float y[J];
 #pragma unroll
   for (int jj = 0; jj < J; ++jj) {
     const int j = p + kP * jj;
@@ -96,9 +95,7 @@ __device__ __forceinline__ void chain_layer_p(const float* xs, float* ys, const 
       if (L.out && live) L.out[(size_t)row * L.ld_out + j] = acc;
       ys[rl * PITCH_OUT + j] = acc;
     }
-    y[jj] = acc;
   }
-  (void)y;
 }
 
 // Staging loads all issue before the first LDS store (a compile-time count per
