@@ -402,7 +402,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // (lane l: row l & 15, k = 8 (l >> 4) + j).
 // GNA: GraphNorm + ReLU + Dropout applied to A as it loads (GnaDesc; one
 // column tile: every A element is loaded, transformed and stored once).
-template <bool BT, int ACT, bool ATT = false, bool BF = false, bool GNP = false, bool GNA = false>
+// QA: A loaded as float4 quads by threads 0..511 (one quad of a tile row per
+// K-tile; K % 4 == 0, lda % 4 == 0, A 16-B aligned) instead of 2 scalars by
+// every thread; GNA always loads quads.
+template <bool BT, int ACT, bool ATT = false, bool BF = false, bool GNP = false, bool GNA = false, bool QA = false>
 __device__ __forceinline__ void gemm16_body(const float* __restrict__ A, int lda,
                                                  const float* __restrict__ B, int ldb,
                                                  const float* __restrict__ bias,
@@ -475,8 +478,9 @@ __device__ __forceinline__ void gemm16_body(const float* __restrict__ A, int lda
   // GNA: A as float4 quads, threads 0..511 (one row quad each per K-tile)
   float4 rq = make_float4(0.f, 0.f, 0.f, 0.f);
   constexpr int QPR = TK / 4;  // quads per tile row
+  constexpr bool QUAD = GNA || QA;
   auto load = [&](int k0) {
-    if constexpr (GNA) {
+    if constexpr (QUAD) {
       if (t < TM * QPR) {
         const int n = n0 + t / QPR, k = k0 + 4 * (t % QPR);
         rq = (n < N && k < K) ? *reinterpret_cast<const float4*>(A + (size_t)n * lda + k)
@@ -488,7 +492,7 @@ __device__ __forceinline__ void gemm16_body(const float* __restrict__ A, int lda
       const int e = t + 1024 * q;
       const int row = e / TK, kc = e % TK;
       const int n = n0 + row, k = k0 + kc;
-      if constexpr (!GNA) ra[q] = (n < N && k < K) ? A[(size_t)n * lda + k] : 0.f;
+      if constexpr (!QUAD) ra[q] = (n < N && k < K) ? A[(size_t)n * lda + k] : 0.f;
       if (BT) {
         const int m = m0 + row;
         rb[q] = (m < M && k < K) ? B[(size_t)m * ldb + k] : 0.f;
@@ -503,11 +507,12 @@ __device__ __forceinline__ void gemm16_body(const float* __restrict__ A, int lda
   if constexpr (GNA) __syncthreads();  // the staged column operands
   int buf = 0;
   for (int k0 = 0; k0 < K; k0 += TK) {
-    if constexpr (GNA) {  // the loaded x quad of this K-tile -> y (stored once: one column tile)
+    if constexpr (QUAD) {  // GNA: the loaded x quad of this K-tile -> y (stored once: one column tile)
       if (t < TM * QPR) {
         const int row = t / QPR, kq = 4 * (t % QPR);
         const int n = n0 + row, k = k0 + kq;
-        if (n < N && k < K) rq = gna_quad(ga, gpar, rq, n, k, K, gbnd, g_it);
+        if constexpr (GNA)
+          if (n < N && k < K) rq = gna_quad(ga, gpar, rq, n, k, K, gbnd, g_it);
         As[buf][row][kq] = rq.x;
         As[buf][row][kq + 1] = rq.y;
         As[buf][row][kq + 2] = rq.z;
@@ -517,7 +522,7 @@ __device__ __forceinline__ void gemm16_body(const float* __restrict__ A, int lda
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
       const int e = t + 1024 * q;
-      if constexpr (!GNA) As[buf][e / TK][e % TK] = ra[q];
+      if constexpr (!QUAD) As[buf][e / TK][e % TK] = ra[q];
       if (BT) Bs[buf][e / TK][e % TK] = rb[q];
       else Bs[buf][e % TN][e / TN] = rb[q];
     }
@@ -639,7 +644,7 @@ __device__ __forceinline__ void gemm16_body(const float* __restrict__ A, int lda
   }
 }
 
-template <bool BT, int ACT, bool ATT = false, bool BF = false, bool GNP = false>
+template <bool BT, int ACT, bool ATT = false, bool BF = false, bool GNP = false, bool QA = false>
 __global__ void __launch_bounds__(1024) k_gemm16(const float* __restrict__ A, int lda, const float* __restrict__ B,
                                                  int ldb, const float* __restrict__ bias,
                                                  const float* __restrict__ aux, int ldaux, float* __restrict__ C,
@@ -648,8 +653,8 @@ __global__ void __launch_bounds__(1024) k_gemm16(const float* __restrict__ A, in
                                                  const float* __restrict__ att_d = nullptr,
                                                  float* __restrict__ a_src = nullptr,
                                                  float* __restrict__ a_dst = nullptr, const GnpDesc gn = GnpDesc{}) {
-  gemm16_body<BT, ACT, ATT, BF, GNP, false>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, N, M, K, att_s, att_d, a_src,
-                                            a_dst, gn);
+  gemm16_body<BT, ACT, ATT, BF, GNP, false, QA>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, N, M, K, att_s, att_d,
+                                                a_src, a_dst, gn);
 }
 
 // the projection GEMM with the GraphNorm applied to its operand (vg_gat_lin_att_gn):
@@ -1519,6 +1524,13 @@ __global__ void __launch_bounds__(1024) k_fold_rows(const float* __restrict__ pa
 
 }  // namespace
 
+#ifndef VG_QUAD_A
+#define VG_QUAD_A 1  // A/B knob: float4 A loads in k_gemm16 where the operand allows
+#endif
+static inline bool quad_a(const float* A, int lda, int K) {
+  return VG_QUAD_A && K % 4 == 0 && lda % 4 == 0 && (reinterpret_cast<uintptr_t>(A) & 15) == 0;
+}
+
 template <bool BF>
 static int gemm(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t b_trans, const float* bias,
                 int32_t act, const float* aux, int32_t ldaux, float* C, int32_t ldc, int32_t N, int32_t M,
@@ -1539,7 +1551,11 @@ static int gemm(const float* A, int32_t lda, const float* B, int32_t ldb, int32_
 #define VG_G(BT, ACT)                                                                                      \
   do {                                                                                                     \
     if ((VG_GEMM16 & (BF ? 8 : 1)) != 0)                                                                   \
-      k_gemm16<BT, ACT, false, BF><<<grid, 1024, 0, s>>>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, N, M, K); \
+      if (quad_a(A, lda, K))                                                                               \
+        k_gemm16<BT, ACT, false, BF, false, true><<<grid, 1024, 0, s>>>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, \
+                                                                       N, M, K);                             \
+      else                                                                                                 \
+        k_gemm16<BT, ACT, false, BF><<<grid, 1024, 0, s>>>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, N, M, K); \
     else                                                                                                   \
       k_gemm<BT, ACT, false, BF><<<grid, 256, 0, s>>>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, N, M, K); \
   } while (0)
@@ -1567,8 +1583,12 @@ static int gemm_gn_bwd(const float* A, int32_t lda, const float* B, int32_t ldb,
   dim3 grid((N + TM - 1) / TM, (M + TN - 1) / TN);
   const GnpDesc gn{gn_x, keep, stats, weight, bias, mean_scale, eps, seg_rows, tpart};
   if ((VG_GEMM16 & 4) && (!BF || (VG_GEMM16 & 8)))
-    k_gemm16<false, 0, false, BF, true><<<grid, 1024, 0, s>>>(A, lda, B, ldb, nullptr, nullptr, 0, C, ldc, N, M, K,
-                                                             nullptr, nullptr, nullptr, nullptr, gn);
+    if (quad_a(A, lda, K))
+      k_gemm16<false, 0, false, BF, true, true><<<grid, 1024, 0, s>>>(A, lda, B, ldb, nullptr, nullptr, 0, C, ldc, N, M,
+                                                                     K, nullptr, nullptr, nullptr, nullptr, gn);
+    else
+      k_gemm16<false, 0, false, BF, true><<<grid, 1024, 0, s>>>(A, lda, B, ldb, nullptr, nullptr, 0, C, ldc, N, M, K,
+                                                               nullptr, nullptr, nullptr, nullptr, gn);
   else
     k_gemm<false, 0, false, BF, true><<<grid, 256, 0, s>>>(A, lda, B, ldb, nullptr, nullptr, 0, C, ldc, N, M, K,
                                                            nullptr, nullptr, nullptr, nullptr, gn);
@@ -1900,8 +1920,12 @@ static int gat_lin_att(const float* X, int32_t ldx, const float* W, int32_t N,
     return 0;
   }
   if ((VG_GEMM16 & 2) && (!BF || (VG_GEMM16 & 8)))
-    k_gemm16<true, 0, true, BF><<<dim3((N + TM - 1) / TM, 1), 1024, 0, s>>>(
-        X, ldx, W, Cin, nullptr, nullptr, 0, H, C, N, C, Cin, att_src, att_dst, a_src, a_dst);
+    if (quad_a(X, ldx, Cin))
+      k_gemm16<true, 0, true, BF, false, true><<<dim3((N + TM - 1) / TM, 1), 1024, 0, s>>>(
+          X, ldx, W, Cin, nullptr, nullptr, 0, H, C, N, C, Cin, att_src, att_dst, a_src, a_dst);
+    else
+      k_gemm16<true, 0, true, BF><<<dim3((N + TM - 1) / TM, 1), 1024, 0, s>>>(
+          X, ldx, W, Cin, nullptr, nullptr, 0, H, C, N, C, Cin, att_src, att_dst, a_src, a_dst);
   else
     k_gemm<true, 0, true, BF><<<dim3((N + TM - 1) / TM, 1), 256, 0, s>>>(
         X, ldx, W, Cin, nullptr, nullptr, 0, H, C, N, C, Cin, att_src, att_dst, a_src, a_dst);
