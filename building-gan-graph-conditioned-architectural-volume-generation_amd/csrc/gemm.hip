@@ -402,9 +402,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // (lane l: row l & 15, k = 8 (l >> 4) + j).
 // GNA: GraphNorm + ReLU + Dropout applied to A as it loads (GnaDesc; one
 // column tile: every A element is loaded, transformed and stored once).
-// QA: A loaded as float4 quads by threads 0..511 (one quad of a tile row per
-// K-tile; K % 4 == 0, lda % 4 == 0, A 16-B aligned) instead of 2 scalars by
-// every thread; GNA always loads quads.
+// QA: A and B loaded as float4 quads by threads 0..511 (one quad per K-tile;
+// K % 4 == 0, leading dimensions % 4 == 0, 16-B aligned operands, quad_ab)
+// instead of 2 scalars each by every thread; GNA loads A as quads.
 template <bool BT, int ACT, bool ATT = false, bool BF = false, bool GNP = false, bool GNA = false, bool QA = false>
 __device__ __forceinline__ void gemm16_body(const float* __restrict__ A, int lda,
                                                  const float* __restrict__ B, int ldb,
@@ -479,6 +479,7 @@ __device__ __forceinline__ void gemm16_body(const float* __restrict__ A, int lda
   float4 rq = make_float4(0.f, 0.f, 0.f, 0.f);
   constexpr int QPR = TK / 4;  // quads per tile row
   constexpr bool QUAD = GNA || QA;
+  float4 rbq = make_float4(0.f, 0.f, 0.f, 0.f);  // QA: B as quads too (along k for BT, along m otherwise)
   auto load = [&](int k0) {
     if constexpr (QUAD) {
       if (t < TM * QPR) {
@@ -487,19 +488,34 @@ __device__ __forceinline__ void gemm16_body(const float* __restrict__ A, int lda
                               : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
+    if constexpr (QA) {
+      if (t < TN * QPR) {
+        if (BT) {
+          const int m = m0 + t / QPR, k = k0 + 4 * (t % QPR);
+          rbq = (m < M && k < K) ? *reinterpret_cast<const float4*>(B + (size_t)m * ldb + k)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+          const int kk = k0 + t / (TN / 4), m = m0 + 4 * (t % (TN / 4));
+          rbq = (m < M && kk < K) ? *reinterpret_cast<const float4*>(B + (size_t)kk * ldb + m)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+    }
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
       const int e = t + 1024 * q;
       const int row = e / TK, kc = e % TK;
       const int n = n0 + row, k = k0 + kc;
       if constexpr (!QUAD) ra[q] = (n < N && k < K) ? A[(size_t)n * lda + k] : 0.f;
-      if (BT) {
-        const int m = m0 + row;
-        rb[q] = (m < M && k < K) ? B[(size_t)m * ldb + k] : 0.f;
-      } else {
-        const int kr = e / TN, j = e % TN;
-        const int m = m0 + j, kk = k0 + kr;
-        rb[q] = (m < M && kk < K) ? B[(size_t)kk * ldb + m] : 0.f;
+      if constexpr (!QA) {
+        if (BT) {
+          const int m = m0 + row;
+          rb[q] = (m < M && k < K) ? B[(size_t)m * ldb + k] : 0.f;
+        } else {
+          const int kr = e / TN, j = e % TN;
+          const int m = m0 + j, kk = k0 + kr;
+          rb[q] = (m < M && kk < K) ? B[(size_t)kk * ldb + m] : 0.f;
+        }
       }
     }
   };
@@ -519,12 +535,31 @@ __device__ __forceinline__ void gemm16_body(const float* __restrict__ A, int lda
         As[buf][row][kq + 3] = rq.w;
       }
     }
+    if constexpr (QA) {
+      if (t < TN * QPR) {
+        if (BT) {
+          const int row = t / QPR, kq = 4 * (t % QPR);
+          Bs[buf][row][kq] = rbq.x;
+          Bs[buf][row][kq + 1] = rbq.y;
+          Bs[buf][row][kq + 2] = rbq.z;
+          Bs[buf][row][kq + 3] = rbq.w;
+        } else {
+          const int kr = t / (TN / 4), j4 = 4 * (t % (TN / 4));
+          Bs[buf][j4][kr] = rbq.x;
+          Bs[buf][j4 + 1][kr] = rbq.y;
+          Bs[buf][j4 + 2][kr] = rbq.z;
+          Bs[buf][j4 + 3][kr] = rbq.w;
+        }
+      }
+    }
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
       const int e = t + 1024 * q;
       if constexpr (!QUAD) As[buf][e / TK][e % TK] = ra[q];
-      if (BT) Bs[buf][e / TK][e % TK] = rb[q];
-      else Bs[buf][e % TN][e / TN] = rb[q];
+      if constexpr (!QA) {
+        if (BT) Bs[buf][e / TK][e % TK] = rb[q];
+        else Bs[buf][e % TN][e / TN] = rb[q];
+      }
     }
     __syncthreads();
     if (k0 + TK < K) load(k0 + TK);
@@ -1527,8 +1562,10 @@ __global__ void __launch_bounds__(1024) k_fold_rows(const float* __restrict__ pa
 #ifndef VG_QUAD_A
 #define VG_QUAD_A 1  // A/B knob: float4 A loads in k_gemm16 where the operand allows
 #endif
-static inline bool quad_a(const float* A, int lda, int K) {
-  return VG_QUAD_A && K % 4 == 0 && lda % 4 == 0 && (reinterpret_cast<uintptr_t>(A) & 15) == 0;
+// both operands as float4 quads: A along k; B along k (bt) or along m
+static inline bool quad_ab(const float* A, int lda, const float* B, int ldb, int K, int M, bool bt) {
+  return VG_QUAD_A && K % 4 == 0 && lda % 4 == 0 && (reinterpret_cast<uintptr_t>(A) & 15) == 0 &&
+         ldb % 4 == 0 && (reinterpret_cast<uintptr_t>(B) & 15) == 0 && (bt || M % 4 == 0);
 }
 
 template <bool BF>
@@ -1551,7 +1588,7 @@ static int gemm(const float* A, int32_t lda, const float* B, int32_t ldb, int32_
 #define VG_G(BT, ACT)                                                                                      \
   do {                                                                                                     \
     if ((VG_GEMM16 & (BF ? 8 : 1)) != 0)                                                                   \
-      if (quad_a(A, lda, K))                                                                               \
+      if (quad_ab(A, lda, B, ldb, K, M, BT))                                                               \
         k_gemm16<BT, ACT, false, BF, false, true><<<grid, 1024, 0, s>>>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, \
                                                                        N, M, K);                             \
       else                                                                                                 \
@@ -1583,7 +1620,7 @@ static int gemm_gn_bwd(const float* A, int32_t lda, const float* B, int32_t ldb,
   dim3 grid((N + TM - 1) / TM, (M + TN - 1) / TN);
   const GnpDesc gn{gn_x, keep, stats, weight, bias, mean_scale, eps, seg_rows, tpart};
   if ((VG_GEMM16 & 4) && (!BF || (VG_GEMM16 & 8)))
-    if (quad_a(A, lda, K))
+    if (quad_ab(A, lda, B, ldb, K, M, false))
       k_gemm16<false, 0, false, BF, true, true><<<grid, 1024, 0, s>>>(A, lda, B, ldb, nullptr, nullptr, 0, C, ldc, N, M,
                                                                      K, nullptr, nullptr, nullptr, nullptr, gn);
     else
@@ -1920,7 +1957,7 @@ static int gat_lin_att(const float* X, int32_t ldx, const float* W, int32_t N,
     return 0;
   }
   if ((VG_GEMM16 & 2) && (!BF || (VG_GEMM16 & 8)))
-    if (quad_a(X, ldx, Cin))
+    if (quad_ab(X, ldx, W, Cin, Cin, C, true))
       k_gemm16<true, 0, true, BF, false, true><<<dim3((N + TM - 1) / TM, 1), 1024, 0, s>>>(
           X, ldx, W, Cin, nullptr, nullptr, 0, H, C, N, C, Cin, att_src, att_dst, a_src, a_dst);
     else
