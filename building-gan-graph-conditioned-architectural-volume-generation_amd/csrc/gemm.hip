@@ -963,7 +963,9 @@ __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, in
 // TMR / 16 row waves x 16 / (TMR / 16) column waves, NJ sub-tiles per wave
 // (as k_gemm16 against k_gemm: 4x the waves to cover the global -> LDS
 // latency of these K <= 128 products).  Same arguments and epilogue.
-template <int NT, int TMR = TM, bool ATT = false, bool MS = false>
+// QL: A and W loaded as float4 quads (every source's ld, column offsets and
+// pointer 16-B aligned; quad_ln) instead of scalars, as in k_gemm16's QA.
+template <int NT, int TMR = TM, bool ATT = false, bool MS = false, bool QL = false>
 __global__ void __launch_bounds__(1024) k_gemm_ln16(const float* __restrict__ A, int lda,
                                                     const float* __restrict__ B, int ldb,
                                                     const float* __restrict__ bias, int N, int M, int K,
@@ -1015,35 +1017,70 @@ __global__ void __launch_bounds__(1024) k_gemm_ln16(const float* __restrict__ A,
     }
   };
   float ra[PA], rb[PB];
+  constexpr int QPR = TK / 4, NQA = TMR * QPR, NQB = TNC * QPR;  // quads per row / of A / of W per K-tile
+  static_assert(!QL || (NQA <= 1024 && NQB <= 1024), "one quad per thread");
+  float4 qa = make_float4(0.f, 0.f, 0.f, 0.f), qb = qa;
   auto load = [&](int k0) {
     const float* asrc;
     int ald, acol, wcol;
     chunk_src(k0, asrc, ald, acol, wcol);
+    if constexpr (QL) {
+      const int kq = 4 * (t % QPR);
+      if (t < NQA) {
+        const int n = n0 + t / QPR;
+        qa = (n < N && k0 + kq < K) ? *reinterpret_cast<const float4*>(asrc + (size_t)n * ald + acol + kq)
+                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      if (t < NQB) {
+        const int m = t / QPR;
+        qb = (m < M && k0 + kq < K) ? *reinterpret_cast<const float4*>(B + (size_t)m * ldb + wcol + kq)
+                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    } else {
 #pragma unroll
-    for (int q = 0; q < PA; ++q) {
-      const int e = t + 1024 * q;
-      const int n = n0 + e / TK, kc = e % TK;
-      ra[q] = (n < N && k0 + kc < K) ? asrc[(size_t)n * ald + acol + kc] : 0.f;
-    }
+      for (int q = 0; q < PA; ++q) {
+        const int e = t + 1024 * q;
+        const int n = n0 + e / TK, kc = e % TK;
+        ra[q] = (n < N && k0 + kc < K) ? asrc[(size_t)n * ald + acol + kc] : 0.f;
+      }
 #pragma unroll
-    for (int q = 0; q < PB; ++q) {
-      const int e = t + 1024 * q;
-      const int m = e / TK, kc = e % TK;
-      rb[q] = (m < M && k0 + kc < K) ? B[(size_t)m * ldb + wcol + kc] : 0.f;
+      for (int q = 0; q < PB; ++q) {
+        const int e = t + 1024 * q;
+        const int m = e / TK, kc = e % TK;
+        rb[q] = (m < M && k0 + kc < K) ? B[(size_t)m * ldb + wcol + kc] : 0.f;
+      }
     }
   };
   load(0);
   int buf = 0;
   for (int k0 = 0; k0 < K; k0 += TK) {
+    if constexpr (QL) {
+      const int kq = 4 * (t % QPR);
+      if (t < NQA) {
+        float* d = &As[buf][t / QPR][kq];
+        d[0] = qa.x;
+        d[1] = qa.y;
+        d[2] = qa.z;
+        d[3] = qa.w;
+      }
+      if (t < NQB) {
+        float* d = &Bs[buf][t / QPR][kq];
+        d[0] = qb.x;
+        d[1] = qb.y;
+        d[2] = qb.z;
+        d[3] = qb.w;
+      }
+    } else {
 #pragma unroll
-    for (int q = 0; q < PA; ++q) {
-      const int e = t + 1024 * q;
-      As[buf][e / TK][e % TK] = ra[q];
-    }
+      for (int q = 0; q < PA; ++q) {
+        const int e = t + 1024 * q;
+        As[buf][e / TK][e % TK] = ra[q];
+      }
 #pragma unroll
-    for (int q = 0; q < PB; ++q) {
-      const int e = t + 1024 * q;
-      Bs[buf][e / TK][e % TK] = rb[q];
+      for (int q = 0; q < PB; ++q) {
+        const int e = t + 1024 * q;
+        Bs[buf][e / TK][e % TK] = rb[q];
+      }
     }
     __syncthreads();
     if (k0 + TK < K) load(k0 + TK);
@@ -1827,6 +1864,8 @@ extern "C" int vg_gemm_tn_group(const vg_tn* prods, int32_t n, void* stream) {
   return 0;
 }
 
+static inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
 template <bool BF>
 static int gemm_ln_act(const float* A, int32_t lda, const float* W, int32_t N, int32_t M,
                        int32_t K, const float* bias, const float* gamma, const float* beta,
@@ -1838,10 +1877,17 @@ static int gemm_ln_act(const float* A, int32_t lda, const float* W, int32_t N, i
   if (N == 0) return 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const dim3 grid((N + TM - 1) / TM, 1);
+  const bool ql = VG_QUAD_A && K % 4 == 0 && lda % 4 == 0 && al16(A) && al16(W);
   if (!BF && VG_LN16) {
-    if (M <= TN)
+    if (M <= TN && ql)
+      k_gemm_ln16<1, TM, false, false, true><<<grid, 1024, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma, beta, eps,
+                                                                  slope, H, Y, mean, rstd);
+    else if (M <= TN)
       k_gemm_ln16<1, TM><<<grid, 1024, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma, beta, eps, slope, H, Y, mean,
                                               rstd);
+    else if (VG_LN_TM32 && ql)
+      k_gemm_ln16<2, 32, false, false, true><<<dim3((N + 31) / 32, 1), 1024, 0, s>>>(
+          A, lda, W, K, bias, N, M, K, gamma, beta, eps, slope, H, Y, mean, rstd);
     else if (VG_LN_TM32)
       k_gemm_ln16<2, 32><<<dim3((N + 31) / 32, 1), 1024, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma, beta, eps,
                                                                 slope, H, Y, mean, rstd);
@@ -1902,7 +1948,13 @@ static int gemm_ln_act_ms(const vg_asrc* src, int32_t nsrc, const float* W, int3
   d.add_rows = add_rows;
   if (N == 0) return 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (!BF && VG_LN16)
+  bool ql = VG_QUAD_A && ldw % 4 == 0 && al16(W);
+  for (int i = 0; i < nsrc; ++i) ql = ql && src[i].ld % 4 == 0 && src[i].w_col0 % 4 == 0 && al16(src[i].ptr);
+  if (!BF && VG_LN16 && ql)
+    k_gemm_ln16<2, 32, false, true, true><<<dim3((N + 31) / 32, 1), 1024, 0, s>>>(
+        nullptr, 0, W, ldw, bias, N, M, K, gamma, beta, eps, slope, nullptr, Y, nullptr, nullptr, nullptr, nullptr,
+        nullptr, nullptr, ldy, d);
+  else if (!BF && VG_LN16)
     k_gemm_ln16<2, 32, false, true><<<dim3((N + 31) / 32, 1), 1024, 0, s>>>(
         nullptr, 0, W, ldw, bias, N, M, K, gamma, beta, eps, slope, nullptr, Y, nullptr, nullptr, nullptr, nullptr,
         nullptr, nullptr, ldy, d);
