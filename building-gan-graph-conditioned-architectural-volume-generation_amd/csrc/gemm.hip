@@ -168,7 +168,10 @@ __device__ __forceinline__ float4 gna_quad(const GnaDesc& ga, const float* gp, f
 // ATT (BT, ACT 0, M <= 64): also a_src[n] = <C[n,:], att_s>, a_dst[n] =
 // <C[n,:], att_d> -- GATConv's attention projections as the epilogue of its
 // own projection GEMM (the output tile is staged through LDS once).
-template <bool BT, int ACT, bool ATT = false, bool BF = false, bool GNP = false>
+// QA (bf16 operands only): A -- and B^T -- loaded as float4 quads (2 per
+// thread per K-tile) and stored to the bf16 images 8 bytes at a time,
+// instead of 8 scalars and 2-byte stores per thread (quad_ab).
+template <bool BT, int ACT, bool ATT = false, bool BF = false, bool GNP = false, bool QA = false>
 __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int lda,
                                               const float* __restrict__ B, int ldb,
                                               const float* __restrict__ bias,
@@ -226,16 +229,34 @@ __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int l
   // 8-byte LDS store per quad instead of four transposing 2-byte stores
   constexpr int QB = (TN * TK / 4) / 256;
   float qb[QB][4];
+  static_assert(!QA || BF, "quad staging for the bf16 images");
+  constexpr int QN = (TM * TK / 4) / 256, QPR = TK / 4;  // quads per thread / per tile row
+  float4 rqa[QA ? QN : 1], rqb[QA ? QN : 1];
   auto load = [&](int k0) {
+    if constexpr (QA) {
+#pragma unroll
+      for (int u = 0; u < QN; ++u) {
+        const int g = t + 256 * u;
+        const int row = g / QPR, k = k0 + 4 * (g % QPR);
+        const int n = n0 + row;
+        rqa[u] = (n < N && k < K) ? *reinterpret_cast<const float4*>(A + (size_t)n * lda + k)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (BT) {
+          const int m = m0 + row;
+          rqb[u] = (m < M && k < K) ? *reinterpret_cast<const float4*>(B + (size_t)m * ldb + k)
+                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+    }
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
       const int e = t + 256 * q;
       const int row = e / TK, kc = e % TK;
       const int n = n0 + row, k = k0 + kc;
-      ra[q] = (n < N && k < K) ? A[(size_t)n * lda + k] : 0.f;
+      if constexpr (!QA) ra[q] = (n < N && k < K) ? A[(size_t)n * lda + k] : 0.f;
       if (BT) {
         const int m = m0 + row;
-        rb[q] = (m < M && k < K) ? B[(size_t)m * ldb + k] : 0.f;
+        if constexpr (!QA) rb[q] = (m < M && k < K) ? B[(size_t)m * ldb + k] : 0.f;
       } else if (!BF) {
         const int kr = e / TN, j = e % TN;
         const int m = m0 + j, kk = k0 + kr;
@@ -262,10 +283,24 @@ __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int l
   load(0);
   int buf = 0;
   for (int k0 = 0; k0 < K; k0 += TK) {
+    if constexpr (QA) {
+#pragma unroll
+      for (int u = 0; u < QN; ++u) {
+        const int g = t + 256 * u;
+        const int row = g / QPR, kq = 4 * (g % QPR);
+        const float va[4] = {rqa[u].x, rqa[u].y, rqa[u].z, rqa[u].w};
+        *reinterpret_cast<bf16x4*>(&Ah[buf][row][kq]) = to_bf4(va);
+        if (BT) {
+          const float vb[4] = {rqb[u].x, rqb[u].y, rqb[u].z, rqb[u].w};
+          *reinterpret_cast<bf16x4*>(&Bh[buf][row][kq]) = to_bf4(vb);
+        }
+      }
+    }
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
       const int e = t + 256 * q;
-      if constexpr (BF) {
+      if constexpr (QA) {
+      } else if constexpr (BF) {
         Ah[buf][e / TK][e % TK] = static_cast<__bf16>(ra[q]);
         if (BT) Bh[buf][e / TK][e % TK] = static_cast<__bf16>(rb[q]);
       } else {
@@ -1630,6 +1665,9 @@ static int gemm(const float* A, int32_t lda, const float* B, int32_t ldb, int32_
                                                                        N, M, K);                             \
       else                                                                                                 \
         k_gemm16<BT, ACT, false, BF><<<grid, 1024, 0, s>>>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, N, M, K); \
+    else if (BF && quad_ab(A, lda, B, ldb, K, M, true))                                                    \
+      k_gemm<BT, ACT, false, BF, false, BF><<<grid, 256, 0, s>>>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, N, M, \
+                                                                 K);                                       \
     else                                                                                                   \
       k_gemm<BT, ACT, false, BF><<<grid, 256, 0, s>>>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, N, M, K); \
   } while (0)
@@ -1662,6 +1700,9 @@ static int gemm_gn_bwd(const float* A, int32_t lda, const float* B, int32_t ldb,
                                                                      K, nullptr, nullptr, nullptr, nullptr, gn);
     else
       k_gemm16<false, 0, false, BF, true><<<grid, 1024, 0, s>>>(A, lda, B, ldb, nullptr, nullptr, 0, C, ldc, N, M, K,
+                                                               nullptr, nullptr, nullptr, nullptr, gn);
+  else if (BF && quad_ab(A, lda, B, ldb, K, M, true))
+    k_gemm<false, 0, false, BF, true, BF><<<grid, 256, 0, s>>>(A, lda, B, ldb, nullptr, nullptr, 0, C, ldc, N, M, K,
                                                                nullptr, nullptr, nullptr, nullptr, gn);
   else
     k_gemm<false, 0, false, BF, true><<<grid, 256, 0, s>>>(A, lda, B, ldb, nullptr, nullptr, 0, C, ldc, N, M, K,
@@ -2015,6 +2056,9 @@ static int gat_lin_att(const float* X, int32_t ldx, const float* W, int32_t N,
     else
       k_gemm16<true, 0, true, BF><<<dim3((N + TM - 1) / TM, 1), 1024, 0, s>>>(
           X, ldx, W, Cin, nullptr, nullptr, 0, H, C, N, C, Cin, att_src, att_dst, a_src, a_dst);
+  else if (BF && quad_ab(X, ldx, W, Cin, Cin, C, true))
+    k_gemm<true, 0, true, BF, false, BF><<<dim3((N + TM - 1) / TM, 1), 256, 0, s>>>(
+        X, ldx, W, Cin, nullptr, nullptr, 0, H, C, N, C, Cin, att_src, att_dst, a_src, a_dst);
   else
     k_gemm<true, 0, true, BF><<<dim3((N + TM - 1) / TM, 1), 256, 0, s>>>(
         X, ldx, W, Cin, nullptr, nullptr, 0, H, C, N, C, Cin, att_src, att_dst, a_src, a_dst);
