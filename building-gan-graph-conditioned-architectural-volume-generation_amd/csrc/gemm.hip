@@ -856,7 +856,8 @@ struct MsDesc {
   int ld_add, add_rows;
 };
 
-template <int NT, int TMR = TM, bool ATT = false, bool MS = false, bool BF = false>
+// QL (bf16 only): operands staged from float4 quads with 8-byte bf16 stores (as k_gemm's QA).
+template <int NT, int TMR = TM, bool ATT = false, bool MS = false, bool BF = false, bool QL = false>
 __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, int lda,
                                                  const float* __restrict__ B, int ldb,
                                                  const float* __restrict__ bias, int N, int M, int K,
@@ -912,38 +913,73 @@ __global__ void __launch_bounds__(256) k_gemm_ln(const float* __restrict__ A, in
   // BF: the same coalesced global loads, staged as bf16 (Ah[buf][n][k], Bh[buf][m][k])
   __bf16(*Ah)[TMR][LDH] = reinterpret_cast<__bf16(*)[TMR][LDH]>(smem);
   __bf16(*Bh)[TNC][LDH] = reinterpret_cast<__bf16(*)[TNC][LDH]>(smem + 2 * TMR * LDP);
-  float ra[PA], rb[PB];
+  static_assert(!QL || BF, "quad staging for the bf16 images");
+  constexpr int QPR = TK / 4, NQA = (TMR * QPR) / 256, NQB = (TNC * QPR) / 256;  // quads per thread
+  float ra[QL ? 1 : PA], rb[QL ? 1 : PB];
+  float4 qa[QL ? NQA : 1], qb[QL ? NQB : 1];
   auto load = [&](int k0) {
     const float* asrc;
     int ald, acol, wcol;
     chunk_src(k0, asrc, ald, acol, wcol);
+    if constexpr (QL) {
 #pragma unroll
-    for (int q = 0; q < PA; ++q) {
-      const int e = t + 256 * q;
-      const int n = n0 + e / TK, kc = e % TK;
-      ra[q] = (n < N && k0 + kc < K) ? asrc[(size_t)n * ald + acol + kc] : 0.f;
-    }
+      for (int u = 0; u < NQA; ++u) {
+        const int g = t + 256 * u;
+        const int n = n0 + g / QPR, kq = 4 * (g % QPR);
+        qa[u] = (n < N && k0 + kq < K) ? *reinterpret_cast<const float4*>(asrc + (size_t)n * ald + acol + kq)
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
 #pragma unroll
-    for (int q = 0; q < PB; ++q) {
-      const int e = t + 256 * q;
-      const int m = e / TK, kc = e % TK;
-      rb[q] = (m < M && k0 + kc < K) ? B[(size_t)m * ldb + wcol + kc] : 0.f;
+      for (int u = 0; u < NQB; ++u) {
+        const int g = t + 256 * u;
+        const int m = g / QPR, kq = 4 * (g % QPR);
+        qb[u] = (m < M && k0 + kq < K) ? *reinterpret_cast<const float4*>(B + (size_t)m * ldb + wcol + kq)
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < PA; ++q) {
+        const int e = t + 256 * q;
+        const int n = n0 + e / TK, kc = e % TK;
+        ra[q] = (n < N && k0 + kc < K) ? asrc[(size_t)n * ald + acol + kc] : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < PB; ++q) {
+        const int e = t + 256 * q;
+        const int m = e / TK, kc = e % TK;
+        rb[q] = (m < M && k0 + kc < K) ? B[(size_t)m * ldb + wcol + kc] : 0.f;
+      }
     }
   };
   load(0);
   int buf = 0;
   for (int k0 = 0; k0 < K; k0 += TK) {
+    if constexpr (QL) {
 #pragma unroll
-    for (int q = 0; q < PA; ++q) {
-      const int e = t + 256 * q;
-      if constexpr (BF) Ah[buf][e / TK][e % TK] = static_cast<__bf16>(ra[q]);
-      else As[buf][e / TK][e % TK] = ra[q];
-    }
+      for (int u = 0; u < NQA; ++u) {
+        const int g = t + 256 * u;
+        const float v[4] = {qa[u].x, qa[u].y, qa[u].z, qa[u].w};
+        *reinterpret_cast<bf16x4*>(&Ah[buf][g / QPR][4 * (g % QPR)]) = to_bf4(v);
+      }
 #pragma unroll
-    for (int q = 0; q < PB; ++q) {
-      const int e = t + 256 * q;
-      if constexpr (BF) Bh[buf][e / TK][e % TK] = static_cast<__bf16>(rb[q]);
-      else Bs[buf][e / TK][e % TK] = rb[q];
+      for (int u = 0; u < NQB; ++u) {
+        const int g = t + 256 * u;
+        const float v[4] = {qb[u].x, qb[u].y, qb[u].z, qb[u].w};
+        *reinterpret_cast<bf16x4*>(&Bh[buf][g / QPR][4 * (g % QPR)]) = to_bf4(v);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < PA; ++q) {
+        const int e = t + 256 * q;
+        if constexpr (BF) Ah[buf][e / TK][e % TK] = static_cast<__bf16>(ra[q]);
+        else As[buf][e / TK][e % TK] = ra[q];
+      }
+#pragma unroll
+      for (int q = 0; q < PB; ++q) {
+        const int e = t + 256 * q;
+        if constexpr (BF) Bh[buf][e / TK][e % TK] = static_cast<__bf16>(rb[q]);
+        else Bs[buf][e / TK][e % TK] = rb[q];
+      }
     }
     __syncthreads();
     if (k0 + TK < K) load(k0 + TK);
@@ -1935,9 +1971,15 @@ static int gemm_ln_act(const float* A, int32_t lda, const float* W, int32_t N, i
     else
       k_gemm_ln16<2, TM><<<grid, 1024, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma, beta, eps, slope, H, Y, mean,
                                               rstd);
-  } else if (M <= TN)
+  } else if (M <= TN && BF && ql)
+    k_gemm_ln<1, TM, false, false, BF, BF><<<grid, 256, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma, beta, eps,
+                                                                 slope, H, Y, mean, rstd);
+  else if (M <= TN)
     k_gemm_ln<1, TM, false, false, BF><<<grid, 256, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma, beta, eps, slope,
                                                              H, Y, mean, rstd);
+  else if (VG_LN_TM32 && BF && ql)
+    k_gemm_ln<2, 32, false, false, BF, BF><<<dim3((N + 31) / 32, 1), 256, 0, s>>>(
+        A, lda, W, K, bias, N, M, K, gamma, beta, eps, slope, H, Y, mean, rstd);
   else if (VG_LN_TM32)
     k_gemm_ln<2, 32, false, false, BF><<<dim3((N + 31) / 32, 1), 256, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma,
                                                                               beta, eps, slope, H, Y, mean, rstd);
@@ -1997,6 +2039,10 @@ static int gemm_ln_act_ms(const vg_asrc* src, int32_t nsrc, const float* W, int3
         nullptr, nullptr, ldy, d);
   else if (!BF && VG_LN16)
     k_gemm_ln16<2, 32, false, true><<<dim3((N + 31) / 32, 1), 1024, 0, s>>>(
+        nullptr, 0, W, ldw, bias, N, M, K, gamma, beta, eps, slope, nullptr, Y, nullptr, nullptr, nullptr, nullptr,
+        nullptr, nullptr, ldy, d);
+  else if (BF && ql)
+    k_gemm_ln<2, 32, false, true, BF, BF><<<dim3((N + 31) / 32, 1), 256, 0, s>>>(
         nullptr, 0, W, ldw, bias, N, M, K, gamma, beta, eps, slope, nullptr, Y, nullptr, nullptr, nullptr, nullptr,
         nullptr, nullptr, ldy, d);
   else
