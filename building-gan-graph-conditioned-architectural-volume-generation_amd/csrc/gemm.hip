@@ -2084,7 +2084,11 @@ static int gat_lin_att(const float* X, int32_t ldx, const float* W, int32_t N,
     return vg_gat_att(H, N, C, att_src, att_dst, a_src, a_dst, stream);
   }
   if (C > TN) {  // whole 128-column rows per block, projections in the epilogue
-    if (!BF && VG_LN16)
+    if (!BF && VG_LN16 && quad_ab(X, ldx, W, Cin, Cin, C, true))
+      k_gemm_ln16<2, 32, true, false, true><<<dim3((N + 31) / 32, 1), 1024, 0, s>>>(
+          X, ldx, W, Cin, nullptr, N, C, Cin, nullptr, nullptr, 0.f, 0.f, H, nullptr, nullptr, nullptr, att_src,
+          att_dst, a_src, a_dst);
+    else if (!BF && VG_LN16)
       k_gemm_ln16<2, 32, true><<<dim3((N + 31) / 32, 1), 1024, 0, s>>>(
           X, ldx, W, Cin, nullptr, N, C, Cin, nullptr, nullptr, 0.f, 0.f, H, nullptr, nullptr, nullptr, att_src,
           att_dst, a_src, a_dst);
