@@ -64,7 +64,7 @@ __global__ void __launch_bounds__(kBlock) k_ln_act_fwd(const float* __restrict__
   }
 }
 
-template <int L, int CPL>
+template <int L, int CPL, bool VEC = false>  // VEC: row vectors as float4 (C % CPL == 0, 16-B aligned rows)
 __global__ void __launch_bounds__(kBlock) k_ln_act_bwd(const float* __restrict__ x, int N, int C,
                                                        const float* __restrict__ gamma,
                                                        const float* __restrict__ beta, float slope,
@@ -86,8 +86,8 @@ __global__ void __launch_bounds__(kBlock) k_ln_act_bwd(const float* __restrict__
   for (int i = lb * G + grp; i < N; i += gridDim.x * G) {
     const float mu = mean[i], rs = rstd[i];
     Vec<CPL> v, g;
-    load_row<CPL, false>(v, x + (size_t)i * C, c0, C);
-    load_row<CPL, false>(g, gy + (size_t)i * C, c0, C);
+    load_row<CPL, VEC>(v, x + (size_t)i * C, c0, C);
+    load_row<CPL, VEC>(g, gy + (size_t)i * C, c0, C);
     float s1 = 0.f, s2 = 0.f;
     Vec<CPL> xh, gz;
 #pragma unroll
@@ -105,7 +105,7 @@ __global__ void __launch_bounds__(kBlock) k_ln_act_bwd(const float* __restrict__
     Vec<CPL> o;
 #pragma unroll
     for (int q = 0; q < CPL; ++q) o.v[q] = rs * (gz.v[q] * ga.v[q] - m1 - xh.v[q] * m2);
-    store_row<CPL, false>(o, gx + (size_t)i * C, c0, C);
+    store_row<CPL, VEC>(o, gx + (size_t)i * C, c0, C);
   }
   Vec<CPL> vals[2] = {pg, pb};
   block_partials<L, CPL>(vals, 2, C, part);
@@ -153,6 +153,12 @@ inline bool ln_shape(int C, int& L, int& CPL) {
   return true;
 }
 
+// float4 row vectors in k_ln_act_bwd: whole lane vectors in or out of C, aligned rows
+inline bool ln_vec(int C, int cpl, const float* x, const float* gy, const float* gx) {
+  auto al = [](const float* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  return C % cpl == 0 && C % 4 == 0 && al(x) && al(gy) && al(gx);
+}
+
 #define VG_LN_DISPATCH(C, CALL)                                                  \
   do {                                                                           \
     int l_, c_;                                                                  \
@@ -189,9 +195,11 @@ extern "C" int vg_ln_act_bwd(const float* x, int32_t N, int32_t C, const float* 
   hipStream_t s = static_cast<hipStream_t>(stream);
   int grid = 0;
   VG_LN_DISPATCH(C, (grid = grid_for(N, L_) < kMaxBlocks ? grid_for(N, L_) : kMaxBlocks,
-                     k_ln_act_bwd<L_, CPL_><<<grid, kBlock, 0, s>>>(x, N, C, gamma, beta, slope,
-                                                                   mean, rstd, g_y, g_x,
-                                                                   workspace)));
+                     (ln_vec(C, CPL_, x, g_y, g_x)
+                          ? k_ln_act_bwd<L_, CPL_, true><<<grid, kBlock, 0, s>>>(x, N, C, gamma, beta, slope, mean,
+                                                                                rstd, g_y, g_x, workspace)
+                          : k_ln_act_bwd<L_, CPL_><<<grid, kBlock, 0, s>>>(x, N, C, gamma, beta, slope, mean, rstd,
+                                                                          g_y, g_x, workspace))));
   k_ln_fold<<<vg_blocks(2 * C, 64), 1024, 0, s>>>(workspace, grid, C, accumulate, g_gamma, g_beta);
   VG_CHECK_LAUNCH();
   return 0;
@@ -209,9 +217,11 @@ extern "C" int vg_ln_act_bwd_deferred(const float* x, int32_t N, int32_t C, cons
   hipStream_t s = static_cast<hipStream_t>(stream);
   int grid = 0;
   VG_LN_DISPATCH(C, (grid = grid_for(N, L_) < kMaxBlocks ? grid_for(N, L_) : kMaxBlocks,
-                     k_ln_act_bwd<L_, CPL_><<<grid, kBlock, 0, s>>>(x, N, C, gamma, beta, slope,
-                                                                   mean, rstd, g_y, g_x,
-                                                                   workspace)));
+                     (ln_vec(C, CPL_, x, g_y, g_x)
+                          ? k_ln_act_bwd<L_, CPL_, true><<<grid, kBlock, 0, s>>>(x, N, C, gamma, beta, slope, mean,
+                                                                                rstd, g_y, g_x, workspace)
+                          : k_ln_act_bwd<L_, CPL_><<<grid, kBlock, 0, s>>>(x, N, C, gamma, beta, slope, mean, rstd,
+                                                                          g_y, g_x, workspace))));
   // partial rows [grid][2C] = [gamma | beta]: two folds for vg_fold_batch
   folds_out[0] = vg_fold{g_gamma, C, C, C, accumulate, 1, {{workspace, grid, 2 * C}, {nullptr, 0, 0}}};
   folds_out[1] = vg_fold{g_beta, C, C, C, accumulate, 1, {{workspace + C, grid, 2 * C}, {nullptr, 0, 0}}};
