@@ -45,11 +45,18 @@ def log(msg: str) -> None:
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-def agg_bytes(n: int, e: int, c: int) -> int:
-    """Algorithmic (compulsory) bytes of one vg_gat_aggregate_fwd launch: read
-    h [N,C], write out [N,C], read row_ptr [N+1] and col [E'], read a_src /
-    a_dst [N], read bias [C], write alpha [E'] (plus alpha)."""
-    return 4 * (2 * n * c + (n + 1) + 2 * e + 2 * n + c)
+def agg_bytes(n: int, e: int, c: int, elem: int = 4) -> int:
+    """Algorithmic (compulsory) bytes of one aggregation launch, SURVEY.md 8(d)
+    strictly: read h [N,C] and write out [N,C] (``elem`` bytes each), read
+    a_src / a_dst [N] f32, col [E'] and row_ptr [N+1] int32.  Outputs the
+    implementation chooses to write besides ``out`` (alpha for the backward,
+    the GraphNorm partials) are not counted."""
+    return 2 * n * c * elem + 4 * (2 * n + e + (n + 1))
+
+
+def agg_extra_bytes(n: int, e: int) -> int:
+    """alpha [E'] f32, written for the backward (not in agg_bytes)."""
+    return 4 * e
 
 
 def step_aggregate_calls(tr, csr):
@@ -131,18 +138,20 @@ def aggregate_roofline(tr, csr, device, reps: int = 20, gnp: bool = False):
     torch.cuda.synchronize()
     total_ms = st.elapsed_time(en)
     launches = reps * len(calls)
-    nbytes = reps * sum(agg_bytes(c_csr.num_nodes, c_csr.num_edges, c) + (gnp_bytes(c_csr, c) if gnp else 0)
-                        for c_csr, c in calls)
+    nbytes = reps * sum(agg_bytes(c_csr.num_nodes, c_csr.num_edges, c) for c_csr, c in calls)
+    extra = reps * sum(agg_extra_bytes(c_csr.num_nodes, c_csr.num_edges) + (gnp_bytes(c_csr, c) if gnp else 0)
+                       for c_csr, c in calls)
     return {"launches": launches, "launches_per_step": len(calls), "avg_us": total_ms * 1e3 / launches,
-            "avg_bytes": nbytes / launches, "achieved_gbs": nbytes / (total_ms * 1e-3) / 1e9}
+            "avg_bytes": nbytes / launches, "achieved_gbs": nbytes / (total_ms * 1e-3) / 1e9,
+            "avg_extra_written_bytes": extra / launches}
 
 
-def load_pmc_traffic():
+def load_pmc_traffic(name: str = "r03_pmc_aggregate_gnp.json"):
     """Per-launch HBM-side bytes of the scatter kernel from the committed
-    rocprofv3 PMC summary (tools/pmc_roofline.sh), or None."""
-    path = os.path.join(ROOT, "profiles", "r02_pmc_aggregate.json")
-    if not os.path.exists(path):
-        path = os.path.join(ROOT, "profiles", "r01_pmc_aggregate.json")
+    rocprofv3 PMC summary of the variant the step runs (tools/pmc_roofline.sh
+    --gnp), or (None, None) when this round has not measured it: an older
+    round's summary describes other kernels and is not reported."""
+    path = os.path.join(ROOT, "profiles", name)
     if not os.path.exists(path):
         return None, None
     with open(path) as f:
@@ -277,6 +286,153 @@ def stress_roofline(device, channels=(128, 64, 1), reps: int = 20):
             "distinct_sources_per_tile": round(uniq / tiles, 1), "edges_per_tile": round(e / tiles, 1)}
 
 
+def fresh_batch_leg(cfg, precision: str, steps: int, warmup: int, batch: int, device, rank: int, world: int):
+    """What ``Trainer.train()`` delivers: every step on a NEW batch from the
+    native data path (GraphStore -> C++ collate into pinned buffers -> async
+    upload -> CSR adopted, prefetched on a side thread), the per-batch
+    type-matched mean / padded columns built, then the step the trainer picks
+    for a batch it has not seen (``Trainer._train_batch``: eager, since a
+    capture per one-shot batch costs more than it saves).  Max over ranks."""
+    import tempfile
+
+    from vgan.loader import GraphLoader
+    from vgan.store import write_store
+    from vgan.synth import SyntheticDataset
+
+    n_batches = warmup + steps
+    tmp = tempfile.mkdtemp(prefix=f"vgan_fresh_{rank}_")
+    ds = SyntheticDataset(n_batches * batch * world, seed=4321)
+    store = write_store(os.path.join(tmp, "store"), ds)
+    loader = GraphLoader(store, batch_size=batch, shuffle=True, device=device, prefetch=3, rank=rank,
+                         world_size=world, seed=4321)
+    torch.manual_seed(cfg.SEED + rank)
+    tr = build_trainer(cfg, precision)
+    cfg.runtime["train_step"] = "auto"
+    it = iter(loader)
+    for _ in range(warmup):
+        loc, vox = next(it)
+        tr._train_batch(loc, vox)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loc, vox = next(it)
+        tr._train_batch(loc, vox)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    del it, loader, store
+    import shutil
+
+    shutil.rmtree(tmp, ignore_errors=True)
+    return {"value": round(batch * world * steps / elapsed, 3), "unit": "graphs/s",
+            "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps, "warmup": warmup,
+            "execution": "eager Trainer step per new batch (Trainer._train_batch), GraphLoader prefetch 3"}
+
+
+def sweep_leg(device, graphs: int = 10000, batch: int = 32, n_taus: int = 10, distinct: int = 20):
+    """BASELINE.json configs[4]: generator-only inference sweep, ``graphs``
+    building samples x a geometric Gumbel temperature schedule 1.0 -> 0.1,
+    f16 (and f32) eval forward, one stacked forward per batch of ``batch``
+    buildings over the ``n_taus`` copies, hipGraph-captured.  The batches cycle
+    over ``distinct`` staged synthetic batches (each replay draws fresh z and
+    Gumbel noise); the first pass captures, the second is timed.  Also the f16
+    scatter kernel (vg_hgat_fwd) over the sweep's own stacked graph and channel
+    schedule, graph-replayed between HIP events."""
+    from vgan import data as vdata
+    from vgan._lib import LIB, check, ptr, stream_handle
+    from vgan.config import Configuration
+    from vgan.half import _r8
+    from vgan.infer import InferenceSweep, geometric_taus
+    from vgan.models import VoxelGNNGenerator
+    from vgan.synth import SyntheticDataset
+
+    cfg = Configuration()
+    cfg.DEVICE = str(device)
+    cfg.runtime["rng"] = "device"
+    torch.manual_seed(cfg.SEED)
+    G = VoxelGNNGenerator(cfg, 17, 12)
+    ds = SyntheticDataset(6500, seed=777)
+    staged = []
+    for b in range(distinct):
+        loc, vox = ds.batch(list(range(3200 + b * batch, 3200 + (b + 1) * batch)))
+        staged.append((loc.to(device), vox.to(device)))
+    n_batches = -(-graphs // batch)
+    plan = [staged[i % distinct] for i in range(n_batches)]
+    taus = geometric_taus(1.0, 0.1, n_taus)
+    out = {"workload": f"configs[4]: {n_batches * batch} generator samples (batches of {batch} cycling over "
+                       f"{distinct} staged synthetic batches), {n_taus} Gumbel temperatures 1.0->0.1 geometric, "
+                       f"eval G forward stacked over the temperatures, hipGraph replay",
+           "unit": "samples/s (buildings x temperatures)"}
+    for dt in ("f16", "f32"):
+        sw = InferenceSweep(G, taus, graphed=True, dtype=dt)
+        sw.run(staged)  # capture every staged batch's graph
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = sw.run(plan)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        out[dt] = {"value": round(res["samples"] / el, 1), "seconds": round(el, 4), "samples": res["samples"],
+                   "ms_per_batch": round(el / n_batches * 1e3, 4)}
+        log(f"sweep {dt}: {out[dt]['value']:.0f} samples/s ({el:.3f} s for {res['samples']} samples)")
+    # the f16 scatter kernel on the sweep's stacked CSR (n_taus copies)
+    loc, vox = staged[0]
+    csr = vdata.prepared(loc, vox, cfg.NUM_CLASSES).csr.stacked(n_taus)
+    rows, e = csr.num_nodes, csr.num_edges
+    widths = G.encoder.widths[1:]
+    gen = torch.Generator(device=device)
+    gen.manual_seed(5)
+    bufs = {}
+    for c in set(widths):
+        ld = _r8(c)
+        h = (torch.randn(rows, ld, device=device, generator=gen) * 0.5).half()
+        bufs[c] = (h, 0.3 * torch.randn(rows, device=device, generator=gen),
+                   0.3 * torch.randn(rows, device=device, generator=gen), torch.randn(c, device=device, generator=gen),
+                   torch.empty(rows, ld, dtype=torch.float16, device=device), ld)
+
+    def launch_all():
+        st = stream_handle(device)
+        for c in widths:
+            h, a_s, a_d, bias, o, ld = bufs[c]
+            check(LIB.vg_hgat_fwd(ptr(csr.row_ptr), ptr(csr.col), rows, c, ld, ptr(h), ptr(a_s), ptr(a_d),
+                                  ptr(bias), 0.2, ptr(o), ld, st), "vg_hgat_fwd")
+
+    side = torch.cuda.Stream(device)
+    side.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(side):
+        launch_all()
+    torch.cuda.current_stream(device).wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        launch_all()
+    g.replay()
+    torch.cuda.synchronize()
+    reps = 20
+    st_ev, en_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    st_ev.record()
+    for _ in range(reps):
+        g.replay()
+    en_ev.record()
+    torch.cuda.synchronize()
+    ms = st_ev.elapsed_time(en_ev)
+    nbytes = reps * sum(agg_bytes(rows, e, c, elem=2) for c in widths)
+    launches = reps * len(widths)
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    out["roofline"] = {"kernel": "vg_hgat_fwd (f16 rows: edge softmax + CSR gather-sum + bias)", "bound": "hbm",
+                       "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": round(gbs / HBM_PEAK_GBS, 4), "avg_launch_us": round(ms * 1e3 / launches, 3),
+                       "avg_algorithmic_bytes": int(nbytes / launches), "rows": rows, "edges": e,
+                       "launches_per_forward": len(widths)}
+    log(f"sweep vg_hgat_fwd: {ms * 1e3 / launches:.2f} us per launch, {gbs:.0f} GB/s")
+    return out
+
+
 def cpu_baseline(cfg_batch: int, seconds_budget: float):
     """Time the CPU oracle (reference step restatement) on a batch-32 step."""
     from oracle import pyg
@@ -341,6 +497,10 @@ def main():
                          "no instrumented / stress / CPU passes")
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the scatter-kernel roofline replays (--steps of them), for rocprofv3 --pmc passes")
+    ap.add_argument("--gnp", action="store_true",
+                    help="with --roofline-only: the variant the step runs (vg_gat_aggregate_fwd_gnp)")
+    ap.add_argument("--no-fresh", action="store_true", help="skip the fresh-batch (Trainer.train path) leg")
+    ap.add_argument("--no-sweep", action="store_true", help="skip the configs[4] inference-sweep leg")
     args = ap.parse_args()
     global GRAPHED
     GRAPHED = not args.eager
@@ -384,7 +544,7 @@ def main():
         from vgan import data as vdata
 
         csr0 = vdata.prepared(pool[0][0], pool[0][1], cfg.NUM_CLASSES).csr
-        kern = aggregate_roofline(tr, csr0, device, reps=args.steps)
+        kern = aggregate_roofline(tr, csr0, device, reps=args.steps, gnp=args.gnp)
         print(json.dumps({"roofline_only": True, **{k: round(v, 3) for k, v in kern.items()}}), flush=True)
         return
 
@@ -430,7 +590,13 @@ def main():
     kern_gnp = aggregate_roofline(tr, csr0, device, reps=max(args.steps, 10), gnp=True)
     if kern_gnp:
         log(f"vg_gat_aggregate_fwd_gnp: avg {kern_gnp['avg_us']:.2f} us, {kern_gnp['achieved_gbs']:.1f} GB/s")
+    head = kern_gnp or kern
     traffic, traffic_src = load_pmc_traffic()
+    # what Trainer.train() delivers: a new batch from the native loader every step
+    fresh = None
+    if not args.no_fresh:
+        fresh = fresh_batch_leg(cfg, args.precision, args.steps, args.warmup, args.batch, device, rank, world)
+        log(f"fresh batches (eager, loader): {fresh['ms_per_step']:.2f} ms/step, {fresh['value']:.1f} graphs/s")
 
     result = None
     if rank == 0:
@@ -440,6 +606,7 @@ def main():
                 log(f"stress C={c}: {r['avg_us']:.1f} us, {r['achieved_gbs']:.0f} GB/s")
             for c, r in stress["per_channels_lds"].items():
                 log(f"stress C={c} (LDS-staged): {r['avg_us']:.1f} us, {r['achieved_gbs']:.0f} GB/s")
+        sweep = None if args.no_sweep else sweep_leg(device)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args.batch, args.cpu_seconds)
@@ -469,33 +636,42 @@ def main():
                               "N_CRITIC critic-engine graphs, one generator-iteration graph") if GRAPHED else "eager",
             },
             "roofline": {
-                "kernel": "vg_gat_aggregate_fwd (GAT edge softmax + CSR gather-sum + bias: the scatter kernel)",
+                "kernel": "vg_gat_aggregate_fwd_gnp (the scatter kernel as the step runs it: GAT edge softmax + "
+                          "CSR gather-sum + bias, with the following GraphNorm's column partials in the epilogue)",
                 "bound": "hbm",
-                "achieved": round(kern["achieved_gbs"], 2),
+                "achieved": round(head["achieved_gbs"], 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": round(kern["achieved_gbs"] / HBM_PEAK_GBS, 5),
+                "frac": round(head["achieved_gbs"] / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "avg_launch_us": round(kern["avg_us"], 3),
-                "avg_algorithmic_bytes": int(kern["avg_bytes"]),
-                "launches_timed": kern["launches"],
-                "launches_per_step": kern["launches_per_step"],
+                "avg_launch_us": round(head["avg_us"], 3),
+                "avg_algorithmic_bytes": int(head["avg_bytes"]),
+                "algorithmic_bytes": "SURVEY.md 8(d) compulsory: 2*N*C*4 (h in, out) + 2*N*4 (a_src, a_dst) + "
+                                     "E'*4 (col) + (N+1)*4 (row_ptr); alpha and the GraphNorm partials written "
+                                     "besides are not counted",
+                "avg_extra_written_bytes": int(head["avg_extra_written_bytes"]),
+                "launches_timed": head["launches"],
+                "launches_per_step": head["launches_per_step"],
                 "timing": "the step's own mix of launches (CSRs, channel counts), hipGraph-replayed between HIP "
                           "events on the replay stream",
-                "step_variant": None if not kern_gnp else {
-                    "kernel": "vg_gat_aggregate_fwd_gnp (the variant the step runs: the following GraphNorm's "
-                              "column partials in the epilogue, replacing that GraphNorm's statistics pass)",
-                    "achieved": round(kern_gnp["achieved_gbs"], 2),
-                    "frac": round(kern_gnp["achieved_gbs"] / HBM_PEAK_GBS, 5),
-                    "avg_launch_us": round(kern_gnp["avg_us"], 3),
-                    "avg_algorithmic_bytes": int(kern_gnp["avg_bytes"]),
+                "plain_kernel": {
+                    "kernel": "vg_gat_aggregate_fwd (no GraphNorm partials; the eager / inference forward)",
+                    "achieved": round(kern["achieved_gbs"], 2),
+                    "frac": round(kern["achieved_gbs"] / HBM_PEAK_GBS, 5),
+                    "avg_launch_us": round(kern["avg_us"], 3),
+                    "avg_algorithmic_bytes": int(kern["avg_bytes"]),
                 },
             },
             "cpu_baseline": cpu,
         }
+        if fresh:
+            result["fresh_batch_ms_per_step"] = fresh["ms_per_step"]
+            result["fresh_batch"] = fresh
         if bf16:
             result["bf16"] = bf16
+        if sweep:
+            result["inference_sweep"] = sweep
         if stress:
             # configs[3]: the faster of the two large-graph aggregations -- the
             # register gather (k_gat_fwd_cp) or the LDS-staged tile plan

@@ -114,7 +114,8 @@ _CHAIN = os.environ.get("VGAN_CHAIN", "1") == "1"
 def linear_chain(x, ldx: int, rows: int, widths, layers, stream) -> bool:
     """vg_linear_chain over ``layers`` (dicts of VgChainLayer fields; device
     pointers as ints / c_void_p); False when the width chain has no kernel
-    (the caller runs its per-layer GEMMs)."""
+    (the caller runs its per-layer GEMMs).  Only VG_EINVAL (no kernel for
+    this width chain / alignment) falls back; a launch error raises."""
     if not _CHAIN:
         return False
     n = len(layers)
@@ -123,8 +124,12 @@ def linear_chain(x, ldx: int, rows: int, widths, layers, stream) -> bool:
         for k, v in l.items():
             setattr(arr[i], k, v.value if isinstance(v, ctypes.c_void_p) else v)
     w = (ctypes.c_int32 * (n + 1))(*widths)
-    fn = LIB.vg_linear_chain_bf16 if _precision == "bf16" else LIB.vg_linear_chain
-    return fn(x, ldx, rows, w, n, arr, stream) == 0
+    name = "vg_linear_chain_bf16" if _precision == "bf16" else "vg_linear_chain"
+    rc = getattr(LIB, name)(x, ldx, rows, w, n, arr, stream)
+    if rc == VG_EINVAL:
+        return False
+    check(rc, name)
+    return True
 
 
 class VgASrc(ctypes.Structure):

@@ -38,6 +38,24 @@ class Prepared:
 _FALLBACK_CACHE: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
 
 
+def _tensor_key(t):
+    """Identity of a tensor's contents without reading them: storage address,
+    shape and autograd version counter (bumped by every in-place write)."""
+    if t is None:
+        return None
+    return (t.data_ptr(), tuple(t.shape), t._version)
+
+
+def _inputs_key(local_graph, voxel_graph):
+    """Every input the prepared structures depend on: the program graph's
+    features and types (type-matched mean), the voxel graph's features, types,
+    one-hot labels and edges (CSR).  A voxel batch paired with another
+    program batch, or edited in place, gets a fresh build."""
+    return tuple(_tensor_key(getattr(g, k, None)) for g, k in (
+        (local_graph, "x"), (local_graph, "type"), (voxel_graph, "x"), (voxel_graph, "type"),
+        (voxel_graph, "types_onehot"), (voxel_graph, "edge_index")))
+
+
 def _build(local_graph, voxel_graph, n_classes: int) -> Prepared:
     vx = voxel_graph.x
     if vx.dtype != torch.float32:
@@ -49,10 +67,11 @@ def _build(local_graph, voxel_graph, n_classes: int) -> Prepared:
     getter = getattr(voxel_graph, "derived", None)
     arrays = getter("csr_arrays") if callable(getter) else None
     if arrays is not None and arrays[0].device == vx.device and arrays[0].numel() == n + 1:
-        csr = ops.CSR.from_arrays(*arrays)  # emitted by the host collate (vgan.store)
+        # emitted by the host collate (vgan.store), with its largest degree: no host sync
+        csr = ops.CSR.from_arrays(*arrays, max_degree=getter("csr_max_degree"))
     else:
         csr = ops.CSR(voxel_graph.edge_index, n)
-    csr.ell()  # the padded column array (one host sync) before any graph capture
+    csr.ell()  # the padded column array before any graph capture (one host sync unless the degree is known)
     mv = torch.empty(n, fl + fv, dtype=torch.float32, device=vx.device)
     ops.type_mean(lx, local_graph.type, voxel_graph.type, n_classes, out=mv, col0=0)
     mv[:, fl:].copy_(vx)
@@ -62,16 +81,26 @@ def _build(local_graph, voxel_graph, n_classes: int) -> Prepared:
 
 
 def prepared(local_graph, voxel_graph, n_classes: int) -> Prepared:
+    """The batch's cached structures, rebuilt when any input they depend on
+    changed (``_inputs_key``): cached on a ``GraphBatch`` itself, and for other
+    batch types (a reference PyG ``Batch``) in a side table keyed weakly on
+    ``voxel_graph.x``."""
+    key = _inputs_key(local_graph, voxel_graph)
     getter = getattr(voxel_graph, "derived", None)
     if callable(getter):
-        prep = getter("prepared")
-        if prep is None:
-            prep = _build(local_graph, voxel_graph, n_classes)
-            voxel_graph.set_derived("prepared", prep)
-        return prep
-    key = voxel_graph.x
-    prep = _FALLBACK_CACHE.get(key)
-    if prep is None:
-        prep = _build(local_graph, voxel_graph, n_classes)
-        _FALLBACK_CACHE[key] = prep
-    return prep
+        hit = getter("prepared")
+        if hit is None or hit[0] != key:
+            if hit is not None:
+                # inputs changed under a cached build: everything derived from
+                # it (captured step / sweep graphs hold its device pointers, a
+                # host-collated CSR its old edges) is dropped with it
+                voxel_graph.clear_derived(keep=("ptr_host",) if hit[0][5] != key[5] else
+                                          ("ptr_host", "csr_arrays", "csr_max_degree"))
+            hit = (key, _build(local_graph, voxel_graph, n_classes))
+            voxel_graph.set_derived("prepared", hit)
+        return hit[1]
+    hit = _FALLBACK_CACHE.get(voxel_graph.x)
+    if hit is None or hit[0] != key:
+        hit = (key, _build(local_graph, voxel_graph, n_classes))
+        _FALLBACK_CACHE[voxel_graph.x] = hit
+    return hit[1]

@@ -46,15 +46,28 @@ def init(backend: Optional[str] = None, configuration=None) -> tuple:
 
 
 class GradSync:
-    """Averages a flat gradient across ranks; broadcasts initial parameters."""
+    """Averages a flat gradient across ranks; broadcasts initial parameters.
 
-    def __init__(self, group=None):
+    ``force=True`` makes a one-rank group active (the collectives become
+    identities): the tests use it to capture RCCL calls in the step graphs on a
+    one-GPU box."""
+
+    def __init__(self, group=None, force: bool = False):
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        up = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if up else 1
+        self.force = bool(force) and up
+        self.backend = dist.get_backend(group) if up else None
 
     @property
     def active(self) -> bool:
-        return self.world > 1
+        return self.world > 1 or self.force
+
+    @property
+    def capturable(self) -> bool:
+        """The collectives can be recorded inside a hipGraph: RCCL ("nccl") is
+        stream-ordered device work; gloo runs on the host."""
+        return self.backend == "nccl"
 
     def broadcast_params(self, flat) -> None:
         if self.active:
@@ -71,3 +84,13 @@ class GradSync:
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
             t.mul_(1.0 / self.world)
         return t
+
+    def reduce_host(self, values, op: str = "sum"):
+        """All-reduce a list of Python floats (epoch metric sums, minima) over
+        the ranks: one small collective, on the device for RCCL."""
+        if not self.active:
+            return [float(v) for v in values]
+        dev = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MIN, group=self.group)
+        return [float(v) for v in t.cpu().tolist()]

@@ -124,6 +124,72 @@ class FlatAdam(torch.optim.Optimizer):
         return {"step": int(self.step_t.item()), "exp_avg": self.exp_avg.clone(),
                 "exp_avg_sq": self.exp_avg_sq.clone()}
 
+    # ------------------------------------------- torch.optim.Adam state format
+    # Checkpoints keep the reference's keys (trainer.py:731-733 saves
+    # optimizer.state_dict() of a torch Adam and :632-633 loads it back), so
+    # the flat moments are written into / read from that per-parameter form.
+    def _slices(self, params):
+        for p in params:
+            off = self.flat._offset(p)
+            if not 0 <= off < self.flat.numel:
+                raise ValueError("optimizer parameter is not in this flat buffer")
+            yield p, off, p.numel()
+
+    def export_to(self, opt: Optional[torch.optim.Optimizer]) -> None:
+        """Write step / exp_avg / exp_avg_sq into ``opt.state`` (a torch Adam
+        over the same parameters; this optimizer itself when ``opt`` is None)
+        in torch.optim.Adam's layout: a float32 scalar tensor step and
+        per-parameter moment tensors."""
+        opt = self if opt is None else opt
+        step = float(self.step_t.item())
+        for group in opt.param_groups:
+            for p, off, n in self._slices(group["params"]):
+                if step == 0:
+                    opt.state.pop(p, None)  # torch Adam keeps no state before its first step
+                    continue
+                opt.state[p] = {"step": torch.tensor(step, dtype=torch.float32),
+                                "exp_avg": self.exp_avg[off:off + n].view_as(p).clone(),
+                                "exp_avg_sq": self.exp_avg_sq[off:off + n].view_as(p).clone()}
+
+    def import_from(self, opt: Optional[torch.optim.Optimizer]) -> None:
+        """Read a torch Adam state (after ``opt.load_state_dict``) into the
+        flat moments and the device step counter."""
+        opt = self if opt is None else opt
+        steps = set()
+        with torch.no_grad():
+            self.exp_avg.zero_()
+            self.exp_avg_sq.zero_()
+            for group in opt.param_groups:
+                for p, off, n in self._slices(group["params"]):
+                    st = opt.state.get(p)
+                    if not st:
+                        steps.add(0)
+                        continue
+                    steps.add(int(float(st["step"])))
+                    self.exp_avg[off:off + n].copy_(st["exp_avg"].reshape(-1))
+                    self.exp_avg_sq[off:off + n].copy_(st["exp_avg_sq"].reshape(-1))
+        if len(steps) > 1:
+            raise ValueError(f"parameters of one optimizer at different Adam steps {sorted(steps)}")
+        step = steps.pop() if steps else 0
+        self.step_t.fill_(step)
+        self.step_count = step
+        self._lr_host = None  # the restored learning rate goes to the device now
+        self.sync_lr()
+
+    def state_dict(self):
+        """torch.optim.Adam-format state (loadable by a torch Adam over the same
+        parameters)."""
+        self.export_to(None)
+        sd = super().state_dict()
+        for g in sd["param_groups"]:
+            g.update({k: v for k, v in dict(amsgrad=False, maximize=False, foreach=None, capturable=False,
+                                            differentiable=False, fused=None).items() if k not in g})
+        return sd
+
+    def load_state_dict(self, state_dict) -> None:
+        super().load_state_dict(state_dict)
+        self.import_from(None)
+
 
 def param_iter(modules: Iterable[nn.Module]):
     for m in modules:

@@ -136,6 +136,8 @@ class GraphBatch(GraphData):
         if "csr_arrays" in self._derived:  # host-built CSR/CSC (vgan.store) travels with the batch
             out._derived["csr_arrays"] = tuple(t.to(device, non_blocking=non_blocking)
                                                for t in self._derived["csr_arrays"])
+            if "csr_max_degree" in self._derived:
+                out._derived["csr_max_degree"] = self._derived["csr_max_degree"]
         return out
 
     # ------------------------------------------------------- derived, per batch
@@ -144,6 +146,12 @@ class GraphBatch(GraphData):
 
     def set_derived(self, key: str, value: Any) -> None:
         self._derived[key] = value
+
+    def clear_derived(self, keep: Iterable[str] = ()) -> None:
+        """Drop every derived structure except ``keep``."""
+        keep = set(keep)
+        for key in [k for k in self._derived if k not in keep]:
+            del self._derived[key]
 
 
 def _same_device(a: torch.device, b: torch.device) -> bool:

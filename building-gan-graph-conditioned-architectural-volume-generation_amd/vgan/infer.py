@@ -81,6 +81,26 @@ class InferenceSweep:
         return hard.reshape(k, n, -1).argmax(-1).to(torch.int8)
 
     @torch.no_grad()
+    def generate(self, local_graph, voxel_graph):
+        """(logits [N, K], label_hard [N, K]) of one sample per voxel at the
+        schedule's single temperature: the evaluation forward of
+        ``Trainer._validate_each_epoch`` / ``test`` (``trainer.py:545-548,
+        769-772``), on the sweep's no-grad path (multi-source first layers, no
+        concatenation).  Eval mode is the caller's."""
+        if len(self.taus) != 1 or self.half is not None:
+            raise ValueError("generate() is the one-temperature f32 forward")
+        G = self.G
+        G.rng.reset()
+        z = G.rng.normal((1, voxel_graph.num_nodes, G.configuration.Z_DIM), voxel_graph.x.device)
+        saved = G.tau
+        G.tau = self.taus[0]
+        try:
+            logits, hard, _ = G(local_graph, voxel_graph, z, stacked=True)
+        finally:
+            G.tau = saved
+        return logits.reshape(-1, logits.shape[-1]), hard.reshape(-1, hard.shape[-1])
+
+    @torch.no_grad()
     def run_batch(self, local_graph, voxel_graph) -> torch.Tensor:
         """[len(taus), N] int8 predicted voxel types (device tensor)."""
         was = self.G.training

@@ -51,18 +51,27 @@ class GraphLoader:
 
     def __init__(self, store: GraphStore, indices: Optional[Sequence[int]] = None, batch_size: int = 1,
                  shuffle: bool = True, drop_last: bool = False, device=None, prefetch: int = 2,
-                 threads: int = 4, rank: int = 0, world_size: int = 1, seed: Optional[int] = None):
+                 threads: int = 4, rank: int = 0, world_size: int = 1, seed: Optional[int] = None,
+                 even: bool = True, resident: bool = False):
         """``rank`` / ``world_size``: data-parallel sharding -- every rank draws
         the same epoch plan and takes batches rank, rank + world, ... of it, so
         ranks see disjoint buildings (weak scaling, one batch of
         ``batch_size`` per rank and step).
 
-        With ``world_size > 1`` the plan is cut to a multiple of
-        ``world_size`` batches (every rank runs the same number of steps, so
-        the per-step gradient all-reduces pair up) and the shuffle draws from
-        its own generator seeded with ``seed + epoch`` -- not the global CPU
-        RNG, which ranks seed differently (``SEED + rank``).  One rank keeps
-        the reference's global-RNG shuffle (``data.py:177-184``)."""
+        With ``world_size > 1`` the shuffle draws from its own generator seeded
+        with ``seed + epoch`` -- not the global CPU RNG, which ranks seed
+        differently (``SEED + rank``) -- and, for a training loader
+        (``even``), the plan is cut to a multiple of ``world_size`` batches
+        (every rank runs the same number of steps, so the per-step gradient
+        all-reduces pair up).  An evaluation loader (``even=False``) keeps
+        every batch: its ranks may get one batch more or less, and the
+        trainer reduces the figures over the ranks once per epoch.  One rank
+        keeps the reference's global-RNG shuffle (``data.py:177-184``).
+
+        ``resident``: the first epoch's batches stay on the device and every
+        later epoch yields the same batch objects in the same order (no
+        reshuffle) -- an evaluation set kept in HBM, whose per-batch graphs
+        the trainer captures once and replays."""
         if not 0 <= rank < world_size:
             raise ValueError("need 0 <= rank < world_size")
         if world_size > 1 and seed is None:
@@ -78,11 +87,16 @@ class GraphLoader:
         self.device = torch.device(device) if device is not None else None
         self.prefetch = max(1, int(prefetch))
         self.threads = threads
+        self.even = bool(even)
+        self.resident = bool(resident)
+        self._resident_batches: Optional[List[Tuple[GraphBatch, GraphBatch]]] = None
 
     def __len__(self) -> int:
         n = len(self.indices)
         total = n // self.batch_size if self.drop_last else (n + self.batch_size - 1) // self.batch_size
-        return total // self.world_size
+        if self.even:
+            return total // self.world_size
+        return len(range(self.rank, total, self.world_size))
 
     def batches(self, epoch: Optional[int] = None) -> List[List[int]]:
         """This rank's building indices per batch for ``epoch`` (default: the
@@ -96,21 +110,31 @@ class GraphLoader:
         dl = DataLoader(_Indices(self.indices), batch_size=self.batch_size, shuffle=self.shuffle,
                         drop_last=self.drop_last, collate_fn=_as_list, num_workers=0, generator=gen)
         plan = list(iter(dl))
-        plan = plan[:len(plan) - len(plan) % self.world_size]
+        if self.even:
+            plan = plan[:len(plan) - len(plan) % self.world_size]
         return plan[self.rank::self.world_size]
 
     def set_epoch(self, epoch: int) -> None:
         self.epoch = int(epoch)
 
     def __iter__(self) -> Iterator[Tuple[GraphBatch, GraphBatch]]:
+        if self._resident_batches is not None:
+            yield from self._resident_batches
+            return
         plan = self.batches()
         self.epoch += 1
         dev = self.device
+        kept = [] if self.resident else None
         if dev is None or dev.type != "cuda":
-            for idx in plan:
-                yield self.store.collate(idx, pin=False, threads=self.threads)
-            return
-        yield from _prefetched(self.store, plan, dev, self.prefetch, self.threads)
+            it = (self.store.collate(idx, pin=False, threads=self.threads) for idx in plan)
+        else:
+            it = _prefetched(self.store, plan, dev, self.prefetch, self.threads)
+        for pair in it:
+            if kept is not None:
+                kept.append(pair)
+            yield pair
+        if kept is not None:
+            self._resident_batches = kept
 
 
 def _prefetched(store: GraphStore, plan: List[List[int]], dev: torch.device, depth: int, threads: int):
@@ -175,7 +199,11 @@ class GraphDataLoaders:
     the reference (``data.py:166-212``) over a GraphStore."""
 
     def __init__(self, configuration, store: GraphStore, device=None, prefetch: int = 2, rank: int = 0,
-                 world_size: int = 1):
+                 world_size: int = 1, resident_eval: bool = False):
+        """``resident_eval``: the validation / test batches are collated once
+        and kept on the device (no per-epoch reshuffle), so the trainer replays
+        their captured evaluation graphs; the reference reshuffles them every
+        epoch (``data.py:186-210``), the default here too."""
         self.configuration = configuration
         self.sanity_checking = bool(getattr(configuration, "SANITY_CHECKING", False))
         self.dataset = store
@@ -190,7 +218,8 @@ class GraphDataLoaders:
         kw = dict(batch_size=configuration.BATCH_SIZE, shuffle=True, drop_last=False, device=device,
                   prefetch=prefetch, rank=rank, world_size=world_size, seed=seed)
         self.train_dataloader = GraphLoader(store, [indices[i] for i in parts[0].indices], **kw)
+        ev = dict(kw, even=False, resident=bool(resident_eval))  # evaluation: every batch, reduced over ranks
         self.validation_dataloader = None if self.sanity_checking else \
-            GraphLoader(store, [indices[i] for i in parts[1].indices], **kw)
+            GraphLoader(store, [indices[i] for i in parts[1].indices], **ev)
         self.test_dataloader = None if self.sanity_checking else \
-            GraphLoader(store, [indices[i] for i in parts[2].indices], **kw)
+            GraphLoader(store, [indices[i] for i in parts[2].indices], **ev)

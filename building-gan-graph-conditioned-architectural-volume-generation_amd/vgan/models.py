@@ -222,14 +222,18 @@ class VoxelGNNGenerator(nn.Module):
         mods = list(self.decoder.children())[3:]
         return run_blocks(mods, d)
 
-    def forward(self, local_graph, voxel_graph, z, noise: Optional[torch.Tensor] = None):
+    def forward(self, local_graph, voxel_graph, z, noise: Optional[torch.Tensor] = None,
+                stacked: Optional[bool] = None):
         """z [1, N, Z] (the reference's shape) -> ([N, 7] x 3).  z [k, N, Z]
         with k > 1 draws k independent samples in ONE stacked forward (the
         critic iterations' generator passes, or an inference sweep) and
-        returns [k, N, 7] tensors; the program-feature encoder runs once."""
+        returns [k, N, 7] tensors; the program-feature encoder runs once.
+        ``stacked=True`` takes that no-grad path (multi-source first layers,
+        no concatenation) at k = 1 too, returning [1, N, 7] tensors."""
         prep = vdata.prepared(local_graph, voxel_graph, self.configuration.NUM_CLASSES)
         k = z.shape[0] if z.dim() == 3 else 1
-        if k > 1 and not torch.is_grad_enabled() and prep.voxel_x.is_cuda:
+        use_stacked = k > 1 if stacked is None else bool(stacked)
+        if use_stacked and not torch.is_grad_enabled() and prep.voxel_x.is_cuda:
             logits = self._forward_stacked_nograd(prep, z, k)
             if logits is not None:
                 n = prep.voxel_x.shape[0]

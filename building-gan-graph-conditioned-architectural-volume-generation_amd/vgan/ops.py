@@ -72,10 +72,12 @@ class CSR:
 
     @classmethod
     def from_arrays(cls, row_ptr: torch.Tensor, col: torch.Tensor, csc_ptr: torch.Tensor, csc_slot: torch.Tensor,
-                    csc_dst: torch.Tensor) -> "CSR":
+                    csc_dst: torch.Tensor, max_degree: Optional[int] = None) -> "CSR":
         """The same structure from arrays built elsewhere -- the host collate of
         ``vgan.store`` emits them in csr.hip's order -- with no device build and
-        no host sync."""
+        no host sync.  ``max_degree`` (the largest row length, known to the
+        host collate) sizes the padded column array (``ell``) without reading
+        row_ptr back."""
         for t in (row_ptr, col, csc_ptr, csc_slot, csc_dst):
             if not t.is_cuda or t.dtype != torch.int32 or t.dim() != 1:
                 raise ValueError("CSR arrays must be int32 vectors on a ROCm device")
@@ -87,6 +89,8 @@ class CSR:
         self.row_ptr, self.col = row_ptr, col
         self.csc_ptr, self.csc_slot, self.csc_dst = csc_ptr, csc_slot, csc_dst
         self.device = row_ptr.device
+        if max_degree is not None:
+            self._ell_w = next((x for x in ELL_WIDTHS if int(max_degree) <= x), 0)
         return self
 
     def stream(self):
@@ -97,6 +101,8 @@ class CSR:
         edge slots offset per copy): several forwards over the same batch run
         as one (the critic engine's real / fake / mix discriminator passes).
         Cached; built with a few device ops, no host sync."""
+        if copies == 1:
+            return self
         cache = self.__dict__.setdefault("_stacked", {})
         if copies in cache:
             return cache[copies]

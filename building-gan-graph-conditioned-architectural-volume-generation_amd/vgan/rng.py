@@ -61,11 +61,26 @@ class RNG:
         for t in self._iters.values():
             t.add_(1)
 
+    def state_dict(self) -> Dict[str, int]:
+        """Seed and device iteration counter (device mode): a resumed run
+        continues the same stream of z / dropout / Gumbel / eps draws."""
+        iters = [int(t.item()) for t in self._iters.values()]
+        return {"mode": self.mode, "seed": int(self.seed), "iter": max(iters) if iters else 0}
+
+    def load_state_dict(self, state: Dict[str, int]) -> None:
+        if state.get("mode") != self.mode:
+            return  # another randomness source: nothing to continue
+        self.seed = int(state["seed"])
+        self._pending_iter = int(state["iter"])
+        for t in self._iters.values():
+            t.fill_(self._pending_iter)
+
     def _iter(self, device) -> torch.Tensor:
         device = torch.device(device)
         t = self._iters.get(device)
         if t is None:
-            t = self._iters[device] = torch.zeros(1, dtype=torch.int64, device=device)
+            t = self._iters[device] = torch.full((1,), getattr(self, "_pending_iter", 0), dtype=torch.int64,
+                                                 device=device)
         return t
 
     def _fixed_draw(self, kind: str, shape, device, make):

@@ -255,6 +255,10 @@ class GraphStore:
         gb.set_derived("ptr_host", [int(v) for v in ptr.tolist()])
         if csr is not None:
             gb.set_derived("csr_arrays", csr)
+            # the largest in-degree (self loop included) from the host row_ptr:
+            # the device side sizes its padded column array (CSR.ell) without a sync
+            rp = csr[0].numpy()
+            gb.set_derived("csr_max_degree", int(np.diff(rp).max()) if rp.size > 1 else 0)
         return gb
 
     def collate(self, indices: Sequence[int], pin: bool = False, threads: int = 4) -> Tuple[GraphBatch, GraphBatch]:

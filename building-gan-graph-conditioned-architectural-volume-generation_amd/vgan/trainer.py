@@ -87,7 +87,15 @@ class Trainer:
         use_engine = (runtime.get("critic", "engine") == "engine" and getattr(configuration, "USE_WGANGP", True)
                       and int(configuration.NUM_CLASSES) <= 32)
         self.critic = CriticEngine(discriminator, configuration) if use_engine else None
-        self.states = {"epoch_start": 1, "best_f1_score": 0.0}
+        self.states = {"epoch_start": 1, "epoch_end": int(configuration.EPOCHS) + 1, "best_f1_score": 0}
+        # resume (trainer.py:628-636): a states.pt in log_dir -- written by this
+        # trainer or by the reference's -- restores models, optimizers, scheduler
+        if os.path.exists(self._states_path()):
+            self.load_states(torch.load(self._states_path(), map_location="cpu", weights_only=True))
+            if self.rank == 0:
+                print(f"Loaded states from {self.log_dir}")
+            self.sync.broadcast_params(self.flat_g)
+            self.sync.broadcast_params(self.flat_d)
         # captured step graphs are cached on the batch, per trainer (two
         # trainers -- e.g. f32 and bf16 -- may step the same batch)
         self._graph_key = f"step_graphs:{next(_TRAINER_IDS)}"
@@ -238,28 +246,42 @@ class Trainer:
         return {"d_losses": torch.stack(d_losses), "g_loss": g_loss.detach(), "label_hard": hard.detach()}
 
     # ------------------------------------------------- hipGraph-captured step
-    def _critic_body(self, local_graph, voxel_graph, acc, with_adam: bool, labels=None, i: int = 0):
+    def _critic_body(self, local_graph, voxel_graph, acc, with_adam: bool, labels=None, i: int = 0,
+                     sync: bool = False):
+        """One critic iteration; its loss goes to acc[i].  ``sync``: the flat
+        D gradient is averaged over the ranks (RCCL, recorded in the graph)
+        before Adam."""
         d_loss = self._critic_iteration(local_graph, voxel_graph, labels, i)
-        acc[0].add_(d_loss.detach())
+        acc[i].copy_(d_loss.detach())
+        if sync:
+            self.sync.all_reduce_grad(self.flat_d)
         if with_adam:
             self.adam_d.step()
 
-    def _gen_body(self, local_graph, voxel_graph, acc, with_adam: bool):
+    def _gen_body(self, local_graph, voxel_graph, acc, with_adam: bool, sync: bool = False):
+        """The generator iteration; its loss goes to acc[-1]."""
         g_loss, hard = self._gen_iteration(local_graph, voxel_graph)
-        acc[1].copy_(g_loss.detach())
+        acc[-1].copy_(g_loss.detach())
+        if sync:
+            self.sync.all_reduce_grad(self.flat_g)
         if with_adam:
             self.adam_g.step()
         return hard.detach()
 
+    def _state_tensors(self):
+        """Everything a step advances in place: parameters, Adam state and the
+        device RNG's iteration counters."""
+        return [self.flat_g.param, self.flat_d.param, self.adam_g.exp_avg, self.adam_g.exp_avg_sq,
+                self.adam_d.exp_avg, self.adam_d.exp_avg_sq, self.adam_g.step_t, self.adam_d.step_t,
+                *getattr(self.rng, "_iters", {}).values()]
+
     def _snapshot(self):
-        return [t.clone() for t in (self.flat_g.param, self.flat_d.param, self.adam_g.exp_avg, self.adam_g.exp_avg_sq,
-                                    self.adam_d.exp_avg, self.adam_d.exp_avg_sq, self.adam_g.step_t,
-                                    self.adam_d.step_t)]
+        return [t.clone() for t in self._state_tensors()]
 
     def _restore(self, snap):
-        dst = (self.flat_g.param, self.flat_d.param, self.adam_g.exp_avg, self.adam_g.exp_avg_sq,
-               self.adam_d.exp_avg, self.adam_d.exp_avg_sq, self.adam_g.step_t, self.adam_d.step_t)
-        for d, s_ in zip(dst, snap):
+        """Undo a capture's warm-up: the captured step then draws exactly what
+        the eager step would from the same state."""
+        for d, s_ in zip(self._state_tensors(), snap):
             d.copy_(s_)
 
     def capture(self, local_graph, voxel_graph):
@@ -275,25 +297,31 @@ class Trainer:
         * otherwise: one critic-iteration graph replayed N_CRITIC times and the
           generator graph.
         RNG counters, parameters and Adam state advance in place on the device.
-        With several ranks the RCCL all-reduce and Adam run eagerly between
-        replays.  Needs device-side randomness (device or fixed RNG)."""
+        With several ranks over RCCL the flat-gradient all-reduce is recorded
+        in each iteration's graph between its backward and its Adam step (no
+        host round trip between replays); over gloo (host collectives, the CPU
+        tests) the all-reduce and Adam run eagerly between replays.  Needs
+        device-side randomness (device or fixed RNG)."""
         if self.rng.mode == "host":
             raise RuntimeError("graph capture needs device-side randomness (runtime['rng'] 'device')")
         dev = voxel_graph.x.device
         n_critic = self.configuration.N_CRITIC
-        with_adam = not self.sync.active
+        sync = self.sync.active and self.sync.capturable
+        with_adam = not self.sync.active or sync
         stacked = self._stacked_labels()
-        acc = torch.zeros(2, dtype=torch.float32, device=dev)
+        acc = torch.zeros(n_critic + 1, dtype=torch.float32, device=dev)
         vdata.prepared(local_graph, voxel_graph, self.configuration.NUM_CLASSES)  # CSR etc. before capture
         self.adam_g.sync_lr()
         self.adam_d.sync_lr()
+        if callable(getattr(self.rng, "_iter", None)):
+            self.rng._iter(dev)  # the counter exists before the snapshot
         snap = self._snapshot()
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):  # warm-up (lazy init) on a side stream, then undo it
             labels = self._critic_labels(local_graph, voxel_graph) if stacked else None
-            self._critic_body(local_graph, voxel_graph, acc, with_adam, labels, 0)
-            self._gen_body(local_graph, voxel_graph, acc, with_adam)
+            self._critic_body(local_graph, voxel_graph, acc, with_adam, labels, 0, sync)
+            self._gen_body(local_graph, voxel_graph, acc, with_adam, sync)
         torch.cuda.current_stream(dev).wait_stream(side)
         self._restore(snap)
         pool = getattr(self, "_graph_pool", None)
@@ -308,141 +336,358 @@ class Trainer:
         for i in range(n_critic if stacked else 1):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool):
-                self._critic_body(local_graph, voxel_graph, acc, with_adam, labels, i)
+                self._critic_body(local_graph, voxel_graph, acc, with_adam, labels, i, sync)
             critic.append(g)
         g_gen = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g_gen, pool=pool):
-            hard = self._gen_body(local_graph, voxel_graph, acc, with_adam)
+            hard = self._gen_body(local_graph, voxel_graph, acc, with_adam, sync)
         self._restore(snap)
         graphs = {"labels": g_labels, "label_tensors": labels, "critic": critic, "gen": g_gen, "acc": acc,
-                  "hard": hard, "with_adam": with_adam}
+                  "hard": hard, "with_adam": with_adam, "sync_in_graph": sync}
         voxel_graph.set_derived(self._graph_key, graphs)
         return graphs
 
     def step_graphed(self, local_graph, voxel_graph) -> Dict[str, torch.Tensor]:
-        """``step`` replayed from hipGraphs (captured on first use per batch)."""
+        """``step`` replayed from hipGraphs (captured on first use per batch).
+        The returned tensors are the graphs' static outputs: valid until the
+        next replay of this batch (clone to keep)."""
         graphs = voxel_graph.derived(self._graph_key) if callable(getattr(voxel_graph, "derived", None)) else None
         if graphs is None:
             graphs = self.capture(local_graph, voxel_graph)
         self.adam_g.sync_lr()
         self.adam_d.sync_lr()
         acc = graphs["acc"]
-        acc.zero_()
+        n_critic = self.configuration.N_CRITIC
         if graphs["labels"] is not None:
             graphs["labels"].replay()
         critic = graphs["critic"]
-        for i in range(self.configuration.N_CRITIC):
-            critic[i if len(critic) > 1 else 0].replay()
+        single = len(critic) == 1 and n_critic > 1  # one graph replayed: its loss slot is acc[0]
+        for i in range(n_critic):
+            critic[0 if single else i].replay()
+            if single:  # iteration 0's loss waits in the generator's slot
+                (acc[n_critic] if i == 0 else acc[i]).copy_(acc[0])
             if not graphs["with_adam"]:
                 self.sync.all_reduce_grad(self.flat_d)
                 self.adam_d.step()
+        if single:
+            acc[0].copy_(acc[n_critic])
         graphs["gen"].replay()
         if not graphs["with_adam"]:
             self.sync.all_reduce_grad(self.flat_g)
             self.adam_g.step()
-        return {"d_loss_mean": acc[0] / self.configuration.N_CRITIC, "g_loss": acc[1], "label_hard": graphs["hard"]}
+        return {"d_losses": acc[:n_critic], "d_loss_mean": acc[:n_critic].mean(), "g_loss": acc[n_critic],
+                "label_hard": graphs["hard"]}
+
 
     # ------------------------------------------------------ orchestration
+    # The epoch loop of trainer.py:445-520 (train), :522-577 (validation),
+    # :641-747 (epochs, checkpoint) and :749-806 (test).  Per batch only device
+    # work is enqueued -- the step, the confusion counts, the losses -- and the
+    # figures are read back once per epoch, so the host keeps queueing ahead of
+    # the GPU.  With several ranks every epoch figure is reduced over the ranks
+    # (sums and minima), so all ranks report, and decide on, the same numbers.
+
+    def _train_mode(self) -> str:
+        """runtime['train_step']: "eager" (``step``), "graphed" (``step_graphed``,
+        a capture per new batch) or "auto" (default: eager on a batch seen for
+        the first time, captured when a batch object comes back -- a resident
+        dataset -- and replayed from then on)."""
+        mode = getattr(self.configuration, "runtime", {}).get("train_step", "auto")
+        if mode not in ("eager", "graphed", "auto"):
+            raise ValueError(f"runtime['train_step'] must be 'eager', 'graphed' or 'auto', not {mode!r}")
+        return "eager" if self.rng.mode == "host" else mode  # host draws cannot be replayed
+
+    def _train_batch(self, local_graph, voxel_graph) -> Dict[str, torch.Tensor]:
+        """One step on a batch, by ``_train_mode``; the returned losses are
+        this step's own (clones of a replay's static outputs)."""
+        mode = self._train_mode()
+        getter = getattr(voxel_graph, "derived", None)
+        if mode == "auto" and callable(getter) and voxel_graph.x.is_cuda:
+            seen_key = self._graph_key + ":seen"
+            if getter(self._graph_key) is None and not getter(seen_key):
+                voxel_graph.set_derived(seen_key, True)
+                mode = "eager"
+            else:
+                mode = "graphed"
+        if mode == "graphed" and callable(getter):
+            out = self.step_graphed(local_graph, voxel_graph)
+            return {"d_losses": out["d_losses"].clone(), "g_loss": out["g_loss"].clone(),
+                    "label_hard": out["label_hard"]}
+        return self.step(local_graph, voxel_graph)
+
+    def _to_device(self, local_graph, voxel_graph):
+        local_graph = local_graph.to(self.configuration.DEVICE)
+        voxel_graph = voxel_graph.to(self.configuration.DEVICE)
+        assert [set(d) for d in local_graph.data_number] == [set(d) for d in voxel_graph.data_number]
+        return local_graph, voxel_graph
+
+    @staticmethod
+    def _read_confusions(confs):
+        """One device-to-host copy for an epoch's confusion counts: per batch
+        (per-building [G, K, K], whole batch [K, K]) -> the metric tuples of
+        trainer.py:443."""
+        if not confs:
+            return []
+        sizes = [c.shape[0] for c, _ in confs]
+        per_graph = torch.cat([c for c, _ in confs]).cpu().numpy()
+        whole = torch.stack([a for _, a in confs]).cpu().numpy()
+        out, lo = [], 0
+        for b, g in enumerate(sizes):
+            out.append(vmetrics.batch_metrics(per_graph[lo:lo + g], whole[b]))
+            lo += g
+        return out
+
+    def _epoch_figures(self, metrics, losses):
+        """Means over the epoch's batches (losses over every recorded value) and
+        the minimum per-building F1.  One rank: the reference's own reductions
+        (``torch.tensor(list).mean().item()`` -- float32 -- and ``min``).
+        Several ranks: float64 sums and counts reduced over the ranks, and the
+        minimum reduced with MIN, so every rank gets the global figures."""
+        f1s = [m[0] for m in metrics]
+        per_graph = [v for m in metrics for v in m[1]]
+        cols = [f1s, [m[2] for m in metrics], [m[3] for m in metrics], [m[4] for m in metrics]]
+        if not self.sync.active:
+            mean = lambda v: torch.tensor(v).mean().item() if len(v) else 0.0  # noqa: E731
+            loss_means = [torch.cat([t.reshape(-1) for t in l]).mean().item() if l else 0.0 for l in losses]
+            return loss_means, [mean(c) for c in cols], (min(per_graph) if per_graph else 0.0)
+        flat_losses = [torch.cat([t.reshape(-1) for t in l]).double().cpu() if l else torch.zeros(0, dtype=torch.float64)
+                       for l in losses]
+        sums = self.sync.reduce_host([float(v.sum()) for v in flat_losses] + [float(v.numel()) for v in flat_losses]
+                                     + [float(sum(c)) for c in cols] + [float(len(f1s))])
+        nl = len(losses)
+        loss_means = [s / c if c else 0.0 for s, c in zip(sums[:nl], sums[nl:2 * nl])]
+        nb = sums[-1]
+        means = [s / nb if nb else 0.0 for s in sums[2 * nl:2 * nl + len(cols)]]
+        lo = self.sync.reduce_host([min(per_graph) if per_graph else float("inf")], op="min")[0]
+        return loss_means, means, (lo if lo != float("inf") else 0.0)
+
     def _train_each_epoch(self):
+        """trainer.py:445-520 -> (g_loss, d_loss, f1, min per-building f1,
+        precision, recall, accuracy)."""
         start = time.time()
-        g_losses, d_losses, f1s, f1_graphs, precs, recs, accs = [], [], [], [], [], [], []
+        g_losses, d_losses, confs = [], [], []
         for local_graph, voxel_graph in self.dataloaders.train_dataloader:
-            local_graph = local_graph.to(self.configuration.DEVICE)
-            voxel_graph = voxel_graph.to(self.configuration.DEVICE)
-            assert [set(d) for d in local_graph.data_number] == [set(d) for d in voxel_graph.data_number]
-            out = self.step(local_graph, voxel_graph)
+            local_graph, voxel_graph = self._to_device(local_graph, voxel_graph)
+            out = self._train_batch(local_graph, voxel_graph)
             d_losses.append(out["d_losses"])
             g_losses.append(out["g_loss"])
-            f1, per_graph, prec, rec, acc = self._compute_metrics(voxel_graph, out["label_hard"])
-            f1s.append(f1)
-            f1_graphs.extend(per_graph)
-            precs.append(prec)
-            recs.append(rec)
-            accs.append(acc)
-        # epoch means of the losses averaged over the data-parallel ranks (one
-        # collective per epoch); the F1 / precision / recall are this rank's
-        means = self.sync.all_reduce_scalars(torch.stack([torch.stack(g_losses).mean(), torch.cat(d_losses).mean()]))
-        g_mean, d_mean = (float(v) for v in means.tolist())
+            confs.append(ops.confusion(voxel_graph.type, out["label_hard"].squeeze(0), voxel_graph.ptr))
+        metrics = self._read_confusions(confs)
+        (g_mean, d_mean), (f1, prec, rec, acc), f1_min = self._epoch_figures(metrics, [g_losses, d_losses])
         print(f"The function _train_each_epoch took {time.time() - start} seconds to run.")
-        return (g_mean, d_mean, float(np.mean(f1s)), min(f1_graphs), float(np.mean(precs)), float(np.mean(recs)),
-                float(np.mean(accs)))
+        return g_mean, d_mean, f1, f1_min, prec, rec, acc
 
-    @torch.no_grad()
-    def _validate_each_epoch(self):
-        if self.sanity_checking or getattr(self.dataloaders, "validation_dataloader", None) is None:
-            return 0.0, 0.0, 0.0, 0.0, 0.0, 0.0
+    # ------------------------------------------------------ evaluation
+    def _eval_forward(self):
+        fwd = getattr(self, "_eval_sweep", None)
+        if fwd is None:
+            from .infer import InferenceSweep
+
+            fwd = self._eval_sweep = InferenceSweep(self.generator, [float(self.generator.tau)])
+        return fwd
+
+    def _eval_body(self, local_graph, voxel_graph, with_loss: bool):
+        """Generator sample + (optionally) its generator loss + confusion
+        counts of one evaluation batch (trainer.py:545-553 / :769-774): the
+        no-grad stacked forward of the inference sweep (vgan.infer)."""
+        logits, hard = self._eval_forward().generate(local_graph, voxel_graph)
+        loss = self._compute_generator_loss(local_graph, voxel_graph, logits, hard.unsqueeze(0)) if with_loss \
+            else torch.zeros((), device=logits.device)
+        conf, conf_all = ops.confusion(voxel_graph.type, hard, voxel_graph.ptr)
+        return loss, conf, conf_all, hard
+
+    def _eval_batch(self, local_graph, voxel_graph, with_loss: bool):
+        """``_eval_body``, eager on a batch's first visit; a batch object that
+        comes back (a resident evaluation set: every epoch's validation) is
+        captured as one hipGraph on its second visit and replayed from then
+        on.  Returns (loss, conf, conf_all) owned by the caller;
+        ``self.eval_record`` (a list, tests) also receives (voxel_graph, a copy
+        of the sampled labels)."""
+        out = self._eval_outputs(local_graph, voxel_graph, with_loss)
+        if getattr(self, "eval_record", None) is not None:
+            self.eval_record.append((voxel_graph, out[3].clone()))
+        return out[:3]
+
+    def _eval_outputs(self, local_graph, voxel_graph, with_loss: bool):
+        getter = getattr(voxel_graph, "derived", None)
+        if self.rng.mode == "host" or not callable(getter) or not voxel_graph.x.is_cuda:
+            return self._eval_body(local_graph, voxel_graph, with_loss)
+        key = f"{self._graph_key}:eval:{int(with_loss)}"
+        cached = getter(key)
+        if cached is None:
+            voxel_graph.set_derived(key, "seen")
+            return self._eval_body(local_graph, voxel_graph, with_loss)
+        if cached == "seen":
+            dev = voxel_graph.x.device
+            pool = getattr(self, "_eval_pool", None)
+            if pool is None:
+                pool = self._eval_pool = torch.cuda.graph_pool_handle()
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):  # lazy allocations outside the capture
+                self._eval_body(local_graph, voxel_graph, with_loss)
+            torch.cuda.current_stream(dev).wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                outs = self._eval_body(local_graph, voxel_graph, with_loss)
+            cached = (g, outs)
+            voxel_graph.set_derived(key, cached)
+        cached[0].replay()
+        loss, conf, conf_all, hard = cached[1]
+        return loss.clone(), conf.clone(), conf_all.clone(), hard  # hard: valid until the next replay
+
+    def _evaluate(self, loader, with_loss: bool):
+        losses, confs = [], []
         self.generator.eval()
         self.discriminator.eval()
-        g_losses, f1s, f1_graphs, precs, recs, accs = [], [], [], [], [], []
-        for local_graph, voxel_graph in self.dataloaders.validation_dataloader:
-            local_graph = local_graph.to(self.configuration.DEVICE)
-            voxel_graph = voxel_graph.to(self.configuration.DEVICE)
-            with gemm_precision_scope(self.precision):
-                logits, hard, _ = self._generate(local_graph, voxel_graph)
-            g_losses.append(self._compute_generator_loss(local_graph, voxel_graph, logits, hard))
-            f1, per_graph, prec, rec, acc = self._compute_metrics(voxel_graph, hard)
-            f1s.append(f1)
-            f1_graphs.extend(per_graph)
-            precs.append(prec)
-            recs.append(rec)
-            accs.append(acc)
-        self.generator.train()
-        self.discriminator.train()
-        return (torch.stack(g_losses).mean().item(), float(np.mean(f1s)), min(f1_graphs), float(np.mean(precs)),
-                float(np.mean(recs)), float(np.mean(accs)))
+        try:
+            with torch.no_grad(), gemm_precision_scope(self.precision):
+                for local_graph, voxel_graph in loader:
+                    local_graph, voxel_graph = self._to_device(local_graph, voxel_graph)
+                    loss, conf, conf_all = self._eval_batch(local_graph, voxel_graph, with_loss)
+                    losses.append(loss)
+                    confs.append((conf, conf_all))
+        finally:
+            self.generator.train()
+            self.discriminator.train()
+        metrics = self._read_confusions(confs)
+        return self._epoch_figures(metrics, [losses] if with_loss else [])
+
+    def _validate_each_epoch(self):
+        """trainer.py:522-577 -> (g_loss, f1, min per-building f1, precision,
+        recall, accuracy).  Sanity mode returns six zeros (the reference returns
+        five and then fails to unpack them, trainer.py:526,666-673)."""
+        if self.sanity_checking or getattr(self.dataloaders, "validation_dataloader", None) is None:
+            return 0.0, 0.0, 0.0, 0.0, 0.0, 0.0
+        start = time.time()
+        (g_mean,), (f1, prec, rec, acc), f1_min = self._evaluate(self.dataloaders.validation_dataloader, True)
+        print(f"The function _validate_each_epoch took {time.time() - start} seconds to run.")
+        return g_mean, f1, f1_min, prec, rec, acc
+
+    def test(self, num_samples_to_viz: int = 0):
+        """trainer.py:749-795: test-split metrics (the qualitative figures of
+        :797-803 are out of scope)."""
+        _, (f1, prec, rec, acc), f1_min = self._evaluate(self.dataloaders.test_dataloader, False)
+        result = {"f1_score_test": f1, "f1_score_min_test": f1_min, "precision_score_test": prec,
+                  "recall_score_test": rec, "accuracy_score_test": acc}
+        if self.rank == 0:
+            print("\n".join(f"{k}: {v}" for k, v in result.items()))
+        return result
+
+    # ------------------------------------------------------ epochs, checkpoint
+    def _set_epoch(self, epoch: int) -> None:
+        """Per-epoch shuffle of a data-parallel loader (like
+        DistributedSampler.set_epoch): a resumed run continues the epochs'
+        shuffles instead of repeating epoch 0's."""
+        for name in ("train_dataloader", "validation_dataloader", "test_dataloader"):
+            ld = getattr(self.dataloaders, name, None)
+            if ld is not None and callable(getattr(ld, "set_epoch", None)):
+                ld.set_epoch(epoch)
 
     def train(self):
-        """Epoch loop of trainer.py:641-747 (metrics printed; checkpoint on best
-        weighted min-F1 with the reference's states.pt keys)."""
+        """trainer.py:641-747: per epoch train + validate, the weighted min-F1
+        score, a checkpoint (states.pt, the reference's keys) on a new best and
+        an epoch_start bump otherwise, then the scheduler step.  Returns the
+        per-epoch figures."""
         cfg = self.configuration
-        best = self.states["best_f1_score"]
-        for epoch in range(self.states["epoch_start"], cfg.EPOCHS + 1):
+        epoch_start = int(self.states["epoch_start"])
+        epoch_end = int(cfg.EPOCHS) + 1
+        best = float(self.states["best_f1_score"])
+        history = []
+        for epoch in range(epoch_start, epoch_end):
+            self._set_epoch(epoch)
             tr = self._train_each_epoch()
             va = self._validate_each_epoch()
             score = tr[3] * cfg.F1_SCORE_TRAIN_WEIGHT + va[2] * cfg.F1_SCORE_VALIDATION_WEIGHT
-            print(f"epoch {epoch}: g_loss {tr[0]:.5f} d_loss {tr[1]:.5f} f1 {tr[2]:.4f} f1_val {va[1]:.4f}")
+            figures = {"epoch": epoch, "g_loss_train": tr[0], "d_loss_train": tr[1], "f1_score_train": tr[2],
+                       "f1_score_min_train": tr[3], "precision_score_train": tr[4], "recall_score_train": tr[5],
+                       "accuracy_score_train": tr[6], "g_loss_validation": va[0], "f1_score_validation": va[1],
+                       "f1_score_min_validation": va[2], "precision_score_validation": va[3],
+                       "recall_score_validation": va[4], "accuracy_score_validation": va[5],
+                       "f1_score_min_weightedsum": score}
+            history.append(figures)
+            if self.rank == 0:
+                print(f"epoch {epoch}: g_loss {tr[0]:.5f} d_loss {tr[1]:.5f} f1 {tr[2]:.4f} "
+                      f"f1_val {va[1]:.4f} score {score:.4f}")
             if best < score:
+                if self.rank == 0:
+                    print(f"Best f1 score updated: {best} -> {score}")
                 best = score
                 if not self.sanity_checking:
-                    self.save_checkpoint(epoch, best)
+                    self.save_checkpoint(epoch, best, figures)
+            elif not self.sanity_checking:
+                self._bump_epoch_start(epoch)
             if self.scheduler_generator is not None:
                 self.scheduler_generator.step()
+        return history
 
-    def save_checkpoint(self, epoch: int, best: float) -> str:
-        os.makedirs(self.log_dir, exist_ok=True)
-        path = os.path.join(self.log_dir, "states.pt")
-        torch.save({
-            "epoch_start": epoch,
-            "epoch_end": self.configuration.EPOCHS + 1,
-            "best_f1_score": best,
+    def _states_path(self) -> str:
+        return os.path.join(self.log_dir, "states.pt")
+
+    def checkpoint_states(self, epoch: int, best: float, figures: Optional[Dict[str, float]] = None) -> Dict:
+        """The states.pt dictionary of trainer.py:715-736: the reference's keys,
+        the models' state_dicts and torch.optim.Adam / scheduler state_dicts
+        (the flat Adam moments written back into the caller's optimizers), so
+        the reference trainer resumes from it and vice versa."""
+        figures = figures or {}
+        self.adam_g.export_to(self.optimizer_generator)
+        self.adam_d.export_to(self.optimizer_discriminator)
+        opt_g = self.optimizer_generator if self.optimizer_generator is not None else self.adam_g
+        opt_d = self.optimizer_discriminator if self.optimizer_discriminator is not None else self.adam_d
+        states = {"epoch_start": epoch, "epoch_end": int(self.configuration.EPOCHS) + 1, "best_f1_score": best}
+        for key in ("f1_score_train", "f1_score_validation", "f1_score_min_train", "f1_score_min_validation",
+                    "f1_score_min_weightedsum", "recall_score_train", "recall_score_validation",
+                    "accuracy_score_train", "accuracy_score_validation"):
+            states[key] = figures.get(key, 0)
+        states.update({
             "generator": self.generator.state_dict(),
             "discriminator": self.discriminator.state_dict(),
-            "optimizer_generator_flat": self.adam_g.state_dict_flat(),
-            "optimizer_discriminator_flat": self.adam_d.state_dict_flat(),
-        }, path)
+            "optimizer_generator": opt_g.state_dict(),
+            "optimizer_discriminator": opt_d.state_dict(),
+            "scheduler_generator": self.scheduler_generator.state_dict() if self.scheduler_generator is not None
+            else None,
+        })
+        # not a reference key (its loader ignores it): the device draw stream,
+        # with the rank term taken out of the seed, so a resumed run continues it
+        rng = self.rng.state_dict()
+        rng["seed"] -= 7919 * self.rank
+        states["vgan_rng"] = rng
+        return states
+
+    def save_checkpoint(self, epoch: int, best: float, figures: Optional[Dict[str, float]] = None) -> str:
+        """Write states.pt (rank 0 only; the ranks hold identical parameters)."""
+        path = self._states_path()
+        states = self.checkpoint_states(epoch, best, figures)
+        if self.rank == 0:
+            os.makedirs(self.log_dir, exist_ok=True)
+            torch.save(states, path)
+        self.states = states
         return path
 
-    @torch.no_grad()
-    def test(self, num_samples_to_viz: int = 0):
-        """trainer.py:749-795 metrics (visualisation is out of scope)."""
-        self.generator.eval()
-        self.discriminator.eval()
-        f1s, f1_graphs, precs, recs, accs = [], [], [], [], []
-        for local_graph, voxel_graph in self.dataloaders.test_dataloader:
-            local_graph = local_graph.to(self.configuration.DEVICE)
-            voxel_graph = voxel_graph.to(self.configuration.DEVICE)
-            with gemm_precision_scope(self.precision):
-                _, hard, _ = self._generate(local_graph, voxel_graph)
-            f1, per_graph, prec, rec, acc = self._compute_metrics(voxel_graph, hard)
-            f1s.append(f1)
-            f1_graphs.extend(per_graph)
-            precs.append(prec)
-            recs.append(rec)
-            accs.append(acc)
-        self.generator.train()
-        self.discriminator.train()
-        result = {"f1_score_test": float(np.mean(f1s)), "f1_score_min_test": min(f1_graphs),
-                  "precision_score_test": float(np.mean(precs)), "recall_score_test": float(np.mean(recs)),
-                  "accuracy_score_test": float(np.mean(accs))}
-        print(result)
-        return result
+    def _bump_epoch_start(self, epoch: int) -> None:
+        """trainer.py:742-745: a non-best epoch only moves states.pt's
+        epoch_start (no file yet: nothing to move, where the reference raises)."""
+        path = self._states_path()
+        if self.rank == 0 and os.path.exists(path):
+            states = torch.load(path, map_location="cpu", weights_only=True)
+            states["epoch_start"] = epoch
+            torch.save(states, path)
+
+    def load_states(self, states: Dict) -> None:
+        """Resume from a states.pt dictionary (trainer.py:628-636): models,
+        optimizers (into the flat Adam state) and scheduler."""
+        self.generator.load_state_dict(states["generator"])
+        self.discriminator.load_state_dict(states["discriminator"])
+        for opt, flat, key in ((self.optimizer_generator, self.adam_g, "optimizer_generator"),
+                               (self.optimizer_discriminator, self.adam_d, "optimizer_discriminator")):
+            if states.get(key) is None:
+                continue
+            (opt if opt is not None else flat).load_state_dict(states[key])
+            if opt is not None:
+                flat.import_from(opt)
+        if self.scheduler_generator is not None and states.get("scheduler_generator") is not None:
+            self.scheduler_generator.load_state_dict(states["scheduler_generator"])
+        rng = states.get("vgan_rng")
+        if isinstance(rng, dict):
+            self.rng.load_state_dict(dict(rng, seed=int(rng["seed"]) + 7919 * self.rank))
+        self.states = dict(states)

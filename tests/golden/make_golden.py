@@ -127,6 +127,65 @@ def make_forward_eval(cfgmod, models, trainer_mod):
     }
 
 
+def make_forward_b32(cfgmod, models, trainer_mod):
+    """The benchmarked size (BASELINE.json configs[1]): batch 32 =
+    SyntheticDataset(6500, seed=777)[0..31] (bench.py's first pooled batch),
+    full-size G and D from torch.manual_seed(777), eval mode.  The inputs are
+    NOT stored (6.5 MB of z alone): the test regenerates them from the seeds
+    below with the same CPU-generator calls and checks the batch checksum.
+    Stored: logits, argmax labels, D scores, the WGAN-GP loss and D gradients,
+    the generator loss and G gradients."""
+    cfg = cfgmod.Configuration()
+    items = [synth.make_building(777, i) for i in range(32)]
+    local, voxel = to_pyg(items)
+    torch.manual_seed(777)
+    G = models.VoxelGNNGenerator(cfg, 17, 12)
+    D = models.VoxelGNNDiscriminator(cfg, 17, 12)
+    G.eval()
+    D.eval()
+    n = voxel.num_nodes
+    torch.manual_seed(2001)
+    z = torch.randn(1, n, cfg.Z_DIM)
+    torch.manual_seed(2002)
+    with torch.no_grad():
+        logits, hard, soft = G(local, voxel, z)  # F.gumbel_softmax draws Exp(1) here
+    opt = torch.optim.Adam(D.parameters())
+    tr = trainer_mod.Trainer(G, D, _Loaders([]), torch.optim.Adam(G.parameters()), opt,
+                             torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=10), cfg,
+                             log_dir=os.path.join("/tmp", "vgan_golden_unused"))
+    with torch.no_grad():
+        d_real = D(local, voxel, voxel.types_onehot.unsqueeze(0))
+        d_hard = D(local, voxel, hard.unsqueeze(0))
+    torch.manual_seed(2003)
+    D.zero_grad()
+    d_loss = tr._compute_discriminator_loss(local, voxel, hard.unsqueeze(0), soft.unsqueeze(0))
+    d_loss.backward()
+    d_grads = {k: p.grad.detach().clone() for k, p in D.named_parameters()}
+    G.zero_grad()
+    D.zero_grad()
+    torch.manual_seed(2002)
+    logits_g, hard_g, _ = G(local, voxel, z)
+    g_loss = tr._compute_generator_loss(local, voxel, logits_g, hard_g.unsqueeze(0))
+    g_loss.backward()
+    g_grads = {k: p.grad.detach().clone() for k, p in G.named_parameters()}
+    return {
+        "batch_checksum": batch_checksum(local, voxel), "num_nodes": n, "num_buildings": len(items),
+        "dataset_seed": 777, "init_seed": 777, "z_seed": 2001, "gumbel_seed": 2002, "gp_seed": 2003,
+        "logits": logits, "label_soft": soft, "label_argmax": hard.argmax(1).to(torch.int8),
+        "d_real": d_real, "d_hard": d_hard, "d_loss": d_loss.detach(), "d_grads": d_grads,
+        "g_loss": g_loss.detach(), "g_grads": g_grads,
+    }
+
+
+def batch_checksum(local, voxel):
+    """float64 sums identifying the collated inputs (features, types, edges)."""
+    parts = [local.x.double().sum(), local.type.double().sum(), voxel.x.double().sum(),
+             (voxel.x.double() * torch.arange(1, voxel.x.shape[1] + 1, dtype=torch.float64)).sum(),
+             voxel.type.double().sum(), voxel.edge_index.double().sum(),
+             (voxel.edge_index[0].double() * voxel.edge_index[1].double()).sum()]
+    return torch.stack(parts)
+
+
 def run_reference_step(cfg, models, trainer_mod, items, init_seed, step_seed):
     local, voxel = to_pyg(items)
     torch.manual_seed(init_seed)
@@ -224,6 +283,7 @@ def main():
     cfgmod, models, trainer_mod = shim.import_reference()
     jobs = {
         "forward_eval.pt": lambda: make_forward_eval(cfgmod, models, trainer_mod),
+        "forward_b32.pt": lambda: make_forward_b32(cfgmod, models, trainer_mod),
         "step_sanity.pt": lambda: make_step_sanity(cfgmod, models, trainer_mod),
         "step_tiny.pt": lambda: make_step_tiny(cfgmod, models, trainer_mod),
         "ops_small.pt": make_ops_small,

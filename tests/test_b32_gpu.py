@@ -1,0 +1,187 @@
+"""Parity at the benchmarked size: configs[1], batch 32 (bench.py's first pooled
+batch: SyntheticDataset(6500, seed=777)[0..31], ~12.7k voxels, ~78k edges with
+self loops), full-size models from torch.manual_seed(777).
+
+* against tests/golden/forward_b32.pt, produced by EXECUTING the reference's
+  models.py / trainer.py (tests/golden/make_golden.py): eval logits within
+  1e-3 (the north-star bar), D scores, the WGAN-GP loss with its second-order D
+  gradients, the generator loss with its G gradients -- through the same
+  Trainer methods the step runs (critic engine, fused loss head);
+* the step per iteration against the CPU oracle with the reference's CPU draws
+  replayed (runtime['rng'] = 'host');
+* the timed path itself -- ``step_graphed`` with device RNG, the stacked
+  critic-label forward, the aggregation's GraphNorm partials (``_gnp``) and the
+  padded column array (ELL) -- against the eager ``step`` iteration by
+  iteration from identical state (the eager step is the one the oracle pins).
+"""
+import pytest
+import torch
+
+from parity_util import _FixedUniform, b32_inputs, grads_close, load_fixture, step_iterations_vs_oracle
+from vgan.config import Configuration
+from vgan.models import VoxelGNNDiscriminator, VoxelGNNGenerator
+from vgan.trainer import Trainer
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def b32():
+    f = load_fixture("forward_b32.pt")
+    return f, b32_inputs(f, device="cuda")
+
+
+def _models(cfg, f):
+    torch.manual_seed(int(f["init_seed"]))
+    return VoxelGNNGenerator(cfg, 17, 12), VoxelGNNDiscriminator(cfg, 17, 12)
+
+
+def test_b32_eval_logits_within_1e3(cuda, b32):
+    f, inp = b32
+    cfg = Configuration()
+    G, D = _models(cfg, f)
+    G.eval()
+    D.eval()
+    loc, vox = inp["vgan"]
+    assert vox.num_nodes == int(f["num_nodes"]) and vox.num_graphs == 32
+    z, noise = inp["z"].to(cuda), inp["noise"].to(cuda)
+    with torch.no_grad():
+        logits, hard, soft = G(loc, vox, z, noise=noise)
+        d_real = D(loc, vox, vox.types_onehot.unsqueeze(0))
+        d_hard = D(loc, vox, hard.unsqueeze(0))
+        # the evaluation path of Trainer._validate_each_epoch / test: the no-grad
+        # multi-source forward (no concatenation), one copy
+        ls, hs, _ = G(loc, vox, z, noise=noise, stacked=True)
+    err = (logits.cpu() - f["logits"]).abs().max().item()
+    print(f"batch 32: max |logits - reference| = {err:.2e}")
+    assert err < 1e-3
+    assert (soft.cpu() - f["label_soft"]).abs().max().item() < 1e-3
+    assert (hard.cpu().argmax(1).to(torch.int8) != f["label_argmax"]).float().mean().item() < 1e-3
+    assert (d_real.cpu() - f["d_real"]).abs().max().item() < 1e-3
+    assert (d_hard.cpu() - f["d_hard"]).abs().max().item() < 1e-3
+    assert (ls.reshape(logits.shape).cpu() - f["logits"]).abs().max().item() < 1e-3
+
+
+def test_b32_critic_loss_and_second_order_grads(cuda, b32):
+    f, inp = b32
+    cfg = Configuration()
+    G, D = _models(cfg, f)
+    G.eval()
+    D.eval()
+    loc, vox = inp["vgan"]
+    with torch.no_grad():
+        _, hard, soft = G(loc, vox, inp["z"].to(cuda), noise=inp["noise"].to(cuda))
+    # the reference's labels (argmax ties aside the same), so D sees identical inputs
+    ref_hard = torch.nn.functional.one_hot(f["label_argmax"].long(), 7).float().to(cuda)
+    ref_hard = ref_hard - f["label_soft"].to(cuda) + f["label_soft"].to(cuda)
+    tr = Trainer(G, D, None, None, None, None, cfg)
+    tr.rng = _FixedUniform(inp["gp_eps"].to(cuda))
+    tr.adam_d.zero_grad()
+    d_loss = tr._critic_loss_backward(loc, vox, ref_hard.unsqueeze(0), f["label_soft"].to(cuda).unsqueeze(0))
+    ref = float(f["d_loss"])
+    print(f"batch 32: d_loss {d_loss.item():.7f} vs reference {ref:.7f}")
+    assert abs(d_loss.item() - ref) <= 1e-4 * max(1.0, abs(ref))
+    ok, worst, total = grads_close({k: p.grad for k, p in D.named_parameters()}, f["d_grads"], rtol=1e-2,
+                                   total_rtol=2e-3)
+    print(f"batch 32: D gradient relative error {total:.2e}")
+    assert ok, (worst, total)
+
+
+def test_b32_generator_loss_and_grads(cuda, b32):
+    f, inp = b32
+    cfg = Configuration()
+    G, D = _models(cfg, f)
+    G.eval()
+    D.eval()
+    loc, vox = inp["vgan"]
+    tr = Trainer(G, D, None, None, None, None, cfg)
+    tr.adam_g.zero_grad()
+    logits, hard, _ = G(loc, vox, inp["z"].to(cuda), noise=inp["noise"].to(cuda))
+    g_loss = tr._compute_generator_loss(loc, vox, logits, hard.unsqueeze(0))
+    g_loss.backward()
+    ref = float(f["g_loss"])
+    assert abs(g_loss.item() - ref) <= 1e-3 * max(1.0, abs(ref))
+    ok, worst, total = grads_close({k: p.grad for k, p in G.named_parameters()}, f["g_grads"], rtol=1e-2,
+                                   total_rtol=5e-3)
+    print(f"batch 32: G gradient relative error {total:.2e}")
+    assert ok, (worst, total)
+
+
+def test_b32_step_each_iteration_matches_oracle(cuda, b32):
+    """trainer.py:466-495 at batch 32 with the reference's CPU draws replayed:
+    every critic iteration and the generator iteration against the oracle."""
+    f, inp = b32
+    cfg = Configuration()
+    torch.manual_seed(int(f["init_seed"]))
+    from oracle import reference as R
+
+    G0, D0 = R.Generator(cfg), R.Discriminator(cfg)
+    sd_g = {k: v.clone() for k, v in G0.state_dict().items()}
+    sd_d = {k: v.clone() for k, v in D0.state_dict().items()}
+    step_iterations_vs_oracle(cuda, cfg, sd_g, sd_d, inp["vgan"], inp["oracle"], step_seed=4242)
+
+
+def _flat_grads(flat, module):
+    return {k: flat.grad[flat._offset(p):flat._offset(p) + p.numel()].clone() for k, p in module.named_parameters()}
+
+
+def _trainer(cfg, seed=777):
+    torch.manual_seed(seed)
+    G, D = VoxelGNNGenerator(cfg, 17, 12), VoxelGNNDiscriminator(cfg, 17, 12)
+    og = torch.optim.Adam(G.parameters(), lr=cfg.LEARNING_RATE_GENERATOR, betas=cfg.BETAS)
+    od = torch.optim.Adam(D.parameters(), lr=cfg.LEARNING_RATE_DISCRIMINATOR, betas=cfg.BETAS)
+    return Trainer(G, D, None, og, od, None, cfg)
+
+
+def _copy_state(dst, src):
+    for a, b in zip(dst._state_tensors(), src._state_tensors()):
+        a.copy_(b)
+
+
+def test_b32_graphed_step_matches_eager(cuda, b32):
+    """The benchmark's timed path (step_graphed: device RNG, stacked critic
+    labels, _gnp aggregation, ELL) against the eager step body by body, from
+    identical state: labels, every critic loss and D gradient, the generator
+    loss and G gradient."""
+    from vgan import data as vdata
+    from vgan import ops
+
+    f, inp = b32
+    cfg = Configuration()
+    cfg.DEVICE = str(cuda)
+    cfg.runtime["rng"] = "device"
+    eager, graphed = _trainer(cfg), _trainer(cfg)
+    loc, vox = inp["vgan"]
+    prep = vdata.prepared(loc, vox, cfg.NUM_CLASSES)
+    assert prep.csr.ell()[0] is not None and ops._GN_FWD_FUSE  # the variants the bench times
+    assert graphed._stacked_labels()
+    graphs = graphed.capture(loc, vox)
+    assert torch.equal(graphed.flat_g.param, eager.flat_g.param)  # capture left no trace
+    graphs["labels"].replay()
+    labels_e = eager._critic_labels(loc, vox)
+    torch.cuda.synchronize()
+    h_g, s_g = graphs["label_tensors"]
+    assert (s_g - labels_e[1]).abs().max().item() < 1e-5
+    assert (h_g.argmax(-1) != labels_e[0].argmax(-1)).float().mean().item() < 1e-4
+    acc_e = torch.zeros(cfg.N_CRITIC + 1, device=cuda)
+    for it in range(cfg.N_CRITIC):
+        _copy_state(graphed, eager)
+        graphs["critic"][it].replay()
+        eager._critic_body(loc, vox, acc_e, True, (h_g, s_g), it)  # the same labels in
+        torch.cuda.synchronize()
+        got, want = graphs["acc"][it].item(), acc_e[it].item()
+        assert abs(got - want) <= 1e-4 * max(1.0, abs(want)), (it, got, want)
+        ok, worst, total = grads_close(_flat_grads(graphed.flat_d, graphed.discriminator),
+                                       _flat_grads(eager.flat_d, eager.discriminator), rtol=5e-3)
+        assert ok, (it, worst, total)
+    _copy_state(graphed, eager)
+    graphs["gen"].replay()
+    eager._gen_body(loc, vox, acc_e, True)
+    torch.cuda.synchronize()
+    assert abs(graphs["acc"][-1].item() - acc_e[-1].item()) <= 1e-4 * max(1.0, abs(acc_e[-1].item()))
+    ok, worst, total = grads_close(_flat_grads(graphed.flat_g, graphed.generator),
+                                   _flat_grads(eager.flat_g, eager.generator), rtol=5e-3)
+    assert ok, (worst, total)
+    # and whole graphed steps keep training sanely at this size
+    outs = [graphed.step_graphed(loc, vox) for _ in range(2)]
+    assert all(torch.isfinite(o["d_losses"]).all() and torch.isfinite(o["g_loss"]) for o in outs)

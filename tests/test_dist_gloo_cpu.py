@@ -8,6 +8,7 @@ import socket
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+import pytest
 
 
 def _free_port():
@@ -135,3 +136,64 @@ def test_sharded_loader_equal_steps_shared_shuffle():
     import pytest
     with pytest.raises(ValueError):
         GraphLoader(None, indices, batch_size=4, rank=0, world_size=2)  # no shared seed
+
+
+def _epoch_worker(rank, world, port, q):
+    """Epoch figures reduced over the ranks: rank 1 has no evaluation batch
+    at all (an uneven, uncut evaluation shard)."""
+    import sys
+
+    from parity_util import PKG_ROOT
+    sys.path.insert(0, PKG_ROOT)
+    from vgan import dist as vdist
+    from vgan.config import Configuration
+    from vgan.models import VoxelGNNDiscriminator, VoxelGNNGenerator
+    from vgan.trainer import Trainer
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    cfg = Configuration()
+    cfg.DEVICE = "cpu"
+    vdist.init("gloo", configuration=cfg)
+    torch.manual_seed(cfg.SEED)
+    tr = Trainer(VoxelGNNGenerator(cfg, 17, 12), VoxelGNNDiscriminator(cfg, 17, 12), None, None, None, None, cfg)
+    if rank == 0:
+        metrics = [(0.5, [0.25, 0.75], 0.4, 0.6, 0.9), (0.7, [0.5], 0.2, 0.8, 0.7)]
+        losses = [[torch.tensor(1.0), torch.tensor(3.0)]]
+    else:
+        metrics, losses = [], [[]]
+    out = tr._epoch_figures(metrics, losses)
+    q.put((rank, out[0], out[1], out[2]))
+    dist.destroy_process_group()
+
+
+def test_gloo_epoch_figures_reduced_over_ranks():
+    (_, l0, m0, lo0), (_, l1, m1, lo1) = _run(_epoch_worker)
+    assert l0 == l1 == [2.0]
+    assert m0 == m1
+    assert m0 == pytest.approx([0.6, 0.3, 0.7, 0.8])
+    assert lo0 == lo1 == 0.25
+
+
+def test_eval_loader_keeps_every_batch_and_resident_replays_objects(tmp_path):
+    """Evaluation loaders are not cut to a multiple of the ranks; a resident
+    loader yields the same device batch objects every epoch."""
+    import sys
+
+    from parity_util import PKG_ROOT
+    if PKG_ROOT not in sys.path:
+        sys.path.insert(0, PKG_ROOT)
+    from vgan.loader import GraphLoader
+    from vgan.store import write_store
+    from vgan.synth import SyntheticDataset
+
+    indices = list(range(100, 141))  # 11 batches of 4
+    a = GraphLoader(None, indices, batch_size=4, rank=0, world_size=2, seed=777, even=False)
+    b = GraphLoader(None, indices, batch_size=4, rank=1, world_size=2, seed=777, even=False)
+    pa, pb = a.batches(), b.batches()
+    assert (len(pa), len(pb)) == (6, 5) == (len(a), len(b))
+    assert sorted(i for bt in pa + pb for i in bt) == indices
+    store = write_store(str(tmp_path / "st"), SyntheticDataset(6, seed=2))
+    ld = GraphLoader(store, None, batch_size=4, resident=True)
+    first = list(ld)
+    second = list(ld)
+    assert len(first) == 2 and all(x[1] is y[1] for x, y in zip(first, second))

@@ -117,92 +117,15 @@ def test_full_step_matches_reference(cuda, name):
 
 @pytest.mark.parametrize("name", ["step_sanity.pt", "step_tiny.pt"])
 def test_step_each_iteration_matches_oracle(cuda, name):
-    """Per-iteration parity of the full step: every critic iteration and the
-    generator iteration start from the reference's parameters (taken from the
-    CPU oracle, which tests/test_oracle_golden.py pins bit-for-bit to the
-    reference's own trainer) and the same replayed CPU RNG state.  Loss within
-    1e-5 relative, gradients within grads_close.
-
-    This isolates kernel parity from trajectory drift: the reference model has
-    GATConv biases feeding a GraphNorm that cancels them exactly (zero true
-    gradient), so their computed gradients are rounding noise, which Adam turns
-    into +-lr steps on both implementations alike (1.07% of D's parameters =
-    exactly its 168 GAT bias entries after the first update)."""
-    from oracle import reference as R
-    from parity_util import oracle_batches
+    """Per-iteration parity of the full step (parity_util.step_iterations_vs_oracle)."""
+    from parity_util import oracle_batches, step_iterations_vs_oracle
 
     f = load_fixture(name)
     cfg = Configuration(sanity_checking=(name == "step_sanity.pt"))
     if name == "step_tiny.pt":
         tiny_config(cfg)
-    cfg.runtime["rng"] = "host"
-    G, D = _models(cfg, f["G0"], f["D0"])
-    tr = Trainer(G, D, None, torch.optim.Adam(G.parameters(), lr=2e-4, betas=cfg.BETAS),
-                 torch.optim.Adam(D.parameters(), lr=2e-4, betas=cfg.BETAS), None, cfg)
-    Go, Do = R.Generator(cfg), R.Discriminator(cfg)
-    Go.load_state_dict(f["G0"])
-    Do.load_state_dict(f["D0"])
-    od = torch.optim.Adam(Do.parameters(), lr=cfg.LEARNING_RATE_DISCRIMINATOR, betas=cfg.BETAS)
-    loc, vox = vgan_batches(f["batch"])
-    ol, ov = oracle_batches(f["batch"])
-    torch.manual_seed(int(f["step_seed"]))
-    for it in range(cfg.N_CRITIC):
-        state = torch.get_rng_state()
-        with torch.no_grad():
-            _, hard, soft = tr._generate(loc, vox)
-        mid = torch.get_rng_state()
-        torch.set_rng_state(state)
-        with torch.no_grad():
-            _, ho, so = Go(ol, ov, torch.randn(1, ov.num_nodes, cfg.Z_DIM))
-        assert torch.equal(torch.get_rng_state(), mid)  # identical RNG consumption
-        # generator (no-grad, train mode) parity: soft labels and argmax
-        assert (soft.squeeze(0).cpu() - so).abs().max().item() < 1e-4
-        assert (hard.squeeze(0).cpu().argmax(1) != ho.argmax(1)).float().mean().item() < 0.01
-        # discriminator on IDENTICAL inputs: the WGAN-GP term is discontinuous in
-        # its input (a 1e-6 label change can flip one ReLU in one node's gradient
-        # path and move the 400-node mean by ~1e-4), so feed the oracle's labels
-        tr.adam_d.zero_grad()
-        d_loss = tr._compute_discriminator_loss(loc, vox, ho.unsqueeze(0).to(cuda), so.unsqueeze(0).to(cuda))
-        d_loss.backward()
-        after = torch.get_rng_state()
-        torch.set_rng_state(mid)
-        od.zero_grad()
-        d_ref = R.discriminator_loss(Do, cfg, ol, ov, ho.unsqueeze(0), so.unsqueeze(0))
-        d_ref.backward()
-        assert torch.equal(torch.get_rng_state(), after)
-        # 1e-4: even on identical inputs, last-bit differences inside D can flip a
-        # ReLU at 0 in one node's gradient path (measured 1.4e-5 on step_tiny)
-        assert abs(d_loss.item() - d_ref.item()) <= 1e-4 * abs(d_ref.item()), (it, d_loss.item(), d_ref.item())
-        # Kink flips: at critic iteration 2 of step_tiny the GP forward has a
-        # ReLU input 1.45e-6 from 0 (scale 0.72; node 551, last GAT block --
-        # tools/debug_kinks.py), inside the f32 rounding difference of two
-        # summation orders.  The GPU's mask differs there, which moves the input
-        # gradient of ~5 neighbouring nodes by 3e-3 and the GP-parameter
-        # gradient by 1.6e-3 overall (tools/debug_gp_iter.py; all other terms
-        # agree to 1e-7).  Bound: 1e-2 per parameter, 5e-3 for the whole gradient.
-        ok, worst, total = grads_close({k: p.grad for k, p in D.named_parameters()},
-                                       {k: p.grad for k, p in Do.named_parameters()}, rtol=1e-2,
-                                       total_rtol=5e-3)
-        assert ok, (it, worst, total)
-        od.step()
-        with torch.no_grad():  # continue from the reference's parameters
-            for p, q in zip(D.parameters(), Do.parameters()):
-                p.copy_(q.to(p.device))
-    state = torch.get_rng_state()
-    tr.adam_g.zero_grad()
-    logits, hard, _ = tr._generate(loc, vox)
-    g_loss = tr._compute_generator_loss(loc, vox, logits, hard)
-    g_loss.backward()
-    torch.set_rng_state(state)
-    Go.zero_grad()
-    lo, ho, _ = Go(ol, ov, torch.randn(1, ov.num_nodes, cfg.Z_DIM))
-    g_ref = R.generator_loss(Do, cfg, ol, ov, lo, ho.unsqueeze(0))
-    g_ref.backward()
-    assert abs(g_loss.item() - g_ref.item()) <= 1e-4 * max(1.0, abs(g_ref.item()))
-    # the G gradient flows through D(label_hard): same ReLU-kink sensitivity as above
-    ok, worst, total = grads_close({k: p.grad for k, p in G.named_parameters()},
-                                   {k: p.grad for k, p in Go.named_parameters()}, rtol=5e-3)
-    assert ok, (worst, total)
+    step_iterations_vs_oracle(cuda, cfg, f["G0"], f["D0"], vgan_batches(f["batch"]), oracle_batches(f["batch"]),
+                              int(f["step_seed"]))
 
 
 def test_direct_param_grads_match_autograd(cuda):

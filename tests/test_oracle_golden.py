@@ -133,3 +133,40 @@ def test_configuration_matches_reference_values():
             continue
         assert k in mine, k
         assert mine[k] == v, (k, mine[k], v)
+
+
+def test_oracle_matches_reference_at_batch_32():
+    """The benchmarked size (configs[1], 32 buildings, ~12.7k voxels): the
+    restatement reproduces the reference-executed forward_b32.pt -- logits,
+    D scores, WGAN-GP loss with its second-order D gradients, generator loss
+    with its G gradients -- bit for bit."""
+    from parity_util import b32_inputs
+
+    f = load_fixture("forward_b32.pt")
+    inp = b32_inputs(f, device=None)
+    local, voxel = inp["oracle"]
+    cfg = Configuration()
+    torch.manual_seed(int(f["init_seed"]))
+    G, D = R.Generator(cfg), R.Discriminator(cfg)
+    G.eval()
+    D.eval()
+    with torch.no_grad():
+        logits, hard, soft = G(local, voxel, inp["z"], noise=inp["noise"])
+        d_real = D(local, voxel, voxel.types_onehot.unsqueeze(0))
+        d_hard = D(local, voxel, hard.unsqueeze(0))
+    assert torch.equal(logits, f["logits"]) and torch.equal(soft, f["label_soft"])
+    assert torch.equal(hard.argmax(1).to(torch.int8), f["label_argmax"])
+    assert torch.equal(d_real, f["d_real"]) and torch.equal(d_hard, f["d_hard"])
+    torch.manual_seed(int(f["gp_seed"]))  # the GP's eps = torch.rand(N, 1), trainer.py:298
+    d_loss = R.discriminator_loss(D, cfg, local, voxel, hard.unsqueeze(0), soft.unsqueeze(0))
+    d_loss.backward()
+    assert torch.equal(d_loss.detach(), f["d_loss"])
+    for k, p in D.named_parameters():
+        assert torch.equal(p.grad, f["d_grads"][k]), k
+    D.zero_grad()
+    logits_g, hard_g, _ = G(local, voxel, inp["z"], noise=inp["noise"])
+    g_loss = R.generator_loss(D, cfg, local, voxel, logits_g, hard_g.unsqueeze(0))
+    g_loss.backward()
+    assert torch.equal(g_loss.detach(), f["g_loss"])
+    for k, p in G.named_parameters():
+        assert torch.equal(p.grad, f["g_grads"][k]), k

@@ -6,7 +6,7 @@
 # Leaves gpurun_out/rooftrace_<tag>/{bench.json, kernel_stats.csv, summary.txt};
 # summary.txt holds the average duration over every aggregate launch.
 set -o pipefail
-TAG=$1
+TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/rooftrace_$TAG
 mkdir -p "$OUT"
@@ -14,7 +14,7 @@ export TMPDIR=/tmp
 cd /tmp || exit 1
 rm -rf "/tmp/rooftrace_$TAG"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "/tmp/rooftrace_$TAG" -o run --output-format csv -- \
-  python3 "$R/bench.py" --roofline-only --steps 20 > "$OUT/bench.json" 2> "$OUT/bench.log" || exit $?
+  python3 "$R/bench.py" --roofline-only --steps 20 "$@" > "$OUT/bench.json" 2> "$OUT/bench.log" || exit $?
 T=$(find "/tmp/rooftrace_$TAG" -name "*kernel_trace.csv" | head -1)
 S=$(find "/tmp/rooftrace_$TAG" -name "*kernel_stats.csv" | head -1)
 [ -n "$S" ] && cp "$S" "$OUT/kernel_stats.csv"
