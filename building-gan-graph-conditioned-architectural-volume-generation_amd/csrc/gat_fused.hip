@@ -73,88 +73,79 @@ __device__ __forceinline__ void load_param(Vec<CPL>& r, const float* __restrict_
 // Per column (count, mean, M2) of the block's rows, two passes over the row
 // values still in registers: sums by xor-shuffles across the wave's L-lane row
 // groups then across the 4 waves in order through LDS, the mean, then the
-// squared deviations the same way (deterministic).  Slot 0 is the segment of
-// the block's first row, slot 1 the next one (reduced and written only when the
-// block straddles one: seg_rows >= the block's rows, vg_gat_gnp_rows).
-// gnp [blocks][2][ldc][3], column cb + c.  v: this lane's CPL columns c0.. of
-// its row (lanes past C hold anything: their columns are not written).
+// squared deviations the same way (deterministic).
+// Blocks are SEGMENT-ALIGNED (gnp_rows): a stacked forward over S copies
+// (seg_rows rows each) gives every copy ceil(seg_rows / G) blocks of its own,
+// the last one short, so each copy's partials -- and the statistics folded
+// from them -- are bit for bit those of a separate forward over that copy.
+// (Blocks dealt over the stacked rows straddled copies at offsets that
+// depended on the copy: the critic engine's stacked real / fake / mix forward
+// then normalised with statistics ~1e-7 off the three separate forwards of
+// autograd's double backward, enough to flip bf16 operand roundings.)
+// gnp [blocks][2][ldc][3], column cb + c, slot 0 (slot 1 unused).  v: this
+// lane's CPL columns c0.. of its row (lanes past C hold anything: their
+// columns are not written).
 // (A first form folded each column serially over the block's rows with
 // Welford updates in one wave: +4 us per launch, slower than the separate
 // statistics pass it replaced.)
+struct GnpRows {
+  int lb, row0, end;  // logical block, its first row, the end of its segment
+};
+
+template <int G>
+__device__ __forceinline__ GnpRows gnp_rows(int seg_rows) {
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int bps = (seg_rows + G - 1) / G;
+  const int seg = lb / bps;
+  return {lb, seg * seg_rows + (lb - seg * bps) * G, (seg + 1) * seg_rows};
+}
+
 template <int L, int CPL>
-__device__ __forceinline__ void gnp_block(const float (&v)[CPL], int row, int lb, int N, int seg_rows, int C,
-                                          int c0, int cb, int ldc, float* __restrict__ gnp) {
+__device__ __forceinline__ void gnp_block(const float (&v)[CPL], int row, const GnpRows& gr, int C, int c0,
+                                          int cb, int ldc, float* __restrict__ gnp) {
   constexpr int G = kBlock / L, W = L * CPL;
-  __shared__ float red[kBlock / 64][2][W];
-  __shared__ float mv[2][W];
-  const int row0 = lb * G;
-  const int bound = (row0 / seg_rows + 1) * seg_rows;
-  const bool straddle = row0 + G > bound && bound < N;  // block-uniform
-  const int n0 = min(min(bound, N), row0 + G) - row0;
-  const int n1 = straddle ? min(N, row0 + G) - bound : 0;
-  const bool in0 = row < N && row < bound, in1 = row < N && row >= bound;
+  __shared__ float red[kBlock / 64][W];
+  __shared__ float mv[W];
+  const int n0 = min(gr.end, gr.row0 + G) - gr.row0;
+  const bool in0 = row < gr.end;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  float s0[CPL], s1[CPL];
+  float s0[CPL];
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
     for (int q = 0; q < CPL; ++q) {
-      float x0 = v[q], x1 = v[q];
+      float x0 = v[q];
       if (pass == 1) {
-        x0 -= mv[0][c0 + q];
+        x0 -= mv[c0 + q];
         x0 *= x0;
-        if (straddle) {
-          x1 -= mv[1][c0 + q];
-          x1 *= x1;
-        }
       }
       s0[q] = in0 ? x0 : 0.f;
-      s1[q] = in1 ? x1 : 0.f;
     }
 #pragma unroll
     for (int off = L; off < 64; off <<= 1)
 #pragma unroll
-      for (int q = 0; q < CPL; ++q) {
-        s0[q] += __shfl_xor(s0[q], off, 64);
-        if (straddle) s1[q] += __shfl_xor(s1[q], off, 64);
-      }
+      for (int q = 0; q < CPL; ++q) s0[q] += __shfl_xor(s0[q], off, 64);
     if (lane < L)
 #pragma unroll
-      for (int q = 0; q < CPL; ++q) {
-        red[wave][0][c0 + q] = s0[q];
-        red[wave][1][c0 + q] = s1[q];
-      }
+      for (int q = 0; q < CPL; ++q) red[wave][c0 + q] = s0[q];
     __syncthreads();
     const int c = threadIdx.x;
     if (pass == 0) {
       if (c < W) {
-        float a0 = 0.f, a1 = 0.f;
+        float a0 = 0.f;
 #pragma unroll
-        for (int w = 0; w < kBlock / 64; ++w) {
-          a0 += red[w][0][c];
-          a1 += red[w][1][c];
-        }
-        mv[0][c] = n0 > 0 ? a0 / static_cast<float>(n0) : 0.f;
-        mv[1][c] = n1 > 0 ? a1 / static_cast<float>(n1) : 0.f;
+        for (int w = 0; w < kBlock / 64; ++w) a0 += red[w][c];
+        mv[c] = a0 / static_cast<float>(n0);
       }
       __syncthreads();
     } else if (c < C) {
-      float m0 = 0.f, m1 = 0.f;
+      float m0 = 0.f;
 #pragma unroll
-      for (int w = 0; w < kBlock / 64; ++w) {
-        m0 += red[w][0][c];
-        m1 += red[w][1][c];
-      }
-      float* p = gnp + ((size_t)lb * 2 * ldc + cb + c) * 3;
+      for (int w = 0; w < kBlock / 64; ++w) m0 += red[w][c];
+      float* p = gnp + ((size_t)gr.lb * 2 * ldc + cb + c) * 3;
       p[0] = static_cast<float>(n0);
-      p[1] = mv[0][c];
+      p[1] = mv[c];
       p[2] = m0;
-      if (straddle) {
-        p += (size_t)ldc * 3;
-        p[0] = static_cast<float>(n1);
-        p[1] = mv[1][c];
-        p[2] = m1;
-      }
     }
   }
 }
@@ -213,12 +204,18 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_cp(
     bias += cb;
   }
   constexpr int T = 4;  // edges per lane kept in registers (rows up to 4L edges)
-  const GroupIdx g = group_index<L>();
-  // GNP keeps every wave to the block barrier: a group past N recomputes row
-  // N - 1 and stores nothing
-  const bool live = g.row < N;
+  GroupIdx g = group_index<L>();
+  // GNP: segment-aligned blocks (gnp_rows), and every wave stays to the block
+  // barrier: a group past its segment recomputes the segment's last row and
+  // stores nothing
+  GnpRows gr{0, 0, N};
+  if constexpr (GNP) {
+    gr = gnp_rows<kBlock / L>(seg_rows);
+    g.row = gr.row0 + threadIdx.x / L;
+  }
+  const bool live = g.row < gr.end;
   if (!GNP && !live) return;
-  const int i = live ? g.row : N - 1;
+  const int i = live ? g.row : gr.end - 1;
   const int beg = row_ptr[i], end = row_ptr[i + 1];
   const int deg = end - beg;
   const float ad = a_dst[i];
@@ -309,8 +306,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_cp(
 #pragma unroll
   for (int q = 0; q < CPL; ++q) acc.v[q] += b.v[q];
   if (live) store_row<CPL, VEC>(acc, out + (size_t)i * ld, c0, C);
-  if constexpr (GNP)
-    gnp_block<L, CPL>(acc.v, g.row, xcd_remap(blockIdx.x, gridDim.x), N, seg_rows, C, c0, cbase, ldc, gnp);
+  if constexpr (GNP) gnp_block<L, CPL>(acc.v, g.row, gr, C, c0, cbase, ldc, gnp);
 }
 
 // C <= 8: 8 lanes per destination row, one edge per lane.
@@ -327,10 +323,15 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_ep(
     int ew = 0, float* __restrict__ gnp = nullptr, int seg_rows = 0) {
   static_assert(!GNP || PRE, "GraphNorm partials with precomputed projections only");
   constexpr int L = 8;
-  const GroupIdx g = group_index<L>();
-  const bool live = g.row < N;
+  GroupIdx g = group_index<L>();
+  GnpRows gr{0, 0, N};  // GNP: segment-aligned blocks, as in k_gat_fwd_cp
+  if constexpr (GNP) {
+    gr = gnp_rows<kBlock / L>(seg_rows);
+    g.row = gr.row0 + threadIdx.x / L;
+  }
+  const bool live = g.row < gr.end;
   if (!GNP && !live) return;
-  const int i = live ? g.row : N - 1;
+  const int i = live ? g.row : gr.end - 1;
   float vs[CMAX];
   float ad = 0.f;
   if constexpr (PRE) {
@@ -452,7 +453,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_ep(
   }
   if constexpr (GNP) {
     const float ov[1] = {o};
-    gnp_block<L, 1>(ov, g.row, xcd_remap(blockIdx.x, gridDim.x), N, seg_rows, C, g.lane, 0, C, gnp);
+    gnp_block<L, 1>(ov, g.row, gr, C, g.lane, 0, C, gnp);
   }
 }
 
@@ -920,8 +921,14 @@ static int aggregate_fwd_launch(const int32_t* row_ptr, const int32_t* col, cons
                                  int32_t seg_rows, hipStream_t s) {
   float* as = const_cast<float*>(a_src);  // read-only under PRE
   float* ad = const_cast<float*>(a_dst);
+  // GNP: segment-aligned blocks of G rows (gnp_rows), S * ceil(seg_rows / G)
+  auto grid_rows = [&](int L) {
+    if (!GNP) return grid_for(N, L);
+    const int G = kBlock / L;
+    return (N / seg_rows) * ((seg_rows + G - 1) / G);
+  };
   if (C <= 8) {
-    const int grid = grid_for(N, 8);
+    const int grid = grid_rows(8);
     const bool e = ell && ew <= 8 * kEP;
 #define VG_EPF(CM)                                                                                           \
   do {                                                                                                       \
@@ -945,23 +952,23 @@ static int aggregate_fwd_launch(const int32_t* row_ptr, const int32_t* col, cons
     // or less of the full-width footprint in its 4 MiB L2
     constexpr int Ls = kSlice / 4;
     if (ell && ew <= 4 * Ls)
-      k_gat_fwd_cp<Ls, 4, true, true, GNP><<<dim3(grid_for(N, Ls), C / kSlice), kBlock, 0, s>>>(
+      k_gat_fwd_cp<Ls, 4, true, true, GNP><<<dim3(grid_rows(Ls), C / kSlice), kBlock, 0, s>>>(
           row_ptr, col, N, kSlice, h, a_src, a_dst, bias, slope, out, alpha, C, ell, ew, gnp, seg_rows);
     else
-      k_gat_fwd_cp<Ls, 4, true, false, GNP><<<dim3(grid_for(N, Ls), C / kSlice), kBlock, 0, s>>>(
+      k_gat_fwd_cp<Ls, 4, true, false, GNP><<<dim3(grid_rows(Ls), C / kSlice), kBlock, 0, s>>>(
           row_ptr, col, N, kSlice, h, a_src, a_dst, bias, slope, out, alpha, C, nullptr, 0, gnp, seg_rows);
   } else if (VG_FWD_C64_L8 && C > 32 && C <= 64 && C % 8 == 0) {
-    k_gat_fwd_cp<8, 8, true, false, GNP><<<grid_for(N, 8), kBlock, 0, s>>>(
+    k_gat_fwd_cp<8, 8, true, false, GNP><<<grid_rows(8), kBlock, 0, s>>>(
         row_ptr, col, N, C, h, a_src, a_dst, bias, slope, out, alpha, 0, nullptr, 0, gnp, seg_rows);
   } else {
     Shape sh;
     pick_fused_shape(C, sh);
     if (ell && ew <= 4 * sh.L)
-      VG_DISPATCH_FUSED(C, (k_gat_fwd_cp<L_, CPL_, V_, true, GNP><<<grid_for(N, L_), kBlock, 0, s>>>(
+      VG_DISPATCH_FUSED(C, (k_gat_fwd_cp<L_, CPL_, V_, true, GNP><<<grid_rows(L_), kBlock, 0, s>>>(
                                row_ptr, col, N, C, h, a_src, a_dst, bias, slope, out, alpha, 0, ell, ew, gnp,
                                seg_rows)));
     else
-      VG_DISPATCH_FUSED(C, (k_gat_fwd_cp<L_, CPL_, V_, false, GNP><<<grid_for(N, L_), kBlock, 0, s>>>(
+      VG_DISPATCH_FUSED(C, (k_gat_fwd_cp<L_, CPL_, V_, false, GNP><<<grid_rows(L_), kBlock, 0, s>>>(
                                row_ptr, col, N, C, h, a_src, a_dst, bias, slope, out, alpha, 0, nullptr, 0, gnp,
                                seg_rows)));
   }
@@ -975,7 +982,7 @@ static int aggregate_fwd(const int32_t* row_ptr, const int32_t* col, const int32
   if (N <= 0 || C <= 0 || C > 256 || !row_ptr || !col || !h || !a_src || !a_dst || !bias ||
       !out || !alpha || (ell && ew <= 0) || agg_rows_per_block(N, C) == 0)
     return VG_EINVAL;
-  // a workgroup's rows span at most two GraphNorm segments
+  // segments of at least one workgroup's rows, dividing N
   if (gnp && (seg_rows < agg_rows_per_block(N, C) || N % seg_rows != 0)) return VG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int rc = gnp ? aggregate_fwd_launch<true>(row_ptr, col, ell, ew, N, C, h, a_src, a_dst, bias, slope, out,
@@ -1007,7 +1014,8 @@ extern "C" int32_t vg_gat_gnp_rows(int32_t N, int32_t C) { return N > 0 ? agg_ro
 extern "C" int64_t vg_gat_gnp_floats(int32_t N, int32_t C) {
   const int g = N > 0 ? agg_rows_per_block(N, C) : 0;
   if (g == 0) return 0;
-  return (((int64_t)N + g - 1) / g) * 2 * C * 3;
+  // segment-aligned blocks: S * ceil(seg_rows / g) <= ceil(N / g) + S, S <= N / g
+  return 2 * (((int64_t)N + g - 1) / g) * 2 * C * 3;
 }
 
 extern "C" int vg_gat_aggregate_fwd_gnp(const int32_t* row_ptr, const int32_t* col, const int32_t* ell,

@@ -145,7 +145,15 @@ __global__ void __launch_bounds__(kBlock) k_stats_partial(const T* __restrict__ 
 // one round trip per segment), then a fixed xor-butterfly across the wave --
 // deterministic, and spread over C/4 workgroups.  A single workgroup folding
 // all partials (the first version) ran at one CU's bandwidth, ~8-10 us.
-__device__ __forceinline__ int fold_col() { return blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); }
+// Waves per fold workgroup (VG_FOLD_WAVES, default 1): the folds' loads gather
+// one column's partials across rows of partials, 64 lines per instruction, so
+// a fold is bound by its CU's address unit; one wave per workgroup spreads the
+// columns over C CUs instead of C / 4.
+#ifndef VG_FOLD_WAVES
+#define VG_FOLD_WAVES 1
+#endif
+constexpr int kFoldWaves = VG_FOLD_WAVES;
+__device__ __forceinline__ int fold_col() { return blockIdx.x * kFoldWaves + (threadIdx.x >> 6); }
 
 __device__ __forceinline__ Welford wave_merge(Welford w) {
   for (int off = 1; off < 64; off <<= 1) {
@@ -188,18 +196,19 @@ __global__ void __launch_bounds__(kBlock) k_stats_final(const float* __restrict_
 }
 
 // The same fold over the block partials the GAT aggregation wrote in its
-// epilogue (vg_gat_aggregate_fwd_gnp): gnp [blocks][2][C][3] for blocks of G
-// rows of the S * N stacked rows, slot 0 = the segment of the block's first
-// row, slot 1 = the next one.  One wave per (column, segment); lane l merges
-// the segment's blocks l, l + 64, ... in order (16 in flight: one round trip
-// at batch 32), then the xor butterfly: deterministic.
+// epilogue (vg_gat_aggregate_fwd_gnp): gnp [blocks][2][C][3], slot 0, for
+// SEGMENT-ALIGNED blocks of G rows -- segment sg owns blocks sg * B ..
+// sg * B + B - 1, B = ceil(N / G) -- so a segment folds exactly what a separate
+// forward over it would.  One wave per (column, segment); lane l merges the
+// segment's blocks l, l + 64, ... in order (16 in flight: one round trip at
+// batch 32), then the xor butterfly: deterministic.
 __global__ void __launch_bounds__(kBlock) k_stats_final_gnp(const float* __restrict__ gnp, int G, int N, int C,
                                                             int S, float* __restrict__ stats) {
   const int c = fold_col(), lane = threadIdx.x & 63;
   const int sg = blockIdx.y;
   if (c >= C || sg >= S) return;
-  const int r0 = sg * N;
-  const int b0 = r0 / G, b1 = (r0 + N - 1) / G;  // inclusive
+  const int nb = (N + G - 1) / G;
+  const int b0 = sg * nb, b1 = b0 + nb - 1;  // inclusive
   constexpr int U = 16;
   Welford acc = {0.f, 0.f, 0.f};
   for (int bb = b0 + lane; bb <= b1; bb += 64 * U) {
@@ -208,8 +217,7 @@ __global__ void __launch_bounds__(kBlock) k_stats_final_gnp(const float* __restr
     for (int u = 0; u < U; ++u) {
       const int b = bb + 64 * u;
       if (b <= b1) {
-        const int slot = b * G < r0 ? 1 : 0;
-        const float* p = gnp + (((size_t)b * 2 + slot) * C + c) * 3;
+        const float* p = gnp + ((size_t)b * 2 * C + c) * 3;
         v[u][0] = p[0];
         v[u][1] = p[1];
         v[u][2] = p[2];
@@ -929,12 +937,12 @@ static int gn_fwd(const float* x, int32_t S, int32_t N, int32_t C, const float* 
     return VG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (gnp) {
-    k_stats_final_gnp<<<dim3(vg_blocks(C, kBlock / 64), S), kBlock, 0, s>>>(gnp, gnp_rows, N, C, S, stats);
+    k_stats_final_gnp<<<dim3(vg_blocks(C, kFoldWaves), S), 64 * kFoldWaves, 0, s>>>(gnp, gnp_rows, N, C, S, stats);
   } else {
     const int chunks = chunks_for(N);
     dim3 grid(chunks, (C + 63) / 64, S);
     k_stats_partial<float><<<grid, kBlock, 0, s>>>(x, N, C, C, ws, stats, nullptr);
-    k_stats_final<<<dim3(vg_blocks(C, kBlock / 64), S), kBlock, 0, s>>>(ws, chunks, C, S, stats);
+    k_stats_final<<<dim3(vg_blocks(C, kFoldWaves), S), 64 * kFoldWaves, 0, s>>>(ws, chunks, C, S, stats);
   }
   (void)sync;  // former last-block-fold counter: accepted, unused
   const long long total = (long long)S * N * C;
@@ -965,7 +973,7 @@ extern "C" int vg_graphnorm_fwd_h(const uint16_t* x, int32_t ld, int32_t S, int3
   const int chunks = chunks_for(N);
   dim3 grid(chunks, (C + 63) / 64, S);
   k_stats_partial<_Float16><<<grid, kBlock, 0, s>>>(X, N, C, ld, ws, stats, nullptr);
-  k_stats_final<<<dim3(vg_blocks(C, kBlock / 64), S), kBlock, 0, s>>>(ws, chunks, C, S, stats);
+  k_stats_final<<<dim3(vg_blocks(C, kFoldWaves), S), 64 * kFoldWaves, 0, s>>>(ws, chunks, C, S, stats);
   const long long pairs = (long long)S * N * (wcols / 2);
   k_gn_apply_h<<<apply_blocks(pairs), 256, 0, s>>>(X, pairs, C, ld, wcols, (long long)N, weight, bias,
                                                    mean_scale, eps, stats, reinterpret_cast<_Float16*>(y), ldy);
@@ -1006,7 +1014,7 @@ extern "C" int vg_graphnorm_fwd_gnp(const float* x, int32_t S, int32_t N, int32_
 extern "C" int vg_graphnorm_stats_gnp(int32_t S, int32_t N, int32_t C, const float* gnp, int32_t gnp_rows,
                                       float* stats, void* stream) {
   if (S <= 0 || N <= 0 || C <= 0 || !gnp || !stats || gnp_rows <= 0 || gnp_rows > N) return VG_EINVAL;
-  k_stats_final_gnp<<<dim3(vg_blocks(C, kBlock / 64), S), kBlock, 0, static_cast<hipStream_t>(stream)>>>(
+  k_stats_final_gnp<<<dim3(vg_blocks(C, kFoldWaves), S), 64 * kFoldWaves, 0, static_cast<hipStream_t>(stream)>>>(
       gnp, gnp_rows, N, C, S, stats);
   VG_CHECK_LAUNCH();
   return 0;
@@ -1041,7 +1049,7 @@ extern "C" int vg_graphnorm_bwd_seg(const float* x, int32_t S, int32_t N, int32_
   k_gn_bwd_partial<<<grid, kBlock, 0, s>>>(x, g_y, N, C, weight, bias, mean_scale, keep, eps,
                                            stats, part, sums, g_w, g_b, g_ms, accumulate, nullptr);
   (void)sync;
-  k_gn_bwd_final<<<vg_blocks(C, kBlock / 64), kBlock, 0, s>>>(part, chunks, C, S, weight, mean_scale, eps,
+  k_gn_bwd_final<<<vg_blocks(C, kFoldWaves), 64 * kFoldWaves, 0, s>>>(part, chunks, C, S, weight, mean_scale, eps,
                                                               stats, sums, g_w, g_b, g_ms, accumulate);
   if (g_x)  // g_x NULL: the column sums only (vg_gat_bwd_gn applies them)
     gn_bwd_apply_launch(x, S, N, C, weight, bias, mean_scale, keep, eps, stats, sums, g_y, g_x, inj, inj_offset, s);
@@ -1069,7 +1077,7 @@ extern "C" int vg_graphnorm_bwd_seg_tiles(const float* x, int32_t S, int32_t N, 
     return VG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
   float* sums = ws + (size_t)S * kChunks * C * 5;
-  k_gn_bwd_final_tiles<<<vg_blocks(C, kBlock / 64), kBlock, 0, s>>>(tpart, N, C, S, weight, mean_scale, eps,
+  k_gn_bwd_final_tiles<<<vg_blocks(C, kFoldWaves), 64 * kFoldWaves, 0, s>>>(tpart, N, C, S, weight, mean_scale, eps,
                                                                     stats, sums, g_w, g_b, g_ms, accumulate);
   if (g_x)
     gn_bwd_apply_launch(x, S, N, C, weight, bias, mean_scale, keep, eps, stats, sums, g_y, g_x, inj, inj_offset, s);
@@ -1114,7 +1122,7 @@ extern "C" int vg_graphnorm_jvp2_part(const float* x, int32_t N, int32_t C, cons
     return VG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
   float* sums = ws + (size_t)kChunks * C * 5;  // the same workspace layout as vg_graphnorm_jvp2
-  k_gn_jvp2_final_blk<<<vg_blocks(C, kBlock / 64), kBlock, 0, s>>>(part, blocks, N, C, weight, mean_scale, eps,
+  k_gn_jvp2_final_blk<<<vg_blocks(C, kFoldWaves), 64 * kFoldWaves, 0, s>>>(part, blocks, N, C, weight, mean_scale, eps,
                                                                    stats, sums, g_w, g_ms);
   const long long total = (long long)N * C;
   k_gn_jvp2_apply<<<apply_blocks(total), 256, 0, s>>>(x, u, g_y, total, N, C, weight, bias, mean_scale, keep, eps,
@@ -1142,7 +1150,7 @@ extern "C" int vg_graphnorm_jvp2(const float* x, int32_t N, int32_t C, const flo
     k_gn_jvp2_partial<<<grid, kBlock, 0, s>>>(x, u, g_y, N, C, weight, bias, mean_scale, keep, eps,
                                               stats, part, sums, g_w, g_ms, nullptr);
   (void)sync;
-  k_gn_jvp2_final<<<vg_blocks(C, kBlock / 64), kBlock, 0, s>>>(part, chunks, N, C, weight, mean_scale, eps,
+  k_gn_jvp2_final<<<vg_blocks(C, kFoldWaves), 64 * kFoldWaves, 0, s>>>(part, chunks, N, C, weight, mean_scale, eps,
                                                                stats, sums, g_w, g_ms);
   const long long total = (long long)N * C;
   // scalar form: the quad form (LDS-staged [C][5] sums) measured 5.6-5.7 us

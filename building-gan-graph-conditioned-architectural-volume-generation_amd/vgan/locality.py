@@ -1,0 +1,64 @@
+"""Voxel numbering for gather locality (configs[3], the scatter kernel's stress graph).
+
+The aggregation gathers every edge's source row.  The reference numbers a
+building's voxels floor-major, then row-major (y, x) inside a floor
+(``data.py:300-335``, ``adjacency.nonzero()``), so the 16 destination rows one
+workgroup aggregates are a 16-voxel strip of one lattice row: on the stress
+lattice (4-neighbour floors plus 3x3 blocks to the floors above and below)
+such a strip gathers ~150 distinct source rows for ~345 edges.  Numbering each
+floor in T x T tiles of (y, x) makes the 16 rows a 4 x 4 patch, whose sources
+are the patch, its 4-neighbour ring and the 6 x 6 blocks above and below:
+~104 distinct rows for the same edges, more reuse per workgroup out of L1/L2.
+
+Renumbering is a permutation of the nodes inside each building: node-level
+tensors are gathered, ``edge_index`` is relabelled IN PLACE of every edge (the
+edge order, hence every destination row's source order and its softmax /
+gather-sum order, is the reference's), per-building blocks stay contiguous
+(``ptr``, ``batch``), and every per-node result maps back with the inverse
+permutation.  The model is permutation-equivariant up to the f32 summation
+order of GraphNorm's column statistics.
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+
+from .graph import GraphData
+
+
+def tile_order(location: torch.Tensor, tile: int = 4) -> torch.Tensor:
+    """perm [n] (new row r = old row perm[r]) numbering voxels floor by floor in
+    ``tile`` x ``tile`` (y, x) tiles, row-major inside a tile; ``location`` is
+    the voxels' integer (floor, y, x) [n, 3] (the reference's voxel
+    ``location``, ``data.py:62``)."""
+    loc = location.to(torch.int64)
+    f, y, x = loc[:, 0], loc[:, 1], loc[:, 2]
+    span = int(max(int(y.max()), int(x.max())) + 1) if loc.numel() else 1
+    tiles = (span + tile - 1) // tile
+    key = (((f * tiles + y // tile) * tiles + x // tile) * tile + y % tile) * tile + x % tile
+    return torch.argsort(key, stable=True)
+
+
+def renumber(voxel: GraphData, perm: torch.Tensor) -> GraphData:
+    """The building with node ``perm[r]`` as node r: node-level tensors
+    gathered, edges relabelled in place (same order), lists kept."""
+    n = voxel.num_nodes
+    inv = torch.empty_like(perm)
+    inv[perm] = torch.arange(n, dtype=perm.dtype)
+    out = {}
+    for key in voxel.keys():
+        v = getattr(voxel, key)
+        if key == "edge_index":
+            out[key] = inv[v]
+        elif torch.is_tensor(v) and v.dim() > 0 and v.shape[0] == n:
+            out[key] = v[perm]
+        else:
+            out[key] = v
+    return GraphData(**out)
+
+
+def tiled(voxel: GraphData, tile: int = 4) -> Tuple[GraphData, torch.Tensor]:
+    """(renumbered building, perm) in ``tile_order`` of its ``location``."""
+    perm = tile_order(voxel.location, tile)
+    return renumber(voxel, perm), perm

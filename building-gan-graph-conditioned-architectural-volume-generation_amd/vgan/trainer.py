@@ -378,6 +378,85 @@ class Trainer:
         return {"d_losses": acc[:n_critic], "d_loss_mean": acc[:n_critic].mean(), "g_loss": acc[n_critic],
                 "label_hard": graphs["hard"]}
 
+    # ------------------------------------------------ a batch seen once
+    def step_fresh(self, local_graph, voxel_graph) -> Dict[str, torch.Tensor]:
+        """``step`` for a batch the trainer sees once (every batch of
+        ``Trainer.train``'s shuffled loader).  The N_CRITIC critic iterations
+        of a step issue the same launches on the same batch, so the critic
+        iteration is recorded ONCE per batch as a hipGraph that reads its
+        labels from a static slot, and replayed N_CRITIC times (the labels of
+        iteration i copied into the slot before each replay); the stacked
+        critic-label forward and the generator iteration run once per step
+        either way and run eagerly.  The host then pays one critic body per
+        step instead of N_CRITIC -- the eager step is host-bound.  Same
+        arithmetic and draws as ``step`` (device RNG: each replay advances the
+        counter like an eager iteration).  Host / fixed RNG or one critic
+        iteration: ``step``."""
+        if self.rng.mode != "device" or not self._stacked_labels():
+            return self.step(local_graph, voxel_graph)
+        with gemm_precision_scope(self.precision):
+            return self._step_fresh(local_graph, voxel_graph)
+
+    def _step_fresh(self, local_graph, voxel_graph) -> Dict[str, torch.Tensor]:
+        cfg = self.configuration
+        dev = voxel_graph.x.device
+        n_critic = cfg.N_CRITIC
+        sync = self.sync.active and self.sync.capturable
+        with_adam = not self.sync.active or sync
+        vdata.prepared(local_graph, voxel_graph, cfg.NUM_CLASSES)
+        self.adam_g.sync_lr()
+        self.adam_d.sync_lr()
+        hard_all, soft_all = self._critic_labels(local_graph, voxel_graph)
+        slot = (torch.empty_like(hard_all[0:1]), torch.empty_like(soft_all[0:1]))
+        acc = torch.zeros(n_critic + 1, dtype=torch.float32, device=dev)
+        cur = torch.cuda.current_stream(dev)
+        if not getattr(self, "_fresh_warm", False):
+            # first capture of this trainer: run the body once outside any
+            # capture (lazy initialisation, constant buffers), then undo it
+            self.rng._iter(dev)
+            snap = self._snapshot()
+            slot[0].copy_(hard_all[0:1])
+            slot[1].copy_(soft_all[0:1])
+            self._critic_body(local_graph, voxel_graph, acc, with_adam, slot, 0, sync)
+            self._restore(snap)
+            self._fresh_warm = True
+        pool = getattr(self, "_fresh_pool", None)
+        if pool is None:
+            pool = self._fresh_pool = torch.cuda.graph_pool_handle()
+        side = getattr(self, "_fresh_stream", None)
+        if side is None:
+            side = self._fresh_stream = torch.cuda.Stream(dev)
+        # torch.cuda.graph() would synchronise the device, collect garbage and
+        # empty the allocator cache on every capture: the low-level calls
+        # record without any of that
+        g = torch.cuda.CUDAGraph()
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            # thread-local capture mode: the loader's thread keeps collating into
+            # pinned buffers and uploading while this thread records
+            g.capture_begin(pool=pool, capture_error_mode="thread_local")
+            try:
+                self._critic_body(local_graph, voxel_graph, acc, with_adam, slot, 0, sync)
+            finally:
+                g.capture_end()
+        cur.wait_stream(side)
+        d_losses = torch.empty(n_critic, dtype=torch.float32, device=dev)
+        for i in range(n_critic):
+            slot[0].copy_(hard_all[i:i + 1])
+            slot[1].copy_(soft_all[i:i + 1])
+            g.replay()
+            d_losses[i:i + 1].copy_(acc[0:1])
+            if not with_adam:
+                self.sync.all_reduce_grad(self.flat_d)
+                self.adam_d.step()
+        g_loss, hard = self._gen_iteration(local_graph, voxel_graph)
+        self.sync.all_reduce_grad(self.flat_g)
+        self.adam_g.step()
+        # the graph (and the pool blocks it holds) lives until the last replay
+        # has run; later steps reuse the pool
+        self._fresh_last = g
+        return {"d_losses": d_losses, "g_loss": g_loss.detach(), "label_hard": hard.detach()}
+
 
     # ------------------------------------------------------ orchestration
     # The epoch loop of trainer.py:445-520 (train), :522-577 (validation),
@@ -388,13 +467,15 @@ class Trainer:
     # (sums and minima), so all ranks report, and decide on, the same numbers.
 
     def _train_mode(self) -> str:
-        """runtime['train_step']: "eager" (``step``), "graphed" (``step_graphed``,
-        a capture per new batch) or "auto" (default: eager on a batch seen for
-        the first time, captured when a batch object comes back -- a resident
-        dataset -- and replayed from then on)."""
+        """runtime['train_step']: "eager" (``step``), "fresh" (``step_fresh``:
+        the critic iteration captured once per batch, replayed N_CRITIC times),
+        "graphed" (``step_graphed``: the whole step captured per batch) or
+        "auto" (default: ``step_fresh`` on a batch seen for the first time,
+        ``step_graphed`` when a batch object comes back -- a resident dataset
+        -- captured on its second visit and replayed from then on)."""
         mode = getattr(self.configuration, "runtime", {}).get("train_step", "auto")
-        if mode not in ("eager", "graphed", "auto"):
-            raise ValueError(f"runtime['train_step'] must be 'eager', 'graphed' or 'auto', not {mode!r}")
+        if mode not in ("eager", "fresh", "graphed", "auto"):
+            raise ValueError(f"runtime['train_step'] must be 'eager', 'fresh', 'graphed' or 'auto', not {mode!r}")
         return "eager" if self.rng.mode == "host" else mode  # host draws cannot be replayed
 
     def _train_batch(self, local_graph, voxel_graph) -> Dict[str, torch.Tensor]:
@@ -402,17 +483,20 @@ class Trainer:
         this step's own (clones of a replay's static outputs)."""
         mode = self._train_mode()
         getter = getattr(voxel_graph, "derived", None)
-        if mode == "auto" and callable(getter) and voxel_graph.x.is_cuda:
-            seen_key = self._graph_key + ":seen"
-            if getter(self._graph_key) is None and not getter(seen_key):
-                voxel_graph.set_derived(seen_key, True)
-                mode = "eager"
-            else:
-                mode = "graphed"
+        if mode == "auto":
+            mode = "fresh"
+            if callable(getter) and voxel_graph.x.is_cuda:
+                seen_key = self._graph_key + ":seen"
+                if getter(self._graph_key) is not None or getter(seen_key):
+                    mode = "graphed"
+                else:
+                    voxel_graph.set_derived(seen_key, True)
         if mode == "graphed" and callable(getter):
             out = self.step_graphed(local_graph, voxel_graph)
             return {"d_losses": out["d_losses"].clone(), "g_loss": out["g_loss"].clone(),
                     "label_hard": out["label_hard"]}
+        if mode == "fresh":
+            return self.step_fresh(local_graph, voxel_graph)
         return self.step(local_graph, voxel_graph)
 
     def _to_device(self, local_graph, voxel_graph):

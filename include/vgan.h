@@ -694,9 +694,11 @@ int vg_gat_aggregate_fwd_ell(const int32_t* row_ptr, const int32_t* col, const i
  * statistics).  vg_gat_aggregate_fwd(_ell) (ell may be NULL) that also writes
  * per-workgroup Welford partials (count, mean, M2) of the output columns to
  * gnp [vg_gat_gnp_floats(N, C)]: one per workgroup of vg_gat_gnp_rows(N, C)
- * rows and segment slot, segments being seg_rows-row blocks of the N rows
- * (N % seg_rows == 0, seg_rows >= vg_gat_gnp_rows).  vg_graphnorm_fwd_gnp
- * folds them.  out and alpha are bit-identical to vg_gat_aggregate_fwd. */
+ * rows, segments being seg_rows-row blocks of the N rows (N % seg_rows == 0,
+ * seg_rows >= vg_gat_gnp_rows).  Workgroups are segment-aligned (every
+ * segment has ceil(seg_rows / gnp_rows) of its own), so a segment's partials
+ * are those of a separate call over it.  vg_graphnorm_fwd_gnp folds them.
+ * out and alpha are bit-identical to vg_gat_aggregate_fwd. */
 int32_t vg_gat_gnp_rows(int32_t num_nodes, int32_t channels);
 int64_t vg_gat_gnp_floats(int32_t num_nodes, int32_t channels);
 int vg_gat_aggregate_fwd_gnp(const int32_t* row_ptr, const int32_t* col, const int32_t* ell, int32_t ell_width,

@@ -101,9 +101,13 @@ def test_b32_generator_loss_and_grads(cuda, b32):
     g_loss.backward()
     ref = float(f["g_loss"])
     assert abs(g_loss.item() - ref) <= 1e-3 * max(1.0, abs(ref))
-    ok, worst, total = grads_close({k: p.grad for k, p in G.named_parameters()}, f["g_grads"], rtol=1e-2,
-                                   total_rtol=5e-3)
-    print(f"batch 32: G gradient relative error {total:.2e}")
+    # per parameter 5e-2: a GraphNorm mean_scale gradient is -mu w A / s with A a
+    # column sum over 12.7k rows that cancels to ~1% of its terms, so its f32
+    # summation order (GPU tree vs the CPU's) shows at the percent level; the
+    # whole gradient is held to 2e-3 (measured 1.0e-3)
+    ok, worst, total = grads_close({k: p.grad for k, p in G.named_parameters()}, f["g_grads"], rtol=5e-2,
+                                   total_rtol=2e-3)
+    print(f"batch 32: G gradient relative error {total:.2e}, worst parameter {worst}")
     assert ok, (worst, total)
 
 
@@ -118,7 +122,9 @@ def test_b32_step_each_iteration_matches_oracle(cuda, b32):
     G0, D0 = R.Generator(cfg), R.Discriminator(cfg)
     sd_g = {k: v.clone() for k, v in G0.state_dict().items()}
     sd_d = {k: v.clone() for k, v in D0.state_dict().items()}
-    step_iterations_vs_oracle(cuda, cfg, sd_g, sd_d, inp["vgan"], inp["oracle"], step_seed=4242)
+    # the generator gradient per parameter at 2e-2 (the mean_scale / att_src
+    # sums over 12.7k rows, see test_b32_generator_loss_and_grads)
+    step_iterations_vs_oracle(cuda, cfg, sd_g, sd_d, inp["vgan"], inp["oracle"], step_seed=4242, g_rtol=2e-2)
 
 
 def _flat_grads(flat, module):

@@ -179,12 +179,17 @@ def test_bf16_critic_loss_and_grads_vs_f32(cuda):
     print(f"critic loss f32 {l32:.6f} bf16 {l16:.6f} bf16-autograd {la:.6f}; D grad rel err {rel_err(g16, g32):.3e} "
           f"(bf16 autograd vs f32 {rel_err(ga, g32):.3e}, bf16 engine vs bf16 autograd {rel_err(g16, ga):.3e})")
     # the fused four-pass engine and autograd's double backward through the
-    # differentiable bf16 ops round the same products: they agree to bf16's
-    # rounding (2^-9).  Measured: 7e-6 relative with the GraphNorm statistics
-    # from the chunked pass, 9.6e-4 with them from the aggregation's partials
-    # (vg_gat_aggregate_fwd_gnp: the same sums grouped differently, ~1e-7 in f32,
-    # moves the autograd path's bf16 operand roundings; the engine moves 1e-5)
-    assert abs(l16 - la) <= 2e-3 * abs(la)
+    # differentiable bf16 ops round the same products.  Round 2 measured 9.6e-4
+    # relative here (7e-6 before the aggregation's GraphNorm partials): the
+    # engine's ONE stacked real / fake / mix forward dealt partial blocks over
+    # the stacked rows, straddling the copies at copy-dependent offsets, so its
+    # statistics were the same sums grouped differently from autograd's three
+    # separate forwards -- ~1e-7 in f32, enough to flip bf16 operand roundings
+    # downstream.  The partial blocks are now segment-aligned, the statistics
+    # bitwise those of separate forwards (test_stacked_statistics_bitwise_
+    # equal_separate), and the round-1 bound holds again.
+    print(f"bf16 engine vs bf16 autograd: loss rel {abs(l16 - la) / abs(la):.2e}")
+    assert abs(l16 - la) <= 1e-4 * abs(la)
     assert rel_err(g16, ga) < 2e-2
     # against f32 the loss moves by bf16's rounding; the gradient moves more:
     # it is dominated by the penalty's second-order term (GP ~ 8 of the loss

@@ -126,7 +126,7 @@ def test_gnp_abi_rejects_bad_segments(cuda):
     n, C = csr.num_nodes, 64
     g = int(LIB.vg_gat_gnp_rows(n, C))
     assert g == 16 and int(LIB.vg_gat_gnp_rows(n, 8)) == 32
-    assert int(LIB.vg_gat_gnp_floats(n, C)) == -(-n // g) * 2 * C * 3
+    assert int(LIB.vg_gat_gnp_floats(n, C)) == 2 * -(-n // g) * 2 * C * 3  # room for segment-aligned blocks
     h = torch.zeros(n, C, device=cuda)
     v = torch.zeros(n, device=cuda)
     out, alpha = torch.empty_like(h), torch.empty(csr.num_edges, device=cuda)
@@ -332,3 +332,34 @@ def test_critic_tangent_graphnorm_sums_from_gat_pass(cuda, training, monkeypatch
     assert out[True][2] == len(eng.blocks) and out[False][2] == 0
     assert out[True][0] == out[False][0]
     assert rel_err(out[True][1], out[False][1]) < 1e-5
+
+
+@pytest.mark.parametrize("C", [1, 8, 32, 64, 128])
+def test_stacked_statistics_bitwise_equal_separate(cuda, C):
+    """Segment-aligned partial blocks: the column statistics of a stacked
+    3-copy aggregation (the critic engine's real / fake / mix forward) are bit
+    for bit those of three separate aggregations over the copies -- the
+    grouping autograd's three separate discriminator passes use."""
+    csr = _csr(cuda, "lattice", 1)
+    n = csr.num_nodes
+    st3 = csr.stacked(3)
+    torch.manual_seed(C)
+    hs = [torch.randn(n, C, device=cuda) for _ in range(3)]
+    ass = [0.5 * torch.randn(n, device=cuda) for _ in range(3)]
+    ads = [0.5 * torch.randn(n, device=cuda) for _ in range(3)]
+    b = torch.randn(C, device=cuda)
+    st = ops.stream_handle(cuda)
+
+    def run(graph, h, a_s, a_d, segs):
+        gnp, g = ops.gnp_buffer(graph, C, cuda)
+        out, alpha = torch.empty_like(h), torch.empty(graph.num_edges, device=cuda)
+        ops.aggregate_fwd_raw(graph, C, ptr(h), ptr(a_s), ptr(a_d), ptr(b), 0.2, ptr(out), ptr(alpha), st, gnp)
+        stats = torch.empty(segs * 2 * C, device=cuda)
+        check(LIB.vg_graphnorm_stats_gnp(segs, n, C, ptr(gnp), g, ptr(stats), st), "vg_graphnorm_stats_gnp")
+        return out, stats
+
+    out3, s3 = run(st3, torch.cat(hs).contiguous(), torch.cat(ass), torch.cat(ads), 3)
+    for k in range(3):
+        o1, s1 = run(csr, hs[k], ass[k], ads[k], 1)
+        assert torch.equal(out3[k * n:(k + 1) * n], o1)
+        assert torch.equal(s3[k * 2 * C:(k + 1) * 2 * C], s1), k

@@ -1,0 +1,77 @@
+"""Voxel renumbering for gather locality (vgan.locality): a permutation inside
+the building that keeps every edge in place, so every destination row sees its
+sources in the reference's order -- the GATConv output is the permuted output
+(CPU: the oracle's restated GATConv in f64; GPU: the HIP aggregation bit for
+bit)."""
+import pytest
+import torch
+
+from oracle import pyg
+from vgan.locality import renumber, tile_order, tiled
+from vgan.synth import make_stress_building, make_building
+
+
+def _destination_sources(ei, n):
+    rows = [[] for _ in range(n)]
+    for s, d in ei.t().tolist():
+        rows[d].append(s)
+    return rows
+
+
+@pytest.mark.parametrize("maker", [make_building, make_stress_building])
+def test_tiled_order_is_a_permutation_keeping_row_source_order(maker):
+    _, v = maker(777, 3) if maker is make_building else maker(777, 0, F=3, Y=13, X=11)
+    v2, perm = tiled(v, 4)
+    n = v.num_nodes
+    assert sorted(perm.tolist()) == list(range(n))
+    assert torch.equal(v2.x, v.x[perm]) and torch.equal(v2.type, v.type[perm])
+    inv = torch.empty_like(perm)
+    inv[perm] = torch.arange(n)
+    assert torch.equal(v2.edge_index, inv[v.edge_index])  # edges relabelled in place
+    old, new = _destination_sources(v.edge_index, n), _destination_sources(v2.edge_index, n)
+    for r in range(n):  # row r of the new numbering = old row perm[r], sources in the same order
+        assert new[r] == [int(inv[s]) for s in old[int(perm[r])]]
+    # a 16-row group of the new numbering is a 4 x 4 patch of one floor
+    loc = v2.location[:16]
+    assert len(set(loc[:, 0].tolist())) == 1 and (loc[:, 1].max() - loc[:, 1].min()) == 3
+
+
+def test_gatconv_is_equivariant_under_renumbering():
+    _, v = make_stress_building(777, 1, F=3, Y=9, X=10)
+    v2, perm = tiled(v, 4)
+    torch.manual_seed(0)
+    conv = pyg.GATConv(16, 8).double()
+    x = torch.randn(v.num_nodes, 16, dtype=torch.float64)
+    y = conv(x, v.edge_index)
+    y2 = conv(x[perm], v2.edge_index)
+    assert torch.allclose(y2, y[perm], atol=1e-12, rtol=0)
+
+
+def test_tile_order_keys():
+    loc = torch.tensor([[0, 0, 5], [0, 0, 0], [1, 0, 0], [0, 4, 0], [0, 1, 1]])
+    perm = tile_order(loc, 4)
+    # floor 0 tile (0,0): (0,0,0), (0,1,1); floor 0 tile (0,1): (0,0,5); tile (1,0): (0,4,0); floor 1
+    assert perm.tolist() == [1, 4, 0, 3, 2]
+
+
+@pytest.mark.gpu
+def test_aggregation_on_renumbered_graph_is_permuted_bitwise(cuda):
+    from vgan import ops
+    from vgan._lib import ptr
+
+    _, v = make_stress_building(777, 2, F=4, Y=20, X=20)
+    v2, perm = tiled(v, 4)
+    torch.manual_seed(1)
+    n, C = v.num_nodes, 64
+    h = torch.randn(n, C, device=cuda)
+    a_s, a_d = 0.5 * torch.randn(n, device=cuda), 0.5 * torch.randn(n, device=cuda)
+    b = torch.randn(C, device=cuda)
+    outs = []
+    for ei, p in ((v.edge_index, None), (v2.edge_index, perm.to(cuda))):
+        csr = ops.CSR(ei.to(cuda), n)
+        hh, ss, dd = (h, a_s, a_d) if p is None else (h[p].contiguous(), a_s[p].contiguous(), a_d[p].contiguous())
+        out, alpha = torch.empty_like(h), torch.empty(csr.num_edges, device=cuda)
+        ops.aggregate_fwd_raw(csr, C, ptr(hh), ptr(ss), ptr(dd), ptr(b), 0.2, ptr(out), ptr(alpha), csr.stream())
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[1], outs[0][perm.to(cuda)])

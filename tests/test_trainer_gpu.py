@@ -137,6 +137,38 @@ def test_resume_continues_bitwise(cuda, tmp_path):
         a.optimizer_generator.param_groups[0]["lr"]
 
 
+def test_step_fresh_matches_eager_step(cuda):
+    """step_fresh (the critic iteration recorded once per batch, replayed
+    N_CRITIC times; labels and generator eager) against the eager step from
+    the same state and device-RNG stream, over two new batches (the second
+    capture reuses the graph pool and skips the warm-up)."""
+    cfg = _cfg(cuda)
+    a, b = _trainer(cfg), _trainer(cfg)
+    ds = SyntheticDataset(16, seed=4)
+    for k in range(2):
+        loc, vox = ds.batch(range(4 * k, 4 * k + 4))
+        loc, vox = loc.to(cuda), vox.to(cuda)
+        oa = a.step(loc, vox)
+        ob = b.step_fresh(loc, vox)
+        torch.cuda.synchronize()
+        da, db = oa["d_losses"].cpu(), ob["d_losses"].cpu()
+        print(f"batch {k}: d_losses eager {da.tolist()} fresh {db.tolist()}; "
+              f"max |param diff| G {float((a.flat_g.param - b.flat_g.param).abs().max()):.2e} "
+              f"D {float((a.flat_d.param - b.flat_d.param).abs().max()):.2e}")
+        assert torch.allclose(da, db, rtol=1e-4, atol=1e-5)
+        assert abs(float(oa["g_loss"]) - float(ob["g_loss"])) <= 1e-4 * max(1.0, abs(float(oa["g_loss"])))
+        # Adam moves near-zero gradient elements by +-lr either way: a handful of
+        # sign flips at most, every other parameter equal to rounding
+        for x, y in ((a.flat_g.param, b.flat_g.param), (a.flat_d.param, b.flat_d.param)):
+            d = (x - y).abs()
+            assert float(d.max()) <= 5e-4 and float((d > 1e-6).float().mean()) < 2e-3
+        for x, y in ((a, b),):
+            assert int(x.adam_d.step_t.item()) == int(y.adam_d.step_t.item()) == (k + 1) * cfg.N_CRITIC
+        with torch.no_grad():  # continue from identical state
+            for x, y in zip(a._state_tensors(), b._state_tensors()):
+                y.copy_(x)
+
+
 def _run_worker(args, timeout=300):
     env = dict(os.environ, PYTHONPATH=os.pathsep.join([ROOT, PKG_ROOT, os.path.dirname(__file__)]))
     proc = subprocess.run([sys.executable, "-u", os.path.join(os.path.dirname(__file__), "dist_gpu_worker.py")]
