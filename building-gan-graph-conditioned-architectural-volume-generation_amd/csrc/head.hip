@@ -121,9 +121,17 @@ __global__ void __launch_bounds__(256) k_confusion(const int64_t* __restrict__ t
     if (t >= 0 && t < K) atomicAdd(&cm[t * K + p], 1);
   }
   __syncthreads();
-  for (int t = threadIdx.x; t < K * K; t += blockDim.x) {
-    conf[(size_t)gi * K * K + t] = cm[t];
-    if (conf_all && cm[t]) atomicAdd(&conf_all[t], cm[t]);
+  for (int t = threadIdx.x; t < K * K; t += blockDim.x) conf[(size_t)gi * K * K + t] = cm[t];
+}
+
+// The whole batch's matrix: per entry the sum over the buildings in order
+// (no memset node and no atomics in a captured evaluation graph; deterministic).
+__global__ void __launch_bounds__(64) k_confusion_all(const int32_t* __restrict__ conf, int G, int KK,
+                                                      int32_t* __restrict__ conf_all) {
+  for (int t = threadIdx.x; t < KK; t += blockDim.x) {
+    int32_t s = 0;
+    for (int g = 0; g < G; ++g) s += conf[(size_t)g * KK + t];
+    conf_all[t] = s;
   }
 }
 
@@ -364,8 +372,8 @@ extern "C" int vg_confusion(const int64_t* truth, const float* label, int32_t cl
       !conf)
     return VG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (conf_all) (void)hipMemsetAsync(conf_all, 0, sizeof(int32_t) * classes * classes, s);
   k_confusion<<<num_graphs, 256, 0, s>>>(truth, label, classes, ptr, conf, conf_all);
+  if (conf_all) k_confusion_all<<<1, 64, 0, s>>>(conf, num_graphs, classes * classes, conf_all);
   VG_CHECK_LAUNCH();
   return 0;
 }

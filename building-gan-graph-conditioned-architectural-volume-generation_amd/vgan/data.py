@@ -35,7 +35,10 @@ class Prepared:
     onehot_f: torch.Tensor
 
 
-_FALLBACK_CACHE: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+# batch objects without a ``derived`` store (a reference PyG Batch): keyed by
+# id(voxel_graph.x), the entry dropped when that tensor dies (a
+# WeakKeyDictionary would compare tensors with ``==``)
+_FALLBACK_CACHE = {}
 
 
 def _tensor_key(t):
@@ -99,8 +102,11 @@ def prepared(local_graph, voxel_graph, n_classes: int) -> Prepared:
             hit = (key, _build(local_graph, voxel_graph, n_classes))
             voxel_graph.set_derived("prepared", hit)
         return hit[1]
-    hit = _FALLBACK_CACHE.get(voxel_graph.x)
+    anchor = voxel_graph.x
+    hit = _FALLBACK_CACHE.get(id(anchor))
     if hit is None or hit[0] != key:
+        if hit is None:
+            weakref.finalize(anchor, _FALLBACK_CACHE.pop, id(anchor), None)
         hit = (key, _build(local_graph, voxel_graph, n_classes))
-        _FALLBACK_CACHE[voxel_graph.x] = hit
+        _FALLBACK_CACHE[id(anchor)] = hit
     return hit[1]

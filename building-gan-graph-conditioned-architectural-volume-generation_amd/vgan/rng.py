@@ -53,11 +53,16 @@ class RNG:
         self._fixed = {}
         self._salt = 0
         self._iters: Dict[torch.device, torch.Tensor] = {}
+        self._early = 0  # resets before the device counter existed (it starts there)
 
     def reset(self) -> None:
-        """Start of an iteration body (fixed draws restart; device masks advance)."""
+        """Start of an iteration body (fixed draws restart; device masks advance).
+        The device counter counts resets whenever it is created, so an eager
+        body and a captured one draw the same numbers from the same state."""
         self._k = 0
         self._salt = 0
+        if not self._iters:
+            self._early += 1
         for t in self._iters.values():
             t.add_(1)
 
@@ -72,6 +77,7 @@ class RNG:
             return  # another randomness source: nothing to continue
         self.seed = int(state["seed"])
         self._pending_iter = int(state["iter"])
+        self._early = 0
         for t in self._iters.values():
             t.fill_(self._pending_iter)
 
@@ -79,8 +85,8 @@ class RNG:
         device = torch.device(device)
         t = self._iters.get(device)
         if t is None:
-            t = self._iters[device] = torch.full((1,), getattr(self, "_pending_iter", 0), dtype=torch.int64,
-                                                 device=device)
+            t = self._iters[device] = torch.full((1,), getattr(self, "_pending_iter", 0) + self._early,
+                                                 dtype=torch.int64, device=device)
         return t
 
     def _fixed_draw(self, kind: str, shape, device, make):

@@ -191,3 +191,63 @@ def test_b32_graphed_step_matches_eager(cuda, b32):
     # and whole graphed steps keep training sanely at this size
     outs = [graphed.step_graphed(loc, vox) for _ in range(2)]
     assert all(torch.isfinite(o["d_losses"]).all() and torch.isfinite(o["g_loss"]) for o in outs)
+
+
+def test_b32_f16_sweep_forward_against_reference(cuda, b32):
+    """configs[4]'s precision against the reference itself, not the f32 HIP
+    path: the f16 generator forward (vgan.half, the inference sweep's) on the
+    batch-32 fixture inputs vs the reference-executed logits.  f16 storage
+    rounding compounds through 14 GAT blocks and a 1-channel bottleneck
+    (tests/test_half_gpu.py): RMS relative error of the logits <= 3e-2,
+    sampled types (argmax of logits + the same Gumbel noise) agreeing on >= 98%
+    of the 12.7k voxels, argmax of the logits on >= 98%."""
+    from vgan.half import HalfGenerator
+
+    f, inp = b32
+    cfg = Configuration()
+    G, _ = _models(cfg, f)
+    G.eval()
+    loc, vox = inp["vgan"]
+    hg = HalfGenerator(G)
+    with torch.no_grad():
+        logits, hard, _ = hg(loc, vox, inp["z"].to(cuda), noise=inp["noise"].to(cuda), tau=1.0)
+    ref = f["logits"]
+    got = logits.reshape(ref.shape).float().cpu()
+    rms = float((got - ref).pow(2).mean().sqrt() / ref.pow(2).mean().sqrt())
+    agree_hard = float((hard.reshape(ref.shape).cpu().argmax(1).to(torch.int8) == f["label_argmax"]).float().mean())
+    agree_logit = float((got.argmax(1) == ref.argmax(1)).float().mean())
+    print(f"batch 32 f16 vs reference: logits RMS rel err {rms:.2e}, sampled-type agreement {agree_hard:.4f}, "
+          f"logit argmax agreement {agree_logit:.4f}")
+    assert rms <= 3e-2 and agree_hard >= 0.98 and agree_logit >= 0.98
+
+
+def test_prepared_cache_keys_on_both_graphs(cuda, b32):
+    """The per-batch structures (type-matched mean, CSR) are rebuilt when the
+    voxel batch is paired with another program batch or an input is edited in
+    place -- for a GraphBatch and for any other batch object (a reference PyG
+    Batch), whose cache is keyed on the tensors' identity and versions."""
+    import types
+
+    from vgan import data as vdata
+    from vgan import ops
+
+    f, inp = b32
+    loc, vox = inp["vgan"]
+    loc2 = types.SimpleNamespace(x=loc.x.flip(0).contiguous(), type=loc.type.flip(0).contiguous())
+    loc2.x[:, :7] = loc2.x[:, :7] * 0.5  # other program features
+
+    def expect(l):
+        out = torch.empty(vox.num_nodes, l.x.shape[1], device=cuda)
+        ops.type_mean(l.x.float().contiguous(), l.type, vox.type, 7, out=out, col0=0)
+        return out
+
+    for v in (vox, types.SimpleNamespace(x=vox.x.clone(), type=vox.type, types_onehot=vox.types_onehot,
+                                         edge_index=vox.edge_index, num_nodes=vox.num_nodes)):
+        p1 = vdata.prepared(loc, v, 7)
+        assert torch.equal(p1.matched_x, expect(loc))
+        assert vdata.prepared(loc, v, 7) is p1  # cached
+        p2 = vdata.prepared(loc2, v, 7)
+        assert p2 is not p1 and torch.equal(p2.matched_x, expect(loc2))
+        loc2.x.mul_(2.0)  # in-place edit: version bump
+        p3 = vdata.prepared(loc2, v, 7)
+        assert p3 is not p2 and torch.equal(p3.matched_x, expect(loc2))
