@@ -200,6 +200,8 @@ SIGNATURES = {
     "vg_graphnorm_jvp2_part": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p,
                                               _c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_p]),
     "vg_linear_chain": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p]),
+    "vg_graph_exec_update": (ctypes.c_int, [_c_p, _c_p]),
+    "vg_graph_launch": (ctypes.c_int, [_c_p, _c_p]),
     "vg_linear_chain_bf16": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p]),
     "vg_gat_gnp_rows": (_c_i32, [_c_i32, _c_i32]),
     "vg_gat_gnp_floats": (_c_i64, [_c_i32, _c_i32]),

@@ -27,6 +27,7 @@ Differences that do not change results:
 """
 from __future__ import annotations
 
+import ctypes
 import datetime
 import itertools
 import os
@@ -40,13 +41,17 @@ import torch.nn.functional as F
 from . import data as vdata
 from . import metrics as vmetrics
 from . import ops
-from ._lib import gemm_precision_scope
+from ._lib import LIB, check, gemm_precision_scope, stream_handle
 from .critic import CriticEngine
 from .dist import GradSync
 from .flat import FlatAdam, FlatParams
+from .genstep import GeneratorEngine
 from .rng import RNG
 
 _TRAINER_IDS = itertools.count()
+# VGAN_FRESH_UPDATE=0: instantiate every fresh batch's critic graph (A/B knob)
+_FRESH_UPDATE = os.environ.get("VGAN_FRESH_UPDATE", "1") == "1"
+_FRESH_KEEP = int(os.environ.get("VGAN_FRESH_KEEP", "256"))  # recorded graphs released per batch
 
 
 class Trainer:
@@ -81,12 +86,18 @@ class Trainer:
         self.sync.broadcast_params(self.flat_g)
         self.sync.broadcast_params(self.flat_d)
         self.skip_dead_d_grads = runtime.get("skip_dead_d_grads", True)
+        self.phase_hook = None  # callable(name) marking host-side phase ends (profiling only)
         # critic iterations: the explicit four-pass engine (vgan/critic.py) or
         # autograd double backward through the differentiable HIP ops
         # (vg_gp_head holds a row's classes in registers: K <= 32)
         use_engine = (runtime.get("critic", "engine") == "engine" and getattr(configuration, "USE_WGANGP", True)
                       and int(configuration.NUM_CLASSES) <= 32)
         self.critic = CriticEngine(discriminator, configuration) if use_engine else None
+        # generator iteration: the explicit schedule (vgan/genstep.py) or
+        # autograd through the differentiable HIP ops
+        gen = GeneratorEngine(generator, discriminator, configuration) \
+            if runtime.get("gen", os.environ.get("VGAN_GEN", "engine")) == "engine" else None
+        self.gen_engine = gen if gen is not None and gen.supported else None
         self.states = {"epoch_start": 1, "epoch_end": int(configuration.EPOCHS) + 1, "best_f1_score": 0}
         # resume (trainer.py:628-636): a states.pt in log_dir -- written by this
         # trainer or by the reference's -- restores models, optimizers, scheduler
@@ -210,6 +221,9 @@ class Trainer:
 
     def _gen_iteration(self, local_graph, voxel_graph):
         self.rng.reset()
+        if self.gen_engine is not None and self.skip_dead_d_grads:
+            self.adam_g.zero_grad()
+            return self.gen_engine.loss_and_grad(local_graph, voxel_graph, self.rng)
         logits, hard, _ = self._generate(local_graph, voxel_graph)
         self.adam_g.zero_grad()
         d_params = list(self.discriminator.parameters())
@@ -403,10 +417,13 @@ class Trainer:
         n_critic = cfg.N_CRITIC
         sync = self.sync.active and self.sync.capturable
         with_adam = not self.sync.active or sync
+        mark = self.phase_hook or (lambda name: None)  # host-time probes (tools/host_profile.py)
         vdata.prepared(local_graph, voxel_graph, cfg.NUM_CLASSES)
         self.adam_g.sync_lr()
         self.adam_d.sync_lr()
+        mark("prepare")
         hard_all, soft_all = self._critic_labels(local_graph, voxel_graph)
+        mark("labels")
         slot = (torch.empty_like(hard_all[0:1]), torch.empty_like(soft_all[0:1]))
         acc = torch.zeros(n_critic + 1, dtype=torch.float32, device=dev)
         cur = torch.cuda.current_stream(dev)
@@ -428,8 +445,11 @@ class Trainer:
             side = self._fresh_stream = torch.cuda.Stream(dev)
         # torch.cuda.graph() would synchronise the device, collect garbage and
         # empty the allocator cache on every capture: the low-level calls
-        # record without any of that
-        g = torch.cuda.CUDAGraph()
+        # record without any of that.  The recorded graph is kept
+        # uninstantiated: it updates the one executable graph in place
+        # (vg_graph_exec_update) -- instantiating a graph per batch and
+        # destroying the previous one cost ~3 ms of host time per step
+        g = torch.cuda.CUDAGraph(keep_graph=True)
         side.wait_stream(cur)
         with torch.cuda.stream(side):
             # thread-local capture mode: the loader's thread keeps collating into
@@ -440,21 +460,43 @@ class Trainer:
             finally:
                 g.capture_end()
         cur.wait_stream(side)
+        owner = getattr(self, "_fresh_owner", None)
+        if owner is None or not _FRESH_UPDATE or \
+                LIB.vg_graph_exec_update(ctypes.c_void_p(owner.raw_cuda_graph_exec()),
+                                         ctypes.c_void_p(g.raw_cuda_graph())) != 0:
+            g.instantiate()  # first batch, or a launch sequence of another shape
+            if owner is not None:
+                self.__dict__.setdefault("_fresh_dead", []).append(owner)
+            owner = self._fresh_owner = g
+        exec_ = ctypes.c_void_p(owner.raw_cuda_graph_exec())
+        mark("capture")
         d_losses = torch.empty(n_critic, dtype=torch.float32, device=dev)
+        st = stream_handle(dev)
         for i in range(n_critic):
             slot[0].copy_(hard_all[i:i + 1])
             slot[1].copy_(soft_all[i:i + 1])
-            g.replay()
+            check(LIB.vg_graph_launch(exec_, st), "vg_graph_launch")
             d_losses[i:i + 1].copy_(acc[0:1])
             if not with_adam:
                 self.sync.all_reduce_grad(self.flat_d)
                 self.adam_d.step()
+        mark("replays")
         g_loss, hard = self._gen_iteration(local_graph, voxel_graph)
         self.sync.all_reduce_grad(self.flat_g)
         self.adam_g.step()
-        # the graph (and the pool blocks it holds) lives until the last replay
-        # has run; later steps reuse the pool
-        self._fresh_last = g
+        mark("gen")
+        # Recorded graphs are released in batches: destroying one while the
+        # device is busy blocks the runtime (every thread's launches) for ~8 ms
+        # (tools/graph_destroy_probe.py; ~0.3 ms on an idle device), so they
+        # are kept until _FRESH_KEEP have gathered and destroyed after one
+        # device synchronisation
+        if g is not owner:
+            dead = self.__dict__.setdefault("_fresh_dead", [])
+            dead.append(g)
+            if len(dead) >= _FRESH_KEEP:
+                torch.cuda.synchronize(dev)
+                dead.clear()
+        mark("release")
         return {"d_losses": d_losses, "g_loss": g_loss.detach(), "label_hard": hard.detach()}
 
 

@@ -33,6 +33,8 @@ extern "C" {
 #endif
 
 #define VG_EINVAL (-1)
+/* vg_graph_exec_update: the recorded graph differs in topology (instantiate it instead). */
+#define VG_EGRAPH_TOPOLOGY (-2)
 
 /* ---- graph structure ---------------------------------------------------- */
 
@@ -882,6 +884,19 @@ int vg_hgat_fwd(const int32_t* row_ptr, const int32_t* col, int32_t n, int32_t c
 int vg_graphnorm_fwd_h(const uint16_t* x, int32_t ld, int32_t S, int32_t N, int32_t C,
                        const float* weight, const float* bias, const float* mean_scale, float eps,
                        uint16_t* y, int32_t ldy, float* stats, float* ws, void* stream);
+
+/* ---- step-graph re-use (host runtime calls, no kernels) ------------------- */
+
+/* Update the executable graph `exec` (a hipGraphExec_t) in place from the
+ * recorded graph `graph` (a hipGraph_t of the same launch sequence: other
+ * pointers, sizes and grid dimensions): the critic iteration Trainer.step_fresh
+ * records per fresh batch (trainer.py:466-481, one iteration body).  0 on
+ * success; VG_EGRAPH_TOPOLOGY when the runtime refuses the update (no error
+ * state is left behind; instantiate `graph` instead). */
+int vg_graph_exec_update(void* exec, void* graph);
+
+/* hipGraphLaunch(exec, stream). */
+int vg_graph_launch(void* exec, void* stream);
 
 #ifdef __cplusplus
 }

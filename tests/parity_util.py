@@ -221,21 +221,29 @@ def step_iterations_vs_oracle(cuda, cfg, g0, d0, vgan_pair, oracle_pair, step_se
             for p, q in zip(D.parameters(), Do.parameters()):
                 p.copy_(q.to(p.device))
     state = torch.get_rng_state()
-    tr.adam_g.zero_grad()
-    logits, hard, _ = tr._generate(loc, vox)
-    g_loss = tr._compute_generator_loss(loc, vox, logits, hard)
-    g_loss.backward()
-    torch.set_rng_state(state)
     Go.zero_grad()
     lo, ho, _ = Go(ol, ov, torch.randn(1, ov.num_nodes, cfg.Z_DIM))
     g_ref = R.generator_loss(Do, cfg, ol, ov, lo, ho.unsqueeze(0))
     g_ref.backward()
-    assert abs(g_loss.item() - g_ref.item()) <= 1e-4 * max(1.0, abs(g_ref.item()))
-    # the G gradient flows through D(label_hard): same ReLU-kink sensitivity as above
-    ok, worst, total = grads_close({k: p.grad for k, p in G.named_parameters()},
-                                   {k: p.grad for k, p in Go.named_parameters()}, rtol=g_rtol, total_rtol=5e-3)
-    print(f"generator iteration: G gradient relative error {total:.2e}, worst parameter {worst}")
-    assert ok, (worst, total)
+    ref_grads = {k: p.grad for k, p in Go.named_parameters()}
+    # the generator iteration through autograd, then through the explicit
+    # schedule the trainer runs (vgan/genstep.py), each from the same CPU draws
+    paths = ["autograd"] + (["engine"] if tr.gen_engine is not None else [])
+    for path in paths:
+        torch.set_rng_state(state)
+        tr.adam_g.zero_grad()
+        if path == "engine":
+            g_loss, hard = tr._gen_iteration(loc, vox)
+        else:
+            logits, hard, _ = tr._generate(loc, vox)
+            g_loss = tr._compute_generator_loss(loc, vox, logits, hard)
+            g_loss.backward()
+        assert abs(g_loss.item() - g_ref.item()) <= 1e-4 * max(1.0, abs(g_ref.item())), (path, g_loss.item())
+        # the G gradient flows through D(label_hard): same ReLU-kink sensitivity as above
+        ok, worst, total = grads_close({k: p.grad for k, p in G.named_parameters()}, ref_grads, rtol=g_rtol,
+                                       total_rtol=5e-3)
+        print(f"generator iteration ({path}): G gradient relative error {total:.2e}, worst parameter {worst}")
+        assert ok, (path, worst, total)
 
 
 def run_smoke() -> None:

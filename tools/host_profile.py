@@ -30,6 +30,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--sort", default="tottime")
+    ap.add_argument("--fresh", action="store_true",
+                    help="profile step_fresh (the fresh-batch path) over distinct staged batches")
     ap.add_argument("--top", type=int, default=45)
     args = ap.parse_args()
     import bench
@@ -44,6 +46,8 @@ def main():
     torch.manual_seed(cfg.SEED)
     pool = bench.make_pool(cfg, 0, 1, 1, 32, dev)
     tr = bench.build_trainer(cfg, "f32")
+    if args.fresh:
+        return fresh(args, cfg, tr, bench, dev)
     loc, vox = pool[0]
     for _ in range(3):
         tr.step(loc, vox)
@@ -76,6 +80,55 @@ def main():
     pr.enable()
     for _ in range(args.steps):
         tr.step(loc, vox)
+    pr.disable()
+    torch.cuda.synchronize()
+    s = io.StringIO()
+    pstats.Stats(pr, stream=s).sort_stats(args.sort).print_stats(args.top)
+    print(s.getvalue())
+
+
+def fresh(args, cfg, tr, bench, dev):
+    """Host time per phase of step_fresh (marks from Trainer.phase_hook), the
+    device drained only between steps, then cProfile over whole steps."""
+    pool = bench.make_pool(cfg, 0, 1, 8, 32, dev)
+    for k in range(3):
+        tr.step_fresh(*pool[k % len(pool)])
+    torch.cuda.synchronize()
+    times = {}
+    last = [0.0]
+
+    def mark(name):
+        now = time.perf_counter()
+        times.setdefault(name, []).append(now - last[0])
+        last[0] = now
+
+    tr.phase_hook = mark
+    totals = []
+    for k in range(args.steps):
+        torch.cuda.synchronize()
+        t0 = last[0] = time.perf_counter()
+        tr.step_fresh(*pool[k % len(pool)])
+        t1 = time.perf_counter()
+        torch.cuda.synchronize()
+        totals.append((t1 - t0, time.perf_counter() - t0))
+    tr.phase_hook = None
+    for name, v in times.items():
+        v = sorted(v)
+        print(f"host {name:8s}: median {v[len(v) // 2] * 1e3:7.3f} ms")
+    enq = sorted(t for t, _ in totals)
+    full = sorted(t for _, t in totals)
+    print(f"host enqueue total: median {enq[len(enq) // 2] * 1e3:7.3f} ms; with device drain {full[len(full) // 2] * 1e3:7.3f} ms")
+    # back-to-back steps (no drain between): the rate the fresh-batch leg sees
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        tr.step_fresh(*pool[k % len(pool)])
+    torch.cuda.synchronize()
+    print(f"back-to-back step_fresh: {(time.perf_counter() - t0) / args.steps * 1e3:.3f} ms/step")
+    pr = cProfile.Profile()
+    pr.enable()
+    for k in range(args.steps):
+        tr.step_fresh(*pool[k % len(pool)])
     pr.disable()
     torch.cuda.synchronize()
     s = io.StringIO()
