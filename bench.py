@@ -146,6 +146,101 @@ def aggregate_roofline(tr, csr, device, reps: int = 20, gnp: bool = False):
             "avg_extra_written_bytes": extra / launches}
 
 
+F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense f32-input MFMA (v_mfma_f32_32x32x2_f32)
+
+
+def step_gemm_calls(tr, n: int):
+    """The step's k_gemm16 products (one f32 step at n voxel rows): every
+    GATConv projection with its attention projections (vg_gat_lin_att) and
+    every GATConv input gradient dX = dH W (vg_gemm NN; the step forms most
+    of them with vg_gemm_gn_bwd, the same tiles plus the GraphNorm partials).
+    (kind, rows, cin, cout) per launch, in step order."""
+    cfg = tr.configuration
+    k = cfg.N_CRITIC
+    dw = [(conv.in_channels, conv.out_channels) for conv, _ in tr.critic.blocks]
+    G = tr.generator
+    gw = [(getattr(G.encoder, f"module_{4 * b}").in_channels, getattr(G.encoder, f"module_{4 * b}").out_channels)
+          for b in range(G.encoder.num_blocks)]
+    calls = [("att", k * n, ci, co) for ci, co in gw]  # stacked critic-label forward
+    for _ in range(k):  # critic iterations: passes A (3 copies), B, C, D (3 copies)
+        calls += [("att", 3 * n, ci, co) for ci, co in dw]
+        calls += [("nn", n, co, ci) for ci, co in reversed(dw[1:])]
+        calls += [("att", n, ci, co) for ci, co in dw]
+        calls += [("nn", 3 * n, co, ci) for ci, co in reversed(dw[1:])]
+    calls += [("att", n, ci, co) for ci, co in gw + dw]  # generator iteration: G and D forward
+    calls += [("nn", n, co, ci) for ci, co in reversed(dw[1:])] + [("nn", n, co, ci) for ci, co in reversed(gw[1:])]
+    return calls
+
+
+def gemm_family_roofline(tr, n: int, device, reps: int = 20):
+    """The dense-product family (k_gemm16) as the step launches it: the shapes
+    of step_gemm_calls, captured in one hipGraph and replayed between HIP
+    events.  FLOPs 2 * rows * cin * cout; compulsory bytes the operand rows,
+    the output rows, the weight (and a_src / a_dst for the projections)."""
+    from vgan._lib import check, dense, ptr, stream_handle
+
+    calls = step_gemm_calls(tr, n)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(4321)
+    bufs = {}
+    for kind, rows, ci, co in calls:
+        key = (kind, rows, ci, co)
+        if key in bufs:
+            continue
+        if kind == "att":
+            bufs[key] = (torch.randn(rows, ci, device=device, generator=gen),
+                         torch.randn(co, ci, device=device, generator=gen),
+                         torch.randn(co, device=device, generator=gen), torch.randn(co, device=device, generator=gen),
+                         torch.empty(rows, co, device=device), torch.empty(rows, device=device),
+                         torch.empty(rows, device=device))
+        else:  # dX [rows, co_in] = dH [rows, ci] W [ci, co_in] with (ci, co) = (c, cin)
+            bufs[key] = (torch.randn(rows, ci, device=device, generator=gen),
+                         torch.randn(ci, co, device=device, generator=gen), torch.empty(rows, co, device=device))
+
+    def launch_all():
+        st = stream_handle(device)
+        for kind, rows, ci, co in calls:
+            b = bufs[(kind, rows, ci, co)]
+            if kind == "att":
+                x, w, vs, vd, h, a_s, a_d = b
+                check(dense("vg_gat_lin_att")(ptr(x), ci, ptr(w), rows, ci, co, ptr(vs), ptr(vd), ptr(h), ptr(a_s),
+                                              ptr(a_d), st), "vg_gat_lin_att")
+            else:
+                a, w, out = b
+                check(dense("vg_gemm")(ptr(a), ci, ptr(w), co, 0, None, 0, None, 0, ptr(out), co, rows, co, ci, st),
+                      "vg_gemm")
+
+    side = torch.cuda.Stream(device)
+    side.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(side):
+        launch_all()
+    torch.cuda.current_stream(device).wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        launch_all()
+    g.replay()
+    torch.cuda.synchronize()
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    st.record()
+    for _ in range(reps):
+        g.replay()
+    en.record()
+    torch.cuda.synchronize()
+    sec = st.elapsed_time(en) * 1e-3
+    flops = reps * sum(2.0 * rows * ci * co for _, rows, ci, co in calls)
+    nbytes = reps * sum(4.0 * (rows * ci + rows * co + ci * co + (2 * rows if kind == "att" else 0))
+                        for kind, rows, ci, co in calls)
+    launches = reps * len(calls)
+    return {"kernel": "k_gemm16 family (vg_gat_lin_att projections + dX products at the step's shapes)",
+            "launches_per_step": len(calls), "avg_launch_us": round(sec * 1e6 / launches, 3),
+            "achieved_tflops": round(flops / sec / 1e12, 3),
+            "frac_of_f32_mfma": round(flops / sec / 1e12 / F32_MFMA_PEAK_TFLOPS, 5),
+            "f32_mfma_peak_tflops": F32_MFMA_PEAK_TFLOPS,
+            "achieved_gbs": round(nbytes / sec / 1e9, 2), "frac_of_hbm": round(nbytes / sec / 1e9 / HBM_PEAK_GBS, 5),
+            "avg_flops": int(flops / launches), "avg_compulsory_bytes": int(nbytes / launches),
+            "timing": "hipGraph-replayed between HIP events on the replay stream (f32 operands)"}
+
+
 def load_pmc_traffic(name: str = "r03_pmc_aggregate_gnp.json"):
     """Per-launch HBM-side bytes of the scatter kernel from the committed
     rocprofv3 PMC summary of the variant the step runs (tools/pmc_roofline.sh
@@ -601,6 +696,11 @@ def main():
         log(f"vg_gat_aggregate_fwd_gnp: avg {kern_gnp['avg_us']:.2f} us, {kern_gnp['achieved_gbs']:.1f} GB/s")
     head = kern_gnp or kern
     traffic, traffic_src = load_pmc_traffic()
+    gemms = gemm_family_roofline(tr, csr0.num_nodes, device, reps=max(args.steps, 10)) \
+        if args.precision == "f32" and tr.critic is not None else None
+    if gemms:
+        log(f"k_gemm16 family: {gemms['launches_per_step']} launches, avg {gemms['avg_launch_us']:.2f} us, "
+            f"{gemms['achieved_tflops']:.2f} TFLOP/s, {gemms['achieved_gbs']:.0f} GB/s")
     # what Trainer.train() delivers: a new batch from the native loader every step
     fresh = None
     if not args.no_fresh:
@@ -676,6 +776,8 @@ def main():
             },
             "cpu_baseline": cpu,
         }
+        if gemms:
+            result["gemm_family"] = gemms
         if fresh:
             result["fresh_batch_ms_per_step"] = fresh["ms_per_step"]
             result["fresh_batch"] = fresh
