@@ -126,7 +126,7 @@ def aggregate_roofline(tr, csr, device, reps: int = 20, gnp: bool = False):
         launch_all()
     torch.cuda.current_stream(device).wait_stream(side)
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
         launch_all()
     g.replay()
     torch.cuda.synchronize()
@@ -216,7 +216,7 @@ def gemm_family_roofline(tr, n: int, device, reps: int = 20):
         launch_all()
     torch.cuda.current_stream(device).wait_stream(side)
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
         launch_all()
     g.replay()
     torch.cuda.synchronize()
@@ -513,7 +513,7 @@ def sweep_leg(device, graphs: int = 10000, batch: int = 32, n_taus: int = 10, di
         launch_all()
     torch.cuda.current_stream(device).wait_stream(side)
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
         launch_all()
     g.replay()
     torch.cuda.synchronize()

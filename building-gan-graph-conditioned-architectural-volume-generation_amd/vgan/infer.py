@@ -118,7 +118,7 @@ class InferenceSweep:
                     self._forward(local_graph, voxel_graph)
                 torch.cuda.current_stream(dev).wait_stream(side)
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=self._pool):
+                with torch.cuda.graph(g, pool=self._pool, capture_error_mode="thread_local"):
                     out = self._forward(local_graph, voxel_graph)
                 cached = (self, g, out)
                 voxel_graph.set_derived("sweep_graph", cached)

@@ -344,16 +344,16 @@ class Trainer:
         g_labels, labels = None, None
         if stacked:
             g_labels = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g_labels, pool=pool):
+            with torch.cuda.graph(g_labels, pool=pool, capture_error_mode="thread_local"):
                 labels = self._critic_labels(local_graph, voxel_graph)
         critic = []
         for i in range(n_critic if stacked else 1):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
+            with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
                 self._critic_body(local_graph, voxel_graph, acc, with_adam, labels, i, sync)
             critic.append(g)
         g_gen = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g_gen, pool=pool):
+        with torch.cuda.graph(g_gen, pool=pool, capture_error_mode="thread_local"):
             hard = self._gen_body(local_graph, voxel_graph, acc, with_adam, sync)
         self._restore(snap)
         graphs = {"labels": g_labels, "label_tensors": labels, "critic": critic, "gen": g_gen, "acc": acc,
@@ -654,7 +654,7 @@ class Trainer:
                 self._eval_body(local_graph, voxel_graph, with_loss)
             torch.cuda.current_stream(dev).wait_stream(side)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
+            with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
                 outs = self._eval_body(local_graph, voxel_graph, with_loss)
             cached = (g, outs)
             voxel_graph.set_derived(key, cached)
