@@ -54,6 +54,19 @@ def agg_bytes(n: int, e: int, c: int, elem: int = 4) -> int:
     return 2 * n * c * elem + 4 * (2 * n + e + (n + 1))
 
 
+L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md: L2 (8 x 4 MiB) aggregate
+L2_GATHER_GBS = 18800.0  # MI355X_MICROARCH.md: rows gathered from the XCD's L2, measured ceiling (16.8-18.8 TB/s)
+
+
+def agg_gather_bytes(n: int, e: int, c: int, elem: int = 4) -> int:
+    """Bytes the aggregation moves between L2 and the CUs: every edge's whole
+    source row (E' * C), its column index and a_src entry, the output row and
+    the per-row operands.  The HBM compulsory bytes (agg_bytes) count each
+    source row once; the gather reads it once per edge (~6.2x at batch 32,
+    ~21.6x on the stress graph), from L2 / the Infinity Cache."""
+    return e * c * elem + 4 * 2 * e + n * c * elem + 4 * (2 * n + (n + 1))
+
+
 def agg_extra_bytes(n: int, e: int) -> int:
     """alpha [E'] f32, written for the backward (not in agg_bytes)."""
     return 4 * e
@@ -139,11 +152,13 @@ def aggregate_roofline(tr, csr, device, reps: int = 20, gnp: bool = False):
     total_ms = st.elapsed_time(en)
     launches = reps * len(calls)
     nbytes = reps * sum(agg_bytes(c_csr.num_nodes, c_csr.num_edges, c) for c_csr, c in calls)
+    gbytes = reps * sum(agg_gather_bytes(c_csr.num_nodes, c_csr.num_edges, c) for c_csr, c in calls)
     extra = reps * sum(agg_extra_bytes(c_csr.num_nodes, c_csr.num_edges) + (gnp_bytes(c_csr, c) if gnp else 0)
                        for c_csr, c in calls)
     return {"launches": launches, "launches_per_step": len(calls), "avg_us": total_ms * 1e3 / launches,
             "avg_bytes": nbytes / launches, "achieved_gbs": nbytes / (total_ms * 1e-3) / 1e9,
-            "avg_extra_written_bytes": extra / launches}
+            "avg_extra_written_bytes": extra / launches, "gather_gbs": gbytes / (total_ms * 1e-3) / 1e9,
+            "avg_gather_bytes": gbytes / launches}
 
 
 F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense f32-input MFMA (v_mfma_f32_32x32x2_f32)
@@ -375,9 +390,10 @@ def stress_roofline(device, channels=(128, 64, 1), reps: int = 20, order: str = 
                 times.append(st.elapsed_time(en))
             return sum(times) / len(times)
 
-        b = agg_bytes(n, e, c)
+        b, gb = agg_bytes(n, e, c), agg_gather_bytes(n, e, c)
         avg = timed(run)
-        res[c] = {"avg_us": avg * 1e3, "bytes": b, "achieved_gbs": b / (avg * 1e-3) / 1e9}
+        res[c] = {"avg_us": avg * 1e3, "bytes": b, "achieved_gbs": b / (avg * 1e-3) / 1e9,
+                  "gather_gbs": gb / (avg * 1e-3) / 1e9}
         if c % 64 == 0:
             avg = timed(run_lds)
             res_lds[c] = {"avg_us": avg * 1e3, "bytes": b, "achieved_gbs": b / (avg * 1e-3) / 1e9}
@@ -693,7 +709,8 @@ def main():
         f"{kern['achieved_gbs']:.1f} GB/s")
     kern_gnp = aggregate_roofline(tr, csr0, device, reps=max(args.steps, 10), gnp=True)
     if kern_gnp:
-        log(f"vg_gat_aggregate_fwd_gnp: avg {kern_gnp['avg_us']:.2f} us, {kern_gnp['achieved_gbs']:.1f} GB/s")
+        log(f"vg_gat_aggregate_fwd_gnp: avg {kern_gnp['avg_us']:.2f} us, {kern_gnp['achieved_gbs']:.1f} GB/s "
+            f"(HBM bytes), {kern_gnp['gather_gbs']:.0f} GB/s L2 gather")
     head = kern_gnp or kern
     traffic, traffic_src = load_pmc_traffic()
     gemms = gemm_family_roofline(tr, csr0.num_nodes, device, reps=max(args.steps, 10)) \
@@ -712,7 +729,8 @@ def main():
         stress_orders = {} if args.no_stress else {o: stress_roofline(device, order=o) for o in ("rowmajor", "tiled")}
         for o, st_ in stress_orders.items():
             for c, r in st_["per_channels"].items():
-                log(f"stress ({o}) C={c}: {r['avg_us']:.1f} us, {r['achieved_gbs']:.0f} GB/s")
+                log(f"stress ({o}) C={c}: {r['avg_us']:.1f} us, {r['achieved_gbs']:.0f} GB/s, "
+                    f"{r['gather_gbs']:.0f} GB/s L2 gather")
             for c, r in st_["per_channels_lds"].items():
                 log(f"stress ({o}) C={c} (LDS-staged): {r['avg_us']:.1f} us, {r['achieved_gbs']:.0f} GB/s")
         # the headline stress figure: the faster numbering at C = 128
@@ -766,6 +784,15 @@ def main():
                 "launches_per_step": head["launches_per_step"],
                 "timing": "the step's own mix of launches (CSRs, channel counts), hipGraph-replayed between HIP "
                           "events on the replay stream",
+                "l2_gather": {
+                    "what": "the same launches against the L2: every edge's source row, col and a_src entry, "
+                            "the output row (agg_gather_bytes); the HBM bytes above count each source row once",
+                    "achieved": round(head["gather_gbs"], 1), "unit": "GB/s",
+                    "frac_of_l2_peak": round(head["gather_gbs"] / L2_PEAK_GBS, 4), "l2_peak": L2_PEAK_GBS,
+                    "frac_of_measured_gather_ceiling": round(head["gather_gbs"] / L2_GATHER_GBS, 4),
+                    "measured_gather_ceiling": L2_GATHER_GBS,
+                    "avg_gather_bytes": int(head["avg_gather_bytes"]),
+                },
                 "plain_kernel": {
                     "kernel": "vg_gat_aggregate_fwd (no GraphNorm partials; the eager / inference forward)",
                     "achieved": round(kern["achieved_gbs"], 2),
@@ -804,6 +831,10 @@ def main():
                              f"{stress['edges_per_tile']} edges per 16-row tile",
                 "bound": "hbm", "achieved": round(c128["achieved_gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(c128["achieved_gbs"] / HBM_PEAK_GBS, 4), "avg_launch_us": round(c128["avg_us"], 2),
+                "l2_gather": ({"achieved": round(c128["gather_gbs"], 1), "unit": "GB/s",
+                               "frac_of_l2_peak": round(c128["gather_gbs"] / L2_PEAK_GBS, 4),
+                               "frac_of_measured_gather_ceiling": round(c128["gather_gbs"] / L2_GATHER_GBS, 4)}
+                              if "gather_gbs" in c128 else None),
                 "by_order": {o: {"distinct_sources_per_tile": r["distinct_sources_per_tile"],
                                  "per_channels_register_gather": {str(c): {k: round(v, 2) for k, v in x.items()}
                                                                   for c, x in r["per_channels"].items()},

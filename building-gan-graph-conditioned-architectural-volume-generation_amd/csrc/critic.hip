@@ -19,10 +19,15 @@
 
 namespace {
 
+// iter != NULL: eps[n] is not read but drawn here -- the uniform vg_rng_fill
+// (kind 1) writes for element n under the same (seed, *iter, salt): lane n % 4
+// of the Philox block n / 4, bit for bit -- one launch fewer per iteration.
 __global__ void k_critic_input(const float* __restrict__ mvx, int N, int F,
                                const float* __restrict__ real, const float* __restrict__ hard,
                                const float* __restrict__ soft, const float* __restrict__ eps,
-                               int K, int copies, float* __restrict__ X) {
+                               int K, int copies, float* __restrict__ X, unsigned long long seed = 0,
+                               const long long* __restrict__ iter = nullptr, unsigned int salt = 0) {
+  const long long it = iter ? *iter : 0;
   const int W = F + K;
   const long long total = (long long)copies * N * W;
   for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
@@ -41,7 +46,14 @@ __global__ void k_critic_input(const float* __restrict__ mvx, int N, int F,
       if (cp == 0) v = real[e];
       else if (cp == 1) v = hard[e];
       else {
-        const float a = eps[n];
+        float a;
+        if (iter) {
+          const uint4 r = vg_keep_block(n >> 2, salt, it, seed);
+          const int l = static_cast<int>(n & 3);
+          a = static_cast<float>((l == 0 ? r.x : l == 1 ? r.y : l == 2 ? r.z : r.w) >> 8) * (1.0f / 16777216.0f);
+        } else {
+          a = eps[n];
+        }
         v = __fadd_rn(__fmul_rn(a, real[e]), __fmul_rn(__fsub_rn(1.f, a), soft[e]));
       }
     }
@@ -124,6 +136,21 @@ extern "C" int vg_critic_input(const float* mvx, int32_t N, int32_t F, const flo
   int blocks = vg_blocks((long long)copies * N * (F + K), 256);
   if (blocks > 4096) blocks = 4096;
   k_critic_input<<<blocks, 256, 0, s>>>(mvx, N, F, real, hard, soft, eps, K, copies, X);
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int vg_critic_input_drawn(const float* mvx, int32_t N, int32_t F, const float* real,
+                                     const float* hard, const float* soft, uint64_t seed, const int64_t* iter,
+                                     uint32_t salt, int32_t K, int32_t copies, float* X, void* stream) {
+  if (N <= 0 || F < 0 || K <= 0 || (F > 0 && !mvx) || !real || !hard || !soft || !iter || !X ||
+      (copies != 3 && copies != 4))
+    return VG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  int blocks = vg_blocks((long long)copies * N * (F + K), 256);
+  if (blocks > 4096) blocks = 4096;
+  k_critic_input<<<blocks, 256, 0, s>>>(mvx, N, F, real, hard, soft, nullptr, K, copies, X,
+                                        (unsigned long long)seed, reinterpret_cast<const long long*>(iter), salt);
   VG_CHECK_LAUNCH();
   return 0;
 }

@@ -49,6 +49,10 @@ constexpr int kEP = 3;                // edge slots per lane in the edge-paralle
 #define VG_FWD_ROWS 4
 #endif
 constexpr int kFwdRows = VG_FWD_ROWS;
+#ifndef VG_FWD_PF
+#define VG_FWD_PF 0  // 8: measured 7.22 vs 7.03 us per step-mix launch (profiles/r03_rejected_fwd_prefetch.txt)
+#endif
+constexpr int kFwdPf = VG_FWD_PF;  // source rows gathered before the softmax (k_gat_fwd_cp; <= L)
 #ifndef VG_FWD_SLICE_ROWS
 #define VG_FWD_SLICE_ROWS 100000
 #endif
@@ -70,10 +74,13 @@ __device__ __forceinline__ void load_param(Vec<CPL>& r, const float* __restrict_
 // GraphNorm column partials of the rows a workgroup aggregated: the forward
 // statistics of the GraphNorm that follows every GATConv (models.py:73-75,
 // 193-195; graphnorm.hip's k_stats_partial re-read the whole output for them).
-// Per column (count, mean, M2) of the block's rows, two passes over the row
-// values still in registers: sums by xor-shuffles across the wave's L-lane row
-// groups then across the 4 waves in order through LDS, the mean, then the
-// squared deviations the same way (deterministic).
+// Per column (count, mean, M2) of the block's rows.  Each wave takes its own
+// rows' two-pass statistics from the values still in registers (sum by
+// xor-shuffles across the wave's L-lane row groups -- every lane ends with the
+// total -- the wave mean, then the squared deviations the same way); the four
+// waves' (count, mean, M2) meet in LDS behind ONE barrier and are merged in
+// wave order with Chan's formula (deterministic).  (The first form took the
+// block's two passes through LDS: three barriers, ~1 us per launch more.)
 // Blocks are SEGMENT-ALIGNED (gnp_rows): a stacked forward over S copies
 // (seg_rows rows each) gives every copy ceil(seg_rows / G) blocks of its own,
 // the last one short, so each copy's partials -- and the statistics folded
@@ -103,50 +110,54 @@ __device__ __forceinline__ GnpRows gnp_rows(int seg_rows) {
 template <int L, int CPL>
 __device__ __forceinline__ void gnp_block(const float (&v)[CPL], int row, const GnpRows& gr, int C, int c0,
                                           int cb, int ldc, float* __restrict__ gnp) {
-  constexpr int G = kBlock / L, W = L * CPL;
-  __shared__ float red[kBlock / 64][W];
-  __shared__ float mv[W];
-  const int n0 = min(gr.end, gr.row0 + G) - gr.row0;
-  const bool in0 = row < gr.end;
+  constexpr int W = L * CPL, RW = 64 / L, NW = kBlock / 64;  // columns, rows per wave, waves
+  __shared__ float red[NW][2][W];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  float s0[CPL];
+  const bool in0 = row < gr.end;
+  const int nw = max(0, min(RW, gr.end - (gr.row0 + wave * RW)));  // this wave's rows in the segment
+  const float inv = nw > 0 ? 1.f / static_cast<float>(nw) : 0.f;
+  float s[CPL], mean[CPL];
 #pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
+  for (int q = 0; q < CPL; ++q) s[q] = in0 ? v[q] : 0.f;
+#pragma unroll
+  for (int off = L; off < 64; off <<= 1)
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) s[q] += __shfl_xor(s[q], off, 64);
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) {
+    mean[q] = s[q] * inv;
+    const float d = in0 ? v[q] - mean[q] : 0.f;
+    s[q] = d * d;
+  }
+#pragma unroll
+  for (int off = L; off < 64; off <<= 1)
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) s[q] += __shfl_xor(s[q], off, 64);
+  if (lane < L)
 #pragma unroll
     for (int q = 0; q < CPL; ++q) {
-      float x0 = v[q];
-      if (pass == 1) {
-        x0 -= mv[c0 + q];
-        x0 *= x0;
-      }
-      s0[q] = in0 ? x0 : 0.f;
+      red[wave][0][c0 + q] = mean[q];
+      red[wave][1][c0 + q] = s[q];
     }
+  __syncthreads();
+  const int c = threadIdx.x;
+  if (c < C) {
+    const int n_blk = min(gr.end, gr.row0 + kBlock / L) - gr.row0;
+    float n = static_cast<float>(min(RW, n_blk)), mu = red[0][0][c], m2 = red[0][1][c];
 #pragma unroll
-    for (int off = L; off < 64; off <<= 1)
-#pragma unroll
-      for (int q = 0; q < CPL; ++q) s0[q] += __shfl_xor(s0[q], off, 64);
-    if (lane < L)
-#pragma unroll
-      for (int q = 0; q < CPL; ++q) red[wave][c0 + q] = s0[q];
-    __syncthreads();
-    const int c = threadIdx.x;
-    if (pass == 0) {
-      if (c < W) {
-        float a0 = 0.f;
-#pragma unroll
-        for (int w = 0; w < kBlock / 64; ++w) a0 += red[w][c];
-        mv[c] = a0 / static_cast<float>(n0);
-      }
-      __syncthreads();
-    } else if (c < C) {
-      float m0 = 0.f;
-#pragma unroll
-      for (int w = 0; w < kBlock / 64; ++w) m0 += red[w][c];
-      float* p = gnp + ((size_t)gr.lb * 2 * ldc + cb + c) * 3;
-      p[0] = static_cast<float>(n0);
-      p[1] = mv[c];
-      p[2] = m0;
+    for (int w = 1; w < NW; ++w) {  // Chan's merge, wave order
+      const int k = min(RW, n_blk - w * RW);
+      if (k <= 0) break;
+      const float nb = static_cast<float>(k), nt = n + nb;
+      const float delta = red[w][0][c] - mu, fb = nb / nt;
+      mu += delta * fb;
+      m2 += red[w][1][c] + delta * delta * n * fb;
+      n = nt;
     }
+    float* p = gnp + ((size_t)gr.lb * 2 * ldc + cb + c) * 3;
+    p[0] = n;
+    p[1] = mu;
+    p[2] = m2;
   }
 }
 
@@ -236,6 +247,24 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_cp(
       v_t[t] = beg + j < end;
       s_t[t] = v_t[t] ? col[beg + j] : 0;
     }
+  }
+  // the first PF source rows are gathered NOW, in flight together with the
+  // a_src gathers below: the softmax no longer stands between the column
+  // indices and the row loads (one dependent round trip per row instead of
+  // two; rows up to PF long -- every row of the training graphs -- are a
+  // single round of loads)
+  const int c0 = g.lane * CPL;
+  constexpr int PF0 = kFwdPf < L ? kFwdPf : L;
+  constexpr int PF = PF0 * CPL > 32 ? 32 / CPL : PF0;  // at most 32 prefetch registers per lane
+  Vec<CPL> hp[PF > 0 ? PF : 1];
+#pragma unroll
+  for (int u = 0; u < PF; ++u) {
+    const int su = __shfl(s_t[0], g.base + u, 64);
+    if (__shfl(static_cast<int>(v_t[0]), g.base + u, 64))
+      load_row<CPL, VEC>(hp[u], h + (size_t)su * ld, c0, C);
+  }
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
     e_t[t] = -INFINITY;
     if (v_t[t]) {
       e_t[t] = lrelu(a_src[s_t[t]] + ad, slope);
@@ -266,13 +295,20 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_cp(
     for (int k = beg + g.lane + T * L; k < end; k += L)
       alpha[k] = expf(lrelu(a_src[col[k]] + ad, slope) - m) / denom;
 
-  // channel-parallel gather-sum, 4 neighbour rows in flight
-  const int c0 = g.lane * CPL;
+  // channel-parallel gather-sum: the prefetched rows, then 4 neighbour rows
+  // in flight (same row order, hence bit-identical sums)
   Vec<CPL> acc;
 #pragma unroll
   for (int q = 0; q < CPL; ++q) acc.v[q] = 0.f;
   const int dreg = deg < T * L ? deg : T * L;
-  for (int j0 = 0; j0 < dreg; j0 += kFwdRows) {
+#pragma unroll
+  for (int u = 0; u < PF; ++u)
+    if (u < dreg) {
+      const float a = __shfl(e_t[0], g.base + u, 64);
+#pragma unroll
+      for (int q = 0; q < CPL; ++q) acc.v[q] = fmaf(a, hp[u].v[q], acc.v[q]);
+    }
+  for (int j0 = PF; j0 < dreg; j0 += kFwdRows) {
     const int nj = dreg - j0 < kFwdRows ? dreg - j0 : kFwdRows;
     Vec<CPL> hv[kFwdRows];
     float a[kFwdRows];

@@ -161,6 +161,27 @@ __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float
 // Same update with the step count and learning rate read from device memory
 // (hipGraph replays: host scalars would be frozen into the graph).  Bias
 // corrections are formed in double exactly as torch forms them in Python.
+// The bookkeeping that opens every training iteration, as one launch: the
+// device RNG's iteration counter += 1 (RNG.reset), the optimizer's step count
+// += 1 (the increment optimizer.step() makes before its update, made here so
+// the update kernel reads a settled count) and the flat gradient zeroed
+// (optimizer.zero_grad(), trainer.py:475, 486).  Each pointer may be NULL.
+__global__ void k_iter_begin(long long* __restrict__ ctr, int32_t* __restrict__ step, float* __restrict__ grad,
+                             long long n) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (ctr) *ctr += 1;
+    if (step) *step += 1;
+  }
+  if (!grad) return;
+  const long long q = n >> 2;
+  float4* g4 = reinterpret_cast<float4*>(grad);
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < q; i += (long long)gridDim.x * blockDim.x)
+    g4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (long long i = 4 * q + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    grad[i] = 0.f;
+}
+
 __global__ void k_adam_dev(float* __restrict__ p, const float* __restrict__ g,
                            float* __restrict__ m, float* __restrict__ v, long long n, double b1,
                            double b2, float eps, float wd, const double* __restrict__ lr_p,
@@ -403,6 +424,16 @@ extern "C" int vg_adam_dev(float* param, const float* grad, float* exp_avg, floa
   if (blocks > 2048) blocks = 2048;
   k_adam_dev<<<blocks, 256, 0, static_cast<hipStream_t>(stream)>>>(
       param, grad, exp_avg, exp_avg_sq, n, beta1, beta2, eps, weight_decay, lr, step);
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int vg_iter_begin(int64_t* rng_iter, int32_t* step, float* grad, int64_t n, void* stream) {
+  if (n < 0 || (grad && (reinterpret_cast<uintptr_t>(grad) & 15))) return VG_EINVAL;
+  long long blocks = vg_blocks((n >> 2) + 1, 256);
+  if (blocks > 1024) blocks = 1024;
+  k_iter_begin<<<static_cast<int>(blocks), 256, 0, static_cast<hipStream_t>(stream)>>>(
+      reinterpret_cast<long long*>(rng_iter), step, n > 0 ? grad : nullptr, n);
   VG_CHECK_LAUNCH();
   return 0;
 }

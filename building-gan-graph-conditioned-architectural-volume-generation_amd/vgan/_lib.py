@@ -269,6 +269,9 @@ SIGNATURES = {
     "vg_ln_act_bwd": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
                                      _c_i32, _c_p, _c_p]),
     "vg_critic_input": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p]),
+    "vg_critic_input_drawn": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, ctypes.c_uint64, _c_p,
+                                             ctypes.c_uint32, _c_i32, _c_i32, _c_p, _c_p]),
+    "vg_iter_begin": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_i64, _c_p]),
     "vg_gp_head_ws_floats": (_c_i64, [_c_i32]),
     "vg_gp_head": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_f32, _c_p, _c_i32, _c_p, _c_p, _c_p, _c_p]),
     "vg_adam_dev": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_p, _c_i64, ctypes.c_double, ctypes.c_double, _c_f32, _c_f32,

@@ -86,15 +86,31 @@ class CriticEngine:
             t = self._consts[key] = make()
         return t
 
+    def prepare_batch(self, prep) -> None:
+        """Build this batch's constants (the adjoint seeds of every critic
+        iteration) and the stacked graph now, outside any capture."""
+        n = prep.matched_voxel_x.shape[0]
+        if "critic_seeds4" not in prep.consts:
+            s_ = torch.zeros(4 * n, 1, dtype=torch.float32, device=prep.matched_voxel_x.device)
+            s_[:n] = -1.0 / n
+            s_[n:2 * n] = 1.0 / n
+            s_[3 * n:] = 1.0
+            prep.consts["critic_seeds4"] = s_
+        prep.csr.stacked(3).ell()
+
     def _keeps(self, rng, n: int, dev, training: bool):
         """Dropout multipliers [3N, C_b] per block and eps [N, 1], drawn in the
         reference's order (D(real) masks, D(fake) masks, eps, D(mix) masks)."""
         widths = [conv.out_channels for conv, _ in self.blocks]
+        # device mode: eps as (seed, counter, salt), drawn by vg_critic_input_drawn
+        # itself -- the same numbers rng.uniform would write, without its launch
+        spec = getattr(rng, "uniform_spec", None)  # (stand-in RNGs of the tests have none)
+        draw_eps = (lambda: (spec((n, 1), dev) if spec is not None else None) or rng.uniform((n, 1), dev))
         if not training:
-            return [None] * len(widths), rng.uniform((n, 1), dev)
+            return [None] * len(widths), draw_eps()
         if rng.mode == "device":  # DropSpecs: drawn inside the GraphNorm kernel
             keeps = [rng.keep_mask((3 * n, c), self.dropout, dev) for c in widths]
-            return keeps, rng.uniform((n, 1), dev)
+            return keeps, draw_eps()
         real = [rng.keep_mask((n, c), self.dropout, dev) for c in widths]
         fake = [rng.keep_mask((n, c), self.dropout, dev) for c in widths]
         eps = rng.uniform((n, 1), dev)
@@ -146,7 +162,8 @@ class CriticEngine:
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
         keeps, eps = self._keeps(rng, n, dev, D.training)
-        eps = eps.reshape(n).contiguous()
+        if isinstance(eps, torch.Tensor):
+            eps = eps.reshape(n).contiguous()
         nb, nd, nm = len(self.blocks), len(self.dec), len(self.mlp)
         # parameter-gradient folds of passes C and D, run as one batch at the end
         folds = FoldCollector()
@@ -213,8 +230,13 @@ class CriticEngine:
 
         # ---------------------------------------------------------- pass A
         X0 = _f(X4, W0, dev=dev)
-        check(LIB.vg_critic_input(ptr(mvx), n, F, ptr(real), ptr(hard), ptr(soft), ptr(eps), K, 4, ptr(X0), st),
-              "vg_critic_input")
+        if isinstance(eps, torch.Tensor):
+            check(LIB.vg_critic_input(ptr(mvx), n, F, ptr(real), ptr(hard), ptr(soft), ptr(eps), K, 4, ptr(X0), st),
+                  "vg_critic_input")
+        else:
+            seed, it, salt = eps
+            check(LIB.vg_critic_input_drawn(ptr(mvx), n, F, ptr(real), ptr(hard), ptr(soft), seed, ptr(it), salt, K,
+                                            4, ptr(X0), st), "vg_critic_input_drawn")
         mlp_out = []
         x, xw = X0, W0
         for lin in self.mlp:
@@ -306,7 +328,9 @@ class CriticEngine:
             s_[3 * n:] = 1.0
             return s_
 
-        seeds = self._const(("seeds4", n), make_seeds)
+        seeds = prep.consts.get("critic_seeds4")
+        if seeds is None:
+            seeds = prep.consts["critic_seeds4"] = make_seeds()
         adj_dec = [_f(X4, l.out_features, dev=dev) for l in self.dec[:-1]] + [seeds]
         adj_H = [_f(X4, B["c"], dev=dev) for B in blk]
         adj_mlp = [_f(X4, l.out_features, dev=dev) for l in self.mlp]

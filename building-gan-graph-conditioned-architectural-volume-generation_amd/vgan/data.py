@@ -19,7 +19,7 @@ ground-truth voxel types), so caching it is exact.
 from __future__ import annotations
 
 import weakref
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import torch
 
@@ -33,6 +33,9 @@ class Prepared:
     voxel_x: torch.Tensor
     matched_voxel_x: torch.Tensor
     onehot_f: torch.Tensor
+    # per-batch constants of the engines (built before any capture: a build
+    # recorded into a graph would be replayed by every launch of it)
+    consts: dict = field(default_factory=dict)
 
 
 # batch objects without a ``derived`` store (a reference PyG Batch): keyed by

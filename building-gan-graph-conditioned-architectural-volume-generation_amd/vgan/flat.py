@@ -39,8 +39,11 @@ class FlatParams:
             off += n
         self.numel = total
 
-    def zero_grad(self) -> None:
-        self.grad.zero_()
+    def zero_grad(self, device: bool = True) -> None:
+        """``device=False``: the caller zeroes the buffer in its own launch
+        (vg_iter_begin); only the parameters' .grad views are checked."""
+        if device:
+            self.grad.zero_()
         for p in self.params:  # re-seat views an external set_to_none may have dropped
             if p.grad is None or p.grad.data_ptr() != self._view_ptr(p):
                 self._reseat_grad(p)
@@ -104,7 +107,9 @@ class FlatAdam(torch.optim.Optimizer):
             self._lr_host = lr
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, counted: bool = False):
+        """``counted``: the device step count was already incremented for this
+        update (vg_iter_begin at the start of the iteration)."""
         self.step_count += 1
         h = self.hyper()
         b1, b2 = h["betas"]
@@ -112,7 +117,8 @@ class FlatAdam(torch.optim.Optimizer):
             raise RuntimeError("FlatAdam runs on the HIP path only")
         if not torch.cuda.is_current_stream_capturing():
             self.sync_lr()
-        self.step_t.add_(1)
+        if not counted:
+            self.step_t.add_(1)
         ops.adam_flat_dev(self.flat.param, self.flat.grad, self.exp_avg, self.exp_avg_sq, b1, b2, h["eps"],
                           h["weight_decay"], self.lr_t, self.step_t)
         return None

@@ -55,16 +55,21 @@ class RNG:
         self._iters: Dict[torch.device, torch.Tensor] = {}
         self._early = 0  # resets before the device counter existed (it starts there)
 
-    def reset(self) -> None:
+    def reset(self, defer: bool = False):
         """Start of an iteration body (fixed draws restart; device masks advance).
         The device counter counts resets whenever it is created, so an eager
-        body and a captured one draw the same numbers from the same state."""
+        body and a captured one draw the same numbers from the same state.
+        ``defer``: the device counters are returned, not advanced -- the caller
+        advances them in its own launch (vg_iter_begin)."""
         self._k = 0
         self._salt = 0
         if not self._iters:
             self._early += 1
+        if defer:
+            return list(self._iters.values())
         for t in self._iters.values():
             t.add_(1)
+        return []
 
     def state_dict(self) -> Dict[str, int]:
         """Seed and device iteration counter (device mode): a resumed run
@@ -131,6 +136,15 @@ class RNG:
         if self.mode == "device" and torch.device(device).type == "cuda":
             return self._device_draw(1, shape, device)
         return self._out(torch.rand(*shape, device=self._dev(device)), device)
+
+    def uniform_spec(self, shape: Sequence[int], device):
+        """Device mode: (seed, iteration counter, salt) of the uniform draw
+        ``uniform(shape, device)`` would make -- for a kernel that draws it
+        itself (vg_critic_input_drawn); None in the other modes."""
+        if self.mode != "device" or torch.device(device).type != "cuda":
+            return None
+        self._salt += 1
+        return int(self.seed) & ((1 << 64) - 1), self._iter(device), 0x40000000 | self._salt
 
     def exponential(self, shape: Sequence[int], device) -> torch.Tensor:
         if self.mode == "fixed":

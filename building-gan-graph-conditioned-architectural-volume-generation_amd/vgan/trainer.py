@@ -41,7 +41,7 @@ import torch.nn.functional as F
 from . import data as vdata
 from . import metrics as vmetrics
 from . import ops
-from ._lib import LIB, check, gemm_precision_scope, stream_handle
+from ._lib import LIB, check, gemm_precision_scope, ptr, stream_handle
 from .critic import CriticEngine
 from .dist import GradSync
 from .flat import FlatAdam, FlatParams
@@ -209,23 +209,37 @@ class Trainer:
             _, hard, soft = self.generator(local_graph, voxel_graph, z)
         return hard, soft
 
+    def _iter_begin(self, adam: FlatAdam) -> None:
+        """Open an iteration whose update ``adam`` makes: RNG.reset(),
+        adam.zero_grad() and the step count optimizer.step() increments, as
+        ONE launch (vg_iter_begin) instead of three; the iteration's update
+        then runs ``adam.step(counted=True)``.  The gradient is zeroed before
+        the no-grad generator forward instead of after it (trainer.py:474-475),
+        which that forward never reads."""
+        ctrs = self.rng.reset(defer=True)
+        for t in ctrs[1:]:  # counters on other devices (not the path's single-device case)
+            t.add_(1)
+        flat = adam.flat
+        flat.zero_grad(device=False)
+        check(LIB.vg_iter_begin(ptr(ctrs[0]) if ctrs else None, ptr(adam.step_t), ptr(flat.grad),
+                                flat.grad.numel(), stream_handle(flat.grad.device)), "vg_iter_begin")
+
     def _critic_iteration(self, local_graph, voxel_graph, labels, i: int) -> torch.Tensor:
-        self.rng.reset()
+        """trainer.py:470-479 up to backward(); the update (adam_d.step(counted=True)) is the caller's."""
+        self._iter_begin(self.adam_d)
         if labels is not None:
             hard, soft = labels[0][i:i + 1], labels[1][i:i + 1]
         else:
             with torch.no_grad():
                 _, hard, soft = self._generate(local_graph, voxel_graph)
-        self.adam_d.zero_grad()
         return self._critic_loss_backward(local_graph, voxel_graph, hard, soft)
 
     def _gen_iteration(self, local_graph, voxel_graph):
-        self.rng.reset()
+        """trainer.py:483-492 up to backward(); the update (adam_g.step(counted=True)) is the caller's."""
+        self._iter_begin(self.adam_g)
         if self.gen_engine is not None and self.skip_dead_d_grads:
-            self.adam_g.zero_grad()
             return self.gen_engine.loss_and_grad(local_graph, voxel_graph, self.rng)
         logits, hard, _ = self._generate(local_graph, voxel_graph)
-        self.adam_g.zero_grad()
         d_params = list(self.discriminator.parameters())
         if self.skip_dead_d_grads:
             for p in d_params:
@@ -253,10 +267,10 @@ class Trainer:
             d_loss = self._critic_iteration(local_graph, voxel_graph, labels, i)
             d_losses.append(d_loss.detach())
             self.sync.all_reduce_grad(self.flat_d)
-            self.adam_d.step()
+            self.adam_d.step(counted=True)
         g_loss, hard = self._gen_iteration(local_graph, voxel_graph)
         self.sync.all_reduce_grad(self.flat_g)
-        self.adam_g.step()
+        self.adam_g.step(counted=True)
         return {"d_losses": torch.stack(d_losses), "g_loss": g_loss.detach(), "label_hard": hard.detach()}
 
     # ------------------------------------------------- hipGraph-captured step
@@ -270,7 +284,7 @@ class Trainer:
         if sync:
             self.sync.all_reduce_grad(self.flat_d)
         if with_adam:
-            self.adam_d.step()
+            self.adam_d.step(counted=True)
 
     def _gen_body(self, local_graph, voxel_graph, acc, with_adam: bool, sync: bool = False):
         """The generator iteration; its loss goes to acc[-1]."""
@@ -279,7 +293,7 @@ class Trainer:
         if sync:
             self.sync.all_reduce_grad(self.flat_g)
         if with_adam:
-            self.adam_g.step()
+            self.adam_g.step(counted=True)
         return hard.detach()
 
     def _state_tensors(self):
@@ -382,13 +396,13 @@ class Trainer:
                 (acc[n_critic] if i == 0 else acc[i]).copy_(acc[0])
             if not graphs["with_adam"]:
                 self.sync.all_reduce_grad(self.flat_d)
-                self.adam_d.step()
+                self.adam_d.step(counted=True)
         if single:
             acc[0].copy_(acc[n_critic])
         graphs["gen"].replay()
         if not graphs["with_adam"]:
             self.sync.all_reduce_grad(self.flat_g)
-            self.adam_g.step()
+            self.adam_g.step(counted=True)
         return {"d_losses": acc[:n_critic], "d_loss_mean": acc[:n_critic].mean(), "g_loss": acc[n_critic],
                 "label_hard": graphs["hard"]}
 
@@ -418,7 +432,13 @@ class Trainer:
         sync = self.sync.active and self.sync.capturable
         with_adam = not self.sync.active or sync
         mark = self.phase_hook or (lambda name: None)  # host-time probes (tools/host_profile.py)
-        vdata.prepared(local_graph, voxel_graph, cfg.NUM_CLASSES)
+        prep = vdata.prepared(local_graph, voxel_graph, cfg.NUM_CLASSES)
+        # the critic's per-batch structures (stacked real / fake / mix graph,
+        # its padded columns, the adjoint seeds) before the capture: built
+        # inside it, their ~25 small launches would be recorded and replayed by
+        # every critic iteration
+        if self.critic is not None:
+            self.critic.prepare_batch(prep)
         self.adam_g.sync_lr()
         self.adam_d.sync_lr()
         mark("prepare")
@@ -479,11 +499,11 @@ class Trainer:
             d_losses[i:i + 1].copy_(acc[0:1])
             if not with_adam:
                 self.sync.all_reduce_grad(self.flat_d)
-                self.adam_d.step()
+                self.adam_d.step(counted=True)
         mark("replays")
         g_loss, hard = self._gen_iteration(local_graph, voxel_graph)
         self.sync.all_reduce_grad(self.flat_g)
-        self.adam_g.step()
+        self.adam_g.step(counted=True)
         mark("gen")
         # Recorded graphs are released in batches: destroying one while the
         # device is busy blocks the runtime (every thread's launches) for ~8 ms

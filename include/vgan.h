@@ -155,6 +155,12 @@ int vg_gat_jvp2_ex(const int32_t* row_ptr, const int32_t* col, const int32_t* cs
 int vg_critic_input(const float* mvx, int32_t N, int32_t F, const float* real, const float* hard,
                     const float* soft, const float* eps, int32_t K, int32_t copies, float* X,
                     void* stream);
+/* The same with eps drawn in the kernel: eps[n] = the uniform vg_rng_fill
+ * (kind 1) draws for element n under (seed, *iter, salt) -- trainer.py:298's
+ * torch.rand(N, 1) in device-RNG mode -- so the draw needs no launch of its own. */
+int vg_critic_input_drawn(const float* mvx, int32_t N, int32_t F, const float* real, const float* hard,
+                          const float* soft, uint64_t seed, const int64_t* iter, uint32_t salt, int32_t K,
+                          int32_t copies, float* X, void* stream);
 
 /* From g [N,K] = dD(mix)/dlabel and the stacked scores [3N]:
  * out[1] = gp = lambda mean_n (|g_n|-1)^2, out[0] = mean(fake) - mean(real) + gp,
@@ -834,6 +840,12 @@ int vg_gat_lin_att_bf16(const float* x, int32_t ldx, const float* w, int32_t num
 int vg_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
             float beta2, float one_minus_beta1, float one_minus_beta2, float eps,
             float weight_decay, float step_size, float bc2_sqrt, void* stream);
+
+/* Opens a training iteration in one launch: *rng_iter += 1 (the device RNG's
+ * reset), *step += 1 (the count optimizer.step() increments, trainer.py:481,
+ * 495) and grad[0, n) = 0 (optimizer.zero_grad(), trainer.py:475, 486).  Every
+ * pointer may be NULL; grad 16-B aligned. */
+int vg_iter_begin(int64_t* rng_iter, int32_t* step, float* grad, int64_t n, void* stream);
 
 /* vg_adam with the learning rate and the (already incremented) step count
  * read from device memory, so a captured hipGraph replays correct updates. */

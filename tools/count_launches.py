@@ -25,7 +25,7 @@ def step():
         labels = tr._critic_labels(loc, vox)
     with record_function("phase:critic_iter"):
         d = tr._critic_iteration(loc, vox, labels, 0)
-        tr.adam_d.step()
+        tr.adam_d.step(counted=True)
     with record_function("phase:gen_fwd"):
         tr.rng.reset()
         logits, hard, _ = tr._generate(loc, vox)
@@ -39,7 +39,7 @@ def step():
             g_loss.backward()
         for p in tr.discriminator.parameters():
             p.requires_grad_(True)
-        tr.adam_g.step()
+        tr.adam_g.step(counted=True)
 
 
 with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:

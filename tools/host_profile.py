@@ -61,10 +61,10 @@ def main():
         t1 = time.perf_counter()
         for i in range(cfg.N_CRITIC):
             tr._critic_iteration(loc, vox, labels, i)
-            tr.adam_d.step()
+            tr.adam_d.step(counted=True)
         t2 = time.perf_counter()
         tr._gen_iteration(loc, vox)
-        tr.adam_g.step()
+        tr.adam_g.step(counted=True)
         t3 = time.perf_counter()
         torch.cuda.synchronize()
         t4 = time.perf_counter()
