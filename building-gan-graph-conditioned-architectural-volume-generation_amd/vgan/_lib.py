@@ -346,11 +346,14 @@ def dense(name: str):
 
 
 def ptr(t: Optional[torch.Tensor]):
-    return None if t is None else ctypes.c_void_p(t.data_ptr())
+    """A tensor's device address for a c_void_p argument: a plain int (ctypes
+    converts it itself; wrapping every pointer in a c_void_p object cost ~0.4
+    us each, ~4 us per ABI call of the eager paths' ~10 pointers), None for NULL."""
+    return None if t is None else t.data_ptr()
 
 
-def stream_handle(device: torch.device) -> ctypes.c_void_p:
-    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+def stream_handle(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
 
 
 _SYNC = {}

@@ -58,9 +58,7 @@ def _f(*shape, dev):
 
 def _off(t: torch.Tensor, floats: int):
     """Device pointer `floats` elements into t."""
-    import ctypes
-
-    return ctypes.c_void_p(t.data_ptr() + 4 * floats)
+    return t.data_ptr() + 4 * floats
 
 
 class CriticEngine:
@@ -158,7 +156,10 @@ class CriticEngine:
         csr = prep.csr
         csr3 = csr.stacked(3)
         E = csr.num_edges
-        for p in D.parameters():
+        params = self.__dict__.get("_params")
+        if params is None:  # (a module walk per iteration cost ~20 us of host time)
+            params = self._params = list(D.parameters())
+        for p in params:
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
         keeps, eps = self._keeps(rng, n, dev, D.training)
@@ -440,8 +441,8 @@ class CriticEngine:
             if _lib._GN_JVP_FUSE:  # the GraphNorm tangent sums from the GAT tangent pass
                 nblk = int(LIB.vg_gat_jvp2_blocks(n, c))
                 gpart = _f(nblk * 5 * c, dev=dev)
-                gn = VgGnJvp(x=gx.value, keep=gkeep.value if gkeep is not None else None, g_y=dY_b[b].data_ptr(),
-                             stats=gstats.value, weight=norm.weight.data_ptr(), bias=norm.bias.data_ptr(),
+                gn = VgGnJvp(x=gx, keep=gkeep, g_y=dY_b[b].data_ptr(),
+                             stats=gstats, weight=norm.weight.data_ptr(), bias=norm.bias.data_ptr(),
                              mean_scale=norm.mean_scale.data_ptr(), eps=float(norm.eps), part=gpart.data_ptr())
                 folds.jvp_gn(jargs, gn, st, keep=(ws, uH, gpart))
                 check(LIB.vg_graphnorm_jvp2_part(gx, n, c, ptr(norm.weight), ptr(norm.bias), ptr(norm.mean_scale),

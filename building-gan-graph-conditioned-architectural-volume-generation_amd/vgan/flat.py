@@ -44,9 +44,15 @@ class FlatParams:
         (vg_iter_begin); only the parameters' .grad views are checked."""
         if device:
             self.grad.zero_()
-        for p in self.params:  # re-seat views an external set_to_none may have dropped
+        # re-seat views an external set_to_none (or a .grad assignment) dropped;
+        # the identity check is cheap, the pointer check runs only on a change
+        views = getattr(self, "_views", None)
+        if views is not None and all(p.grad is v for p, v in zip(self.params, views)):
+            return
+        for p in self.params:
             if p.grad is None or p.grad.data_ptr() != self._view_ptr(p):
                 self._reseat_grad(p)
+        self._views = [p.grad for p in self.params]
 
     def _offset(self, p) -> int:
         return (p.data.data_ptr() - self.param.data_ptr()) // 4

@@ -29,6 +29,7 @@ import torch.nn as nn
 
 from . import data as vdata
 from . import ops
+from ._lib import gemm_precision
 from .nn import MLP, Linear, linear_att, linear_ln_act, run_blocks
 from .rng import RNG
 
@@ -91,6 +92,10 @@ class GATEncoder(nn.Module):
     187-210: ``depth`` halving blocks then ``depth`` doubling blocks, each
     [GATConv -> GraphNorm -> ReLU -> Dropout] (children ``module_{4b+0..3}``)."""
 
+    # no-grad forwards apply each GraphNorm in the next projection GEMM
+    # (_forward_nograd_fused); False: the module path (tests compare the two)
+    fused_nograd = True
+
     def __init__(self, width: int, depth: int, dropout: float = 0.2):
         super().__init__()
         self.dropout = dropout
@@ -114,12 +119,94 @@ class GATEncoder(nn.Module):
     def forward(self, x: torch.Tensor, csr: ops.CSR, rng: RNG, segments: int = 1) -> torch.Tensor:
         """``segments`` > 1: x holds that many stacked copies of the batch (csr
         block-diagonal), each normalised on its own as a separate forward."""
+        if self.fused_nograd and ops._GN_FWD_FUSE and not torch.is_grad_enabled() and x.is_cuda and x.dim() == 2 \
+                and gemm_precision() == "f32":
+            y = self._forward_nograd_fused(x, csr, rng, segments)
+            if y is not None:
+                return y
         for b in range(self.num_blocks):
             conv: GATConv = getattr(self, f"module_{4 * b}")
             norm: GraphNorm = getattr(self, f"module_{4 * b + 1}")
             h = conv(x, csr)
             keep = rng.keep_mask(h.shape, self.dropout, h.device) if self.training else None
             x = ops.graphnorm_relu_dropout(h, norm.weight, norm.bias, norm.mean_scale, keep, norm.eps, segments)
+        return x
+
+
+    def _forward_nograd_fused(self, x: torch.Tensor, csr: ops.CSR, rng: RNG, segments: int):
+        """The no-grad forward (critic labels, validation, inference) with each
+        block's GraphNorm + ReLU + Dropout applied by the NEXT block's
+        projection GEMM as it loads its operand (vg_gat_lin_att_gn) -- nothing
+        needs the normalised activations afterwards, so they are never
+        written: one launch and one [rows, C] write + read fewer per block.
+        The statistics still come from the aggregation's partials
+        (vg_graphnorm_stats_gnp); the dropout multipliers are the same Philox
+        draws (in-kernel, device RNG) or none (eval).  The projection sees the
+        apply kernel's values up to FMA contraction (1e-6,
+        tests/test_gnp_gpu.py).  None (the caller runs the module path) for
+        host-drawn masks, C > 64 projections or short segments."""
+        from ._lib import LIB, VgGnApply, check, dense, ptr, stream_handle
+
+        rows = x.shape[0]
+        S = int(segments)
+        n = rows // S
+        if rows % S or n < 64 or not x.is_contiguous():
+            return None
+        if self.training and getattr(rng, "mode", None) != "device":
+            return None  # host / fixed masks are tensors: the module path (decided before any draw)
+        if csr.seg_rows != n or csr.num_nodes != rows:
+            return None
+        for c in self.widths[1:]:  # every block's aggregation must form its GraphNorm partials
+            g = int(LIB.vg_gat_gnp_rows(rows, c))
+            if g <= 0 or n < g:
+                return None
+        dev = x.device
+        st = stream_handle(dev)
+        pend = None  # (O, desc, stats, c): the previous block's GraphNorm, applied in this projection
+        for b in range(self.num_blocks):
+            conv: GATConv = getattr(self, f"module_{4 * b}")
+            norm: GraphNorm = getattr(self, f"module_{4 * b + 1}")
+            c = conv.out_channels
+            spec = rng.keep_mask((rows, c), self.dropout, dev) if self.training else None
+            if spec is not None and isinstance(spec, torch.Tensor):
+                raise RuntimeError("device RNG returned a mask tensor")
+            H = torch.empty(rows, c, dtype=torch.float32, device=dev)
+            a_s = torch.empty(rows, dtype=torch.float32, device=dev)
+            a_d = torch.empty(rows, dtype=torch.float32, device=dev)
+            if pend is not None:
+                xin, desc, _, cin = pend
+                check(LIB.vg_gat_lin_att_gn(ptr(xin), ptr(conv.lin.weight), rows, cin, c, ptr(conv.att_src),
+                                            ptr(conv.att_dst), ptr(H), ptr(a_s), ptr(a_d), ctypes.byref(desc), st),
+                      "vg_gat_lin_att_gn")
+                pend = None
+            else:
+                cin = x.shape[1]
+                check(dense("vg_gat_lin_att")(ptr(x), cin, ptr(conv.lin.weight), rows, cin, c, ptr(conv.att_src),
+                                              ptr(conv.att_dst), ptr(H), ptr(a_s), ptr(a_d), st), "vg_gat_lin_att")
+            O = torch.empty(rows, c, dtype=torch.float32, device=dev)
+            alpha = torch.empty(csr.num_edges, dtype=torch.float32, device=dev)
+            gnp, g = ops.gnp_buffer(csr, c, dev)
+            if gnp is None:
+                raise RuntimeError("GraphNorm partials unavailable (VGAN_GN_FWD_FUSE=0 disables the fused path)")
+            ops.aggregate_fwd_raw(csr, c, ptr(H), ptr(a_s), ptr(a_d), ptr(conv.bias), float(conv.negative_slope),
+                                  ptr(O), ptr(alpha), st, gnp)
+            stats = torch.empty(S * 2 * c, dtype=torch.float32, device=dev)
+            nxt = getattr(self, f"module_{4 * (b + 1)}").out_channels if b + 1 < self.num_blocks else 0
+            drop = (float(spec.p), int(spec.seed), ptr(spec.iter), int(spec.salt) & 0xFFFFFFFF) if spec is not None \
+                else (0.0, 0, None, 0)
+            if 0 < nxt <= 64 and c <= 128 and c % 4 == 0:
+                check(LIB.vg_graphnorm_stats_gnp(S, n, c, ptr(gnp), g, ptr(stats), st), "vg_graphnorm_stats_gnp")
+                desc = VgGnApply(stats=stats.data_ptr(), weight=norm.weight.data_ptr(), bias=norm.bias.data_ptr(),
+                                 mean_scale=norm.mean_scale.data_ptr(), keep=None, eps=float(norm.eps),
+                                 p_drop=drop[0], seg_rows=n, salt=drop[3], seed=drop[1], iter=drop[2], y=None,
+                                 keep_out=None)
+                pend = (O, desc, stats, c)  # stats / O stay referenced until the GEMM is enqueued
+                continue
+            y = torch.empty(rows, c, dtype=torch.float32, device=dev)
+            check(LIB.vg_graphnorm_fwd_gnp(ptr(O), S, n, c, ptr(norm.weight), ptr(norm.bias), ptr(norm.mean_scale),
+                                           None, *drop, float(norm.eps), ptr(y), None, ptr(stats), ptr(gnp), g, st),
+                  "vg_graphnorm_fwd_gnp")
+            x = y
         return x
 
 
