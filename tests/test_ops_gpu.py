@@ -673,3 +673,4 @@ def test_aggregate_ell_bit_identical(cuda, graph, C):
     ops.aggregate_fwd_raw(csr, C, ptr(h), ptr(a_s), ptr(a_d), ptr(b), 0.2, ptr(out), ptr(alpha), csr.stream())
     ref_out, ref_alpha = _aggregate_ref_kernel(csr, h, a_s, a_d, b)
     assert torch.equal(out, ref_out) and torch.equal(alpha, ref_alpha)
+
