@@ -64,6 +64,18 @@ def rccl1():
     assert graphs["sync_in_graph"] and graphs["with_adam"]
     assert torch.equal(a["d_losses"], b["d_losses"]) and torch.equal(a["g_loss"], b["g_loss"])
     assert torch.equal(ref.flat_g.param, dp.flat_g.param) and torch.equal(ref.flat_d.param, dp.flat_d.param)
+    # the fresh-batch path (what Trainer.train runs at N > 1): the critic
+    # iteration with its all-reduce recorded per NEW batch, the one executable
+    # graph updated in place from each recording
+    ds = SyntheticDataset(64, seed=8)
+    for k in range(3):
+        fl, fv = ds.batch(range(4 * k, 4 * k + 4))
+        fl, fv = fl.to(dev), fv.to(dev)
+        a = ref.step_fresh(fl, fv)
+        b = dp.step_fresh(fl, fv)
+        torch.cuda.synchronize()
+        assert torch.equal(a["d_losses"], b["d_losses"]) and torch.equal(a["g_loss"], b["g_loss"]), k
+    assert torch.equal(ref.flat_g.param, dp.flat_g.param) and torch.equal(ref.flat_d.param, dp.flat_d.param)
     dist.destroy_process_group()
     print("RCCL_GRAPH_OK", flush=True)
 

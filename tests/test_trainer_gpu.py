@@ -181,7 +181,10 @@ def _run_worker(args, timeout=300):
 def test_rccl_all_reduce_recorded_in_step_graphs(cuda):
     """One rank over RCCL with the gradient sync forced on: the all-reduce is
     recorded inside the critic and generator graphs, and the trajectory is
-    bit-identical to the single-process step (a one-rank sum is exact)."""
+    bit-identical to the single-process step (a one-rank sum is exact) --
+    for replays of a cached batch and for three new batches through
+    step_fresh (the collective recorded per batch, the executable graph
+    updated in place)."""
     out = _run_worker(["rccl1"])
     assert "RCCL_GRAPH_OK" in out
 
