@@ -2,7 +2,11 @@
 
 Each model's parameters are re-seated as views into ONE contiguous fp32 buffer
 (G: 274,185 floats = 1.10 MB, D: 15,665 = 63 KB) and their ``.grad`` as views
-into one flat gradient buffer.  Consequences:
+into one flat gradient buffer.  Each parameter starts on a 128-byte boundary
+(ALIGN floats; the gaps stay zero in both buffers, and Adam keeps them zero):
+the GEMMs take their float4 operand loads only from 16-byte-aligned weights,
+and a packed layout left most weights after the GAT stack's 1- and 2-wide
+attention vectors misaligned.  Consequences:
 
 * ``optimizer.step()`` (``trainer.py:481,495``) is one ``vg_adam`` launch over
   the buffer instead of a Python loop over ~100 tensors;
@@ -12,6 +16,7 @@ into one flat gradient buffer.  Consequences:
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Iterable, List, Optional
 
 import torch
@@ -20,14 +25,22 @@ import torch.nn as nn
 from . import ops
 
 
+# floats: every parameter's view starts on a 128-byte boundary (VGAN_FLAT_ALIGN=1: packed, for A/B runs)
+ALIGN = max(1, int(os.environ.get("VGAN_FLAT_ALIGN", "32")))
+
+
+def _padded(n: int) -> int:
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
 class FlatParams:
     def __init__(self, module: nn.Module):
         params = [p for p in module.parameters() if p.requires_grad]
         if not params:
             raise ValueError("module has no trainable parameters")
         dev = params[0].device
-        total = sum(p.numel() for p in params)
-        self.param = torch.empty(total, dtype=torch.float32, device=dev)
+        total = sum(_padded(p.numel()) for p in params)
+        self.param = torch.zeros(total, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(total, dtype=torch.float32, device=dev)
         self.params: List[nn.Parameter] = params
         off = 0
@@ -36,8 +49,9 @@ class FlatParams:
             self.param[off:off + n].copy_(p.detach().reshape(-1))
             p.data = self.param[off:off + n].view_as(p)
             p.grad = self.grad[off:off + n].view_as(p)
-            off += n
-        self.numel = total
+            off += _padded(n)
+        self.numel = total  # buffer length, padding included
+        self.num_params = sum(p.numel() for p in params)
 
     def zero_grad(self, device: bool = True) -> None:
         """``device=False``: the caller zeroes the buffer in its own launch
@@ -53,6 +67,15 @@ class FlatParams:
             if p.grad is None or p.grad.data_ptr() != self._view_ptr(p):
                 self._reseat_grad(p)
         self._views = [p.grad for p in self.params]
+
+    def live_mask(self) -> torch.Tensor:
+        """Bool mask over the buffer: True on parameter elements, False on the
+        alignment gaps."""
+        m = torch.zeros(self.numel, dtype=torch.bool, device=self.param.device)
+        for p in self.params:
+            off = self._offset(p)
+            m[off:off + p.numel()] = True
+        return m
 
     def _offset(self, p) -> int:
         return (p.data.data_ptr() - self.param.data_ptr()) // 4

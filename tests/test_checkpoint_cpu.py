@@ -46,9 +46,10 @@ def _perturb(tr, seed=3):
     g = torch.Generator().manual_seed(seed)
     with torch.no_grad():
         for flat, adam, step in ((tr.flat_g, tr.adam_g, 7), (tr.flat_d, tr.adam_d, 12)):
-            flat.param.add_(0.01 * torch.randn(flat.param.shape, generator=g))
-            adam.exp_avg.copy_(torch.randn(flat.param.shape, generator=g))
-            adam.exp_avg_sq.copy_(torch.rand(flat.param.shape, generator=g))
+            live = flat.live_mask()  # the alignment gaps stay zero
+            flat.param.add_(0.01 * torch.randn(flat.param.shape, generator=g) * live)
+            adam.exp_avg.copy_(torch.randn(flat.param.shape, generator=g) * live)
+            adam.exp_avg_sq.copy_(torch.rand(flat.param.shape, generator=g) * live)
             adam.step_t.fill_(step)
     import warnings
     with warnings.catch_warnings():
@@ -156,8 +157,8 @@ def test_flat_adam_state_dict_is_torch_adam_format(tmp_path):
 
     flat = FlatParams(G)
     adam = FlatAdam(flat, lr=3e-4, betas=(0.5, 0.999))
-    adam.exp_avg.normal_()
-    adam.exp_avg_sq.uniform_()
+    adam.exp_avg.normal_().mul_(flat.live_mask())  # the alignment gaps stay zero
+    adam.exp_avg_sq.uniform_().mul_(flat.live_mask())
     adam.step_t.fill_(4)
     sd = adam.state_dict()
     ref = torch.optim.Adam(G.parameters(), lr=1.0)
