@@ -258,6 +258,24 @@ def test_type_mean(cuda):
     assert (got2[vox.type.to(cuda) == 4] == 0).all()
 
 
+@pytest.mark.parametrize("n_local,F", [(1, 17), (15, 17), (17, 5), (257, 17), (700, 63), (4099, 29), (300_001, 17)])
+def test_type_mean_sizes(cuda, n_local, F):
+    """vg_type_mean (16 waves, every 16th program row per wave, rows of
+    out-of-range types skipped) against a float64 mean, over sizes around the
+    wave boundaries up to 300k program rows."""
+    g = torch.Generator().manual_seed(n_local * 64 + F)
+    lx = torch.randn(n_local, F, generator=g)
+    lt = torch.randint(-1, 9, (n_local,), generator=g)  # -1 and 7, 8: outside the 7 types
+    vt = torch.randint(0, 7, (997,), generator=g)
+    got = ops.type_mean(lx.to(cuda), lt.to(cuda), vt.to(cuda), 7).cpu()
+    want = torch.zeros(vt.numel(), F, dtype=torch.float64)
+    for t in range(7):
+        m = lt == t
+        if m.any():
+            want[vt == t] = lx[m].double().mean(0)
+    assert torch.allclose(got.double(), want, atol=2e-6, rtol=1e-6)
+
+
 def test_gumbel_head(cuda):
     torch.manual_seed(0)
     n, k = 4000, 7
