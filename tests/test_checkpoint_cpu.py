@@ -174,3 +174,24 @@ def test_flat_adam_state_dict_is_torch_adam_format(tmp_path):
         st["state"][first]["step"] = torch.tensor(9.0)
         ref.load_state_dict(st)
         adam2.import_from(ref)
+
+
+def test_flat_params_aligned_views():
+    """Every parameter view starts on a 128-byte boundary of the flat buffer
+    (the GEMMs' float4 operand loads need 16-byte-aligned weights), holds the
+    module's initial values, and the gaps between views stay zero."""
+    cfg = _cfg()
+    torch.manual_seed(4)
+    G = VoxelGNNGenerator(cfg, 17, 12)
+    from vgan.flat import ALIGN, FlatParams
+
+    init = {k: p.detach().clone() for k, p in G.named_parameters()}
+    flat = FlatParams(G)
+    assert ALIGN * 4 % 128 == 0
+    for k, p in G.named_parameters():
+        assert (p.data_ptr() - flat.param.data_ptr()) % 128 == 0, k
+        assert p.grad is not None and p.grad.data_ptr() - flat.grad.data_ptr() == p.data_ptr() - flat.param.data_ptr()
+        assert torch.equal(p.detach(), init[k]), k
+    live = flat.live_mask()
+    assert int(live.sum()) == flat.num_params == 274185
+    assert flat.numel >= flat.num_params and not flat.param[~live].any() and not flat.grad[~live].any()
