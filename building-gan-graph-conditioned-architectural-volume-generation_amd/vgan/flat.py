@@ -140,6 +140,11 @@ class FlatAdam(torch.optim.Optimizer):
         """``counted``: the device step count was already incremented for this
         update (vg_iter_begin at the start of the iteration)."""
         self.step_count += 1
+        if self.source is not None:
+            # what the LR scheduler's wrapper of source.step() records: this
+            # update IS the caller's optimizer.step() (the scheduler otherwise
+            # warns that it stepped first)
+            self.source._opt_called = True
         h = self.hyper()
         b1, b2 = h["betas"]
         if not self.flat.param.is_cuda:

@@ -40,9 +40,20 @@ def tile_order(location: torch.Tensor, tile: int = 4) -> torch.Tensor:
     return torch.argsort(key, stable=True)
 
 
+# node-level attributes of a voxel building (VoxelGraphData, data.py:48-77 and
+# the keys vgan.synth / vgan.convert add): gathered by the permutation
+NODE_KEYS = ("x", "type", "types_onehot", "voxel_level", "coordinate", "dimension", "location", "site_area",
+             "data_number")
+# per-building attributes (vgan.convert's type ratio vector [K]): carried unchanged
+GRAPH_KEYS = ("node_ratio",)
+
+
 def renumber(voxel: GraphData, perm: torch.Tensor) -> GraphData:
-    """The building with node ``perm[r]`` as node r: node-level tensors
-    gathered, edges relabelled in place (same order), lists kept."""
+    """The building with node ``perm[r]`` as node r: the node-level attributes
+    (``NODE_KEYS``) gathered, edges relabelled in place (same order).  Any
+    other key is refused rather than guessed from its shape (an edge-level
+    attribute whose length happens to equal the node count would otherwise be
+    permuted as if it were per node)."""
     n = voxel.num_nodes
     inv = torch.empty_like(perm)
     inv[perm] = torch.arange(n, dtype=perm.dtype)
@@ -51,14 +62,41 @@ def renumber(voxel: GraphData, perm: torch.Tensor) -> GraphData:
         v = getattr(voxel, key)
         if key == "edge_index":
             out[key] = inv[v]
-        elif torch.is_tensor(v) and v.dim() > 0 and v.shape[0] == n:
-            out[key] = v[perm]
-        else:
+        elif key in NODE_KEYS:
+            if len(v) != n:
+                raise ValueError(f"node attribute {key!r} has {len(v)} rows for {n} nodes")
+            out[key] = v[perm] if torch.is_tensor(v) else [v[int(i)] for i in perm]
+        elif key in GRAPH_KEYS:
             out[key] = v
+        else:
+            raise ValueError(f"renumber: unknown voxel attribute {key!r} (add it to NODE_KEYS or GRAPH_KEYS)")
     return GraphData(**out)
+
+
+def block_order(location: torch.Tensor, block=(4, 4, 4)) -> torch.Tensor:
+    """perm [n] numbering voxels in (floor, y, x) blocks of ``block`` = (bf, by,
+    bx), blocks in (floor, y, x) order, row-major inside a block.  A 64-row
+    aggregation tile is then a 4 x 4 x 4 block of the lattice: on the stress
+    lattice its sources are the block grown by one voxel in y and x on each of
+    its floors and on the floors just above and below -- about 6 x 6 x 6 =
+    216 distinct rows for ~1,400 edges (6.4 edges per distinct source row,
+    against 3.1 for the 4 x 4 floor tiles of ``tile_order``)."""
+    loc = location.to(torch.int64)
+    bf, by, bx = (int(b) for b in block)
+    f, y, x = loc[:, 0], loc[:, 1], loc[:, 2]
+    ny = int(y.max()) // by + 1 if loc.numel() else 1
+    nx = int(x.max()) // bx + 1 if loc.numel() else 1
+    key = (((f // bf) * ny + y // by) * nx + x // bx) * (bf * by * bx) + ((f % bf) * by + y % by) * bx + x % bx
+    return torch.argsort(key, stable=True)
 
 
 def tiled(voxel: GraphData, tile: int = 4) -> Tuple[GraphData, torch.Tensor]:
     """(renumbered building, perm) in ``tile_order`` of its ``location``."""
     perm = tile_order(voxel.location, tile)
+    return renumber(voxel, perm), perm
+
+
+def blocked(voxel: GraphData, block=(4, 4, 4)) -> Tuple[GraphData, torch.Tensor]:
+    """(renumbered building, perm) in ``block_order`` of its ``location``."""
+    perm = block_order(voxel.location, block)
     return renumber(voxel, perm), perm

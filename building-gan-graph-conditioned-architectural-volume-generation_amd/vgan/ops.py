@@ -176,6 +176,23 @@ class CSR:
         return plan
 
 
+    def stage_plan(self) -> torch.Tensor:
+        """The staged-tile plan of this graph (vg_gat_stage_plan: per 64-row
+        tile the distinct sources and every edge's LDS slot), built once and
+        cached; consumed by aggregate_staged."""
+        plan = self.__dict__.get("_stage_plan")
+        if plan is None:
+            n_ints = int(LIB.vg_gat_stage_plan_ints(self.num_nodes, self.num_edges))
+            plan = torch.empty(n_ints, dtype=torch.int32, device=self.device)
+            check(LIB.vg_gat_stage_plan(ptr(self.row_ptr), ptr(self.col), self.num_nodes, self.num_edges,
+                                        ptr(plan), self.stream()), "vg_gat_stage_plan")
+            self._stage_plan = plan
+        return plan
+
+    def stage_tiles(self) -> int:
+        return (self.num_nodes + 63) // 64
+
+
 def aggregate_fwd_raw(csr: "CSR", c: int, h, a_src, a_dst, bias, slope: float, out, alpha, stream,
                       gnp=None) -> None:
     """vg_gat_aggregate_fwd over raw device pointers (ctypes), through the
@@ -255,6 +272,25 @@ def aggregate_lds(csr: "CSR", h: torch.Tensor, a_src: torch.Tensor, a_dst: torch
     check(LIB.vg_gat_aggregate_fwd_lds(ptr(csr.row_ptr), ptr(csr.col), n, c, ptr(h), ptr(_f32(a_src)),
                                        ptr(_f32(a_dst)), ptr(_f32(bias)), float(slope), ptr(out), ptr(alpha),
                                        ptr(csr.tile_plan()), csr._tile_umax, csr.stream()), "vg_gat_aggregate_fwd_lds")
+    return out, alpha
+
+
+def aggregate_staged(csr: "CSR", h: torch.Tensor, a_src: torch.Tensor, a_dst: torch.Tensor, bias: torch.Tensor,
+                     slope: float = 0.2, out: Optional[torch.Tensor] = None, alpha: Optional[torch.Tensor] = None):
+    """(out, alpha) of vg_gat_aggregate_fwd_staged: GATConv's edge softmax and
+    gather-sum by the persistent kernel that stages each 64-row tile's
+    distinct source rows in LDS (large graphs, C = 64 or 128).  Bit-identical
+    to the register-gather kernel."""
+    h = _f32(h)
+    require_cuda(h, a_src, a_dst, bias)
+    n, c = h.shape
+    if n != csr.num_nodes or c not in (64, 128):
+        raise ValueError("aggregate_staged: h must be [num_nodes, 64 or 128]")
+    out = torch.empty_like(h) if out is None else out
+    alpha = torch.empty(csr.num_edges, dtype=torch.float32, device=h.device) if alpha is None else alpha
+    check(LIB.vg_gat_aggregate_fwd_staged(ptr(csr.row_ptr), ptr(csr.col), n, c, ptr(h), ptr(_f32(a_src)),
+                                          ptr(_f32(a_dst)), ptr(_f32(bias)), float(slope), ptr(out), ptr(alpha),
+                                          ptr(csr.stage_plan()), csr.stream()), "vg_gat_aggregate_fwd_staged")
     return out, alpha
 
 

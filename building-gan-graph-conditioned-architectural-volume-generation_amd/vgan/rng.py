@@ -75,7 +75,9 @@ class RNG:
         """Seed and device iteration counter (device mode): a resumed run
         continues the same stream of z / dropout / Gumbel / eps draws."""
         iters = [int(t.item()) for t in self._iters.values()]
-        return {"mode": self.mode, "seed": int(self.seed), "iter": max(iters) if iters else 0}
+        # no device counter yet: the value it will start from (resets so far count)
+        start = getattr(self, "_pending_iter", 0) + self._early
+        return {"mode": self.mode, "seed": int(self.seed), "iter": max(iters) if iters else start}
 
     def load_state_dict(self, state: Dict[str, int]) -> None:
         if state.get("mode") != self.mode:

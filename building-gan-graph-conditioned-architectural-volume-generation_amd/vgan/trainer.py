@@ -480,14 +480,27 @@ class Trainer:
             finally:
                 g.capture_end()
         cur.wait_stream(side)
-        owner = getattr(self, "_fresh_owner", None)
+        # Two executable graphs, used by alternate batches.  An update rewrites
+        # an executable graph's kernel arguments, and HIP does not promise that
+        # launches of it already queued keep the old ones (its kernel arguments
+        # may live in device memory written at update time), so an executable
+        # graph is updated only after its last launches -- two batches back --
+        # have finished (a host wait on the event recorded behind them; the
+        # device is normally less than one batch behind the host, so the wait
+        # rarely stalls)
+        owners = self.__dict__.setdefault("_fresh_owners", [None, None])
+        events = self.__dict__.setdefault("_fresh_events", [None, None])
+        j = self._fresh_parity = (getattr(self, "_fresh_parity", 1) + 1) % 2
+        owner = owners[j]
+        if events[j] is not None:
+            events[j].synchronize()
         if owner is None or not _FRESH_UPDATE or \
                 LIB.vg_graph_exec_update(ctypes.c_void_p(owner.raw_cuda_graph_exec()),
                                          ctypes.c_void_p(g.raw_cuda_graph())) != 0:
-            g.instantiate()  # first batch, or a launch sequence of another shape
+            g.instantiate()  # first batches, or a launch sequence of another shape
             if owner is not None:
                 self.__dict__.setdefault("_fresh_dead", []).append(owner)
-            owner = self._fresh_owner = g
+            owner = owners[j] = g
         exec_ = ctypes.c_void_p(owner.raw_cuda_graph_exec())
         mark("capture")
         d_losses = torch.empty(n_critic, dtype=torch.float32, device=dev)
@@ -500,6 +513,8 @@ class Trainer:
             if not with_adam:
                 self.sync.all_reduce_grad(self.flat_d)
                 self.adam_d.step(counted=True)
+        ev = events[j] = torch.cuda.Event()
+        ev.record(cur)  # behind this batch's last launch of owners[j]
         mark("replays")
         g_loss, hard = self._gen_iteration(local_graph, voxel_graph)
         self.sync.all_reduce_grad(self.flat_g)
@@ -668,11 +683,19 @@ class Trainer:
             pool = getattr(self, "_eval_pool", None)
             if pool is None:
                 pool = self._eval_pool = torch.cuda.graph_pool_handle()
+            # the warm-up draws like a visit (its RNG reset advances the device
+            # counter): undo that, so the draw stream does not depend on which
+            # epoch captured the batch (a resumed run captures at another one)
+            if callable(getattr(self.rng, "_iter", None)):
+                self.rng._iter(dev)
+            iters = {d: t.clone() for d, t in getattr(self.rng, "_iters", {}).items()}
             side = torch.cuda.Stream(dev)
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):  # lazy allocations outside the capture
                 self._eval_body(local_graph, voxel_graph, with_loss)
             torch.cuda.current_stream(dev).wait_stream(side)
+            for d, t in iters.items():
+                self.rng._iters[d].copy_(t)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
                 outs = self._eval_body(local_graph, voxel_graph, with_loss)

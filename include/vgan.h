@@ -730,6 +730,33 @@ int vg_gat_aggregate_fwd_lds(const int32_t* row_ptr, const int32_t* col, int32_t
                              const float* a_dst, const float* bias, float slope, float* out,
                              float* alpha, const int32_t* plan, int32_t umax, void* stream);
 
+/* Build stamp: "<hash> <compiler>" -- the first 16 hex digits of the sha256
+ * of every source this library was built from (csrc/*.hip, csrc/*.h and this
+ * header, concatenated in sorted path order) and the hipcc version.  The
+ * Python binding recomputes the hash from its tree and refuses a library
+ * built from other sources. */
+const char* vg_build_stamp(void);
+
+/* Staged-tile plan (configs[3]), once per graph: for every tile of 64
+ * destination rows the sorted distinct sources of its edges (at most 288) and
+ * each edge's slot among them; tiles with more distinct sources, more than
+ * 2048 edges or a row longer than 64 edges get count -1 (aggregated from
+ * global memory).  plan: vg_gat_stage_plan_ints(N, E') int32s. */
+int64_t vg_gat_stage_plan_ints(int32_t num_nodes, int32_t num_edges);
+int vg_gat_stage_plan(const int32_t* row_ptr, const int32_t* col, int32_t num_nodes, int32_t num_edges,
+                      int32_t* plan_out, void* stream);
+
+/* vg_gat_aggregate_fwd (GATConv edge softmax + gather-sum + bias,
+ * models.py:144) by a persistent, software-pipelined kernel that stages each
+ * 64-row tile's distinct source rows in LDS while the previous tile is
+ * aggregated out of it (one 1024-thread workgroup per CU).  Bit-identical to
+ * vg_gat_aggregate_fwd.  C = 64 or 128; h 16-B and out 8-B aligned; plan from
+ * vg_gat_stage_plan over the same CSR.  Pays off with voxels numbered in
+ * lattice blocks (vgan.locality.block_order). */
+int vg_gat_aggregate_fwd_staged(const int32_t* row_ptr, const int32_t* col, int32_t num_nodes, int32_t channels,
+                                const float* h, const float* a_src, const float* a_dst, const float* bias,
+                                float slope, float* out, float* alpha, const int32_t* plan, void* stream);
+
 /* ---- GraphNorm backward partials in the producing GEMM -------------------- */
 
 /* C[N,M] = A[N,K] B[K,M] (vg_gemm, b_trans 0, no bias / activation) is the

@@ -62,3 +62,22 @@ def test_ops_refuse_cpu_tensors():
 
     with pytest.raises(RuntimeError, match="ROCm device"):
         ops.CSR(torch.zeros(2, 3, dtype=torch.long), 4)
+
+
+def test_build_stamp_matches_tree_and_stale_library_is_refused():
+    """libvgan_hip.so carries the hash of the sources it was built from; the
+    binding recomputes it from the tree, and a library built from other
+    sources (a stale prebuilt .so) is refused at import."""
+    import vgan._lib as L
+
+    stamp = L.build_stamp()
+    assert stamp.split(" ")[0] == L.source_hash(os.path.join(os.path.dirname(L.__file__), "..", "csrc"))
+    assert "HIP version" in stamp
+
+    class Stale:
+        @staticmethod
+        def vg_build_stamp():
+            return b"0123456789abcdef HIP version: 0"
+
+    with pytest.raises(ImportError, match="other sources"):
+        L._check_stamp(Stale())

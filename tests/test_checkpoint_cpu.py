@@ -195,3 +195,21 @@ def test_flat_params_aligned_views():
     live = flat.live_mask()
     assert int(live.sum()) == flat.num_params == 274185
     assert flat.numel >= flat.num_params and not flat.param[~live].any() and not flat.grad[~live].any()
+
+
+def test_rng_state_before_the_device_counter_exists():
+    """RNG.state_dict taken after resets but before the device counter was
+    created records those resets: the resumed stream starts where the
+    original one would have (not at iteration 0)."""
+    from vgan.rng import RNG
+
+    a = RNG("device", seed=5)
+    for _ in range(3):
+        a.reset()
+    st = a.state_dict()
+    assert st["iter"] == 3
+    b = RNG("device", seed=1)
+    b.load_state_dict(st)
+    assert b.seed == 5 and b._pending_iter + b._early == 3
+    b.reset()
+    assert b.state_dict()["iter"] == 4

@@ -7,7 +7,8 @@ import pytest
 import torch
 
 from oracle import pyg
-from vgan.locality import renumber, tile_order, tiled
+from vgan.graph import GraphData
+from vgan.locality import block_order, blocked, renumber, tile_order, tiled
 from vgan.synth import make_stress_building, make_building
 
 
@@ -52,6 +53,45 @@ def test_tile_order_keys():
     perm = tile_order(loc, 4)
     # floor 0 tile (0,0): (0,0,0), (0,1,1); floor 0 tile (0,1): (0,0,5); tile (1,0): (0,4,0); floor 1
     assert perm.tolist() == [1, 4, 0, 3, 2]
+
+
+def test_block_order_is_a_3d_block_permutation():
+    _, v = make_stress_building(777, 0, F=8, Y=12, X=12)
+    v2, perm = blocked(v, (4, 4, 4))
+    n = v.num_nodes
+    assert sorted(perm.tolist()) == list(range(n))
+    inv = torch.empty_like(perm)
+    inv[perm] = torch.arange(n)
+    assert torch.equal(v2.edge_index, inv[v.edge_index])
+    # every 64-row group is one 4 x 4 x 4 block of the lattice
+    for g in range(n // 64):
+        loc = v2.location[64 * g:64 * g + 64]
+        for c in range(3):
+            assert int(loc[:, c].max() - loc[:, c].min()) == 3 and int(loc[:, c].min()) % 4 == 0
+    # fewer distinct sources per 64-row tile than the floor tiles give
+    def distinct(ei):
+        dst, src = ei[1], ei[0]
+        return sum(len(set(src[(dst >= lo) & (dst < lo + 64)].tolist())) for lo in range(0, n, 64)) / (n // 64)
+    assert distinct(v2.edge_index) < 0.8 * distinct(tiled(v, 4)[0].edge_index)
+
+
+def test_block_order_ragged_edges():
+    loc = torch.tensor([[0, 0, 5], [0, 0, 0], [5, 0, 0], [0, 4, 0], [1, 1, 1]])
+    # blocks (f//4, y//4, x//4): (0,0,1) (0,0,0) (1,0,0) (0,1,0) (0,0,0); ny = 2, nx = 2
+    assert block_order(loc, (4, 4, 4)).tolist() == [1, 4, 0, 3, 2]
+
+
+def test_renumber_refuses_unknown_attributes():
+    _, v = make_building(777, 3)
+    n = v.num_nodes
+    perm = torch.randperm(n)
+    attrs = {k: getattr(v, k) for k in v.keys()}
+    # an edge-level attribute whose length happens to equal the node count
+    bad = GraphData(**attrs, edge_weight=torch.zeros(n))
+    with pytest.raises(ValueError, match="edge_weight"):
+        renumber(bad, perm)
+    v2 = renumber(v, perm)
+    assert v2.data_number == [v.data_number[int(i)] for i in perm]
 
 
 @pytest.mark.gpu

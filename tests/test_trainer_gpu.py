@@ -17,6 +17,7 @@ drop-in's state around it, on the GPU.
 import os
 import subprocess
 import sys
+import warnings
 
 import pytest
 import torch
@@ -82,7 +83,11 @@ def test_train_epochs_figures_match_reference_reductions(cuda, tmp_path):
         return out
 
     tr._train_batch = rec
-    history = tr.train()
+    with warnings.catch_warnings(record=True) as caught:
+        warnings.simplefilter("always")
+        history = tr.train()
+    # FlatAdam's update is the caller's optimizer.step(): no scheduler-order warning
+    assert not [w for w in caught if "lr_scheduler.step()" in str(w.message)]
     assert [h["epoch"] for h in history] == [1, 2, 3]
     for e, h in enumerate(history):
         batches = train_rec[3 * e:3 * e + 3]
@@ -167,6 +172,34 @@ def test_step_fresh_matches_eager_step(cuda):
         with torch.no_grad():  # continue from identical state
             for x, y in zip(a._state_tensors(), b._state_tensors()):
                 y.copy_(x)
+
+
+def test_step_fresh_back_to_back_without_sync(cuda):
+    """Six new batches through step_fresh with no host synchronisation between
+    them (the host records and updates batch k+1's critic graph while batch
+    k's replays may still be queued) against the same six batches with a
+    device synchronisation after every step: losses, parameters, Adam state
+    and RNG counters bit-identical.  An executable graph updated under its own
+    queued launches would hand those launches the next batch's arguments."""
+    cfg = _cfg(cuda)
+    a, b = _trainer(cfg), _trainer(cfg)
+    ds = SyntheticDataset(32, seed=11)
+    batches = []
+    for k in range(6):
+        loc, vox = ds.batch(range(4 * k, 4 * k + 4 + (k % 3)))  # sizes vary: updates and re-instantiations
+        batches.append((loc.to(cuda), vox.to(cuda)))
+    torch.cuda.synchronize()
+    outs_a = [a.step_fresh(loc, vox) for loc, vox in batches]  # no sync in between
+    outs_b = []
+    for loc, vox in batches:
+        outs_b.append(b.step_fresh(loc, vox))
+        torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    for k, (oa, ob) in enumerate(zip(outs_a, outs_b)):
+        assert torch.equal(oa["d_losses"], ob["d_losses"]), k
+        assert torch.equal(oa["g_loss"], ob["g_loss"]), k
+    for x, y in zip(a._state_tensors(), b._state_tensors()):
+        assert torch.equal(x, y)
 
 
 def _run_worker(args, timeout=300):
