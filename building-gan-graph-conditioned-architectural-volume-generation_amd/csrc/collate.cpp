@@ -85,6 +85,27 @@ extern "C" int vgh_collate_sizes(const int64_t* node_ptr, const int64_t* edge_pt
   return 0;
 }
 
+extern "C" int vgh_collate_max_in_degree(const int64_t* node_ptr, const int64_t* edge_ptr, const int32_t* esrc,
+                                         const int32_t* edst, int64_t num_buildings, const int64_t* index,
+                                         int32_t count, int32_t* max_degree) {
+  if (!node_ptr || !edge_ptr || !esrc || !edst || !index || !max_degree || count <= 0) return VGH_EINVAL;
+  int32_t best = 0;
+  std::vector<int32_t> deg;
+  for (int32_t b = 0; b < count; ++b) {
+    const int64_t g = index[b];
+    if (g < 0 || g >= num_buildings) return VGH_EINDEX;
+    const int64_t n = node_ptr[g + 1] - node_ptr[g];
+    deg.assign(n, 1);  // the self loop
+    for (int64_t e = edge_ptr[g]; e < edge_ptr[g + 1]; ++e) {
+      if (edst[e] < 0 || edst[e] >= n) return VGH_EEDGE;
+      if (esrc[e] != edst[e]) ++deg[edst[e]];
+    }
+    for (int64_t i = 0; i < n; ++i) best = std::max(best, deg[i]);
+  }
+  *max_degree = best;
+  return 0;
+}
+
 extern "C" int vgh_collate_rows(const void* src, int64_t row_bytes, const int64_t* node_ptr,
                                 int64_t num_buildings, const int64_t* index, int32_t count, void* dst,
                                 int32_t threads) {
@@ -168,6 +189,90 @@ extern "C" int vgh_collate_graph(const int64_t* node_ptr, const int64_t* edge_pt
   if (want_csr) {
     row_ptr[n_total] = static_cast<int32_t>(p.csr_off[count]);
     csc_ptr[n_total] = static_cast<int32_t>(p.csr_off[count]);
+  }
+  return 0;
+}
+
+// ----------------------------------------------------------------------------
+// Per-batch structures of vgan.data.prepared, built on the host beside the
+// collate so a new batch reaches the device as ONE upload (vgan/store.py)
+// instead of ~25 copies plus ~30 small build launches per step.
+
+extern "C" int vgh_csr_ell(const int32_t* row_ptr, const int32_t* col, int32_t n, int32_t width, int32_t* ell) {
+  if (!row_ptr || !col || !ell || n <= 0 || width <= 0) return VGH_EINVAL;
+  for (int32_t i = 0; i < n; ++i) {
+    const int32_t b = row_ptr[i], d = row_ptr[i + 1] - b;
+    if (d > width || d < 0) return VGH_ERANGE;
+    int32_t* row = ell + static_cast<int64_t>(i) * width;
+    for (int32_t j = 0; j < d; ++j) row[j] = col[b + j];
+    for (int32_t j = d; j < width; ++j) row[j] = -1;
+  }
+  return 0;
+}
+
+extern "C" int vgh_csr_stacked(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr,
+                               const int32_t* csc_slot, const int32_t* csc_dst, int32_t n, int32_t slots,
+                               int32_t copies, int32_t* s_row_ptr, int32_t* s_col, int32_t* s_csc_ptr,
+                               int32_t* s_csc_slot, int32_t* s_csc_dst) {
+  if (!row_ptr || !col || !csc_ptr || !csc_slot || !csc_dst || !s_row_ptr || !s_col || !s_csc_ptr || !s_csc_slot ||
+      !s_csc_dst || n <= 0 || slots <= 0 || copies <= 0)
+    return VGH_EINVAL;
+  if (static_cast<int64_t>(n) * copies > INT32_MAX || static_cast<int64_t>(slots) * copies > INT32_MAX)
+    return VGH_ERANGE;
+  for (int32_t c = 0; c < copies; ++c) {
+    const int32_t no = c * n, eo = c * slots;
+    for (int32_t i = 0; i < n; ++i) {
+      s_row_ptr[no + i] = row_ptr[i] + eo;
+      s_csc_ptr[no + i] = csc_ptr[i] + eo;
+    }
+    for (int32_t k = 0; k < slots; ++k) {
+      s_col[eo + k] = col[k] + no;
+      s_csc_slot[eo + k] = csc_slot[k] + eo;
+      s_csc_dst[eo + k] = csc_dst[k] + no;
+    }
+  }
+  s_row_ptr[n * copies] = slots * copies;
+  s_csc_ptr[n * copies] = slots * copies;
+  return 0;
+}
+
+// models.py:122-129 on the host, in vg_type_mean's exact f32 order (typemean.hip:
+// 16 partial sums per type, program row r into partial r % 16 in row order,
+// the partials then summed in order, the count likewise, mean = sum / count),
+// so the result is bit for bit the device kernel's.
+extern "C" int vgh_type_mean(const float* local_x, const int64_t* local_type, int32_t n_local, int32_t feat,
+                             const int64_t* voxel_type, int32_t n_voxel, int32_t n_types, float* out,
+                             int32_t out_stride, int32_t out_col0) {
+  constexpr int kParts = 16;
+  if (n_local < 0 || n_voxel <= 0 || feat <= 0 || n_types <= 0 || !voxel_type || !out ||
+      out_stride < out_col0 + feat || (n_local > 0 && (!local_x || !local_type)))
+    return VGH_EINVAL;
+  std::vector<float> acc(static_cast<size_t>(kParts) * n_types * feat, 0.f), cnt(kParts * n_types, 0.f);
+  for (int32_t r = 0; r < n_local; ++r) {
+    const int64_t t = local_type[r];
+    if (t < 0 || t >= n_types) continue;
+    const int w = r % kParts;
+    float* a = acc.data() + (static_cast<size_t>(w) * n_types + t) * feat;
+    const float* x = local_x + static_cast<int64_t>(r) * feat;
+    for (int32_t f = 0; f < feat; ++f) a[f] += x[f];
+    cnt[w * n_types + t] += 1.f;
+  }
+  std::vector<float> table(static_cast<size_t>(n_types) * feat, 0.f), count(n_types, 0.f);
+  for (int32_t t = 0; t < n_types; ++t) {
+    float c = 0.f;
+    for (int w = 0; w < kParts; ++w) c += cnt[w * n_types + t];
+    count[t] = c;
+    for (int32_t f = 0; f < feat; ++f) {
+      float s = 0.f;
+      for (int w = 0; w < kParts; ++w) s += acc[(static_cast<size_t>(w) * n_types + t) * feat + f];
+      table[static_cast<size_t>(t) * feat + f] = c > 0.f ? s / c : 0.f;
+    }
+  }
+  for (int32_t v = 0; v < n_voxel; ++v) {
+    const int64_t t = voxel_type[v];
+    float* o = out + static_cast<int64_t>(v) * out_stride + out_col0;
+    const bool hit = t >= 0 && t < n_types && count[t] > 0.f;
+    for (int32_t f = 0; f < feat; ++f) o[f] = hit ? table[static_cast<size_t>(t) * feat + f] : 0.f;
   }
   return 0;
 }

@@ -62,7 +62,46 @@ def _inputs_key(local_graph, voxel_graph):
         (voxel_graph, "types_onehot"), (voxel_graph, "edge_index")))
 
 
+def _from_host(local_graph, voxel_graph, n_classes: int):
+    """The Prepared structures the host collate built with the batch
+    (vgan.store ``prepare``; uploaded in the batch's one copy), or None when
+    absent or not for this pairing / device / class count."""
+    getter = getattr(voxel_graph, "derived", None)
+    pa = getter("prepared_arrays") if callable(getter) else None
+    arrays = getter("csr_arrays") if callable(getter) else None
+    if pa is None or arrays is None or pa["n_classes"] != n_classes:
+        return None
+    vx = voxel_graph.x
+    v = pa["views"]
+    versions = tuple(t._version for t in (local_graph.x, local_graph.type, vx, voxel_graph.type,
+                                          voxel_graph.types_onehot, voxel_graph.edge_index))
+    if pa["local"] != (local_graph.x.data_ptr(), local_graph.type.data_ptr()) or vx.dtype != torch.float32 \
+            or pa.get("versions") != versions \
+            or any(t.device != vx.device for t in v.values()) or arrays[0].device != vx.device:
+        return None
+    n = vx.shape[0]
+    w = pa["ell_width"]
+    csr = ops.CSR.from_arrays(*arrays, max_degree=pa["max_degree"])
+    if ops._ELL:
+        csr._ell = (v["ell"], w) if w else (None, 0)
+    csr._stacked = {}
+    for c in pa["copies"]:
+        st = ops.CSR.from_arrays(*(v[f"stacked{c}.{k}"] for k in ("row_ptr", "col", "csc_ptr", "csc_slot", "csc_dst")),
+                                 max_degree=pa["max_degree"])
+        st._seg_rows = n
+        if ops._ELL:
+            st._ell = (v[f"stacked{c}_ell"], w) if w else (None, 0)
+        csr._stacked[c] = st
+    prep = Prepared(csr=csr, matched_x=v["matched_x"], voxel_x=vx.contiguous(), matched_voxel_x=v["matched_voxel_x"],
+                    onehot_f=v["onehot_f"])
+    prep.consts["critic_seeds4"] = v["critic_seeds4"]
+    return prep
+
+
 def _build(local_graph, voxel_graph, n_classes: int) -> Prepared:
+    hit = _from_host(local_graph, voxel_graph, n_classes)
+    if hit is not None:
+        return hit
     vx = voxel_graph.x
     if vx.dtype != torch.float32:
         vx = vx.float()

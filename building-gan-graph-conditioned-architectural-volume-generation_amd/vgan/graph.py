@@ -138,6 +138,10 @@ class GraphBatch(GraphData):
                                                for t in self._derived["csr_arrays"])
             if "csr_max_degree" in self._derived:
                 out._derived["csr_max_degree"] = self._derived["csr_max_degree"]
+        pa = self._derived.get("prepared_arrays")
+        if pa is not None and "x" in self._store:  # host-built per-batch structures (vgan.store)
+            out._derived["prepared_arrays"] = dict(pa, views={k: t.to(device, non_blocking=non_blocking)
+                                                              for k, t in pa["views"].items()}, local=None)
         return out
 
     # ------------------------------------------------------- derived, per batch

@@ -127,6 +127,99 @@ class InferenceSweep:
         finally:
             self.G.train(was)
 
+    @torch.no_grad()
+    def run_fresh(self, local_graph, voxel_graph) -> torch.Tensor:
+        """``run_batch`` for a batch seen once (a stream of distinct
+        buildings): the stacked forward is RECORDED as a hipGraph and two
+        executable graphs, used by alternate batches, are updated in place
+        with its kernel parameters (vg_graph_exec_update) -- no instantiation
+        per batch; a recording of another launch shape (the f16 kernels pick
+        their shapes from the sizes) instantiates a new one.  An executable
+        graph is updated only after its previous launch finished (the event
+        recorded behind it, two batches back).  Returns [len(taus), N] int8,
+        valid until the next call (clone to keep)."""
+        import ctypes
+
+        from ._lib import LIB, check, stream_handle
+
+        was = self.G.training
+        self.G.eval()
+        try:
+            prep = vdata.prepared(local_graph, voxel_graph, self.G.configuration.NUM_CLASSES)
+            k = len(self.taus)
+            if k > 1:  # the stacked graph (and its padded columns) before the recording
+                prep.csr.stacked(k).ell()
+            dev = voxel_graph.x.device
+            cur = torch.cuda.current_stream(dev)
+            st = self.__dict__.setdefault("_stream_state", {"owners": [None, None], "events": [None, None],
+                                                            "parity": 1, "dead": [], "side": None,
+                                                            "out": None, "warm": False})
+            if self._pool is None:
+                self._pool = torch.cuda.graph_pool_handle()
+            if st["side"] is None:
+                st["side"] = torch.cuda.Stream(dev)
+                st["out"] = torch.empty(0, dtype=torch.int8, device=dev)
+            side = st["side"]
+            if not st["warm"]:  # lazy initialisation outside any recording; its draws undone
+                ctr = self.G.rng._iter(dev) if callable(getattr(self.G.rng, "_iter", None)) else None
+                keep = ctr.clone() if ctr is not None else None
+                self._forward(local_graph, voxel_graph)
+                if ctr is not None:
+                    ctr.copy_(keep)
+                st["warm"] = True
+            g = torch.cuda.CUDAGraph(keep_graph=True)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                g.capture_begin(pool=self._pool, capture_error_mode="thread_local")
+                try:
+                    out = self._forward(local_graph, voxel_graph)
+                finally:
+                    g.capture_end()
+            cur.wait_stream(side)
+            j = st["parity"] = (st["parity"] + 1) % 2
+            owner = st["owners"][j]
+            if st["events"][j] is not None:
+                st["events"][j].synchronize()
+            if owner is None or LIB.vg_graph_exec_update(ctypes.c_void_p(owner.raw_cuda_graph_exec()),
+                                                         ctypes.c_void_p(g.raw_cuda_graph())) != 0:
+                g.instantiate()
+                if owner is not None:
+                    st["dead"].append(owner)
+                owner = st["owners"][j] = g
+            check(LIB.vg_graph_launch(ctypes.c_void_p(owner.raw_cuda_graph_exec()), stream_handle(dev)),
+                  "vg_graph_launch")
+            if st["out"].shape != out.shape:
+                st["out"] = torch.empty_like(out)
+            res = st["out"]
+            res.copy_(out)  # out lives in the recording's pool, reused by the next batch
+            ev = st["events"][j] = torch.cuda.Event()
+            ev.record(cur)
+            if g is not owner:
+                st["dead"].append(g)
+            if len(st["dead"]) >= 64:  # graphs released in batches, on an idle device (DESIGN.md 4.14)
+                torch.cuda.synchronize(dev)
+                st["dead"].clear()
+            return res
+        finally:
+            self.G.train(was)
+
+    def run_stream(self, batches: Iterable, collect: bool = False) -> Dict[str, object]:
+        """Sweep a stream of batches each seen once (``run_fresh``): counts
+        and, with ``collect``, every batch's [k, N] predictions."""
+        outs: List[torch.Tensor] = []
+        graphs = samples = nb = 0
+        for local_graph, voxel_graph in batches:
+            pred = self.run_fresh(local_graph, voxel_graph)
+            graphs += voxel_graph.num_graphs
+            samples += voxel_graph.num_graphs * len(self.taus)
+            nb += 1
+            if collect:
+                outs.append(pred.clone())
+        res: Dict[str, object] = {"graphs": graphs, "samples": samples, "batches": nb}
+        if collect:
+            res["predictions"] = [o.cpu() for o in outs]
+        return res
+
     def run(self, batches: Iterable, collect: bool = False) -> Dict[str, object]:
         """Sweep every (local_graph, voxel_graph) batch; returns counts and,
         with ``collect``, the per-batch [k, N] predictions (copied to the host

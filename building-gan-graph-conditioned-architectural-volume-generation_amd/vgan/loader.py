@@ -28,7 +28,7 @@ import torch
 from torch.utils.data import DataLoader, random_split
 
 from .graph import GraphBatch
-from .store import GraphStore
+from .store import GraphStore, upload_pair
 
 
 class _Indices(torch.utils.data.Dataset):
@@ -52,7 +52,7 @@ class GraphLoader:
     def __init__(self, store: GraphStore, indices: Optional[Sequence[int]] = None, batch_size: int = 1,
                  shuffle: bool = True, drop_last: bool = False, device=None, prefetch: int = 2,
                  threads: int = 4, rank: int = 0, world_size: int = 1, seed: Optional[int] = None,
-                 even: bool = True, resident: bool = False):
+                 even: bool = True, resident: bool = False, prepare=None):
         """``rank`` / ``world_size``: data-parallel sharding -- every rank draws
         the same epoch plan and takes batches rank, rank + world, ... of it, so
         ranks see disjoint buildings (weak scaling, one batch of
@@ -67,6 +67,13 @@ class GraphLoader:
         every batch: its ranks may get one batch more or less, and the
         trainer reduces the figures over the ranks once per epoch.  One rank
         keeps the reference's global-RNG shuffle (``data.py:177-184``).
+
+        ``prepare`` (the number of classes, or (classes, stacked copy counts)
+        -- vgan.store._prepare_spec): every batch also carries the
+        per-batch structures vgan.data would build on the device (padded
+        columns, the critic's stacked graph, the type-matched mean, the float
+        one-hot, the critic's seeds), built by the host collate and uploaded
+        with the batch in its one host-to-device copy.
 
         ``resident``: the first epoch's batches stay on the device and every
         later epoch yields the same batch objects in the same order (no
@@ -90,6 +97,7 @@ class GraphLoader:
         self.even = bool(even)
         self.resident = bool(resident)
         self._resident_batches: Optional[List[Tuple[GraphBatch, GraphBatch]]] = None
+        self.prepare = prepare
 
     def __len__(self) -> int:
         n = len(self.indices)
@@ -126,9 +134,9 @@ class GraphLoader:
         dev = self.device
         kept = [] if self.resident else None
         if dev is None or dev.type != "cuda":
-            it = (self.store.collate(idx, pin=False, threads=self.threads) for idx in plan)
+            it = (self.store.collate(idx, pin=False, threads=self.threads, prepare=self.prepare) for idx in plan)
         else:
-            it = _prefetched(self.store, plan, dev, self.prefetch, self.threads)
+            it = _prefetched(self.store, plan, dev, self.prefetch, self.threads, self.prepare)
         for pair in it:
             if kept is not None:
                 kept.append(pair)
@@ -137,7 +145,8 @@ class GraphLoader:
             self._resident_batches = kept
 
 
-def _prefetched(store: GraphStore, plan: List[List[int]], dev: torch.device, depth: int, threads: int):
+def _prefetched(store: GraphStore, plan: List[List[int]], dev: torch.device, depth: int, threads: int,
+                prepare=None):
     copy_stream = torch.cuda.Stream(device=dev)
     q: "queue.Queue" = queue.Queue(maxsize=depth)
     stop = threading.Event()
@@ -148,9 +157,9 @@ def _prefetched(store: GraphStore, plan: List[List[int]], dev: torch.device, dep
             for idx in plan:
                 if stop.is_set():
                     return
-                host = store.collate(idx, pin=True, threads=threads)
+                host = store.collate(idx, pin=True, threads=threads, prepare=prepare)
                 with torch.cuda.stream(copy_stream):
-                    moved = tuple(g.to(dev, non_blocking=True) for g in host)
+                    moved = upload_pair(*host, dev, non_blocking=True)  # one copy of the pair's buffer
                     ev = torch.cuda.Event()
                     ev.record(copy_stream)
                 q.put((moved, host, ev))  # host buffers stay referenced until the copy is waited on
@@ -185,6 +194,10 @@ def _prefetched(store: GraphStore, plan: List[List[int]], dev: torch.device, dep
 
 
 def _tensors(g: GraphBatch):
+    blob = g.derived("device_blob")
+    if blob is not None:  # every tensor of the pair is a view of it
+        yield blob
+        return
     for key in g.keys():
         v = getattr(g, key)
         if torch.is_tensor(v):
@@ -199,7 +212,7 @@ class GraphDataLoaders:
     the reference (``data.py:166-212``) over a GraphStore."""
 
     def __init__(self, configuration, store: GraphStore, device=None, prefetch: int = 2, rank: int = 0,
-                 world_size: int = 1, resident_eval: bool = False):
+                 world_size: int = 1, resident_eval: bool = False, prepare: bool = True):
         """``resident_eval``: the validation / test batches are collated once
         and kept on the device (no per-epoch reshuffle), so the trainer replays
         their captured evaluation graphs; the reference reshuffles them every
@@ -216,7 +229,8 @@ class GraphDataLoaders:
         split_gen = torch.Generator().manual_seed(seed) if seed is not None else torch.default_generator
         parts = random_split(indices, configuration.SPLIT_RATIOS, generator=split_gen)
         kw = dict(batch_size=configuration.BATCH_SIZE, shuffle=True, drop_last=False, device=device,
-                  prefetch=prefetch, rank=rank, world_size=world_size, seed=seed)
+                  prefetch=prefetch, rank=rank, world_size=world_size, seed=seed,
+                  prepare=int(configuration.NUM_CLASSES) if prepare else None)
         self.train_dataloader = GraphLoader(store, [indices[i] for i in parts[0].indices], **kw)
         ev = dict(kw, even=False, resident=bool(resident_eval))  # evaluation: every batch, reduced over ranks
         self.validation_dataloader = None if self.sanity_checking else \

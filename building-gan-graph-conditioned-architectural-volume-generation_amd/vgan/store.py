@@ -45,7 +45,24 @@ HOST_SIGNATURES = {
     "vgh_collate_sizes": (ctypes.c_int, [_p, _p, _p, _p, _i64, _p, _i32, _p]),
     "vgh_collate_rows": (ctypes.c_int, [_p, _i64, _p, _i64, _p, _i32, _p, _i32]),
     "vgh_collate_graph": (ctypes.c_int, [_p, _p, _p, _p, _i64, _p, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "vgh_collate_max_in_degree": (ctypes.c_int, [_p, _p, _p, _p, _i64, _p, _i32, _p]),
+    "vgh_csr_ell": (ctypes.c_int, [_p, _p, _i32, _i32, _p]),
+    "vgh_csr_stacked": (ctypes.c_int, [_p, _p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p]),
+    "vgh_type_mean": (ctypes.c_int, [_p, _p, _i32, _i32, _p, _i32, _i32, _p, _i32, _i32]),
 }
+ELL_WIDTHS = (8, 16, 32)  # vgan.ops.ELL_WIDTHS
+CRITIC_COPIES = 3  # the critic engine's stacked real / fake / mix graph (vgan.critic)
+
+
+def _prepare_spec(prepare):
+    """``prepare``: the number of classes, or (classes, stacked copy counts):
+    the block-diagonal copies to build besides the critic's 3 (the inference
+    sweep's one per temperature)."""
+    if isinstance(prepare, (tuple, list)):
+        k, copies = int(prepare[0]), tuple(sorted({int(c) for c in prepare[1]} | {CRITIC_COPIES}))
+    else:
+        k, copies = int(prepare), (CRITIC_COPIES,)
+    return k, copies
 _HOST_ERRORS = {1: "invalid argument", 2: "building index out of range", 3: "edge endpoint outside its building",
                 4: "batch too large for int32 ids"}
 
@@ -210,64 +227,223 @@ class GraphStore:
         return self._graph("local", i), self._graph("voxel", i)
 
     # ---------------------------------------------------------------- collate
-    def _collate_kind(self, kind: str, index: np.ndarray, pin: bool, threads: int) -> GraphBatch:
+    # Every tensor of a collated (local, voxel) pair -- and, with ``prepare``,
+    # the per-batch structures vgan.data would otherwise build on the device
+    # -- is carved out of ONE host buffer (page-locked for the loader), so a
+    # new batch reaches the GPU as one host-to-device copy (``upload_pair``).
+
+    def _layout(self, index: np.ndarray, prepare):
+        """(sizes per kind, [(name, shape, torch dtype)]) of a pair's buffer."""
         lib = host_lib()
-        a = self._arr[kind]
-        g = self.meta["graphs"][kind]
         count = int(index.size)
-        common = (_np_ptr(a["node_ptr"]), _np_ptr(a["edge_ptr"]), _np_ptr(a["esrc"]), _np_ptr(a["edst"]),
-                  self.num_buildings, _np_ptr(index), count)
-        sizes = np.zeros(3, dtype=np.int64)
-        _host_check(lib.vgh_collate_sizes(*common, _np_ptr(sizes)), "vgh_collate_sizes")
-        n, e, ep = (int(v) for v in sizes)
+        items, sizes = [], {}
+        for kind in KINDS:
+            a = self._arr[kind]
+            common = (_np_ptr(a["node_ptr"]), _np_ptr(a["edge_ptr"]), _np_ptr(a["esrc"]), _np_ptr(a["edst"]),
+                      self.num_buildings, _np_ptr(index), count)
+            sz = np.zeros(3, dtype=np.int64)
+            _host_check(lib.vgh_collate_sizes(*common, _np_ptr(sz)), "vgh_collate_sizes")
+            n, e, ep = (int(v) for v in sz)
+            sizes[kind] = (n, e, ep, common)
+            items += [(f"{kind}.ptr", (count + 1,), torch.int64), (f"{kind}.batch", (n,), torch.int64),
+                      (f"{kind}.edge_index", (2, e), torch.int64)]
+            if kind in CSR_KINDS:
+                items += [(f"{kind}.csr.{k}", (n + 1,) if k.endswith("ptr") else (ep,), torch.int32)
+                          for k in ("row_ptr", "col", "csc_ptr", "csc_slot", "csc_dst")]
+            g = self.meta["graphs"][kind]
+            for key in g["keys"]:
+                if key != "edge_index" and key not in g["lists"]:
+                    src = a[key]
+                    items.append((f"{kind}.{key}", (n,) + tuple(src.shape[1:]), _NP_TO_TORCH[src.dtype]))
+        extras = None
+        if prepare is not None:
+            n, _, ep, common = sizes["voxel"]
+            md = np.zeros(1, dtype=np.int32)
+            _host_check(host_lib().vgh_collate_max_in_degree(*common, _np_ptr(md)), "vgh_collate_max_in_degree")
+            w = next((x for x in ELL_WIDTHS if int(md[0]) <= x), 0)
+            fl = int(self._arr["local"]["x"].shape[1])
+            fv = int(self._arr["voxel"]["x"].shape[1])
+            k, copies = _prepare_spec(prepare)
+            extras = {"max_degree": int(md[0]), "ell_width": w, "n_classes": k, "fl": fl, "copies": copies}
+            items += [("prep.matched_voxel_x", (n, fl + fv), torch.float32), ("prep.matched_x", (n, fl), torch.float32),
+                      ("prep.onehot_f", (n, k), torch.float32), ("prep.critic_seeds4", (4 * n, 1), torch.float32)]
+            for c in copies:
+                items += [(f"prep.stacked{c}.{kk}", (c * n + 1,) if kk.endswith("ptr") else (c * ep,), torch.int32)
+                          for kk in ("row_ptr", "col", "csc_ptr", "csc_slot", "csc_dst")]
+                if w:
+                    items.append((f"prep.stacked{c}_ell", (c * n * w,), torch.int32))
+            if w:
+                items.append(("prep.ell", (n * w,), torch.int32))
+        return sizes, items, extras
 
-        def empty(shape, dtype):
-            return torch.empty(shape, dtype=dtype, pin_memory=pin)
-
-        out = {}
-        ptr = empty((count + 1,), torch.int64)
-        batch = empty((n,), torch.int64)
-        edge_index = empty((2, e), torch.int64)
-        csr = None
-        if kind in CSR_KINDS:
-            csr = (empty((n + 1,), torch.int32), empty((ep,), torch.int32), empty((n + 1,), torch.int32),
-                   empty((ep,), torch.int32), empty((ep,), torch.int32))
-        _host_check(lib.vgh_collate_graph(*common, threads, _t_ptr(ptr), _t_ptr(batch), _t_ptr(edge_index),
-                                          *(_t_ptr(t) for t in (csr or (None,) * 5))), "vgh_collate_graph")
-        for key in g["keys"]:
-            if key == "edge_index":
-                out[key] = edge_index
-            elif key in g["lists"]:
-                vals = g["lists"][key]
-                out[key] = [[vals[int(b)]] * self.num_nodes(kind, int(b)) for b in index]
-            else:
-                src = a[key]
-                dst = empty((n,) + tuple(src.shape[1:]), _NP_TO_TORCH[src.dtype])
-                row_bytes = int(src.strides[0]) if src.ndim > 1 else src.dtype.itemsize
-                if not src.flags.c_contiguous:
-                    raise ValueError(f"{kind}.{key} is not C-contiguous")
-                _host_check(lib.vgh_collate_rows(_np_ptr(src), row_bytes, _np_ptr(a["node_ptr"]), self.num_buildings,
-                                                 _np_ptr(index), count, _t_ptr(dst), threads), "vgh_collate_rows")
-                out[key] = dst
-        out["batch"] = batch
-        out["ptr"] = ptr
-        gb = GraphBatch(**out)
-        gb.set_derived("ptr_host", [int(v) for v in ptr.tolist()])
-        if csr is not None:
-            gb.set_derived("csr_arrays", csr)
-            # the largest in-degree (self loop included) from the host row_ptr:
-            # the device side sizes its padded column array (CSR.ell) without a sync
-            rp = csr[0].numpy()
-            gb.set_derived("csr_max_degree", int(np.diff(rp).max()) if rp.size > 1 else 0)
-        return gb
-
-    def collate(self, indices: Sequence[int], pin: bool = False, threads: int = 4) -> Tuple[GraphBatch, GraphBatch]:
-        """(local, voxel) GraphBatch of the buildings ``indices`` (in order);
-        ``pin`` allocates page-locked buffers for an asynchronous upload."""
+    def collate_pair(self, indices: Sequence[int], pin: bool = False, threads: int = 4,
+                     prepare=None) -> Tuple[GraphBatch, GraphBatch]:
+        """(local, voxel) GraphBatch of the buildings ``indices`` (in order), all
+        tensors views of one host buffer (page-locked with ``pin``).
+        ``prepare`` = the number of classes (or (classes, extra stacked copy
+        counts), ``_prepare_spec``): also the voxel batch's per-batch
+        structures (vgan.data.prepared: padded columns, the critic's stacked
+        graph and its padded columns, the type-matched mean | voxel.x, the float
+        one-hot, the critic's adjoint seeds), bit for bit what the device
+        would build."""
         index = np.ascontiguousarray(np.asarray(list(indices), dtype=np.int64))
         if index.size == 0:
             raise ValueError("collate needs at least one building")
-        return tuple(self._collate_kind(kind, index, pin, threads) for kind in KINDS)  # type: ignore[return-value]
+        lib = host_lib()
+        sizes, items, extras = self._layout(index, prepare)
+        layout, off = {}, 0
+        for name, shape, dt in items:
+            nbytes = int(np.prod(shape)) * torch.empty((), dtype=dt).element_size()
+            layout[name] = (off, tuple(shape), dt)
+            off += (nbytes + 255) // 256 * 256
+        blob = torch.empty(max(off, 256), dtype=torch.uint8, pin_memory=pin)
+        v = {name: _view(blob, *layout[name]) for name in layout}
+        out = []
+        for kind in KINDS:
+            n, e, ep, common = sizes[kind]
+            csr = tuple(v[f"{kind}.csr.{k}"] for k in ("row_ptr", "col", "csc_ptr", "csc_slot", "csc_dst")) \
+                if kind in CSR_KINDS else (None,) * 5
+            _host_check(lib.vgh_collate_graph(*common, threads, _t_ptr(v[f"{kind}.ptr"]), _t_ptr(v[f"{kind}.batch"]),
+                                              _t_ptr(v[f"{kind}.edge_index"]), *(_t_ptr(t) for t in csr)),
+                        "vgh_collate_graph")
+            a = self._arr[kind]
+            g = self.meta["graphs"][kind]
+            attrs = {}
+            for key in g["keys"]:
+                if key == "edge_index":
+                    attrs[key] = v[f"{kind}.edge_index"]
+                elif key in g["lists"]:
+                    vals = g["lists"][key]
+                    attrs[key] = [[vals[int(b)]] * self.num_nodes(kind, int(b)) for b in index]
+                else:
+                    src, dst = a[key], v[f"{kind}.{key}"]
+                    if not src.flags.c_contiguous:
+                        raise ValueError(f"{kind}.{key} is not C-contiguous")
+                    row_bytes = int(src.strides[0]) if src.ndim > 1 else src.dtype.itemsize
+                    _host_check(lib.vgh_collate_rows(_np_ptr(src), row_bytes, _np_ptr(a["node_ptr"]),
+                                                     self.num_buildings, _np_ptr(index), int(index.size),
+                                                     _t_ptr(dst), threads), "vgh_collate_rows")
+                    attrs[key] = dst
+            attrs["batch"] = v[f"{kind}.batch"]
+            attrs["ptr"] = v[f"{kind}.ptr"]
+            gb = GraphBatch(**attrs)
+            gb.set_derived("ptr_host", [int(x) for x in attrs["ptr"].tolist()])
+            if kind in CSR_KINDS:
+                gb.set_derived("csr_arrays", csr)
+                # the largest in-degree (self loop included) from the host row_ptr:
+                # the device side sizes its padded column array without a sync
+                rp = csr[0].numpy()
+                gb.set_derived("csr_max_degree", int(np.diff(rp).max()) if rp.size > 1 else 0)
+            out.append(gb)
+        local, voxel = out
+        if extras is not None:
+            self._prepare(local, voxel, v, extras)
+        for gb in out:
+            gb.set_derived("blob", (blob, layout))
+        return local, voxel
+
+    @staticmethod
+    def _prepare(local: GraphBatch, voxel: GraphBatch, v: Dict[str, torch.Tensor], extras: dict) -> None:
+        lib = host_lib()
+        n = voxel.num_nodes
+        rp, col, cp, cs, cd = voxel.derived("csr_arrays")
+        ep = col.numel()
+        k, fl, w = extras["n_classes"], extras["fl"], extras["ell_width"]
+        lx = local.x
+        if lx.dtype != torch.float32 or not lx.is_contiguous() or local.type.dtype != torch.int64 \
+                or voxel.type.dtype != torch.int64 or voxel.x.dtype != torch.float32:
+            raise ValueError("prepare: local.x / voxel.x must be float32 and the types int64")
+        mv = v["prep.matched_voxel_x"]
+        _host_check(lib.vgh_type_mean(_t_ptr(lx), _t_ptr(local.type), lx.shape[0], fl, _t_ptr(voxel.type), n, k,
+                                      _t_ptr(mv), mv.shape[1], 0), "vgh_type_mean")
+        mv[:, fl:].copy_(voxel.x)
+        v["prep.matched_x"].copy_(mv[:, :fl])
+        v["prep.onehot_f"].copy_(voxel.types_onehot)
+        seeds = v["prep.critic_seeds4"]  # vgan.critic.CriticEngine.prepare_batch
+        seeds.zero_()
+        seeds[:n] = -1.0 / n
+        seeds[n:2 * n] = 1.0 / n
+        seeds[3 * n:] = 1.0
+        names = ["matched_voxel_x", "matched_x", "onehot_f", "critic_seeds4"]
+        if w:
+            _host_check(lib.vgh_csr_ell(_t_ptr(rp), _t_ptr(col), n, w, _t_ptr(v["prep.ell"])), "vgh_csr_ell")
+            names.append("ell")
+        for c in extras["copies"]:
+            st = tuple(v[f"prep.stacked{c}.{kk}"] for kk in ("row_ptr", "col", "csc_ptr", "csc_slot", "csc_dst"))
+            _host_check(lib.vgh_csr_stacked(*(_t_ptr(t) for t in (rp, col, cp, cs, cd)), n, ep, c,
+                                            *(_t_ptr(t) for t in st)), "vgh_csr_stacked")
+            names += [f"stacked{c}.{kk}" for kk in ("row_ptr", "col", "csc_ptr", "csc_slot", "csc_dst")]
+            if w:
+                _host_check(lib.vgh_csr_ell(_t_ptr(st[0]), _t_ptr(st[1]), c * n, w, _t_ptr(v[f"prep.stacked{c}_ell"])),
+                            "vgh_csr_ell")
+                names.append(f"stacked{c}_ell")
+        voxel.set_derived("prepared_arrays", {
+            "names": names, "views": {nm: v[f"prep.{nm}"] for nm in names}, "ell_width": w,
+            "max_degree": extras["max_degree"], "n_classes": k, "copies": extras["copies"],
+            # the program batch these were built from (vgan.data checks the pairing)
+            "local": (local.x.data_ptr(), local.type.data_ptr())})
+        _stamp_versions(local, voxel)
+
+    def collate(self, indices: Sequence[int], pin: bool = False, threads: int = 4,
+                prepare=None) -> Tuple[GraphBatch, GraphBatch]:
+        """(local, voxel) GraphBatch of the buildings ``indices`` (in order);
+        ``pin`` allocates the page-locked buffer of an asynchronous upload."""
+        return self.collate_pair(indices, pin=pin, threads=threads, prepare=prepare)
+
+
+def _view(blob: torch.Tensor, off: int, shape, dtype) -> torch.Tensor:
+    nbytes = int(np.prod(shape)) * torch.empty((), dtype=dtype).element_size()
+    return blob[off:off + nbytes].view(dtype).view(shape)
+
+
+def upload_pair(local: GraphBatch, voxel: GraphBatch, device, non_blocking: bool = True
+                ) -> Tuple[GraphBatch, GraphBatch]:
+    """A collated pair on ``device``: its host buffer copied in ONE
+    host-to-device copy, every tensor (node attributes, the CSR / CSC, the
+    prepared structures) a view of the device copy.  Pairs without a shared
+    buffer fall back to per-tensor ``.to``."""
+    b1, b2 = local.derived("blob"), voxel.derived("blob")
+    if b1 is None or b2 is None or b1[0] is not b2[0]:
+        return local.to(device, non_blocking=non_blocking), voxel.to(device, non_blocking=non_blocking)
+    blob, layout = b1
+    dev_blob = blob.to(device, non_blocking=non_blocking)
+    by_ptr = {}
+    for name, (off, shape, dt) in layout.items():
+        by_ptr[_view(blob, off, shape, dt).data_ptr(), tuple(shape), dt] = _view(dev_blob, off, shape, dt)
+
+    def move(t):
+        if not torch.is_tensor(t):
+            return t
+        hit = by_ptr.get((t.data_ptr(), tuple(t.shape), t.dtype))
+        return hit if hit is not None else t.to(device, non_blocking=non_blocking)
+
+    out = []
+    for gb in (local, voxel):
+        moved = GraphBatch(**{k: move(getattr(gb, k)) for k in gb.keys()})
+        for key in ("ptr_host", "csr_max_degree"):
+            if gb.derived(key) is not None:
+                moved.set_derived(key, gb.derived(key))
+        if gb.derived("csr_arrays") is not None:
+            moved.set_derived("csr_arrays", tuple(move(t) for t in gb.derived("csr_arrays")))
+        pa = gb.derived("prepared_arrays")
+        if pa is not None:
+            moved.set_derived("prepared_arrays", dict(pa, views={k: move(t) for k, t in pa["views"].items()}))
+        moved.set_derived("device_blob", dev_blob)
+        out.append(moved)
+    lo, vo = out
+    pa = vo.derived("prepared_arrays")
+    if pa is not None:  # the pairing key, now of the device tensors
+        vo.set_derived("prepared_arrays", dict(pa, local=(lo.x.data_ptr(), lo.type.data_ptr())))
+        _stamp_versions(lo, vo)
+    return lo, vo
+
+
+def _stamp_versions(local: GraphBatch, voxel: GraphBatch) -> None:
+    """The inputs' autograd version counters when the prepared structures
+    were built: an in-place edit afterwards invalidates them (vgan.data)."""
+    pa = voxel.derived("prepared_arrays")
+    pa["versions"] = tuple(t._version for t in (local.x, local.type, voxel.x, voxel.type, voxel.types_onehot,
+                                                voxel.edge_index))
 
 
 def write_store(path: str, dataset, indices: Optional[Sequence[int]] = None) -> GraphStore:

@@ -148,17 +148,14 @@ def _building(rng: np.random.Generator, number: int, F: int, Y: int, X: int,
         ],
         1,
     )
-    # same-floor chain + same-type link to the next floor
-    pairs = set()
-    for a in range(m):
-        for b in range(m):
-            if a == b:
-                continue
-            if lf[a] == lf[b] and abs(a - b) == 1:
-                pairs.add((a, b))
-            elif abs(int(lf[a]) - int(lf[b])) == 1 and lt[a] == lt[b] and l_id[a] == l_id[b]:
-                pairs.add((a, b))
-    lei = np.array(sorted(pairs), dtype=np.int64).reshape(-1, 2).T
+    # same-floor chain + same-type link to the next floor; pairs (a, b) in
+    # lexicographic order (the nonzeros of the m x m relation, row-major)
+    ida = np.array(l_id, dtype=np.int64)
+    idx = np.arange(m)
+    chain = (lf[:, None] == lf[None, :]) & (np.abs(idx[:, None] - idx[None, :]) == 1)
+    link = (np.abs(lf[:, None] - lf[None, :]) == 1) & (lt[:, None] == lt[None, :]) & (ida[:, None] == ida[None, :])
+    rel = (chain | link) & (idx[:, None] != idx[None, :])
+    lei = np.stack(np.nonzero(rel)).astype(np.int64).reshape(2, -1)
     local = GraphData(
         x=torch.tensor(lx, dtype=torch.float32),
         edge_index=torch.from_numpy(np.ascontiguousarray(lei)),

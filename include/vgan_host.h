@@ -33,6 +33,12 @@ int vgh_collate_sizes(const int64_t* node_ptr, const int64_t* edge_ptr, const in
                       const int32_t* edst, int64_t num_buildings, const int64_t* index, int32_t count,
                       int64_t* sizes);
 
+/* The largest in-degree of the batch's GATConv graph (self loop included,
+ * i->i edges dropped as remove_self_loops does): sizes the padded column array. */
+int vgh_collate_max_in_degree(const int64_t* node_ptr, const int64_t* edge_ptr, const int32_t* esrc,
+                              const int32_t* edst, int64_t num_buildings, const int64_t* index, int32_t count,
+                              int32_t* max_degree);
+
 /* One node-level attribute (x, type, types_onehot, site_area ...; data.py:117-147):
  * the selected buildings' row blocks of `row_bytes` bytes concatenated into dst
  * (torch.cat(..., dim=0) of Batch.from_data_list). */
@@ -49,6 +55,24 @@ int vgh_collate_graph(const int64_t* node_ptr, const int64_t* edge_ptr, const in
                       const int32_t* edst, int64_t num_buildings, const int64_t* index, int32_t count,
                       int32_t threads, int64_t* ptr, int64_t* batch, int64_t* edge_index, int32_t* row_ptr,
                       int32_t* col, int32_t* csc_ptr, int32_t* csc_slot, int32_t* csc_dst);
+
+/* ---- per-batch structures of vgan.data.prepared, built on the host ---- */
+
+/* ell[n * width]: row i's CSR sources in order, -1 past its degree (vg_csr_ell). */
+int vgh_csr_ell(const int32_t* row_ptr, const int32_t* col, int32_t n, int32_t width, int32_t* ell);
+
+/* The block-diagonal CSR/CSC of `copies` copies of a CSR/CSC over n nodes and
+ * `slots` slots (node ids and slots offset per copy): vgan.ops.CSR.stacked. */
+int vgh_csr_stacked(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_ptr, const int32_t* csc_slot,
+                    const int32_t* csc_dst, int32_t n, int32_t slots, int32_t copies, int32_t* s_row_ptr,
+                    int32_t* s_col, int32_t* s_csc_ptr, int32_t* s_csc_slot, int32_t* s_csc_dst);
+
+/* The type-matched mean of models.py:122-129 (vg_type_mean, bit for bit): out[v,
+ * out_col0 + f] = mean of local_x[:, f] over the program nodes whose type is
+ * voxel v's, 0 where no program node has it. */
+int vgh_type_mean(const float* local_x, const int64_t* local_type, int32_t n_local, int32_t feat,
+                  const int64_t* voxel_type, int32_t n_voxel, int32_t n_types, float* out, int32_t out_stride,
+                  int32_t out_col0);
 
 #ifdef __cplusplus
 }

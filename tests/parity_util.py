@@ -246,6 +246,92 @@ def step_iterations_vs_oracle(cuda, cfg, g0, d0, vgan_pair, oracle_pair, step_se
         assert ok, (path, worst, total)
 
 
+def _rel_cos(got: dict, want: dict):
+    """(relative L2 error, cosine) of two gradient dicts as whole vectors."""
+    a = torch.cat([got[k].detach().reshape(-1).double().cpu() for k in sorted(want)])
+    b = torch.cat([want[k].detach().reshape(-1).double().cpu() for k in sorted(want)])
+    return float((a - b).norm() / b.norm().clamp_min(1e-30)), float(torch.nn.functional.cosine_similarity(a, b, dim=0))
+
+
+def step_iterations_bf16_vs_oracle(cuda, cfg, g0, d0, vgan_pair, oracle_pair, step_seed: int,
+                                   bounds: dict) -> dict:
+    """configs[2]'s arithmetic against the f32 reference step: every critic
+    iteration and the generator iteration in bf16 (every dense product on
+    bf16 operands, f32 accumulation -- runtime['precision'] = 'bf16') from
+    the reference's parameters and replayed CPU draws, against the CPU oracle
+    in f32.  Returns the measured deviations; asserts ``bounds``:
+    label_soft (max |d soft|), label_mismatch (argmax fraction), d_loss /
+    g_loss (relative), d_grad / g_grad (relative L2 of the whole gradient),
+    d_cos / g_cos (cosine, lower bound)."""
+    from oracle import reference as R
+    from vgan._lib import gemm_precision_scope
+    from vgan.models import VoxelGNNDiscriminator, VoxelGNNGenerator
+    from vgan.trainer import Trainer
+
+    cfg.runtime["rng"] = "host"
+    cfg.runtime["precision"] = "bf16"
+    G, D = VoxelGNNGenerator(cfg, 17, 12), VoxelGNNDiscriminator(cfg, 17, 12)
+    G.load_state_dict(g0)
+    D.load_state_dict(d0)
+    tr = Trainer(G, D, None, torch.optim.Adam(G.parameters(), lr=2e-4, betas=cfg.BETAS),
+                 torch.optim.Adam(D.parameters(), lr=2e-4, betas=cfg.BETAS), None, cfg)
+    Go, Do = R.Generator(cfg), R.Discriminator(cfg)
+    Go.load_state_dict(g0)
+    Do.load_state_dict(d0)
+    od = torch.optim.Adam(Do.parameters(), lr=cfg.LEARNING_RATE_DISCRIMINATOR, betas=cfg.BETAS)
+    loc, vox = vgan_pair
+    ol, ov = oracle_pair
+    torch.manual_seed(step_seed)
+    m = {k: 0.0 for k in ("label_soft", "label_mismatch", "d_loss", "d_grad", "g_loss", "g_grad")}
+    m["d_cos"] = m["g_cos"] = 1.0
+    with gemm_precision_scope("bf16"):
+        for it in range(cfg.N_CRITIC):
+            state = torch.get_rng_state()
+            with torch.no_grad():
+                _, hard, soft = tr._generate(loc, vox)
+            mid = torch.get_rng_state()
+            torch.set_rng_state(state)
+            with torch.no_grad():
+                _, ho, so = Go(ol, ov, torch.randn(1, ov.num_nodes, cfg.Z_DIM))
+            m["label_soft"] = max(m["label_soft"], (soft.squeeze(0).cpu() - so).abs().max().item())
+            m["label_mismatch"] = max(m["label_mismatch"],
+                                      (hard.squeeze(0).cpu().argmax(1) != ho.argmax(1)).float().mean().item())
+            tr.adam_d.zero_grad()
+            d_loss = tr._critic_loss_backward(loc, vox, ho.unsqueeze(0).to(cuda), so.unsqueeze(0).to(cuda))
+            after = torch.get_rng_state()
+            torch.set_rng_state(mid)
+            od.zero_grad()
+            d_ref = R.discriminator_loss(Do, cfg, ol, ov, ho.unsqueeze(0), so.unsqueeze(0))
+            d_ref.backward()
+            assert torch.equal(torch.get_rng_state(), after)  # the critic engine drew eps as the reference
+            m["d_loss"] = max(m["d_loss"], abs(d_loss.item() - d_ref.item()) / max(1.0, abs(d_ref.item())))
+            rel, cos = _rel_cos({k: p.grad for k, p in D.named_parameters()},
+                                {k: p.grad for k, p in Do.named_parameters()})
+            m["d_grad"], m["d_cos"] = max(m["d_grad"], rel), min(m["d_cos"], cos)
+            od.step()
+            with torch.no_grad():  # continue from the reference's parameters
+                for p, q in zip(D.parameters(), Do.parameters()):
+                    p.copy_(q.to(p.device))
+        state = torch.get_rng_state()
+        Go.zero_grad()
+        lo, ho, _ = Go(ol, ov, torch.randn(1, ov.num_nodes, cfg.Z_DIM))
+        g_ref = R.generator_loss(Do, cfg, ol, ov, lo, ho.unsqueeze(0))
+        g_ref.backward()
+        torch.set_rng_state(state)
+        tr.adam_g.zero_grad()
+        g_loss, hard = tr._gen_iteration(loc, vox)
+        m["g_loss"] = abs(g_loss.item() - g_ref.item()) / max(1.0, abs(g_ref.item()))
+        m["g_grad"], m["g_cos"] = _rel_cos({k: p.grad for k, p in G.named_parameters()},
+                                           {k: p.grad for k, p in Go.named_parameters()})
+    print("bf16 step vs f32 oracle:", {k: f"{v:.3e}" for k, v in m.items()})
+    for k, v in bounds.items():
+        if k.endswith("_cos"):
+            assert m[k] >= v, (k, m[k], v)
+        else:
+            assert m[k] <= v, (k, m[k], v)
+    return m
+
+
 def run_smoke() -> None:
     """One small G forward + D WGAN-GP loss backward on cuda:0 vs the oracle."""
     from oracle import reference as R

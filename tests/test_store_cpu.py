@@ -270,3 +270,57 @@ def test_host_library_exports_header():
     assert syms and not [s for s in syms if s not in exported]
     assert sorted(store.HOST_SIGNATURES) == syms
     ctypes.CDLL(lib)
+
+
+def test_host_prepared_structures(tmp_path):
+    """collate(prepare=K): the per-batch structures vgan.data builds on the
+    device, built on the host into the pair's one buffer -- the type-matched
+    mean (models.py:122-129; the oracle's restatement) | voxel.x, the float
+    one-hot, the padded column array, the critic's stacked real / fake / mix
+    CSR / CSC and its padded columns, the adjoint seeds -- and every tensor of
+    the pair is a view of that buffer."""
+    from oracle.reference import type_matched_mean
+    from oracle import pyg
+    from vgan.store import write_store
+    from vgan.synth import SyntheticDataset
+
+    ds = SyntheticDataset(10, seed=31)
+    st = write_store(str(tmp_path / "s"), ds)
+    loc, vox = st.collate([3, 1, 8, 1], prepare=7)
+    pa = vox.derived("prepared_arrays")
+    v = pa["views"]
+    n = vox.num_nodes
+    blob = vox.derived("blob")[0]
+    assert loc.derived("blob")[0] is blob
+    lo, hi = blob.data_ptr(), blob.data_ptr() + blob.numel()
+    for t in [getattr(g, k) for g in (loc, vox) for k in g.keys() if torch.is_tensor(getattr(g, k))] + \
+            list(v.values()) + list(vox.derived("csr_arrays")):
+        assert lo <= t.data_ptr() < hi
+    want_tm = type_matched_mean(loc.x, loc.type, vox.type)
+    assert torch.allclose(v["matched_x"], want_tm, rtol=1e-6, atol=1e-7)
+    assert torch.equal(v["matched_voxel_x"][:, :17], v["matched_x"]) and torch.equal(v["matched_voxel_x"][:, 17:], vox.x)
+    assert torch.equal(v["onehot_f"], vox.types_onehot.float())
+    seeds = v["critic_seeds4"].view(-1)
+    assert torch.equal(seeds[:n], torch.full((n,), -1.0 / n)) and torch.equal(seeds[n:2 * n], torch.full((n,), 1.0 / n))
+    assert not seeds[2 * n:3 * n].any() and torch.equal(seeds[3 * n:], torch.ones(n))
+    rp, col, cp, cs, cd = vox.derived("csr_arrays")
+    w = pa["ell_width"]
+    assert w == 8 and pa["max_degree"] == int((rp[1:] - rp[:-1]).max())
+    ell = v["ell"].view(n, w)
+    for i in range(n):
+        d = int(rp[i + 1] - rp[i])
+        assert torch.equal(ell[i, :d], col[rp[i]:rp[i + 1]]) and (ell[i, d:] == -1).all()
+    e = col.numel()
+    s = {k: v[f"stacked3.{k}"] for k in ("row_ptr", "col", "csc_ptr", "csc_slot", "csc_dst")}
+    for c in range(3):  # vgan.ops.CSR.stacked: node ids and slots offset per copy
+        assert torch.equal(s["row_ptr"][c * n:(c + 1) * n], rp[:-1] + c * e)
+        assert torch.equal(s["csc_ptr"][c * n:(c + 1) * n], cp[:-1] + c * e)
+        assert torch.equal(s["col"][c * e:(c + 1) * e], col + c * n)
+        assert torch.equal(s["csc_slot"][c * e:(c + 1) * e], cs + c * e)
+        assert torch.equal(s["csc_dst"][c * e:(c + 1) * e], cd + c * n)
+    assert int(s["row_ptr"][-1]) == int(s["csc_ptr"][-1]) == 3 * e
+    sell = v["stacked3_ell"].view(3 * n, w)
+    assert torch.equal(sell[n:2 * n], torch.where(ell >= 0, ell + n, ell))
+    # and the CSR itself is the oracle's GATConv edge list
+    want = pyg.gat_csr(vox.edge_index, n)
+    assert torch.equal(rp, want[0]) and torch.equal(col, want[1])

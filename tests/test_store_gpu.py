@@ -78,3 +78,49 @@ def test_generator_forward_identical_on_loader_batch(cuda, ds_store):
     assert data.prepared(loc_b, vox_b, 7).csr.row_ptr is vox_b.derived("csr_arrays")[0]
     for a, b in zip(out_a, out_b):
         _same(a, b, "generator output")
+
+
+def test_host_prepared_batch_equals_device_build(cuda, ds_store):
+    """A batch from the loader with ``prepare``: one host-to-device copy of the
+    pair's buffer, and vgan.data adopts the host-built structures -- each bit
+    for bit what the device builds from the same batch (vg_type_mean, the
+    float one-hot, vg_csr_ell, CSR.stacked(3) and its padded columns, the
+    critic's seeds); a step on it equals a step on the device-built batch."""
+    from vgan.critic import CriticEngine  # noqa: F401  (prepare_batch semantics)
+
+    _, st = ds_store
+    loader = GraphLoader(st, [2, 7, 5, 0, 9], batch_size=5, shuffle=False, device=cuda, prefetch=1, prepare=7)
+    (loc, vox), = list(loader)
+    blob = vox.derived("device_blob")
+    assert blob is not None and loc.derived("device_blob") is blob
+    prep = data.prepared(loc, vox, 7)
+    v = vox.derived("prepared_arrays")["views"]
+    assert prep.matched_voxel_x is v["matched_voxel_x"] and prep.consts["critic_seeds4"] is v["critic_seeds4"]
+    # the same batch rebuilt on the device
+    loc2 = type(loc)(**{k: (getattr(loc, k).clone() if torch.is_tensor(getattr(loc, k)) else getattr(loc, k))
+                        for k in loc.keys()})
+    vox2 = type(vox)(**{k: (getattr(vox, k).clone() if torch.is_tensor(getattr(vox, k)) else getattr(vox, k))
+                        for k in vox.keys()})
+    ref = data.prepared(loc2, vox2, 7)
+    assert "critic_seeds4" not in ref.consts
+    from vgan.critic import CriticEngine as CE
+
+    CE.prepare_batch(None, ref)
+    _same(prep.matched_voxel_x, ref.matched_voxel_x, "type-matched mean | voxel.x")
+    _same(prep.matched_x, ref.matched_x, "matched_x")
+    _same(prep.onehot_f, ref.onehot_f, "onehot_f")
+    _same(prep.consts["critic_seeds4"], ref.consts["critic_seeds4"], "seeds")
+    for name in ("row_ptr", "col", "csc_ptr", "csc_slot", "csc_dst"):
+        _same(getattr(prep.csr, name), getattr(ref.csr, name), name)
+    e1, w1 = prep.csr.ell()
+    e2, w2 = ref.csr.ell()
+    assert w1 == w2 == 8
+    _same(e1, e2, "ell")
+    s1, s2 = prep.csr.stacked(3), ref.csr.stacked(3)
+    for name in ("row_ptr", "col", "csc_ptr", "csc_slot", "csc_dst"):
+        _same(getattr(s1, name), getattr(s2, name), "stacked " + name)
+    assert s1.seg_rows == s2.seg_rows == vox.num_nodes
+    _same(s1.ell()[0], s2.ell()[0], "stacked ell")
+    # an in-place edit of the batch invalidates the host-built structures
+    vox.x.mul_(1.0)
+    assert data.prepared(loc, vox, 7).matched_voxel_x is not v["matched_voxel_x"]

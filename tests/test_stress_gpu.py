@@ -1,0 +1,157 @@
+"""configs[3] at full size: 8 x 50k-voxel stress buildings (20 floors of 50 x 50,
+4-neighbour floors plus 3 x 3 blocks to the floors above and below; N = 400,000,
+E' = 8,626,816 with the self loops), the scatter / LDS bandwidth stress graph the
+bench times.
+
+* every aggregation kernel -- the register gather (vg_gat_aggregate_fwd: the
+  64-channel slice path at this size), the padded-column form (ELL), the
+  16-row LDS tile kernel and the persistent staged kernel -- at C = 128 / 64 / 1
+  where it applies, in three voxel numberings (the reference's row-major, 4 x 4
+  floor tiles, 4 x 4 x 4 lattice blocks), against the f64 oracle
+  (``oracle.pyg.gat_propagate``, the restated PyG 2.6.1 GATConv propagate) on
+  ~5,000 sampled destination rows -- the rows' exact in-edge subgraphs, so the
+  oracle sees the same softmax segments -- and bit for bit against each other;
+* one GATConv block (64 -> 128 channels) forward and backward on the whole
+  graph against autograd of the oracle's GATConv in f64: the upstream gradient
+  lives on the sampled rows, so every gradient (x, lin.weight, att_src,
+  att_dst, bias) is exactly that of the rows' subgraph.
+
+Match: models.py:144 (GATConv in the encoder stacks), SURVEY.md 8(d) cfg #4.
+"""
+import pytest
+import torch
+
+from oracle import pyg
+from parity_util import rel_err
+from vgan import ops, synth
+from vgan._lib import LIB, check, ptr
+from vgan.graph import GraphBatch
+from vgan.locality import blocked, tiled
+
+pytestmark = pytest.mark.gpu
+
+ORDERS = ("rowmajor", "tiled", "blocked")
+
+
+@pytest.fixture(scope="module")
+def stress_items():
+    return [synth.make_stress_building(777, i)[1] for i in range(8)]
+
+
+_GRAPHS = {}
+
+
+def _graph(order, items, cuda):
+    if order not in _GRAPHS:
+        vs = items if order == "rowmajor" else [tiled(v, 4)[0] if order == "tiled" else blocked(v)[0] for v in items]
+        vox = GraphBatch.from_data_list(vs)
+        ei = vox.edge_index
+        csr = ops.CSR(ei.to(cuda), vox.num_nodes)
+        _GRAPHS.clear()  # one numbering resident at a time
+        _GRAPHS[order] = (ei, vox.num_nodes, csr)
+    return _GRAPHS[order]
+
+
+def _sample_rows(n, seed=0, k=4096):
+    g = torch.Generator().manual_seed(seed)
+    edges = torch.cat([torch.arange(64), torch.arange(n - 64, n)]
+                      + [torch.arange(b * 50000 - 8, b * 50000 + 8) for b in range(1, 8)])
+    return torch.unique(torch.cat([torch.randint(0, n, (k,), generator=g), edges]))
+
+
+def _subgraph(ei, rows):
+    """The rows' in-edges (self loops removed: GATConv re-adds them), relabelled
+    onto the compact node set V = rows + their sources; (V, edges, rows in V)."""
+    ei = pyg.remove_self_loops(ei)
+    sub = ei[:, torch.isin(ei[1], rows)]
+    V = torch.unique(torch.cat([rows, sub[0]]))
+    return V, torch.searchsorted(V, sub), torch.searchsorted(V, rows)
+
+
+def _oracle_rows(h, a_s, a_d, bias, ei, rows):
+    V, sub, rl = _subgraph(ei, rows)
+    out = pyg.gat_propagate(h.cpu()[V].double(), a_s.cpu()[V].double(), a_d.cpu()[V].double(), sub)
+    return (out + bias.cpu().double())[rl]
+
+
+def _run(kind, csr, c, h, a_s, a_d, b):
+    n = csr.num_nodes
+    out = torch.empty(n, c, device=h.device)
+    alpha = torch.empty(csr.num_edges, device=h.device)
+    args = (c, ptr(h), ptr(a_s), ptr(a_d), ptr(b), 0.2, ptr(out), ptr(alpha))
+    if kind == "register":
+        check(LIB.vg_gat_aggregate_fwd(ptr(csr.row_ptr), ptr(csr.col), n, *args, csr.stream()), kind)
+    elif kind == "ell":
+        ell, w = csr.ell()
+        assert ell is not None and w == 32  # the stress lattice's largest degree is 23
+        check(LIB.vg_gat_aggregate_fwd_ell(ptr(csr.row_ptr), ptr(csr.col), ptr(ell), w, n, *args, csr.stream()), kind)
+    elif kind == "lds":
+        plan = csr.tile_plan()
+        check(LIB.vg_gat_aggregate_fwd_lds(ptr(csr.row_ptr), ptr(csr.col), n, *args, ptr(plan), csr._tile_umax,
+                                           csr.stream()), kind)
+    else:
+        check(LIB.vg_gat_aggregate_fwd_staged(ptr(csr.row_ptr), ptr(csr.col), n, *args, ptr(csr.stage_plan()),
+                                              csr.stream()), kind)
+    return out, alpha
+
+
+@pytest.mark.parametrize("order", ORDERS)
+@pytest.mark.parametrize("C", [128, 64, 1])
+def test_stress_aggregations_against_oracle(cuda, stress_items, order, C):
+    ei, n, csr = _graph(order, stress_items, cuda)
+    assert n == 400000 and csr.num_edges == 8626816
+    torch.manual_seed(C)
+    h = torch.randn(n, C, device=cuda)
+    a_s, a_d = 0.5 * torch.randn(n, device=cuda), 0.5 * torch.randn(n, device=cuda)
+    b = torch.randn(C, device=cuda)
+    kinds = ["register", "ell"] + (["lds"] if C % 64 == 0 else []) + (["staged"] if C in (64, 128) else [])
+    outs = {k: _run(k, csr, C, h, a_s, a_d, b) for k in kinds}
+    torch.cuda.synchronize()
+    ref_out, ref_alpha = outs["register"]
+    for k in kinds[1:]:  # the same 16-lane softmax grouping and gather order: bit for bit
+        assert torch.equal(outs[k][0], ref_out), k
+        assert torch.equal(outs[k][1], ref_alpha), k
+    rows = _sample_rows(n, seed=C)
+    want = _oracle_rows(h, a_s, a_d, b, ei, rows)
+    err = rel_err(ref_out.cpu()[rows], want)
+    print(f"{order} C={C}: {len(rows)} rows, rel err vs f64 oracle {err:.2e}")
+    assert err < 1e-5
+    if "staged" in kinds:
+        ucount = csr.stage_plan()[:csr.stage_tiles()].cpu()
+        print(f"{order}: {int((ucount > 0).sum())} staged tiles, {int((ucount < 0).sum())} from global memory")
+        if order == "blocked":
+            assert (ucount > 0).all()  # every 4 x 4 x 4 block fits the 288-row image
+
+
+def test_stress_gat_block_forward_backward_against_oracle(cuda, stress_items):
+    from vgan.models import GATConv
+
+    ei, n, csr = _graph("blocked", stress_items, cuda)
+    torch.manual_seed(5)
+    conv = GATConv(64, 128).to(cuda)
+    with torch.no_grad():
+        conv.bias.normal_()
+    ref = pyg.GATConv(64, 128).double()
+    ref.load_state_dict({k: v.detach().cpu().double() for k, v in conv.state_dict().items()})
+    x = torch.randn(n, 64, device=cuda, requires_grad=True)
+    y = conv(x, csr)
+    rows = _sample_rows(n, seed=7, k=2048)
+    g = torch.zeros(n, 128, device=cuda)
+    g[rows.to(cuda)] = torch.randn(len(rows), 128, device=cuda)
+    y.backward(g)
+    torch.cuda.synchronize()
+    V, sub, rl = _subgraph(ei, rows)
+    xr = x.detach().cpu()[V].double().requires_grad_(True)
+    yr = ref(xr, sub)
+    (yr[rl] * g.cpu()[rows].double()).sum().backward()
+    assert rel_err(y.detach().cpu()[rows], yr.detach()[rl]) < 1e-5
+    gx = x.grad.cpu()
+    outside = torch.ones(n, dtype=torch.bool)
+    outside[V] = False
+    assert torch.count_nonzero(gx[outside]) == 0  # no gradient outside the rows' subgraph
+    errs = {"x": rel_err(gx[V], xr.grad)}
+    for name, p in conv.named_parameters():
+        errs[name] = rel_err(p.grad.cpu().reshape(-1), dict(ref.named_parameters())[name].grad.reshape(-1))
+    print({k: f"{v:.2e}" for k, v in errs.items()})
+    for k, v in errs.items():
+        assert v < 1e-4, k
