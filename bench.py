@@ -337,29 +337,35 @@ def timed_steps(tr, pool, steps: int, warmup: int, world: int, device, profile: 
 
 def stress_roofline(device, channels=(128, 64, 1), reps: int = 20, order: str = "rowmajor"):
     """vg_gat_aggregate_fwd on config #4 (8 x 50k-node buildings), cold MALL;
-    for C a multiple of 64 also vg_gat_aggregate_fwd_lds (the tile plan's
-    distinct source rows staged through LDS, bit-identical output).
-    order "tiled": each building's voxels renumbered floor by floor in 4 x 4
-    (y, x) tiles (vgan.locality), so a 16-row workgroup aggregates a patch
-    instead of a strip; "rowmajor": the reference's numbering."""
+    for C a multiple of 64 also vg_gat_aggregate_fwd_lds (16-row tiles'
+    distinct source rows staged through LDS) and, for C = 64 / 128,
+    vg_gat_aggregate_fwd_staged (the persistent kernel staging 64-row tiles
+    while the previous tile is aggregated); all bit-identical.  order:
+    "rowmajor" (the reference's numbering), "tiled" (4 x 4 (y, x) tiles per
+    floor) or "blocked" (4 x 4 x 4 lattice blocks), vgan.locality."""
     from vgan import ops
     from vgan._lib import LIB, check, ptr, stream_handle
     from vgan.synth import make_stress_building
     from vgan.graph import GraphBatch
-    from vgan.locality import tiled
+    from vgan.locality import blocked, tiled
 
-    items = [make_stress_building(777, i) for i in range(8)]
-    voxels = [v for _, v in items] if order == "rowmajor" else [tiled(v, 4)[0] for _, v in items]
+    items = [make_stress_building(777, i)[1] for i in range(8)]
+    voxels = items if order == "rowmajor" else [tiled(v, 4)[0] if order == "tiled" else blocked(v)[0] for v in items]
     vox = GraphBatch.from_data_list(voxels).to(device)
     csr = ops.CSR(vox.edge_index, vox.num_nodes)
     n, e = csr.num_nodes, csr.num_edges
     plan = csr.tile_plan()
     tiles = (n + 15) // 16
     uniq = plan[:tiles].clamp_min(0).sum().item()
-    log(f"tile plan ({order}): {uniq / tiles:.1f} distinct sources for {e / tiles:.1f} edges per tile, "
-        f"largest {csr._tile_umax}, unplanned tiles {int((plan[:tiles] < 0).sum().item())}")
+    splan = csr.stage_plan()
+    uc = splan[:csr.stage_tiles()]
+    staged_tiles = int((uc > 0).sum().item())
+    s_uniq = float(uc.clamp_min(0).sum().item()) / max(1, staged_tiles)
+    log(f"tile plans ({order}): 16-row {uniq / tiles:.1f} distinct sources for {e / tiles:.1f} edges, "
+        f"64-row {s_uniq:.1f} for {4 * e / tiles:.1f} ({staged_tiles} staged, "
+        f"{int((uc < 0).sum().item())} from global memory)")
     scratch = torch.empty(512 * 1024 * 1024 // 4, device=device)  # flush the 256 MB MALL between reps
-    res, res_lds = {}, {}
+    res, res_lds, res_st = {}, {}, {}
     for c in channels:
         h = torch.randn(n, c, device=device)
         a_s, a_d = 0.3 * torch.randn(n, device=device), 0.3 * torch.randn(n, device=device)
@@ -375,6 +381,12 @@ def stress_roofline(device, channels=(128, 64, 1), reps: int = 20, order: str = 
                                                ptr(bias), 0.2, ptr(out), ptr(alpha), ptr(plan), csr._tile_umax,
                                                stream_handle(device)),
                   "vg_gat_aggregate_fwd_lds")
+
+        def run_staged():
+            check(LIB.vg_gat_aggregate_fwd_staged(ptr(csr.row_ptr), ptr(csr.col), n, c, ptr(h), ptr(a_s),
+                                                  ptr(a_d), ptr(bias), 0.2, ptr(out), ptr(alpha), ptr(splan),
+                                                  stream_handle(device)),
+                  "vg_gat_aggregate_fwd_staged")
 
         def timed(fn):
             for _ in range(3):
@@ -397,9 +409,15 @@ def stress_roofline(device, channels=(128, 64, 1), reps: int = 20, order: str = 
         if c % 64 == 0:
             avg = timed(run_lds)
             res_lds[c] = {"avg_us": avg * 1e3, "bytes": b, "achieved_gbs": b / (avg * 1e-3) / 1e9}
+        if c in (64, 128):
+            avg = timed(run_staged)
+            res_st[c] = {"avg_us": avg * 1e3, "bytes": b, "achieved_gbs": b / (avg * 1e-3) / 1e9}
     del scratch
-    return {"nodes": n, "edges": e, "per_channels": res, "per_channels_lds": res_lds, "order": order,
-            "distinct_sources_per_tile": round(uniq / tiles, 1), "edges_per_tile": round(e / tiles, 1)}
+    return {"nodes": n, "edges": e, "per_channels": res, "per_channels_lds": res_lds, "per_channels_staged": res_st,
+            "order": order, "distinct_sources_per_tile": round(uniq / tiles, 1), "edges_per_tile": round(e / tiles, 1),
+            "staged_plan": {"distinct_sources_per_64_row_tile": round(s_uniq, 1),
+                            "edges_per_64_row_tile": round(4 * e / tiles, 1), "staged_tiles": staged_tiles,
+                            "global_tiles": int((uc < 0).sum().item())}}
 
 
 def fresh_batch_leg(cfg, precision: str, steps: int, warmup: int, batch: int, device, rank: int, world: int):
@@ -422,7 +440,7 @@ def fresh_batch_leg(cfg, precision: str, steps: int, warmup: int, batch: int, de
     ds = SyntheticDataset(n_batches * batch * world, seed=4321)
     store = write_store(os.path.join(tmp, "store"), ds)
     loader = GraphLoader(store, batch_size=batch, shuffle=True, device=device, prefetch=3, rank=rank,
-                         world_size=world, seed=4321)
+                         world_size=world, seed=4321, prepare=cfg.NUM_CLASSES)
     torch.manual_seed(cfg.SEED + rank)
     tr = build_trainer(cfg, precision)
     cfg.runtime["train_step"] = "auto"
@@ -453,56 +471,85 @@ def fresh_batch_leg(cfg, precision: str, steps: int, warmup: int, batch: int, de
             "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps, "warmup": warmup,
             "execution": "Trainer._train_batch per new batch (step_fresh: critic iteration captured once per batch, "
                          "replayed N_CRITIC times; label forward and generator iteration eager), GraphLoader "
-                         "prefetch 3"}
+                         "prefetch 3: host collate + host-built per-batch structures, one upload per batch"}
 
 
-def sweep_leg(device, graphs: int = 10000, batch: int = 32, n_taus: int = 10, distinct: int = 20):
-    """BASELINE.json configs[4]: generator-only inference sweep, ``graphs``
-    building samples x a geometric Gumbel temperature schedule 1.0 -> 0.1,
-    f16 (and f32) eval forward, one stacked forward per batch of ``batch``
-    buildings over the ``n_taus`` copies, hipGraph-captured.  The batches cycle
-    over ``distinct`` staged synthetic batches (each replay draws fresh z and
-    Gumbel noise); the first pass captures, the second is timed.  Also the f16
-    scatter kernel (vg_hgat_fwd) over the sweep's own stacked graph and channel
-    schedule, graph-replayed between HIP events."""
+def start_sweep_store(graphs: int = 10000, seed: int = 2024):
+    """Write the inference sweep's store of ``graphs`` distinct synthetic
+    buildings in a child process (no GPU in it), while the GPU legs run.
+    Returns (process, path)."""
+    import multiprocessing as mp
+    import tempfile
+
+    from vgan.synth import write_synthetic_store
+
+    path = os.path.join(tempfile.mkdtemp(prefix="vgan_sweep_"), "store")
+    proc = mp.get_context("spawn").Process(target=write_synthetic_store, args=(path, graphs, seed), daemon=True)
+    proc.start()
+    return proc, path
+
+
+def sweep_leg(device, store_job, batch: int = 32, n_taus: int = 10):
+    """BASELINE.json configs[4]: generator-only inference sweep over a STREAM
+    of distinct buildings (the store written by ``start_sweep_store``: 10,000
+    synthetic buildings, 313 batches of 32), a geometric Gumbel temperature
+    schedule 1.0 -> 0.1, f16 (and f32) eval forward, one stacked forward per
+    batch over the ``n_taus`` temperature copies.  Each batch comes through
+    the native loader (host collate + host-built per-batch structures + one
+    upload, prefetched on a thread); its forward is recorded as a hipGraph
+    and an executable graph is updated in place (InferenceSweep.run_fresh).
+    The timed region is the whole pass: collate, upload, record, update,
+    replay.  Also the f16 scatter kernel (vg_hgat_fwd) over the sweep's own
+    stacked graph and channel schedule, graph-replayed between HIP events."""
     from vgan import data as vdata
     from vgan._lib import LIB, check, ptr, stream_handle
     from vgan.config import Configuration
     from vgan.half import _r8
     from vgan.infer import InferenceSweep, geometric_taus
+    from vgan.loader import GraphLoader
     from vgan.models import VoxelGNNGenerator
-    from vgan.synth import SyntheticDataset
+    from vgan.store import GraphStore
 
+    proc, path = store_job
+    t0 = time.perf_counter()
+    proc.join()
+    if proc.exitcode != 0:
+        raise RuntimeError(f"sweep store writer exited with {proc.exitcode}")
+    log(f"sweep store ready ({time.perf_counter() - t0:.1f} s wait)")
+    store = GraphStore(path)
     cfg = Configuration()
     cfg.DEVICE = str(device)
     cfg.runtime["rng"] = "device"
     torch.manual_seed(cfg.SEED)
     G = VoxelGNNGenerator(cfg, 17, 12)
-    ds = SyntheticDataset(6500, seed=777)
-    staged = []
-    for b in range(distinct):
-        loc, vox = ds.batch(list(range(3200 + b * batch, 3200 + (b + 1) * batch)))
-        staged.append((loc.to(device), vox.to(device)))
-    n_batches = -(-graphs // batch)
-    plan = [staged[i % distinct] for i in range(n_batches)]
     taus = geometric_taus(1.0, 0.1, n_taus)
-    out = {"workload": f"configs[4]: {n_batches * batch} generator samples (batches of {batch} cycling over "
-                       f"{distinct} staged synthetic batches), {n_taus} Gumbel temperatures 1.0->0.1 geometric, "
-                       f"eval G forward stacked over the temperatures, hipGraph replay",
-           "unit": "samples/s (buildings x temperatures)"}
+
+    def loader(indices=None):
+        return GraphLoader(store, indices, batch_size=batch, shuffle=False, device=device, prefetch=4,
+                           prepare=(cfg.NUM_CLASSES, ()))
+
+    n_batches = -(-len(store) // batch)
+    out = {"workload": f"configs[4]: {len(store)} distinct synthetic buildings ({n_batches} batches of {batch}) "
+                       f"streamed through the native loader, {n_taus} Gumbel temperatures 1.0->0.1 geometric, eval G "
+                       f"forward stacked over the temperatures; per batch its forward recorded as a hipGraph and "
+                       f"an executable graph updated in place; collate, upload, record, update and replay timed",
+           "unit": "samples/s (buildings x temperatures)", "distinct_batches": n_batches,
+           "distinct_buildings": len(store)}
     for dt in ("f16", "f32"):
-        sw = InferenceSweep(G, taus, graphed=True, dtype=dt)
-        sw.run(staged)  # capture every staged batch's graph
+        sw = InferenceSweep(G, taus, dtype=dt)
+        sw.run_stream(loader(list(range(4 * batch))))  # warm-up: lazy initialisation, first instantiations
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        res = sw.run(plan)
+        res = sw.run_stream(loader())
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         out[dt] = {"value": round(res["samples"] / el, 1), "seconds": round(el, 4), "samples": res["samples"],
-                   "ms_per_batch": round(el / n_batches * 1e3, 4)}
-        log(f"sweep {dt}: {out[dt]['value']:.0f} samples/s ({el:.3f} s for {res['samples']} samples)")
+                   "batches": res["batches"], "ms_per_batch": round(el / res["batches"] * 1e3, 4)}
+        log(f"sweep {dt}: {out[dt]['value']:.0f} samples/s ({el:.3f} s for {res['samples']} samples, "
+            f"{res['batches']} distinct batches)")
+        del sw
+    loc, vox = next(iter(loader(list(range(batch)))))
     # the f16 scatter kernel on the sweep's stacked CSR (n_taus copies)
-    loc, vox = staged[0]
     csr = vdata.prepared(loc, vox, cfg.NUM_CLASSES).csr.stacked(n_taus)
     rows, e = csr.num_nodes, csr.num_edges
     widths = G.encoder.widths[1:]
@@ -627,6 +674,10 @@ def main():
 
     rank, world, local = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(
         os.environ.get("LOCAL_RANK", 0))
+    # configs[4]'s 10,000 distinct buildings are generated in a child process
+    # (before this process touches the GPU) while the other legs run
+    store_job = start_sweep_store() if (rank == 0 and not args.no_sweep and not args.profile
+                                        and not args.roofline_only) else None
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     if not torch.cuda.is_available():
@@ -726,16 +777,14 @@ def main():
 
     result = None
     if rank == 0:
-        stress_orders = {} if args.no_stress else {o: stress_roofline(device, order=o) for o in ("rowmajor", "tiled")}
+        stress_orders = {} if args.no_stress else {o: stress_roofline(device, order=o)
+                                                   for o in ("rowmajor", "tiled", "blocked")}
         for o, st_ in stress_orders.items():
-            for c, r in st_["per_channels"].items():
-                log(f"stress ({o}) C={c}: {r['avg_us']:.1f} us, {r['achieved_gbs']:.0f} GB/s, "
-                    f"{r['gather_gbs']:.0f} GB/s L2 gather")
-            for c, r in st_["per_channels_lds"].items():
-                log(f"stress ({o}) C={c} (LDS-staged): {r['avg_us']:.1f} us, {r['achieved_gbs']:.0f} GB/s")
-        # the headline stress figure: the faster numbering at C = 128
-        stress = min(stress_orders.values(), key=lambda r: r["per_channels"][128]["avg_us"]) if stress_orders else None
-        sweep = None if args.no_sweep else sweep_leg(device)
+            for kind, key in (("register", "per_channels"), ("LDS 16-row", "per_channels_lds"),
+                              ("staged", "per_channels_staged")):
+                for c, r in st_[key].items():
+                    log(f"stress ({o}) C={c} ({kind}): {r['avg_us']:.1f} us, {r['achieved_gbs']:.0f} GB/s")
+        sweep = None if store_job is None else sweep_leg(device, store_job)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args.batch, args.cpu_seconds)
@@ -812,34 +861,44 @@ def main():
             result["bf16"] = bf16
         if sweep:
             result["inference_sweep"] = sweep
-        if stress:
-            # configs[3]: the faster of the two large-graph aggregations -- the
-            # register gather (k_gat_fwd_cp) or the LDS-staged tile plan
-            # (k_gat_fwd_lds); both are reported, DESIGN.md 4.10 explains the pick
-            reg, lds = stress["per_channels"][128], stress["per_channels_lds"].get(128)
-            use_lds = lds is not None and lds["avg_us"] < reg["avg_us"]
-            c128 = lds if use_lds else reg
-            kname = ("vg_gat_aggregate_fwd_lds (tile plan: each 16-row tile's distinct source rows staged "
-                     "through LDS)" if use_lds else
-                     "vg_gat_aggregate_fwd (register gather: 16-lane rows, 4 source rows in flight per lane group)")
+        if stress_orders:
+            # configs[3]: the fastest (numbering, kernel) at C = 128 -- the
+            # register gather (k_gat_fwd_cp), the 16-row LDS tiles (k_gat_fwd_lds)
+            # or the persistent staged kernel (k_gat_fwd_staged); all are
+            # reported, DESIGN.md 4.10 / 4.20 explain the pick
+            kinds = {"per_channels": "vg_gat_aggregate_fwd (register gather: 16-lane rows, 4 source rows in flight "
+                                     "per lane group)",
+                     "per_channels_lds": "vg_gat_aggregate_fwd_lds (each 16-row tile's distinct source rows staged "
+                                         "through LDS)",
+                     "per_channels_staged": "vg_gat_aggregate_fwd_staged (persistent 1024-thread workgroup per CU; "
+                                            "each 64-row tile's distinct source rows staged through LDS while the "
+                                            "previous tile is aggregated)"}
+            cands = [(r[key][128]["avg_us"], o, key) for o, r in stress_orders.items() for key in kinds
+                     if 128 in r.get(key, {})]
+            _, o_best, k_best = min(cands)
+            best = stress_orders[o_best]
+            c128 = best[k_best][128]
+            names = {"rowmajor": "row-major (the reference's numbering)",
+                     "tiled": "4 x 4 (y, x) tiles per floor, vgan.locality.tile_order",
+                     "blocked": "4 x 4 x 4 lattice blocks, vgan.locality.block_order"}
+            gb = agg_gather_bytes(best["nodes"], best["edges"], 128)
             result["roofline_stress"] = {
-                "workload": f"configs[3]: 8 x 50k-node buildings, N={stress['nodes']}, E'={stress['edges']}, "
-                            f"C=128 fp32, cold MALL, voxels numbered {stress['order']}"
-                            + (" (4 x 4 (y, x) tiles per floor, vgan.locality)" if stress["order"] == "tiled" else ""),
-                "kernel": kname,
-                "tile_plan": f"{stress['distinct_sources_per_tile']} distinct source rows for "
-                             f"{stress['edges_per_tile']} edges per 16-row tile",
+                "workload": f"configs[3]: 8 x 50k-node buildings, N={best['nodes']}, E'={best['edges']}, "
+                            f"C=128 fp32, cold MALL, voxels numbered {names[o_best]}",
+                "kernel": kinds[k_best],
+                "tile_plan": (f"{best['staged_plan']['distinct_sources_per_64_row_tile']} distinct source rows for "
+                              f"{best['staged_plan']['edges_per_64_row_tile']} edges per 64-row tile"
+                              if k_best == "per_channels_staged" else
+                              f"{best['distinct_sources_per_tile']} distinct source rows for "
+                              f"{best['edges_per_tile']} edges per 16-row tile"),
                 "bound": "hbm", "achieved": round(c128["achieved_gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(c128["achieved_gbs"] / HBM_PEAK_GBS, 4), "avg_launch_us": round(c128["avg_us"], 2),
-                "l2_gather": ({"achieved": round(c128["gather_gbs"], 1), "unit": "GB/s",
-                               "frac_of_l2_peak": round(c128["gather_gbs"] / L2_PEAK_GBS, 4),
-                               "frac_of_measured_gather_ceiling": round(c128["gather_gbs"] / L2_GATHER_GBS, 4)}
-                              if "gather_gbs" in c128 else None),
-                "by_order": {o: {"distinct_sources_per_tile": r["distinct_sources_per_tile"],
-                                 "per_channels_register_gather": {str(c): {k: round(v, 2) for k, v in x.items()}
-                                                                  for c, x in r["per_channels"].items()},
-                                 "per_channels_lds": {str(c): {k: round(v, 2) for k, v in x.items()}
-                                                      for c, x in r["per_channels_lds"].items()}}
+                "algorithmic_bytes": int(c128["bytes"]),
+                "edge_gather_bytes": int(gb),
+                "by_order": {o: {"distinct_sources_per_16_row_tile": r["distinct_sources_per_tile"],
+                                 "staged_plan": r["staged_plan"],
+                                 **{key: {str(c): {k: round(v, 2) for k, v in x.items()} for c, x in r[key].items()}
+                                    for key in kinds}}
                              for o, r in stress_orders.items()},
             }
     if world > 1:

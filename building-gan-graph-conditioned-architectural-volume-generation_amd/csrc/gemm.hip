@@ -77,6 +77,22 @@ __device__ __forceinline__ float act_fn(float v, float aux) {
   else return v;
 }
 
+// Fragment-ordered operand images for the 16 x 16 x 4 f32 MFMA (k_gemm_ln16).
+// The MFMA lane (row r = lane % 16, k-group g = lane / 16) consumes k = g, g + 4,
+// ..., g + 28 of a 32-wide K-tile, one per MFMA.  Row r of the image keeps its
+// 32 values as slot 8 (k % 4) + k / 4 -- a lane's 8 values contiguous --
+// XOR-swizzled in 4-float units by r % 8 with a 48-float pitch, so the lane
+// reads them as two ds_read_b128, conflict-free across the instruction's lane
+// groups (MI355X_MICROARCH.md LDS table), instead of eight ds_read_b32: half
+// the LDS cycles per MFMA.  The MFMAs see the same operands in the same order
+// (bit-identical results).
+#ifndef VG_FRAG128
+#define VG_FRAG128 1  // 0: the row-major images with 33-float pitch (A/B knob)
+#endif
+constexpr int FP = 48;
+__device__ __forceinline__ int frag_pos(int r, int k) { return r * FP + ((8 * (k & 3) + (k >> 2)) ^ (4 * (r & 7))); }
+__device__ __forceinline__ int frag_at(int r, int g, int h) { return r * FP + ((8 * g + 4 * h) ^ (4 * (r & 7))); }
+
 // Logical (row tile, column tile) of this workgroup, XCD-aware: the hardware
 // deals workgroups round-robin over the 8 XCDs in dispatch order (x fastest),
 // so linear id b runs on XCD b % 8; every XCD gets one contiguous range of
@@ -440,7 +456,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // QA: A and B loaded as float4 quads by threads 0..511 (one quad per K-tile;
 // K % 4 == 0, leading dimensions % 4 == 0, 16-B aligned operands, quad_ab)
 // instead of 2 scalars each by every thread; GNA loads A as quads.
-template <bool BT, int ACT, bool ATT = false, bool BF = false, bool GNP = false, bool GNA = false, bool QA = false>
+template <bool BT, int ACT, bool ATT = false, bool BF = false, bool GNP = false, bool GNA = false, bool QA = false,
+          int NW = 16>
 __device__ __forceinline__ void gemm16_body(const float* __restrict__ A, int lda,
                                                  const float* __restrict__ B, int ldb,
                                                  const float* __restrict__ bias,
@@ -455,40 +472,56 @@ __device__ __forceinline__ void gemm16_body(const float* __restrict__ A, int lda
   __shared__ __attribute__((aligned(16))) float smem[2 * TM * LDQ + 2 * TN * LDQ];
   float(*As)[TM][LDQ] = reinterpret_cast<float(*)[TM][LDQ]>(smem);
   float(*Bs)[TN][LDQ] = reinterpret_cast<float(*)[TN][LDQ]>(smem + 2 * TM * LDQ);  // Bs[j][k] = op(B)[k][j]
-  constexpr int PER = (TM * TK) / 1024;
+  // NW = 16: 4 x 4 waves, one 16 x 16 sub-tile each; NW = 8: 4 x 2 waves,
+  // two side-by-side 16 x 16 sub-tiles each (NS), the A fragment shared
+  static_assert(NW == 16 || NW == 8, "16 or 8 waves");
+  constexpr int NT = 64 * NW, NS = 16 / NW;
+  constexpr int PER = (TM * TK) / NT;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int wr = wave >> 2, wc = wave & 3;  // 4 x 4 sub-tiles of 16 x 16
+  const int wr = NW == 16 ? wave >> 2 : wave >> 1;
+  const int wc0 = NW == 16 ? wave & 3 : (wave & 1) * 2;  // the first sub-tile column
   int tx, ty;
   tile_xy(tx, ty);
   const int n0 = tx * TM, m0 = ty * TN;
-  const int mc = m0 + wc * 16 + (lane & 15);  // this lane's output column
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  int mcs[NS];  // this lane's output column per sub-tile
+#pragma unroll
+  for (int s_ = 0; s_ < NS; ++s_) mcs[s_] = m0 + (wc0 + s_) * 16 + (lane & 15);
+  f32x4 accs[NS];
+#pragma unroll
+  for (int s_ = 0; s_ < NS; ++s_) accs[s_] = f32x4{0.f, 0.f, 0.f, 0.f};
   // GNP: the epilogue's GraphNorm operands (the lane's 4 rows of x / keep, the
   // two segments' statistics, the column's parameters) loaded before the K loop
-  float gx_[GNP ? 4 : 1], gk_[GNP ? 4 : 1];
-  float gmu[2] = {0.f, 0.f}, gsd[2] = {1.f, 1.f}, gw_ = 0.f, gb_ = 0.f, gms_ = 0.f;
+  float gx_[NS][GNP ? 4 : 1], gk_[NS][GNP ? 4 : 1];
+  float gmu[NS][2], gsd[NS][2], gw_[NS], gb_[NS], gms_[NS];
   int gbound = 0;
   if constexpr (GNP) {
     const int seg0 = n0 / gn.seg_rows;
     gbound = (seg0 + 1) * gn.seg_rows;
-    if (mc < M) {
-      gw_ = gn.w[mc];
-      gb_ = gn.b[mc];
-      gms_ = gn.ms[mc];
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
-        if (q == 0 || gbound < N) {
-          const float* st = gn.stats + (size_t)(seg0 + q) * 2 * M;
-          gmu[q] = st[mc];
-          gsd[q] = st[M + mc] + gn.eps;
-        }
-    }
+    for (int s_ = 0; s_ < NS; ++s_) {
+      const int mc = mcs[s_];
+      gmu[s_][0] = gmu[s_][1] = 0.f;
+      gsd[s_][0] = gsd[s_][1] = 1.f;
+      gw_[s_] = gb_[s_] = gms_[s_] = 0.f;
+      if (mc < M) {
+        gw_[s_] = gn.w[mc];
+        gb_[s_] = gn.b[mc];
+        gms_[s_] = gn.ms[mc];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = n0 + wr * 16 + 4 * (lane >> 4) + r;
-      const bool ok = n < N && mc < M;
-      gx_[r] = ok ? gn.x[(size_t)n * M + mc] : 0.f;
-      gk_[r] = ok && gn.keep ? gn.keep[(size_t)n * M + mc] : 1.f;
+        for (int q = 0; q < 2; ++q)
+          if (q == 0 || gbound < N) {
+            const float* st = gn.stats + (size_t)(seg0 + q) * 2 * M;
+            gmu[s_][q] = st[mc];
+            gsd[s_][q] = st[M + mc] + gn.eps;
+          }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wr * 16 + 4 * (lane >> 4) + r;
+        const bool ok = n < N && mc < M;
+        gx_[s_][r] = ok ? gn.x[(size_t)n * M + mc] : 0.f;
+        gk_[s_][r] = ok && gn.keep ? gn.keep[(size_t)n * M + mc] : 1.f;
+      }
     }
   }
   float ra[PER], rb[PER];
@@ -499,7 +532,7 @@ __device__ __forceinline__ void gemm16_body(const float* __restrict__ A, int lda
     const int seg0 = n0 / ga.seg_rows;
     gbnd = (seg0 + 1) * ga.seg_rows;
     const bool two = gbnd < N;
-    for (int k = t; k < K; k += 1024) {
+    for (int k = t; k < K; k += NT) {
       gpar[k] = ga.w[k];
       gpar[K + k] = ga.b[k];
       gpar[2 * K + k] = ga.ms[k];
@@ -538,7 +571,7 @@ __device__ __forceinline__ void gemm16_body(const float* __restrict__ A, int lda
     }
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
-      const int e = t + 1024 * q;
+      const int e = t + NT * q;
       const int row = e / TK, kc = e % TK;
       const int n = n0 + row, k = k0 + kc;
       if constexpr (!QUAD) ra[q] = (n < N && k < K) ? A[(size_t)n * lda + k] : 0.f;
@@ -589,7 +622,7 @@ __device__ __forceinline__ void gemm16_body(const float* __restrict__ A, int lda
     }
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
-      const int e = t + 1024 * q;
+      const int e = t + NT * q;
       if constexpr (!QUAD) As[buf][e / TK][e % TK] = ra[q];
       if constexpr (!QA) {
         if (BT) Bs[buf][e / TK][e % TK] = rb[q];
@@ -600,88 +633,117 @@ __device__ __forceinline__ void gemm16_body(const float* __restrict__ A, int lda
     if (k0 + TK < K) load(k0 + TK);
     if constexpr (BF) {
       const float4* ap = reinterpret_cast<const float4*>(&As[buf][wr * 16 + (lane & 15)][8 * (lane >> 4)]);
-      const float4* bp = reinterpret_cast<const float4*>(&Bs[buf][wc * 16 + (lane & 15)][8 * (lane >> 4)]);
-      const float4 a0 = ap[0], a1 = ap[1], b0 = bp[0], b1 = bp[1];
-      bf16x8 ha, hb;
+      const float4 a0 = ap[0], a1 = ap[1];
+      bf16x8 ha;
       ha[0] = static_cast<__bf16>(a0.x); ha[1] = static_cast<__bf16>(a0.y);
       ha[2] = static_cast<__bf16>(a0.z); ha[3] = static_cast<__bf16>(a0.w);
       ha[4] = static_cast<__bf16>(a1.x); ha[5] = static_cast<__bf16>(a1.y);
       ha[6] = static_cast<__bf16>(a1.z); ha[7] = static_cast<__bf16>(a1.w);
-      hb[0] = static_cast<__bf16>(b0.x); hb[1] = static_cast<__bf16>(b0.y);
-      hb[2] = static_cast<__bf16>(b0.z); hb[3] = static_cast<__bf16>(b0.w);
-      hb[4] = static_cast<__bf16>(b1.x); hb[5] = static_cast<__bf16>(b1.y);
-      hb[6] = static_cast<__bf16>(b1.z); hb[7] = static_cast<__bf16>(b1.w);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ha, hb, acc, 0, 0, 0);
+#pragma unroll
+      for (int s_ = 0; s_ < NS; ++s_) {
+        const float4* bp = reinterpret_cast<const float4*>(&Bs[buf][(wc0 + s_) * 16 + (lane & 15)][8 * (lane >> 4)]);
+        const float4 b0 = bp[0], b1 = bp[1];
+        bf16x8 hb;
+        hb[0] = static_cast<__bf16>(b0.x); hb[1] = static_cast<__bf16>(b0.y);
+        hb[2] = static_cast<__bf16>(b0.z); hb[3] = static_cast<__bf16>(b0.w);
+        hb[4] = static_cast<__bf16>(b1.x); hb[5] = static_cast<__bf16>(b1.y);
+        hb[6] = static_cast<__bf16>(b1.z); hb[7] = static_cast<__bf16>(b1.w);
+        accs[s_] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ha, hb, accs[s_], 0, 0, 0);
+      }
     } else {
       const float* ar = &As[buf][wr * 16 + (lane & 15)][lane >> 4];
-      const float* br = &Bs[buf][wc * 16 + (lane & 15)][lane >> 4];
 #pragma unroll
-      for (int kk = 0; kk < TK; kk += 4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ar[kk], br[kk], acc, 0, 0, 0);
+      for (int kk = 0; kk < TK; kk += 4) {
+        const float av = ar[kk];
+#pragma unroll
+        for (int s_ = 0; s_ < NS; ++s_)
+          accs[s_] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, Bs[buf][(wc0 + s_) * 16 + (lane & 15)][(lane >> 4) + kk],
+                                                          accs[s_], 0, 0, 0);
+      }
     }
     buf ^= 1;
   }
-  const float bv = (bias && mc < M) ? bias[mc] : 0.f;
+  float bvs[NS];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int n = n0 + wr * 16 + 4 * (lane >> 4) + r;
-    if (n < N && mc < M) {
-      const float av = ACT == 3 ? aux[(size_t)n * ldaux + mc] : 0.f;
-      C[(size_t)n * ldc + mc] = act_fn<ACT>(acc[r] + bv, av);
+  for (int s_ = 0; s_ < NS; ++s_) {
+    const int mc = mcs[s_];
+    const f32x4 acc = accs[s_];
+    const float bv = (bias && mc < M) ? bias[mc] : 0.f;
+    bvs[s_] = bv;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + wr * 16 + 4 * (lane >> 4) + r;
+      if (n < N && mc < M) {
+        const float av = ACT == 3 ? aux[(size_t)n * ldaux + mc] : 0.f;
+        C[(size_t)n * ldc + mc] = act_fn<ACT>(acc[r] + bv, av);
+      }
     }
   }
   if constexpr (GNP) {
     // column partials of gz = g_y [z > 0] keep and gz * xhat per segment slot:
     // the lane's 4 rows in order, the 4 lanes of the column (xor 16, 32),
     // then the 4 row waves of the column through LDS in order: deterministic
-    float pa[2] = {0.f, 0.f}, pb[2] = {0.f, 0.f};
-    if (mc < M) {
+    float pa[NS][2], pb[NS][2];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = n0 + wr * 16 + 4 * (lane >> 4) + r;
-        if (n < N) {
-          const int sl = n >= gbound;
-          const float xh = (gx_[r] - (sl ? gmu[1] : gmu[0]) * gms_) / (sl ? gsd[1] : gsd[0]);
-          const float gz = xh * gw_ + gb_ > 0.f ? acc[r] * gk_[r] : 0.f;
-          if (sl) {
-            pa[1] += gz;
-            pb[1] = fmaf(gz, xh, pb[1]);
-          } else {
-            pa[0] += gz;
-            pb[0] = fmaf(gz, xh, pb[0]);
+    for (int s_ = 0; s_ < NS; ++s_) {
+      const int mc = mcs[s_];
+      const f32x4 acc = accs[s_];
+      pa[s_][0] = pa[s_][1] = pb[s_][0] = pb[s_][1] = 0.f;
+      if (mc < M) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = n0 + wr * 16 + 4 * (lane >> 4) + r;
+          if (n < N) {
+            const int sl = n >= gbound;
+            const float xh = (gx_[s_][r] - (sl ? gmu[s_][1] : gmu[s_][0]) * gms_[s_]) / (sl ? gsd[s_][1] : gsd[s_][0]);
+            const float gz = xh * gw_[s_] + gb_[s_] > 0.f ? acc[r] * gk_[s_][r] : 0.f;
+            if (sl) {
+              pa[s_][1] += gz;
+              pb[s_][1] = fmaf(gz, xh, pb[s_][1]);
+            } else {
+              pa[s_][0] += gz;
+              pb[s_][0] = fmaf(gz, xh, pb[s_][0]);
+            }
           }
         }
       }
-    }
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      pa[q] += __shfl_xor(pa[q], 16, 64);
-      pb[q] += __shfl_xor(pb[q], 16, 64);
-      pa[q] += __shfl_xor(pa[q], 32, 64);
-      pb[q] += __shfl_xor(pb[q], 32, 64);
+      for (int q = 0; q < 2; ++q) {
+        pa[s_][q] += __shfl_xor(pa[s_][q], 16, 64);
+        pb[s_][q] += __shfl_xor(pb[s_][q], 16, 64);
+        pa[s_][q] += __shfl_xor(pa[s_][q], 32, 64);
+        pb[s_][q] += __shfl_xor(pb[s_][q], 32, 64);
+      }
     }
     __syncthreads();  // every wave is done with the last K-tile's LDS images
     float* red = smem;  // [wr][64 columns][4]
-    if (lane < 16) {
-      float* rp = red + ((wr * 64) + wc * 16 + lane) * 4;
-      rp[0] = pa[0];
-      rp[1] = pb[0];
-      rp[2] = pa[1];
-      rp[3] = pb[1];
-    }
-    __syncthreads();
-    if (wr == 0 && lane < 16 && mc < M) {
-      float s[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int w = 0; w < 4; ++w) {
-        const float* rp = red + ((w * 64) + wc * 16 + lane) * 4;
+    if (lane < 16)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) s[q] += rp[q];
+      for (int s_ = 0; s_ < NS; ++s_) {
+        float* rp = red + ((wr * 64) + (wc0 + s_) * 16 + lane) * 4;
+        rp[0] = pa[s_][0];
+        rp[1] = pb[s_][0];
+        rp[2] = pa[s_][1];
+        rp[3] = pb[s_][1];
       }
-      float* tp = gn.tpart + (size_t)tx * 2 * M * 2;
-      tp[(size_t)mc * 2] = s[0];
-      tp[(size_t)mc * 2 + 1] = s[1];
-      tp[(size_t)(M + mc) * 2] = s[2];
-      tp[(size_t)(M + mc) * 2 + 1] = s[3];
-    }
+    __syncthreads();
+    if (wr == 0 && lane < 16)
+#pragma unroll
+      for (int s_ = 0; s_ < NS; ++s_) {
+        const int mc = mcs[s_];
+        if (mc >= M) continue;
+        float sm[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int w = 0; w < 4; ++w) {
+          const float* rp = red + ((w * 64) + (wc0 + s_) * 16 + lane) * 4;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) sm[q] += rp[q];
+        }
+        float* tp = gn.tpart + (size_t)tx * 2 * M * 2;
+        tp[(size_t)mc * 2] = sm[0];
+        tp[(size_t)mc * 2 + 1] = sm[1];
+        tp[(size_t)(M + mc) * 2] = sm[2];
+        tp[(size_t)(M + mc) * 2 + 1] = sm[3];
+      }
   }
   if constexpr (ATT) {
     // the 64 x 64 tile staged in LDS, then 16 threads per row dot 4 columns
@@ -689,27 +751,33 @@ __device__ __forceinline__ void gemm16_body(const float* __restrict__ A, int lda
     float(*Ct)[TN + 1] = reinterpret_cast<float(*)[TN + 1]>(smem);
     __syncthreads();  // every wave is done with the last K-tile's images
 #pragma unroll
-    for (int r = 0; r < 4; ++r) Ct[wr * 16 + 4 * (lane >> 4) + r][wc * 16 + (lane & 15)] = acc[r] + bv;
+    for (int s_ = 0; s_ < NS; ++s_)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Ct[wr * 16 + 4 * (lane >> 4) + r][(wc0 + s_) * 16 + (lane & 15)] = accs[s_][r] + bvs[s_];
     __syncthreads();
-    const int row = t >> 4, q = t & 15;
-    float ss = 0.f, sd = 0.f;
+    const int q = t & 15;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = q * 4 + j;
-      if (c < M) {
-        const float v = Ct[row][c];
-        ss = fmaf(v, att_s[c], ss);
-        sd = fmaf(v, att_d[c], sd);
+    for (int row = t >> 4; row < TM; row += NT / 16) {
+      float ss = 0.f, sd = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = q * 4 + j;
+        if (c < M) {
+          const float v = Ct[row][c];
+          ss = fmaf(v, att_s[c], ss);
+          sd = fmaf(v, att_d[c], sd);
+        }
       }
-    }
 #pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-      ss += __shfl_xor(ss, o, 64);
-      sd += __shfl_xor(sd, o, 64);
-    }
-    if (q == 0 && n0 + row < N) {
-      a_src[n0 + row] = ss;
-      a_dst[n0 + row] = sd;
+      for (int o = 1; o < 16; o <<= 1) {
+        ss += __shfl_xor(ss, o, 64);
+        sd += __shfl_xor(sd, o, 64);
+      }
+      if (q == 0 && n0 + row < N) {
+        a_src[n0 + row] = ss;
+        a_dst[n0 + row] = sd;
+      }
     }
   }
 }
@@ -725,6 +793,24 @@ __global__ void __launch_bounds__(1024) k_gemm16(const float* __restrict__ A, in
                                                  float* __restrict__ a_dst = nullptr, const GnpDesc gn = GnpDesc{}) {
   gemm16_body<BT, ACT, ATT, BF, GNP, false, QA>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, N, M, K, att_s, att_d,
                                                 a_src, a_dst, gn);
+}
+
+// 8-wave form (4 x 2 waves, two 16 x 16 sub-tiles each): four workgroups fit a
+// CU where two 16-wave ones do, so a product of more than 512 row tiles (the
+// critic's 38k stacked rows: 596) runs in one workgroup round instead of two
+// (a second round costs a whole workgroup latency, ~1.7 us: DESIGN.md 9.5).
+// Bit-identical to k_gemm16: the same sub-tiles, MFMA order and epilogues.
+template <bool BT, int ACT, bool ATT = false, bool BF = false, bool GNP = false, bool QA = false>
+__global__ void __launch_bounds__(512) k_gemm8w(const float* __restrict__ A, int lda, const float* __restrict__ B,
+                                                int ldb, const float* __restrict__ bias,
+                                                const float* __restrict__ aux, int ldaux, float* __restrict__ C,
+                                                int ldc, int N, int M, int K,
+                                                const float* __restrict__ att_s = nullptr,
+                                                const float* __restrict__ att_d = nullptr,
+                                                float* __restrict__ a_src = nullptr,
+                                                float* __restrict__ a_dst = nullptr, const GnpDesc gn = GnpDesc{}) {
+  gemm16_body<BT, ACT, ATT, BF, GNP, false, QA, 8>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, N, M, K, att_s, att_d,
+                                                   a_src, a_dst, gn);
 }
 
 // the projection GEMM with the GraphNorm applied to its operand (vg_gat_lin_att_gn):
@@ -1056,10 +1142,13 @@ __global__ void __launch_bounds__(1024) k_gemm_ln16(const float* __restrict__ A,
   constexpr int WRW = TMR / 16, WCW = 16 / WRW;  // row / column waves
   constexpr int NJ = TNC / (16 * WCW);           // 16-column sub-tiles per wave
   static_assert(NJ >= 1 && WRW * WCW == 16, "tile shape");
-  __shared__ __attribute__((aligned(16))) float smem[2 * TMR * LDP + 2 * TNC * LDP];
+  constexpr bool FR = VG_FRAG128;
+  constexpr int PIT = FR ? FP : LDP;  // image row pitch
+  __shared__ __attribute__((aligned(16))) float smem[2 * TMR * PIT + 2 * TNC * PIT];
   __shared__ float s_mu[TMR], s_rs[TMR];
-  float(*As)[TMR][LDP] = reinterpret_cast<float(*)[TMR][LDP]>(smem);
-  float(*Bs)[TNC][LDP] = reinterpret_cast<float(*)[TNC][LDP]>(smem + 2 * TMR * LDP);
+  float* As = smem;                   // [2][TMR * PIT]
+  float* Bs = smem + 2 * TMR * PIT;   // [2][TNC * PIT]
+  auto at = [&](int r, int kc) { return FR ? frag_pos(r, kc) : r * LDP + kc; };
   constexpr int PA = (TMR * TK) / 1024, PB = (TNC * TK) / 1024;
   static_assert(PA >= 1 && PB >= 1, "tile shape");
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -1128,40 +1217,61 @@ __global__ void __launch_bounds__(1024) k_gemm_ln16(const float* __restrict__ A,
     if constexpr (QL) {
       const int kq = 4 * (t % QPR);
       if (t < NQA) {
-        float* d = &As[buf][t / QPR][kq];
-        d[0] = qa.x;
-        d[1] = qa.y;
-        d[2] = qa.z;
-        d[3] = qa.w;
+        float* d = As + buf * TMR * PIT;
+        const int r = t / QPR;
+        d[at(r, kq)] = qa.x;
+        d[at(r, kq + 1)] = qa.y;
+        d[at(r, kq + 2)] = qa.z;
+        d[at(r, kq + 3)] = qa.w;
       }
       if (t < NQB) {
-        float* d = &Bs[buf][t / QPR][kq];
-        d[0] = qb.x;
-        d[1] = qb.y;
-        d[2] = qb.z;
-        d[3] = qb.w;
+        float* d = Bs + buf * TNC * PIT;
+        const int r = t / QPR;
+        d[at(r, kq)] = qb.x;
+        d[at(r, kq + 1)] = qb.y;
+        d[at(r, kq + 2)] = qb.z;
+        d[at(r, kq + 3)] = qb.w;
       }
     } else {
 #pragma unroll
       for (int q = 0; q < PA; ++q) {
         const int e = t + 1024 * q;
-        As[buf][e / TK][e % TK] = ra[q];
+        As[buf * TMR * PIT + at(e / TK, e % TK)] = ra[q];
       }
 #pragma unroll
       for (int q = 0; q < PB; ++q) {
         const int e = t + 1024 * q;
-        Bs[buf][e / TK][e % TK] = rb[q];
+        Bs[buf * TNC * PIT + at(e / TK, e % TK)] = rb[q];
       }
     }
     __syncthreads();
     if (k0 + TK < K) load(k0 + TK);
-    const float* ar = &As[buf][wr * 16 + (lane & 15)][lane >> 4];
+    if constexpr (FR) {
+      const float* Ai = As + buf * TMR * PIT;
+      const float* Bi = Bs + buf * TNC * PIT;
+      const int ra_ = wr * 16 + (lane & 15), g = lane >> 4;
+      const float4 a0 = *reinterpret_cast<const float4*>(Ai + frag_at(ra_, g, 0));
+      const float4 a1 = *reinterpret_cast<const float4*>(Ai + frag_at(ra_, g, 1));
+      const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
 #pragma unroll
-    for (int kk = 0; kk < TK; kk += 4)
+      for (int j = 0; j < NJ; ++j) {
+        const int rb_ = j * 16 * WCW + wc * 16 + (lane & 15);
+        const float4 b0 = *reinterpret_cast<const float4*>(Bi + frag_at(rb_, g, 0));
+        const float4 b1 = *reinterpret_cast<const float4*>(Bi + frag_at(rb_, g, 1));
+        const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-      for (int j = 0; j < NJ; ++j)
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-            ar[kk], Bs[buf][j * 16 * WCW + wc * 16 + (lane & 15)][(lane >> 4) + kk], acc[j], 0, 0, 0);
+        for (int i = 0; i < 8; ++i) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[i], acc[j], 0, 0, 0);
+      }
+    } else {
+      const float* ar = As + buf * TMR * PIT + (wr * 16 + (lane & 15)) * LDP + (lane >> 4);
+#pragma unroll
+      for (int kk = 0; kk < TK; kk += 4)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+              ar[kk], Bs[buf * TNC * PIT + (j * 16 * WCW + wc * 16 + (lane & 15)) * LDP + (lane >> 4) + kk], acc[j], 0,
+              0, 0);
+    }
     buf ^= 1;
   }
   // stage the full-width tile (+ bias, + addend) in LDS
@@ -1676,6 +1786,15 @@ static inline bool quad_ab(const float* A, int lda, const float* B, int ldb, int
          ldb % 4 == 0 && (reinterpret_cast<uintptr_t>(B) & 15) == 0 && (bt || M % 4 == 0);
 }
 
+// 8-wave k_gemm16 workgroups (k_gemm8w) when the product has more row tiles
+// than two 16-wave workgroups per CU hold: one workgroup round instead of two
+#ifndef VG_GEMM8_MIN_TILES
+#define VG_GEMM8_MIN_TILES 513  // 0: never (A/B knob)
+#endif
+static inline bool use_8w(const dim3& grid) {
+  return VG_GEMM8_MIN_TILES > 0 && (long long)grid.x * grid.y >= VG_GEMM8_MIN_TILES;
+}
+
 template <bool BF>
 static int gemm(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t b_trans, const float* bias,
                 int32_t act, const float* aux, int32_t ldaux, float* C, int32_t ldc, int32_t N, int32_t M,
@@ -1697,8 +1816,14 @@ static int gemm(const float* A, int32_t lda, const float* B, int32_t ldb, int32_
   do {                                                                                                     \
     if ((VG_GEMM16 & (BF ? 8 : 1)) != 0)                                                                   \
       if (quad_ab(A, lda, B, ldb, K, M, BT))                                                               \
-        k_gemm16<BT, ACT, false, BF, false, true><<<grid, 1024, 0, s>>>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, \
-                                                                       N, M, K);                             \
+        if (use_8w(grid))                                                                                  \
+          k_gemm8w<BT, ACT, false, BF, false, true><<<grid, 512, 0, s>>>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, \
+                                                                         N, M, K);                           \
+        else                                                                                               \
+          k_gemm16<BT, ACT, false, BF, false, true><<<grid, 1024, 0, s>>>(A, lda, B, ldb, bias, aux, ldaux, C,  \
+                                                                         ldc, N, M, K);                      \
+      else if (use_8w(grid))                                                                               \
+        k_gemm8w<BT, ACT, false, BF><<<grid, 512, 0, s>>>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, N, M, K); \
       else                                                                                                 \
         k_gemm16<BT, ACT, false, BF><<<grid, 1024, 0, s>>>(A, lda, B, ldb, bias, aux, ldaux, C, ldc, N, M, K); \
     else if (BF && quad_ab(A, lda, B, ldb, K, M, true))                                                    \
@@ -1732,8 +1857,15 @@ static int gemm_gn_bwd(const float* A, int32_t lda, const float* B, int32_t ldb,
   const GnpDesc gn{gn_x, keep, stats, weight, bias, mean_scale, eps, seg_rows, tpart};
   if ((VG_GEMM16 & 4) && (!BF || (VG_GEMM16 & 8)))
     if (quad_ab(A, lda, B, ldb, K, M, false))
-      k_gemm16<false, 0, false, BF, true, true><<<grid, 1024, 0, s>>>(A, lda, B, ldb, nullptr, nullptr, 0, C, ldc, N, M,
-                                                                     K, nullptr, nullptr, nullptr, nullptr, gn);
+      if (use_8w(grid))
+        k_gemm8w<false, 0, false, BF, true, true><<<grid, 512, 0, s>>>(A, lda, B, ldb, nullptr, nullptr, 0, C, ldc, N,
+                                                                       M, K, nullptr, nullptr, nullptr, nullptr, gn);
+      else
+        k_gemm16<false, 0, false, BF, true, true><<<grid, 1024, 0, s>>>(A, lda, B, ldb, nullptr, nullptr, 0, C, ldc, N,
+                                                                       M, K, nullptr, nullptr, nullptr, nullptr, gn);
+    else if (use_8w(grid))
+      k_gemm8w<false, 0, false, BF, true><<<grid, 512, 0, s>>>(A, lda, B, ldb, nullptr, nullptr, 0, C, ldc, N, M, K,
+                                                               nullptr, nullptr, nullptr, nullptr, gn);
     else
       k_gemm16<false, 0, false, BF, true><<<grid, 1024, 0, s>>>(A, lda, B, ldb, nullptr, nullptr, 0, C, ldc, N, M, K,
                                                                nullptr, nullptr, nullptr, nullptr, gn);
@@ -2101,7 +2233,14 @@ static int gat_lin_att(const float* X, int32_t ldx, const float* W, int32_t N,
   }
   if ((VG_GEMM16 & 2) && (!BF || (VG_GEMM16 & 8)))
     if (quad_ab(X, ldx, W, Cin, Cin, C, true))
-      k_gemm16<true, 0, true, BF, false, true><<<dim3((N + TM - 1) / TM, 1), 1024, 0, s>>>(
+      if (use_8w(dim3((N + TM - 1) / TM, 1)))
+        k_gemm8w<true, 0, true, BF, false, true><<<dim3((N + TM - 1) / TM, 1), 512, 0, s>>>(
+            X, ldx, W, Cin, nullptr, nullptr, 0, H, C, N, C, Cin, att_src, att_dst, a_src, a_dst);
+      else
+        k_gemm16<true, 0, true, BF, false, true><<<dim3((N + TM - 1) / TM, 1), 1024, 0, s>>>(
+            X, ldx, W, Cin, nullptr, nullptr, 0, H, C, N, C, Cin, att_src, att_dst, a_src, a_dst);
+    else if (use_8w(dim3((N + TM - 1) / TM, 1)))
+      k_gemm8w<true, 0, true, BF><<<dim3((N + TM - 1) / TM, 1), 512, 0, s>>>(
           X, ldx, W, Cin, nullptr, nullptr, 0, H, C, N, C, Cin, att_src, att_dst, a_src, a_dst);
     else
       k_gemm16<true, 0, true, BF><<<dim3((N + TM - 1) / TM, 1), 1024, 0, s>>>(

@@ -8,11 +8,13 @@ batch 32) and the gradients are averaged once per backward:
 * 5 x D gradient (15,665 floats, 63 KB) per step -- the critic updates;
 * 1 x G gradient (274,185 floats, 1.10 MB) per step.
 
-Both are single flat buffers (``vgan.flat``), i.e. one collective per backward:
-over xGMI (point-to-point links, ~153 GB/s each) a ring all-reduce of 1.1 MB at
-8 ranks is ~12 us, latency-dominated, so one bucket per model is right and there
-is nothing to gain from splitting it to overlap with the (already finished)
-backward.  ``torch.distributed`` backend "nccl" is RCCL on ROCm; "gloo" is used
+Both are single flat buffers (``vgan.flat``).  Over xGMI (point-to-point
+links, ~153 GB/s each) a ring all-reduce of 1.1 MB at 8 ranks is ~12 us,
+latency-dominated: D's gradient is one bucket per critic iteration (its
+parameter gradients are all formed by the backward's final fold batch), G's
+two -- the decoder's, reduced on a side stream while the encoders' backward
+runs, then the rest (Trainer._gen_iteration_synced).  RCCL averages in the
+collective (ReduceOp.AVG): no scale launch.  ``torch.distributed`` backend "nccl" is RCCL on ROCm; "gloo" is used
 for the CPU multi-process tests.
 """
 from __future__ import annotations
@@ -73,10 +75,29 @@ class GradSync:
         if self.active:
             dist.broadcast(flat.param, src=0, group=self.group)
 
+    @property
+    def avg_op(self) -> bool:
+        """RCCL averages in the collective itself (ncclAvg): no separate scale
+        launch after every all-reduce -- six fewer dependent launches per step
+        (and per captured graph).  gloo has no AVG: sum, then scale."""
+        return self.backend == "nccl" and hasattr(dist.ReduceOp, "AVG")
+
     def all_reduce_grad(self, flat) -> None:
         if self.active:
-            dist.all_reduce(flat.grad, op=dist.ReduceOp.SUM, group=self.group)
-            flat.grad.mul_(1.0 / self.world)
+            if self.avg_op:
+                dist.all_reduce(flat.grad, op=dist.ReduceOp.AVG, group=self.group)
+            else:
+                dist.all_reduce(flat.grad, op=dist.ReduceOp.SUM, group=self.group)
+                flat.grad.mul_(1.0 / self.world)
+
+    def all_reduce_tensor(self, t: torch.Tensor) -> None:
+        """Average a (contiguous) gradient bucket in place over the ranks."""
+        if self.active:
+            if self.avg_op:
+                dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.group)
+            else:
+                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+                t.mul_(1.0 / self.world)
 
     def all_reduce_scalars(self, t: torch.Tensor) -> torch.Tensor:
         if self.active:

@@ -231,9 +231,14 @@ class GeneratorEngine:
         return dH
 
     # ------------------------------------------------------------ engine
-    def loss_and_grad(self, local_graph, voxel_graph, rng):
+    def loss_and_grad(self, local_graph, voxel_graph, rng, early=None):
         """(g_loss device scalar, label_hard [1, N, K]) of trainer.py:483-490;
-        the generator's gradients are added to its .grad."""
+        the generator's gradients are added to its .grad.  ``early``: called
+        (no arguments) as soon as the decoder's gradient is complete -- its
+        weight-gradient products and folds flushed right after the decoder's
+        backward instead of with the rest -- while the encoders' backward is
+        still to run (the data-parallel trainer starts the decoder bucket's
+        all-reduce there, on a side stream).  Bit-identical either way."""
         G, D = self.G, self.D
         K = self.n_classes
         prep = vdata.prepared(local_graph, voxel_graph, K)
@@ -398,6 +403,9 @@ class GeneratorEngine:
         tp = self._gemm_dy(st, dev, ptr(g_h), m, ptr(Wd), kd, g_enc, n, ec, m, genc[-1])
         g_xem = _f(n, hg + hl, dev=dev)  # [x | em] columns of the decoder input (enc taken above)
         self._gemm(st, ptr(g_h), m, _off(Wd, ec), kd, 0, ptr(g_xem), hg + hl, n, hg + hl, m)
+        if early is not None:  # the decoder's gradient complete: its bucket can go
+            folds.flush(st)
+            early()
         g_y = g_enc
         g_x = None
         for b in range(len(genc) - 1, -1, -1):

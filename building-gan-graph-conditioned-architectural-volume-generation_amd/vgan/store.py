@@ -55,11 +55,12 @@ CRITIC_COPIES = 3  # the critic engine's stacked real / fake / mix graph (vgan.c
 
 
 def _prepare_spec(prepare):
-    """``prepare``: the number of classes, or (classes, stacked copy counts):
-    the block-diagonal copies to build besides the critic's 3 (the inference
-    sweep's one per temperature)."""
+    """``prepare``: the number of classes (training batches: the critic's 3
+    block-diagonal copies are built too), or (classes, stacked copy counts)
+    -- e.g. (7, ()) for inference batches, which build their stacked graph
+    on the device."""
     if isinstance(prepare, (tuple, list)):
-        k, copies = int(prepare[0]), tuple(sorted({int(c) for c in prepare[1]} | {CRITIC_COPIES}))
+        k, copies = int(prepare[0]), tuple(sorted({int(c) for c in prepare[1] if int(c) > 1}))
     else:
         k, copies = int(prepare), (CRITIC_COPIES,)
     return k, copies

@@ -214,3 +214,12 @@ class SyntheticDataset:
 
     def batch(self, indices: Sequence[int]):
         return self.collate_fn([self[i] for i in indices])
+
+
+def write_synthetic_store(path: str, size: int, seed: int = 777) -> None:
+    """A GraphStore of ``size`` synthetic buildings (vgan.store.write_store over
+    SyntheticDataset(size, seed)); the bench runs it in a child process while
+    the GPU legs run."""
+    from .store import write_store
+
+    write_store(path, SyntheticDataset(size, seed=seed))

@@ -234,11 +234,13 @@ class Trainer:
                 _, hard, soft = self._generate(local_graph, voxel_graph)
         return self._critic_loss_backward(local_graph, voxel_graph, hard, soft)
 
-    def _gen_iteration(self, local_graph, voxel_graph):
+    def _gen_iteration(self, local_graph, voxel_graph, early=None):
         """trainer.py:483-492 up to backward(); the update (adam_g.step(counted=True)) is the caller's."""
         self._iter_begin(self.adam_g)
         if self.gen_engine is not None and self.skip_dead_d_grads:
-            return self.gen_engine.loss_and_grad(local_graph, voxel_graph, self.rng)
+            return self.gen_engine.loss_and_grad(local_graph, voxel_graph, self.rng, early=early)
+        if early is not None:  # the autograd path has no early bucket: the caller reduces it whole
+            early()
         logits, hard, _ = self._generate(local_graph, voxel_graph)
         d_params = list(self.discriminator.parameters())
         if self.skip_dead_d_grads:
@@ -254,6 +256,44 @@ class Trainer:
                     p.requires_grad_(True)
         return g_loss, hard
 
+    def _overlap_ready(self) -> bool:
+        """Overlap the generator's all-reduce with its backward: RCCL ranks
+        (capturable, stream-ordered collectives), the explicit generator
+        schedule, runtime['overlap_allreduce'] (default on)."""
+        return (self.sync.active and self.sync.capturable and self.gen_engine is not None
+                and self.skip_dead_d_grads and getattr(self.configuration, "runtime", {}).get("overlap_allreduce", True))
+
+    def _gen_iteration_synced(self, local_graph, voxel_graph):
+        """The generator iteration with its flat gradient averaged over the
+        ranks.  With RCCL the gradient goes in two buckets: the decoder's
+        (the last parameters of the flat buffer, models.py:92-113), reduced on
+        a side stream as soon as the decoder's backward has formed it, while
+        the GAT encoder and MLP backward run; then the rest.  (north_star:
+        "RCCL gradient all-reduce over xGMI overlapped with backward"; inside
+        a captured graph the side stream is a parallel branch.)"""
+        if not self._overlap_ready():
+            out = self._gen_iteration(local_graph, voxel_graph)
+            self.sync.all_reduce_grad(self.flat_g)
+            return out
+        flat = self.flat_g
+        lo = self.__dict__.get("_dec_offset")
+        if lo is None:
+            lo = self._dec_offset = min(flat._offset(p) for p in self.generator.decoder.parameters())
+        cur = torch.cuda.current_stream(flat.grad.device)
+        side = self.__dict__.get("_ar_stream")
+        if side is None:
+            side = self._ar_stream = torch.cuda.Stream(flat.grad.device)
+
+        def early():
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                self.sync.all_reduce_tensor(flat.grad[lo:])
+
+        out = self._gen_iteration(local_graph, voxel_graph, early=early)
+        self.sync.all_reduce_tensor(flat.grad[:lo])
+        cur.wait_stream(side)
+        return out
+
     def step(self, local_graph, voxel_graph) -> Dict[str, torch.Tensor]:
         """One full G+D step (trainer.py:466-495); returns device tensors."""
         with gemm_precision_scope(self.precision):
@@ -268,8 +308,7 @@ class Trainer:
             d_losses.append(d_loss.detach())
             self.sync.all_reduce_grad(self.flat_d)
             self.adam_d.step(counted=True)
-        g_loss, hard = self._gen_iteration(local_graph, voxel_graph)
-        self.sync.all_reduce_grad(self.flat_g)
+        g_loss, hard = self._gen_iteration_synced(local_graph, voxel_graph)
         self.adam_g.step(counted=True)
         return {"d_losses": torch.stack(d_losses), "g_loss": g_loss.detach(), "label_hard": hard.detach()}
 
@@ -288,10 +327,11 @@ class Trainer:
 
     def _gen_body(self, local_graph, voxel_graph, acc, with_adam: bool, sync: bool = False):
         """The generator iteration; its loss goes to acc[-1]."""
-        g_loss, hard = self._gen_iteration(local_graph, voxel_graph)
-        acc[-1].copy_(g_loss.detach())
         if sync:
-            self.sync.all_reduce_grad(self.flat_g)
+            g_loss, hard = self._gen_iteration_synced(local_graph, voxel_graph)
+        else:
+            g_loss, hard = self._gen_iteration(local_graph, voxel_graph)
+        acc[-1].copy_(g_loss.detach())
         if with_adam:
             self.adam_g.step(counted=True)
         return hard.detach()
@@ -516,8 +556,7 @@ class Trainer:
         ev = events[j] = torch.cuda.Event()
         ev.record(cur)  # behind this batch's last launch of owners[j]
         mark("replays")
-        g_loss, hard = self._gen_iteration(local_graph, voxel_graph)
-        self.sync.all_reduce_grad(self.flat_g)
+        g_loss, hard = self._gen_iteration_synced(local_graph, voxel_graph)
         self.adam_g.step(counted=True)
         mark("gen")
         # Recorded graphs are released in batches: destroying one while the

@@ -731,8 +731,8 @@ int vg_gat_aggregate_fwd_lds(const int32_t* row_ptr, const int32_t* col, int32_t
                              float* alpha, const int32_t* plan, int32_t umax, void* stream);
 
 /* Build stamp: "<hash> <compiler>" -- the first 16 hex digits of the sha256
- * of every source this library was built from (csrc/*.hip, csrc/*.h and this
- * header, concatenated in sorted path order) and the hipcc version.  The
+ * of every source this library was built from (the csrc .hip and .h files and
+ * this header, concatenated in sorted path order) and the hipcc version.  The
  * Python binding recomputes the hash from its tree and refuses a library
  * built from other sources. */
 const char* vg_build_stamp(void);

@@ -56,6 +56,14 @@ def rccl1():
     dp = _trainer(cfg, 777)
     dp.sync = GradSync(force=True)
     assert dp.sync.active and dp.sync.capturable and not ref.sync.active
+    # the generator's gradient in two buckets, the decoder's reduced on a side
+    # stream during the encoders' backward (RCCL AVG: no scale launch)
+    assert dp._overlap_ready() and dp.sync.avg_op
+    a = ref.step(loc, vox)  # eager: the overlap outside any capture
+    b = dp.step(loc, vox)
+    torch.cuda.synchronize()
+    assert torch.equal(a["d_losses"], b["d_losses"]) and torch.equal(a["g_loss"], b["g_loss"])
+    assert torch.equal(ref.flat_g.param, dp.flat_g.param) and torch.equal(ref.flat_d.param, dp.flat_d.param)
     for _ in range(2):
         a = ref.step_graphed(loc, vox)
         b = dp.step_graphed(loc, vox)

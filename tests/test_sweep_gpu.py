@@ -32,7 +32,7 @@ def test_stream_sweep_equals_eager(cuda, tmp_path, dtype):
 
     def loader():
         return GraphLoader(st, list(range(len(st))), batch_size=5, shuffle=False, device=cuda, prefetch=2,
-                           prepare=(7, (len(taus),)))
+                           prepare=(7, ()))
 
     G.rng = RNG("device", seed=99)
     res = InferenceSweep(G, taus, dtype=dtype).run_stream(loader(), collect=True)
