@@ -20,6 +20,8 @@ step_sanity.pt    config #1: one building (number 4001, sanity.py:15), full
                   5 d_losses, g_loss, metrics, post-step state dicts.
 step_tiny.pt      the same step for a 4-building batch and a reduced config
                   (hidden 16, GAT depth 2) -- exercises the per-building loops.
+forward_b32_f64.pt  forward_b32.pt's generator loss and G gradients in f64
+                  (same models, draws and reference code; default dtype f64).
 ops_small.pt      oracle per-op goldens (GATConv at C_out 1..128, GraphNorm,
                   type-matched mean), cross-checked against ``oracle.dense``.
 
@@ -177,6 +179,61 @@ def make_forward_b32(cfgmod, models, trainer_mod):
     }
 
 
+def make_forward_b32_f64(cfgmod, models, trainer_mod):
+    """forward_b32.pt's generator loss and G gradients once more, in f64: the
+    same reference code, the same f32-initialised models widened to f64
+    (exactly), the same z and Gumbel draws (f32, widened; F.gumbel_softmax
+    gets the draw injected instead of drawing in f64), every default-dtype
+    tensor the reference creates in f64.  It measures the f32 rounding error
+    of the reference's own gradients, so tests/test_b32_gpu.py can hold the
+    GPU's per parameter to a small multiple of it instead of a flat 5e-2."""
+    import torch.nn.functional as F
+
+    cfg = cfgmod.Configuration()
+    items = [synth.make_building(777, i) for i in range(32)]
+    local, voxel = to_pyg(items)
+    torch.manual_seed(777)
+    G = models.VoxelGNNGenerator(cfg, 17, 12)
+    D = models.VoxelGNNDiscriminator(cfg, 17, 12)
+    G.eval()
+    D.eval()
+    n = voxel.num_nodes
+    torch.manual_seed(2001)
+    z = torch.randn(1, n, cfg.Z_DIM)
+    torch.manual_seed(2002)
+    noise = torch.empty(n, 7).exponential_()  # the draw F.gumbel_softmax makes after manual_seed(2002)
+    G.double()
+    D.double()
+    for key in ("x",):
+        setattr(local, key, getattr(local, key).double())
+        setattr(voxel, key, getattr(voxel, key).double())
+    real_gs = F.gumbel_softmax
+
+    def injected(logits, tau=1, hard=False, eps=1e-10, dim=-1):
+        gumbels = -noise.to(logits.dtype).log()
+        return ((logits + gumbels) / tau).softmax(dim)
+
+    opt = torch.optim.Adam(D.parameters())
+    prev = torch.get_default_dtype()
+    F.gumbel_softmax = injected
+    torch.set_default_dtype(torch.float64)
+    try:
+        tr = trainer_mod.Trainer(G, D, _Loaders([]), torch.optim.Adam(G.parameters()), opt,
+                                 torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=10), cfg,
+                                 log_dir=os.path.join("/tmp", "vgan_golden_unused"))
+        G.zero_grad()
+        D.zero_grad()
+        logits_g, hard_g, _ = G(local, voxel, z.double())
+        g_loss = tr._compute_generator_loss(local, voxel, logits_g, hard_g.unsqueeze(0))
+        g_loss.backward()
+    finally:
+        F.gumbel_softmax = real_gs
+        torch.set_default_dtype(prev)
+    return {"batch_checksum": batch_checksum(local, voxel), "g_loss": g_loss.detach(),
+            "label_argmax": hard_g.argmax(1).to(torch.int8),
+            "g_grads": {k: p.grad.detach().clone() for k, p in G.named_parameters()}}
+
+
 def batch_checksum(local, voxel):
     """float64 sums identifying the collated inputs (features, types, edges)."""
     parts = [local.x.double().sum(), local.type.double().sum(), voxel.x.double().sum(),
@@ -284,6 +341,7 @@ def main():
     jobs = {
         "forward_eval.pt": lambda: make_forward_eval(cfgmod, models, trainer_mod),
         "forward_b32.pt": lambda: make_forward_b32(cfgmod, models, trainer_mod),
+        "forward_b32_f64.pt": lambda: make_forward_b32_f64(cfgmod, models, trainer_mod),
         "step_sanity.pt": lambda: make_step_sanity(cfgmod, models, trainer_mod),
         "step_tiny.pt": lambda: make_step_tiny(cfgmod, models, trainer_mod),
         "ops_small.pt": make_ops_small,

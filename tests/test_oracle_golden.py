@@ -170,3 +170,36 @@ def test_oracle_matches_reference_at_batch_32():
     assert torch.equal(g_loss.detach(), f["g_loss"])
     for k, p in G.named_parameters():
         assert torch.equal(p.grad, f["g_grads"][k]), k
+
+
+def test_oracle_matches_f64_reference_at_batch_32():
+    """The restatement run in f64 (the f32-initialised models widened, the same
+    draws) against the reference's own code run in f64
+    (forward_b32_f64.pt): generator loss and every G gradient to f64
+    rounding -- the baseline tests/test_b32_gpu.py measures f32 errors from."""
+    from parity_util import b32_inputs
+
+    f = load_fixture("forward_b32.pt")
+    f64 = load_fixture("forward_b32_f64.pt")
+    inp = b32_inputs(f, device=None)
+    local, voxel = inp["oracle"]
+    local.x, voxel.x = local.x.double(), voxel.x.double()
+    cfg = Configuration()
+    torch.manual_seed(int(f["init_seed"]))
+    G, D = R.Generator(cfg).double(), R.Discriminator(cfg).double()
+    G.eval()
+    D.eval()
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float64)
+    try:
+        logits, hard, _ = G(local, voxel, inp["z"].double(), noise=inp["noise"].double())
+        g_loss = R.generator_loss(D, cfg, local, voxel, logits, hard.unsqueeze(0))
+        g_loss.backward()
+    finally:
+        torch.set_default_dtype(prev)
+    assert torch.equal(hard.argmax(1).to(torch.int8), f64["label_argmax"])
+    assert abs(float(g_loss) - float(f64["g_loss"])) <= 1e-12 * abs(float(f64["g_loss"]))
+    scale = float(torch.cat([v.reshape(-1) for v in f64["g_grads"].values()]).norm())
+    for k, p in G.named_parameters():
+        want = f64["g_grads"][k]
+        assert float((p.grad - want).norm()) <= 1e-9 * float(want.norm()) + 1e-12 * scale, k
