@@ -416,71 +416,117 @@ __global__ void __launch_bounds__(kBlock) k_gn_bwd_final(
   }
 }
 
+// One group of up to kSegs segments of k_gn_bwd_final_tiles' fold.
+template <int kSegs, int kU>
+__device__ __forceinline__ void bwd_tiles_group(const float* __restrict__ tpart, int N, int C, int S, int s0,
+                                                int c, int lane, const float* __restrict__ w, float eps,
+                                                const float* __restrict__ stats, float* __restrict__ sums,
+                                                const float* __restrict__ g3[3], float g0[3],
+                                                float& tw, float& tb, float& tm) {
+  constexpr int kTile = 64;
+  float va[kSegs][kU], vb[kSegs][kU], mu[kSegs], sd[kSegs];
+  int t0[kSegs], t1[kSegs];
+#pragma unroll
+  for (int j = 0; j < kSegs; ++j) {
+    const int sg = min(s0 + j, S - 1);
+    const long long r0 = (long long)sg * N;
+    t0[j] = static_cast<int>(r0 / kTile);
+    t1[j] = static_cast<int>((r0 + N - 1) / kTile);
+    mu[j] = stats[(size_t)sg * 2 * C + c];
+    sd[j] = stats[(size_t)sg * 2 * C + C + c];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int t = t0[j] + lane + 64 * u;
+      const int tc = min(t, t1[j]);
+      const int slot = (long long)tc * kTile >= r0 ? 0 : 1;  // first row in this segment, or in the previous one
+      const float2 v = *reinterpret_cast<const float2*>(tpart + ((size_t)(2 * tc + slot) * C + c) * 2);
+      va[j][u] = v.x;
+      vb[j][u] = v.y;
+    }
+  }
+  // the per-column operands and (first group) the accumulated gradients, in
+  // flight with the partials
+  const float wc = w[c];
+  if (g3) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) g0[q] = g3[q][c];
+  }
+#pragma unroll
+  for (int j = 0; j < kSegs; ++j) {
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const bool ok = s0 + j < S && t0[j] + lane + 64 * u <= t1[j];
+      va[j][u] = ok ? va[j][u] : 0.f;
+      vb[j][u] = ok ? vb[j][u] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < kSegs; ++j) {
+    const int sg = s0 + j;
+    if (sg >= S) break;
+    float a = 0.f, bb = 0.f;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      a += va[j][u];
+      bb += vb[j][u];
+    }
+    const long long r0 = (long long)sg * N;
+    for (int t = t0[j] + lane + 64 * kU; t <= t1[j]; t += 64) {  // segments of more than 16k rows
+      const int slot = (long long)t * kTile >= r0 ? 0 : 1;
+      const float* p = tpart + ((size_t)(2 * t + slot) * C + c) * 2;
+      a += p[0];
+      bb += p[1];
+    }
+    a = wave_sum(a);
+    bb = wave_sum(bb);
+    if (lane == 0) {
+      sums[(size_t)sg * 2 * C + c] = a;
+      sums[(size_t)sg * 2 * C + C + c] = bb;
+    }
+    tw += bb;
+    tb += a;
+    tm += -mu[j] * wc * a / (sd[j] + eps);
+  }
+}
+
 // The same fold over the partials that the producing GEMM wrote in its
 // epilogue (vg_gemm_gn_bwd): tpart[tile][slot][C][2] for 64-row tiles of the
 // S * N stacked rows, slot 0 = the segment of the tile's first row, slot 1 =
 // the next segment (a tile straddles at most two: N >= 64).  One wave per
 // column; segment sg sums its tiles in tile order (deterministic).
+//
+// Every load of the fold is issued before the first wait: the partials at
+// clamped (always valid) addresses, zeroed afterwards when out of range, the
+// per-column operands and the accumulated gradients unconditionally, and no
+// loop around the common S <= 4 case (a loop header made the compiler drain
+// the loads issued before it).  The guarded form (`ok ? p[0] : 0`) compiled to
+// a branch per load and a vmcnt(0) per segment group, then a round trip each
+// for the statistics and the gradients' read-modify-write: ~6 dependent round
+// trips per launch.  Same values, same summation order (bit-identical).
 __global__ void __launch_bounds__(kBlock) k_gn_bwd_final_tiles(
     const float* __restrict__ tpart, int N, int C, int S, const float* __restrict__ w,
     const float* __restrict__ ms, float eps, const float* __restrict__ stats, float* __restrict__ sums,
     float* __restrict__ g_w, float* __restrict__ g_b, float* __restrict__ g_ms, int accumulate) {
-  constexpr int kTile = 64, kSegs = 4, kU = 4;  // segments in flight together, tiles per lane and segment
+  constexpr int kSegs = 4, kU = 4;  // segments in flight together, tiles per lane and segment
   const int c = fold_col(), lane = threadIdx.x & 63;
   if (c >= C) return;
+  const bool acc = g_w && accumulate;
+  const float* g3[3] = {acc ? g_w : w, acc ? g_b : w, acc ? g_ms : w};
+  float g0[3] = {0.f, 0.f, 0.f};
   float tw = 0.f, tb = 0.f, tm = 0.f;
-  for (int s0 = 0; s0 < S; s0 += kSegs) {
-    float va[kSegs][kU], vb[kSegs][kU];
-    int t0[kSegs], t1[kSegs];
-#pragma unroll
-    for (int j = 0; j < kSegs; ++j) {
-      const long long r0 = (long long)(s0 + j) * N;
-      t0[j] = static_cast<int>(r0 / kTile);
-      t1[j] = static_cast<int>((r0 + N - 1) / kTile);
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int t = t0[j] + lane + 64 * u;
-        const bool ok = s0 + j < S && t <= t1[j];
-        const int slot = (long long)t * kTile >= r0 ? 0 : 1;  // first row in this segment, or in the previous one
-        const float* p = tpart + ((size_t)(2 * t + slot) * C + c) * 2;
-        va[j][u] = ok ? p[0] : 0.f;
-        vb[j][u] = ok ? p[1] : 0.f;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < kSegs; ++j) {
-      const int sg = s0 + j;
-      if (sg >= S) break;
-      float a = 0.f, bb = 0.f;
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        a += va[j][u];
-        bb += vb[j][u];
-      }
-      const long long r0 = (long long)sg * N;
-      for (int t = t0[j] + lane + 64 * kU; t <= t1[j]; t += 64) {  // segments of more than 16k rows
-        const int slot = (long long)t * kTile >= r0 ? 0 : 1;
-        const float* p = tpart + ((size_t)(2 * t + slot) * C + c) * 2;
-        a += p[0];
-        bb += p[1];
-      }
-      a = wave_sum(a);
-      bb = wave_sum(bb);
-      const float* st = stats + (size_t)sg * 2 * C;
-      if (lane == 0) {
-        sums[(size_t)sg * 2 * C + c] = a;
-        sums[(size_t)sg * 2 * C + C + c] = bb;
-      }
-      tw += bb;
-      tb += a;
-      tm += -st[c] * w[c] * a / (st[C + c] + eps);
-    }
+  if (S <= kSegs) {
+    bwd_tiles_group<kSegs, kU>(tpart, N, C, S, 0, c, lane, w, eps, stats, sums, g3, g0, tw, tb, tm);
+  } else {
+    for (int s0 = 0; s0 < S; s0 += kSegs)
+      bwd_tiles_group<kSegs, kU>(tpart, N, C, S, s0, c, lane, w, eps, stats, sums, s0 == 0 ? g3 : nullptr, g0,
+                                 tw, tb, tm);
   }
   if (lane == 0 && g_w) {
-    g_w[c] = accumulate ? g_w[c] + tw : tw;
-    g_b[c] = accumulate ? g_b[c] + tb : tb;
-    g_ms[c] = accumulate ? g_ms[c] + tm : tm;
+    g_w[c] = acc ? g0[0] + tw : tw;
+    g_b[c] = acc ? g0[1] + tb : tb;
+    g_ms[c] = acc ? g0[2] + tm : tm;
   }
+  (void)ms;
 }
 
 // g_x (+ inj for elements t >= inj_off: the second-order adjoint of the
@@ -687,25 +733,30 @@ __global__ void __launch_bounds__(kBlock) k_gn_jvp2_final_blk(
   const int c = fold_col(), lane = threadIdx.x & 63;
   if (c >= C) return;
   constexpr int U = 16;
+  // the per-column operands and the gradients are loaded with the partials
+  // (one round trip, not three: k_gn_bwd_final_tiles' note); the partials at
+  // clamped addresses, zeroed when out of range (same sums, same order)
+  const float mu = stats[c], sd = stats[C + c], msc = ms[c], wc = w[c];
+  const float gw0 = g_w[c], gm0 = g_ms[c];
   float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   for (int b0 = lane; b0 < blocks; b0 += 64 * U) {
     float t[U][5];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int b = b0 + 64 * u;
+      const int b = min(b0 + 64 * u, blocks - 1);
 #pragma unroll
-      for (int q = 0; q < 5; ++q) t[u][q] = b < blocks ? part[((size_t)b * 5 + q) * C + c] : 0.f;
+      for (int q = 0; q < 5; ++q) t[u][q] = part[((size_t)b * 5 + q) * C + c];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int q = 0; q < 5; ++q) v[q] += t[u][q];
+      for (int q = 0; q < 5; ++q) v[q] += b0 + 64 * u < blocks ? t[u][q] : 0.f;
   }
 #pragma unroll
   for (int q = 0; q < 5; ++q) v[q] = wave_sum(v[q]);
   if (lane != 0) return;
   const float inv_n = 1.f / static_cast<float>(N);
-  const float mu = stats[c], sd = stats[C + c], d = sd + eps, msc = ms[c], wc = w[c];
+  const float d = sd + eps;
   const float mup = v[0] * inv_n, M = v[1] * inv_n, Sp = v[2];
   const float P1 = v[3] - msc * mup * Sp;
   const float P2 = v[4] + (1.f - msc) * mu * Sp;
@@ -716,8 +767,8 @@ __global__ void __launch_bounds__(kBlock) k_gn_jvp2_final_blk(
   sm[2] = Sp;
   sm[3] = P1;
   sm[4] = P2;
-  g_w[c] += P1 / d - P2 * M * isd / (d * d);
-  g_ms[c] += wc * (-mup * Sp / d + mu * Sp * M * isd / (d * d));
+  g_w[c] = gw0 + (P1 / d - P2 * M * isd / (d * d));
+  g_ms[c] = gm0 + wc * (-mup * Sp / d + mu * Sp * M * isd / (d * d));
 }
 
 // u_out = keep [z>0] w (c'/d - c sigma'/d^2);  x_inj = dQ/dx

@@ -507,7 +507,14 @@ __global__ void k_rng_fill(float* __restrict__ out, long long n, int kind, unsig
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float u = static_cast<float>(w[q] >> 8) * (1.0f / 16777216.0f);  // [0, 1)
-        v[q] = kind == 1 ? u : -logf(1.f - u);  // uniform / Exp(1)
+        // Exp(1) strictly positive: the Gumbel noise g = -log(E) (models.py:150)
+        // is +inf at E = 0 and the label softmax NaN.  -log(1 - u) with u = 0
+        // hit that once per 2^24 draws -- ~130 training steps at 16 buildings.
+        // u' = (x + 0.5) / 2^23 on 23 bits lies in [2^-24, 1 - 2^-24], both
+        // exact, so E in [6e-8, 16.6] (torch's GPU exponential_ likewise keeps
+        // its log away from 0).
+        const float ue = (static_cast<float>(w[q] >> 9) + 0.5f) * (1.0f / 8388608.0f);
+        v[q] = kind == 1 ? u : -logf(1.f - ue);  // uniform / Exp(1)
       }
     }
 #pragma unroll

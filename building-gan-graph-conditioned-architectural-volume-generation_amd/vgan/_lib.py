@@ -332,7 +332,11 @@ def source_hash(csrc: str) -> Optional[str]:
 
 def _check_stamp(lib) -> None:
     """A library built from other sources than the tree's fails loudly (a
-    stale prebuilt .so would otherwise run old kernels under new tests)."""
+    stale prebuilt .so would otherwise run old kernels under new tests).
+    An explicit VGAN_LIB (an A/B build of other sources, tools/ab_libs.sh)
+    is exempt."""
+    if os.environ.get("VGAN_LIB"):
+        return
     stamp = lib.vg_build_stamp().decode()
     want = source_hash(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc"))
     if want is not None and stamp.split(" ")[0] != want:

@@ -317,6 +317,18 @@ def step_iterations_bf16_vs_oracle(cuda, cfg, g0, d0, vgan_pair, oracle_pair, st
         lo, ho, _ = Go(ol, ov, torch.randn(1, ov.num_nodes, cfg.Z_DIM))
         g_ref = R.generator_loss(Do, cfg, ol, ov, lo, ho.unsqueeze(0))
         g_ref.backward()
+        # the G gradient's conditioning: the same oracle iteration with every G
+        # and D parameter rounded to bf16 (a 2^-9 relative perturbation of the
+        # parameters alone, no bf16 arithmetic) -- tools/bf16_g_probe.py
+        rnd = lambda sd: {k: v.to(torch.bfloat16).float() if v.is_floating_point() else v for k, v in sd.items()}
+        Gr, Dr = R.Generator(cfg), R.Discriminator(cfg)
+        Gr.load_state_dict(rnd(Go.state_dict()))
+        Dr.load_state_dict(rnd(Do.state_dict()))
+        torch.set_rng_state(state)
+        lr_, hr_, _ = Gr(ol, ov, torch.randn(1, ov.num_nodes, cfg.Z_DIM))
+        R.generator_loss(Dr, cfg, ol, ov, lr_, hr_.unsqueeze(0)).backward()
+        m["g_cond"], m["g_cos_cond"] = _rel_cos({k: p.grad for k, p in Gr.named_parameters()},
+                                                {k: p.grad for k, p in Go.named_parameters()})
         torch.set_rng_state(state)
         tr.adam_g.zero_grad()
         g_loss, hard = tr._gen_iteration(loc, vox)
@@ -325,7 +337,11 @@ def step_iterations_bf16_vs_oracle(cuda, cfg, g0, d0, vgan_pair, oracle_pair, st
                                            {k: p.grad for k, p in Go.named_parameters()})
     print("bf16 step vs f32 oracle:", {k: f"{v:.3e}" for k, v in m.items()})
     for k, v in bounds.items():
-        if k.endswith("_cos"):
+        if k == "g_grad_over_cond":  # bf16 deviation within v x the conditioning's (+ 0.05)
+            assert m["g_grad"] <= v * m["g_cond"] + 0.05, (k, m["g_grad"], m["g_cond"], v)
+        elif k == "g_cos_over_cond":  # 1 - cos ~ rel^2 / 2: v on the relative error is v^2 here
+            assert 1 - m["g_cos"] <= v * v * (1 - m["g_cos_cond"]) + 0.02, (k, m["g_cos"], m["g_cos_cond"], v)
+        elif k.endswith("_cos"):
             assert m[k] >= v, (k, m[k], v)
         else:
             assert m[k] <= v, (k, m[k], v)
