@@ -20,7 +20,9 @@ collate_fn=GraphDataset.collate_fn, num_workers=NUM_WORKERS)``.  Here:
 """
 from __future__ import annotations
 
+import os
 import queue
+import sys
 import threading
 from typing import Iterator, List, Optional, Sequence, Tuple
 
@@ -29,6 +31,9 @@ from torch.utils.data import DataLoader, random_split
 
 from .graph import GraphBatch
 from .store import GraphStore, upload_pair
+
+# GIL switch interval while a prefetch thread runs (seconds; _prefetched)
+_SWITCH_INTERVAL = float(os.environ.get("VGAN_LOADER_SWITCH_INTERVAL", "1e-4"))
 
 
 class _Indices(torch.utils.data.Dataset):
@@ -168,6 +173,15 @@ def _prefetched(store: GraphStore, plan: List[List[int]], dev: torch.device, dep
             q.put(exc)
 
     th = threading.Thread(target=worker, name="vgan-loader", daemon=True)
+    # While the worker runs, the interpreter hands the GIL over every 0.1 ms
+    # instead of every 5 ms: the consumer (the training step) is host-bound on
+    # ctypes launches, each of which releases the GIL, and on return it
+    # otherwise waits out whatever Python the worker is running (tensor views,
+    # the batch objects) -- 10.1-10.7 vs 8.5 ms per fresh-batch step
+    # (tools/fresh_probe.py, profiles/r04_fresh_probe.jsonl).  Restored when
+    # the iteration ends.
+    old_switch = sys.getswitchinterval()
+    sys.setswitchinterval(min(old_switch, _SWITCH_INTERVAL))
     th.start()
     try:
         while True:
@@ -184,6 +198,7 @@ def _prefetched(store: GraphStore, plan: List[List[int]], dev: torch.device, dep
             del host
             yield moved
     finally:
+        sys.setswitchinterval(old_switch)
         stop.set()
         while th.is_alive():
             try:

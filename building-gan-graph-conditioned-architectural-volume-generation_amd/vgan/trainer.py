@@ -482,12 +482,25 @@ class Trainer:
         self.adam_g.sync_lr()
         self.adam_d.sync_lr()
         mark("prepare")
-        hard_all, soft_all = self._critic_labels(local_graph, voxel_graph)
-        mark("labels")
-        slot = (torch.empty_like(hard_all[0:1]), torch.empty_like(soft_all[0:1]))
         acc = torch.zeros(n_critic + 1, dtype=torch.float32, device=dev)
         cur = torch.cuda.current_stream(dev)
-        if not getattr(self, "_fresh_warm", False):
+        warm = getattr(self, "_fresh_warm", False)
+        if warm:
+            # The critic graph is recorded BEFORE the label forward is enqueued:
+            # the recording (~2 ms of host time) then overlaps the device's
+            # work on the previous step's generator iteration, where after the
+            # label forward the device idled through most of it.  The recorded
+            # body reads its labels from the slot at replay time and draws
+            # from the device counter at replay time, so the order of
+            # recording and enqueueing changes no value.
+            hard_all = soft_all = None
+            n_nodes, k_cls = voxel_graph.num_nodes, cfg.NUM_CLASSES
+            slot = (torch.empty((1, n_nodes, k_cls), dtype=torch.float32, device=dev),
+                    torch.empty((1, n_nodes, k_cls), dtype=torch.float32, device=dev))
+        else:
+            hard_all, soft_all = self._critic_labels(local_graph, voxel_graph)
+            mark("labels")
+            slot = (torch.empty_like(hard_all[0:1]), torch.empty_like(soft_all[0:1]))
             # first capture of this trainer: run the body once outside any
             # capture (lazy initialisation, constant buffers), then undo it
             self.rng._iter(dev)
@@ -543,6 +556,12 @@ class Trainer:
             owner = owners[j] = g
         exec_ = ctypes.c_void_p(owner.raw_cuda_graph_exec())
         mark("capture")
+        if hard_all is None:
+            hard_all, soft_all = self._critic_labels(local_graph, voxel_graph)
+            if hard_all.dtype != slot[0].dtype or hard_all.shape[1:] != slot[0].shape[1:] \
+                    or soft_all.dtype != slot[1].dtype:
+                raise RuntimeError("critic label slot of an unexpected shape / dtype")
+            mark("labels")
         d_losses = torch.empty(n_critic, dtype=torch.float32, device=dev)
         st = stream_handle(dev)
         for i in range(n_critic):

@@ -5,11 +5,18 @@
 Variants of bench.py's fresh-batch leg (a NEW batch every step through
 Trainer._train_batch -> step_fresh), each timed between device syncs:
 
-  loader    GraphLoader prefetching 3 batches on its thread (bench.py's leg)
-  staged    the same batches collated and uploaded before the timed region
-            (each batch still new to the trainer: CSR adopt, type-mean, ELL,
-            capture inside the timed region)
-  switch    loader, with sys.setswitchinterval(1e-4) (GIL hand-off)
+  loader    GraphLoader prefetching 3 batches on its thread, per-batch
+            structures built on the device
+  prepared  the same with prepare=NUM_CLASSES (bench.py's leg: the host
+            collate also builds type-mean, CSR / ELL, the critic's stacked
+            graph, one upload)
+  staged    the prepared batches collated and uploaded before the timed
+            region (each batch still new to the trainer: capture inside it)
+  switch    prepared, with the default 5 ms GIL switch interval (the loader
+            lowers it to 0.1 ms while prefetching, vgan/loader.py)
+
+Each line also carries the host time per step phase (Trainer.phase_hook:
+prepare / labels / capture / replays / gen / release), medians in ms.
 """
 from __future__ import annotations
 
@@ -37,13 +44,15 @@ def run(variant, cfg, bench, dev, steps, warmup, batch=32):
     tmp = tempfile.mkdtemp(prefix="vgan_probe_")
     ds = SyntheticDataset(n * batch, seed=4321)
     store = write_store(os.path.join(tmp, "store"), ds)
-    loader = GraphLoader(store, batch_size=batch, shuffle=True, device=dev, prefetch=3, seed=4321)
+    prep = None if variant == "loader" else cfg.NUM_CLASSES
+    loader = GraphLoader(store, batch_size=batch, shuffle=True, device=dev, prefetch=3, seed=4321, prepare=prep)
     torch.manual_seed(cfg.SEED)
     tr = bench.build_trainer(cfg, "f32")
     cfg.runtime["train_step"] = "auto"
-    old = sys.getswitchinterval()
+    import vgan.loader as vl
+    old = vl._SWITCH_INTERVAL
     if variant == "switch":
-        sys.setswitchinterval(1e-4)
+        vl._SWITCH_INTERVAL = 5e-3
     if variant == "staged":
         batches = list(loader)
         torch.cuda.synchronize()
@@ -53,27 +62,40 @@ def run(variant, cfg, bench, dev, steps, warmup, batch=32):
     for _ in range(warmup):
         tr._train_batch(*next(it))
     torch.cuda.synchronize()
+    phases = {}
+    last = [0.0]
+
+    def mark(name):
+        t = time.perf_counter()
+        phases.setdefault(name, []).append((t - last[0]) * 1e3)
+        last[0] = t
+
+    tr.phase_hook = mark
+    time.sleep(0.05)  # a >= 40 ms idle gap: tools/prof_summary.py --after-gap keeps what follows
     per = []
     t0 = time.perf_counter()
     for _ in range(steps):
         a = time.perf_counter()
+        last[0] = a
         tr._train_batch(*next(it))
         per.append((time.perf_counter() - a) * 1e3)
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / steps * 1e3
-    sys.setswitchinterval(old)
+    vl._SWITCH_INTERVAL = old
     del it, loader
     shutil.rmtree(tmp, ignore_errors=True)
+    tr.phase_hook = None
     per.sort()
+    med = {k: round(sorted(v)[len(v) // 2], 3) for k, v in phases.items()}
     return {"variant": variant, "ms_per_step": round(el, 3), "host_call_ms_median": round(per[len(per) // 2], 3),
-            "host_call_ms_max": round(per[-1], 3)}
+            "host_call_ms_max": round(per[-1], 3), "phase_ms_median": med}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--variants", default="loader,staged,switch,loader")
+    ap.add_argument("--variants", default="prepared,loader,staged,switch,prepared")
     args = ap.parse_args()
     import bench
     from vgan.config import Configuration
