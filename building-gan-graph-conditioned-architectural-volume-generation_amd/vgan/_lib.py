@@ -136,6 +136,45 @@ class VgASrc(ctypes.Structure):
     """vg_asrc (include/vgan.h): one column block of vg_gemm_ln_act_ms's A."""
     _fields_ = [("ptr", _c_p), ("ld", _c_i32), ("cols", _c_i32), ("w_col0", _c_i32), ("rows_mod", _c_i32)]
 
+
+VG_CRITIC_MAX_LAYERS = 8
+
+
+class VgCriticLinear(ctypes.Structure):
+    """vg_critic_linear (include/vgan.h)."""
+    _fields_ = [(k, _c_p) for k in ("weight", "bias", "g_weight", "g_bias")] + [("in_", _c_i32), ("out", _c_i32)]
+
+
+class VgCriticBlock(ctypes.Structure):
+    """vg_critic_block (include/vgan.h): one GATConv + GraphNorm block."""
+    _fields_ = [(k, _c_p) for k in ("lin_weight", "att_src", "att_dst", "bias", "g_lin_weight", "g_att_src",
+                                    "g_att_dst", "g_bias", "gn_weight", "gn_bias", "gn_mean_scale", "g_gn_weight",
+                                    "g_gn_bias", "g_gn_mean_scale")] + \
+               [("gn_eps", _c_f32), ("slope", _c_f32), ("in_", _c_i32), ("out", _c_i32)]
+
+
+class VgCriticModel(ctypes.Structure):
+    """vg_critic_model (include/vgan.h)."""
+    _fields_ = [("n_mlp", _c_i32), ("n_blocks", _c_i32), ("n_dec", _c_i32), ("bf16", _c_i32),
+                ("lambda_gp", _c_f32), ("p_drop", _c_f32), ("mlp", VgCriticLinear * VG_CRITIC_MAX_LAYERS),
+                ("block", VgCriticBlock * VG_CRITIC_MAX_LAYERS), ("dec", VgCriticLinear * VG_CRITIC_MAX_LAYERS)]
+
+
+class VgCsrRef(ctypes.Structure):
+    """vg_csr_ref (include/vgan.h)."""
+    _fields_ = [(k, _c_p) for k in ("row_ptr", "col", "csc_ptr", "csc_slot", "csc_dst", "ell")] + \
+               [("num_nodes", _c_i32), ("num_edges", _c_i32), ("ell_width", _c_i32)]
+
+
+class VgCriticBatch(ctypes.Structure):
+    """vg_critic_batch (include/vgan.h)."""
+    _fields_ = [("n", _c_i32), ("feat", _c_i32), ("classes", _c_i32)] + \
+               [(k, _c_p) for k in ("mvx", "real", "hard", "soft", "seeds4")] + \
+               [("g1", VgCsrRef), ("g3", VgCsrRef), ("seed", ctypes.c_uint64), ("iter", _c_p),
+                ("eps_salt", ctypes.c_uint32), ("keep_salt", ctypes.c_uint32 * VG_CRITIC_MAX_LAYERS),
+                ("gp_counter", _c_p)]
+
+
 # name -> (restype, argtypes); every function listed here is declared in include/vgan.h
 SIGNATURES = {
     "vg_fold_batch": (ctypes.c_int, [_c_p, _c_i32, _c_p]),
@@ -207,6 +246,9 @@ SIGNATURES = {
     "vg_linear_chain": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p]),
     "vg_graph_exec_update": (ctypes.c_int, [_c_p, _c_p]),
     "vg_graph_launch": (ctypes.c_int, [_c_p, _c_p]),
+    "vg_critic_arena_floats": (ctypes.c_int64, [ctypes.POINTER(VgCriticModel), ctypes.POINTER(VgCriticBatch)]),
+    "vg_critic_loss_and_grad": (ctypes.c_int, [ctypes.POINTER(VgCriticModel), ctypes.POINTER(VgCriticBatch), _c_p,
+                                               _c_i64, _c_p, _c_p]),
     "vg_linear_chain_bf16": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p]),
     "vg_gat_gnp_rows": (_c_i32, [_c_i32, _c_i32]),
     "vg_gat_gnp_floats": (_c_i64, [_c_i32, _c_i32]),

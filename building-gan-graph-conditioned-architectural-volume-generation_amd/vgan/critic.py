@@ -50,6 +50,10 @@ _CHAIN_TANGENT = os.environ.get("VGAN_CHAIN_TANGENT", "1") == "1"
 # VGAN_GN_FUSE=0: the GraphNorm backward's column partials in their own pass
 # instead of the epilogue of the GEMM producing its g_y (A/B knob)
 _GN_FUSE = os.environ.get("VGAN_GN_FUSE", "1") == "1"
+# VGAN_NATIVE_CRITIC=0: every critic iteration through the Python engine below
+# instead of vg_critic_loss_and_grad (the same launches issued from C++,
+# bit-identical; include/vgan.h) -- A/B and parity knob
+_NATIVE = os.environ.get("VGAN_NATIVE_CRITIC", "1") == "1"
 
 
 def _f(*shape, dev):
@@ -86,15 +90,171 @@ class CriticEngine:
 
     def prepare_batch(self, prep) -> None:
         """Build this batch's constants (the adjoint seeds of every critic
-        iteration) and the stacked graph now, outside any capture."""
+        iteration) and the stacked graph now, outside any capture -- and size
+        the native engine's arena for it (a capture cannot grow it)."""
         n = prep.matched_voxel_x.shape[0]
-        if "critic_seeds4" not in prep.consts:
+        self._seeds(prep)
+        prep.csr.stacked(3).ell()
+        if self._native_config_ok(n):
+            model = self._native_model()
+            if model is not None:
+                batch = self._native_batch(prep, None, None, None, None)
+                if batch is not None:
+                    self._arena_for(model, batch, prep.matched_voxel_x.device)
+
+    @staticmethod
+    def _seeds(prep) -> torch.Tensor:
+        """The batch's adjoint seeds [4N, 1]: -1/N real | +1/N fake | 0 mix |
+        1 pass-B seed (built once per batch)."""
+        s_ = prep.consts.get("critic_seeds4")
+        if s_ is None:
+            n = prep.matched_voxel_x.shape[0]
             s_ = torch.zeros(4 * n, 1, dtype=torch.float32, device=prep.matched_voxel_x.device)
             s_[:n] = -1.0 / n
             s_[n:2 * n] = 1.0 / n
             s_[3 * n:] = 1.0
             prep.consts["critic_seeds4"] = s_
-        prep.csr.stacked(3).ell()
+        return s_
+
+    # --------------------------------------------------- native engine
+    # vg_critic_loss_and_grad issues loss_and_grad's launches from C++ (same
+    # kernels, order and arguments: bit-identical) with every temporary in
+    # one arena: ~1-2 us of host time per launch instead of ~10.  Used when
+    # the configuration is loss_and_grad's default one (the knobs below at
+    # their defaults, device-drawn dropout and eps, n >= 64); anything else
+    # runs the Python engine.
+    def _native_config_ok(self, n: int) -> bool:
+        return (_NATIVE and _GN_FUSE and n >= 64 and _CHAIN_TANGENT and _lib._GN_ROWS and not _lib._GN_APPLY_GEMM
+                and not _lib._GN_JVP_FUSE and not _lib._JVP_GROUP and _lib._TN_GROUP and _lib._CHAIN
+                and not _lib._LAST_BLOCK and ops._GN_FWD_FUSE and self.D.training
+                and max(len(self.mlp), len(self.blocks), len(self.dec)) <= _lib.VG_CRITIC_MAX_LAYERS)
+
+    def _native_model(self):
+        """The vg_critic_model of D's parameters and gradient views (rebuilt
+        when any of their addresses changes), or None."""
+        params = self.__dict__.get("_params")
+        if params is None:
+            params = self._params = list(self.D.parameters())
+        for p in params:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        key = (gemm_precision(),) + tuple(p.data_ptr() for p in params) + tuple(p.grad.data_ptr() for p in params)
+        cached = self.__dict__.get("_native_key")
+        if cached is not None and cached == key:
+            return self._native_md
+        m = _lib.VgCriticModel()
+        m.n_mlp, m.n_blocks, m.n_dec = len(self.mlp), len(self.blocks), len(self.dec)
+        m.bf16 = 1 if gemm_precision() == "bf16" else 0
+        m.lambda_gp, m.p_drop = self.lam, self.dropout
+
+        def lin(dst, l):
+            dst.weight, dst.bias = l.weight.data_ptr(), l.bias.data_ptr()
+            dst.g_weight, dst.g_bias = l.weight.grad.data_ptr(), l.bias.grad.data_ptr()
+            dst.in_, dst.out = l.in_features, l.out_features
+
+        for i, l in enumerate(self.mlp):
+            lin(m.mlp[i], l)
+        for i, l in enumerate(self.dec):
+            lin(m.dec[i], l)
+        for i, (conv, norm) in enumerate(self.blocks):
+            b = m.block[i]
+            if getattr(conv.lin, "bias", None) is not None:  # (GATConv's lin has none)
+                return None
+            b.lin_weight, b.att_src, b.att_dst, b.bias = (conv.lin.weight.data_ptr(), conv.att_src.data_ptr(),
+                                                          conv.att_dst.data_ptr(), conv.bias.data_ptr())
+            b.g_lin_weight, b.g_att_src, b.g_att_dst, b.g_bias = (conv.lin.weight.grad.data_ptr(),
+                                                                  conv.att_src.grad.data_ptr(),
+                                                                  conv.att_dst.grad.data_ptr(), conv.bias.grad.data_ptr())
+            b.gn_weight, b.gn_bias, b.gn_mean_scale = (norm.weight.data_ptr(), norm.bias.data_ptr(),
+                                                       norm.mean_scale.data_ptr())
+            b.g_gn_weight, b.g_gn_bias, b.g_gn_mean_scale = (norm.weight.grad.data_ptr(), norm.bias.grad.data_ptr(),
+                                                             norm.mean_scale.grad.data_ptr())
+            b.gn_eps, b.slope = float(norm.eps), float(conv.negative_slope)
+            b.in_, b.out = conv.in_channels, conv.out_channels
+        self._native_key, self._native_md = key, m
+        return m
+
+    @staticmethod
+    def _csr_ref(dst, csr, ell=None, w=0) -> None:
+        dst.row_ptr, dst.col = csr.row_ptr.data_ptr(), csr.col.data_ptr()
+        dst.csc_ptr, dst.csc_slot, dst.csc_dst = (csr.csc_ptr.data_ptr(), csr.csc_slot.data_ptr(),
+                                                  csr.csc_dst.data_ptr())
+        dst.ell = ell.data_ptr() if ell is not None else None
+        dst.num_nodes, dst.num_edges, dst.ell_width = csr.num_nodes, csr.num_edges, w if ell is not None else 0
+
+    def _native_batch(self, prep, hard, soft, eps, keeps):
+        """vg_critic_batch of this batch (labels and draw specs None: sizes only)."""
+        mvx = prep.matched_voxel_x
+        seeds = self._seeds(prep)
+        if mvx.dtype != torch.float32 or not mvx.is_contiguous():
+            return None
+        b = _lib.VgCriticBatch()
+        b.n, b.feat = mvx.shape
+        b.classes = self.n_classes
+        b.mvx, b.real, b.seeds4 = mvx.data_ptr(), prep.onehot_f.data_ptr(), seeds.data_ptr()
+        csr = prep.csr
+        csr3 = csr.stacked(3)
+        self._csr_ref(b.g1, csr)
+        ell3, w3 = csr3.ell()
+        self._csr_ref(b.g3, csr3, ell3, w3)
+        if hard is not None:
+            seed, it, salt = eps
+            b.hard, b.soft = hard.data_ptr(), soft.data_ptr()
+            b.seed, b.iter, b.eps_salt = seed, it.data_ptr(), salt & 0xFFFFFFFF
+            for i, k in enumerate(keeps):
+                b.keep_salt[i] = int(k.salt) & 0xFFFFFFFF
+            dev = mvx.device
+            b.gp_counter = self._const(("gp_counter", dev),
+                                       lambda: torch.zeros(1, dtype=torch.int32, device=dev)).data_ptr()
+        return b
+
+    def _arena_for(self, model, batch, dev):
+        """(arena tensor, floats) holding the native engine's temporaries for
+        this batch, grown outside a capture (grown 25 % ahead); a replaced
+        arena is kept alive, since recorded graphs may still reference it.
+        None when it is too small and a capture is running."""
+        need = int(LIB.vg_critic_arena_floats(ctypes.byref(model), ctypes.byref(batch)))
+        if need < 0:
+            return None
+        cur = self.__dict__.get("_arena")
+        if cur is not None and cur[1] >= need and cur[0].device == dev:
+            return cur
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        floats = (need * 5 // 4 + 63) // 64 * 64
+        t = torch.empty(floats + 64, dtype=torch.float32, device=dev)
+        off = (-t.data_ptr() % 256) // 4  # 256-byte aligned base
+        if cur is not None:
+            self.__dict__.setdefault("_old_arenas", []).append(cur)
+        self._arena = (t, floats, t.data_ptr() + 4 * off)
+        return self._arena
+
+    def _native(self, prep, hard, soft, keeps, eps, dev, st):
+        """loss_and_grad through vg_critic_loss_and_grad, or None (the
+        configuration or this batch is not the native engine's)."""
+        n = prep.matched_voxel_x.shape[0]
+        if not self._native_config_ok(n) or isinstance(eps, torch.Tensor) or eps is None:
+            return None
+        if len(keeps) != len(self.blocks) or any(k is None or isinstance(k, torch.Tensor) for k in keeps):
+            return None
+        seed, it, _ = eps
+        if any(k.seed != seed or k.iter is not it for k in keeps):
+            return None
+        model = self._native_model()
+        if model is None:
+            return None
+        batch = self._native_batch(prep, hard, soft, eps, keeps)
+        if batch is None:
+            return None
+        arena = self._arena_for(model, batch, dev)
+        if arena is None:
+            return None
+        out = _f(2, dev=dev)
+        check(LIB.vg_critic_loss_and_grad(ctypes.byref(model), ctypes.byref(batch), arena[2], arena[1], ptr(out), st),
+              "vg_critic_loss_and_grad")
+        self.native_calls = self.__dict__.get("native_calls", 0) + 1
+        self.last_gp = out[1]
+        return out[0]
 
     def _keeps(self, rng, n: int, dev, training: bool):
         """Dropout multipliers [3N, C_b] per block and eps [N, 1], drawn in the
@@ -165,6 +325,10 @@ class CriticEngine:
         keeps, eps = self._keeps(rng, n, dev, D.training)
         if isinstance(eps, torch.Tensor):
             eps = eps.reshape(n).contiguous()
+        else:  # the launches below, issued from C++ (vg_critic_loss_and_grad)
+            loss = self._native(prep, hard, soft, keeps, eps, dev, st)
+            if loss is not None:
+                return loss
         nb, nd, nm = len(self.blocks), len(self.dec), len(self.mlp)
         # parameter-gradient folds of passes C and D, run as one batch at the end
         folds = FoldCollector()
@@ -322,16 +486,7 @@ class CriticEngine:
             raise ValueError("the critic must output one score per node")
 
         # adjoint buffers of pass D (rows [0,3N)) whose rows [3N,4N) pass B fills
-        def make_seeds():  # [-1/N real | +1/N fake | 0 mix | 1 pass-B seed]
-            s_ = torch.zeros(X4, 1, dtype=torch.float32, device=dev)
-            s_[:n] = -1.0 / n
-            s_[n:2 * n] = 1.0 / n
-            s_[3 * n:] = 1.0
-            return s_
-
-        seeds = prep.consts.get("critic_seeds4")
-        if seeds is None:
-            seeds = prep.consts["critic_seeds4"] = make_seeds()
+        seeds = self._seeds(prep)
         adj_dec = [_f(X4, l.out_features, dev=dev) for l in self.dec[:-1]] + [seeds]
         adj_H = [_f(X4, B["c"], dev=dev) for B in blk]
         adj_mlp = [_f(X4, l.out_features, dev=dev) for l in self.mlp]

@@ -937,6 +937,97 @@ int vg_graph_exec_update(void* exec, void* graph);
 /* hipGraphLaunch(exec, stream). */
 int vg_graph_launch(void* exec, void* stream);
 
+/* ---- the critic iteration as one native call (host orchestration) -------- */
+
+/* The WGAN-GP critic loss and discriminator gradient of ONE critic iteration
+ * -- _compute_discriminator_loss followed by d_loss.backward()
+ * (trainer.py:291-332, :476-479) -- issued from C++: the same ~165 launches
+ * of the same kernels, in the same order and with the same arguments, as
+ * vgan/critic.py's CriticEngine.loss_and_grad in its default configuration
+ * (device-drawn dropout and GP eps, GraphNorm partials from the GAT
+ * aggregation and the producing GEMMs, grouped weight-gradient products and
+ * deferred folds), so results are bit-identical to it.  The Python engine
+ * spends ~10 us of interpreter time per launch (argument marshalling, buffer
+ * allocation); this one ~1-2 us, which is what a fresh batch's recording
+ * (Trainer.step_fresh) and an eager critic iteration pay.
+ *
+ * Model: the discriminator's parameters and their gradient buffers (views of
+ * the flat buffers, fixed for the model's life).  Batch: the prepared batch
+ * (vgan.data.prepared: matched voxel features, float one-hot, the single and
+ * 3-copy stacked CSR / CSC / padded columns, the adjoint seeds), the labels
+ * and the device-RNG draw specs.  Every temporary lives in `arena` (float
+ * offsets 256-byte aligned; vg_critic_arena_floats says how many); the
+ * caller keeps it alive while any recorded graph may replay launches that
+ * reference it, and runs nothing else on it concurrently.  Gradients are
+ * ACCUMULATED; out[0] = d_loss, out[1] = the gradient penalty. */
+#define VG_CRITIC_MAX_LAYERS 8
+
+typedef struct {
+  const float* weight; /* [out][in] */
+  const float* bias;   /* [out] */
+  float* g_weight;
+  float* g_bias;
+  int32_t in, out;
+} vg_critic_linear;
+
+typedef struct {
+  const float* lin_weight; /* GATConv.lin [out][in] */
+  const float* att_src;
+  const float* att_dst;
+  const float* bias;
+  float* g_lin_weight;
+  float* g_att_src;
+  float* g_att_dst;
+  float* g_bias;
+  const float* gn_weight; /* GraphNorm */
+  const float* gn_bias;
+  const float* gn_mean_scale;
+  float* g_gn_weight;
+  float* g_gn_bias;
+  float* g_gn_mean_scale;
+  float gn_eps, slope;
+  int32_t in, out;
+} vg_critic_block;
+
+typedef struct {
+  int32_t n_mlp, n_blocks, n_dec;
+  int32_t bf16; /* dense products on bf16 operands (the *_bf16 entry points) */
+  float lambda_gp, p_drop;
+  vg_critic_linear mlp[VG_CRITIC_MAX_LAYERS];
+  vg_critic_block block[VG_CRITIC_MAX_LAYERS];
+  vg_critic_linear dec[VG_CRITIC_MAX_LAYERS];
+} vg_critic_model;
+
+typedef struct {
+  const int32_t* row_ptr;
+  const int32_t* col;
+  const int32_t* csc_ptr;
+  const int32_t* csc_slot;
+  const int32_t* csc_dst;
+  const int32_t* ell; /* NULL: none */
+  int32_t num_nodes, num_edges, ell_width;
+} vg_csr_ref;
+
+typedef struct {
+  int32_t n, feat, classes; /* nodes per copy, matched-feature width, K */
+  const float* mvx;         /* [n][feat] */
+  const float* real;        /* [n][K] float one-hot */
+  const float* hard;        /* [n][K] */
+  const float* soft;        /* [n][K] */
+  const float* seeds4;      /* [4n]: -1/n | 1/n | 0 | 1 */
+  vg_csr_ref g1;            /* the batch graph */
+  vg_csr_ref g3;            /* its 3-copy block-diagonal stack (real / fake / mix) */
+  uint64_t seed;            /* device RNG: seed, iteration counter, salts */
+  const int64_t* iter;
+  uint32_t eps_salt;
+  uint32_t keep_salt[VG_CRITIC_MAX_LAYERS];
+  int32_t* gp_counter; /* a zeroed int32 the GP head leaves at 0 */
+} vg_critic_batch;
+
+int64_t vg_critic_arena_floats(const vg_critic_model* model, const vg_critic_batch* batch);
+int vg_critic_loss_and_grad(const vg_critic_model* model, const vg_critic_batch* batch, float* arena,
+                            int64_t arena_floats, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -12,6 +12,8 @@ Trainer._train_batch -> step_fresh), each timed between device syncs:
             graph, one upload)
   staged    the prepared batches collated and uploaded before the timed
             region (each batch still new to the trainer: capture inside it)
+  sync      staged, with a device synchronisation after every step (the
+            device time of a step without host work overlapping it)
   switch    prepared, with the default 5 ms GIL switch interval (the loader
             lowers it to 0.1 ms while prefetching, vgan/loader.py)
 
@@ -34,6 +36,8 @@ sys.path.insert(0, os.path.join(ROOT, "building-gan-graph-conditioned-architectu
 
 import torch  # noqa: E402
 
+TIMELINE = os.environ.get("FRESH_TIMELINE", "0") == "1"  # events at the phase marks (device lag per phase)
+
 
 def run(variant, cfg, bench, dev, steps, warmup, batch=32):
     from vgan.loader import GraphLoader
@@ -53,7 +57,7 @@ def run(variant, cfg, bench, dev, steps, warmup, batch=32):
     old = vl._SWITCH_INTERVAL
     if variant == "switch":
         vl._SWITCH_INTERVAL = 5e-3
-    if variant == "staged":
+    if variant in ("staged", "sync"):
         batches = list(loader)
         torch.cuda.synchronize()
         it = iter(batches)
@@ -65,19 +69,30 @@ def run(variant, cfg, bench, dev, steps, warmup, batch=32):
     phases = {}
     last = [0.0]
 
+    timeline = []  # (phase, host time at its end, event recorded there)
+
     def mark(name):
         t = time.perf_counter()
         phases.setdefault(name, []).append((t - last[0]) * 1e3)
         last[0] = t
+        if TIMELINE:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            timeline.append((name, t, ev))
 
     tr.phase_hook = mark
     time.sleep(0.05)  # a >= 40 ms idle gap: tools/prof_summary.py --after-gap keeps what follows
+    ref = torch.cuda.Event(enable_timing=True)
+    ref.record()  # the device is idle: it reaches ref at ~host time t_ref
+    t_ref = time.perf_counter()
     per = []
     t0 = time.perf_counter()
     for _ in range(steps):
         a = time.perf_counter()
         last[0] = a
         tr._train_batch(*next(it))
+        if variant == "sync":  # no host / device overlap: each step's device time alone
+            torch.cuda.synchronize()
         per.append((time.perf_counter() - a) * 1e3)
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / steps * 1e3
@@ -85,10 +100,26 @@ def run(variant, cfg, bench, dev, steps, warmup, batch=32):
     del it, loader
     shutil.rmtree(tmp, ignore_errors=True)
     tr.phase_hook = None
+    lag = {}
+    if TIMELINE:
+        # device time at which each phase-end marker executed, minus the host
+        # time it was enqueued: ~0 = the device had caught up with the host
+        # there (it idled before); large = work was queued ahead of it
+        for name, t, ev in timeline:
+            dev_ms = ref.elapsed_time(ev)
+            lag.setdefault(name, []).append(dev_ms - (t - t_ref) * 1e3)
+        lag = {k: {"median": round(sorted(v)[len(v) // 2], 3), "min": round(min(v), 3)} for k, v in lag.items()}
+        # device time between consecutive markers = the device time of the work
+        # enqueued in that phase, when the device never idled (lag stays > 0)
+        dd = {}
+        for (n0, _, e0), (n1, _, e1) in zip(timeline, timeline[1:]):
+            dd.setdefault(n1, []).append(e0.elapsed_time(e1))
+        lag["device_ms_per_phase"] = {k: round(sorted(v)[len(v) // 2], 3) for k, v in dd.items()}
     per.sort()
     med = {k: round(sorted(v)[len(v) // 2], 3) for k, v in phases.items()}
     return {"variant": variant, "ms_per_step": round(el, 3), "host_call_ms_median": round(per[len(per) // 2], 3),
-            "host_call_ms_max": round(per[-1], 3), "phase_ms_median": med}
+            "host_call_ms_max": round(per[-1], 3), "phase_ms_median": med,
+            **({"device_lag_ms": lag} if TIMELINE else {})}
 
 
 def main():
