@@ -465,6 +465,68 @@ class Trainer:
         with gemm_precision_scope(self.precision):
             return self._step_fresh(local_graph, voxel_graph)
 
+    def _fresh_record(self, fn):
+        """(recorded graph, fn's result): fn's launches recorded -- not run --
+        on the fresh path's side stream into its memory pool.
+        torch.cuda.graph() would synchronise the device, collect garbage and
+        empty the allocator cache on every capture: the low-level calls
+        record without any of that.  Thread-local capture mode: the loader's
+        thread keeps collating into pinned buffers and uploading meanwhile."""
+        dev = torch.cuda.current_device()
+        pool = getattr(self, "_fresh_pool", None)
+        if pool is None:
+            pool = self._fresh_pool = torch.cuda.graph_pool_handle()
+        side = getattr(self, "_fresh_stream", None)
+        if side is None:
+            side = self._fresh_stream = torch.cuda.Stream(dev)
+        cur = torch.cuda.current_stream(dev)
+        g = torch.cuda.CUDAGraph(keep_graph=True)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            g.capture_begin(pool=pool, capture_error_mode="thread_local")
+            try:
+                out = fn()
+            finally:
+                g.capture_end()
+        cur.wait_stream(side)
+        return g, out
+
+    def _fresh_exec(self, kind: str, g) -> ctypes.c_void_p:
+        """The executable graph that replays recording ``g`` of graph kind
+        ``kind`` (step_fresh: "critic").  Two executable graphs per kind,
+        used by alternate batches, are updated in place from each new
+        recording (vg_graph_exec_update) -- instantiating a graph per batch
+        and destroying the previous one cost ~3 ms of host time per step.  An
+        update rewrites an executable graph's kernel arguments, and HIP does
+        not promise that launches of it already queued keep the old ones, so
+        an executable graph is updated only after its last launches -- two
+        batches back -- have finished (a host wait on the event recorded
+        behind them by _fresh_done; the device is normally less than one
+        batch behind the host, so the wait rarely stalls)."""
+        st = self.__dict__.setdefault("_fresh_state", {})
+        k = st.setdefault(kind, {"owners": [None, None], "events": [None, None], "parity": 1})
+        j = k["parity"] = (k["parity"] + 1) % 2
+        owner = k["owners"][j]
+        if k["events"][j] is not None:
+            k["events"][j].synchronize()
+        if owner is None or not _FRESH_UPDATE or \
+                LIB.vg_graph_exec_update(ctypes.c_void_p(owner.raw_cuda_graph_exec()),
+                                         ctypes.c_void_p(g.raw_cuda_graph())) != 0:
+            g.instantiate()  # first batches, or a launch sequence of another shape
+            if owner is not None:
+                self.__dict__.setdefault("_fresh_dead", []).append(owner)
+            owner = k["owners"][j] = g
+        elif g is not owner:
+            self.__dict__.setdefault("_fresh_dead", []).append(g)
+        return ctypes.c_void_p(owner.raw_cuda_graph_exec())
+
+    def _fresh_done(self, kind: str, stream) -> None:
+        """Record the event behind the last launch of ``kind``'s current
+        executable graph (see _fresh_exec)."""
+        k = self._fresh_state[kind]
+        ev = k["events"][k["parity"]] = torch.cuda.Event()
+        ev.record(stream)
+
     def _step_fresh(self, local_graph, voxel_graph) -> Dict[str, torch.Tensor]:
         cfg = self.configuration
         dev = voxel_graph.x.device
@@ -481,26 +543,18 @@ class Trainer:
             self.critic.prepare_batch(prep)
         self.adam_g.sync_lr()
         self.adam_d.sync_lr()
-        mark("prepare")
         acc = torch.zeros(n_critic + 1, dtype=torch.float32, device=dev)
         cur = torch.cuda.current_stream(dev)
+        st = stream_handle(dev)
         warm = getattr(self, "_fresh_warm", False)
-        if warm:
-            # The critic graph is recorded BEFORE the label forward is enqueued:
-            # the recording (~2 ms of host time) then overlaps the device's
-            # work on the previous step's generator iteration, where after the
-            # label forward the device idled through most of it.  The recorded
-            # body reads its labels from the slot at replay time and draws
-            # from the device counter at replay time, so the order of
-            # recording and enqueueing changes no value.
-            hard_all = soft_all = None
-            n_nodes, k_cls = voxel_graph.num_nodes, cfg.NUM_CLASSES
-            slot = (torch.empty((1, n_nodes, k_cls), dtype=torch.float32, device=dev),
-                    torch.empty((1, n_nodes, k_cls), dtype=torch.float32, device=dev))
-        else:
-            hard_all, soft_all = self._critic_labels(local_graph, voxel_graph)
-            mark("labels")
-            slot = (torch.empty_like(hard_all[0:1]), torch.empty_like(soft_all[0:1]))
+        mark("prepare")
+        # the label forward and the generator iteration run eagerly: each runs
+        # once per batch, so recording them costs the host what launching
+        # them does -- measured no faster recorded
+        hard_all, soft_all = self._critic_labels(local_graph, voxel_graph)
+        mark("labels")
+        slot = (torch.empty_like(hard_all[0:1]), torch.empty_like(soft_all[0:1]))
+        if not warm:
             # first capture of this trainer: run the body once outside any
             # capture (lazy initialisation, constant buffers), then undo it
             self.rng._iter(dev)
@@ -510,60 +564,11 @@ class Trainer:
             self._critic_body(local_graph, voxel_graph, acc, with_adam, slot, 0, sync)
             self._restore(snap)
             self._fresh_warm = True
-        pool = getattr(self, "_fresh_pool", None)
-        if pool is None:
-            pool = self._fresh_pool = torch.cuda.graph_pool_handle()
-        side = getattr(self, "_fresh_stream", None)
-        if side is None:
-            side = self._fresh_stream = torch.cuda.Stream(dev)
-        # torch.cuda.graph() would synchronise the device, collect garbage and
-        # empty the allocator cache on every capture: the low-level calls
-        # record without any of that.  The recorded graph is kept
-        # uninstantiated: it updates the one executable graph in place
-        # (vg_graph_exec_update) -- instantiating a graph per batch and
-        # destroying the previous one cost ~3 ms of host time per step
-        g = torch.cuda.CUDAGraph(keep_graph=True)
-        side.wait_stream(cur)
-        with torch.cuda.stream(side):
-            # thread-local capture mode: the loader's thread keeps collating into
-            # pinned buffers and uploading while this thread records
-            g.capture_begin(pool=pool, capture_error_mode="thread_local")
-            try:
-                self._critic_body(local_graph, voxel_graph, acc, with_adam, slot, 0, sync)
-            finally:
-                g.capture_end()
-        cur.wait_stream(side)
-        # Two executable graphs, used by alternate batches.  An update rewrites
-        # an executable graph's kernel arguments, and HIP does not promise that
-        # launches of it already queued keep the old ones (its kernel arguments
-        # may live in device memory written at update time), so an executable
-        # graph is updated only after its last launches -- two batches back --
-        # have finished (a host wait on the event recorded behind them; the
-        # device is normally less than one batch behind the host, so the wait
-        # rarely stalls)
-        owners = self.__dict__.setdefault("_fresh_owners", [None, None])
-        events = self.__dict__.setdefault("_fresh_events", [None, None])
-        j = self._fresh_parity = (getattr(self, "_fresh_parity", 1) + 1) % 2
-        owner = owners[j]
-        if events[j] is not None:
-            events[j].synchronize()
-        if owner is None or not _FRESH_UPDATE or \
-                LIB.vg_graph_exec_update(ctypes.c_void_p(owner.raw_cuda_graph_exec()),
-                                         ctypes.c_void_p(g.raw_cuda_graph())) != 0:
-            g.instantiate()  # first batches, or a launch sequence of another shape
-            if owner is not None:
-                self.__dict__.setdefault("_fresh_dead", []).append(owner)
-            owner = owners[j] = g
-        exec_ = ctypes.c_void_p(owner.raw_cuda_graph_exec())
+        g_crit, _ = self._fresh_record(
+            lambda: self._critic_body(local_graph, voxel_graph, acc, with_adam, slot, 0, sync))
+        exec_ = self._fresh_exec("critic", g_crit)
         mark("capture")
-        if hard_all is None:
-            hard_all, soft_all = self._critic_labels(local_graph, voxel_graph)
-            if hard_all.dtype != slot[0].dtype or hard_all.shape[1:] != slot[0].shape[1:] \
-                    or soft_all.dtype != slot[1].dtype:
-                raise RuntimeError("critic label slot of an unexpected shape / dtype")
-            mark("labels")
         d_losses = torch.empty(n_critic, dtype=torch.float32, device=dev)
-        st = stream_handle(dev)
         for i in range(n_critic):
             slot[0].copy_(hard_all[i:i + 1])
             slot[1].copy_(soft_all[i:i + 1])
@@ -572,8 +577,7 @@ class Trainer:
             if not with_adam:
                 self.sync.all_reduce_grad(self.flat_d)
                 self.adam_d.step(counted=True)
-        ev = events[j] = torch.cuda.Event()
-        ev.record(cur)  # behind this batch's last launch of owners[j]
+        self._fresh_done("critic", cur)
         mark("replays")
         g_loss, hard = self._gen_iteration_synced(local_graph, voxel_graph)
         self.adam_g.step(counted=True)
@@ -583,15 +587,12 @@ class Trainer:
         # (tools/graph_destroy_probe.py; ~0.3 ms on an idle device), so they
         # are kept until _FRESH_KEEP have gathered and destroyed after one
         # device synchronisation
-        if g is not owner:
-            dead = self.__dict__.setdefault("_fresh_dead", [])
-            dead.append(g)
-            if len(dead) >= _FRESH_KEEP:
-                torch.cuda.synchronize(dev)
-                dead.clear()
+        dead = self.__dict__.setdefault("_fresh_dead", [])
+        if len(dead) >= _FRESH_KEEP:
+            torch.cuda.synchronize(dev)
+            dead.clear()
         mark("release")
         return {"d_losses": d_losses, "g_loss": g_loss.detach(), "label_hard": hard.detach()}
-
 
     # ------------------------------------------------------ orchestration
     # The epoch loop of trainer.py:445-520 (train), :522-577 (validation),

@@ -63,7 +63,27 @@ def main():
         tr._gen_iteration(loc, vox)
         tr.adam_g.step(counted=True)
 
+    # the critic iteration as step_fresh records it (raw capture into the fresh
+    # pool, executable graph instantiated / updated in place, vg_graph_launch)
+    from vgan._lib import LIB, check, stream_handle
+
+    with torch.no_grad():
+        hard_all, soft_all = tr._critic_labels(loc, vox)
+    slot = (hard_all[0:1].clone(), soft_all[0:1].clone())
+    acc = torch.zeros(cfg.N_CRITIC + 1, device=dev)
+    execs = []
+    for _ in range(3):  # the first instantiates, the next two update in place (ping-pong)
+        g_c, _ = tr._fresh_record(lambda: tr._critic_body(loc, vox, acc, True, slot, 0, False))
+        execs.append(tr._fresh_exec("critic", g_c))
+        tr._fresh_done("critic", torch.cuda.current_stream())
+    st = stream_handle(dev)
+
+    def fresh_critic(ex):
+        return lambda: check(LIB.vg_graph_launch(ex, st), "vg_graph_launch")
+
     res = {
+        "critic_fresh_instantiated_ms": timed(fresh_critic(execs[0])),
+        "critic_fresh_updated_ms": timed(fresh_critic(execs[2])),
         "labels_eager_ms": timed(eager_labels),
         "labels_graph_ms": timed(lambda: graphs["labels"].replay()),
         "gen_eager_ms": timed(eager_gen),

@@ -14,6 +14,9 @@ Trainer._train_batch -> step_fresh), each timed between device syncs:
             region (each batch still new to the trainer: capture inside it)
   sync      staged, with a device synchronisation after every step (the
             device time of a step without host work overlapping it)
+  quiet     staged, the host waiting for the device after the labels, the
+            critic replays and the generator iteration (no host activity
+            while they run)
   switch    prepared, with the default 5 ms GIL switch interval (the loader
             lowers it to 0.1 ms while prefetching, vgan/loader.py)
 
@@ -57,7 +60,7 @@ def run(variant, cfg, bench, dev, steps, warmup, batch=32):
     old = vl._SWITCH_INTERVAL
     if variant == "switch":
         vl._SWITCH_INTERVAL = 5e-3
-    if variant in ("staged", "sync"):
+    if variant in ("staged", "sync", "quiet"):
         batches = list(loader)
         torch.cuda.synchronize()
         it = iter(batches)
@@ -79,6 +82,8 @@ def run(variant, cfg, bench, dev, steps, warmup, batch=32):
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
             timeline.append((name, t, ev))
+        if variant == "quiet" and name in ("labels", "replays", "gen"):
+            torch.cuda.synchronize()  # the host idles while those phases run
 
     tr.phase_hook = mark
     time.sleep(0.05)  # a >= 40 ms idle gap: tools/prof_summary.py --after-gap keeps what follows
