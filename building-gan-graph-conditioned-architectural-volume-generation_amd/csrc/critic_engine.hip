@@ -11,7 +11,6 @@
 // cost per launch changes (Python: marshalling + one torch allocation per
 // temporary; here: a bump allocator over the caller's arena).  Host code
 // only: every launch goes through the library's own extern "C" entry points.
-#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <algorithm>
@@ -29,20 +28,6 @@ struct Ctx {
   void* stream;
   float* base;
   int64_t cap, off;
-  void* side = nullptr;  // the weight-gradient branch (NULL: none)
-  std::vector<hipEvent_t> events;
-
-  // fork: `to` waits for everything enqueued on `from` so far
-  int fork(void* from, void* to) {
-    hipEvent_t e;
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return VG_EINVAL;
-    events.push_back(e);
-    if (hipEventRecord(e, static_cast<hipStream_t>(from)) != hipSuccess) return VG_EINVAL;
-    return hipStreamWaitEvent(static_cast<hipStream_t>(to), e, 0) == hipSuccess ? 0 : VG_EINVAL;
-  }
-  ~Ctx() {
-    for (hipEvent_t e : events) (void)hipEventDestroy(e);
-  }
 
   // 256-byte aligned temporaries (the quad / float4 kernel forms need 16 B)
   float* take(int64_t floats) {
@@ -77,7 +62,6 @@ struct Ctx {
 struct Folds {
   std::vector<vg_fold> folds;
   std::vector<vg_tn> prods;  // planned, not yet launched
-  bool branched = false;     // products launched on the side stream
 
   void add(const vg_fold* f, int n) { folds.insert(folds.end(), f, f + n); }
 
@@ -110,25 +94,10 @@ struct Folds {
     return 0;
   }
 
-  // The products planned so far, launched on the side stream once their
-  // operands are complete on the main stream (everything enqueued there so
-  // far): they run beside the rest of the backward -- latency-bound kernels
-  // that leave most of the chip idle -- instead of after it.  Each product
-  // writes only its own partials; the folds still run at flush, in the same
-  // order: bit-identical.
-  int branch(Ctx& cx) {
-    if (cx.dry || !cx.side || prods.empty()) return 0;
-    const int rc = cx.fork(cx.stream, cx.side);
-    if (rc) return rc;
-    branched = true;
-    return launch_products(cx.side);
-  }
-
   int flush(Ctx& cx) {
     if (cx.dry) return 0;
     int rc = launch_products(cx.stream);  // the products first: their partials feed the folds
     if (rc) return rc;
-    if (branched && (rc = cx.fork(cx.side, cx.stream))) return rc;  // join the branch
     // folds into one destination merge into a two-source fold (applied in
     // call order); one that cannot merge starts a new batch, so the two never race
     std::vector<std::vector<vg_fold>> batches;
@@ -482,7 +451,6 @@ int run(Ctx& cx, const vg_critic_model* md, const vg_critic_batch* bt, float* ou
       VG_TRY(gemm_dy(adj_dec[0], aw, L.weight, m, dY, R, m, aw, nb - 1, false, &tp));
     }
   }
-  VG_TRY(folds.branch(cx));  // the decoder's weight gradients beside the encoder's backward
   for (int b = nb - 1; b >= 0; --b) {
     const vg_critic_block& B = md->block[b];
     const Blk& S = blk[b];
@@ -500,7 +468,6 @@ int run(Ctx& cx, const vg_critic_model* md, const vg_critic_batch* bt, float* ou
       folds.add(f, nf);
     }
     VG_TRY(gemm_tn(adj_H[b], c, S.X, cin, X4, c, cin, B.g_lin_weight, cin, nullptr, X4));
-    VG_TRY(folds.branch(cx));  // block b's projection weight gradient beside blocks b-1..0
     if (b > 0) {
       dY = cx.take((int64_t)R * cin);
       VG_TRY(gemm_dy(adj_H[b], c, B.lin_weight, cin, dY, R, cin, c, b - 1, false, &tp));
@@ -555,7 +522,7 @@ extern "C" int64_t vg_critic_arena_floats(const vg_critic_model* model, const vg
 }
 
 extern "C" int vg_critic_loss_and_grad(const vg_critic_model* model, const vg_critic_batch* batch, float* arena,
-                                       int64_t arena_floats, float* out, void* stream, void* side_stream) {
+                                       int64_t arena_floats, float* out, void* stream) {
   if (!model_ok(model, batch) || !arena || !out || !batch->mvx || !batch->real || !batch->hard || !batch->soft ||
       !batch->seeds4 || !batch->iter || !batch->gp_counter)
     return VG_EINVAL;
@@ -563,6 +530,5 @@ extern "C" int vg_critic_loss_and_grad(const vg_critic_model* model, const vg_cr
   const int64_t need = vg_critic_arena_floats(model, batch);
   if (need < 0 || need > arena_floats) return VG_EINVAL;
   Ctx cx{false, model->bf16, stream, arena, arena_floats, 0};
-  cx.side = side_stream != stream ? side_stream : nullptr;
   return run(cx, model, batch, out);
 }

@@ -248,7 +248,7 @@ SIGNATURES = {
     "vg_graph_launch": (ctypes.c_int, [_c_p, _c_p]),
     "vg_critic_arena_floats": (ctypes.c_int64, [ctypes.POINTER(VgCriticModel), ctypes.POINTER(VgCriticBatch)]),
     "vg_critic_loss_and_grad": (ctypes.c_int, [ctypes.POINTER(VgCriticModel), ctypes.POINTER(VgCriticBatch), _c_p,
-                                               _c_i64, _c_p, _c_p, _c_p]),
+                                               _c_i64, _c_p, _c_p]),
     "vg_linear_chain_bf16": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p]),
     "vg_gat_gnp_rows": (_c_i32, [_c_i32, _c_i32]),
     "vg_gat_gnp_floats": (_c_i64, [_c_i32, _c_i32]),
@@ -494,7 +494,6 @@ class FoldCollector:
         self.keep = []
         self.products = []
         self.jvp_src = []
-        self.branched = None  # the side stream products were launched on (branch)
 
     def call(self, fn, args_before_stream, stream, keep=(), name="deferred"):
         arr = (VgFold * 3)()
@@ -568,26 +567,10 @@ class FoldCollector:
                 check(LIB.vg_gemm_tn_group(arr, len(part), stream), "vg_gemm_tn_group")
         self.products = []
 
-    def branch(self, side: "torch.cuda.Stream") -> None:
-        """Launch the products planned so far on ``side``, after everything
-        enqueued on the current stream (their operands): a branch beside the
-        rest of the backward -- latency-bound kernels that leave most of the
-        chip idle -- joined by flush() before the folds.  Each product writes
-        only its own partials and the folds run in the same order, so the
-        result is bit-identical; ``keep`` holds the operands until flush."""
-        if not self.products:
-            return
-        side.wait_stream(torch.cuda.current_stream(side.device))
-        self._launch_products(side.cuda_stream)
-        self.branched = side
-
     def flush(self, stream) -> None:
         self.run_jvp_src(stream)  # (their att_src partials feed folds)
         # the grouped products first: their partials feed the folds
         self._launch_products(stream)
-        if self.branched is not None:  # join the branch (``stream`` is the current stream)
-            torch.cuda.current_stream(self.branched.device).wait_stream(self.branched)
-            self.branched = None
         batches, cur, where = [], [], {}
         for f in self.folds:
             j = where.get(f.out)

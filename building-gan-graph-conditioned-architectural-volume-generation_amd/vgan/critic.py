@@ -54,9 +54,6 @@ _GN_FUSE = os.environ.get("VGAN_GN_FUSE", "1") == "1"
 # instead of vg_critic_loss_and_grad (the same launches issued from C++,
 # bit-identical; include/vgan.h) -- A/B and parity knob
 _NATIVE = os.environ.get("VGAN_NATIVE_CRITIC", "1") == "1"
-# VGAN_CRITIC_BRANCH=0: the native engine's weight-gradient products after
-# the final backward pass instead of on a side-stream branch beside it
-_NATIVE_BRANCH = os.environ.get("VGAN_CRITIC_BRANCH", "0") == "1"
 
 
 def _f(*shape, dev):
@@ -253,14 +250,8 @@ class CriticEngine:
         if arena is None:
             return None
         out = _f(2, dev=dev)
-        side = None
-        if _NATIVE_BRANCH:
-            s_ = self.__dict__.get("_tn_stream")
-            if s_ is None or s_.device != dev:
-                s_ = self._tn_stream = torch.cuda.Stream(dev)
-            side = s_.cuda_stream
-        check(LIB.vg_critic_loss_and_grad(ctypes.byref(model), ctypes.byref(batch), arena[2], arena[1], ptr(out), st,
-                                          side), "vg_critic_loss_and_grad")
+        check(LIB.vg_critic_loss_and_grad(ctypes.byref(model), ctypes.byref(batch), arena[2], arena[1], ptr(out), st),
+              "vg_critic_loss_and_grad")
         self.native_calls = self.__dict__.get("native_calls", 0) + 1
         self.last_gp = out[1]
         return out[0]

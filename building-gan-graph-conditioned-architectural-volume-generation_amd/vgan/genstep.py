@@ -35,7 +35,6 @@ differs only in the summation grouping of fused reductions
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import List
 
 import torch
@@ -45,10 +44,6 @@ from . import data as vdata
 from . import ops
 from ._lib import _GN_ROWS, LIB, FoldCollector, VgGnBwdIn, check, dense, linear_chain, ptr, stream_handle, sync_counter
 from .critic import _GN_FUSE, ACT_MASK, ACT_NONE, ACT_RELU, _f, _off
-
-# VGAN_GEN_BRANCH=0: the generator iteration's weight-gradient products after
-# its backward instead of on a side-stream branch beside it (A/B knob)
-_BRANCH = os.environ.get("VGAN_GEN_BRANCH", "0") == "1"
 
 
 class GeneratorEngine:
@@ -236,16 +231,6 @@ class GeneratorEngine:
         return dH
 
     # ------------------------------------------------------------ engine
-    def _branch(self, folds: FoldCollector, dev) -> None:
-        """The weight-gradient products planned so far, on this engine's side
-        stream (FoldCollector.branch; VGAN_GEN_BRANCH=0: at the flush)."""
-        if not _BRANCH:
-            return
-        s_ = self.__dict__.get("_tn_stream")
-        if s_ is None or s_.device != dev:
-            s_ = self._tn_stream = torch.cuda.Stream(dev)
-        folds.branch(s_)
-
     def loss_and_grad(self, local_graph, voxel_graph, rng, early=None):
         """(g_loss device scalar, label_hard [1, N, K]) of trainer.py:483-490;
         the generator's gradients are added to its .grad.  ``early``: called
@@ -421,8 +406,6 @@ class GeneratorEngine:
         if early is not None:  # the decoder's gradient complete: its bucket can go
             folds.flush(st)
             early()
-        else:
-            self._branch(folds, dev)  # the decoder's weight gradients beside the encoders' backward
         g_y = g_enc
         g_x = None
         for b in range(len(genc) - 1, -1, -1):
@@ -431,7 +414,6 @@ class GeneratorEngine:
             dH = self._gat_bwd(folds, st, sy, dev, csr, B, g_y, tp, True)
             Wl = B["conv"].lin.weight
             self._tn(folds, st, dev, dH, c, B["X"], cin, n, c, cin, ptr(Wl.grad), cin)
-            self._branch(folds, dev)
             if b > 0:
                 g_y = _f(n, cin, dev=dev)
                 tp = self._gemm_dy(st, dev, ptr(dH), c, ptr(Wl), cin, g_y, n, cin, c, genc[b - 1])

@@ -1025,11 +1025,8 @@ typedef struct {
 } vg_critic_batch;
 
 int64_t vg_critic_arena_floats(const vg_critic_model* model, const vg_critic_batch* batch);
-/* side_stream (NULL or == stream: none): the weight-gradient products of the
- * final backward pass are launched on it as their operands complete -- a
- * branch beside the rest of that backward, joined before the folds. */
 int vg_critic_loss_and_grad(const vg_critic_model* model, const vg_critic_batch* batch, float* arena,
-                            int64_t arena_floats, float* out, void* stream, void* side_stream);
+                            int64_t arena_floats, float* out, void* stream);
 
 #ifdef __cplusplus
 }

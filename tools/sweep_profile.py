@@ -1,0 +1,110 @@
+"""Where the configs[4] stream sweep spends its time per batch.
+
+bench.py's sweep leg (InferenceSweep.run_stream over a GraphLoader of
+distinct synthetic buildings) timed three ways on the same store:
+
+  stream   the leg as the bench times it (loader thread prefetching)
+  loader   the loader alone: collate + upload per batch, no forward
+  staged   the same batches collated and uploaded first: run_fresh alone
+  device   one batch's stacked forward replayed from its graph: the device
+           time per batch
+plus a cProfile of run_fresh over the staged batches (host time per call).
+
+    python tools/sweep_profile.py [--graphs 3200] [--dtype f16]
+"""
+from __future__ import annotations
+
+import argparse
+import cProfile
+import io
+import json
+import os
+import pstats
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "building-gan-graph-conditioned-architectural-volume-generation_amd"))
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--graphs", type=int, default=3200)
+    ap.add_argument("--dtype", default="f16")
+    ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--threads", type=int, default=4, help="the loader's collate threads")
+    args = ap.parse_args()
+    from vgan.config import Configuration
+    from vgan.infer import InferenceSweep, geometric_taus
+    from vgan.loader import GraphLoader
+    from vgan.models import VoxelGNNGenerator
+    from vgan.store import write_store
+    from vgan.synth import SyntheticDataset
+
+    dev = torch.device("cuda", 0)
+    tmp = tempfile.mkdtemp(prefix="vgan_sweep_")
+    store = write_store(os.path.join(tmp, "store"), SyntheticDataset(args.graphs, seed=2024))
+    cfg = Configuration()
+    cfg.DEVICE = str(dev)
+    cfg.runtime["rng"] = "device"
+    torch.manual_seed(cfg.SEED)
+    G = VoxelGNNGenerator(cfg, 17, 12)
+    taus = geometric_taus(1.0, 0.1, 10)
+
+    def loader(idx=None):
+        return GraphLoader(store, idx, batch_size=32, shuffle=False, device=dev, prefetch=4,
+                           prepare=(cfg.NUM_CLASSES, ()), threads=args.threads)
+
+    sw = InferenceSweep(G, taus, dtype=args.dtype)
+    sw.run_stream(loader(list(range(4 * 32))))
+    torch.cuda.synchronize()
+    out = {"threads": args.threads}
+    t0 = time.perf_counter()
+    nb = sum(1 for _ in loader())
+    torch.cuda.synchronize()
+    out["loader_ms_per_batch"] = round((time.perf_counter() - t0) / nb * 1e3, 3)
+    t0 = time.perf_counter()
+    res = sw.run_stream(loader())
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    out["stream_ms_per_batch"] = round(el / res["batches"] * 1e3, 3)
+    batches = list(loader())
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for b in batches:
+        sw.run_fresh(*b)
+    torch.cuda.synchronize()
+    out["staged_ms_per_batch"] = round((time.perf_counter() - t0) / len(batches) * 1e3, 3)
+    # host time per run_fresh call (no synchronisation inside)
+    pr = cProfile.Profile()
+    t0 = time.perf_counter()
+    pr.enable()
+    for b in batches:
+        sw.run_fresh(*b)
+    pr.disable()
+    out["staged_host_ms_per_batch"] = round((time.perf_counter() - t0) / len(batches) * 1e3, 3)
+    torch.cuda.synchronize()
+    # device time of one batch's forward, replayed from a graph
+    sw2 = InferenceSweep(G, taus, graphed=True, dtype=args.dtype)
+    loc, vox = batches[0]
+    sw2.run_batch(loc, vox)
+    torch.cuda.synchronize()
+    a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(20):
+        sw2.run_batch(loc, vox)
+    e.record()
+    torch.cuda.synchronize()
+    out["device_ms_per_batch"] = round(a.elapsed_time(e) / 20, 3)
+    print(json.dumps(out), flush=True)
+    s = io.StringIO()
+    pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(args.top)
+    print(s.getvalue())
+
+
+if __name__ == "__main__":
+    main()
