@@ -105,7 +105,8 @@ def test_host_prepared_batch_equals_device_build(cuda, ds_store):
     assert "critic_seeds4" not in ref.consts
     from vgan.critic import CriticEngine as CE
 
-    CE.prepare_batch(None, ref)
+    CE._seeds(ref)  # the device build of prepare_batch's constants
+    ref.csr.stacked(3).ell()
     _same(prep.matched_voxel_x, ref.matched_voxel_x, "type-matched mean | voxel.x")
     _same(prep.matched_x, ref.matched_x, "matched_x")
     _same(prep.onehot_f, ref.onehot_f, "onehot_f")
