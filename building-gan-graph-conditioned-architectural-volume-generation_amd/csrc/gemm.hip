@@ -1918,19 +1918,22 @@ extern "C" int vg_gemm_bf16(const float* A, int32_t lda, const float* B, int32_t
 #define VG_TN_GROUP_TARGET 64  // with tn_tile_direct; step A/B over 16..192: profiles/r02_ab_tn_direct.txt
 #endif
 // (a product planned for vg_gemm_tn_group shares the grid with the other
-// products of its backward: VG_TN_GROUP_TARGET workgroups each, but chunks
-// of at most VG_TN_GROUP_MAX_ROWS rows.  Every workgroup of a group computes
-// one 64 x 64 tile over its chunk, so its time is set by the chunk's rows:
-// without the cap the generator's 128 x 524 input-layer product got 3 chunks
-// of 4,384 rows, 5x the rows of any other workgroup in its launch, and the
-// whole launch waited on those 54 workgroups.)
-#ifndef VG_TN_GROUP_MAX_ROWS
-#define VG_TN_GROUP_MAX_ROWS 832
+// products of its backward: VG_TN_GROUP_TARGET workgroups each, and at least
+// min(VG_TN_GROUP_TARGET, N / VG_TN_GROUP_MIN_ROWS) chunks whatever its
+// tile count.  Every workgroup of a group computes one 64 x 64 tile over its
+// chunk, so its time is set by the chunk's rows: the generator's 128 x 524
+// input-layer product got 3 chunks of 4,384 rows (5x the rows of any other
+// workgroup in its launch) and its 128 x 128 products 16 of 832, and the
+// launch waited on them.  The floor on chunks leaves the critic's products
+// (N = 52k rows, 64 x 64) at their 64 chunks: more chunks there cost more in
+// partials than they spread (profiles/r04_ab_tn_rows.txt).)
+#ifndef VG_TN_GROUP_MIN_ROWS
+#define VG_TN_GROUP_MIN_ROWS 416
 #endif
-static inline int tn_rows(int N, int M, int K, int wg_target = VG_TN_TARGET, int max_rows = 0) {
+static inline int tn_rows(int N, int M, int K, int wg_target = VG_TN_TARGET, int min_rows = 0) {
   const int tiles = ((M + TM - 1) / TM) * ((K + TN - 1) / TN);
   int target = wg_target / tiles;
-  if (max_rows > 0) target = max(target, (N + max_rows - 1) / max_rows);
+  if (min_rows > 0) target = max(target, min(wg_target, (N + min_rows - 1) / min_rows));
   if (target > 256) target = 256;
   if (target < 1) target = 1;
   int rows = (N + target - 1) / target;
@@ -1941,7 +1944,7 @@ static inline int tn_rows(int N, int M, int K, int wg_target = VG_TN_TARGET, int
 extern "C" int64_t vg_gemm_tn_ws_floats(int32_t N, int32_t M, int32_t K) {
   if (N <= 0) return 1;
   // enough for either plan: one launch per product or a grouped product
-  const int r = min(tn_rows(N, M, K), tn_rows(N, M, K, VG_TN_GROUP_TARGET, VG_TN_GROUP_MAX_ROWS));
+  const int r = min(tn_rows(N, M, K), tn_rows(N, M, K, VG_TN_GROUP_TARGET, VG_TN_GROUP_MIN_ROWS));
   const int64_t chunks = (N + r - 1) / r;
   return chunks * ((int64_t)M * K + M);
 }
@@ -2014,7 +2017,7 @@ static int gemm_tn_plan(const float* A, int32_t lda, const float* B, int32_t ldb
   if (!prod_out || !folds_out || !n_out || N <= 0 || M <= 0 || K <= 0 || ldc < K || !A || !B || !C ||
       !workspace || db_rows < 0)
     return VG_EINVAL;
-  const int rows = tn_rows(N, M, K, VG_TN_GROUP_TARGET, VG_TN_GROUP_MAX_ROWS);
+  const int rows = tn_rows(N, M, K, VG_TN_GROUP_TARGET, VG_TN_GROUP_MIN_ROWS);
   const int chunks = (N + rows - 1) / rows;
   float* part = workspace;
   float* pdb = workspace + (size_t)chunks * M * K;

@@ -8,7 +8,8 @@ distinct synthetic buildings) timed three ways on the same store:
   staged   the same batches collated and uploaded first: run_fresh alone
   device   one batch's stacked forward replayed from its graph: the device
            time per batch
-plus a cProfile of run_fresh over the staged batches (host time per call).
+plus a cProfile of run_fresh over the staged batches (host time per call)
+and of the loader's per-batch host collate (pinned, on this thread).
 
     python tools/sweep_profile.py [--graphs 3200] [--dtype f16]
 """
@@ -72,21 +73,36 @@ def main():
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     out["stream_ms_per_batch"] = round(el / res["batches"] * 1e3, 3)
+    # the loader's host collate alone, on this thread
+    plan = [list(range(i, i + 32)) for i in range(0, 32 * 50, 32)]
+    prep = (cfg.NUM_CLASSES, ())
+    for idx in plan[:3]:
+        store.collate(idx, pin=True, threads=args.threads, prepare=prep)
+    t0 = time.perf_counter()
+    for idx in plan:
+        store.collate(idx, pin=True, threads=args.threads, prepare=prep)
+    out["collate_ms_per_batch"] = round((time.perf_counter() - t0) / len(plan) * 1e3, 3)
+    pc = cProfile.Profile()
+    pc.enable()
+    for idx in plan:
+        store.collate(idx, pin=True, threads=args.threads, prepare=prep)
+    pc.disable()
     batches = list(loader())
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for b in batches:
-        sw.run_fresh(*b)
-    torch.cuda.synchronize()
-    out["staged_ms_per_batch"] = round((time.perf_counter() - t0) / len(batches) * 1e3, 3)
-    # host time per run_fresh call (no synchronisation inside)
-    pr = cProfile.Profile()
-    t0 = time.perf_counter()
-    pr.enable()
-    for b in batches:
-        sw.run_fresh(*b)
-    pr.disable()
-    out["staged_host_ms_per_batch"] = round((time.perf_counter() - t0) / len(batches) * 1e3, 3)
+    with sw._eval():  # as run_stream: eval mode set once
+        t0 = time.perf_counter()
+        for b in batches:
+            sw.run_fresh(*b)
+        torch.cuda.synchronize()
+        out["staged_ms_per_batch"] = round((time.perf_counter() - t0) / len(batches) * 1e3, 3)
+        # host time per run_fresh call (no synchronisation inside)
+        pr = cProfile.Profile()
+        t0 = time.perf_counter()
+        pr.enable()
+        for b in batches:
+            sw.run_fresh(*b)
+        pr.disable()
+        out["staged_host_ms_per_batch"] = round((time.perf_counter() - t0) / len(batches) * 1e3, 3)
     torch.cuda.synchronize()
     # device time of one batch's forward, replayed from a graph
     sw2 = InferenceSweep(G, taus, graphed=True, dtype=args.dtype)
@@ -101,9 +117,10 @@ def main():
     torch.cuda.synchronize()
     out["device_ms_per_batch"] = round(a.elapsed_time(e) / 20, 3)
     print(json.dumps(out), flush=True)
-    s = io.StringIO()
-    pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(args.top)
-    print(s.getvalue())
+    for name, prof in (("run_fresh", pr), ("collate", pc)):
+        s = io.StringIO()
+        pstats.Stats(prof, stream=s).sort_stats("tottime").print_stats(args.top)
+        print(f"--- {name}\n{s.getvalue()}")
 
 
 if __name__ == "__main__":
