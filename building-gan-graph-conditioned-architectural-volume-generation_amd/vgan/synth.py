@@ -26,6 +26,7 @@ types drawn from the ``analyze.py:100`` ratios, and a FAR that satisfies the
 """
 from __future__ import annotations
 
+import os
 from typing import List, Sequence, Tuple
 
 import numpy as np
@@ -219,7 +220,13 @@ class SyntheticDataset:
 def write_synthetic_store(path: str, size: int, seed: int = 777) -> None:
     """A GraphStore of ``size`` synthetic buildings (vgan.store.write_store over
     SyntheticDataset(size, seed)); the bench runs it in a child process while
-    the GPU legs run."""
+    the GPU legs run: one intra-op thread at a lowered priority, so that it
+    takes no more than a core from the host-bound legs it runs beside."""
     from .store import write_store
 
+    torch.set_num_threads(1)
+    try:
+        os.nice(10)
+    except OSError:
+        pass
     write_store(path, SyntheticDataset(size, seed=seed))
