@@ -693,6 +693,13 @@ def main():
     local_dev = local % n_dev
     torch.cuda.set_device(local_dev)
     device = torch.device("cuda", local_dev)
+    bound = None
+    if os.environ.get("VGAN_NUMA_BIND", "1") == "1":  # host threads on the GPU's NUMA node (vgan/affinity.py)
+        from vgan.affinity import bind_to_device_numa
+
+        bound = bind_to_device_numa(device)
+        log(f"host threads bound to the GPU's NUMA node: {len(bound)} CPUs" if bound else
+            "host threads not bound (NUMA topology unknown)")
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
@@ -772,7 +779,11 @@ def main():
     # what Trainer.train() delivers: a new batch from the native loader every step
     fresh = None
     if not args.no_fresh:
-        fresh = fresh_batch_leg(cfg, args.precision, args.steps, args.warmup, args.batch, device, rank, world)
+        # its own step counts: at ~8.5 ms a step, 20 steps after 5 warm-up
+        # ones spread 8.1-10.1 ms between runs on one box (host-bound leg;
+        # profiles/r04_fresh_ab.txt); 60 after 10 cost half a second
+        fresh = fresh_batch_leg(cfg, args.precision, max(args.steps, 60), max(args.warmup, 10), args.batch, device,
+                                rank, world)
         log(f"fresh batches (loader, step_fresh): {fresh['ms_per_step']:.2f} ms/step, {fresh['value']:.1f} graphs/s")
 
     result = None
@@ -813,6 +824,8 @@ def main():
                 "execution": ("hipGraph replay: one stacked no-grad G forward for the N_CRITIC critic labels, "
                               "N_CRITIC critic-engine graphs, one generator-iteration graph") if GRAPHED else "eager",
             },
+            "host": {"numa_bound_cpus": len(bound) if bound else None,
+                     "note": "host threads on the GPU's NUMA node (vgan.affinity; VGAN_NUMA_BIND=0: unbound)"},
             "roofline": {
                 "kernel": "vg_gat_aggregate_fwd_gnp (the scatter kernel as the step runs it: GAT edge softmax + "
                           "CSR gather-sum + bias, with the following GraphNorm's column partials in the epilogue)",
