@@ -444,21 +444,24 @@ def fresh_batch_leg(cfg, precision: str, steps: int, warmup: int, batch: int, de
     torch.manual_seed(cfg.SEED + rank)
     tr = build_trainer(cfg, precision)
     cfg.runtime["train_step"] = "auto"
+    from vgan.gcscope import gc_frozen
+
     it = iter(loader)
-    for _ in range(warmup):
-        loc, vox = next(it)
-        tr._train_batch(loc, vox)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        loc, vox = next(it)
-        tr._train_batch(loc, vox)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    with gc_frozen():  # as Trainer._train_each_epoch's batch loop
+        for _ in range(warmup):
+            loc, vox = next(it)
+            tr._train_batch(loc, vox)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            loc, vox = next(it)
+            tr._train_batch(loc, vox)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -778,6 +781,16 @@ def main():
             f"{gemms['achieved_tflops']:.2f} TFLOP/s, {gemms['achieved_gbs']:.0f} GB/s")
     # what Trainer.train() delivers: a new batch from the native loader every step
     fresh = None
+    if os.environ.get("VGAN_BENCH_RELEASE", "1") == "1":
+        # the replayed legs' trainers, batches and recorded graphs are done
+        # with (the fresh leg also runs its loop under vgan.gcscope.gc_frozen,
+        # as Trainer.train does: beside them, unfrozen, it took 10.6-11.4 ms)
+        del tr, pool, csr0
+        import gc
+
+        gc.collect()
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
     if not args.no_fresh:
         # its own step counts: at ~8.5 ms a step, 20 steps after 5 warm-up
         # ones spread 8.1-10.1 ms between runs on one box (host-bound leg;

@@ -25,6 +25,7 @@ from typing import Dict, Iterable, List, Optional, Sequence
 import torch
 
 from . import data as vdata
+from .gcscope import gc_frozen
 
 
 def geometric_taus(t0: float = 1.0, t1: float = 0.1, steps: int = 10) -> List[float]:
@@ -216,7 +217,7 @@ class InferenceSweep:
         and, with ``collect``, every batch's [k, N] predictions."""
         outs: List[torch.Tensor] = []
         graphs = samples = nb = 0
-        with self._eval():
+        with self._eval(), gc_frozen():  # vgan/gcscope.py
             for local_graph, voxel_graph in batches:
                 pred = self.run_fresh(local_graph, voxel_graph)
                 graphs += voxel_graph.num_graphs
@@ -235,7 +236,7 @@ class InferenceSweep:
         once at the end)."""
         outs: List[torch.Tensor] = []
         graphs = samples = 0
-        with self._eval():
+        with self._eval(), gc_frozen():  # vgan/gcscope.py
             for local_graph, voxel_graph in batches:
                 pred = self.run_batch(local_graph, voxel_graph)
                 graphs += voxel_graph.num_graphs

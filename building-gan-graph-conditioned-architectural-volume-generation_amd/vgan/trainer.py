@@ -45,6 +45,7 @@ from ._lib import LIB, check, gemm_precision_scope, ptr, stream_handle
 from .critic import CriticEngine
 from .dist import GradSync
 from .flat import FlatAdam, FlatParams
+from .gcscope import gc_frozen
 from .genstep import GeneratorEngine
 from .rng import RNG
 
@@ -686,12 +687,13 @@ class Trainer:
         precision, recall, accuracy)."""
         start = time.time()
         g_losses, d_losses, confs = [], [], []
-        for local_graph, voxel_graph in self.dataloaders.train_dataloader:
-            local_graph, voxel_graph = self._to_device(local_graph, voxel_graph)
-            out = self._train_batch(local_graph, voxel_graph)
-            d_losses.append(out["d_losses"])
-            g_losses.append(out["g_loss"])
-            confs.append(ops.confusion(voxel_graph.type, out["label_hard"].squeeze(0), voxel_graph.ptr))
+        with gc_frozen():  # the batch loop's GC passes skip everything alive before it (vgan/gcscope.py)
+            for local_graph, voxel_graph in self.dataloaders.train_dataloader:
+                local_graph, voxel_graph = self._to_device(local_graph, voxel_graph)
+                out = self._train_batch(local_graph, voxel_graph)
+                d_losses.append(out["d_losses"])
+                g_losses.append(out["g_loss"])
+                confs.append(ops.confusion(voxel_graph.type, out["label_hard"].squeeze(0), voxel_graph.ptr))
         metrics = self._read_confusions(confs)
         (g_mean, d_mean), (f1, prec, rec, acc), f1_min = self._epoch_figures(metrics, [g_losses, d_losses])
         print(f"The function _train_each_epoch took {time.time() - start} seconds to run.")
