@@ -260,9 +260,15 @@ class Trainer:
     def _overlap_ready(self) -> bool:
         """Overlap the generator's all-reduce with its backward: RCCL ranks
         (capturable, stream-ordered collectives), the explicit generator
-        schedule, runtime['overlap_allreduce'] (default on)."""
+        schedule, runtime['overlap_allreduce'] (default OFF).  Measured on one
+        GPU with the collectives recorded (tools/dp_overlap_probe.py,
+        profiles/r04_dp_overlap.jsonl): the side-stream branch in the captured
+        step costs 0.86-0.88 ms per replayed step (8.55 vs 7.69 ms), against
+        the ~12-20 us an 8-rank all-reduce of the 1.1 MB bucket takes over
+        xGMI -- graph branches on this stack cost more than any overlap they
+        buy."""
         return (self.sync.active and self.sync.capturable and self.gen_engine is not None
-                and self.skip_dead_d_grads and getattr(self.configuration, "runtime", {}).get("overlap_allreduce", True))
+                and self.skip_dead_d_grads and getattr(self.configuration, "runtime", {}).get("overlap_allreduce", False))
 
     def _gen_iteration_synced(self, local_graph, voxel_graph):
         """The generator iteration with its flat gradient averaged over the

@@ -57,7 +57,10 @@ def rccl1():
     dp.sync = GradSync(force=True)
     assert dp.sync.active and dp.sync.capturable and not ref.sync.active
     # the generator's gradient in two buckets, the decoder's reduced on a side
-    # stream during the encoders' backward (RCCL AVG: no scale launch)
+    # stream during the encoders' backward (RCCL AVG: no scale launch) -- an
+    # opt-in (runtime['overlap_allreduce']; off by default)
+    assert not dp._overlap_ready()
+    cfg.runtime["overlap_allreduce"] = True
     assert dp._overlap_ready() and dp.sync.avg_op
     a = ref.step(loc, vox)  # eager: the overlap outside any capture
     b = dp.step(loc, vox)
@@ -84,6 +87,19 @@ def rccl1():
         torch.cuda.synchronize()
         assert torch.equal(a["d_losses"], b["d_losses"]) and torch.equal(a["g_loss"], b["g_loss"]), k
     assert torch.equal(ref.flat_g.param, dp.flat_g.param) and torch.equal(ref.flat_d.param, dp.flat_d.param)
+    # the default: the generator's gradient in one all-reduce after its
+    # backward, recorded in the generator-iteration graph
+    cfg.runtime["overlap_allreduce"] = False
+    ref2, dp2 = _trainer(cfg, 778), _trainer(cfg, 778)
+    dp2.sync = GradSync(force=True)
+    assert not dp2._overlap_ready()
+    for _ in range(2):
+        a = ref2.step_graphed(loc, vox)
+        b = dp2.step_graphed(loc, vox)
+    torch.cuda.synchronize()
+    assert vox.derived(dp2._graph_key)["sync_in_graph"]
+    assert torch.equal(a["d_losses"], b["d_losses"]) and torch.equal(a["g_loss"], b["g_loss"])
+    assert torch.equal(ref2.flat_g.param, dp2.flat_g.param) and torch.equal(ref2.flat_d.param, dp2.flat_d.param)
     dist.destroy_process_group()
     print("RCCL_GRAPH_OK", flush=True)
 
