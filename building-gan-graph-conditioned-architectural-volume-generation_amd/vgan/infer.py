@@ -178,15 +178,16 @@ class InferenceSweep:
                 if ctr is not None:
                     ctr.copy_(keep)
                 st["warm"] = True
+            # recorded on the side stream with no stream waits around it: a
+            # recording enqueues no device work, and each cross-stream wait
+            # costs the device a queue drain
             g = torch.cuda.CUDAGraph(keep_graph=True)
-            side.wait_stream(cur)
             with torch.cuda.stream(side):
                 g.capture_begin(pool=self._pool, capture_error_mode="thread_local")
                 try:
                     out = self._forward(local_graph, voxel_graph)
                 finally:
                     g.capture_end()
-            cur.wait_stream(side)
             j = st["parity"] = (st["parity"] + 1) % 2
             owner = st["owners"][j]
             if st["events"][j] is not None:

@@ -486,16 +486,18 @@ class Trainer:
         side = getattr(self, "_fresh_stream", None)
         if side is None:
             side = self._fresh_stream = torch.cuda.Stream(dev)
-        cur = torch.cuda.current_stream(dev)
+        # No stream waits around the recording: it enqueues no device work,
+        # so neither side.wait_stream(cur) nor cur.wait_stream(side) would
+        # order anything -- and each costs the device a drain of its queue
+        # (a cross-queue barrier): 8.30-8.46 vs 7.71-7.72 ms per fresh step
+        # with them (profiles/r04_record_waits_ab.txt).
         g = torch.cuda.CUDAGraph(keep_graph=True)
-        side.wait_stream(cur)
         with torch.cuda.stream(side):
             g.capture_begin(pool=pool, capture_error_mode="thread_local")
             try:
                 out = fn()
             finally:
                 g.capture_end()
-        cur.wait_stream(side)
         return g, out
 
     def _fresh_exec(self, kind: str, g) -> ctypes.c_void_p:
