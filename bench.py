@@ -499,10 +499,9 @@ def sweep_leg(device, store_job, batch: int = 32, n_taus: int = 10):
     schedule 1.0 -> 0.1, f16 (and f32) eval forward, one stacked forward per
     batch over the ``n_taus`` temperature copies.  Each batch comes through
     the native loader (host collate + host-built per-batch structures + one
-    upload, prefetched on a thread); its forward is recorded as a hipGraph
-    and an executable graph is updated in place (InferenceSweep.run_fresh).
-    The timed region is the whole pass: collate, upload, record, update,
-    replay.  Also the f16 scatter kernel (vg_hgat_fwd) over the sweep's own
+    upload, prefetched on a thread); its forward is launched eagerly
+    (InferenceSweep.run_stream; recording it per batch measured slower).
+    The timed region is the whole pass: collate, upload, forward.  Also the f16 scatter kernel (vg_hgat_fwd) over the sweep's own
     stacked graph and channel schedule, graph-replayed between HIP events."""
     from vgan import data as vdata
     from vgan._lib import LIB, check, ptr, stream_handle
@@ -534,8 +533,8 @@ def sweep_leg(device, store_job, batch: int = 32, n_taus: int = 10):
     n_batches = -(-len(store) // batch)
     out = {"workload": f"configs[4]: {len(store)} distinct synthetic buildings ({n_batches} batches of {batch}) "
                        f"streamed through the native loader, {n_taus} Gumbel temperatures 1.0->0.1 geometric, eval G "
-                       f"forward stacked over the temperatures; per batch its forward recorded as a hipGraph and "
-                       f"an executable graph updated in place; collate, upload, record, update and replay timed",
+                       f"forward stacked over the temperatures, launched eagerly per batch (InferenceSweep.run_stream); "
+                       f"collate, upload, per-batch structures and forward timed",
            "unit": "samples/s (buildings x temperatures)", "distinct_batches": n_batches,
            "distinct_buildings": len(store)}
     for dt in ("f16", "f32"):

@@ -20,12 +20,21 @@ from __future__ import annotations
 
 import contextlib
 import math
+import os
 from typing import Dict, Iterable, List, Optional, Sequence
 
 import torch
 
 from . import data as vdata
 from .gcscope import gc_frozen
+
+
+# run_stream launches each batch's forward eagerly; VGAN_SWEEP_STREAM=record
+# records it and updates an executable graph instead (run_fresh).  Eager
+# measured faster: recording costs the host what launching does, and the
+# update, the graph launch and its event come on top -- f16 147-204k vs
+# 129-167k samples/s, alternated (profiles/r04_sweep_eager_ab.txt)
+_STREAM = os.environ.get("VGAN_SWEEP_STREAM", "eager")
 
 
 def geometric_taus(t0: float = 1.0, t1: float = 0.1, steps: int = 10) -> List[float]:
@@ -214,13 +223,16 @@ class InferenceSweep:
             return res
 
     def run_stream(self, batches: Iterable, collect: bool = False) -> Dict[str, object]:
-        """Sweep a stream of batches each seen once (``run_fresh``): counts
-        and, with ``collect``, every batch's [k, N] predictions."""
+        """Sweep a stream of batches each seen once (each batch's forward
+        launched eagerly, or recorded with ``run_fresh`` under
+        VGAN_SWEEP_STREAM=record): counts and, with ``collect``, every
+        batch's [k, N] predictions."""
         outs: List[torch.Tensor] = []
         graphs = samples = nb = 0
+        eager = _STREAM == "eager" and not self.graphed
         with self._eval(), gc_frozen():  # vgan/gcscope.py
             for local_graph, voxel_graph in batches:
-                pred = self.run_fresh(local_graph, voxel_graph)
+                pred = self.run_batch(local_graph, voxel_graph) if eager else self.run_fresh(local_graph, voxel_graph)
                 graphs += voxel_graph.num_graphs
                 samples += voxel_graph.num_graphs * len(self.taus)
                 nb += 1

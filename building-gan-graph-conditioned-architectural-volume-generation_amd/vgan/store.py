@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import ctypes
 import json
+import math
 import os
 from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
@@ -294,7 +295,7 @@ class GraphStore:
         sizes, items, extras = self._layout(index, prepare)
         layout, off = {}, 0
         for name, shape, dt in items:
-            nbytes = int(np.prod(shape)) * torch.empty((), dtype=dt).element_size()
+            nbytes = _nbytes(shape, dt)
             layout[name] = (off, tuple(shape), dt)
             off += (nbytes + 255) // 256 * 256
         blob = torch.empty(max(off, 256), dtype=torch.uint8, pin_memory=pin)
@@ -328,7 +329,7 @@ class GraphStore:
             attrs["batch"] = v[f"{kind}.batch"]
             attrs["ptr"] = v[f"{kind}.ptr"]
             gb = GraphBatch(**attrs)
-            gb.set_derived("ptr_host", [int(x) for x in attrs["ptr"].tolist()])
+            gb.set_derived("ptr_host", attrs["ptr"].tolist())
             if kind in CSR_KINDS:
                 gb.set_derived("csr_arrays", csr)
                 # the largest in-degree (self loop included) from the host row_ptr:
@@ -396,9 +397,17 @@ class GraphStore:
         return self.collate_pair(indices, pin=pin, threads=threads, prepare=prepare)
 
 
+_ELEM_SIZE = {dt: torch.empty((), dtype=dt).element_size() for dt in (torch.int32, torch.int64, torch.float32,
+                                                                        torch.float64, torch.int8, torch.uint8,
+                                                                        torch.int16, torch.float16, torch.bool)}
+
+
+def _nbytes(shape, dtype) -> int:
+    return math.prod(shape) * _ELEM_SIZE[dtype]
+
+
 def _view(blob: torch.Tensor, off: int, shape, dtype) -> torch.Tensor:
-    nbytes = int(np.prod(shape)) * torch.empty((), dtype=dtype).element_size()
-    return blob[off:off + nbytes].view(dtype).view(shape)
+    return blob[off:off + _nbytes(shape, dtype)].view(dtype).view(shape)
 
 
 def upload_pair(local: GraphBatch, voxel: GraphBatch, device, non_blocking: bool = True
