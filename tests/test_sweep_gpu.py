@@ -2,8 +2,9 @@
 reference's test loop, trainer.py:749-806, over a whole split; Gumbel tau
 annealed, models.py:150): every batch comes through the native loader (host
 collate + host-built per-batch structures + one upload), its stacked forward
-is recorded as a hipGraph and an executable graph is updated in place per
-batch (InferenceSweep.run_fresh).  The predictions equal, bit for bit, the
+launched eagerly (run_stream's default) or recorded as a hipGraph with an
+executable graph updated in place per batch (InferenceSweep.run_fresh,
+VGAN_SWEEP_STREAM=record).  The predictions equal, bit for bit, the
 eager forward over the same batches from the same device-RNG state -- f16 and
 f32, batches of varying size (updates and re-instantiations), back to back
 with no host synchronisation."""
@@ -21,8 +22,12 @@ from vgan.synth import SyntheticDataset
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("stream", ["eager", "record"])
 @pytest.mark.parametrize("dtype", ["f16", "f32"])
-def test_stream_sweep_equals_eager(cuda, tmp_path, dtype):
+def test_stream_sweep_equals_eager(cuda, tmp_path, dtype, stream, monkeypatch):
+    from vgan import infer
+
+    monkeypatch.setattr(infer, "_STREAM", stream)
     st = write_store(str(tmp_path / "s"), SyntheticDataset(23, seed=17))
     cfg = Configuration()
     cfg.DEVICE = str(cuda)
