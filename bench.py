@@ -676,10 +676,7 @@ def main():
 
     rank, world, local = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(
         os.environ.get("LOCAL_RANK", 0))
-    # configs[4]'s 10,000 distinct buildings are generated in a child process
-    # (before this process touches the GPU) while the other legs run
-    store_job = start_sweep_store() if (rank == 0 and not args.no_sweep and not args.profile
-                                        and not args.roofline_only) else None
+    want_sweep = rank == 0 and not args.no_sweep and not args.profile and not args.roofline_only
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     if not torch.cuda.is_available():
@@ -798,6 +795,10 @@ def main():
                                 rank, world)
         log(f"fresh batches (loader, step_fresh): {fresh['ms_per_step']:.2f} ms/step, {fresh['value']:.1f} graphs/s")
 
+    # configs[4]'s 10,000 distinct buildings are generated in a child process
+    # while the stress legs run -- after the host-bound fresh leg, which the
+    # writer slowed by ~0.2 ms per step when it ran beside it
+    store_job = start_sweep_store() if want_sweep else None
     result = None
     if rank == 0:
         stress_orders = {} if args.no_stress else {o: stress_roofline(device, order=o)
