@@ -191,7 +191,12 @@ def _prefetched(store: GraphStore, plan: List[List[int]], dev: torch.device, dep
             if isinstance(item, BaseException):
                 raise item
             moved, host, ev = item
-            torch.cuda.current_stream(dev).wait_event(ev)
+            # The host waits for the upload -- issued `depth` batches earlier,
+            # long finished -- instead of the consumer's stream waiting on the
+            # copy stream's event: a cross-queue barrier on the device per
+            # batch, which took the fresh-batch step to 7.72-8.36 ms against
+            # 7.69-7.71 (profiles/r04_loader_wait_ab.txt)
+            ev.synchronize()
             for g in moved:  # the consumer stream now owns these allocations
                 for t in _tensors(g):
                     t.record_stream(torch.cuda.current_stream(dev))
