@@ -229,9 +229,10 @@ class CriticEngine:
         self._arena = (t, floats, t.data_ptr() + 4 * off)
         return self._arena
 
-    def _native(self, prep, hard, soft, keeps, eps, dev, st):
+    def _native(self, prep, hard, soft, keeps, eps, dev, st, out=None):
         """loss_and_grad through vg_critic_loss_and_grad, or None (the
-        configuration or this batch is not the native engine's)."""
+        configuration or this batch is not the native engine's).  ``out``: two
+        contiguous device floats to write (d_loss, penalty) into."""
         n = prep.matched_voxel_x.shape[0]
         if not self._native_config_ok(n) or isinstance(eps, torch.Tensor) or eps is None:
             return None
@@ -249,7 +250,9 @@ class CriticEngine:
         arena = self._arena_for(model, batch, dev)
         if arena is None:
             return None
-        out = _f(2, dev=dev)
+        if out is None or out.numel() != 2 or not out.is_contiguous() or out.dtype != torch.float32 \
+                or out.device != dev:
+            out = _f(2, dev=dev)
         check(LIB.vg_critic_loss_and_grad(ctypes.byref(model), ctypes.byref(batch), arena[2], arena[1], ptr(out), st),
               "vg_critic_loss_and_grad")
         self.native_calls = self.__dict__.get("native_calls", 0) + 1
@@ -288,7 +291,7 @@ class CriticEngine:
                  keep=(ws,))
 
     # ------------------------------------------------------------ engine
-    def loss_and_grad(self, local_graph, voxel_graph, label_hard, label_soft, rng) -> torch.Tensor:
+    def loss_and_grad(self, local_graph, voxel_graph, label_hard, label_soft, rng, out=None) -> torch.Tensor:
         """d_loss (device scalar) of trainer.py:318-332; D's parameter gradients
         are added to their .grad.
 
@@ -326,7 +329,7 @@ class CriticEngine:
         if isinstance(eps, torch.Tensor):
             eps = eps.reshape(n).contiguous()
         else:  # the launches below, issued from C++ (vg_critic_loss_and_grad)
-            loss = self._native(prep, hard, soft, keeps, eps, dev, st)
+            loss = self._native(prep, hard, soft, keeps, eps, dev, st, out)
             if loss is not None:
                 return loss
         nb, nd, nm = len(self.blocks), len(self.dec), len(self.mlp)
