@@ -71,6 +71,17 @@ def _loss_pair(acc: torch.Tensor, i: int):
     return base[i]
 
 
+class _StepOut(dict):
+    """step_graphed's result: "d_loss_mean" is formed when first read (an
+    eager reduction launch per step otherwise, whether read or not)."""
+
+    def __missing__(self, key):
+        if key != "d_loss_mean":
+            raise KeyError(key)
+        v = self[key] = self["d_losses"].mean()
+        return v
+
+
 class Trainer:
     def __init__(self, generator, discriminator, dataloaders, optimizer_generator, optimizer_discriminator,
                  scheduler_generator, configuration, log_dir: Optional[str] = None):
@@ -469,8 +480,7 @@ class Trainer:
         if not graphs["with_adam"]:
             self.sync.all_reduce_grad(self.flat_g)
             self.adam_g.step(counted=True)
-        return {"d_losses": acc[:n_critic], "d_loss_mean": acc[:n_critic].mean(), "g_loss": acc[n_critic],
-                "label_hard": graphs["hard"]}
+        return _StepOut(d_losses=acc[:n_critic], g_loss=acc[n_critic], label_hard=graphs["hard"])
 
     # ------------------------------------------------ a batch seen once
     def step_fresh(self, local_graph, voxel_graph) -> Dict[str, torch.Tensor]:
