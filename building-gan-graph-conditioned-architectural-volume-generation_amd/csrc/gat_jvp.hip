@@ -114,7 +114,7 @@ __global__ void __launch_bounds__(kBlock) k_jvp_rows(
       const int c = c0 + q;
       const bool ok = c < C;
       gmu.v[q] = ok ? gj.stats[c] : 0.f;
-      gs.v[q] = ok ? gj.stats[C + c] + gj.eps : 1.f;
+      gs.v[q] = ok ? gj.stats[C + c] : 1.f;  // d, the whole denominator
       gw.v[q] = ok ? gj.w[c] : 0.f;
       gb.v[q] = ok ? gj.b[c] : 0.f;
       gms.v[q] = ok ? gj.ms[c] : 0.f;

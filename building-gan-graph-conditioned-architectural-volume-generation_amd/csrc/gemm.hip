@@ -126,7 +126,7 @@ struct GnpDesc {
 // GraphNorm + ReLU + Dropout applied to the A operand as it is loaded
 // (vg_gat_lin_att_gn: the GraphNorm that ends a GATConv block feeding the next
 // block's projection, models.py:73-77): A holds the GraphNorm INPUT x [rows, K]
-// (lda = K); every element becomes y = keep * relu(w (x - ms mu)/(sd + eps) + b)
+// (lda = K); every element becomes y = keep * relu(w (x - ms mu)/d + b)
 // with the statistics of its row's segment -- the formula and operation order
 // of k_gn_apply4 -- and y (and a drawn keep) are stored for the backward when
 // y != NULL.  keep: multipliers read (iter == NULL) or drawn in-kernel
@@ -151,7 +151,7 @@ constexpr int kGnaMaxK = 128;  // GraphNorm channels the operand transform stage
 // Four consecutive columns k .. k+3 of row n (k % 4 == 0, K % 4 == 0): one
 // Philox block draws all four multipliers (vg_keep4_raw: the values vg_keep
 // gives each element), float4 stores of y / keep.  gp = the block's staged
-// column operands [w | b | ms | mu0 | sd0 + eps | mu1 | sd1 + eps] (segment
+// column operands [w | b | ms | mu0 | d0 | mu1 | d1] (segment
 // slots 0 / 1: the tile's first row's segment and the next).
 __device__ __forceinline__ float4 gna_quad(const GnaDesc& ga, const float* gp, float4 x, int n, int k, int K,
                                            int bound, long long it) {
@@ -229,7 +229,7 @@ __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int l
         if (q == 0 || gbound < N) {
           const float* st = gn.stats + (size_t)(seg0 + q) * 2 * M;
           gmu[q] = st[mc];
-          gsd[q] = st[M + mc] + gn.eps;
+          gsd[q] = st[M + mc];
         }
     }
 #pragma unroll
@@ -512,7 +512,7 @@ __device__ __forceinline__ void gemm16_body(const float* __restrict__ A, int lda
           if (q == 0 || gbound < N) {
             const float* st = gn.stats + (size_t)(seg0 + q) * 2 * M;
             gmu[s_][q] = st[mc];
-            gsd[s_][q] = st[M + mc] + gn.eps;
+            gsd[s_][q] = st[M + mc];
           }
       }
 #pragma unroll
@@ -538,9 +538,9 @@ __device__ __forceinline__ void gemm16_body(const float* __restrict__ A, int lda
       gpar[2 * K + k] = ga.ms[k];
       const float* st = ga.stats + (size_t)seg0 * 2 * K;
       gpar[3 * K + k] = st[k];
-      gpar[4 * K + k] = st[K + k] + ga.eps;
+      gpar[4 * K + k] = st[K + k];
       gpar[5 * K + k] = two ? st[2 * K + k] : 0.f;
-      gpar[6 * K + k] = two ? st[3 * K + k] + ga.eps : 1.f;
+      gpar[6 * K + k] = two ? st[3 * K + k] : 1.f;
     }
   }
   // GNA: A as float4 quads, threads 0..511 (one row quad each per K-tile)

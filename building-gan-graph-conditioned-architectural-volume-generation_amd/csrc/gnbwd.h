@@ -1,14 +1,14 @@
 // GraphNorm(+ReLU+Dropout) backward, elementwise part, shared by the
 // GraphNorm apply kernels (graphnorm.hip) and the GAT backward row pass that
 // computes it in its prologue (gat_fused.hip, vg_gat_bwd_gn): one formula, so
-// the fused and the separate paths agree.
+// the fused and the separate paths agree.  torch_geometric 2.6.1 GraphNorm
+// (batch=None, models.py:73-75 / 193-195), with stats = [mu | d]:
 //
-//   s = sigma + eps,  xhat = (x - ms mu) / s,  z = w xhat + b
-//   gz = g_y [z > 0] keep
-//   g_x = (w / s)(gz - ms A / N) - [sigma > 0] (w B / (N s sigma)) (x - mu)
-// with A = sum gz, B = sum gz xhat over the segment's N rows (torch's
-// GraphNorm backward, models.py:73-75 / 193-195; sigma == 0 masks the second
-// term as torch's std backward does).
+//   d = sqrt(mean((x - ms mu)^2) + eps),  ohat = (x - ms mu) / d,  z = w ohat + b
+//   gz = g_y [z > 0] keep,  A = sum gz,  B = sum gz ohat  (the segment's N rows)
+//   a = (1 - ms) mu = mean(x - ms mu)
+//   g_x  = (w / d)(gz - B ohat / N - (ms / N)(A - B a / d))
+//   g_ms = -mu (w / d)(A - B a / d)
 #pragma once
 #include "rowgroup.h"
 
@@ -17,14 +17,18 @@ namespace vg {
 __device__ __forceinline__ float gn_bwd_elem(float xv, float gyv, float kv, bool has_keep, float mu, float sd,
                                              float wc, float bc, float msc, float A, float B, float eps,
                                              float inv_n) {
-  const float s = sd + eps;
-  const float xh = (xv - mu * msc) / s;
-  const float z = xh * wc + bc;
+  (void)eps;  // folded into sd = d by the statistics pass
+  const float oh = (xv - mu * msc) / sd;
+  const float z = oh * wc + bc;
   float gz = z > 0.f ? gyv : 0.f;
   if (has_keep) gz *= kv;
-  float g = (wc / s) * (gz - msc * A * inv_n);
-  if (sd > 0.f) g -= (wc * B * inv_n / (s * sd)) * (xv - mu);
-  return g;
+  const float colsum = A - B * ((1.f - msc) * mu) / sd;  // sum over rows of (gz - B ohat / N)
+  return (wc / sd) * (gz - B * oh * inv_n - msc * inv_n * colsum);
+}
+
+// mean_scale's gradient of one segment from its column sums A, B
+__device__ __forceinline__ float gn_g_ms(float mu, float sd, float wc, float msc, float A, float B) {
+  return -mu * (wc / sd) * (A - B * ((1.f - msc) * mu) / sd);
 }
 
 // The GraphNorm backward a GAT backward row pass forms in its prologue
@@ -38,7 +42,7 @@ struct GnRows {
   const float* weight;
   const float* bias;
   const float* mean_scale;
-  const float* stats;  // [S][2C] mean | std
+  const float* stats;  // [S][2C] mean | d (the GraphNorm denominator)
   const float* sums;   // [S][2C] A | B
   float* g_out;        // g_x, written for the source pass
   float eps;

@@ -1,11 +1,16 @@
 // GraphNorm(batch=None) fused with the ReLU and Dropout that follow it in every
-// encoder block (models.py:73-75,83-85,193-195,203-205).
+// encoder block (models.py:73-75,83-85,193-195,203-205), with torch_geometric
+// 2.6.1 nn/norm/graph_norm.py semantics (requirements.txt:11):
 //
-// Forward   mu, sigma = population column mean / std over all N rows
-//           y = keep * relu(w * (x - ms*mu) / (sigma + eps) + b)
-// Backward  gz = g_y * keep * [z > 0];  A = sum gz;  B = sum gz * xhat
-//           g_x = (w/s)(gz - ms*A/N) - (w*B/(N*s*sigma)) (x - mu)   (0 if sigma == 0,
-//           matching torch's std backward mask), g_w = B, g_b = A, g_ms = -mu*w*A/s
+// Forward   mu = mean_rows(x);  o = x - ms*mu;  var_o = mean_rows(o^2)
+//           d = sqrt(var_o + eps);  y = keep * relu(w * o / d + b)
+//           var_o = var(x) + ((1 - ms) mu)^2, so the statistics are the
+//           population (mean, var) of x (Welford) and the fold stores
+//           stats = [mu | d] per column -- every consumer divides by d.
+// Backward  gz = g_y * keep * [z > 0];  A = sum gz;  B = sum gz * ohat
+//           (ohat = o / d);  a = (1 - ms) mu  (= mean_rows(o))
+//           g_x = (w/d) (gz - B ohat / N - (ms/N)(A - B a / d))
+//           g_w = B, g_b = A, g_ms = -mu (w/d) (A - B a / d)
 //
 // Segments: S independent row blocks of Ns rows each (the discriminator's
 // real / fake / mix copies stacked as one [3N, C] tensor) each normalise with
@@ -13,12 +18,12 @@
 // segments.
 //
 // Second order (the WGAN-GP critic engine, vgan/critic.py): for a tangent u of
-// x and the adjoint g_y of y, with p = g_y * keep * [z > 0], xt = x - mu,
-// c = x - ms*mu, d = sigma + eps:
-//   y'   = keep [z > 0] w (c'/d - c sigma'/d^2),  c' = u - ms*mean(u),
-//          sigma' = M / sigma,  M = mean(xt u)
-//   Q    = <g_y, y'>;  dQ/dw, dQ/dms and dQ/dx in closed form from the column
-//          sums (sum u, sum xt u, sum p, sum p u, sum p xt)   (k_gn_jvp2_*)
+// x and the adjoint g_y of y, with p = g_y * keep * [z > 0], m_u = mean(u),
+// c' = u - ms*m_u, K = mean(o c') (so d' = K/d):
+//   y'  = keep [z > 0] w (c'/d - o K/d^3)
+//   Q   = <g_y, y'> = w (P1/d - P2 K/d^3),  P1 = sum p c',  P2 = sum p o
+//   dQ/dw, dQ/dms and dQ/dx in closed form from the column sums
+//   (sum u, sum xt u, sum p, sum p u, sum p xt), xt = x - mu   (k_gn_jvp2_*)
 //
 // The column statistics are a two-level deterministic reduction: R row-chunk
 // blocks per 64-column slab produce (count, mean, M2) Welford partials, a
@@ -171,12 +176,22 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// The GraphNorm denominator from the column's population (mean, M2):
+// d = sqrt(mean((x - ms mu)^2) + eps) = sqrt(var + ((1 - ms) mu)^2 + eps)
+__device__ __forceinline__ float gn_denom(Welford a, float msc, float eps) {
+  const float var = fmaxf(a.m2 / a.n, 0.f);
+  const float sh = (1.f - msc) * a.mean;
+  return sqrtf(fmaf(sh, sh, var) + eps);
+}
+
 // One wave per (column, segment): grid (C / 4, S).
 __global__ void __launch_bounds__(kBlock) k_stats_final(const float* __restrict__ part, int chunks,
-                                                        int C, int S, float* __restrict__ stats) {
+                                                        int C, int S, const float* __restrict__ ms, float eps,
+                                                        float* __restrict__ stats) {
   const int c = fold_col(), lane = threadIdx.x & 63;
   const int sg = blockIdx.y;
   if (c >= C || sg >= S) return;
+  const float msc = ms[c];
   const float* pp = part + (size_t)sg * chunks * C * 3;
   float v[kFoldU][3];
 #pragma unroll
@@ -191,7 +206,7 @@ __global__ void __launch_bounds__(kBlock) k_stats_final(const float* __restrict_
   acc = wave_merge(acc);
   if (lane == 0) {
     stats[(size_t)sg * 2 * C + c] = acc.mean;
-    stats[(size_t)sg * 2 * C + C + c] = sqrtf(fmaxf(acc.m2 / acc.n, 0.f));
+    stats[(size_t)sg * 2 * C + C + c] = gn_denom(acc, msc, eps);
   }
 }
 
@@ -203,10 +218,12 @@ __global__ void __launch_bounds__(kBlock) k_stats_final(const float* __restrict_
 // segment's blocks l, l + 64, ... in order (16 in flight: one round trip at
 // batch 32), then the xor butterfly: deterministic.
 __global__ void __launch_bounds__(kBlock) k_stats_final_gnp(const float* __restrict__ gnp, int G, int N, int C,
-                                                            int S, float* __restrict__ stats) {
+                                                            int S, const float* __restrict__ ms, float eps,
+                                                            float* __restrict__ stats) {
   const int c = fold_col(), lane = threadIdx.x & 63;
   const int sg = blockIdx.y;
   if (c >= C || sg >= S) return;
+  const float msc = ms[c];
   const int nb = (N + G - 1) / G;
   const int b0 = sg * nb, b1 = b0 + nb - 1;  // inclusive
   constexpr int U = 16;
@@ -231,7 +248,7 @@ __global__ void __launch_bounds__(kBlock) k_stats_final_gnp(const float* __restr
   acc = wave_merge(acc);
   if (lane == 0) {
     stats[(size_t)sg * 2 * C + c] = acc.mean;
-    stats[(size_t)sg * 2 * C + C + c] = sqrtf(fmaxf(acc.m2 / acc.n, 0.f));
+    stats[(size_t)sg * 2 * C + C + c] = gn_denom(acc, msc, eps);
   }
 }
 
@@ -252,7 +269,7 @@ __global__ void k_gn_apply(const float* __restrict__ x, long long total, int C, 
     const float* st = stats + 2 * C * (t / seg_elems);
     const float mu = st[c], sd = st[C + c];
     const float o = x[t] - mu * ms[c];
-    const float z = (o / (sd + eps)) * w[c] + b[c];
+    const float z = (o / sd) * w[c] + b[c];
     float r = z > 0.f ? z : 0.f;
     if (draw) {
       const float k = vg_keep(t, salt, it, seed, p_drop);
@@ -284,7 +301,7 @@ __global__ void k_gn_apply_h(const _Float16* __restrict__ x, long long pairs, in
     for (int q = 0; q < 2; ++q) {
       const int cc = c + q;
       if (cc < C) {
-        const float z = ((static_cast<float>(xp[q]) - st[cc] * ms[cc]) / (st[C + cc] + eps)) * w[cc] + b[cc];
+        const float z = ((static_cast<float>(xp[q]) - st[cc] * ms[cc]) / st[C + cc]) * w[cc] + b[cc];
         r[q] = z > 0.f ? z : 0.f;
       } else {
         r[q] = 0.f;
@@ -321,7 +338,7 @@ __global__ void __launch_bounds__(kBlock) k_gn_bwd_partial(
   part += (size_t)blockIdx.z * gridDim.x * C * 2;
   float sa = 0.f, sb = 0.f;
   if (c < C) {
-    const float mu = stats[c], s = stats[C + c] + eps, wc = w[c], bc = b[c], msc = ms[c];
+    const float mu = stats[c], s = stats[C + c], wc = w[c], bc = b[c], msc = ms[c];
 #pragma unroll 4
     for (int r = r0 + rsub; r < r1; r += rstep) {
       const size_t t = (size_t)r * C + c;
@@ -406,7 +423,7 @@ __global__ void __launch_bounds__(kBlock) k_gn_bwd_final(
       }
       tw += bb;
       tb += a;
-      tm += -st[c] * w[c] * a / (st[C + c] + eps);
+      tm += vg::gn_g_ms(st[c], st[C + c], w[c], ms[c], a, bb);
     }
   }
   if (lane == 0 && g_w) {
@@ -419,7 +436,8 @@ __global__ void __launch_bounds__(kBlock) k_gn_bwd_final(
 // One group of up to kSegs segments of k_gn_bwd_final_tiles' fold.
 template <int kSegs, int kU>
 __device__ __forceinline__ void bwd_tiles_group(const float* __restrict__ tpart, int N, int C, int S, int s0,
-                                                int c, int lane, const float* __restrict__ w, float eps,
+                                                int c, int lane, const float* __restrict__ w,
+                                                const float* __restrict__ ms,
                                                 const float* __restrict__ stats, float* __restrict__ sums,
                                                 const float* __restrict__ g3[3], float g0[3],
                                                 float& tw, float& tb, float& tm) {
@@ -446,7 +464,7 @@ __device__ __forceinline__ void bwd_tiles_group(const float* __restrict__ tpart,
   }
   // the per-column operands and (first group) the accumulated gradients, in
   // flight with the partials
-  const float wc = w[c];
+  const float wc = w[c], msc = ms[c];
   if (g3) {
 #pragma unroll
     for (int q = 0; q < 3; ++q) g0[q] = g3[q][c];
@@ -485,7 +503,7 @@ __device__ __forceinline__ void bwd_tiles_group(const float* __restrict__ tpart,
     }
     tw += bb;
     tb += a;
-    tm += -mu[j] * wc * a / (sd[j] + eps);
+    tm += vg::gn_g_ms(mu[j], sd[j], wc, msc, a, bb);
   }
 }
 
@@ -515,10 +533,10 @@ __global__ void __launch_bounds__(kBlock) k_gn_bwd_final_tiles(
   float g0[3] = {0.f, 0.f, 0.f};
   float tw = 0.f, tb = 0.f, tm = 0.f;
   if (S <= kSegs) {
-    bwd_tiles_group<kSegs, kU>(tpart, N, C, S, 0, c, lane, w, eps, stats, sums, g3, g0, tw, tb, tm);
+    bwd_tiles_group<kSegs, kU>(tpart, N, C, S, 0, c, lane, w, ms, stats, sums, g3, g0, tw, tb, tm);
   } else {
     for (int s0 = 0; s0 < S; s0 += kSegs)
-      bwd_tiles_group<kSegs, kU>(tpart, N, C, S, s0, c, lane, w, eps, stats, sums, s0 == 0 ? g3 : nullptr, g0,
+      bwd_tiles_group<kSegs, kU>(tpart, N, C, S, s0, c, lane, w, ms, stats, sums, s0 == 0 ? g3 : nullptr, g0,
                                  tw, tb, tm);
   }
   if (lane == 0 && g_w) {
@@ -526,7 +544,7 @@ __global__ void __launch_bounds__(kBlock) k_gn_bwd_final_tiles(
     g_b[c] = acc ? g0[1] + tb : tb;
     g_ms[c] = acc ? g0[2] + tm : tm;
   }
-  (void)ms;
+  (void)eps;
 }
 
 // g_x (+ inj for elements t >= inj_off: the second-order adjoint of the
@@ -573,7 +591,7 @@ __global__ void __launch_bounds__(kBlock) k_gn_jvp2_partial(
   const int r1 = min(N, r0 + rows_per_chunk);
   float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   if (c < C) {
-    const float mu = stats[c], s = stats[C + c] + eps, wc = w[c], bc = b[c], msc = ms[c];
+    const float mu = stats[c], s = stats[C + c], wc = w[c], bc = b[c], msc = ms[c];
 #pragma unroll 4
     for (int r = r0 + rsub; r < r1; r += rstep) {
       const size_t t = (size_t)r * C + c;
@@ -632,7 +650,7 @@ __global__ void __launch_bounds__(kBlock) k_gn_jvp2_partial4(
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       mu[q] = stats[c0 + q];
-      sd[q] = stats[C + c0 + q] + eps;
+      sd[q] = stats[C + c0 + q];
       wc[q] = w[c0 + q];
       bc[q] = b[c0 + q];
       msc[q] = ms[c0 + q];
@@ -683,9 +701,33 @@ __global__ void __launch_bounds__(kBlock) k_gn_jvp2_partial4(
   }
 }
 
-// one wave per column: mu' = mean u, M = mean(xt u), Sp, P1 = sum p c',
-// P2 = sum p c;  g_w += P1/d - P2 M/(sigma d^2);
-// g_ms += w (-mu' Sp/d + mu Sp M/(sigma d^2))
+// The column terms of the second-order pass from the five column sums
+// v = [sum u, sum xt u, sum p, sum p u, sum p xt] (xt = x - mu):
+//   m_u = mean u, a = (1 - ms) mu = mean o, K = mean(o c') = mean(o u) - ms m_u a,
+//   P1 = sum p c' = sum p u - ms m_u Sp, P2 = sum p o = sum p xt + a Sp;
+//   Q / w = P1/d - P2 K/d^3  ->  g_w += Q / w;
+//   g_ms += w d(Q/w)/dms with dd/dms = -a mu/d, dK/dms = -2 a m_u,
+//           dP1/dms = -m_u Sp, dP2/dms = -mu Sp.
+// sums <- [m_u, K, Sp, P1, P2] for the elementwise pass.
+__device__ __forceinline__ void gn_jvp2_cols(const float v[5], float inv_n, float mu, float d, float msc, float wc,
+                                             float* __restrict__ sm, float& dgw, float& dgms) {
+  const float mup = v[0] * inv_n, Sp = v[2];
+  const float a = (1.f - msc) * mu;
+  const float K = (v[1] + a * v[0]) * inv_n - msc * mup * a;
+  const float P1 = v[3] - msc * mup * Sp;
+  const float P2 = v[4] + a * Sp;
+  const float id = 1.f / d, id2 = id * id, id3 = id2 * id;
+  const float dd = -a * mu * id, dK = -2.f * a * mup;
+  sm[0] = mup;
+  sm[1] = K;
+  sm[2] = Sp;
+  sm[3] = P1;
+  sm[4] = P2;
+  dgw = P1 * id - P2 * K * id3;
+  dgms = wc * (-mup * Sp * id - P1 * dd * id2 + mu * Sp * K * id3 - P2 * dK * id3 + 3.f * P2 * K * dd * id3 * id);
+}
+
+// one wave per column: the five sums, then gn_jvp2_cols
 __global__ void __launch_bounds__(kBlock) k_gn_jvp2_final(
     const float* __restrict__ part, int chunks, int N, int C, const float* __restrict__ w,
     const float* __restrict__ ms, float eps, const float* __restrict__ stats,
@@ -707,20 +749,11 @@ __global__ void __launch_bounds__(kBlock) k_gn_jvp2_final(
     v[q] = wave_sum(v[q]);
   }
   if (lane != 0) return;
-  const float inv_n = 1.f / static_cast<float>(N);
-  const float mu = stats[c], sd = stats[C + c], d = sd + eps, msc = ms[c], wc = w[c];
-  const float mup = v[0] * inv_n, M = v[1] * inv_n, Sp = v[2];
-  const float P1 = v[3] - msc * mup * Sp;
-  const float P2 = v[4] + (1.f - msc) * mu * Sp;
-  const float isd = sd > 0.f ? 1.f / sd : 0.f;
-  float* sm = sums + (size_t)c * 5;
-  sm[0] = mup;
-  sm[1] = M;
-  sm[2] = Sp;
-  sm[3] = P1;
-  sm[4] = P2;
-  g_w[c] += P1 / d - P2 * M * isd / (d * d);
-  g_ms[c] += wc * (-mup * Sp / d + mu * Sp * M * isd / (d * d));
+  float dgw, dgms;
+  gn_jvp2_cols(v, 1.f / static_cast<float>(N), stats[c], stats[C + c], ms[c], w[c], sums + (size_t)c * 5, dgw, dgms);
+  g_w[c] += dgw;
+  g_ms[c] += dgms;
+  (void)eps;
 }
 
 // The same fold over the rows of partials the GAT tangent pass wrote
@@ -755,23 +788,15 @@ __global__ void __launch_bounds__(kBlock) k_gn_jvp2_final_blk(
 #pragma unroll
   for (int q = 0; q < 5; ++q) v[q] = wave_sum(v[q]);
   if (lane != 0) return;
-  const float inv_n = 1.f / static_cast<float>(N);
-  const float d = sd + eps;
-  const float mup = v[0] * inv_n, M = v[1] * inv_n, Sp = v[2];
-  const float P1 = v[3] - msc * mup * Sp;
-  const float P2 = v[4] + (1.f - msc) * mu * Sp;
-  const float isd = sd > 0.f ? 1.f / sd : 0.f;
-  float* sm = sums + (size_t)c * 5;
-  sm[0] = mup;
-  sm[1] = M;
-  sm[2] = Sp;
-  sm[3] = P1;
-  sm[4] = P2;
-  g_w[c] = gw0 + (P1 / d - P2 * M * isd / (d * d));
-  g_ms[c] = gm0 + wc * (-mup * Sp / d + mu * Sp * M * isd / (d * d));
+  float dgw, dgms;
+  gn_jvp2_cols(v, 1.f / static_cast<float>(N), mu, sd, msc, wc, sums + (size_t)c * 5, dgw, dgms);
+  g_w[c] = gw0 + dgw;
+  g_ms[c] = gm0 + dgms;
+  (void)eps;
 }
 
-// u_out = keep [z>0] w (c'/d - c sigma'/d^2);  x_inj = dQ/dx
+// u_out = y' = keep [z>0] w (c'/d - o K/d^3);  x_inj = dQ/dx with
+// dd/dx = (o - ms a)/(N d), dK/dx = (c' - ms (1 - ms) m_u)/N, dP2/dx = p - ms Sp/N
 __global__ void k_gn_jvp2_apply(const float* __restrict__ x, const float* __restrict__ u,
                                 const float* __restrict__ gy, long long total, int N, int C,
                                 const float* __restrict__ w, const float* __restrict__ b,
@@ -779,29 +804,30 @@ __global__ void k_gn_jvp2_apply(const float* __restrict__ x, const float* __rest
                                 float eps, const float* __restrict__ stats,
                                 const float* __restrict__ sums, float* __restrict__ u_out,
                                 float* __restrict__ x_inj) {
-  const float fn = static_cast<float>(N);
+  const float inv_n = 1.f / static_cast<float>(N);
   for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
        t += (long long)gridDim.x * blockDim.x) {
     const int c = static_cast<int>(t % C);
-    const float mu = stats[c], sd = stats[C + c], d = sd + eps;
+    const float mu = stats[c], d = stats[C + c];
     const float wc = w[c], msc = ms[c];
     const float* sm = sums + (size_t)c * 5;
-    const float mup = sm[0], M = sm[1], Sp = sm[2], P1 = sm[3], P2 = sm[4];
+    const float mup = sm[0], K = sm[1], Sp = sm[2], P1 = sm[3], P2 = sm[4];
     const float xv = x[t], uv = u[t];
-    const float xt = xv - mu, ut = uv - mup;
-    const float cc = xv - msc * mu, cp = uv - msc * mup;
-    const float z = (cc / d) * wc + b[c];
+    const float o = xv - msc * mu, cp = uv - msc * mup;
+    const float z = (o / d) * wc + b[c];
     float mk = z > 0.f ? 1.f : 0.f;
     if (keep) mk *= keep[t];
-    const float isd = sd > 0.f ? 1.f / sd : 0.f;
-    const float sigp = M * isd;
-    u_out[t] = mk * wc * (cp / d - cc * sigp / (d * d));
+    const float id = 1.f / d, id2 = id * id, id3 = id2 * id;
+    u_out[t] = mk * wc * (cp * id - o * K * id3);
     const float p = gy[t] * mk;
-    const float k1 = isd / (fn * d * d);  // 1 / (N sigma d^2)
-    float g = -P1 * xt * k1 - (p - msc * Sp / fn) * M * isd / (d * d) - P2 * ut * k1;
-    g += P2 * M * xt * (isd * isd / (d * d) + 2.f * isd / (d * d * d)) * isd / fn;
+    const float a = (1.f - msc) * mu;
+    const float ddx = (o - msc * a) * inv_n * id;
+    const float dKx = (cp - msc * (1.f - msc) * mup) * inv_n;
+    const float dP2x = p - msc * Sp * inv_n;
+    const float g = -P1 * ddx * id2 - (dP2x * K + P2 * dKx) * id3 + 3.f * P2 * K * ddx * id3 * id;
     x_inj[t] = wc * g;
   }
+  (void)eps;
 }
 
 // ------------------------------------------------ quad elementwise passes
@@ -885,7 +911,7 @@ __global__ void k_gn_apply4(const float* __restrict__ x, int quads, int N, int C
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float o = xv.v[j] - muv.v[j] * mv.v[j];
-      const float z = (o / (sdv.v[j] + eps)) * wv.v[j] + bv.v[j];
+      const float z = (o / sdv.v[j]) * wv.v[j] + bv.v[j];
       r.v[j] = z > 0.f ? z : 0.f;
       if (draw || keep) r.v[j] *= k4.v[j];
     }
@@ -988,12 +1014,14 @@ static int gn_fwd(const float* x, int32_t S, int32_t N, int32_t C, const float* 
     return VG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (gnp) {
-    k_stats_final_gnp<<<dim3(vg_blocks(C, kFoldWaves), S), 64 * kFoldWaves, 0, s>>>(gnp, gnp_rows, N, C, S, stats);
+    k_stats_final_gnp<<<dim3(vg_blocks(C, kFoldWaves), S), 64 * kFoldWaves, 0, s>>>(gnp, gnp_rows, N, C, S, mean_scale,
+                                                                                 eps, stats);
   } else {
     const int chunks = chunks_for(N);
     dim3 grid(chunks, (C + 63) / 64, S);
     k_stats_partial<float><<<grid, kBlock, 0, s>>>(x, N, C, C, ws, stats, nullptr);
-    k_stats_final<<<dim3(vg_blocks(C, kFoldWaves), S), 64 * kFoldWaves, 0, s>>>(ws, chunks, C, S, stats);
+    k_stats_final<<<dim3(vg_blocks(C, kFoldWaves), S), 64 * kFoldWaves, 0, s>>>(ws, chunks, C, S, mean_scale, eps,
+                                                                             stats);
   }
   (void)sync;  // former last-block-fold counter: accepted, unused
   const long long total = (long long)S * N * C;
@@ -1024,7 +1052,8 @@ extern "C" int vg_graphnorm_fwd_h(const uint16_t* x, int32_t ld, int32_t S, int3
   const int chunks = chunks_for(N);
   dim3 grid(chunks, (C + 63) / 64, S);
   k_stats_partial<_Float16><<<grid, kBlock, 0, s>>>(X, N, C, ld, ws, stats, nullptr);
-  k_stats_final<<<dim3(vg_blocks(C, kFoldWaves), S), 64 * kFoldWaves, 0, s>>>(ws, chunks, C, S, stats);
+  k_stats_final<<<dim3(vg_blocks(C, kFoldWaves), S), 64 * kFoldWaves, 0, s>>>(ws, chunks, C, S, mean_scale, eps,
+                                                                             stats);
   const long long pairs = (long long)S * N * (wcols / 2);
   k_gn_apply_h<<<apply_blocks(pairs), 256, 0, s>>>(X, pairs, C, ld, wcols, (long long)N, weight, bias,
                                                    mean_scale, eps, stats, reinterpret_cast<_Float16*>(y), ldy);
@@ -1063,10 +1092,11 @@ extern "C" int vg_graphnorm_fwd_gnp(const float* x, int32_t S, int32_t N, int32_
 }
 
 extern "C" int vg_graphnorm_stats_gnp(int32_t S, int32_t N, int32_t C, const float* gnp, int32_t gnp_rows,
-                                      float* stats, void* stream) {
-  if (S <= 0 || N <= 0 || C <= 0 || !gnp || !stats || gnp_rows <= 0 || gnp_rows > N) return VG_EINVAL;
+                                      const float* mean_scale, float eps, float* stats, void* stream) {
+  if (S <= 0 || N <= 0 || C <= 0 || !gnp || !mean_scale || !stats || gnp_rows <= 0 || gnp_rows > N)
+    return VG_EINVAL;
   k_stats_final_gnp<<<dim3(vg_blocks(C, kFoldWaves), S), 64 * kFoldWaves, 0, static_cast<hipStream_t>(stream)>>>(
-      gnp, gnp_rows, N, C, S, stats);
+      gnp, gnp_rows, N, C, S, mean_scale, eps, stats);
   VG_CHECK_LAUNCH();
   return 0;
 }

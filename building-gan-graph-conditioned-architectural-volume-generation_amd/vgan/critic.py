@@ -443,7 +443,8 @@ class CriticEngine:
                                 c=c))
                 nxt = self.blocks[bi + 1][0].out_channels if bi + 1 < nb else 0
                 if _lib._GN_APPLY_GEMM and 0 < nxt <= 64 and c <= 128 and n >= 64 and gemm_precision() == "f32":
-                    check(LIB.vg_graphnorm_stats_gnp(3, n, c, ptr(gnp), g, ptr(stats), st), "vg_graphnorm_stats_gnp")
+                    check(LIB.vg_graphnorm_stats_gnp(3, n, c, ptr(gnp), g, ptr(norm.mean_scale), float(norm.eps),
+                                                     ptr(stats), st), "vg_graphnorm_stats_gnp")
                     desc = VgGnApply(stats=stats.data_ptr(), weight=norm.weight.data_ptr(),
                                      bias=norm.bias.data_ptr(), mean_scale=norm.mean_scale.data_ptr(),
                                      keep=None if spec is not None or keep is None else keep.data_ptr(),

@@ -195,7 +195,8 @@ class GATEncoder(nn.Module):
             drop = (float(spec.p), int(spec.seed), ptr(spec.iter), int(spec.salt) & 0xFFFFFFFF) if spec is not None \
                 else (0.0, 0, None, 0)
             if 0 < nxt <= 64 and c <= 128 and c % 4 == 0:
-                check(LIB.vg_graphnorm_stats_gnp(S, n, c, ptr(gnp), g, ptr(stats), st), "vg_graphnorm_stats_gnp")
+                check(LIB.vg_graphnorm_stats_gnp(S, n, c, ptr(gnp), g, ptr(norm.mean_scale), float(norm.eps),
+                                                 ptr(stats), st), "vg_graphnorm_stats_gnp")
                 desc = VgGnApply(stats=stats.data_ptr(), weight=norm.weight.data_ptr(), bias=norm.bias.data_ptr(),
                                  mean_scale=norm.mean_scale.data_ptr(), keep=None, eps=float(norm.eps),
                                  p_drop=drop[0], seg_rows=n, salt=drop[3], seed=drop[1], iter=drop[2], y=None,

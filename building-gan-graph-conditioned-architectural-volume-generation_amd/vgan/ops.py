@@ -675,7 +675,7 @@ def graphnorm_relu_dropout_torch(x, weight, bias, mean_scale, keep, eps):
     """torch expression of the fused op (used only to build the create_graph
     backward; same formula as torch_geometric GraphNorm, batch=None)."""
     centred = x - x.mean(dim=0, keepdim=True) * mean_scale
-    z = centred / (centred.std(dim=0, unbiased=False, keepdim=True) + eps) * weight + bias
+    z = weight * centred / (centred.pow(2).mean(dim=0, keepdim=True) + eps).sqrt() + bias
     y = torch.relu(z)
     return y * keep if keep is not None else y
 

@@ -201,12 +201,14 @@ int vg_scatter_src(const int32_t* csc_ptr, const int32_t* csc_slot, int32_t num_
 /* Workspace (floats) for vg_graphnorm_fwd / _bwd. */
 int64_t vg_graphnorm_ws_floats(int32_t num_nodes, int32_t channels);
 
-/* y = keep * relu(weight * (x - mean_scale*mu) / (sigma + eps) + bias)
- * with mu, sigma the population column statistics over all N rows.
- * Replaces GraphNorm(x) (torch_geometric/nn/norm/graph_norm.py, batch=None) ->
- * nn.ReLU(True) -> nn.Dropout(0.2) at models.py:73-75,83-85,193-195,203-205.
+/* o = x - mean_scale*mu, d = sqrt(mean_rows(o^2) + eps),
+ * y = keep * relu(weight * o / d + bias), with mu the column mean over all N
+ * rows.  Replaces GraphNorm(x) (torch_geometric 2.6.1
+ * nn/norm/graph_norm.py, batch=None) -> nn.ReLU(True) -> nn.Dropout(0.2) at
+ * models.py:73-75,83-85,193-195,203-205.
  * keep (N*C, already scaled by 1/(1-p)) may be NULL (eval / no dropout).
- * stats (2C) receives [mu | sigma]. */
+ * stats (2C) receives [mu | d]; every function below that reads stats takes
+ * d as the whole denominator (its eps argument is the statistics pass's). */
 int vg_graphnorm_fwd(const float* x, int32_t num_nodes, int32_t channels, const float* weight,
                      const float* bias, const float* mean_scale, const float* keep, float eps,
                      float* y, float* stats, float* workspace, void* stream);
@@ -588,7 +590,7 @@ int vg_gat_lin_att_gn(const float* X, const float* W, int32_t N, int32_t Cin, in
 /* Only the column statistics of vg_graphnorm_fwd_gnp (the fold of the
  * aggregation's partials), for vg_gat_lin_att_gn. */
 int vg_graphnorm_stats_gnp(int32_t segments, int32_t rows, int32_t channels, const float* gnp, int32_t gnp_rows,
-                           float* stats, void* stream);
+                           const float* mean_scale, float eps, float* stats, void* stream);
 
 /* ---- the tangent sweep's GraphNorm sums in the GAT tangent pass ------------ */
 

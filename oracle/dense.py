@@ -33,7 +33,11 @@ def gat_dense(x, weight, att_src, att_dst, bias, edge_index, slope: float = 0.2)
 
 
 def graphnorm_dense(x, weight, bias, mean_scale, eps: float = 1e-5):
+    """Column sums written out: mu = 1'x / n, o = x - s*mu, and the second
+    moment of o expanded as var(x) + ((1 - s) mu)^2 (o's mean is (1 - s) mu),
+    rather than oracle.pyg's mean(o^2) directly."""
     n = x.shape[0]
     mu = x.sum(0) / n
-    var = ((x - mu) ** 2).sum(0) / n  # std is shift invariant: std(x - s*mu) == std(x)
-    return weight * (x - mean_scale * mu) / (var.sqrt() + eps) + bias
+    var_x = (x * x).sum(0) / n - mu * mu
+    var_o = var_x + ((1 - mean_scale) * mu) ** 2
+    return weight * (x - mean_scale * mu) / torch.sqrt(var_o + eps) + bias

@@ -138,7 +138,11 @@ def gat_propagate(h: torch.Tensor, a_src: torch.Tensor, a_dst: torch.Tensor, edg
 
 # ------------------------------------------------------------ graph_norm.py
 class GraphNorm(nn.Module):
-    """GraphNorm(C); the reference only ever calls it as ``norm(x)`` (batch=None)."""
+    """GraphNorm(C); the reference only ever calls it as ``norm(x)`` (batch=None).
+
+    nn/norm/graph_norm.py (2.6.1) ``forward``, batch=None branch:
+    ``out = x - mean(x) * mean_scale``; ``var = mean(out ** 2)``;
+    ``std = sqrt(var + eps)``; ``weight * out / std + bias``."""
 
     def __init__(self, in_channels: int, eps: float = GRAPHNORM_EPS):
         super().__init__()
@@ -151,9 +155,10 @@ class GraphNorm(nn.Module):
                 batch_size: Optional[int] = None) -> torch.Tensor:
         if batch is not None:
             raise NotImplementedError("the reference path never passes a batch vector")
-        centred = x - x.mean(dim=0, keepdim=True) * self.mean_scale
-        scaled = centred / (centred.std(dim=0, unbiased=False, keepdim=True) + self.eps)
-        return scaled * self.weight + self.bias
+        out = x - x.mean(dim=0, keepdim=True) * self.mean_scale
+        var = out.pow(2).mean(dim=0, keepdim=True)
+        std = (var + self.eps).sqrt()
+        return self.weight * out / std + self.bias
 
 
 # ------------------------------------------------------------ sequential.py

@@ -78,7 +78,7 @@ def gat_fn(edge_index, n):
 def gnrd_fn(keep, eps=1e-5):
     def f(o, w, b, s):
         c = o - o.mean(dim=0, keepdim=True) * s
-        y = c / (c.std(dim=0, unbiased=False, keepdim=True) + eps) * w + b
+        y = w * c / (c.pow(2).mean(dim=0, keepdim=True) + eps).sqrt() + b
         y = torch.relu(y)
         return y * keep if keep is not None else y
     return f

@@ -22,6 +22,11 @@ step_tiny.pt      the same step for a 4-building batch and a reduced config
                   (hidden 16, GAT depth 2) -- exercises the per-building loops.
 forward_b32_f64.pt  forward_b32.pt's generator loss and G gradients in f64
                   (same models, draws and reference code; default dtype f64).
+forward_b32_perturbed.pt  forward_b32.pt's outputs with every G / D parameter
+                  moved off its initial value (``perturb``: GraphNorm weight /
+                  bias / mean_scale in U(0.3, 1.5) / U(-0.5, 0.5) / U(0.2, 1.2),
+                  nonzero GATConv biases, LayerNorm affine and every weight
+                  scaled), the perturbed state dicts stored with them.
 ops_small.pt      oracle per-op goldens (GATConv at C_out 1..128, GraphNorm,
                   type-matched mean), cross-checked against ``oracle.dense``.
 
@@ -129,7 +134,29 @@ def make_forward_eval(cfgmod, models, trainer_mod):
     }
 
 
-def make_forward_b32(cfgmod, models, trainer_mod):
+def perturb(module, gen):
+    """Trained-like parameters: every tensor of the state dict moved off its
+    initial value with draws from ``gen`` (state_dict order)."""
+    with torch.no_grad():
+        for name, p in module.named_parameters():
+            leaf = name.rsplit(".", 1)[-1]
+            u = lambda lo, hi: torch.empty(p.shape).uniform_(lo, hi, generator=gen)  # noqa: E731
+            owner = module.get_submodule(name.rsplit(".", 1)[0])
+            if type(owner).__name__ == "GraphNorm":
+                p.copy_({"weight": u(0.3, 1.5), "bias": u(-0.5, 0.5), "mean_scale": u(0.2, 1.2)}[leaf])
+            elif type(owner).__name__ == "LayerNorm":
+                p.copy_(u(0.6, 1.4) if leaf == "weight" else u(-0.3, 0.3))
+            elif leaf == "bias":  # Linear and GATConv biases
+                p.copy_(u(-0.3, 0.3))
+            else:  # Linear / GATConv lin weights, att_src / att_dst
+                p.mul_(u(0.7, 1.3))
+
+
+def make_forward_b32_perturbed(cfgmod, models, trainer_mod):
+    return make_forward_b32(cfgmod, models, trainer_mod, perturb_seed=3001)
+
+
+def make_forward_b32(cfgmod, models, trainer_mod, perturb_seed=None):
     """The benchmarked size (BASELINE.json configs[1]): batch 32 =
     SyntheticDataset(6500, seed=777)[0..31] (bench.py's first pooled batch),
     full-size G and D from torch.manual_seed(777), eval mode.  The inputs are
@@ -143,6 +170,10 @@ def make_forward_b32(cfgmod, models, trainer_mod):
     torch.manual_seed(777)
     G = models.VoxelGNNGenerator(cfg, 17, 12)
     D = models.VoxelGNNDiscriminator(cfg, 17, 12)
+    if perturb_seed is not None:
+        gen = torch.Generator().manual_seed(perturb_seed)
+        perturb(G, gen)
+        perturb(D, gen)
     G.eval()
     D.eval()
     n = voxel.num_nodes
@@ -170,13 +201,16 @@ def make_forward_b32(cfgmod, models, trainer_mod):
     g_loss = tr._compute_generator_loss(local, voxel, logits_g, hard_g.unsqueeze(0))
     g_loss.backward()
     g_grads = {k: p.grad.detach().clone() for k, p in G.named_parameters()}
-    return {
+    out = {
         "batch_checksum": batch_checksum(local, voxel), "num_nodes": n, "num_buildings": len(items),
         "dataset_seed": 777, "init_seed": 777, "z_seed": 2001, "gumbel_seed": 2002, "gp_seed": 2003,
         "logits": logits, "label_soft": soft, "label_argmax": hard.argmax(1).to(torch.int8),
         "d_real": d_real, "d_hard": d_hard, "d_loss": d_loss.detach(), "d_grads": d_grads,
         "g_loss": g_loss.detach(), "g_grads": g_grads,
     }
+    if perturb_seed is not None:
+        out.update({"perturb_seed": perturb_seed, "G": clone_sd(G), "D": clone_sd(D)})
+    return out
 
 
 def make_forward_b32_f64(cfgmod, models, trainer_mod):
@@ -342,6 +376,7 @@ def main():
         "forward_eval.pt": lambda: make_forward_eval(cfgmod, models, trainer_mod),
         "forward_b32.pt": lambda: make_forward_b32(cfgmod, models, trainer_mod),
         "forward_b32_f64.pt": lambda: make_forward_b32_f64(cfgmod, models, trainer_mod),
+        "forward_b32_perturbed.pt": lambda: make_forward_b32_perturbed(cfgmod, models, trainer_mod),
         "step_sanity.pt": lambda: make_step_sanity(cfgmod, models, trainer_mod),
         "step_tiny.pt": lambda: make_step_tiny(cfgmod, models, trainer_mod),
         "ops_small.pt": make_ops_small,

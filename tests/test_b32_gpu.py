@@ -13,6 +13,13 @@ self loops), full-size models from torch.manual_seed(777).
   critic-label forward, the aggregation's GraphNorm partials (``_gnp``) and the
   padded column array (ELL) -- against the eager ``step`` iteration by
   iteration from identical state (the eager step is the one the oracle pins).
+
+Every test runs twice: at the initial parameters (forward_b32.pt) and at
+trained-like ones (forward_b32_perturbed.pt: every GraphNorm weight / bias /
+mean_scale, GATConv bias, LayerNorm affine and weight moved off its initial
+value, the reference executed on them) -- at init GraphNorm's mean_scale is 1
+and the GATConv biases 0, which leaves terms of the forward and of every
+gradient at exactly zero.
 """
 import pytest
 import torch
@@ -25,15 +32,24 @@ from vgan.trainer import Trainer
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def b32():
-    f = load_fixture("forward_b32.pt")
+@pytest.fixture(scope="module", params=["forward_b32.pt", "forward_b32_perturbed.pt"], ids=["init", "perturbed"])
+def b32(request):
+    f = load_fixture(request.param)
     return f, b32_inputs(f, device="cuda")
+
+
+def _load_perturbed(f, G, D):
+    """The perturbed fixture's trained-like parameters (no-op at init)."""
+    if "G" in f:
+        G.load_state_dict(f["G"])
+        D.load_state_dict(f["D"])
 
 
 def _models(cfg, f):
     torch.manual_seed(int(f["init_seed"]))
-    return VoxelGNNGenerator(cfg, 17, 12), VoxelGNNDiscriminator(cfg, 17, 12)
+    G, D = VoxelGNNGenerator(cfg, 17, 12), VoxelGNNDiscriminator(cfg, 17, 12)
+    _load_perturbed(f, G, D)
+    return G, D
 
 
 def test_b32_eval_logits_within_1e3(cuda, b32):
@@ -125,6 +141,8 @@ def test_b32_generator_grads_against_f64_reference(cuda, b32):
     from parity_util import load_fixture
 
     f, inp = b32
+    if "G" in f:
+        pytest.skip("the f64 reference fixture is at the initial parameters")
     f64 = load_fixture("forward_b32_f64.pt")
     assert torch.equal(f64["batch_checksum"], f["batch_checksum"])
     assert torch.equal(f64["label_argmax"], f["label_argmax"])
@@ -166,6 +184,7 @@ def test_b32_step_each_iteration_matches_oracle(cuda, b32):
     from oracle import reference as R
 
     G0, D0 = R.Generator(cfg), R.Discriminator(cfg)
+    _load_perturbed(f, G0, D0)
     sd_g = {k: v.clone() for k, v in G0.state_dict().items()}
     sd_d = {k: v.clone() for k, v in D0.state_dict().items()}
     # the generator gradient per parameter at 2e-2 (the mean_scale / att_src
@@ -177,9 +196,10 @@ def _flat_grads(flat, module):
     return {k: flat.grad[flat._offset(p):flat._offset(p) + p.numel()].clone() for k, p in module.named_parameters()}
 
 
-def _trainer(cfg, seed=777):
+def _trainer(cfg, f, seed=777):
     torch.manual_seed(seed)
     G, D = VoxelGNNGenerator(cfg, 17, 12), VoxelGNNDiscriminator(cfg, 17, 12)
+    _load_perturbed(f, G, D)
     og = torch.optim.Adam(G.parameters(), lr=cfg.LEARNING_RATE_GENERATOR, betas=cfg.BETAS)
     od = torch.optim.Adam(D.parameters(), lr=cfg.LEARNING_RATE_DISCRIMINATOR, betas=cfg.BETAS)
     return Trainer(G, D, None, og, od, None, cfg)
@@ -202,7 +222,7 @@ def test_b32_graphed_step_matches_eager(cuda, b32):
     cfg = Configuration()
     cfg.DEVICE = str(cuda)
     cfg.runtime["rng"] = "device"
-    eager, graphed = _trainer(cfg), _trainer(cfg)
+    eager, graphed = _trainer(cfg, f), _trainer(cfg, f)
     loc, vox = inp["vgan"]
     prep = vdata.prepared(loc, vox, cfg.NUM_CLASSES)
     assert prep.csr.ell()[0] is not None and ops._GN_FWD_FUSE  # the variants the bench times
@@ -278,6 +298,8 @@ def test_prepared_cache_keys_on_both_graphs(cuda, b32):
     from vgan import ops
 
     f, inp = b32
+    if "G" in f:
+        pytest.skip("parameter-independent")
     loc, vox = inp["vgan"]
     loc2 = types.SimpleNamespace(x=loc.x.flip(0).contiguous(), type=loc.type.flip(0).contiguous())
     loc2.x[:, :7] = loc2.x[:, :7] * 0.5  # other program features

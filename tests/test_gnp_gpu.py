@@ -42,9 +42,9 @@ def _gn_torch(x, S, w, b, ms, keep=None):
     for xs in x.chunk(S):
         mu = xs.mean(0)
         c = xs - mu * ms
-        sd = c.std(0, unbiased=False)
-        ys.append(torch.relu(c / (sd + EPS) * w + b))
-        stats.append(torch.cat([mu, sd]))
+        d = (c.pow(2).mean(0) + EPS).sqrt()  # PyG 2.6.1 GraphNorm(batch=None): stats = [mu | d]
+        ys.append(torch.relu(w * c / d + b))
+        stats.append(torch.cat([mu, d]))
     y = torch.cat(ys)
     return (y * keep if keep is not None else y), torch.cat(stats)
 
@@ -348,6 +348,7 @@ def test_stacked_statistics_bitwise_equal_separate(cuda, C):
     ass = [0.5 * torch.randn(n, device=cuda) for _ in range(3)]
     ads = [0.5 * torch.randn(n, device=cuda) for _ in range(3)]
     b = torch.randn(C, device=cuda)
+    ms = torch.rand(C, device=cuda) + 0.2
     st = ops.stream_handle(cuda)
 
     def run(graph, h, a_s, a_d, segs):
@@ -355,7 +356,8 @@ def test_stacked_statistics_bitwise_equal_separate(cuda, C):
         out, alpha = torch.empty_like(h), torch.empty(graph.num_edges, device=cuda)
         ops.aggregate_fwd_raw(graph, C, ptr(h), ptr(a_s), ptr(a_d), ptr(b), 0.2, ptr(out), ptr(alpha), st, gnp)
         stats = torch.empty(segs * 2 * C, device=cuda)
-        check(LIB.vg_graphnorm_stats_gnp(segs, n, C, ptr(gnp), g, ptr(stats), st), "vg_graphnorm_stats_gnp")
+        check(LIB.vg_graphnorm_stats_gnp(segs, n, C, ptr(gnp), g, ptr(ms), 1e-5, ptr(stats), st),
+              "vg_graphnorm_stats_gnp")
         return out, stats
 
     out3, s3 = run(st3, torch.cat(hs).contiguous(), torch.cat(ass), torch.cat(ads), 3)

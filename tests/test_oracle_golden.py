@@ -103,13 +103,31 @@ def test_oracle_graphnorm_matches_dense_and_zero_variance():
     y = gn(x)
     assert torch.allclose(y.float(), f["out"], atol=1e-5)
     assert torch.allclose(y, dense.graphnorm_dense(x, gn.weight, gn.bias, gn.mean_scale), atol=1e-10)
-    # a constant column: std 0 -> torch masks the std gradient to 0 (finite grads)
+    # a constant column: var(o) = ((1 - ms) mu)^2, finite gradients (eps inside the sqrt)
     xc = torch.randn(50, 3, dtype=torch.float64)
     xc[:, 1] = 2.5
     xc.requires_grad_(True)
     gn3 = pyg.GraphNorm(3).double()
     gn3(xc).sum().backward()
     assert torch.isfinite(xc.grad).all()
+    # the published semantics: variance of o = x - ms * mu itself, eps under the
+    # square root (torch_geometric 2.6.1 nn/norm/graph_norm.py); f64 gradgradcheck
+    # of the oracle at mean_scale != 1 against the dense derivation's autograd
+    gn4 = pyg.GraphNorm(4).double()
+    with torch.no_grad():
+        gn4.mean_scale.copy_(torch.tensor([0.3, 0.8, 1.0, 1.4], dtype=torch.float64))
+        gn4.weight.uniform_(0.5, 1.5)
+    x4 = (torch.randn(40, 4, dtype=torch.float64) * 0.2 + 0.5).requires_grad_(True)
+    o = x4.detach() - x4.detach().mean(0) * gn4.mean_scale.detach()
+    want = gn4.weight.detach() * o / (o.pow(2).mean(0) + 1e-5).sqrt() + gn4.bias.detach()
+    assert torch.allclose(gn4(x4), want, atol=1e-12)
+    params = (x4, gn4.weight, gn4.bias, gn4.mean_scale)
+    dense_fn = lambda x, w, b, s: dense.graphnorm_dense(x, w, b, s)  # noqa: E731
+    assert torch.autograd.gradgradcheck(dense_fn, params)
+    g1 = torch.autograd.grad(gn4(x4).pow(2).sum(), params, create_graph=True)
+    g2 = torch.autograd.grad(dense_fn(*params).pow(2).sum(), params, create_graph=True)
+    for a, b in zip(g1, g2):
+        assert torch.allclose(a, b, atol=1e-10)
 
 
 def test_oracle_type_mean_fixture():
@@ -135,19 +153,25 @@ def test_configuration_matches_reference_values():
         assert mine[k] == v, (k, mine[k], v)
 
 
-def test_oracle_matches_reference_at_batch_32():
+@pytest.mark.parametrize("name", ["forward_b32.pt", "forward_b32_perturbed.pt"])
+def test_oracle_matches_reference_at_batch_32(name):
     """The benchmarked size (configs[1], 32 buildings, ~12.7k voxels): the
     restatement reproduces the reference-executed forward_b32.pt -- logits,
     D scores, WGAN-GP loss with its second-order D gradients, generator loss
-    with its G gradients -- bit for bit."""
+    with its G gradients -- bit for bit; and so at the perturbed, trained-like
+    parameters of forward_b32_perturbed.pt (GraphNorm mean_scale != 1, GATConv
+    biases != 0)."""
     from parity_util import b32_inputs
 
-    f = load_fixture("forward_b32.pt")
+    f = load_fixture(name)
     inp = b32_inputs(f, device=None)
     local, voxel = inp["oracle"]
     cfg = Configuration()
     torch.manual_seed(int(f["init_seed"]))
     G, D = R.Generator(cfg), R.Discriminator(cfg)
+    if "G" in f:
+        G.load_state_dict(f["G"])
+        D.load_state_dict(f["D"])
     G.eval()
     D.eval()
     with torch.no_grad():
