@@ -3,6 +3,11 @@
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N ...
 
+``--gpus N`` (N > 1) without a torch.distributed environment starts the N
+ranks itself (``torch.distributed.run`` in a child process, before anything
+touches the GPU) and relays rank 0's line; under torchrun each rank reads
+RANK / LOCAL_RANK / WORLD_SIZE from the environment.
+
 Workload (BASELINE.json configs[1]): 6-type synthetic dataset, batch = 32
 voxel graphs per GPU, fp32, the full step of trainer.py:466-495 (5 critic
 iterations with WGAN-GP + 1 generator iteration, Adam steps included, sklearn
@@ -306,10 +311,12 @@ def run_steps(tr, pool, k: int, offset: int = 0):
     return out
 
 
-def timed_steps(tr, pool, steps: int, warmup: int, world: int, device, profile: bool = False):
+def timed_steps(tr, pool, steps: int, warmup: int, world: int, device, profile: bool = False, per_step=None):
     """Warm-up (every pooled batch once: its CSR / type-mean / graphs), then
     ``steps`` timed steps between barrier + synchronize on both sides; the
-    max over ranks.  Returns seconds."""
+    max over ranks.  Returns seconds.  ``per_step`` (a list) receives each
+    step's milliseconds from HIP events recorded between the steps on the
+    replay stream (no host synchronisation inside the timed region)."""
     for (loc, vox) in pool:
         run_steps(tr, [(loc, vox)], 1)
     run_steps(tr, pool, warmup)
@@ -319,15 +326,22 @@ def timed_steps(tr, pool, steps: int, warmup: int, world: int, device, profile: 
     torch.cuda.synchronize()
     if profile:
         time.sleep(0.05)  # idle gap that tools/prof_summary.py --after-gap keys on
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)] if per_step is not None else None
     t0 = time.perf_counter()
+    if evs:
+        evs[0].record()
     for s in range(steps):
         run_steps(tr, pool, 1, offset=s)
+        if evs:
+            evs[s + 1].record()
         if (s + 1) % 10 == 0:
             log(f"step {s + 1}/{steps}")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if evs:
+        per_step.extend(evs[i].elapsed_time(evs[i + 1]) for i in range(steps))
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -609,11 +623,16 @@ def cpu_baseline(cfg_batch: int, seconds_budget: float):
     from vgan.config import Configuration
     from vgan.synth import SyntheticDataset
 
-    threads = len(os.sched_getaffinity(0))
+    affinity = len(os.sched_getaffinity(0))
     cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    if cap > 0:
-        threads = min(threads, cap)
+    threads = min(affinity, cap) if cap > 0 else affinity
     torch.set_num_threads(threads)
+    cpu_model = None
+    try:
+        with open("/proc/cpuinfo") as fh:
+            cpu_model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), None)
+    except OSError:
+        pass
     cfg = Configuration()
     ds = SyntheticDataset(6500, seed=777)
     items = [ds[i] for i in range(cfg_batch)]
@@ -625,25 +644,102 @@ def cpu_baseline(cfg_batch: int, seconds_budget: float):
     G, D = R.Generator(cfg), R.Discriminator(cfg)
     og = torch.optim.Adam(G.parameters(), lr=cfg.LEARNING_RATE_GENERATOR, betas=cfg.BETAS)
     od = torch.optim.Adam(D.parameters(), lr=cfg.LEARNING_RATE_DISCRIMINATOR, betas=cfg.BETAS)
-    steps, t_total = 0, 0.0
-    while True:
+    t0 = time.perf_counter()
+    R.train_step(G, D, og, od, cfg, local, voxel)  # warm-up: allocator, thread pool
+    log(f"cpu baseline warm-up step: {time.perf_counter() - t0:.2f} s")
+    times = []
+    while True:  # at least 3 timed steps, more while the budget lasts (at most 7)
         t0 = time.perf_counter()
         R.train_step(G, D, og, od, cfg, local, voxel)
-        t_total += time.perf_counter() - t0
-        steps += 1
-        log(f"cpu baseline step {steps}: {t_total / steps:.2f} s/step")
-        if t_total >= seconds_budget * 0.5 or steps >= 3:
+        times.append(time.perf_counter() - t0)
+        log(f"cpu baseline step {len(times)}: {times[-1]:.2f} s")
+        if len(times) >= 3 and (sum(times) >= seconds_budget or len(times) >= 7):
             break
+    med = sorted(times)[len(times) // 2]
     return {
-        "value": round(cfg_batch * steps / t_total, 3),
+        "value": round(cfg_batch / med, 3),
         "unit": "graphs/s",
         "cores": torch.get_num_threads(),
         "kind": "port",
-        "sample": f"{steps} full G+D step(s) of batch {cfg_batch} synthetic buildings "
+        "cpu_model": cpu_model,
+        "affinity_cpus": affinity,
+        "threads_note": (f"torch threads = min(sched_getaffinity {affinity}, OMP_NUM_THREADS {cap}): the pool sets "
+                         f"OMP_NUM_THREADS to the per-GPU CPU share of the box" if cap > 0 and cap < affinity else
+                         "torch threads = every CPU of sched_getaffinity"),
+        "statistic": f"median of {len(times)} timed steps after 1 warm-up step",
+        "step_seconds": [round(t, 3) for t in times],
+        "sample": f"full G+D steps of batch {cfg_batch} synthetic buildings "
                   f"({voxel.num_nodes} voxel nodes) through the CPU oracle (oracle/reference.py, "
                   f"pinned bit-for-bit to the reference's own trainer.py step), fp32, "
-                  f"{t_total / steps:.2f} s/step",
+                  f"{med:.2f} s/step (median)",
     }
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def self_launch(n: int) -> int:
+    """``--gpus N`` with no torch.distributed environment: run the N ranks as
+    ``python -m torch.distributed.run --nproc-per-node N ... bench.py <same
+    arguments>`` in a child process (this process never touches the GPU and
+    never execs); the ranks inherit stdout, so rank 0's JSON line is this
+    command's output.  Returns the launcher's exit status."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    log(f"--gpus {n}: launching {n} ranks ({' '.join(cmd[1:6])} ...)")
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", os.environ.get("OMP_NUM_THREADS", "8"))
+    return subprocess.call(cmd, env=env)
+
+
+def rehearse(args, rank: int, world: int) -> None:
+    """``--rehearse``: the N-rank plumbing without a GPU (CPU container,
+    VGAN_DIST_BACKEND=gloo) -- self-launch, process group, barriers around the
+    timed region, max over ranks, one line from rank 0.  The "step" is a fixed
+    CPU matmul, so the line carries no throughput (value null)."""
+    if world > 1:
+        dist.init_process_group(os.environ.get("VGAN_DIST_BACKEND", "gloo"), rank=rank, world_size=world)
+    a = torch.randn(256, 256)
+    for _ in range(args.warmup):
+        a = torch.tanh(a @ a)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        a = torch.tanh(a @ a)
+    if world > 1:
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    ws = dist.get_world_size() if world > 1 else 1
+    if world > 1:
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "graphs/s", "n_gpus": world, "world_size": ws,
+                          "steps": args.steps, "warmup": args.warmup, "rehearsal": True,
+                          "elapsed_s_max_over_ranks": round(float(el), 6)}), flush=True)
+
+
+def median_leg(tr, pool, steps: int, world: int, device):
+    """SURVEY.md 8(d)'s statistic: the median of ``steps`` steps' HIP-event
+    durations (max over ranks of each rank's median), after the pool's
+    batches have run once."""
+    per = []
+    timed_steps(tr, pool, steps, 0, world, device, per_step=per)
+    med = sorted(per)[len(per) // 2]
+    if world > 1:
+        t = torch.tensor([med], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        med = float(t.item())
+    return med
 
 
 def main():
@@ -670,15 +766,24 @@ def main():
                     help="with --roofline-only: the variant the step runs (vg_gat_aggregate_fwd_gnp)")
     ap.add_argument("--no-fresh", action="store_true", help="skip the fresh-batch (Trainer.train path) leg")
     ap.add_argument("--no-sweep", action="store_true", help="skip the configs[4] inference-sweep leg")
+    ap.add_argument("--median-steps", type=int, default=50,
+                    help="steps of the extra median leg (SURVEY.md 8(d): median of 50); 0 skips it")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="the N-rank launch / barrier / max-over-ranks plumbing on the CPU (no GPU, no throughput)")
     args = ap.parse_args()
     global GRAPHED
     GRAPHED = not args.eager
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(self_launch(args.gpus))  # before anything touches the GPU
     rank, world, local = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(
         os.environ.get("LOCAL_RANK", 0))
-    want_sweep = rank == 0 and not args.no_sweep and not args.profile and not args.roofline_only
     if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.rehearse:
+        rehearse(args, rank, world)
+        return
+    want_sweep = rank == 0 and not args.no_sweep and not args.profile and not args.roofline_only
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a ROCm GPU")
     # VGAN_DIST_BACKEND=gloo rehearses the N>1 path (barriers, rank sharding,
@@ -726,11 +831,24 @@ def main():
         return
 
     # warm-up (also builds every batch's CSR / type-mean once, as the first step of a batch would)
-    elapsed = timed_steps(tr, pool, args.steps, args.warmup, world, device, profile=args.profile)
+    per_step = []
+    elapsed = timed_steps(tr, pool, args.steps, args.warmup, world, device, profile=args.profile,
+                          per_step=None if args.profile else per_step)
     value = args.batch * world * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
     log(f"timed ({'hipGraph' if GRAPHED else 'eager'}, {args.precision}): {ms_per_step:.2f} ms/step, "
         f"{value:.1f} graphs/s")
+    median = None
+    if not args.profile and args.median_steps > 0:
+        med = median_leg(tr, pool, args.median_steps, world, device)
+        k_med = sorted(per_step)[len(per_step) // 2] if per_step else None
+        median = {"ms_per_step": round(med, 4), "value": round(args.batch * world / (med * 1e-3), 3),
+                  "steps": args.median_steps,
+                  "timed_region_median_ms": round(k_med, 4) if k_med is not None else None,
+                  "how": f"median of {args.median_steps} further steps' HIP-event durations (events between "
+                         f"steps on the replay stream, no host sync inside), max over ranks; "
+                         f"timed_region_median_ms: the same over the {args.steps} steps of the timed region"}
+        log(f"median of {args.median_steps} steps: {med:.3f} ms/step ({median['value']:.1f} graphs/s)")
 
     if args.profile:
         if rank == 0:
@@ -820,6 +938,8 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
+            "median": median,
+            "world_size": dist.get_world_size() if world > 1 else 1,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

@@ -73,10 +73,10 @@ def _from_host(local_graph, voxel_graph, n_classes: int):
         return None
     vx = voxel_graph.x
     v = pa["views"]
-    versions = tuple(t._version for t in (local_graph.x, local_graph.type, vx, voxel_graph.type,
-                                          voxel_graph.types_onehot, voxel_graph.edge_index))
-    if pa["local"] != (local_graph.x.data_ptr(), local_graph.type.data_ptr()) or vx.dtype != torch.float32 \
-            or pa.get("versions") != versions \
+    # every input exactly as stamped at upload (address, shape, version): a
+    # replaced attribute (voxel.x = voxel.x + noise, a new edge_index) starts
+    # at version 0 again and is caught by its address
+    if pa.get("inputs_key") != _inputs_key(local_graph, voxel_graph) or vx.dtype != torch.float32 \
             or any(t.device != vx.device for t in v.values()) or arrays[0].device != vx.device:
         return None
     n = vx.shape[0]

@@ -41,11 +41,13 @@ def tile_order(location: torch.Tensor, tile: int = 4) -> torch.Tensor:
 
 
 # node-level attributes of a voxel building (VoxelGraphData, data.py:48-77 and
-# the keys vgan.synth / vgan.convert add): gathered by the permutation
+# the keys vgan.synth / vgan.convert add): gathered by the permutation.
+# node_ratio is per node on a voxel graph ([N, 1]: the building's ratio of
+# each voxel's type, data.py:76-77,144; vgan/convert.py:165,184).
 NODE_KEYS = ("x", "type", "types_onehot", "voxel_level", "coordinate", "dimension", "location", "site_area",
-             "data_number")
-# per-building attributes (vgan.convert's type ratio vector [K]): carried unchanged
-GRAPH_KEYS = ("node_ratio",)
+             "data_number", "node_ratio")
+# per-building attributes: carried unchanged (none on a voxel graph today)
+GRAPH_KEYS: tuple = ()
 
 
 def renumber(voxel: GraphData, perm: torch.Tensor) -> GraphData:

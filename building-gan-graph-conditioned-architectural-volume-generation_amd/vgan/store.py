@@ -453,11 +453,14 @@ def upload_pair(local: GraphBatch, voxel: GraphBatch, device, non_blocking: bool
 
 
 def _stamp_versions(local: GraphBatch, voxel: GraphBatch) -> None:
-    """The inputs' autograd version counters when the prepared structures
-    were built: an in-place edit afterwards invalidates them (vgan.data)."""
+    """The identity of every input when the prepared structures were built --
+    address, shape and autograd version of each tensor (``vgan.data._inputs_key``):
+    an in-place edit, or an attribute REPLACED by a new tensor (whose version
+    is 0 again), afterwards invalidates them."""
+    from .data import _inputs_key
+
     pa = voxel.derived("prepared_arrays")
-    pa["versions"] = tuple(t._version for t in (local.x, local.type, voxel.x, voxel.type, voxel.types_onehot,
-                                                voxel.edge_index))
+    pa["inputs_key"] = _inputs_key(local, voxel)
 
 
 def write_store(path: str, dataset, indices: Optional[Sequence[int]] = None) -> GraphStore:

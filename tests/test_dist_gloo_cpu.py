@@ -197,3 +197,26 @@ def test_eval_loader_keeps_every_batch_and_resident_replays_objects(tmp_path):
     first = list(ld)
     second = list(ld)
     assert len(first) == 2 and all(x[1] is y[1] for x, y in zip(first, second))
+
+
+def test_bench_launches_its_own_ranks():
+    """``python bench.py --gpus 2`` with no torchrun environment starts the two
+    ranks itself and relays rank 0's one JSON line; the
+    CPU rehearsal (gloo, no GPU) runs the launch, the process group, the
+    barriers and the max over ranks."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT")}
+    env["VGAN_DIST_BACKEND"] = "gloo"
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--rehearse", "--steps", "3",
+                          "--warmup", "1"], env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["world_size"] == 2 and rec["rehearsal"] is True

@@ -94,6 +94,30 @@ def test_renumber_refuses_unknown_attributes():
     assert v2.data_number == [v.data_number[int(i)] for i in perm]
 
 
+def test_renumber_converted_building_permutes_node_ratio():
+    """A building converted from the reference's JSON (vgan.convert, pinned by
+    tests/golden/convert_small.pt): every per-node attribute -- node_ratio
+    [N, 1] included -- follows the permutation."""
+    import json
+    import os
+
+    from vgan import convert
+    from vgan.config import Configuration
+
+    fx = torch.load(os.path.join(os.path.dirname(__file__), "golden", "convert_small.pt"), weights_only=True)
+    b = fx["buildings"][0]
+    lo, vo = convert.process_building(json.loads(b["global_json"]), json.loads(b["local_json"]),
+                                      json.loads(b["voxel_json"]), Configuration(), b["data_number"])
+    _, v = convert.to_graph_pair(lo, vo)  # every attribute the store keeps
+    n = v.num_nodes
+    assert v.node_ratio.shape == (n, 1) and v.node_ratio.unique().numel() > 1
+    v2, perm = tiled(v, 4)
+    assert torch.equal(v2.node_ratio, v.node_ratio[perm])
+    assert torch.equal(v2.type, v.type[perm]) and torch.equal(v2.location, v.location[perm])
+    v3, perm3 = blocked(v, (4, 4, 4))
+    assert torch.equal(v3.node_ratio, v.node_ratio[perm3])
+
+
 @pytest.mark.gpu
 def test_aggregation_on_renumbered_graph_is_permuted_bitwise(cuda):
     from vgan import ops

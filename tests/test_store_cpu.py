@@ -324,3 +324,35 @@ def test_host_prepared_structures(tmp_path):
     # and the CSR itself is the oracle's GATConv edge list
     want = pyg.gat_csr(vox.edge_index, n)
     assert torch.equal(rp, want[0]) and torch.equal(col, want[1])
+
+
+def test_host_prepared_structures_refused_after_an_input_is_replaced(tmp_path, monkeypatch):
+    """vgan.data takes the host-built structures only for the exact tensors
+    they were built from: an attribute replaced by a NEW tensor (version 0
+    again, so a version check alone would pass) or edited in place gets a
+    fresh build instead of the stale type-mean / CSR."""
+    from vgan import data as vdata
+    from vgan.store import write_store
+    from vgan.synth import SyntheticDataset
+
+    class _CpuCSR:  # ops.CSR wants device arrays; the pairing check is what is tested
+        @staticmethod
+        def from_arrays(*arrays, max_degree=None):
+            return _CpuCSR()
+
+    monkeypatch.setattr(vdata.ops, "CSR", _CpuCSR)
+    ds = SyntheticDataset(6, seed=5)
+    st = write_store(str(tmp_path / "s"), ds)
+    loc, vox = st.collate([0, 2, 4], prepare=7)
+    assert vdata._from_host(loc, vox, 7) is not None
+    assert vdata._from_host(loc, vox, 5) is None  # another class count
+    old_x, old_ei = vox.x, vox.edge_index
+    vox.x = vox.x + 0.25  # replaced, version 0
+    assert vox.x._version == 0 and vdata._from_host(loc, vox, 7) is None
+    vox.x = old_x
+    assert vdata._from_host(loc, vox, 7) is not None
+    vox.edge_index = old_ei.flip(0).contiguous()  # new edges
+    assert vdata._from_host(loc, vox, 7) is None
+    vox.edge_index = old_ei
+    loc.x.mul_(2.0)  # in place
+    assert vdata._from_host(loc, vox, 7) is None
