@@ -150,6 +150,30 @@ class GraphLoader:
             self._resident_batches = kept
 
 
+# Prefetchers running at once and the switch interval before the first of
+# them: overlapping iterators (a validation loader started while a training
+# iterator is suspended) finish in any order, and the interval goes back only
+# when the last one ends (reference-counted like vgan.gcscope).
+_SWITCH_LOCK = threading.Lock()
+_SWITCH_STATE = {"active": 0, "saved": None}
+
+
+def _switch_enter() -> None:
+    with _SWITCH_LOCK:
+        if _SWITCH_STATE["active"] == 0:
+            _SWITCH_STATE["saved"] = sys.getswitchinterval()
+            sys.setswitchinterval(min(_SWITCH_STATE["saved"], _SWITCH_INTERVAL))
+        _SWITCH_STATE["active"] += 1
+
+
+def _switch_exit() -> None:
+    with _SWITCH_LOCK:
+        _SWITCH_STATE["active"] -= 1
+        if _SWITCH_STATE["active"] == 0:
+            sys.setswitchinterval(_SWITCH_STATE["saved"])
+            _SWITCH_STATE["saved"] = None
+
+
 def _prefetched(store: GraphStore, plan: List[List[int]], dev: torch.device, depth: int, threads: int,
                 prepare=None):
     copy_stream = torch.cuda.Stream(device=dev)
@@ -179,9 +203,8 @@ def _prefetched(store: GraphStore, plan: List[List[int]], dev: torch.device, dep
     # otherwise waits out whatever Python the worker is running (tensor views,
     # the batch objects) -- 10.1-10.7 vs 8.5 ms per fresh-batch step
     # (tools/fresh_probe.py, profiles/r04_fresh_probe.jsonl).  Restored when
-    # the iteration ends.
-    old_switch = sys.getswitchinterval()
-    sys.setswitchinterval(min(old_switch, _SWITCH_INTERVAL))
+    # the last running prefetcher ends.
+    _switch_enter()
     th.start()
     try:
         while True:
@@ -203,7 +226,7 @@ def _prefetched(store: GraphStore, plan: List[List[int]], dev: torch.device, dep
             del host
             yield moved
     finally:
-        sys.setswitchinterval(old_switch)
+        _switch_exit()
         stop.set()
         while th.is_alive():
             try:

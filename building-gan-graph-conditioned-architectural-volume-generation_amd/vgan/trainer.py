@@ -73,13 +73,29 @@ def _loss_pair(acc: torch.Tensor, i: int):
 
 class _StepOut(dict):
     """step_graphed's result: "d_loss_mean" is formed when first read (an
-    eager reduction launch per step otherwise, whether read or not)."""
+    eager reduction launch per step otherwise, whether read or not); ``in``,
+    ``get`` and ``keys()`` see it like any other key.
+
+    The tensors ALIAS the captured graphs' persistent slots: the next
+    ``step_graphed`` replay of the same batch overwrites them (clone to keep),
+    and a "d_loss_mean" first read after that replay is the later step's."""
+
+    _LAZY = ("d_loss_mean",)
 
     def __missing__(self, key):
-        if key != "d_loss_mean":
+        if key not in self._LAZY:
             raise KeyError(key)
         v = self[key] = self["d_losses"].mean()
         return v
+
+    def __contains__(self, key):
+        return key in self._LAZY or dict.__contains__(self, key)
+
+    def get(self, key, default=None):
+        return self[key] if key in self else default
+
+    def keys(self):
+        return list(dict.keys(self)) + [k for k in self._LAZY if not dict.__contains__(self, k)]
 
 
 class Trainer:
@@ -268,8 +284,9 @@ class Trainer:
         self._iter_begin(self.adam_g)
         if self.gen_engine is not None and self.skip_dead_d_grads:
             return self.gen_engine.loss_and_grad(local_graph, voxel_graph, self.rng, early=early)
-        if early is not None:  # the autograd path has no early bucket: the caller reduces it whole
-            early()
+        # the autograd path forms every gradient in one backward: an early
+        # bucket would be all-reduced before it holds anything
+        assert early is None, "early all-reduce needs the explicit generator schedule (gen_engine)"
         logits, hard, _ = self._generate(local_graph, voxel_graph)
         d_params = list(self.discriminator.parameters())
         if self.skip_dead_d_grads:

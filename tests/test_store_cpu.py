@@ -356,3 +356,22 @@ def test_host_prepared_structures_refused_after_an_input_is_replaced(tmp_path, m
     vox.edge_index = old_ei
     loc.x.mul_(2.0)  # in place
     assert vdata._from_host(loc, vox, 7) is None
+
+
+def test_prefetch_switch_interval_restored_after_the_last_prefetcher():
+    """Two overlapping loader iterators finishing in the opposite order: the
+    GIL switch interval stays lowered while either runs and is restored only
+    when the last one ends."""
+    import sys
+
+    from vgan import loader
+
+    base = sys.getswitchinterval()
+    loader._switch_enter()
+    low = sys.getswitchinterval()
+    assert low <= loader._SWITCH_INTERVAL
+    loader._switch_enter()  # a second iterator starts
+    loader._switch_exit()   # the FIRST one finishes
+    assert sys.getswitchinterval() == low
+    loader._switch_exit()
+    assert sys.getswitchinterval() == base
