@@ -395,16 +395,27 @@ int run(Ctx& cx, const vg_critic_model* md, const vg_critic_batch* bt, float* ou
     const float* gstats = S.stats ? S.stats + 2 * 2 * c : nullptr;
     float* oinj = cx.take((int64_t)n * c);
     float* gws2 = cx.take(vg_graphnorm_seg_ws_floats(1, n, c));
-    if (!cx.dry) {  // the GAT tangent with its folds deferred (FoldCollector.jvp)
+    if (!cx.dry) {
+      // the GAT tangent's destination-row pass, its folds deferred
+      // (FoldCollector.jvp) and its source pass described: the source pass
+      // writes only pass D's injection and att_src partials, so it runs in the
+      // GraphNorm fold's launch (vg_graphnorm_jvp2_fold_src) instead of one of
+      // its own -- the same kernels and values as vg_gat_jvp2_deferred +
+      // vg_graphnorm_jvp2, one launch fewer per block
       vg_fold f[2];
       int32_t nf = 0;
-      VG_TRY(vg_gat_jvp2_deferred(g1.row_ptr, g1.col, g1.csc_ptr, g1.csc_slot, g1.csc_dst, n, E, c, rows(S.H, mrow, c),
-                                  uH, dO_b[b], B.att_src, B.att_dst, S.a_s + mrow, S.a_d + mrow, S.alpha + 2LL * E,
-                                  B.slope, uO, hinj, B.g_att_src, B.g_att_dst, up_s, up_d, ws, f, &nf, cx.stream));
+      vg_jvp_src src;
+      VG_TRY(vg_gat_jvp2_plan(g1.row_ptr, g1.col, g1.csc_ptr, g1.csc_slot, g1.csc_dst, n, E, c, rows(S.H, mrow, c),
+                              uH, dO_b[b], B.att_src, B.att_dst, S.a_s + mrow, S.a_d + mrow, S.alpha + 2LL * E,
+                              B.slope, uO, hinj, B.g_att_src, B.g_att_dst, up_s, up_d, ws, f, &nf, &src, cx.stream));
       folds.add(f, nf);
+      VG_TRY(vg_graphnorm_jvp2_sums(gx, n, c, B.gn_weight, B.gn_bias, B.gn_mean_scale, gkeep, B.gn_eps, gstats, uO,
+                                    dY_b[b], gws2, cx.stream));
+      VG_TRY(vg_graphnorm_jvp2_fold_src(n, c, B.gn_weight, B.gn_mean_scale, gstats, gws2, B.g_gn_weight,
+                                        B.g_gn_mean_scale, &src, cx.stream));
+      VG_TRY(vg_graphnorm_jvp2_apply(gx, n, c, B.gn_weight, B.gn_bias, B.gn_mean_scale, gkeep, B.gn_eps, gstats, uO,
+                                     dY_b[b], rows(S.Y, trow, c), oinj, gws2, cx.stream));
     }
-    VG_RUN(vg_graphnorm_jvp2(gx, n, c, B.gn_weight, B.gn_bias, B.gn_mean_scale, gkeep, B.gn_eps, gstats, uO, dY_b[b],
-                             rows(S.Y, trow, c), oinj, B.g_gn_weight, B.g_gn_mean_scale, gws2, nullptr, cx.stream));
     hinj_b[b] = hinj;
     oinj_b[b] = oinj;
     u_in = rows(S.Y, trow, c);

@@ -22,6 +22,9 @@ namespace {
 #define VG_FOLD_SHORT_ROWS 256
 #endif
 constexpr int kShortRows = VG_FOLD_SHORT_ROWS;
+#ifndef VG_FOLD_PACK
+#define VG_FOLD_PACK 1  // narrow long folds with packed (row, column) lanes (0: the round-4 mapping, A/B)
+#endif
 
 struct FoldBatch {
   int32_t n;
@@ -155,7 +158,7 @@ extern "C" int vg_fold_batch(const vg_fold* folds, int32_t n, void* stream) {
     b.waves[i] = rows <= kShortRows ? 4 : 16;
     b.block0[i] = blocks;
     int cw = 0;
-    if (rows > kShortRows && f.width <= 32) {
+    if (VG_FOLD_PACK && rows > kShortRows && f.width <= 32) {
       cw = 1;
       while (cw < f.width) cw <<= 1;
     }

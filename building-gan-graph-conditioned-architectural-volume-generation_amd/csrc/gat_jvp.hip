@@ -21,6 +21,7 @@
 // destination rows (J u, per-edge gz / gzp / alpha', block partials of
 // dQ/datt_dst), source nodes over the CSC (dQ/dh, partials of dQ/datt_src),
 // then one fold that ADDS into g_att_src / g_att_dst.
+#include "gnjvp.h"
 #include "rowgroup.h"
 
 namespace {
@@ -326,6 +327,38 @@ __global__ void __launch_bounds__(kBlock) k_jvp_src_group(const JvpSrcGroup g) {
 #undef VG_JS
 }
 
+// The GraphNorm second-order fold (gnjvp.h: one wave per column, blocks
+// [0, C): wave 0 works, the others exit) and a described GAT tangent source
+// pass (blocks C ..: jvp_src_body) in ONE launch: the source pass's injections
+// and att_src partials are read only by the later VJP pass and the folds, so
+// it need not be a launch of its own on the tangent sweep's dependent chain
+// (vg_graphnorm_jvp2_fold_src).
+__global__ void __launch_bounds__(kBlock) k_jvp2_fold_src(const float* __restrict__ part, int chunks, int N, int C,
+                                                          const float* __restrict__ w, const float* __restrict__ ms,
+                                                          const float* __restrict__ stats, float* __restrict__ sums,
+                                                          float* __restrict__ g_w, float* __restrict__ g_ms,
+                                                          const vg_jvp_src d) {
+  if ((int)blockIdx.x < C) {
+    const int lane = threadIdx.x & 63;
+    if ((threadIdx.x >> 6) == 0) vg::gn_jvp2_fold_col(part, chunks, N, C, w, ms, stats, sums, g_w, g_ms, blockIdx.x, lane);
+    return;
+  }
+  const int nb = gridDim.x - C;
+  const int lb = xcd_remap(blockIdx.x - C, nb);
+#define VG_JS(L_, CPL_)                                                                                   \
+  jvp_src_body<L_, CPL_, true>(lb, nb, d.csc_ptr, d.csc_slot, d.csc_dst, d.N, d.C, d.h, d.u, d.g_out,      \
+                               d.att_src, d.att_dst, d.e_gz, d.e_gzp, d.e_alp, d.n_gad, d.h_inj, d.part)
+  switch (d.shape) {
+    case 0: VG_JS(8, 1); break;
+    case 1: VG_JS(8, 2); break;
+    case 2: VG_JS(8, 4); break;
+    case 3: VG_JS(16, 4); break;
+    case 4: VG_JS(16, 8); break;
+    default: VG_JS(32, 8); break;
+  }
+#undef VG_JS
+}
+
 inline int jvp_shape_id(int C, const Shape& sh) {
   if (C <= 8) return 0;
   if (!sh.vec) return -1;
@@ -559,6 +592,25 @@ static int jvp2(const int32_t* row_ptr, const int32_t* col, const int32_t* csc_p
     k_fold_add2<<<dim3(vg_blocks(C, 64), 2), 1024, 0, s>>>(part_r, grid, part_s, grid, C,
                                                            g_att_dst, g_att_src);
   }
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int vg_graphnorm_jvp2_fold_src(int32_t N, int32_t C, const float* weight, const float* mean_scale,
+                                          const float* stats, float* ws, float* g_w, float* g_ms,
+                                          const vg_jvp_src* src, void* stream) {
+  if (N <= 0 || C <= 0 || !weight || !mean_scale || !stats || !ws || !g_w || !g_ms) return VG_EINVAL;
+  const bool with_src = src && src->shape >= 0;
+  if (with_src && (src->shape > 5 || src->blocks <= 0 || src->blocks > kMaxBlocks || src->N <= 0 || src->C <= 0 ||
+                   !src->csc_ptr || !src->csc_slot || !src->csc_dst || !src->h || !src->u || !src->g_out ||
+                   !src->att_src || !src->att_dst || !src->e_gz || !src->e_gzp || !src->e_alp || !src->n_gad ||
+                   !src->h_inj || !src->part))
+    return VG_EINVAL;
+  const int chunks = vg::gn_chunks_for(N);
+  float* sums = ws + (size_t)vg::kGnChunks * C * 5;  // vg_graphnorm_jvp2's workspace layout
+  const vg_jvp_src d = with_src ? *src : vg_jvp_src{};
+  k_jvp2_fold_src<<<C + (with_src ? src->blocks : 0), kBlock, 0, static_cast<hipStream_t>(stream)>>>(
+      ws, chunks, N, C, weight, mean_scale, stats, sums, g_w, g_ms, d);
   VG_CHECK_LAUNCH();
   return 0;
 }

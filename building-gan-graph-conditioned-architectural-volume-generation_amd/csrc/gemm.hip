@@ -1301,6 +1301,174 @@ __global__ void __launch_bounds__(1024) k_gemm_ln16(const float* __restrict__ A,
                                        att_d, a_src, a_dst, ldy);
 }
 
+// k_gemm_ln16<2, 32> (M in (64, 128], 32-row tiles, 16 waves, the same
+// fragment-ordered images and MFMA sequence -- bit-identical results) as a
+// PERSISTENT launch with W resident in LDS: one 1024-thread workgroup per CU
+// stages the whole weight image (K <= 32 * KT) once and walks a contiguous
+// range of row tiles; each tile's A is loaded into registers while the
+// previous tile's MFMAs and LayerNorm epilogue run.  k_gemm_ln16 re-streamed
+// W (4x the bytes of A at M = 128) through a 32-wide K-tile pipeline one
+// step deep, so every K-tile waited for an L2 round trip: 33-35 % of the f32
+// MFMA rate at 63.5k rows.  The A image doubles as the epilogue's staged
+// tile (Ct), so W + A fit the LDS at K = 160.
+template <int KT, bool MS>
+__global__ void __launch_bounds__(1024) k_gemm_ln_wres(const float* __restrict__ A, int lda,
+                                                       const float* __restrict__ B, int ldb,
+                                                       const float* __restrict__ bias, int N, int M, int K,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, float eps, float slope,
+                                                       float* __restrict__ H, float* __restrict__ Y,
+                                                       float* __restrict__ mean, float* __restrict__ rstd, int ldy,
+                                                       const MsDesc ms) {
+  constexpr int TMR = 32, NT = 2, TNC = TN * NT, CT = TNC + 1;
+  constexpr int WRW = TMR / 16, WCW = 16 / WRW;  // 2 row waves x 8 column waves, one 16 x 16 sub-tile each
+  static_assert(TNC / (16 * WCW) == 1, "one sub-tile per wave");
+  constexpr int AIMG = TMR * FP, BIMG = TNC * FP;  // floats per 32-wide K-tile image
+  extern __shared__ float4 dyn4[];
+  float* Ws = reinterpret_cast<float*>(dyn4);  // [KT][BIMG]
+  float* As = Ws + KT * BIMG;                  // [KT][AIMG], Ct during the epilogue
+  __shared__ float s_mu[TMR], s_rs[TMR];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wr = wave / WCW, wc = wave % WCW;
+  const int kq4 = K / 4;  // quads per row (K % 4 == 0)
+  // the tile range of this workgroup (XCD-aware: contiguous tiles per XCD)
+  const int tiles = (N + TMR - 1) / TMR;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int t0 = (int)((long long)tiles * lb / gridDim.x), t1 = (int)((long long)tiles * (lb + 1) / gridDim.x);
+  auto a_src = [&](int k, const float*& p, int& ld, int& col) {
+    p = A;
+    ld = lda;
+    col = k;
+    if constexpr (MS) {
+      int sidx = 0;
+#pragma unroll
+      for (int i = 0; i < kMaxSrc - 1; ++i)
+        if (i < ms.nsrc - 1 && k >= ms.kend[i]) sidx = i + 1;
+      const int kb = sidx > 0 ? ms.kend[sidx - 1] : 0;
+      p = ms.p[sidx];
+      ld = ms.ld[sidx];
+      col = k - kb;
+    }
+  };
+  auto w_col = [&](int k) {
+    if constexpr (MS) {
+      int sidx = 0;
+#pragma unroll
+      for (int i = 0; i < kMaxSrc - 1; ++i)
+        if (i < ms.nsrc - 1 && k >= ms.kend[i]) sidx = i + 1;
+      const int kb = sidx > 0 ? ms.kend[sidx - 1] : 0;
+      return ms.wcol[sidx] + (k - kb);
+    }
+    return k;
+  };
+  // W image, once: quads along k of each output column's row of W
+  for (int g = t; g < TNC * kq4; g += 1024) {
+    const int m = g / kq4, k = 4 * (g % kq4);
+    const float4 v = m < M ? *reinterpret_cast<const float4*>(B + (size_t)m * ldb + w_col(k)) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float* d = Ws + (k >> 5) * BIMG;
+    const int kk = k & 31;
+    d[frag_pos(m, kk)] = v.x;
+    d[frag_pos(m, kk + 1)] = v.y;
+    d[frag_pos(m, kk + 2)] = v.z;
+    d[frag_pos(m, kk + 3)] = v.w;
+  }
+  // the zero columns of a K-tile past K (K % 32 != 0)
+  for (int g = t; g < TNC * (KT * 32 - K); g += 1024) {
+    const int m = g / (KT * 32 - K), k = K + g % (KT * 32 - K);
+    Ws[(k >> 5) * BIMG + frag_pos(m, k & 31)] = 0.f;
+  }
+  constexpr int QPT = (TMR * KT * 8 + 1023) / 1024;  // A quads per thread and tile (<= 32 * K / 4)
+  float4 qa[QPT];
+  auto load_a = [&](int tile) {
+    const int n0 = tile * TMR;
+#pragma unroll
+    for (int u = 0; u < QPT; ++u) {
+      const int g = t + 1024 * u;
+      const int r = g / kq4, k = 4 * (g % kq4);
+      qa[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (g < TMR * kq4 && n0 + r < N) {
+        const float* p;
+        int ld, col;
+        a_src(k, p, ld, col);
+        qa[u] = *reinterpret_cast<const float4*>(p + (size_t)(n0 + r) * ld + col);
+      }
+    }
+  };
+  auto store_a = [&]() {
+#pragma unroll
+    for (int u = 0; u < QPT; ++u) {
+      const int g = t + 1024 * u;
+      if (g < TMR * kq4) {
+        const int r = g / kq4, k = 4 * (g % kq4);
+        float* d = As + (k >> 5) * AIMG;
+        const int kk = k & 31;
+        d[frag_pos(r, kk)] = qa[u].x;
+        d[frag_pos(r, kk + 1)] = qa[u].y;
+        d[frag_pos(r, kk + 2)] = qa[u].z;
+        d[frag_pos(r, kk + 3)] = qa[u].w;
+      }
+    }
+    for (int g = t; g < TMR * (KT * 32 - K); g += 1024) {
+      const int r = g / (KT * 32 - K), k = K + g % (KT * 32 - K);
+      As[(k >> 5) * AIMG + frag_pos(r, k & 31)] = 0.f;
+    }
+  };
+  if (t0 < t1) {
+    load_a(t0);
+    store_a();
+  }
+  const int c = wc * 16 + (lane & 15);
+  const float bv = (bias && c < M) ? bias[c] : 0.f;
+  __syncthreads();
+  for (int tile = t0; tile < t1; ++tile) {
+    const int n0 = tile * TMR;
+    if (tile + 1 < t1) load_a(tile + 1);  // in flight under the MFMAs and the epilogue
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int ra_ = wr * 16 + (lane & 15), g = lane >> 4;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      const float* Ai = As + kt * AIMG;
+      const float* Bi = Ws + kt * BIMG;
+      const float4 a0 = *reinterpret_cast<const float4*>(Ai + frag_at(ra_, g, 0));
+      const float4 a1 = *reinterpret_cast<const float4*>(Ai + frag_at(ra_, g, 1));
+      const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      const float4 b0 = *reinterpret_cast<const float4*>(Bi + frag_at(c, g, 0));
+      const float4 b1 = *reinterpret_cast<const float4*>(Bi + frag_at(c, g, 1));
+      const float bw[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bw[i], acc, 0, 0, 0);
+    }
+    __syncthreads();  // every wave is done with the A images: they become Ct
+    float* Ct = As;
+    const int add0 = MS && ms.add ? n0 % ms.add_rows : 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rl = wr * 16 + 4 * (lane >> 4) + r;
+      float v = acc[r] + bv;
+      if constexpr (MS) {
+        if (ms.add && n0 + rl < N && c < M) {
+          int ar2 = add0 + rl;
+          if (ar2 >= ms.add_rows) ar2 -= ms.add_rows;
+          v += ms.add[(size_t)ar2 * ms.ld_add + c];
+        }
+      }
+      Ct[rl * CT + c] = v;
+    }
+    __syncthreads();
+    ln_tile_epilogue<NT, TMR, false, 1024>(Ct, s_mu, s_rs, t, n0, N, M, gamma, beta, eps, slope, H, Y, mean, rstd,
+                                           nullptr, nullptr, nullptr, nullptr, ldy);
+    __syncthreads();  // Ct read out
+    if (tile + 1 < t1) store_a();
+    __syncthreads();
+  }
+}
+
+// W images + the A region (the A images, or the staged tile if larger)
+template <int KT>
+constexpr int wres_lds_bytes() {
+  return (KT * TN * 2 * FP + (KT * 32 * FP > 32 * (2 * TN + 1) ? KT * 32 * FP : 32 * (2 * TN + 1))) * 4;
+}
+
 // part[chunk][M][K] = A[chunk rows]^T . B[chunk rows];  pdb[chunk][M] = column sums of A.
 // `rows` rows of the N reduction per chunk (a multiple of TK), pipelined like k_gemm.
 // G row groups of 4 waves per workgroup: group g takes the chunk's K-steps
@@ -1546,6 +1714,9 @@ struct TnGroup {
 #ifndef VG_TN_DU
 #define VG_TN_DU 8
 #endif
+#ifndef VG_TN_PIPE
+#define VG_TN_PIPE 1  // software-pipelined tn_tile_direct (0: the round-4 loop, A/B)
+#endif
 constexpr int kTnDU = VG_TN_DU;  // row pairs (MFMA K-steps) per wave per block of 2 * kTnDU rows
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const float* p, int bytes) {
@@ -1587,28 +1758,35 @@ __device__ __forceinline__ void tn_tile_direct(float* red, const float* __restri
   const auto rb = uniform_rsrc(B, N * ldb * 4);
   const unsigned oa0 = m0 + col < M ? (m0 + col) * 4u : kOob, oa1 = m0 + 32 + col < M ? (m0 + 32 + col) * 4u : kOob;
   const unsigned ob0 = k0 + col < K ? (k0 + col) * 4u : kOob, ob1 = k0 + 32 + col < K ? (k0 + 32 + col) * 4u : kOob;
-#pragma nounroll
-  for (int n16 = nb + 2 * kTnDU * wave; n16 < ne; n16 += 8 * kTnDU) {
-    float a0[kTnDU], a1[kTnDU], b0[kTnDU], b1[kTnDU];
+  // Software pipelined: the next 16-row block's loads are issued before the
+  // current block's MFMAs (two register sets), so a wave waits for one load
+  // round trip per chunk instead of one per block (a critic chunk is ~12
+  // blocks per wave: the loop was a chain of dependent round trips).
+  float a0[kTnDU], a1[kTnDU], b0[kTnDU], b1[kTnDU];
+  auto load_block = [&](int n16, float (&xa0)[kTnDU], float (&xa1)[kTnDU], float (&xb0)[kTnDU],
+                        float (&xb1)[kTnDU]) {
     const unsigned ra_n = (unsigned)(n16 + hrow) * lda * 4u, rb_n = (unsigned)(n16 + hrow) * ldb * 4u;
 #pragma unroll
     for (int p = 0; p < kTnDU; ++p) {
       const int sa = prow * p * lda * 4, sb = prow * p * ldb * 4;
-      a0[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra, ra_n + oa0, sa, 0));
-      b0[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, rb_n + ob0, sb, 0));
-      if constexpr (M1) a1[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra, ra_n + oa1, sa, 0));
-      else a1[p] = 0.f;
-      if constexpr (K1) b1[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, rb_n + ob1, sb, 0));
-      else b1[p] = 0.f;
+      xa0[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra, ra_n + oa0, sa, 0));
+      xb0[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, rb_n + ob0, sb, 0));
+      if constexpr (M1) xa1[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra, ra_n + oa1, sa, 0));
+      else xa1[p] = 0.f;
+      if constexpr (K1) xb1[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, rb_n + ob1, sb, 0));
+      else xb1[p] = 0.f;
     }
+  };
+  auto mfma_block = [&](int n16, const float (&xa0)[kTnDU], const float (&xa1)[kTnDU], const float (&xb0)[kTnDU],
+                        const float (&xb1)[kTnDU]) {
     if constexpr (BF) {
       bf16x8 ha0, ha1, hb0, hb1;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        ha0[j] = static_cast<__bf16>(a0[j]);
-        hb0[j] = static_cast<__bf16>(b0[j]);
-        ha1[j] = static_cast<__bf16>(a1[j]);
-        hb1[j] = static_cast<__bf16>(b1[j]);
+        ha0[j] = static_cast<__bf16>(xa0[j]);
+        hb0[j] = static_cast<__bf16>(xb0[j]);
+        ha1[j] = static_cast<__bf16>(xa1[j]);
+        hb1[j] = static_cast<__bf16>(xb1[j]);
       }
       c00 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha0, hb0, c00, 0, 0, 0);
       if constexpr (K1) c01 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ha0, hb1, c01, 0, 0, 0);
@@ -1617,18 +1795,38 @@ __device__ __forceinline__ void tn_tile_direct(float* red, const float* __restri
     } else {
 #pragma unroll
       for (int p = 0; p < kTnDU; ++p) {
-        c00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[p], b0[p], c00, 0, 0, 0);
-        if constexpr (K1) c01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[p], b1[p], c01, 0, 0, 0);
-        if constexpr (M1) c10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[p], b0[p], c10, 0, 0, 0);
-        if constexpr (M1 && K1) c11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[p], b1[p], c11, 0, 0, 0);
+        c00 = __builtin_amdgcn_mfma_f32_32x32x2f32(xa0[p], xb0[p], c00, 0, 0, 0);
+        if constexpr (K1) c01 = __builtin_amdgcn_mfma_f32_32x32x2f32(xa0[p], xb1[p], c01, 0, 0, 0);
+        if constexpr (M1) c10 = __builtin_amdgcn_mfma_f32_32x32x2f32(xa1[p], xb0[p], c10, 0, 0, 0);
+        if constexpr (M1 && K1) c11 = __builtin_amdgcn_mfma_f32_32x32x2f32(xa1[p], xb1[p], c11, 0, 0, 0);
       }
     }
 #pragma unroll
     for (int p = 0; p < kTnDU; ++p)
       if (do_db && n16 + hrow + prow * p < db_rows) {  // the f32 values (as tn_tile)
-        db0 += a0[p];
-        db1 += a1[p];
+        db0 += xa0[p];
+        db1 += xa1[p];
       }
+  };
+  constexpr int kStep = 8 * kTnDU;  // 4 waves x 2 kTnDU rows
+  int n16 = nb + 2 * kTnDU * wave;
+#if VG_TN_PIPE == 0  // A/B: one register set, loads then MFMAs per block
+#pragma nounroll
+  for (; n16 < ne; n16 += kStep) {
+    load_block(n16, a0, a1, b0, b1);
+    mfma_block(n16, a0, a1, b0, b1);
+  }
+#endif
+  if (n16 < ne) load_block(n16, a0, a1, b0, b1);
+#pragma nounroll
+  for (; n16 < ne; n16 += 2 * kStep) {
+    float e0[kTnDU], e1[kTnDU], f0[kTnDU], f1[kTnDU];
+    const bool more = n16 + kStep < ne;  // wave-uniform
+    if (more) load_block(n16 + kStep, e0, e1, f0, f1);
+    mfma_block(n16, a0, a1, b0, b1);
+    if (!more) break;
+    if (n16 + 2 * kStep < ne) load_block(n16 + 2 * kStep, a0, a1, b0, b1);
+    mfma_block(n16 + kStep, e0, e1, f0, f1);
   }
   // Cross-wave sum, one accumulator at a time (so the epilogue never holds
   // all 64 accumulators in VGPRs): ((w0 + w2) + (w1 + w3)), deterministic;
@@ -2087,6 +2285,60 @@ extern "C" int vg_gemm_tn_group(const vg_tn* prods, int32_t n, void* stream) {
 
 static inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// The persistent W-resident form (k_gemm_ln_wres) for f32, 64 < M <= 128,
+// K % 4 == 0, K <= 32 * VG_WRES_KT, at least VG_WRES_MIN_ROWS rows (enough
+// 32-row tiles per CU to amortise staging W); VG_WRES=0: k_gemm_ln16 (A/B).
+#ifndef VG_WRES
+#define VG_WRES 1
+#endif
+#ifndef VG_WRES_MIN_ROWS
+#define VG_WRES_MIN_ROWS 16384
+#endif
+static int wres_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                  hipSuccess || n <= 0)
+      n = 256;
+    cus = n;
+  }
+  return cus;
+}
+
+template <int KT, bool MS>
+static void launch_wres(const float* A, int lda, const float* W, int ldw, const float* bias, int N, int M, int K,
+                        const float* gamma, const float* beta, float eps, float slope, float* H, float* Y, float* mean,
+                        float* rstd, int ldy, const MsDesc& d, hipStream_t s) {
+  static bool attr = false;  // dynamic LDS above the 64 KB default, once per instantiation
+  constexpr int bytes = wres_lds_bytes<KT>();
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_ln_wres<KT, MS>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    attr = true;
+  }
+  const int tiles = (N + 31) / 32;
+  const int grid = tiles < wres_cus() ? tiles : wres_cus();
+  k_gemm_ln_wres<KT, MS><<<grid, 1024, bytes, s>>>(A, lda, W, ldw, bias, N, M, K, gamma, beta, eps, slope, H, Y, mean,
+                                                   rstd, ldy, d);
+}
+
+// true: launched (K <= 160 in whole 32-wide tiles of the LDS image)
+template <bool MS>
+static bool try_wres(const float* A, int lda, const float* W, int ldw, const float* bias, int N, int M, int K,
+                     const float* gamma, const float* beta, float eps, float slope, float* H, float* Y, float* mean,
+                     float* rstd, int ldy, const MsDesc& d, hipStream_t s) {
+  if (!VG_WRES || N < VG_WRES_MIN_ROWS || M <= TN || M > 2 * TN || K % 4 || K <= 0) return false;
+  switch ((K + 31) / 32) {
+    case 1: launch_wres<1, MS>(A, lda, W, ldw, bias, N, M, K, gamma, beta, eps, slope, H, Y, mean, rstd, ldy, d, s); return true;
+    case 2: launch_wres<2, MS>(A, lda, W, ldw, bias, N, M, K, gamma, beta, eps, slope, H, Y, mean, rstd, ldy, d, s); return true;
+    case 3: launch_wres<3, MS>(A, lda, W, ldw, bias, N, M, K, gamma, beta, eps, slope, H, Y, mean, rstd, ldy, d, s); return true;
+    case 4: launch_wres<4, MS>(A, lda, W, ldw, bias, N, M, K, gamma, beta, eps, slope, H, Y, mean, rstd, ldy, d, s); return true;
+    case 5: launch_wres<5, MS>(A, lda, W, ldw, bias, N, M, K, gamma, beta, eps, slope, H, Y, mean, rstd, ldy, d, s); return true;
+    default: return false;
+  }
+}
+
 template <bool BF>
 static int gemm_ln_act(const float* A, int32_t lda, const float* W, int32_t N, int32_t M,
                        int32_t K, const float* bias, const float* gamma, const float* beta,
@@ -2099,7 +2351,8 @@ static int gemm_ln_act(const float* A, int32_t lda, const float* W, int32_t N, i
   hipStream_t s = static_cast<hipStream_t>(stream);
   const dim3 grid((N + TM - 1) / TM, 1);
   const bool ql = VG_QUAD_A && K % 4 == 0 && lda % 4 == 0 && al16(A) && al16(W);
-  if (!BF && VG_LN16) {
+  if (!BF && ql && try_wres<false>(A, lda, W, K, bias, N, M, K, gamma, beta, eps, slope, H, Y, mean, rstd, M, MsDesc{}, s)) {
+  } else if (!BF && VG_LN16) {
     if (M <= TN && ql)
       k_gemm_ln16<1, TM, false, false, true><<<grid, 1024, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma, beta, eps,
                                                                   slope, H, Y, mean, rstd);
@@ -2177,7 +2430,9 @@ static int gemm_ln_act_ms(const vg_asrc* src, int32_t nsrc, const float* W, int3
   hipStream_t s = static_cast<hipStream_t>(stream);
   bool ql = VG_QUAD_A && ldw % 4 == 0 && al16(W);
   for (int i = 0; i < nsrc; ++i) ql = ql && src[i].ld % 4 == 0 && src[i].w_col0 % 4 == 0 && al16(src[i].ptr);
-  if (!BF && VG_LN16 && ql)
+  if (!BF && ql && try_wres<true>(nullptr, 0, W, ldw, bias, N, M, K, gamma, beta, eps, slope, nullptr, Y, nullptr,
+                                  nullptr, ldy, d, s)) {
+  } else if (!BF && VG_LN16 && ql)
     k_gemm_ln16<2, 32, false, true, true><<<dim3((N + 31) / 32, 1), 1024, 0, s>>>(
         nullptr, 0, W, ldw, bias, N, M, K, gamma, beta, eps, slope, nullptr, Y, nullptr, nullptr, nullptr, nullptr,
         nullptr, nullptr, ldy, d);

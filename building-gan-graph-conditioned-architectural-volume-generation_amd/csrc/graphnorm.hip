@@ -32,6 +32,7 @@
 // (C = 1..32) still use every lane of the wave.
 #include "common.h"
 #include "gnbwd.h"
+#include "gnjvp.h"
 
 #include <initializer_list>
 
@@ -43,6 +44,7 @@ constexpr int kBlock = 256;
 #endif
 constexpr int kChunks = VG_GN_CHUNKS;  // max row chunks per column slab
 constexpr int kFoldU = kChunks / 64;
+static_assert(kChunks == vg::kGnChunks, "gnjvp.h folds the same chunk partials");
 #ifndef VG_GN_CHUNK_ROWS
 #define VG_GN_CHUNK_ROWS 32
 #endif
@@ -701,58 +703,14 @@ __global__ void __launch_bounds__(kBlock) k_gn_jvp2_partial4(
   }
 }
 
-// The column terms of the second-order pass from the five column sums
-// v = [sum u, sum xt u, sum p, sum p u, sum p xt] (xt = x - mu):
-//   m_u = mean u, a = (1 - ms) mu = mean o, K = mean(o c') = mean(o u) - ms m_u a,
-//   P1 = sum p c' = sum p u - ms m_u Sp, P2 = sum p o = sum p xt + a Sp;
-//   Q / w = P1/d - P2 K/d^3  ->  g_w += Q / w;
-//   g_ms += w d(Q/w)/dms with dd/dms = -a mu/d, dK/dms = -2 a m_u,
-//           dP1/dms = -m_u Sp, dP2/dms = -mu Sp.
-// sums <- [m_u, K, Sp, P1, P2] for the elementwise pass.
-__device__ __forceinline__ void gn_jvp2_cols(const float v[5], float inv_n, float mu, float d, float msc, float wc,
-                                             float* __restrict__ sm, float& dgw, float& dgms) {
-  const float mup = v[0] * inv_n, Sp = v[2];
-  const float a = (1.f - msc) * mu;
-  const float K = (v[1] + a * v[0]) * inv_n - msc * mup * a;
-  const float P1 = v[3] - msc * mup * Sp;
-  const float P2 = v[4] + a * Sp;
-  const float id = 1.f / d, id2 = id * id, id3 = id2 * id;
-  const float dd = -a * mu * id, dK = -2.f * a * mup;
-  sm[0] = mup;
-  sm[1] = K;
-  sm[2] = Sp;
-  sm[3] = P1;
-  sm[4] = P2;
-  dgw = P1 * id - P2 * K * id3;
-  dgms = wc * (-mup * Sp * id - P1 * dd * id2 + mu * Sp * K * id3 - P2 * dK * id3 + 3.f * P2 * K * dd * id3 * id);
-}
-
-// one wave per column: the five sums, then gn_jvp2_cols
+// one wave per column: the five sums, then the column terms (gnjvp.h)
 __global__ void __launch_bounds__(kBlock) k_gn_jvp2_final(
     const float* __restrict__ part, int chunks, int N, int C, const float* __restrict__ w,
     const float* __restrict__ ms, float eps, const float* __restrict__ stats,
     float* __restrict__ sums, float* __restrict__ g_w, float* __restrict__ g_ms) {
   const int c = fold_col(), lane = threadIdx.x & 63;
   if (c >= C) return;
-  float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-  float t[kFoldU][5];
-#pragma unroll
-  for (int u = 0; u < kFoldU; ++u) {
-    const int k = lane + 64 * u;
-#pragma unroll
-    for (int q = 0; q < 5; ++q) t[u][q] = k < chunks ? part[((size_t)k * C + c) * 5 + q] : 0.f;
-  }
-#pragma unroll
-  for (int q = 0; q < 5; ++q) {
-#pragma unroll
-    for (int u = 0; u < kFoldU; ++u) v[q] += t[u][q];
-    v[q] = wave_sum(v[q]);
-  }
-  if (lane != 0) return;
-  float dgw, dgms;
-  gn_jvp2_cols(v, 1.f / static_cast<float>(N), stats[c], stats[C + c], ms[c], w[c], sums + (size_t)c * 5, dgw, dgms);
-  g_w[c] += dgw;
-  g_ms[c] += dgms;
+  vg::gn_jvp2_fold_col(part, chunks, N, C, w, ms, stats, sums, g_w, g_ms, c, lane);
   (void)eps;
 }
 
@@ -789,7 +747,7 @@ __global__ void __launch_bounds__(kBlock) k_gn_jvp2_final_blk(
   for (int q = 0; q < 5; ++q) v[q] = wave_sum(v[q]);
   if (lane != 0) return;
   float dgw, dgms;
-  gn_jvp2_cols(v, 1.f / static_cast<float>(N), mu, sd, msc, wc, sums + (size_t)c * 5, dgw, dgms);
+  vg::gn_jvp2_cols(v, 1.f / static_cast<float>(N), mu, sd, msc, wc, sums + (size_t)c * 5, dgw, dgms);
   g_w[c] = gw0 + dgw;
   g_ms[c] = gm0 + dgms;
   (void)eps;
@@ -1239,6 +1197,39 @@ extern "C" int vg_graphnorm_jvp2(const float* x, int32_t N, int32_t C, const flo
   k_gn_jvp2_apply<<<apply_blocks(total), 256, 0, s>>>(x, u, g_y, total, N, C, weight, bias,
                                                       mean_scale, keep, eps, stats, sums, u_out,
                                                       x_inj);
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+// vg_graphnorm_jvp2 in three launches the caller sequences (include/vgan.h):
+// the column-sum partials, the fold (vg_graphnorm_jvp2_fold_src, gat_jvp.hip,
+// optionally beside a GAT tangent source pass), the elementwise pass.  The
+// same kernels and workspace layout as vg_graphnorm_jvp2: bit-identical.
+extern "C" int vg_graphnorm_jvp2_sums(const float* x, int32_t N, int32_t C, const float* weight, const float* bias,
+                                      const float* mean_scale, const float* keep, float eps, const float* stats,
+                                      const float* u, const float* g_y, float* ws, void* stream) {
+  if (N <= 0 || C <= 0 || !x || !weight || !bias || !mean_scale || !stats || !u || !g_y || !ws) return VG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int chunks = chunks_for(N);
+  dim3 grid(chunks, (C + 63) / 64);
+  if (quad_ok((long long)N * C, C, 0, {x, u, g_y, keep}))
+    k_gn_jvp2_partial4<<<grid, kBlock, 0, s>>>(x, u, g_y, N, C, weight, bias, mean_scale, keep, eps, stats, ws);
+  else
+    k_gn_jvp2_partial<<<grid, kBlock, 0, s>>>(x, u, g_y, N, C, weight, bias, mean_scale, keep, eps, stats, ws,
+                                              nullptr, nullptr, nullptr, nullptr);
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int vg_graphnorm_jvp2_apply(const float* x, int32_t N, int32_t C, const float* weight, const float* bias,
+                                       const float* mean_scale, const float* keep, float eps, const float* stats,
+                                       const float* u, const float* g_y, float* u_out, float* x_inj, const float* ws,
+                                       void* stream) {
+  if (N <= 0 || C <= 0 || !x || !weight || !bias || !mean_scale || !stats || !u || !g_y || !u_out || !x_inj || !ws)
+    return VG_EINVAL;
+  const long long total = (long long)N * C;
+  k_gn_jvp2_apply<<<apply_blocks(total), 256, 0, static_cast<hipStream_t>(stream)>>>(
+      x, u, g_y, total, N, C, weight, bias, mean_scale, keep, eps, stats, ws + (size_t)kChunks * C * 5, u_out, x_inj);
   VG_CHECK_LAUNCH();
   return 0;
 }

@@ -192,6 +192,9 @@ SIGNATURES = {
                                                 _c_p, _c_p, _c_i32, _c_p]),
     "vg_gat_jvp2_plan": (ctypes.c_int, [_c_p] * 5 + [_c_i32] * 3 + [_c_p] * 8 + [_c_f32] + [_c_p] * 7 + [_c_p] * 4),
     "vg_gat_jvp_src_group": (ctypes.c_int, [_c_p, _c_i32, _c_p]),
+    "vg_graphnorm_jvp2_sums": (ctypes.c_int, [_c_p, _c_i32, _c_i32] + [_c_p] * 4 + [_c_f32] + [_c_p] * 5),
+    "vg_graphnorm_jvp2_fold_src": (ctypes.c_int, [_c_i32, _c_i32] + [_c_p] * 8),
+    "vg_graphnorm_jvp2_apply": (ctypes.c_int, [_c_p, _c_i32, _c_i32] + [_c_p] * 4 + [_c_f32] + [_c_p] * 7),
     "vg_gemm_gn_tpart_floats": (_c_i64, [_c_i32, _c_i32]),
     "vg_gemm_gn_bwd": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p,
                                       _c_i32, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_p, _c_p]),

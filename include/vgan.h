@@ -627,6 +627,22 @@ int vg_graphnorm_jvp2_part(const float* x, int32_t rows, int32_t channels, const
                            const float* mean_scale, const float* keep, float eps, const float* stats, const float* u,
                            const float* g_y, float* u_out, float* x_inj, float* g_w, float* g_ms, const float* part,
                            int32_t blocks, float* workspace, void* stream);
+/* vg_graphnorm_jvp2 as three launches the caller sequences: _sums (the
+ * column-sum partials, into workspace), _fold_src (the fold, g_w / g_ms ADDED;
+ * src != NULL with shape >= 0: a GAT tangent source pass described by
+ * vg_gat_jvp2_plan runs in the same launch -- its injections and att_src
+ * partials are read only by the later VJP pass and the folds, so it leaves
+ * the tangent sweep's dependent chain), _apply (u_out, x_inj).  workspace as
+ * for vg_graphnorm_jvp2 (segments 1); results bit-identical to it. */
+int vg_graphnorm_jvp2_sums(const float* x, int32_t rows, int32_t channels, const float* weight, const float* bias,
+                           const float* mean_scale, const float* keep, float eps, const float* stats, const float* u,
+                           const float* g_y, float* workspace, void* stream);
+int vg_graphnorm_jvp2_fold_src(int32_t rows, int32_t channels, const float* weight, const float* mean_scale,
+                               const float* stats, float* workspace, float* g_w, float* g_ms, const vg_jvp_src* src,
+                               void* stream);
+int vg_graphnorm_jvp2_apply(const float* x, int32_t rows, int32_t channels, const float* weight, const float* bias,
+                            const float* mean_scale, const float* keep, float eps, const float* stats, const float* u,
+                            const float* g_y, float* u_out, float* x_inj, const float* workspace, void* stream);
 
 /* ---- row-local chains of narrow linear layers ------------------------------ */
 

@@ -238,6 +238,73 @@ def test_graphnorm_jvp2_matches_autograd(cuda, C, last_block_fold):
         assert ok, err
 
 
+@pytest.mark.parametrize("C", [1, 8, 32, 64])
+def test_graphnorm_jvp2_split_with_source_pass_bitwise(cuda, C):
+    """vg_graphnorm_jvp2 as _sums / _fold_src / _apply (the native critic
+    engine's pass C) with a GAT tangent source pass run inside the fold's
+    launch: u_out, x_inj, the parameter gradients, the source pass's h_inj and
+    att_src partials all bit-identical to vg_graphnorm_jvp2 + the source pass
+    as its own launch (vg_gat_jvp2_deferred)."""
+    import ctypes
+
+    from vgan._lib import VgFold, VgJvpSrc
+
+    n = 900
+    x, P, keep = _gn_inputs(n, C, seed=5)
+    g = torch.Generator().manual_seed(6)
+    xd, kd, wd, bd, sd = (t.float().to(cuda).contiguous() for t in (x, keep, P["w"], P["b"], P["s"]))
+    u, gy = (torch.randn(n, C, generator=g).to(cuda) for _ in range(2))
+    st = stream_handle(cuda)
+    y = torch.empty(n, C, device=cuda)
+    stats = torch.empty(2 * C, device=cuda)
+    ws = torch.empty(int(LIB.vg_graphnorm_seg_ws_floats(1, n, C)), device=cuda)
+    check(LIB.vg_graphnorm_fwd_seg(ptr(xd), 1, n, C, ptr(wd), ptr(bd), ptr(sd), ptr(kd), 1e-5, ptr(y), ptr(stats),
+                                   ptr(ws), None, st), "vg_graphnorm_fwd_seg")
+    # a GAT tangent over a lattice of n nodes for the source pass
+    _, vox = _graph((1, 2))
+    csr = ops.CSR(vox.edge_index.to(cuda), vox.num_nodes)
+    m, e = csr.num_nodes, csr.num_edges
+    h, uh, go = (torch.randn(m, C, generator=g).to(cuda) for _ in range(3))
+    att_s, att_d = (0.3 * torch.randn(C, generator=g)).to(cuda), (0.3 * torch.randn(C, generator=g)).to(cuda)
+    a_s, a_d = h @ att_s, h @ att_d
+    out, alpha = torch.empty(m, C, device=cuda), torch.empty(e, device=cuda)
+    ops.aggregate_fwd_raw(csr, C, ptr(h), ptr(a_s), ptr(a_d), ptr(torch.zeros(C, device=cuda)), 0.2, ptr(out),
+                          ptr(alpha), st)
+    res = {}
+    for split in (False, True):
+        gw, gs = torch.zeros(C, device=cuda), torch.zeros(C, device=cuda)
+        u_out, x_inj = torch.empty(n, C, device=cuda), torch.empty(n, C, device=cuda)
+        wsj = torch.zeros(int(LIB.vg_gat_jvp2_ws_floats(m, e, C)), device=cuda)
+        uo2, hinj = torch.empty(m, C, device=cuda), torch.zeros(m, C, device=cuda)
+        ga_s, ga_d = torch.zeros(C, device=cuda), torch.zeros(C, device=cuda)
+        folds = (VgFold * 2)()
+        nf = ctypes.c_int32(0)
+        args = (ptr(csr.row_ptr), ptr(csr.col), ptr(csr.csc_ptr), ptr(csr.csc_slot), ptr(csr.csc_dst), m, e, C,
+                ptr(h), ptr(uh), ptr(go), ptr(att_s), ptr(att_d), ptr(a_s), ptr(a_d), ptr(alpha), 0.2, ptr(uo2),
+                ptr(hinj), ptr(ga_s), ptr(ga_d), None, None, ptr(wsj), folds, ctypes.byref(nf))
+        gws = torch.zeros_like(ws)
+        if split:
+            src = VgJvpSrc()
+            check(LIB.vg_gat_jvp2_plan(*args, ctypes.byref(src), st), "vg_gat_jvp2_plan")
+            check(LIB.vg_graphnorm_jvp2_sums(ptr(xd), n, C, ptr(wd), ptr(bd), ptr(sd), ptr(kd), 1e-5, ptr(stats), ptr(u),
+                                             ptr(gy), ptr(gws), st), "vg_graphnorm_jvp2_sums")
+            check(LIB.vg_graphnorm_jvp2_fold_src(n, C, ptr(wd), ptr(sd), ptr(stats), ptr(gws), ptr(gw), ptr(gs),
+                                                 ctypes.byref(src), st), "vg_graphnorm_jvp2_fold_src")
+            check(LIB.vg_graphnorm_jvp2_apply(ptr(xd), n, C, ptr(wd), ptr(bd), ptr(sd), ptr(kd), 1e-5, ptr(stats),
+                                              ptr(u), ptr(gy), ptr(u_out), ptr(x_inj), ptr(gws), st),
+                  "vg_graphnorm_jvp2_apply")
+        else:
+            check(LIB.vg_gat_jvp2_deferred(*args, st), "vg_gat_jvp2_deferred")
+            check(LIB.vg_graphnorm_jvp2(ptr(xd), n, C, ptr(wd), ptr(bd), ptr(sd), ptr(kd), 1e-5, ptr(stats), ptr(u),
+                                        ptr(gy), ptr(u_out), ptr(x_inj), ptr(gw), ptr(gs), ptr(gws), None, st),
+                  "vg_graphnorm_jvp2")
+        torch.cuda.synchronize()
+        part_s = wsj[5 * e + 3 * m:].view(-1)  # both partial blocks (vg_gat_jvp2_ws_floats layout)
+        res[split] = [t.clone() for t in (u_out, x_inj, gw, gs, uo2, hinj, part_s)]
+    for a, b in zip(res[False], res[True]):
+        assert torch.equal(a, b)
+
+
 # -------------------------------------------------------------- helpers
 @pytest.mark.parametrize("n", [333, 5000])
 def test_critic_input_and_gp_head(cuda, n):

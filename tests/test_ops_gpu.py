@@ -468,6 +468,57 @@ def test_linear_ln_act_fused_matches_unfused(cuda, m, k, n):
         assert rel_err(u, v) < 1e-5
 
 
+@pytest.mark.parametrize("m,k", [(128, 128), (100, 64), (128, 160), (128, 20), (72, 96)])
+@pytest.mark.parametrize("ms", [False, True])
+def test_gemm_ln_act_w_resident_bitwise(cuda, m, k, ms):
+    """The persistent W-resident LayerNorm GEMM (k_gemm_ln_wres, >= 16384 rows)
+    runs k_gemm_ln16's fragment images and MFMA sequence, so every row equals
+    k_gemm_ln16's (the same rows through a call below the row threshold) bit
+    for bit -- Y and, with H / mean / rstd, the stored LayerNorm inputs; also
+    through the multi-source entry (vg_gemm_ln_act_ms: two column blocks with
+    their own strides and a row-broadcast addend)."""
+    from vgan._lib import LIB, VgASrc, check, ptr
+
+    torch.manual_seed(m * 7 + k)
+    n_big, n_small = 16411, 3001  # the first runs k_gemm_ln_wres (a ragged last tile), the second k_gemm_ln16
+    w = torch.randn(m, k, device=cuda) / k ** 0.5
+    bias, g, be = torch.randn(m, device=cuda), 1 + 0.1 * torch.randn(m, device=cuda), 0.1 * torch.randn(m, device=cuda)
+    st = ops.stream_handle(cuda)
+    if not ms:
+        x = torch.randn(n_big, k, device=cuda)
+        outs = []
+        for n in (n_big, n_small):
+            h, y = torch.empty(n, m, device=cuda), torch.empty(n, m, device=cuda)
+            mu, rs = torch.empty(n, device=cuda), torch.empty(n, device=cuda)
+            check(LIB.vg_gemm_ln_act(ptr(x), k, ptr(w), n, m, k, ptr(bias), ptr(g), ptr(be), 1e-5, 0.2, ptr(h), ptr(y),
+                                     ptr(mu), ptr(rs), st), "vg_gemm_ln_act")
+            outs.append((h, y, mu, rs))
+        for a_, b_ in zip(*outs):
+            assert torch.equal(a_[:n_small], b_)
+        ref = torch.nn.functional.leaky_relu(torch.nn.functional.layer_norm(
+            x.double() @ w.double().t() + bias.double(), (m,), g.double(), be.double(), 1e-5), 0.2)
+        assert rel_err(outs[0][1], ref) < 1e-5
+        return
+    if k % 32:
+        pytest.skip("multi-source column blocks are whole 32-wide tiles")
+    k1 = 32
+    a1 = torch.randn(n_big, 40, device=cuda)  # block 1: columns 0..31 of a 40-wide buffer
+    a2 = torch.randn(n_big, k - k1 + 8, device=cuda)  # block 2: a wider buffer
+    add = torch.randn(64, m, device=cuda)  # row-broadcast addend, rows modulo 64
+    outs = []
+    for n in (n_big, n_small):
+        src = (VgASrc * 2)(VgASrc(a1.data_ptr(), 40, k1, 0, 0), VgASrc(a2.data_ptr(), k - k1 + 8, k - k1, k1, 0))
+        y = torch.empty(n, m, device=cuda)
+        check(LIB.vg_gemm_ln_act_ms(src, 2, ptr(w), k, n, m, ptr(bias), ptr(add), m, 64, ptr(g), ptr(be), 1e-5, 0.2,
+                                    ptr(y), m, st), "vg_gemm_ln_act_ms")
+        outs.append(y)
+    assert torch.equal(outs[0][:n_small], outs[1])
+    xd = torch.cat([a1[:, :k1], a2[:, :k - k1]], 1).double()
+    pre = xd @ w.double().t() + bias.double() + add.double().repeat(-(-n_big // 64), 1)[:n_big]
+    ref = torch.nn.functional.leaky_relu(torch.nn.functional.layer_norm(pre, (m,), g.double(), be.double(), 1e-5), 0.2)
+    assert rel_err(outs[0], ref) < 1e-5
+
+
 @pytest.mark.parametrize("C", [1, 8, 64])
 @pytest.mark.parametrize("case", ["edgeless", "single_node", "self_loops_only"])
 def test_gat_conv_degenerate_graphs(cuda, C, case):
