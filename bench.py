@@ -506,6 +506,11 @@ def start_sweep_store(graphs: int = 10000, seed: int = 2024):
     return proc, path
 
 
+# collating threads of the sweep's loader (tools/sweep_probe.py: 2 kept the
+# loader under the f16 forward's device time; 3 lost to GIL contention)
+SWEEP_WORKERS = int(os.environ.get("VGAN_SWEEP_WORKERS", "2"))
+
+
 def sweep_leg(device, store_job, batch: int = 32, n_taus: int = 10):
     """BASELINE.json configs[4]: generator-only inference sweep over a STREAM
     of distinct buildings (the store written by ``start_sweep_store``: 10,000
@@ -513,10 +518,12 @@ def sweep_leg(device, store_job, batch: int = 32, n_taus: int = 10):
     schedule 1.0 -> 0.1, f16 (and f32) eval forward, one stacked forward per
     batch over the ``n_taus`` temperature copies.  Each batch comes through
     the native loader (host collate + host-built per-batch structures + one
-    upload, prefetched on a thread); its forward is launched eagerly
-    (InferenceSweep.run_stream; recording it per batch measured slower).
-    The timed region is the whole pass: collate, upload, forward.  Also the f16 scatter kernel (vg_hgat_fwd) over the sweep's own
-    stacked graph and channel schedule, graph-replayed between HIP events."""
+    upload, prefetched on SWEEP_WORKERS threads); its forward is enqueued
+    eagerly (InferenceSweep.run_stream; recording it per batch measured
+    slower): f16 as one native call per batch (vg_hgen_sweep), f32 from
+    Python.  The timed region is the whole pass: collate, upload, forward.
+    Also the f16 scatter kernel (vg_hgat_fwd) over the sweep's own stacked
+    graph and channel schedule, graph-replayed between HIP events."""
     from vgan import data as vdata
     from vgan._lib import LIB, check, ptr, stream_handle
     from vgan.config import Configuration
@@ -542,13 +549,15 @@ def sweep_leg(device, store_job, batch: int = 32, n_taus: int = 10):
 
     def loader(indices=None):
         return GraphLoader(store, indices, batch_size=batch, shuffle=False, device=device, prefetch=4,
-                           prepare=(cfg.NUM_CLASSES, ()))
+                           prepare=(cfg.NUM_CLASSES, ()), workers=SWEEP_WORKERS)
 
     n_batches = -(-len(store) // batch)
     out = {"workload": f"configs[4]: {len(store)} distinct synthetic buildings ({n_batches} batches of {batch}) "
                        f"streamed through the native loader, {n_taus} Gumbel temperatures 1.0->0.1 geometric, eval G "
-                       f"forward stacked over the temperatures, launched eagerly per batch (InferenceSweep.run_stream); "
-                       f"collate, upload, per-batch structures and forward timed",
+                       f"forward stacked over the temperatures (InferenceSweep.run_stream; f16: the whole batch -- z and noise "
+                       f"draws, forward, Gumbel head, argmax -- one native call, vg_hgen_sweep; f32: launched from "
+                       f"Python), {SWEEP_WORKERS} collating loader threads; collate, upload, per-batch structures and "
+                       f"forward timed",
            "unit": "samples/s (buildings x temperatures)", "distinct_batches": n_batches,
            "distinct_buildings": len(store)}
     for dt in ("f16", "f32"):

@@ -15,8 +15,14 @@
 // block-diagonal graph, so each worker thread owns whole buildings and writes
 // disjoint output ranges whose offsets a serial prefix pass fixes first.
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdint>
 #include <cstring>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -51,8 +57,76 @@ int plan(const int64_t* node_ptr, const int64_t* edge_ptr, const int32_t* esrc, 
   return 0;
 }
 
-// Threads pay off only past ~64k items of work each (a spawn costs ~20 us).
+// Threads pay off only past ~64k items of work each.
 constexpr int64_t kWorkPerThread = 1 << 16;
+
+// A persistent pool of helper threads (a spawn + join per call cost ~20-50 us
+// a thread, a few hundred us per batch with the loader's two graph collates):
+// a call hands its building ranges to idle helpers and runs the first range
+// itself.  Concurrent calls (several loader workers) share the helpers; a call
+// whose ranges no helper took in time runs them itself, so it never waits on
+// another call's work.
+class Pool {
+ public:
+  static Pool& get() {
+    static Pool* p = new Pool();  // never destroyed: helpers may outlive static teardown
+    return *p;
+  }
+
+  // run fn(w) for w in [0, t): w = 0 on the calling thread
+  template <class F>
+  void run(int32_t t, F& fn) {
+    struct Call {
+      std::atomic<int32_t> next{1}, done{0};
+      int32_t t;
+      std::function<void(int32_t)> body;
+    };
+    auto call = std::make_shared<Call>();
+    call->t = t;
+    call->body = [&fn](int32_t w) { fn(w); };
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      grow(t - 1);
+      for (int32_t i = 1; i < t; ++i)
+        jobs_.push_back([call] {
+          const int32_t w = call->next.fetch_add(1);
+          if (w < call->t) {
+            call->body(w);
+            call->done.fetch_add(1);
+          }
+        });
+    }
+    cv_.notify_all();
+    fn(0);
+    // ranges no helper has started: run them here
+    for (int32_t w = call->next.fetch_add(1); w < t; w = call->next.fetch_add(1)) {
+      fn(w);
+      call->done.fetch_add(1);
+    }
+    while (call->done.load() < t - 1) std::this_thread::yield();
+  }
+
+ private:
+  void grow(int32_t want) {  // mu_ held
+    while ((int32_t)threads_.size() < std::min<int32_t>(want, 32))
+      threads_.emplace_back([this] {
+        for (;;) {
+          std::function<void()> job;
+          {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_.wait(lk, [this] { return !jobs_.empty(); });
+            job = std::move(jobs_.front());
+            jobs_.pop_front();
+          }
+          job();
+        }
+      });
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> jobs_;
+  std::vector<std::thread> threads_;
+};
 
 template <class F>
 void parallel_buildings(int32_t count, int32_t threads, int64_t work, F&& fn) {
@@ -62,13 +136,10 @@ void parallel_buildings(int32_t count, int32_t threads, int64_t work, F&& fn) {
     for (int32_t b = 0; b < count; ++b) fn(b);
     return;
   }
-  std::vector<std::thread> pool;
-  pool.reserve(t);
-  for (int32_t w = 0; w < t; ++w)
-    pool.emplace_back([&, w] {
-      for (int32_t b = w; b < count; b += t) fn(b);
-    });
-  for (auto& th : pool) th.join();
+  auto range = [&](int32_t w) {
+    for (int32_t b = w; b < count; b += t) fn(b);
+  };
+  Pool::get().run(t, range);
 }
 
 }  // namespace

@@ -175,6 +175,40 @@ class VgCriticBatch(ctypes.Structure):
                 ("gp_counter", _c_p)]
 
 
+VG_HGEN_MAX_LAYERS = 8
+VG_HGEN_MAX_BLOCKS = 32
+
+
+class VgHgenLinear(ctypes.Structure):
+    """vg_hgen_linear (include/vgan.h): an f16 [Linear, LayerNorm, LeakyReLU] block (or the head)."""
+    _fields_ = [("weight", _c_p), ("ldw", _c_i32), ("bias", _c_p), ("gamma", _c_p), ("beta", _c_p),
+                ("eps", _c_f32), ("slope", _c_f32), ("in_", _c_i32), ("out", _c_i32)]
+
+
+class VgHgenBlock(ctypes.Structure):
+    """vg_hgen_block (include/vgan.h): an f16 GATConv + GraphNorm block."""
+    _fields_ = [("lin_weight", _c_p), ("ldw", _c_i32), ("att_src", _c_p), ("att_dst", _c_p), ("bias", _c_p),
+                ("slope", _c_f32), ("gn_weight", _c_p), ("gn_bias", _c_p), ("gn_mean_scale", _c_p),
+                ("gn_eps", _c_f32), ("in_", _c_i32), ("out", _c_i32)]
+
+
+class VgHgenModel(ctypes.Structure):
+    """vg_hgen_model (include/vgan.h)."""
+    _fields_ = [("n_matched", _c_i32), ("n_mlp", _c_i32), ("n_blocks", _c_i32), ("n_dec", _c_i32),
+                ("matched", VgHgenLinear * VG_HGEN_MAX_LAYERS), ("mlp", VgHgenLinear * VG_HGEN_MAX_LAYERS),
+                ("block", VgHgenBlock * VG_HGEN_MAX_BLOCKS), ("dec", VgHgenLinear * VG_HGEN_MAX_LAYERS),
+                ("head", VgHgenLinear)]
+
+
+class VgHgenBatch(ctypes.Structure):
+    """vg_hgen_batch (include/vgan.h)."""
+    _fields_ = [("n", _c_i32), ("copies", _c_i32), ("voxel_dim", _c_i32), ("matched_dim", _c_i32),
+                ("z_dim", _c_i32), ("num_edges", _c_i32)] + \
+               [(k, _c_p) for k in ("voxel_x", "matched_x", "row_ptr", "col", "taus")] + \
+               [("seed", ctypes.c_uint64), ("iter", _c_p), ("advance_iter", _c_i32), ("z_salt", ctypes.c_uint32),
+                ("noise_salt", ctypes.c_uint32)]
+
+
 # name -> (restype, argtypes); every function listed here is declared in include/vgan.h
 SIGNATURES = {
     "vg_fold_batch": (ctypes.c_int, [_c_p, _c_i32, _c_p]),
@@ -249,6 +283,9 @@ SIGNATURES = {
     "vg_linear_chain": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p]),
     "vg_graph_exec_update": (ctypes.c_int, [_c_p, _c_p]),
     "vg_graph_launch": (ctypes.c_int, [_c_p, _c_p]),
+    "vg_hgen_arena_bytes": (ctypes.c_int64, [ctypes.POINTER(VgHgenModel), ctypes.POINTER(VgHgenBatch)]),
+    "vg_hgen_sweep": (ctypes.c_int, [ctypes.POINTER(VgHgenModel), ctypes.POINTER(VgHgenBatch), _c_p, ctypes.c_int64,
+                                     _c_p, _c_p, _c_p]),
     "vg_critic_arena_floats": (ctypes.c_int64, [ctypes.POINTER(VgCriticModel), ctypes.POINTER(VgCriticBatch)]),
     "vg_critic_loss_and_grad": (ctypes.c_int, [ctypes.POINTER(VgCriticModel), ctypes.POINTER(VgCriticBatch), _c_p,
                                                _c_i64, _c_p, _c_p]),

@@ -59,6 +59,7 @@ class HalfGenerator:
     @torch.no_grad()
     def refresh(self) -> None:
         G = self.G
+        self._md = None  # the native model descriptor points at the images below
         dev = next(G.parameters()).device
         if dev.type != "cuda":
             raise RuntimeError("vgan HIP ops require tensors on a ROCm device (no CPU fallback)")
@@ -182,6 +183,103 @@ class HalfGenerator:
         check(LIB.vg_hgemm(ptr(d), ldd, ptr(w), w.shape[1], rows, m, _r8(kin), ptr(bias), 0, 0.0, ptr(logits), m, 1,
                            s), "vg_hgemm")
         return logits
+
+    # ------------------------------------------------- one native call per batch
+    def _native_model(self):
+        """The vg_hgen_model of the current weight images (rebuilt by refresh)."""
+        from ._lib import VG_HGEN_MAX_BLOCKS, VG_HGEN_MAX_LAYERS, VgHgenModel
+
+        md = self.__dict__.get("_md")
+        if md is not None:
+            return md
+        if max(len(self.matched), len(self.mlp), len(self.decoder)) > VG_HGEN_MAX_LAYERS or \
+                len(self.gat) > VG_HGEN_MAX_BLOCKS:
+            raise ValueError("generator too deep for vg_hgen_sweep")
+        md = VgHgenModel()
+        md.n_matched, md.n_mlp, md.n_blocks, md.n_dec = len(self.matched), len(self.mlp), len(self.gat), \
+            len(self.decoder)
+
+        def lin(dst, blk):
+            w, b, g, be, eps, slope, m, kin = blk
+            dst.weight, dst.ldw, dst.bias, dst.gamma, dst.beta = w.data_ptr(), w.shape[1], b.data_ptr(), \
+                g.data_ptr(), be.data_ptr()
+            dst.eps, dst.slope, dst.in_, dst.out = eps, slope, kin, m
+
+        for dst, src in ((md.matched, self.matched), (md.mlp, self.mlp), (md.dec, self.decoder)):
+            for i, blk in enumerate(src):
+                lin(dst[i], blk)
+        w, bias, m, kin = self.head
+        md.head.weight, md.head.ldw, md.head.bias, md.head.in_, md.head.out = w.data_ptr(), w.shape[1], \
+            bias.data_ptr(), kin, m
+        for i, (w, att_s, att_d, bias, cin, cout, slope, gw, gb, gms, eps) in enumerate(self.gat):
+            d = md.block[i]
+            d.lin_weight, d.ldw, d.att_src, d.att_dst, d.bias, d.slope = w.data_ptr(), w.shape[1], att_s.data_ptr(), \
+                att_d.data_ptr(), bias.data_ptr(), slope
+            d.gn_weight, d.gn_bias, d.gn_mean_scale, d.gn_eps, d.in_, d.out = gw.data_ptr(), gb.data_ptr(), \
+                gms.data_ptr(), eps, cin, cout
+        self._md = md
+        return md
+
+    @torch.no_grad()
+    def sweep_labels(self, local_graph, voxel_graph, copies: int, taus: torch.Tensor,
+                     logits: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """InferenceSweep._forward on this f16 generator as ONE native call
+        (vg_hgen_sweep): RNG.reset(), z for ``copies`` stacked copies, the
+        forward, Exp(1) noise, the Gumbel head at ``taus`` [copies] and the
+        argmax -- the same kernels in the same order as ``__call__`` preceded
+        by the reset and z draw, so the [copies, N] int8 labels are
+        bit-identical to that path's.  ``logits`` [copies * N, classes] f32
+        receives the logits when given."""
+        import ctypes
+
+        from ._lib import LIB, VgHgenBatch
+
+        G = self.G
+        cfg = G.configuration
+        prep = vdata.prepared(local_graph, voxel_graph, cfg.NUM_CLASSES)
+        dev = self.device
+        rng = G.rng
+        if rng.mode != "device":
+            raise ValueError("vg_hgen_sweep draws z and the noise on the device (RNG mode 'device')")
+        had = dict(rng._iters)
+        ctrs = rng.reset(defer=True)
+        for t in ctrs:  # counters of other devices advance as RNG.reset would
+            if t.device != dev:
+                t.add_(1)
+        it = rng._iter(dev)
+        advance = 1 if any(t.device == dev for t in had.values()) else 0
+        salt0 = rng._salt
+        rng._salt = salt0 + 2  # z (RNG.normal) and the Gumbel noise (RNG.exponential)
+        vx, mx = prep.voxel_x.contiguous(), prep.matched_x.contiguous()
+        csr = prep.csr
+        n = int(vx.shape[0])
+        tt = taus.reshape(-1).to(torch.float32).contiguous()
+        if tt.numel() != copies:
+            raise ValueError("one temperature per stacked copy")
+        bt = VgHgenBatch()
+        bt.n, bt.copies, bt.voxel_dim, bt.matched_dim, bt.z_dim, bt.num_edges = n, int(copies), vx.shape[1], \
+            mx.shape[1], int(cfg.Z_DIM), csr.num_edges
+        bt.voxel_x, bt.matched_x, bt.row_ptr, bt.col, bt.taus = vx.data_ptr(), mx.data_ptr(), \
+            csr.row_ptr.data_ptr(), csr.col.data_ptr(), tt.data_ptr()
+        bt.seed, bt.iter, bt.advance_iter = int(rng.seed) & ((1 << 64) - 1), it.data_ptr(), advance
+        bt.z_salt, bt.noise_salt = 0x40000000 | (salt0 + 1), 0x40000000 | (salt0 + 2)
+        md = self._native_model()
+        need = int(LIB.vg_hgen_arena_bytes(ctypes.byref(md), ctypes.byref(bt)))
+        if need < 0:
+            raise ValueError(f"vg_hgen_arena_bytes: {need}")
+        arena = self.__dict__.get("_arena")
+        if arena is None or arena.numel() < need:
+            # earlier arenas stay alive: a captured sweep graph may still replay on them
+            self.__dict__.setdefault("_old_arenas", []).append(arena)
+            arena = self._arena = torch.empty(need + need // 4, dtype=torch.uint8, device=dev)
+        labels = torch.empty(copies, n, dtype=torch.int8, device=dev)
+        if logits is not None and (logits.dtype != torch.float32 or not logits.is_contiguous() or
+                                   logits.numel() != copies * n * self.head[2]):
+            raise ValueError("logits must be a contiguous f32 [copies * N, classes] tensor")
+        check(LIB.vg_hgen_sweep(ctypes.byref(md), ctypes.byref(bt), arena.data_ptr(), arena.numel(),
+                                labels.data_ptr(), None if logits is None else logits.data_ptr(), stream_handle(dev)),
+              "vg_hgen_sweep")
+        return labels
 
     @torch.no_grad()
     def __call__(self, local_graph, voxel_graph, z: torch.Tensor, noise: Optional[torch.Tensor] = None,

@@ -35,6 +35,9 @@ from .gcscope import gc_frozen
 # update, the graph launch and its event come on top -- f16 147-204k vs
 # 129-167k samples/s, alternated (profiles/r04_sweep_eager_ab.txt)
 _STREAM = os.environ.get("VGAN_SWEEP_STREAM", "eager")
+# the f16 sweep's forward of a batch as one native call (vg_hgen_sweep, csrc/
+# hgen_engine.hip) instead of ~70 launches issued from Python; 0: the Python path
+_NATIVE = os.environ.get("VGAN_HGEN_NATIVE", "1") == "1"
 
 
 def geometric_taus(t0: float = 1.0, t1: float = 0.1, steps: int = 10) -> List[float]:
@@ -92,6 +95,9 @@ class InferenceSweep:
     def _forward(self, local_graph, voxel_graph) -> torch.Tensor:
         G = self.G
         k = len(self.taus)
+        if self.half is not None and _NATIVE and getattr(G.rng, "mode", None) == "device":
+            # the whole batch in one native call (vg_hgen_sweep): bit-identical labels
+            return self.half.sweep_labels(local_graph, voxel_graph, k, self.tau_t)
         n = voxel_graph.num_nodes
         G.rng.reset()  # advance the device counter: every (replayed) batch draws fresh z and noise
         z = G.rng.normal((k, n, G.configuration.Z_DIM), voxel_graph.x.device)

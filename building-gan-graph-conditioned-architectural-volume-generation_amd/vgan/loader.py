@@ -57,7 +57,7 @@ class GraphLoader:
     def __init__(self, store: GraphStore, indices: Optional[Sequence[int]] = None, batch_size: int = 1,
                  shuffle: bool = True, drop_last: bool = False, device=None, prefetch: int = 2,
                  threads: int = 4, rank: int = 0, world_size: int = 1, seed: Optional[int] = None,
-                 even: bool = True, resident: bool = False, prepare=None):
+                 even: bool = True, resident: bool = False, prepare=None, workers: int = 1):
         """``rank`` / ``world_size``: data-parallel sharding -- every rank draws
         the same epoch plan and takes batches rank, rank + world, ... of it, so
         ranks see disjoint buildings (weak scaling, one batch of
@@ -83,7 +83,13 @@ class GraphLoader:
         ``resident``: the first epoch's batches stay on the device and every
         later epoch yields the same batch objects in the same order (no
         reshuffle) -- an evaluation set kept in HBM, whose per-batch graphs
-        the trainer captures once and replays."""
+        the trainer captures once and replays.
+
+        ``workers``: collating threads (batch i on worker i % workers, yielded
+        in plan order).  The C++ collate releases the GIL, so two or three
+        workers overlap it; the training step keeps one (its ctypes launches
+        are host-bound and every extra Python thread competes for the GIL), a
+        sweep whose forward is one native call takes more."""
         if not 0 <= rank < world_size:
             raise ValueError("need 0 <= rank < world_size")
         if world_size > 1 and seed is None:
@@ -103,6 +109,7 @@ class GraphLoader:
         self.resident = bool(resident)
         self._resident_batches: Optional[List[Tuple[GraphBatch, GraphBatch]]] = None
         self.prepare = prepare
+        self.workers = max(1, int(workers))
 
     def __len__(self) -> int:
         n = len(self.indices)
@@ -141,7 +148,7 @@ class GraphLoader:
         if dev is None or dev.type != "cuda":
             it = (self.store.collate(idx, pin=False, threads=self.threads, prepare=self.prepare) for idx in plan)
         else:
-            it = _prefetched(self.store, plan, dev, self.prefetch, self.threads, self.prepare)
+            it = _prefetched(self.store, plan, dev, self.prefetch, self.threads, self.prepare, self.workers)
         for pair in it:
             if kept is not None:
                 kept.append(pair)
@@ -175,15 +182,18 @@ def _switch_exit() -> None:
 
 
 def _prefetched(store: GraphStore, plan: List[List[int]], dev: torch.device, depth: int, threads: int,
-                prepare=None):
+                prepare=None, workers: int = 1):
     copy_stream = torch.cuda.Stream(device=dev)
-    q: "queue.Queue" = queue.Queue(maxsize=depth)
+    nw = max(1, min(int(workers), len(plan) or 1))
+    # worker w collates batches w, w + nw, ...; its own queue keeps them in plan order
+    qs: List["queue.Queue"] = [queue.Queue(maxsize=max(1, -(-depth // nw))) for _ in range(nw)]
     stop = threading.Event()
     _END = object()
 
-    def worker():
+    def worker(w: int):
+        q = qs[w]
         try:
-            for idx in plan:
+            for idx in plan[w::nw]:
                 if stop.is_set():
                     return
                 host = store.collate(idx, pin=True, threads=threads, prepare=prepare)
@@ -196,7 +206,7 @@ def _prefetched(store: GraphStore, plan: List[List[int]], dev: torch.device, dep
         except BaseException as exc:  # surfaced on the consumer thread
             q.put(exc)
 
-    th = threading.Thread(target=worker, name="vgan-loader", daemon=True)
+    ths = [threading.Thread(target=worker, args=(w,), name=f"vgan-loader-{w}", daemon=True) for w in range(nw)]
     # While the worker runs, the interpreter hands the GIL over every 0.1 ms
     # instead of every 5 ms: the consumer (the training step) is host-bound on
     # ctypes launches, each of which releases the GIL, and on return it
@@ -205,10 +215,11 @@ def _prefetched(store: GraphStore, plan: List[List[int]], dev: torch.device, dep
     # (tools/fresh_probe.py, profiles/r04_fresh_probe.jsonl).  Restored when
     # the last running prefetcher ends.
     _switch_enter()
-    th.start()
+    for th in ths:
+        th.start()
     try:
-        while True:
-            item = q.get()
+        for i in range(len(plan) + 1):
+            item = qs[i % nw].get()
             if item is _END:
                 return
             if isinstance(item, BaseException):
@@ -228,12 +239,13 @@ def _prefetched(store: GraphStore, plan: List[List[int]], dev: torch.device, dep
     finally:
         _switch_exit()
         stop.set()
-        while th.is_alive():
-            try:
-                q.get(timeout=0.1)
-            except queue.Empty:
-                pass
-        th.join()
+        for q, th in zip(qs, ths):
+            while th.is_alive():
+                try:
+                    q.get(timeout=0.1)
+                except queue.Empty:
+                    pass
+            th.join()
 
 
 def _tensors(g: GraphBatch):

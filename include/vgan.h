@@ -1046,6 +1046,81 @@ int64_t vg_critic_arena_floats(const vg_critic_model* model, const vg_critic_bat
 int vg_critic_loss_and_grad(const vg_critic_model* model, const vg_critic_batch* batch, float* arena,
                             int64_t arena_floats, float* out, void* stream);
 
+/* ---- the f16 inference-sweep forward as one native call (configs[4]) ----- */
+
+/* One batch of the configs[4] sweep -- InferenceSweep._forward with the f16
+ * generator (vgan/half.py HalfGenerator.logits + the Gumbel head + argmax;
+ * the eval forward of models.py:119-155 stacked over `copies` temperatures,
+ * trainer.py:749-806 sampling) -- issued from C++: the same f16 kernels in
+ * the same order with the same arguments, so the labels are bit-identical to
+ * the Python path's; the per-launch host cost (~10 us of interpreter time and
+ * one torch allocation per temporary there) drops to ~1-2 us, so a sweep of
+ * distinct batches is bound by the device instead of the host.
+ *
+ * Model: the f16 weight images HalfGenerator.refresh builds (rows padded to
+ * multiples of 8 halves) and the f32 vectors.  Batch: the prepared batch's
+ * voxel features and type-matched program features (f32, one copy), its CSR
+ * (one copy: the engine stacks `copies` block-diagonal copies itself), the
+ * per-copy temperatures on the device, and the device-RNG draw spec of z and
+ * of the Gumbel noise (vg_rng_fill kinds 0 and 2; advance_iter != 0 first
+ * adds 1 to *iter, the RNG's reset).  labels [copies * n] int8 (the argmax
+ * class of every voxel of every copy); logits [copies * n][classes] f32 is
+ * optional (NULL: kept in the arena).  Temporaries live in `arena`
+ * (vg_hgen_arena_bytes, 256-byte aligned). */
+#define VG_HGEN_MAX_LAYERS 8
+#define VG_HGEN_MAX_BLOCKS 32
+
+typedef struct {
+  const uint16_t* weight; /* [out][ldw] f16, ldw = in rounded up to 8 (zero pad) */
+  int32_t ldw;
+  const float* bias;
+  const float* gamma; /* LayerNorm (NULL for the decoder head) */
+  const float* beta;
+  float eps, slope;
+  int32_t in, out;
+} vg_hgen_linear;
+
+typedef struct {
+  const uint16_t* lin_weight; /* GATConv.lin [out][ldw] f16 */
+  int32_t ldw;
+  const float* att_src;
+  const float* att_dst;
+  const float* bias;
+  float slope;
+  const float* gn_weight; /* GraphNorm */
+  const float* gn_bias;
+  const float* gn_mean_scale;
+  float gn_eps;
+  int32_t in, out;
+} vg_hgen_block;
+
+typedef struct {
+  int32_t n_matched, n_mlp, n_blocks, n_dec;
+  vg_hgen_linear matched[VG_HGEN_MAX_LAYERS]; /* matched-feature encoder */
+  vg_hgen_linear mlp[VG_HGEN_MAX_LAYERS];     /* MLP encoder over [em | voxel.x | z] */
+  vg_hgen_block block[VG_HGEN_MAX_BLOCKS];    /* GAT encoder */
+  vg_hgen_linear dec[VG_HGEN_MAX_LAYERS];     /* decoder [Linear, LayerNorm, LeakyReLU] blocks */
+  vg_hgen_linear head;                        /* decoder head (f32 logits) */
+} vg_hgen_model;
+
+typedef struct {
+  int32_t n, copies;                    /* voxel nodes per copy, stacked copies (temperatures) */
+  int32_t voxel_dim, matched_dim, z_dim, num_edges;
+  const float* voxel_x;                 /* [n][voxel_dim] */
+  const float* matched_x;               /* [n][matched_dim] */
+  const int32_t* row_ptr;               /* [n + 1], self loops included (vgan.ops.CSR) */
+  const int32_t* col;                   /* [num_edges] */
+  const float* taus;                    /* [copies] */
+  uint64_t seed;
+  int64_t* iter;
+  int32_t advance_iter;
+  uint32_t z_salt, noise_salt;
+} vg_hgen_batch;
+
+int64_t vg_hgen_arena_bytes(const vg_hgen_model* model, const vg_hgen_batch* batch);
+int vg_hgen_sweep(const vg_hgen_model* model, const vg_hgen_batch* batch, void* arena, int64_t arena_bytes,
+                  int8_t* labels, float* logits, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

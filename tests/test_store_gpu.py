@@ -35,9 +35,13 @@ def test_host_csr_matches_device_build(cuda, ds_store):
         _same(got, want, name)
 
 
-def test_loader_delivers_device_batches(cuda, ds_store):
+@pytest.mark.parametrize("workers", [1, 3])
+def test_loader_delivers_device_batches(cuda, ds_store, workers):
+    """Every batch in plan order, device-resident, equal to the reference
+    collate -- with one collating thread and with three (round-robin)."""
     ds, st = ds_store
-    loader = GraphLoader(st, list(range(len(st))), batch_size=5, shuffle=True, device=cuda, prefetch=2)
+    loader = GraphLoader(st, list(range(len(st))), batch_size=5, shuffle=True, device=cuda, prefetch=2,
+                         workers=workers)
     torch.manual_seed(9)
     plan = loader.batches()
     torch.manual_seed(9)  # the iteration below draws the same plan

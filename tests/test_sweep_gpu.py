@@ -48,3 +48,60 @@ def test_stream_sweep_equals_eager(cuda, tmp_path, dtype, stream, monkeypatch):
     torch.cuda.synchronize()
     for a, b in zip(res["predictions"], ref["predictions"]):
         assert a.shape == b.shape and torch.equal(a, b)
+
+
+@pytest.mark.parametrize("copies", [1, 4])
+def test_native_f16_sweep_equals_python_path(cuda, tmp_path, monkeypatch, copies):
+    """The f16 sweep forward of a batch as one native call (vg_hgen_sweep,
+    csrc/hgen_engine.hip) against the Python path over the same kernels
+    (VGAN_HGEN_NATIVE=0): the int8 labels and the logits bit for bit, batch
+    after batch from one device-RNG stream (the counter advanced in the
+    engine's first launch, salts as RNG.normal / RNG.exponential), on one
+    temperature and on a stacked schedule; the RNG state afterwards is the
+    same."""
+    from vgan import infer
+
+    st = write_store(str(tmp_path / "s"), SyntheticDataset(17, seed=23))
+    cfg = Configuration()
+    cfg.DEVICE = str(cuda)
+    torch.manual_seed(6)
+    G = VoxelGNNGenerator(cfg, 17, 12).to(cuda)
+    taus = geometric_taus(1.0, 0.1, copies)
+
+    def run(native):
+        monkeypatch.setattr(infer, "_NATIVE", native)
+        G.rng = RNG("device", seed=41)
+        sw = InferenceSweep(G, taus, dtype="f16")
+        loader = GraphLoader(st, list(range(len(st))), batch_size=6, shuffle=False, device=cuda, prefetch=2,
+                             prepare=(7, ()))
+        out = sw.run_stream(loader, collect=True)["predictions"]
+        torch.cuda.synchronize()
+        return out, G.rng.state_dict(), G.rng._salt
+
+    got, st_n, salt_n = run(True)
+    want, st_p, salt_p = run(False)
+    assert len(got) == len(want) == 3
+    for a, b in zip(got, want):
+        assert a.dtype == torch.int8 and a.shape == b.shape and torch.equal(a, b)
+    assert st_n == st_p and salt_n == salt_p
+    # the logits of one batch, native against HalfGenerator.logits from the same state
+    from vgan import data as vdata
+    from vgan.half import HalfGenerator
+
+    loc, vox = next(iter(GraphLoader(st, [3, 1, 4, 1, 5], batch_size=5, shuffle=False, device=cuda, prefetch=1,
+                                     prepare=(7, ()))))
+    G.eval()
+    hg = HalfGenerator(G)
+    n = vdata.prepared(loc, vox, 7).voxel_x.shape[0]
+    tt = torch.tensor(taus, device=cuda)
+    G.rng = RNG("device", seed=3)
+    G.rng.reset()
+    lg = torch.empty(copies * n, 7, device=cuda)
+    hg.sweep_labels(loc, vox, copies, tt, logits=lg)
+    G.rng = RNG("device", seed=3)
+    G.rng.reset()
+    G.rng.reset()
+    z = G.rng.normal((copies, n, cfg.Z_DIM), cuda)
+    ref = hg.logits(loc, vox, z)
+    torch.cuda.synchronize()
+    assert torch.equal(lg, ref)
