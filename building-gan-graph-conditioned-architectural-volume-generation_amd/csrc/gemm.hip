@@ -1886,6 +1886,96 @@ __device__ __forceinline__ void tn_tile_direct(float* red, const float* __restri
 
 constexpr int kTnDirectRed = 2 * 16 * 64;  // floats of the cross-wave buffer (8 KB)
 
+// Narrow products (M <= 16 and K <= 16: the critic's and the generator's
+// bottleneck layers, 8 x 16, 16 x 8, 1 x 8 ...) on the 16x16x4 f32 MFMA:
+// lane l's A operand is A[n + l / 16][l % 16] and its B operand
+// B[n + l / 16][l % 16], four rows per instruction, so a 16-wide product
+// wastes none of the 32x32x2 form's 3/4 of idle output lanes and takes a
+// quarter of its MFMA cycles per row (32 vs 2 x 64 cycles per 4 rows).  Each
+// wave takes 32-row blocks (8 MFMA steps, the next block's loads in flight),
+// the waves' sums are added through LDS in the fixed order ((w0 + w2) + (w1 +
+// w3)).  The sums differ from the 32x32x2 form's only in order.
+#ifndef VG_TN_NARROW
+#define VG_TN_NARROW 1
+#endif
+__device__ __forceinline__ void tn_tile_narrow16(float* red, const float* __restrict__ A, int lda,
+                                                 const float* __restrict__ B, int ldb, int N, int M, int K, int rows,
+                                                 int chunk, float* __restrict__ part, float* __restrict__ pdb,
+                                                 int db_rows) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int nb = chunk * rows, ne = min(N, nb + rows);
+  const int col = lane & 15, rq = lane >> 4;
+  constexpr unsigned kOob = 1u << 30;
+  const auto ra = uniform_rsrc(A, N * lda * 4);
+  const auto rb = uniform_rsrc(B, N * ldb * 4);
+  const unsigned oa = col < M ? col * 4u : kOob, ob = col < K ? col * 4u : kOob;
+  f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f};
+  float db = 0.f;
+  constexpr int kS = 8;  // MFMA steps (4 rows each) per block
+  float a0[kS], b0[kS], a1[kS], b1[kS];
+  auto load_block = [&](int n32, float (&xa)[kS], float (&xb)[kS]) {
+    const unsigned ra_n = (unsigned)(n32 + rq) * lda * 4u, rb_n = (unsigned)(n32 + rq) * ldb * 4u;
+#pragma unroll
+    for (int p = 0; p < kS; ++p) {
+      xa[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra, ra_n + oa, 4 * p * lda * 4, 0));
+      xb[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, rb_n + ob, 4 * p * ldb * 4, 0));
+    }
+  };
+  auto mfma_block = [&](int n32, const float (&xa)[kS], const float (&xb)[kS]) {
+#pragma unroll
+    for (int p = 0; p < kS; ++p) c = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[p], xb[p], c, 0, 0, 0);
+    if (pdb)
+#pragma unroll
+      for (int p = 0; p < kS; ++p)
+        if (n32 + rq + 4 * p < db_rows) db += xa[p];
+  };
+  constexpr int kStep = 4 * 32;  // 4 waves x 32 rows
+  int n32 = nb + 32 * wave;
+  if (n32 < ne) load_block(n32, a0, b0);
+#pragma nounroll
+  for (; n32 < ne; n32 += 2 * kStep) {
+    const bool more = n32 + kStep < ne;  // wave-uniform
+    if (more) load_block(n32 + kStep, a1, b1);
+    mfma_block(n32, a0, b0);
+    if (!more) break;
+    if (n32 + 2 * kStep < ne) load_block(n32 + 2 * kStep, a0, b0);
+    mfma_block(n32 + kStep, a1, b1);
+  }
+  // cross-wave sum ((w0 + w2) + (w1 + w3)); lane l holds D[4 (l / 16) + r][l % 16]
+  if (wave >= 2)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[((wave - 2) * 4 + r) * 64 + lane] = c[r];
+  __syncthreads();
+  if (wave < 2)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) c[r] += red[(wave * 4 + r) * 64 + lane];
+  __syncthreads();
+  if (wave == 1)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[r * 64 + lane] = c[r];
+  __syncthreads();
+  if (wave == 0) {
+    float* out = part + (size_t)chunk * M * K;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = 4 * rq + r, k = col;
+      if (m < M && k < K) out[(size_t)m * K + k] = c[r] + red[r * 64 + lane];
+    }
+  }
+  if (pdb) {  // column sums of A: lanes l, l + 16, l + 32, l + 48 hold one column's rows
+    db += __shfl_xor(db, 16, 64);
+    db += __shfl_xor(db, 32, 64);
+    __syncthreads();
+    if (wave >= 2) red[(wave - 2) * 64 + lane] = db;
+    __syncthreads();
+    if (wave < 2) db += red[wave * 64 + lane];
+    __syncthreads();
+    if (wave == 1) red[lane] = db;
+    __syncthreads();
+    if (wave == 0 && rq == 0 && col < M) pdb[(size_t)chunk * M + col] = db + red[lane];
+  }
+}
+
 template <bool BF>
 __global__ void __launch_bounds__(256) k_gemm_tn_group_direct(const TnGroup g) {
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
@@ -1898,7 +1988,9 @@ __global__ void __launch_bounds__(256) k_gemm_tn_group_direct(const TnGroup g) {
   __shared__ float red[kTnDirectRed];
   const int m0 = (rem % gx) * TM, k0 = (rem / gx) * TN;
   const bool m1 = m0 + 32 < d.M, k1 = k0 + 32 < d.K;
-  if (m1 && k1)
+  if (!BF && VG_TN_NARROW && d.M <= 16 && d.K <= 16)
+    tn_tile_narrow16(red, d.A, d.lda, d.B, d.ldb, d.N, d.M, d.K, d.rows, chunk, d.part, d.pdb, d.db_rows);
+  else if (m1 && k1)
     tn_tile_direct<true, true, BF>(red, d.A, d.lda, d.B, d.ldb, d.N, d.M, d.K, d.rows, chunk, m0, k0, d.part, d.pdb,
                                d.db_rows);
   else if (m1)
@@ -2139,10 +2231,33 @@ static inline int tn_rows(int N, int M, int K, int wg_target = VG_TN_TARGET, int
   return rows < TK ? TK : rows;
 }
 
+// Rows per chunk of a product planned for vg_gemm_tn_group.  A grouped launch
+// lasts as long as its slowest workgroup, so each product's chunk count
+// follows its tile's MFMA cost per row: 64 x 64 tiles (four 32x32x2
+// accumulators) get 4x, half-wide ones 2x the workgroups of a 32 x 32 tile,
+// and the narrow 16x16x4 products (M, K <= 16: a quarter of a 32 x 32 tile's
+// MFMA time per row; f32 only: the bf16 products keep the plain rule) a
+// quarter -- every workgroup of the launch then carries
+// about the same work.  Products of several output tiles (the generator's
+// 128-wide layers, already at the VG_TN_GROUP_MIN_ROWS floor) keep the plain
+// rule (VG_TN_BALANCE=0: VG_TN_GROUP_TARGET workgroups for every tile, the
+// round-4 plan).
+#ifndef VG_TN_BALANCE
+#define VG_TN_BALANCE 1
+#endif
+static inline int tn_group_rows(int N, int M, int K, bool bf = false) {
+  int target = VG_TN_GROUP_TARGET;
+  if (VG_TN_BALANCE && !bf && M <= TM && K <= TN) {  // one output tile (products over several keep the plain rule)
+    const int mw = min(M, TM) > 32 ? 2 : 1, kw = min(K, TN) > 32 ? 2 : 1;
+    target = VG_TN_NARROW && M <= 16 && K <= 16 ? VG_TN_GROUP_TARGET / 4 : VG_TN_GROUP_TARGET * mw * kw;
+  }
+  return tn_rows(N, M, K, target, VG_TN_GROUP_MIN_ROWS);
+}
+
 extern "C" int64_t vg_gemm_tn_ws_floats(int32_t N, int32_t M, int32_t K) {
   if (N <= 0) return 1;
   // enough for either plan: one launch per product or a grouped product
-  const int r = min(tn_rows(N, M, K), tn_rows(N, M, K, VG_TN_GROUP_TARGET, VG_TN_GROUP_MIN_ROWS));
+  const int r = min(min(tn_rows(N, M, K), tn_group_rows(N, M, K)), tn_group_rows(N, M, K, true));
   const int64_t chunks = (N + r - 1) / r;
   return chunks * ((int64_t)M * K + M);
 }
@@ -2215,7 +2330,7 @@ static int gemm_tn_plan(const float* A, int32_t lda, const float* B, int32_t ldb
   if (!prod_out || !folds_out || !n_out || N <= 0 || M <= 0 || K <= 0 || ldc < K || !A || !B || !C ||
       !workspace || db_rows < 0)
     return VG_EINVAL;
-  const int rows = tn_rows(N, M, K, VG_TN_GROUP_TARGET, VG_TN_GROUP_MIN_ROWS);
+  const int rows = tn_group_rows(N, M, K, BF);
   const int chunks = (N + rows - 1) / rows;
   float* part = workspace;
   float* pdb = workspace + (size_t)chunks * M * K;

@@ -834,3 +834,35 @@ def test_stage_plan_lists_and_slots(cuda):
         lst = usrc[t, :u]
         assert torch.equal(lst, torch.unique(srcs))  # sorted, distinct
         assert torch.equal(lst[lidx[e0:e1]], srcs)
+
+
+def test_grouped_weight_gradient_products_match_f64(cuda):
+    """vg_gemm_tn_group over the critic's product list (the shapes of one
+    backward, N = 52,428 rows; narrow 1x8 .. 16x16 products on the 16x16x4
+    MFMA, wider ones on 32x32x2) plus ragged and short-row cases: every
+    C += A^T B and db += column sums of A within 1e-5 of f64, through the
+    deferred folds (FoldCollector)."""
+    from vgan._lib import LIB, FoldCollector, ptr
+
+    torch.manual_seed(11)
+    shapes = [(52428, 1, 8), (52428, 8, 16), (52428, 16, 32), (52428, 32, 64), (52428, 64, 64), (52428, 16, 8),
+              (52428, 64, 36), (13107, 4, 2), (13107, 2, 1), (777, 16, 16), (31, 7, 5), (52428, 128, 128)]
+    st = ops.stream_handle(cuda)
+    fc = FoldCollector()
+    cases = []
+    for n, m, k in shapes:
+        a = torch.randn(n, m + 3, device=cuda)[:, :m]  # row strides past the width
+        b = torch.randn(n, k + 1, device=cuda)[:, :k]
+        c = torch.randn(m, k, device=cuda)
+        db = torch.randn(m, device=cuda)
+        c0, db0 = c.clone(), db.clone()
+        ws = torch.empty(int(LIB.vg_gemm_tn_ws_floats(n, m, k)), device=cuda)
+        fc.tn((ptr(a), a.stride(0), ptr(b), b.stride(0), n, m, k, ptr(c), k, ptr(db), n - n // 3, 1, ptr(ws)), st,
+              keep=(a, b, ws))
+        cases.append((a, b, c, db, c0, db0, n - n // 3))
+    fc.flush(st)
+    torch.cuda.synchronize()
+    for a, b, c, db, c0, db0, dbr in cases:
+        ref = c0.double() + a.double().t() @ b.double()
+        assert rel_err(c, ref) < 1e-5, a.shape
+        assert rel_err(db, db0.double() + a[:dbr].double().sum(0)) < 1e-5, a.shape
