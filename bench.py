@@ -261,7 +261,7 @@ def gemm_family_roofline(tr, n: int, device, reps: int = 20):
             "timing": "hipGraph-replayed between HIP events on the replay stream (f32 operands)"}
 
 
-def load_pmc_traffic(name: str = "r04_pmc_aggregate_gnp.json"):
+def load_pmc_traffic(name: str = "r05_pmc_aggregate_gnp.json"):
     """Per-launch HBM-side bytes of the scatter kernel from the committed
     rocprofv3 PMC summary of the variant the step runs (tools/pmc_roofline.sh
     --gnp), or (None, None) when this round has not measured it: an older
