@@ -372,6 +372,7 @@ def stress_roofline(device, channels=(128, 64, 1), reps: int = 20, order: str = 
     tiles = (n + 15) // 16
     uniq = plan[:tiles].clamp_min(0).sum().item()
     splan = csr.stage_plan()
+    rplan = csr.ring_plan()
     uc = splan[:csr.stage_tiles()]
     staged_tiles = int((uc > 0).sum().item())
     s_uniq = float(uc.clamp_min(0).sum().item()) / max(1, staged_tiles)
@@ -379,7 +380,7 @@ def stress_roofline(device, channels=(128, 64, 1), reps: int = 20, order: str = 
         f"64-row {s_uniq:.1f} for {4 * e / tiles:.1f} ({staged_tiles} staged, "
         f"{int((uc < 0).sum().item())} from global memory)")
     scratch = torch.empty(512 * 1024 * 1024 // 4, device=device)  # flush the 256 MB MALL between reps
-    res, res_lds, res_st = {}, {}, {}
+    res, res_lds, res_st, res_ring = {}, {}, {}, {}
     for c in channels:
         h = torch.randn(n, c, device=device)
         a_s, a_d = 0.3 * torch.randn(n, device=device), 0.3 * torch.randn(n, device=device)
@@ -401,6 +402,14 @@ def stress_roofline(device, channels=(128, 64, 1), reps: int = 20, order: str = 
                                                   ptr(a_d), ptr(bias), 0.2, ptr(out), ptr(alpha), ptr(splan),
                                                   stream_handle(device)),
                   "vg_gat_aggregate_fwd_staged")
+
+        ring_err = torch.zeros(1, dtype=torch.int32, device=device)
+
+        def run_ring():
+            check(LIB.vg_gat_aggregate_fwd_ring(ptr(csr.row_ptr), ptr(csr.col), n, c, ptr(h), ptr(a_s), ptr(a_d),
+                                                ptr(bias), 0.2, ptr(out), ptr(alpha), ptr(rplan), ptr(ring_err),
+                                                stream_handle(device)),
+                  "vg_gat_aggregate_fwd_ring")
 
         def timed(fn):
             for _ in range(3):
@@ -426,8 +435,13 @@ def stress_roofline(device, channels=(128, 64, 1), reps: int = 20, order: str = 
         if c in (64, 128):
             avg = timed(run_staged)
             res_st[c] = {"avg_us": avg * 1e3, "bytes": b, "achieved_gbs": b / (avg * 1e-3) / 1e9}
+            avg = timed(run_ring)
+            if int(ring_err.item()) != 0:
+                raise RuntimeError("vg_gat_aggregate_fwd_ring: a hand-over wait expired")
+            res_ring[c] = {"avg_us": avg * 1e3, "bytes": b, "achieved_gbs": b / (avg * 1e-3) / 1e9}
     del scratch
     return {"nodes": n, "edges": e, "per_channels": res, "per_channels_lds": res_lds, "per_channels_staged": res_st,
+            "per_channels_ring": res_ring,
             "order": order, "distinct_sources_per_tile": round(uniq / tiles, 1), "edges_per_tile": round(e / tiles, 1),
             "staged_plan": {"distinct_sources_per_64_row_tile": round(s_uniq, 1),
                             "edges_per_64_row_tile": round(4 * e / tiles, 1), "staged_tiles": staged_tiles,
@@ -932,7 +946,7 @@ def main():
                                                    for o in ("rowmajor", "tiled", "blocked")}
         for o, st_ in stress_orders.items():
             for kind, key in (("register", "per_channels"), ("LDS 16-row", "per_channels_lds"),
-                              ("staged", "per_channels_staged")):
+                              ("staged", "per_channels_staged"), ("ring", "per_channels_ring")):
                 for c, r in st_[key].items():
                     log(f"stress ({o}) C={c} ({kind}): {r['avg_us']:.1f} us, {r['achieved_gbs']:.0f} GB/s")
         sweep = None if store_job is None else sweep_leg(device, store_job)
@@ -1027,7 +1041,11 @@ def main():
                                          "through LDS)",
                      "per_channels_staged": "vg_gat_aggregate_fwd_staged (persistent 1024-thread workgroup per CU; "
                                             "each 64-row tile's distinct source rows staged through LDS while the "
-                                            "previous tile is aggregated)"}
+                                            "previous tile is aggregated)",
+                     "per_channels_ring": "vg_gat_aggregate_fwd_ring (wave-specialised workgroup per CU: 4 loader "
+                                          "waves fill a two-slot LDS ring with each 64-row tile's distinct source "
+                                          "rows by LDS-DMA, 8 consumer waves aggregate the other slot; LDS-counter "
+                                          "hand-over, no barrier)"}
             cands = [(r[key][128]["avg_us"], o, key) for o, r in stress_orders.items() for key in kinds
                      if 128 in r.get(key, {})]
             _, o_best, k_best = min(cands)
@@ -1043,7 +1061,7 @@ def main():
                 "kernel": kinds[k_best],
                 "tile_plan": (f"{best['staged_plan']['distinct_sources_per_64_row_tile']} distinct source rows for "
                               f"{best['staged_plan']['edges_per_64_row_tile']} edges per 64-row tile"
-                              if k_best == "per_channels_staged" else
+                              if k_best in ("per_channels_staged", "per_channels_ring") else
                               f"{best['distinct_sources_per_tile']} distinct source rows for "
                               f"{best['edges_per_tile']} edges per 16-row tile"),
                 "bound": "hbm", "achieved": round(c128["achieved_gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

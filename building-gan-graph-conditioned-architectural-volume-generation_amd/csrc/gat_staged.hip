@@ -54,22 +54,23 @@ constexpr int kRPW = kSRT / (kSNT / 64);  // destination rows per wave and tile 
 // ---------------------------------------------------------------- plan
 // tile t (rows [64 t, 64 t + 64)): ucount[t] distinct sources, sorted, in
 // usrc[t * kSU + u]; lidx[k] = the slot of edge k's source in that list.
+template <int RT, int SU, int SE>
 __global__ void __launch_bounds__(kSNT) k_stage_plan(const int32_t* __restrict__ row_ptr,
                                                      const int32_t* __restrict__ col, int N,
                                                      int32_t* __restrict__ ucount, int32_t* __restrict__ usrc,
                                                      uint16_t* __restrict__ lidx) {
-  __shared__ unsigned long long key[kSE];  // (source << 32) | edge offset in the tile
-  __shared__ int scan[kSE];
+  __shared__ unsigned long long key[SE];  // (source << 32) | edge offset in the tile
+  __shared__ int scan[SE];
   __shared__ int s_long;
   const int t = blockIdx.x, tid = threadIdx.x;
-  const int r0 = t * kSRT, r1 = min(N, r0 + kSRT);
+  const int r0 = t * RT, r1 = min(N, r0 + RT);
   const int e0 = row_ptr[r0], e1 = row_ptr[r1];
   const int ne = e1 - e0;
   if (tid == 0) s_long = 0;
   __syncthreads();
   if (tid < r1 - r0 && row_ptr[r0 + tid + 1] - row_ptr[r0 + tid] > kSDeg) s_long = 1;
   __syncthreads();
-  if (s_long || ne > kSE || ne <= 0) {
+  if (s_long || ne > SE || ne <= 0) {
     if (tid == 0) ucount[t] = ne <= 0 ? 0 : -1;
     return;
   }
@@ -97,28 +98,28 @@ __global__ void __launch_bounds__(kSNT) k_stage_plan(const int32_t* __restrict__
     scan[i] = (i < ne && (i == 0 || (key[i] >> 32) != (key[i - 1] >> 32))) ? 1 : 0;
   __syncthreads();
   for (int off = 1; off < P; off <<= 1) {
-    int v[kSE / kSNT];
+    int v[SE / kSNT];
 #pragma unroll
-    for (int q = 0; q < kSE / kSNT; ++q) {
+    for (int q = 0; q < SE / kSNT; ++q) {
       const int i = tid + kSNT * q;
       v[q] = (i < P && i >= off) ? scan[i - off] : 0;
     }
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < kSE / kSNT; ++q) {
+    for (int q = 0; q < SE / kSNT; ++q) {
       const int i = tid + kSNT * q;
       if (i < P) scan[i] += v[q];
     }
     __syncthreads();
   }
   const int U = scan[ne - 1];
-  if (U > kSU) {
+  if (U > SU) {
     if (tid == 0) ucount[t] = -1;
     return;
   }
   for (int i = tid; i < ne; i += kSNT) {
     const int slot = scan[i] - 1;
-    if (i == 0 || (key[i] >> 32) != (key[i - 1] >> 32)) usrc[(size_t)t * kSU + slot] = static_cast<int>(key[i] >> 32);
+    if (i == 0 || (key[i] >> 32) != (key[i - 1] >> 32)) usrc[(size_t)t * SU + slot] = static_cast<int>(key[i] >> 32);
     lidx[e0 + static_cast<int>(key[i] & 0xffffffffu)] = static_cast<uint16_t>(slot);
   }
   if (tid == 0) ucount[t] = U;
@@ -388,6 +389,473 @@ __global__ void __launch_bounds__(kSNT) k_gat_fwd_staged(
   }
 }
 
+// ------------------------------------------------------ wave-specialised ring
+// k_gat_fwd_ring: the plan's tiles through an LDS ring filled by LOADER waves
+// while CONSUMER waves aggregate the slots already filled, with no workgroup
+// barrier after the prologue.  k_gat_fwd_staged had all 16
+// waves stage, barrier, aggregate, barrier: its 1024-thread workgroups sat
+// parked on those barriers for 47 % of their cycles.  Here, one 16-wave
+// workgroup per CU:
+//
+// * 4 loader waves fill slot (item % NS) -- an item is one 64-channel slice
+//   of a tile -- with the tile's distinct source rows by global_load_lds
+//   (LDS-DMA: 16 B a lane, four 256-B rows a wave instruction, no VGPR round
+//   trip) and, on its first slice, its metadata (row_ptr, a_dst, the edges'
+//   LDS slots, the a_src rows); the next tile's indices are loaded behind the
+//   DMA (one tile ahead).  Then they wait for their loads and bump the slot's
+//   FULL counter;
+// * 12 consumer waves claim (tile, 4-row group) units in order from an LDS
+//   counter, wait for FULL, aggregate their group's rows in 16-lane row groups
+//   out of LDS and bump the slot's FREE counter once per group; a unit spans
+//   the tile's slices, its softmax kept in registers.  A loader refills a slot
+//   once FREE says every group is done with it.  Counters only grow
+//   (generation = item / NS), so nothing is reset inside a launch; every wait
+//   is bounded (on expiry the launch sets *err and ends -- the caller treats
+//   the output as invalid);
+// * the per-row arithmetic is k_gat_fwd_cp<16, 4>'s (16 lanes x 4 channels,
+//   edge j on lane j % 16, slot j / 16; the same max, the same sum order, the
+//   same gather order): bit-identical to vg_gat_aggregate_fwd.  Edge j's
+//   (slot, alpha) reach the row's 16 lanes by DPP row_newbcast and the
+//   softmax's group reductions run on DPP row rotations (no LDS round trip);
+// * tiles the plan could not stage (ucount < 0) are aggregated from global
+//   memory by the consumers with the same arithmetic.
+#ifndef VG_RING_LW
+#define VG_RING_LW 4
+#endif
+#ifndef VG_RING_RT
+#define VG_RING_RT 64  // rows per ring tile: 64 (two slots) or 32 (three; measured slower)
+#endif
+constexpr int kRLW = VG_RING_LW, kRCW = 16 - kRLW;  // loader / consumer waves
+constexpr int kRNT = (kRLW + kRCW) * 64;            // threads per workgroup
+constexpr int kRSpin = 1 << 22;
+
+// A ring's tile geometry: RT rows a tile, up to SU distinct source rows and SE
+// edges staged, NS slots of [SU rows x 64 channels | a_src | row_ptr | a_dst |
+// edge slots] in LDS (+ the counters).
+template <int RT_, int SU_, int SE_, int NS_>
+struct RingGeom {
+  static constexpr int RT = RT_, SU = SU_, SE = SE_, NS = NS_;
+  static constexpr int Groups = RT / 4;                     // 4-row consumer groups per tile
+  static constexpr int RowsB = SU * 64 * 4;
+  static constexpr int RpB = ((RT + 1) * 4 + 15) / 16 * 16;
+  static constexpr int SlotB = RowsB + SU * 4 + RpB + RT * 4 + SE * 2;
+  static constexpr int RingB = NS * SlotB + 64;
+  static constexpr int RowI = (SU / 4 + kRLW - 1) / kRLW;      // row-staging instructions per loader wave
+  static constexpr int AsQ = (SU + kRLW * 64 - 1) / (kRLW * 64);  // a_src entries per loader lane
+  static constexpr int LiQ = (SE + kRLW * 64 - 1) / (kRLW * 64);  // edge slots per loader lane
+  static_assert(RingB <= 160 * 1024, "ring fits the LDS");
+  static_assert(RT <= 64 && kRLW * 64 > RT, "a loader lane per row_ptr entry");
+  static_assert(SU % 4 == 0, "four rows a staging instruction");
+};
+using RingG = RingGeom<VG_RING_RT, VG_RING_RT == 64 ? kSU : 192, VG_RING_RT == 64 ? kSE : 1024,
+                       VG_RING_RT == 64 ? 2 : 3>;
+
+struct RingSlot {
+  float4* rows;   // [SU][16]
+  float* as;      // [SU]
+  int* rp;        // [RT + 1]
+  float* ad;      // [RT]
+  uint16_t* li;   // [SE]
+};
+
+template <class G>
+__device__ __forceinline__ RingSlot ring_slot(char* base, int s) {
+  char* p = base + s * G::SlotB;
+  RingSlot r;
+  r.rows = reinterpret_cast<float4*>(p);
+  r.as = reinterpret_cast<float*>(p + G::RowsB);
+  r.rp = reinterpret_cast<int*>(p + G::RowsB + G::SU * 4);
+  r.ad = reinterpret_cast<float*>(p + G::RowsB + G::SU * 4 + G::RpB);
+  r.li = reinterpret_cast<uint16_t*>(p + G::RowsB + G::SU * 4 + G::RpB + G::RT * 4);
+  return r;
+}
+
+// wait until *flag >= target (LDS counter, workgroup scope); false on expiry
+#ifndef VG_RING_PROF
+#define VG_RING_PROF 0  // 1: per-wave wait / busy clocks into g_ring_prof (tools/ring_probe.py; A/B builds only)
+#endif
+#if VG_RING_PROF
+__device__ unsigned long long g_ring_prof[2048 * 16 * 4];
+#endif
+
+__device__ __forceinline__ bool ring_wait(int* flag, int target) {
+  for (int it = 0; it < kRSpin; ++it) {
+    if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) return true;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return false;
+}
+
+// lane k of each 16-lane DPP row to the whole row (row_newbcast, gfx90a+)
+template <int K>
+__device__ __forceinline__ int row_bcast16(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, 0x150 + K, 0xF, 0xF, false);
+}
+
+#ifndef VG_RING_GDEPTH
+#define VG_RING_GDEPTH 8  // source rows read out of LDS before their FMAs (8 or 4)
+#endif
+#ifndef VG_RING_DPPRED
+#define VG_RING_DPPRED 1  // the softmax's group reductions by DPP row rotations (0: group_max / group_sum)
+#endif
+// group_sum<16> / group_max<16> (rowgroup.h: the xor butterfly over offsets
+// 8, 4, 2, 1) by DPP row rotations inside each 16-lane row: after the
+// offset-8 step every value has period 8, so rotating by 4 pairs the same
+// lanes as xor 4 (and then 2, 1) -- the same additions, commutative, so every
+// lane ends with the butterfly's value bit for bit, with no LDS round trip.
+template <int R>
+__device__ __forceinline__ float row_ror16(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x120 + R, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float ring_sum16(float v) {
+  v += row_ror16<8>(v);
+  v += row_ror16<4>(v);
+  v += row_ror16<2>(v);
+  v += row_ror16<1>(v);
+  return v;
+}
+__device__ __forceinline__ float ring_max16(float v) {
+  v = fmaxf(v, row_ror16<8>(v));
+  v = fmaxf(v, row_ror16<4>(v));
+  v = fmaxf(v, row_ror16<2>(v));
+  v = fmaxf(v, row_ror16<1>(v));
+  return v;
+}
+
+// edges 16 Q .. 16 Q + 15 of the group's row: slot / alpha from lane j % 16,
+// eight source rows read out of LDS before their FMAs (in edge order)
+template <int Q>
+__device__ __forceinline__ void ring_gather_q(const RingSlot& R, int sq, float eq, int dreg, int dmax, int l16,
+                                              float (&acc)[4]) {
+  const int eqb = __float_as_int(eq);
+#define VG_RG_LD(K)                                                                       \
+  const int s##K = row_bcast16<(K)>(sq);                                                  \
+  const float a##K = __int_as_float(row_bcast16<(K)>(eqb));                               \
+  const float4 h##K = 16 * Q + (K) < dreg ? R.rows[s##K * 16 + l16] : make_float4(0.f, 0.f, 0.f, 0.f);
+#define VG_RG_FMA(K)                                                                      \
+  if (16 * Q + (K) < dreg) {                                                              \
+    acc[0] = fmaf(a##K, h##K.x, acc[0]);                                                  \
+    acc[1] = fmaf(a##K, h##K.y, acc[1]);                                                  \
+    acc[2] = fmaf(a##K, h##K.z, acc[2]);                                                  \
+    acc[3] = fmaf(a##K, h##K.w, acc[3]);                                                  \
+  }
+#if VG_RING_GDEPTH == 8
+  if (16 * Q < dmax) {
+    VG_RG_LD(0) VG_RG_LD(1) VG_RG_LD(2) VG_RG_LD(3) VG_RG_LD(4) VG_RG_LD(5) VG_RG_LD(6) VG_RG_LD(7)
+    VG_RG_FMA(0) VG_RG_FMA(1) VG_RG_FMA(2) VG_RG_FMA(3) VG_RG_FMA(4) VG_RG_FMA(5) VG_RG_FMA(6) VG_RG_FMA(7)
+  }
+  if (16 * Q + 8 < dmax) {
+    VG_RG_LD(8) VG_RG_LD(9) VG_RG_LD(10) VG_RG_LD(11) VG_RG_LD(12) VG_RG_LD(13) VG_RG_LD(14) VG_RG_LD(15)
+    VG_RG_FMA(8) VG_RG_FMA(9) VG_RG_FMA(10) VG_RG_FMA(11) VG_RG_FMA(12) VG_RG_FMA(13) VG_RG_FMA(14) VG_RG_FMA(15)
+  }
+#else  // four rows in flight
+  if (16 * Q < dmax) { VG_RG_LD(0) VG_RG_LD(1) VG_RG_LD(2) VG_RG_LD(3) VG_RG_FMA(0) VG_RG_FMA(1) VG_RG_FMA(2) VG_RG_FMA(3) }
+  if (16 * Q + 4 < dmax) { VG_RG_LD(4) VG_RG_LD(5) VG_RG_LD(6) VG_RG_LD(7) VG_RG_FMA(4) VG_RG_FMA(5) VG_RG_FMA(6) VG_RG_FMA(7) }
+  if (16 * Q + 8 < dmax) { VG_RG_LD(8) VG_RG_LD(9) VG_RG_LD(10) VG_RG_LD(11) VG_RG_FMA(8) VG_RG_FMA(9) VG_RG_FMA(10) VG_RG_FMA(11) }
+  if (16 * Q + 12 < dmax) { VG_RG_LD(12) VG_RG_LD(13) VG_RG_LD(14) VG_RG_LD(15) VG_RG_FMA(12) VG_RG_FMA(13) VG_RG_FMA(14) VG_RG_FMA(15) }
+#endif
+#undef VG_RG_LD
+#undef VG_RG_FMA
+}
+
+// One tile's indices held by a loader lane between its two phases (and
+// across the tile's channel slices): edge slots, the a_src rows, the source
+// rows of this wave's LDS-DMA instructions.
+template <class G>
+struct RingIdx {
+  int U, e0, ne, rp, lq[G::LiQ], ua[G::AsQ], sr[G::RowI];
+  float ad;
+};
+
+template <class G>
+__device__ __forceinline__ void ring_load_idx(RingIdx<G>& x, int t, int N, int wave, int lane,
+                                              const int32_t* __restrict__ row_ptr, const float* __restrict__ a_dst,
+                                              const int32_t* __restrict__ ucount, const int32_t* __restrict__ usrc,
+                                              const uint16_t* __restrict__ lidx) {
+  const int lt = wave * 64 + lane;
+  const int r0 = t * G::RT;
+  x.U = ucount[t];
+  x.e0 = row_ptr[r0];
+  x.ne = row_ptr[min(r0 + G::RT, N)] - x.e0;
+  x.rp = row_ptr[min(r0 + min(lt, G::RT), N)];
+  x.ad = a_dst[min(r0 + min(lt, G::RT - 1), N - 1)];
+  if (x.U > 0) {
+    const int32_t* us = usrc + (size_t)t * G::SU;
+#pragma unroll
+    for (int q = 0; q < G::LiQ; ++q) {
+      const int e = lt + q * kRLW * 64;
+      x.lq[q] = e < x.ne ? static_cast<int>(lidx[x.e0 + e]) : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < G::AsQ; ++q) x.ua[q] = us[min(lt + q * kRLW * 64, x.U - 1)];
+#pragma unroll
+    for (int q = 0; q < G::RowI; ++q) x.sr[q] = us[min(4 * (wave + q * kRLW) + (lane >> 4), x.U - 1)];
+  }
+}
+
+// a consumer group's row state, kept across the tile's channel slices
+struct RingRow {
+  int s_t[4];
+  float e_t[4];
+  int beg, deg, dreg, r;
+  float ad, m, denom;
+};
+
+template <class G>
+__global__ void __launch_bounds__(kRNT) k_gat_fwd_ring(
+    const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, int N, int C,
+    const float* __restrict__ h, const float* __restrict__ a_src, const float* __restrict__ a_dst,
+    const float* __restrict__ bias, float slope, float* __restrict__ out, float* __restrict__ alpha,
+    const int32_t* __restrict__ ucount, const int32_t* __restrict__ usrc, const uint16_t* __restrict__ lidx,
+    int tiles, int* __restrict__ err) {
+  extern __shared__ float4 ring4[];
+  char* base = reinterpret_cast<char*>(ring4);
+  int* cnt = reinterpret_cast<int*>(base + G::NS * G::SlotB);  // full[NS], free[NS], the next unit
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int slices = C / 64;
+  // static, XCD-aware schedule as k_gat_fwd_staged; item k = (tile k / slices, slice k % slices)
+  const int per = gridDim.x >> 3, xcd = blockIdx.x & 7, wslot = blockIdx.x >> 3;
+  const int tb = static_cast<int>((long long)tiles * xcd / 8);
+  const int te = static_cast<int>((long long)tiles * (xcd + 1) / 8);
+  const int my_tiles = tb + wslot < te ? (te - tb - wslot + per - 1) / per : 0;
+  const int items = my_tiles * slices;
+  if (tid < 2 * G::NS + 1) cnt[tid] = 0;
+  __syncthreads();
+  if (items == 0) return;
+#if VG_RING_PROF
+  const unsigned long long t_start = __builtin_readcyclecounter();
+  unsigned long long waited = 0, t_soft = 0, t_gath = 0;
+  auto prof_out = [&]() {
+    if (lane == 0) {
+      g_ring_prof[(blockIdx.x * 16 + wave) * 4] = waited;
+      g_ring_prof[(blockIdx.x * 16 + wave) * 4 + 1] = __builtin_readcyclecounter() - t_start;
+      g_ring_prof[(blockIdx.x * 16 + wave) * 4 + 2] = t_soft;
+      g_ring_prof[(blockIdx.x * 16 + wave) * 4 + 3] = t_gath;
+    }
+  };
+#define VG_RING_WAIT(flag, target, code)                         \
+  do {                                                           \
+    const unsigned long long w0_ = __builtin_readcyclecounter(); \
+    if (!ring_wait(flag, target)) {                              \
+      if (lane == 0) atomicOr(err, code);                        \
+      return;                                                    \
+    }                                                            \
+    waited += __builtin_readcyclecounter() - w0_;                \
+  } while (0)
+#else
+#define VG_RING_WAIT(flag, target, code)  \
+  do {                                    \
+    if (!ring_wait(flag, target)) {       \
+      if (lane == 0) atomicOr(err, code); \
+      return;                             \
+    }                                     \
+  } while (0)
+#endif
+
+  if (wave < kRLW) {  // ------------------------------------------------ loaders
+    const int lt = wave * 64 + lane;  // 0 .. 255
+    RingIdx<G> cur, nxt;
+    ring_load_idx<G>(cur, tb + wslot, N, wave, lane, row_ptr, a_dst, ucount, usrc, lidx);
+    for (int k = 0; k < items; ++k) {
+      const int s = k % G::NS, gen = k / G::NS, sl = k % slices;
+      const int j = k / slices;
+      const int t = tb + wslot + j * per;
+      if (k >= G::NS) VG_RING_WAIT(&cnt[G::NS + s], G::Groups * gen, 1);
+      RingSlot R = ring_slot<G>(base, s);
+      // this slice's rows by LDS-DMA (and, on the tile's first slice, its a_src rows)
+      float av[G::AsQ];
+      if (cur.U > 0) {
+        if (sl == 0)
+#pragma unroll
+          for (int q = 0; q < G::AsQ; ++q) av[q] = a_src[cur.ua[q]];
+        const int ni = (cur.U + 3) / 4;
+#pragma unroll
+        for (int q = 0; q < G::RowI; ++q) {
+          const int i = wave + q * kRLW;
+          if (i < ni) {
+            const float* src = h + (size_t)cur.sr[q] * C + sl * 64 + (lane & 15) * 4;
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
+                                             (__attribute__((address_space(3))) void*)(R.rows + 4 * i * 16), 16, 0, 0);
+          }
+        }
+      }
+      // the next tile's indices in flight behind them (its first slice's item)
+      const bool pre = sl == slices - 1 && j + 1 < my_tiles;
+      if (pre) ring_load_idx<G>(nxt, t + per, N, wave, lane, row_ptr, a_dst, ucount, usrc, lidx);
+      if (sl == 0) {  // the tile's metadata: row_ptr, a_dst, edge slots, a_src (consumers keep them per tile)
+        if (lt <= G::RT) R.rp[lt] = cur.rp;
+        if (lt < G::RT) R.ad[lt] = cur.ad;
+        if (cur.U > 0) {
+#pragma unroll
+          for (int q = 0; q < G::LiQ; ++q) {
+            const int e = lt + q * kRLW * 64;
+            if (e < cur.ne) R.li[e] = static_cast<uint16_t>(cur.lq[q]);
+          }
+#pragma unroll
+          for (int q = 0; q < G::AsQ; ++q) {
+            const int u = lt + q * kRLW * 64;
+            if (u < cur.U) R.as[u] = av[q];
+          }
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_fetch_add(&cnt[s], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (pre) cur = nxt;
+    }
+#if VG_RING_PROF
+    prof_out();
+#endif
+    return;
+  }
+
+  // -------------------------------------------------------------- consumers
+  // units (tile j, 4-row group g) are claimed in order from an LDS counter,
+  // so the consumer waves share a tile's 16 groups whatever their count; a
+  // unit spans the tile's channel slices (its softmax is kept in registers)
+  constexpr int L = 16, T = 4;
+  const int l16 = lane & 15, gbase = lane & 48;
+  const int units = my_tiles * G::Groups;
+  for (;;) {
+    int u = 0;
+    if (lane == 0) u = __hip_atomic_fetch_add(&cnt[2 * G::NS], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    u = __builtin_amdgcn_readfirstlane(u);
+    if (u >= units) break;
+    const int j = u / G::Groups, grp = u % G::Groups;
+    RingRow w;
+    for (int sl = 0; sl < slices; ++sl) {
+    const int k = j * slices + sl;
+    const int s = k % G::NS, gen = k / G::NS;
+    const int t = tb + wslot + j * per;
+    VG_RING_WAIT(&cnt[s], kRLW * (gen + 1), 2);
+    RingSlot R = ring_slot<G>(base, s);
+    const int r0 = t * G::RT;
+    const int U = ucount[t];
+    const bool staged = U >= 0;
+    const float* hs = h + sl * 64;
+    const float4 bv = *reinterpret_cast<const float4*>(bias + sl * 64 + l16 * 4);
+    {
+#if VG_RING_PROF
+      const unsigned long long p0 = __builtin_readcyclecounter();
+#endif
+      if (sl == 0) {  // the row's softmax, once per tile (its slices reuse it)
+        const int e0 = R.rp[0];
+        const int ri = 4 * grp + (lane >> 4);  // this group's row in the tile
+        w.r = r0 + ri;
+        w.beg = R.rp[ri];
+        const int end = R.rp[ri + 1];
+        w.deg = end - w.beg;
+        w.ad = R.ad[ri];
+        bool v_t[T];
+        float m = -INFINITY;
+#pragma unroll
+        for (int q = 0; q < T; ++q) {
+          const int jj = l16 + q * L;
+          v_t[q] = jj < w.deg;
+          w.s_t[q] = v_t[q] ? (staged ? static_cast<int>(R.li[w.beg - e0 + jj]) : col[w.beg + jj]) : 0;
+        }
+#pragma unroll
+        for (int q = 0; q < T; ++q) {
+          w.e_t[q] = -INFINITY;
+          if (v_t[q]) {
+            w.e_t[q] = lrelu((staged ? R.as[w.s_t[q]] : a_src[w.s_t[q]]) + w.ad, slope);
+            m = fmaxf(m, w.e_t[q]);
+          }
+        }
+        for (int kk = w.beg + l16 + T * L; kk < end; kk += L) m = fmaxf(m, lrelu(a_src[col[kk]] + w.ad, slope));
+        m = VG_RING_DPPRED ? ring_max16(m) : group_max<L>(m);
+        float ssum = 0.f;
+#pragma unroll
+        for (int q = 0; q < T; ++q)
+          if (v_t[q]) {
+            w.e_t[q] = expf(w.e_t[q] - m);
+            ssum += w.e_t[q];
+          }
+        for (int kk = w.beg + l16 + T * L; kk < end; kk += L) ssum += expf(lrelu(a_src[col[kk]] + w.ad, slope) - m);
+        const float denom = (VG_RING_DPPRED ? ring_sum16(ssum) : group_sum<L>(ssum)) + kSoftmaxEps;
+        const bool live = w.r < N;
+#pragma unroll
+        for (int q = 0; q < T; ++q)
+          if (v_t[q]) {
+            w.e_t[q] = w.e_t[q] / denom;
+            if (live) alpha[w.beg + l16 + q * L] = w.e_t[q];
+          }
+        if (live)
+          for (int kk = w.beg + l16 + T * L; kk < end; kk += L)
+            alpha[kk] = expf(lrelu(a_src[col[kk]] + w.ad, slope) - m) / denom;
+        w.m = m;
+        w.denom = denom;
+        w.dreg = w.deg < T * L ? w.deg : T * L;
+      }
+#if VG_RING_PROF
+      const unsigned long long p1 = __builtin_readcyclecounter();
+      t_soft += p1 - p0;
+#endif
+      // gather-sum over the edges in CSR order
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      const int dreg = w.dreg;
+      if (staged) {
+        // edge j's (slot, alpha) broadcast from lane j % 16 of the row's
+        // 16-lane group by DPP row_newbcast (no LDS round trip), four source
+        // rows read out of LDS in flight, the FMAs in edge order
+        int dmax = dreg;
+        for (int off = 16; off < 64; off <<= 1) dmax = max(dmax, __shfl_xor(dmax, off, 64));
+        dmax = __builtin_amdgcn_readfirstlane(dmax);
+        ring_gather_q<0>(R, w.s_t[0], w.e_t[0], dreg, dmax, l16, acc);
+        ring_gather_q<1>(R, w.s_t[1], w.e_t[1], dreg, dmax, l16, acc);
+        ring_gather_q<2>(R, w.s_t[2], w.e_t[2], dreg, dmax, l16, acc);
+        ring_gather_q<3>(R, w.s_t[3], w.e_t[3], dreg, dmax, l16, acc);
+      }
+      for (int j0 = 0; !staged && j0 < dreg; j0 += 4) {
+        const int nj = dreg - j0 < 4 ? dreg - j0 : 4;
+        float4 hv[4];
+        float a[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (u < nj) {
+            const int jj = j0 + u;
+            const int q = jj / L;
+            const int sv = q == 0 ? w.s_t[0] : q == 1 ? w.s_t[1] : q == 2 ? w.s_t[2] : w.s_t[3];
+            const float avv = q == 0 ? w.e_t[0] : q == 1 ? w.e_t[1] : q == 2 ? w.e_t[2] : w.e_t[3];
+            const int sr = __shfl(sv, gbase + (jj & (L - 1)), 64);
+            a[u] = __shfl(avv, gbase + (jj & (L - 1)), 64);
+            hv[u] = *reinterpret_cast<const float4*>(hs + (size_t)sr * C + l16 * 4);
+          }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (u < nj) {
+            acc[0] = fmaf(a[u], hv[u].x, acc[0]);
+            acc[1] = fmaf(a[u], hv[u].y, acc[1]);
+            acc[2] = fmaf(a[u], hv[u].z, acc[2]);
+            acc[3] = fmaf(a[u], hv[u].w, acc[3]);
+          }
+      }
+      for (int jj = T * L; jj < w.deg; ++jj) {  // very long rows (global tiles only): alpha recomputed
+        const int sj = col[w.beg + jj];
+        const float aa = expf(lrelu(a_src[sj] + w.ad, slope) - w.m) / w.denom;
+        const float4 v = *reinterpret_cast<const float4*>(hs + (size_t)sj * C + l16 * 4);
+        acc[0] = fmaf(aa, v.x, acc[0]);
+        acc[1] = fmaf(aa, v.y, acc[1]);
+        acc[2] = fmaf(aa, v.z, acc[2]);
+        acc[3] = fmaf(aa, v.w, acc[3]);
+      }
+      if (w.r < N)
+        *reinterpret_cast<float4*>(out + (size_t)w.r * C + sl * 64 + l16 * 4) =
+            make_float4(acc[0] + bv.x, acc[1] + bv.y, acc[2] + bv.z, acc[3] + bv.w);
+#if VG_RING_PROF
+      t_gath += __builtin_readcyclecounter() - p1;
+#endif
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add(&cnt[G::NS + s], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+#if VG_RING_PROF
+  prof_out();
+#endif
+#undef VG_RING_WAIT
+}
+
 int g_num_cu = 0;
 
 int num_cu() {
@@ -411,6 +879,60 @@ int num_cu() {
 #undef VG_STAGE_LOAD
 #undef VG_STAGE_STORE
 
+extern "C" int64_t vg_gat_ring_plan_ints(int32_t num_nodes, int32_t num_edges) {
+  const int64_t tiles = ((int64_t)num_nodes + RingG::RT - 1) / RingG::RT;
+  return tiles + tiles * RingG::SU + ((int64_t)num_edges + 1) / 2;
+}
+
+extern "C" int vg_gat_ring_plan(const int32_t* row_ptr, const int32_t* col, int32_t N, int32_t E, int32_t* plan,
+                                void* stream) {
+  if (N <= 0 || E <= 0 || !row_ptr || !col || !plan) return VG_EINVAL;
+  const int tiles = (N + RingG::RT - 1) / RingG::RT;
+  int32_t* ucount = plan;
+  int32_t* usrc = plan + tiles;
+  uint16_t* lidx = reinterpret_cast<uint16_t*>(usrc + (size_t)tiles * RingG::SU);
+  k_stage_plan<RingG::RT, RingG::SU, RingG::SE><<<tiles, kSNT, 0, static_cast<hipStream_t>(stream)>>>(
+      row_ptr, col, N, ucount, usrc, lidx);
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int vg_gat_aggregate_fwd_ring(const int32_t* row_ptr, const int32_t* col, int32_t N, int32_t C,
+                                         const float* h, const float* a_src, const float* a_dst, const float* bias,
+                                         float slope, float* out, float* alpha, const int32_t* plan, int32_t* err,
+                                         void* stream) {
+  if (N <= 0 || (C != 64 && C != 128) || !row_ptr || !col || !h || !a_src || !a_dst || !bias || !out || !alpha ||
+      !plan || !err || (reinterpret_cast<uintptr_t>(h) & 15) || (reinterpret_cast<uintptr_t>(out) & 15) ||
+      (reinterpret_cast<uintptr_t>(bias) & 15))
+    return VG_EINVAL;
+  const int tiles = (N + RingG::RT - 1) / RingG::RT;
+  const int32_t* ucount = plan;
+  const int32_t* usrc = plan + tiles;
+  const uint16_t* lidx = reinterpret_cast<const uint16_t*>(usrc + (size_t)tiles * RingG::SU);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gat_fwd_ring<RingG>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, RingG::RingB);
+    attr = true;
+  }
+  // one workgroup per CU (the ring takes the LDS), a multiple of 8 (the XCD schedule)
+  int grid = num_cu();
+  const int need = (tiles + 7) / 8 * 8;
+  if (grid > need) grid = need;
+  grid = (grid + 7) / 8 * 8;
+  k_gat_fwd_ring<RingG><<<grid, kRNT, RingG::RingB, static_cast<hipStream_t>(stream)>>>(
+      row_ptr, col, N, C, h, a_src, a_dst, bias, slope, out, alpha, ucount, usrc, lidx, tiles, err);
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+#if VG_RING_PROF
+// the per-wave (waited, total) clocks of the last ring launch (profiling builds only)
+extern "C" int vg_ring_prof_read(unsigned long long* host, int n) {
+  return static_cast<int>(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ring_prof), sizeof(unsigned long long) * n));
+}
+#endif
+
 extern "C" int64_t vg_gat_stage_plan_ints(int32_t num_nodes, int32_t num_edges) {
   const int64_t tiles = ((int64_t)num_nodes + kSRT - 1) / kSRT;
   // ucount [tiles] + usrc [tiles * kSU] (int32) + lidx [E'] (uint16, rounded up to int32s)
@@ -424,7 +946,8 @@ extern "C" int vg_gat_stage_plan(const int32_t* row_ptr, const int32_t* col, int
   int32_t* ucount = plan;
   int32_t* usrc = plan + tiles;
   uint16_t* lidx = reinterpret_cast<uint16_t*>(usrc + (size_t)tiles * kSU);
-  k_stage_plan<<<tiles, kSNT, 0, static_cast<hipStream_t>(stream)>>>(row_ptr, col, N, ucount, usrc, lidx);
+  k_stage_plan<kSRT, kSU, kSE><<<tiles, kSNT, 0, static_cast<hipStream_t>(stream)>>>(row_ptr, col, N, ucount, usrc,
+                                                                                     lidx);
   VG_CHECK_LAUNCH();
   return 0;
 }

@@ -192,6 +192,19 @@ class CSR:
     def stage_tiles(self) -> int:
         return (self.num_nodes + 63) // 64
 
+    def ring_plan(self) -> torch.Tensor:
+        """The ring aggregation's tile plan (vg_gat_ring_plan: per 32-row tile
+        the distinct sources and every edge's LDS slot), built once and
+        cached; consumed by vg_gat_aggregate_fwd_ring."""
+        plan = self.__dict__.get("_ring_plan")
+        if plan is None:
+            n_ints = int(LIB.vg_gat_ring_plan_ints(self.num_nodes, self.num_edges))
+            plan = torch.empty(n_ints, dtype=torch.int32, device=self.device)
+            check(LIB.vg_gat_ring_plan(ptr(self.row_ptr), ptr(self.col), self.num_nodes, self.num_edges, ptr(plan),
+                                       self.stream()), "vg_gat_ring_plan")
+            self._ring_plan = plan
+        return plan
+
 
 def aggregate_fwd_raw(csr: "CSR", c: int, h, a_src, a_dst, bias, slope: float, out, alpha, stream,
                       gnp=None) -> None:

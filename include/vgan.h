@@ -775,6 +775,22 @@ int vg_gat_aggregate_fwd_staged(const int32_t* row_ptr, const int32_t* col, int3
                                 const float* h, const float* a_src, const float* a_dst, const float* bias,
                                 float slope, float* out, float* alpha, const int32_t* plan, void* stream);
 
+/* The same aggregation with wave-specialised workgroups (one per CU): loader
+ * waves fill a three-slot LDS ring with each 32-row tile's metadata and
+ * distinct source rows (LDS-DMA, one 64-channel slice at a time) while
+ * consumer waves aggregate the slots already filled out of LDS in 16-lane row
+ * groups; the slots are handed over by LDS counters, no workgroup barrier.
+ * Bit-identical to vg_gat_aggregate_fwd.  C = 64 or 128; h, out, bias 16-B
+ * aligned; plan from vg_gat_ring_plan over the same CSR (its tile plan:
+ * vg_gat_ring_plan_ints(N, E') int32s).  *err (a zeroed int32) is left
+ * nonzero if a hand-over wait expired (the output is then invalid). */
+int64_t vg_gat_ring_plan_ints(int32_t num_nodes, int32_t num_edges);
+int vg_gat_ring_plan(const int32_t* row_ptr, const int32_t* col, int32_t num_nodes, int32_t num_edges,
+                     int32_t* plan_out, void* stream);
+int vg_gat_aggregate_fwd_ring(const int32_t* row_ptr, const int32_t* col, int32_t num_nodes, int32_t channels,
+                              const float* h, const float* a_src, const float* a_dst, const float* bias, float slope,
+                              float* out, float* alpha, const int32_t* plan, int32_t* err, void* stream);
+
 /* ---- GraphNorm backward partials in the producing GEMM -------------------- */
 
 /* C[N,M] = A[N,K] B[K,M] (vg_gemm, b_trans 0, no bias / activation) is the

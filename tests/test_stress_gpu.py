@@ -89,9 +89,14 @@ def _run(kind, csr, c, h, a_s, a_d, b):
         plan = csr.tile_plan()
         check(LIB.vg_gat_aggregate_fwd_lds(ptr(csr.row_ptr), ptr(csr.col), n, *args, ptr(plan), csr._tile_umax,
                                            csr.stream()), kind)
-    else:
+    elif kind == "staged":
         check(LIB.vg_gat_aggregate_fwd_staged(ptr(csr.row_ptr), ptr(csr.col), n, *args, ptr(csr.stage_plan()),
                                               csr.stream()), kind)
+    else:  # the wave-specialised ring
+        err = torch.zeros(1, dtype=torch.int32, device=h.device)
+        check(LIB.vg_gat_aggregate_fwd_ring(ptr(csr.row_ptr), ptr(csr.col), n, *args, ptr(csr.ring_plan()), ptr(err),
+                                            csr.stream()), kind)
+        assert int(err.item()) == 0, "ring hand-over wait expired"
     return out, alpha
 
 
@@ -104,7 +109,7 @@ def test_stress_aggregations_against_oracle(cuda, stress_items, order, C):
     h = torch.randn(n, C, device=cuda)
     a_s, a_d = 0.5 * torch.randn(n, device=cuda), 0.5 * torch.randn(n, device=cuda)
     b = torch.randn(C, device=cuda)
-    kinds = ["register", "ell"] + (["lds"] if C % 64 == 0 else []) + (["staged"] if C in (64, 128) else [])
+    kinds = ["register", "ell"] + (["lds"] if C % 64 == 0 else []) + (["staged", "ring"] if C in (64, 128) else [])
     outs = {k: _run(k, csr, C, h, a_s, a_d, b) for k in kinds}
     torch.cuda.synchronize()
     ref_out, ref_alpha = outs["register"]
@@ -155,3 +160,34 @@ def test_stress_gat_block_forward_backward_against_oracle(cuda, stress_items):
     print({k: f"{v:.2e}" for k, v in errs.items()})
     for k, v in errs.items():
         assert v < 1e-4, k
+
+
+@pytest.mark.parametrize("C", [64, 128])
+def test_ring_aggregation_ragged_graph_bitwise(cuda, C):
+    """The wave-specialised ring kernel on a graph that exercises its other
+    paths: a ragged last tile (N % 64 != 0), rows with no in-edges, hub rows
+    longer than 64 edges (their tiles aggregated from global memory) and tiles
+    with more distinct sources than the ring's 192-row image -- bit-identical to the
+    register kernel, with the hand-over flag untouched."""
+    from vgan import ops
+
+    g = torch.Generator().manual_seed(C)
+    n = 5000 + 37
+    e_loc = torch.randint(0, 40, (2, 30000), generator=g)  # mostly local edges
+    e_loc[1] = (e_loc[0] + torch.randint(0, 40, (30000,), generator=g)) % n
+    e_loc[0] = (e_loc[0] * 97 + torch.randint(0, n, (30000,), generator=g) // 50) % n
+    hubs = torch.stack([torch.randint(0, n, (600,), generator=g), torch.full((600,), 123)])  # deg 600 row
+    wide = torch.stack([torch.randint(0, n, (900,), generator=g), torch.randint(640, 704, (900,), generator=g)])
+    ei = torch.cat([e_loc, hubs, wide], 1)
+    ei = ei[:, ei[1] != 4000]  # row 4000: only its self loop
+    csr = ops.CSR(ei.to(cuda), n)
+    torch.manual_seed(C)
+    h = torch.randn(n, C, device=cuda)
+    a_s, a_d = 0.5 * torch.randn(n, device=cuda), 0.5 * torch.randn(n, device=cuda)
+    b = torch.randn(C, device=cuda)
+    ref_out, ref_alpha = _run("register", csr, C, h, a_s, a_d, b)
+    out, alpha = _run("ring", csr, C, h, a_s, a_d, b)
+    torch.cuda.synchronize()
+    ucount = csr.ring_plan()[:(n + 31) // 32].cpu()
+    assert (ucount < 0).any() and (ucount > 0).any()  # both tile kinds ran
+    assert torch.equal(out, ref_out) and torch.equal(alpha, ref_alpha)
