@@ -305,7 +305,8 @@ def _train_stream(cuda, precision, batches, steps, rng_seed_offset: int = 0):
 
 def test_bf16_training_tracks_f32_over_200_steps(cuda):
     """configs[2]'s training quality: 200 graphed steps in bf16 and in f32 on
-    the same synthetic stream (10 batches of 16 buildings, cycled) from the
+    the same synthetic stream (10 batches of 32 buildings -- configs[2]'s
+    batch -- cycled) from the
     same initialisation and device-RNG stream, against the spread of two f32
     runs that differ only in the device-RNG seed (WGAN-GP training is chaotic:
     a run's trajectory is only defined up to that spread).  Stated band
@@ -317,10 +318,10 @@ def test_bf16_training_tracks_f32_over_200_steps(cuda):
     (tests/test_rng_gpu.py::test_exponential_strictly_positive)."""
     from vgan.synth import SyntheticDataset
 
-    ds = SyntheticDataset(160, seed=777)
+    ds = SyntheticDataset(320, seed=777)
     batches = []
     for b in range(10):
-        loc, vox = ds.batch(range(16 * b, 16 * b + 16))
+        loc, vox = ds.batch(range(32 * b, 32 * b + 32))
         batches.append((loc.to(cuda), vox.to(cuda)))
     (l32, f32_, _) = _train_stream(cuda, "f32", batches, 200)
     (l16, f16_, _) = _train_stream(cuda, "bf16", batches, 200)
