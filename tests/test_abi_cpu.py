@@ -55,6 +55,46 @@ def test_workspace_queries_are_host_only():
     assert lib.vg_graphnorm_ws_floats(1000, 16) >= 2 * 16
 
 
+def test_hgen_arena_sizing_is_host_only():
+    """vg_hgen_arena_bytes runs the f16 sweep engine's orchestration dry (no
+    launch, no device pointer read): a consistent generator description sizes
+    a 256-byte-granular arena that grows with the batch; an MLP whose input
+    width does not match the row buffer, or an empty batch, is refused."""
+    import ctypes as ct
+
+    from vgan._lib import LIB as lib, VgHgenBatch, VgHgenModel
+
+    md = VgHgenModel()
+    md.n_matched, md.n_mlp, md.n_blocks, md.n_dec = 1, 1, 2, 1
+    fl, vd, zd, hl, hg = 17, 12, 128, 32, 64
+
+    def lin(d, i, o, ln=True):
+        d.weight, d.ldw, d.bias = 1, (i + 7) // 8 * 8, 1
+        d.gamma = d.beta = 1 if ln else None
+        d.eps, d.slope, d.in_, d.out = 1e-5, 0.2, i, o
+
+    lin(md.matched[0], fl, hl)
+    lin(md.mlp[0], hl + vd + zd, hg)
+    for b, (i, o) in enumerate(((hg, 32), (32, 8))):
+        d = md.block[b]
+        d.lin_weight, d.ldw, d.att_src, d.att_dst, d.bias, d.slope = 1, (i + 7) // 8 * 8, 1, 1, 1, 0.2
+        d.gn_weight = d.gn_bias = d.gn_mean_scale = 1
+        d.gn_eps, d.in_, d.out = 1e-5, i, o
+    lin(md.dec[0], 8 + hg + hl + vd + zd, 64)
+    lin(md.head, 64, 7, ln=False)
+
+    def size(n, copies):
+        bt = VgHgenBatch()
+        bt.n, bt.copies, bt.voxel_dim, bt.matched_dim, bt.z_dim, bt.num_edges = n, copies, vd, fl, zd, 9 * n
+        return int(lib.vg_hgen_arena_bytes(ct.byref(md), ct.byref(bt)))
+
+    a, b = size(1000, 1), size(1000, 10)
+    assert a > 0 and b > a and a % 256 == 0 and b % 256 == 0
+    assert size(0, 10) < 0
+    md.mlp[0].in_ = hl + vd  # not the [em | voxel.x | z] width
+    assert size(1000, 10) < 0
+
+
 def test_ops_refuse_cpu_tensors():
     import torch
 
