@@ -401,9 +401,9 @@ __global__ void __launch_bounds__(kSNT) k_gat_fwd_staged(
 //   of a tile -- with the tile's distinct source rows by global_load_lds
 //   (LDS-DMA: 16 B a lane, four 256-B rows a wave instruction, no VGPR round
 //   trip) and, on its first slice, its metadata (row_ptr, a_dst, the edges'
-//   LDS slots, the a_src rows); the next tile's indices are loaded behind the
-//   DMA (one tile ahead).  Then they wait for their loads and bump the slot's
-//   FULL counter;
+//   LDS slots, the a_src rows); the index loads run two stages ahead (the
+//   next tile's body, the head of the one after).  Then they wait for their
+//   loads and bump the slot's FULL counter;
 // * 12 consumer waves claim (tile, 4-row group) units in order from an LDS
 //   counter, wait for FULL, aggregate their group's rows in 16-lane row groups
 //   out of LDS and bump the slot's FREE counter once per group; a unit spans
@@ -423,9 +423,12 @@ __global__ void __launch_bounds__(kSNT) k_gat_fwd_staged(
 #define VG_RING_LW 4
 #endif
 #ifndef VG_RING_RT
-#define VG_RING_RT 64  // rows per ring tile: 64 (two slots) or 32 (three; measured slower)
+#define VG_RING_RT 64  // rows per ring tile: 64 (two slots); 48 (two) and 32 (three) measured slower, DESIGN.md 4.41
 #endif
-constexpr int kRLW = VG_RING_LW, kRCW = 16 - kRLW;  // loader / consumer waves
+#ifndef VG_RING_CW
+#define VG_RING_CW (16 - VG_RING_LW)
+#endif
+constexpr int kRLW = VG_RING_LW, kRCW = VG_RING_CW;  // loader / consumer waves
 constexpr int kRNT = (kRLW + kRCW) * 64;            // threads per workgroup
 constexpr int kRSpin = 1 << 22;
 
@@ -447,8 +450,8 @@ struct RingGeom {
   static_assert(RT <= 64 && kRLW * 64 > RT, "a loader lane per row_ptr entry");
   static_assert(SU % 4 == 0, "four rows a staging instruction");
 };
-using RingG = RingGeom<VG_RING_RT, VG_RING_RT == 64 ? kSU : 192, VG_RING_RT == 64 ? kSE : 1024,
-                       VG_RING_RT == 64 ? 2 : 3>;
+using RingG = RingGeom<VG_RING_RT, VG_RING_RT == 64 ? kSU : VG_RING_RT == 48 ? 240 : 192,
+                       VG_RING_RT == 32 ? 1024 : kSE, VG_RING_RT == 32 ? 3 : 2>;
 
 struct RingSlot {
   float4* rows;   // [SU][16]
@@ -472,7 +475,8 @@ __device__ __forceinline__ RingSlot ring_slot(char* base, int s) {
 
 // wait until *flag >= target (LDS counter, workgroup scope); false on expiry
 #ifndef VG_RING_PROF
-#define VG_RING_PROF 0  // 1: per-wave wait / busy clocks into g_ring_prof (tools/ring_probe.py; A/B builds only)
+#define VG_RING_PROF 0  // per-wave clocks into g_ring_prof (tools/ring_probe.py; A/B builds only): 1 waits,
+                        // softmax, gather; 2 consumer waits by slice, loader FREE -> loaded clocks and items
 #endif
 #if VG_RING_PROF
 __device__ unsigned long long g_ring_prof[2048 * 16 * 4];
@@ -567,18 +571,36 @@ struct RingIdx {
   float ad;
 };
 
+// A tile's head (distinct-source count, edge range, the lane's row_ptr and
+// a_dst entries): loaded one tile before its body, whose addresses need it.
+struct RingHead {
+  int U, e0, e1, rp;  // e1 - e0 is formed in the body: no use of a load result here
+  float ad;
+};
+
 template <class G>
-__device__ __forceinline__ void ring_load_idx(RingIdx<G>& x, int t, int N, int wave, int lane,
-                                              const int32_t* __restrict__ row_ptr, const float* __restrict__ a_dst,
-                                              const int32_t* __restrict__ ucount, const int32_t* __restrict__ usrc,
-                                              const uint16_t* __restrict__ lidx) {
+__device__ __forceinline__ void ring_load_head(RingHead& x, int t, int N, int wave, int lane,
+                                               const int32_t* __restrict__ row_ptr, const float* __restrict__ a_dst,
+                                               const int32_t* __restrict__ ucount) {
   const int lt = wave * 64 + lane;
   const int r0 = t * G::RT;
   x.U = ucount[t];
   x.e0 = row_ptr[r0];
-  x.ne = row_ptr[min(r0 + G::RT, N)] - x.e0;
+  x.e1 = row_ptr[min(r0 + G::RT, N)];
   x.rp = row_ptr[min(r0 + min(lt, G::RT), N)];
   x.ad = a_dst[min(r0 + min(lt, G::RT - 1), N - 1)];
+}
+
+// the body: the edges' LDS slots, the a_src rows, this wave's DMA source rows
+template <class G>
+__device__ __forceinline__ void ring_load_body(RingIdx<G>& x, const RingHead& hd, int t, int wave, int lane,
+                                               const int32_t* __restrict__ usrc, const uint16_t* __restrict__ lidx) {
+  const int lt = wave * 64 + lane;
+  x.U = hd.U;
+  x.e0 = hd.e0;
+  x.ne = hd.e1 - hd.e0;
+  x.rp = hd.rp;
+  x.ad = hd.ad;
   if (x.U > 0) {
     const int32_t* us = usrc + (size_t)t * G::SU;
 #pragma unroll
@@ -655,34 +677,40 @@ __global__ void __launch_bounds__(kRNT) k_gat_fwd_ring(
 
   if (wave < kRLW) {  // ------------------------------------------------ loaders
     const int lt = wave * 64 + lane;  // 0 .. 255
+    // Index loads run two stages ahead of the DMA and are issued before the
+    // FREE wait: the head of tile j + 2 and the body of tile j + 1 during the
+    // last slice of tile j, tile j's a_src rows before its first slice.  No
+    // load of an item depends on another load of the same item, so a refill
+    // after FREE is one round trip (the DMA) -- with the head and body loaded
+    // in one step, the body's addresses waited for the head and for the DMA
+    // issued before it (hipcc waits vmcnt(0) at the first use of a plain
+    // load's result while an LDS-DMA is outstanding).
     RingIdx<G> cur, nxt;
-    ring_load_idx<G>(cur, tb + wslot, N, wave, lane, row_ptr, a_dst, ucount, usrc, lidx);
+    RingHead hn;
+    {
+      RingHead h0;
+      ring_load_head<G>(h0, tb + wslot, N, wave, lane, row_ptr, a_dst, ucount);
+      ring_load_body<G>(cur, h0, tb + wslot, wave, lane, usrc, lidx);
+      if (my_tiles > 1) ring_load_head<G>(hn, tb + wslot + per, N, wave, lane, row_ptr, a_dst, ucount);
+    }
+    float av[G::AsQ];
     for (int k = 0; k < items; ++k) {
       const int s = k % G::NS, gen = k / G::NS, sl = k % slices;
       const int j = k / slices;
       const int t = tb + wslot + j * per;
-      if (k >= G::NS) VG_RING_WAIT(&cnt[G::NS + s], G::Groups * gen, 1);
-      RingSlot R = ring_slot<G>(base, s);
-      // this slice's rows by LDS-DMA (and, on the tile's first slice, its a_src rows)
-      float av[G::AsQ];
-      if (cur.U > 0) {
-        if (sl == 0)
-#pragma unroll
-          for (int q = 0; q < G::AsQ; ++q) av[q] = a_src[cur.ua[q]];
-        const int ni = (cur.U + 3) / 4;
-#pragma unroll
-        for (int q = 0; q < G::RowI; ++q) {
-          const int i = wave + q * kRLW;
-          if (i < ni) {
-            const float* src = h + (size_t)cur.sr[q] * C + sl * 64 + (lane & 15) * 4;
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
-                                             (__attribute__((address_space(3))) void*)(R.rows + 4 * i * 16), 16, 0, 0);
-          }
-        }
-      }
-      // the next tile's indices in flight behind them (its first slice's item)
       const bool pre = sl == slices - 1 && j + 1 < my_tiles;
-      if (pre) ring_load_idx<G>(nxt, t + per, N, wave, lane, row_ptr, a_dst, ucount, usrc, lidx);
+      if (pre) {
+        ring_load_body<G>(nxt, hn, t + per, wave, lane, usrc, lidx);
+        if (j + 2 < my_tiles) ring_load_head<G>(hn, t + 2 * per, N, wave, lane, row_ptr, a_dst, ucount);
+      }
+      if (sl == 0 && cur.U > 0)
+#pragma unroll
+        for (int q = 0; q < G::AsQ; ++q) av[q] = a_src[cur.ua[q]];
+      if (k >= G::NS) VG_RING_WAIT(&cnt[G::NS + s], G::Groups * gen, 1);
+#if VG_RING_PROF == 2
+      const unsigned long long f0_ = __builtin_readcyclecounter();
+#endif
+      RingSlot R = ring_slot<G>(base, s);
       if (sl == 0) {  // the tile's metadata: row_ptr, a_dst, edge slots, a_src (consumers keep them per tile)
         if (lt <= G::RT) R.rp[lt] = cur.rp;
         if (lt < G::RT) R.ad[lt] = cur.ad;
@@ -699,7 +727,24 @@ __global__ void __launch_bounds__(kRNT) k_gat_fwd_ring(
           }
         }
       }
+      // this slice's rows by LDS-DMA
+      if (cur.U > 0) {
+        const int ni = (cur.U + 3) / 4;
+#pragma unroll
+        for (int q = 0; q < G::RowI; ++q) {
+          const int i = wave + q * kRLW;
+          if (i < ni) {
+            const float* src = h + (size_t)cur.sr[q] * C + sl * 64 + (lane & 15) * 4;
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
+                                             (__attribute__((address_space(3))) void*)(R.rows + 4 * i * 16), 16, 0, 0);
+          }
+        }
+      }
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#if VG_RING_PROF == 2
+      t_soft += __builtin_readcyclecounter() - f0_;  // FREE -> loaded
+      t_gath += 1;
+#endif
       if (lane == 0) __hip_atomic_fetch_add(&cnt[s], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (pre) cur = nxt;
     }
@@ -727,15 +772,22 @@ __global__ void __launch_bounds__(kRNT) k_gat_fwd_ring(
     const int k = j * slices + sl;
     const int s = k % G::NS, gen = k / G::NS;
     const int t = tb + wslot + j * per;
+    // the tile's plan entry and the slice's bias in flight under the FULL wait
+    const int U = ucount[t];
+    const float4 bv = *reinterpret_cast<const float4*>(bias + sl * 64 + l16 * 4);
+#if VG_RING_PROF == 2
+    const unsigned long long wb_ = waited;
+#endif
     VG_RING_WAIT(&cnt[s], kRLW * (gen + 1), 2);
+#if VG_RING_PROF == 2
+    (sl == 0 ? t_soft : t_gath) += waited - wb_;  // waits by slice (probe builds)
+#endif
     RingSlot R = ring_slot<G>(base, s);
     const int r0 = t * G::RT;
-    const int U = ucount[t];
     const bool staged = U >= 0;
     const float* hs = h + sl * 64;
-    const float4 bv = *reinterpret_cast<const float4*>(bias + sl * 64 + l16 * 4);
     {
-#if VG_RING_PROF
+#if VG_RING_PROF == 1
       const unsigned long long p0 = __builtin_readcyclecounter();
 #endif
       if (sl == 0) {  // the row's softmax, once per tile (its slices reuse it)
@@ -787,7 +839,7 @@ __global__ void __launch_bounds__(kRNT) k_gat_fwd_ring(
         w.denom = denom;
         w.dreg = w.deg < T * L ? w.deg : T * L;
       }
-#if VG_RING_PROF
+#if VG_RING_PROF == 1
       const unsigned long long p1 = __builtin_readcyclecounter();
       t_soft += p1 - p0;
 #endif
@@ -842,7 +894,7 @@ __global__ void __launch_bounds__(kRNT) k_gat_fwd_ring(
       if (w.r < N)
         *reinterpret_cast<float4*>(out + (size_t)w.r * C + sl * 64 + l16 * 4) =
             make_float4(acc[0] + bv.x, acc[1] + bv.y, acc[2] + bv.z, acc[3] + bv.w);
-#if VG_RING_PROF
+#if VG_RING_PROF == 1
       t_gath += __builtin_readcyclecounter() - p1;
 #endif
     }

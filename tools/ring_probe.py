@@ -6,6 +6,11 @@ the clocks it spent in hand-over waits and its lifetime; printed per role
 configs[3] stress graph in lattice-block order, C = 128 and 64.
 
     VGAN_LIB=.../libvgan_hip_ringprof.so python tools/ring_probe.py
+
+A VG_RING_PROF=2 build fills the same four counters with: consumers' waits
+on the first slice ("softmax_frac") and on later slices ("gather_frac");
+loaders' FREE -> loaded clocks ("softmax_frac") and item count ("gather_frac"
+x life).
 """
 from __future__ import annotations
 
