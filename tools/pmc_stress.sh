@@ -4,7 +4,8 @@
 # blocked numbering, C = 128): HBM-side bytes (FETCH_SIZE, WRITE_SIZE), the
 # L1 -> L2 read requests (the gather), and the SQ wait / LDS profile of the
 # register gather (k_gat_fwd_cp / _ep) and the staged kernel
-# (k_gat_fwd_staged).  One rocprofv3 run per pass (tools/pmc_kernel.sh).
+# (k_gat_fwd_staged) and the ring kernel (k_gat_fwd_ring).  One rocprofv3 run
+# per pass (tools/pmc_kernel.sh).
 set -o pipefail
 TAG=$1
 R=${GRAFT_REPO_ROOT:-$(pwd)}

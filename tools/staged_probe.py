@@ -1,6 +1,7 @@
-"""configs[3] stress graph: the register gather, the 16-row LDS kernel and the
-persistent staged kernel (vg_gat_aggregate_fwd_staged) in three voxel
-numberings, cold MALL, HIP events.  One JSON line per (order, kernel, C).
+"""configs[3] stress graph: the register gather, the persistent staged kernel
+(vg_gat_aggregate_fwd_staged) and the wave-specialised ring kernel
+(vg_gat_aggregate_fwd_ring) in three voxel numberings, cold MALL, HIP events.
+One JSON line per (order, kernel, C).
 
     python tools/staged_probe.py [--reps 20] [--orders rowmajor,tiled,blocked]
 """
@@ -43,6 +44,7 @@ def main():
         csr = ops.CSR(vox.edge_index, vox.num_nodes)
         n, e = csr.num_nodes, csr.num_edges
         plan = csr.stage_plan()
+        rplan = csr.ring_plan()
         tiles = csr.stage_tiles()
         uc = plan[:tiles]
         info = {"order": order, "nodes": n, "edges": e, "staged_tiles": int((uc > 0).sum()),
@@ -56,6 +58,8 @@ def main():
             bias = torch.randn(c, device=dev)
             out, alpha = torch.empty(n, c, device=dev), torch.empty(e, device=dev)
             out2, alpha2 = torch.empty(n, c, device=dev), torch.empty(e, device=dev)
+            out3, alpha3 = torch.empty(n, c, device=dev), torch.empty(e, device=dev)
+            err = torch.zeros(1, dtype=torch.int32, device=dev)
 
             def reg():
                 ops.aggregate_fwd_raw(csr, c, ptr(h), ptr(a_s), ptr(a_d), ptr(bias), 0.2, ptr(out), ptr(alpha), st)
@@ -64,6 +68,11 @@ def main():
                 check(LIB.vg_gat_aggregate_fwd_staged(ptr(csr.row_ptr), ptr(csr.col), n, c, ptr(h), ptr(a_s),
                                                       ptr(a_d), ptr(bias), 0.2, ptr(out2), ptr(alpha2), ptr(plan), st),
                       "staged")
+
+            def ring():
+                check(LIB.vg_gat_aggregate_fwd_ring(ptr(csr.row_ptr), ptr(csr.col), n, c, ptr(h), ptr(a_s), ptr(a_d),
+                                                    ptr(bias), 0.2, ptr(out3), ptr(alpha3), ptr(rplan), ptr(err), st),
+                      "ring")
 
             def timed(fn, cold=True):
                 for _ in range(3):
@@ -82,14 +91,16 @@ def main():
                 return sum(ts) / len(ts), ts[len(ts) // 2]
 
             by = agg_bytes(n, e, c)
-            for name, fn in (("register", reg), ("staged", staged)):
+            for name, fn in (("register", reg), ("staged", staged), ("ring", ring)):
                 avg, med = timed(fn)
                 warm, _ = timed(fn, cold=False)
                 print(json.dumps({"order": order, "kernel": name, "C": c, "avg_us": round(avg, 2),
                                   "median_us": round(med, 2), "warm_us": round(warm, 2),
                                   "frac": round(by / (avg * 1e-6) / 8e12, 4)}), flush=True)
             torch.cuda.synchronize()
-            same = torch.equal(out, out2) and torch.equal(alpha, alpha2)
+            if int(err.item()) != 0:
+                raise RuntimeError("ring: a hand-over wait expired")
+            same = all(torch.equal(out, o) and torch.equal(alpha, a) for o, a in ((out2, alpha2), (out3, alpha3)))
             print(json.dumps({"order": order, "C": c, "bit_identical": same}), flush=True)
 
 
