@@ -1044,7 +1044,8 @@ def main():
                                             "previous tile is aggregated)",
                      "per_channels_ring": "vg_gat_aggregate_fwd_ring (wave-specialised workgroup per CU: 4 loader "
                                           "waves fill a two-slot LDS ring with each 64-row tile's distinct source "
-                                          "rows by LDS-DMA, 8 consumer waves aggregate the other slot; LDS-counter "
+                                          "rows by LDS-DMA, index loads two stages ahead; 12 consumer waves claim "
+                                          "(tile, 4-row group) units and aggregate out of LDS; LDS-counter "
                                           "hand-over, no barrier)"}
             cands = [(r[key][128]["avg_us"], o, key) for o, r in stress_orders.items() for key in kinds
                      if 128 in r.get(key, {})]
