@@ -532,10 +532,10 @@ def sweep_leg(device, store_job, batch: int = 32, n_taus: int = 10):
     schedule 1.0 -> 0.1, f16 (and f32) eval forward, one stacked forward per
     batch over the ``n_taus`` temperature copies.  Each batch comes through
     the native loader (host collate + host-built per-batch structures + one
-    upload, prefetched on SWEEP_WORKERS threads); its forward is enqueued
-    eagerly (InferenceSweep.run_stream; recording it per batch measured
-    slower): f16 as one native call per batch (vg_hgen_sweep), f32 from
-    Python.  The timed region is the whole pass: collate, upload, forward.
+    upload, prefetched on SWEEP_WORKERS threads); f16: the batch's forward
+    captured from the native engine into a hipGraph and launched as one
+    (vg_hgen_sweep_graphed, one of two executable graphs updated in place),
+    f32: launched from Python (InferenceSweep.run_stream).  The timed region is the whole pass: collate, upload, forward.
     Also the f16 scatter kernel (vg_hgat_fwd) over the sweep's own stacked
     graph and channel schedule, graph-replayed between HIP events."""
     from vgan import data as vdata
@@ -569,7 +569,7 @@ def sweep_leg(device, store_job, batch: int = 32, n_taus: int = 10):
     out = {"workload": f"configs[4]: {len(store)} distinct synthetic buildings ({n_batches} batches of {batch}) "
                        f"streamed through the native loader, {n_taus} Gumbel temperatures 1.0->0.1 geometric, eval G "
                        f"forward stacked over the temperatures (InferenceSweep.run_stream; f16: the whole batch -- z and noise "
-                       f"draws, forward, Gumbel head, argmax -- one native call, vg_hgen_sweep; f32: launched from "
+                       f"draws, forward, Gumbel head, argmax -- captured from the native engine into a hipGraph, one graph launch per batch, vg_hgen_sweep_graphed; f32: launched from "
                        f"Python), {SWEEP_WORKERS} collating loader threads; collate, upload, per-batch structures and "
                        f"forward timed",
            "unit": "samples/s (buildings x temperatures)", "distinct_batches": n_batches,

@@ -17,6 +17,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <new>
 
 #include "../../include/vgan.h"
 #include "common.h"
@@ -286,3 +287,117 @@ extern "C" int vg_hgen_sweep(const vg_hgen_model* model, const vg_hgen_batch* ba
   Arena ar{false, static_cast<char*>(arena)};
   return run(ar, model, batch, labels, logits, static_cast<hipStream_t>(stream));
 }
+
+// ---------------------------------------------------------------- graphed
+// The same batch forward CAPTURED into a hipGraph (stream capture of run()
+// on a private stream -- capturing records, it runs nothing, and the caller's
+// stream may be the legacy one, which cannot capture; thread-local mode:
+// other host threads' uploads are unaffected) and launched on the caller's
+// stream as one graph.  Two executable graphs alternate; each is updated in place
+// from the new capture (hipGraphExecUpdate: same launch sequence, new
+// pointers and grid sizes) and re-instantiated only when the update is
+// refused, and only after the event behind its previous launch -- two
+// batches back -- has completed.
+#define VG_HIP_RET(expr)                                    \
+  do {                                                      \
+    const hipError_t _e = (expr);                           \
+    if (_e != hipSuccess) return static_cast<int>(_e);      \
+  } while (0)
+
+namespace {
+struct HgenGraph {
+  hipGraphExec_t exec[2] = {nullptr, nullptr};
+  hipEvent_t done[2] = {nullptr, nullptr};
+  hipStream_t cap = nullptr;
+  bool used[2] = {false, false};
+  int next = 0;
+  int32_t instantiations = 0, updates = 0;
+};
+}  // namespace
+
+extern "C" void vg_hgen_graph_destroy(void* handle);
+
+extern "C" void* vg_hgen_graph_create(void) {
+  HgenGraph* g = new (std::nothrow) HgenGraph();
+  if (!g) return nullptr;
+  bool ok = hipStreamCreateWithFlags(&g->cap, hipStreamNonBlocking) == hipSuccess;
+  for (int i = 0; ok && i < 2; ++i) ok = hipEventCreateWithFlags(&g->done[i], hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    vg_hgen_graph_destroy(g);
+    return nullptr;
+  }
+  return g;
+}
+
+extern "C" void vg_hgen_graph_destroy(void* handle) {
+  HgenGraph* g = static_cast<HgenGraph*>(handle);
+  if (!g) return;
+  for (int i = 0; i < 2; ++i) {
+    if (g->used[i]) (void)hipEventSynchronize(g->done[i]);
+    if (g->exec[i]) (void)hipGraphExecDestroy(g->exec[i]);
+    if (g->done[i]) (void)hipEventDestroy(g->done[i]);
+  }
+  if (g->cap) (void)hipStreamDestroy(g->cap);
+  delete g;
+}
+
+extern "C" int vg_hgen_graph_stats(const void* handle, int32_t* instantiations, int32_t* updates) {
+  const HgenGraph* g = static_cast<const HgenGraph*>(handle);
+  if (!g || !instantiations || !updates) return VG_EINVAL;
+  *instantiations = g->instantiations;
+  *updates = g->updates;
+  return 0;
+}
+
+extern "C" int vg_hgen_sweep_graphed(void* handle, const vg_hgen_model* model, const vg_hgen_batch* batch,
+                                     void* arena, int64_t arena_bytes, int8_t* labels, float* logits,
+                                     void* stream) {
+  HgenGraph* G = static_cast<HgenGraph*>(handle);
+  if (!G || !model || !batch || !arena) return VG_EINVAL;
+  const int64_t need = vg_hgen_arena_bytes(model, batch);
+  if (need < 0) return static_cast<int>(need);
+  if (arena_bytes < need || (reinterpret_cast<uintptr_t>(arena) & 255)) return VG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int slot = G->next;
+  if (G->used[slot]) VG_HIP_RET(hipEventSynchronize(G->done[slot]));
+  VG_HIP_RET(hipStreamBeginCapture(G->cap, hipStreamCaptureModeThreadLocal));
+  Arena ar{false, static_cast<char*>(arena)};
+  const int rc = run(ar, model, batch, labels, logits, G->cap);
+  hipGraph_t graph = nullptr;
+  const hipError_t ec = hipStreamEndCapture(G->cap, &graph);
+  if (rc || ec != hipSuccess || !graph) {
+    if (graph) (void)hipGraphDestroy(graph);
+    (void)hipGetLastError();
+    return rc ? rc : static_cast<int>(ec != hipSuccess ? ec : hipErrorStreamCaptureInvalidated);
+  }
+  bool updated = false;
+  if (G->exec[slot]) {
+    hipGraphNode_t err_node = nullptr;
+    hipGraphExecUpdateResult res = hipGraphExecUpdateError;
+    if (hipGraphExecUpdate(G->exec[slot], graph, &err_node, &res) == hipSuccess && res == hipGraphExecUpdateSuccess) {
+      updated = true;
+      ++G->updates;
+    } else {
+      (void)hipGetLastError();
+      (void)hipGraphExecDestroy(G->exec[slot]);
+      G->exec[slot] = nullptr;
+    }
+  }
+  if (!updated) {
+    const hipError_t ei = hipGraphInstantiate(&G->exec[slot], graph, nullptr, nullptr, 0);
+    if (ei != hipSuccess) {
+      G->exec[slot] = nullptr;
+      (void)hipGraphDestroy(graph);
+      return static_cast<int>(ei);
+    }
+    ++G->instantiations;
+  }
+  (void)hipGraphDestroy(graph);
+  VG_HIP_RET(hipGraphLaunch(G->exec[slot], s));
+  VG_HIP_RET(hipEventRecord(G->done[slot], s));
+  G->used[slot] = true;
+  G->next ^= 1;
+  return 0;
+}
+
+#undef VG_HIP_RET

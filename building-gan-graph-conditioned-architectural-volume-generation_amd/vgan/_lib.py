@@ -290,6 +290,11 @@ SIGNATURES = {
     "vg_hgen_arena_bytes": (ctypes.c_int64, [ctypes.POINTER(VgHgenModel), ctypes.POINTER(VgHgenBatch)]),
     "vg_hgen_sweep": (ctypes.c_int, [ctypes.POINTER(VgHgenModel), ctypes.POINTER(VgHgenBatch), _c_p, ctypes.c_int64,
                                      _c_p, _c_p, _c_p]),
+    "vg_hgen_graph_create": (_c_p, []),
+    "vg_hgen_graph_destroy": (None, [_c_p]),
+    "vg_hgen_graph_stats": (ctypes.c_int, [_c_p, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i32)]),
+    "vg_hgen_sweep_graphed": (ctypes.c_int, [_c_p, ctypes.POINTER(VgHgenModel), ctypes.POINTER(VgHgenBatch), _c_p,
+                                             ctypes.c_int64, _c_p, _c_p, _c_p]),
     "vg_critic_arena_floats": (ctypes.c_int64, [ctypes.POINTER(VgCriticModel), ctypes.POINTER(VgCriticBatch)]),
     "vg_critic_loss_and_grad": (ctypes.c_int, [ctypes.POINTER(VgCriticModel), ctypes.POINTER(VgCriticBatch), _c_p,
                                                _c_i64, _c_p, _c_p]),

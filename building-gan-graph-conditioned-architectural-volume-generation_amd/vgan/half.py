@@ -24,6 +24,8 @@ Call ``refresh()`` after the generator's weights change.
 """
 from __future__ import annotations
 
+import os
+import weakref
 from typing import List, Optional, Tuple
 
 import torch
@@ -32,6 +34,11 @@ import torch.nn as nn
 from . import data as vdata
 from . import ops
 from ._lib import LIB, check, ptr, stream_handle
+
+# sweep_labels as ONE hipGraph launch per batch (vg_hgen_sweep_graphed: the
+# native call captured, an executable graph updated in place); 0: the native
+# call launches its kernels directly (vg_hgen_sweep)
+_GRAPH = os.environ.get("VGAN_HGEN_GRAPH", "1") == "1"
 
 
 def _r8(c: int) -> int:
@@ -222,14 +229,16 @@ class HalfGenerator:
 
     @torch.no_grad()
     def sweep_labels(self, local_graph, voxel_graph, copies: int, taus: torch.Tensor,
-                     logits: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     logits: Optional[torch.Tensor] = None, graph: Optional[bool] = None) -> torch.Tensor:
         """InferenceSweep._forward on this f16 generator as ONE native call
         (vg_hgen_sweep): RNG.reset(), z for ``copies`` stacked copies, the
         forward, Exp(1) noise, the Gumbel head at ``taus`` [copies] and the
         argmax -- the same kernels in the same order as ``__call__`` preceded
         by the reset and z draw, so the [copies, N] int8 labels are
         bit-identical to that path's.  ``logits`` [copies * N, classes] f32
-        receives the logits when given."""
+        receives the logits when given.  ``graph`` (default VGAN_HGEN_GRAPH):
+        the call captured into a hipGraph and launched as one
+        (vg_hgen_sweep_graphed), unless the stream is already capturing."""
         import ctypes
 
         from ._lib import LIB, VgHgenBatch
@@ -276,10 +285,38 @@ class HalfGenerator:
         if logits is not None and (logits.dtype != torch.float32 or not logits.is_contiguous() or
                                    logits.numel() != copies * n * self.head[2]):
             raise ValueError("logits must be a contiguous f32 [copies * N, classes] tensor")
-        check(LIB.vg_hgen_sweep(ctypes.byref(md), ctypes.byref(bt), arena.data_ptr(), arena.numel(),
-                                labels.data_ptr(), None if logits is None else logits.data_ptr(), stream_handle(dev)),
-              "vg_hgen_sweep")
+        lg = None if logits is None else logits.data_ptr()
+        if (_GRAPH if graph is None else graph) and not torch.cuda.is_current_stream_capturing():
+            check(LIB.vg_hgen_sweep_graphed(self._graph_handle(), ctypes.byref(md), ctypes.byref(bt),
+                                            arena.data_ptr(), arena.numel(), labels.data_ptr(), lg,
+                                            stream_handle(dev)), "vg_hgen_sweep_graphed")
+        else:
+            check(LIB.vg_hgen_sweep(ctypes.byref(md), ctypes.byref(bt), arena.data_ptr(), arena.numel(),
+                                    labels.data_ptr(), lg, stream_handle(dev)), "vg_hgen_sweep")
         return labels
+
+    def _graph_handle(self) -> int:
+        """The two executable graphs of vg_hgen_sweep_graphed, destroyed with
+        this object (after their last launches complete)."""
+        h = self.__dict__.get("_hgraph")
+        if h is None:
+            h = LIB.vg_hgen_graph_create()
+            if not h:
+                raise RuntimeError("vg_hgen_graph_create failed")
+            self._hgraph = h
+            weakref.finalize(self, LIB.vg_hgen_graph_destroy, h)
+        return h
+
+    def graph_stats(self) -> Tuple[int, int]:
+        """(instantiations, in-place updates) of the graphed sweep so far."""
+        import ctypes
+
+        h = self.__dict__.get("_hgraph")
+        if h is None:
+            return 0, 0
+        a, b = ctypes.c_int32(0), ctypes.c_int32(0)
+        check(LIB.vg_hgen_graph_stats(h, ctypes.byref(a), ctypes.byref(b)), "vg_hgen_graph_stats")
+        return a.value, b.value
 
     @torch.no_grad()
     def __call__(self, local_graph, voxel_graph, z: torch.Tensor, noise: Optional[torch.Tensor] = None,

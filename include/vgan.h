@@ -1137,6 +1137,19 @@ int64_t vg_hgen_arena_bytes(const vg_hgen_model* model, const vg_hgen_batch* bat
 int vg_hgen_sweep(const vg_hgen_model* model, const vg_hgen_batch* batch, void* arena, int64_t arena_bytes,
                   int8_t* labels, float* logits, void* stream);
 
+/* The same forward as ONE hipGraph launch: vg_hgen_sweep's launches captured
+ * (thread-local stream capture) into a graph that updates one of two
+ * alternating executable graphs in place (re-instantiated only when the
+ * update is refused), after the event behind that executable graph's
+ * previous launch has completed.  Same results bit for bit.  A handle holds
+ * the two executable graphs; vg_hgen_graph_stats reports how many were
+ * instantiated and how many updated in place. */
+void* vg_hgen_graph_create(void);
+void vg_hgen_graph_destroy(void* handle);
+int vg_hgen_graph_stats(const void* handle, int32_t* instantiations, int32_t* updates);
+int vg_hgen_sweep_graphed(void* handle, const vg_hgen_model* model, const vg_hgen_batch* batch, void* arena,
+                          int64_t arena_bytes, int8_t* labels, float* logits, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

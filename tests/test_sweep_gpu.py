@@ -105,3 +105,46 @@ def test_native_f16_sweep_equals_python_path(cuda, tmp_path, monkeypatch, copies
     ref = hg.logits(loc, vox, z)
     torch.cuda.synchronize()
     assert torch.equal(lg, ref)
+
+
+@pytest.mark.gpu
+def test_graphed_native_sweep_equals_direct(cuda, tmp_path):
+    """vg_hgen_sweep_graphed (the native call captured into a hipGraph, one of
+    two executable graphs updated in place per batch) against vg_hgen_sweep
+    launching the same kernels: labels and logits bit for bit over batches of
+    varying size from one device-RNG stream, the RNG state after equal; the
+    executable graphs are mostly updated in place (a batch whose shape picks
+    another kernel variant re-instantiates its slot)."""
+    from vgan import data as vdata
+    from vgan.half import HalfGenerator
+
+    st = write_store(str(tmp_path / "s"), SyntheticDataset(23, seed=31))
+    cfg = Configuration()
+    cfg.DEVICE = str(cuda)
+    torch.manual_seed(9)
+    G = VoxelGNNGenerator(cfg, 17, 12).to(cuda)
+    G.eval()
+    taus = torch.tensor(geometric_taus(1.0, 0.1, 4), device=cuda)
+    plan = [[0, 1, 2], [3, 4, 5, 6, 7], [8], [9, 10, 11, 12], [13, 14], [15, 16, 17, 18, 19, 20], [21, 22]]
+
+    def run(graph):
+        G.rng = RNG("device", seed=77)
+        hg = HalfGenerator(G)
+        outs = []
+        for idx in plan:
+            loc, vox = next(iter(GraphLoader(st, idx, batch_size=len(idx), shuffle=False, device=cuda, prefetch=1,
+                                             prepare=(7, ()))))
+            n = vdata.prepared(loc, vox, 7).voxel_x.shape[0]
+            lg = torch.empty(4 * n, 7, device=cuda)
+            lab = hg.sweep_labels(loc, vox, 4, taus, logits=lg, graph=graph)
+            outs.append((lab, lg))
+        torch.cuda.synchronize()
+        return outs, G.rng.state_dict(), hg.graph_stats()
+
+    got, st_g, (inst, upd) = run(True)
+    want, st_d, (inst_d, upd_d) = run(False)
+    assert (inst_d, upd_d) == (0, 0)
+    for (la, ga), (lb, gb) in zip(got, want):
+        assert torch.equal(la, lb) and torch.equal(ga, gb)
+    assert st_g == st_d
+    assert inst + upd == len(plan) and upd >= len(plan) // 2, (inst, upd)
