@@ -121,3 +121,21 @@ def test_build_stamp_matches_tree_and_stale_library_is_refused():
 
     with pytest.raises(ImportError, match="other sources"):
         L._check_stamp(Stale())
+
+
+def test_graphed_sweep_refuses_bad_arguments_host_only():
+    """vg_hgen_sweep_graphed / vg_hgen_graph_stats check their arguments on
+    the host before any runtime call: a NULL handle, model or arena is
+    VG_EINVAL (no capture started, no device touched)."""
+    import ctypes as ct
+
+    from vgan._lib import LIB as lib, VgHgenBatch, VgHgenModel
+
+    VG_EINVAL = -1
+    md, bt = VgHgenModel(), VgHgenBatch()
+    assert lib.vg_hgen_sweep_graphed(None, ct.byref(md), ct.byref(bt), None, 0, None, None, None) == VG_EINVAL
+    assert lib.vg_hgen_sweep_graphed(1, None, ct.byref(bt), 256, 0, None, None, None) == VG_EINVAL
+    assert lib.vg_hgen_sweep_graphed(1, ct.byref(md), ct.byref(bt), None, 0, None, None, None) == VG_EINVAL
+    a, b = ct.c_int32(7), ct.c_int32(7)
+    assert lib.vg_hgen_graph_stats(None, ct.byref(a), ct.byref(b)) == VG_EINVAL
+    lib.vg_hgen_graph_destroy(None)  # a NULL handle is a no-op
