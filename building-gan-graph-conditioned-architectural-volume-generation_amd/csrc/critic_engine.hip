@@ -59,9 +59,15 @@ struct Ctx {
 // grouped launches and their folds (and the GAT / GraphNorm parameter folds)
 // in vg_fold_batch launches at the end, merged exactly as the Python
 // collector merges them.
+#ifndef VG_CRITIC_FOLD_SPLIT
+#define VG_CRITIC_FOLD_SPLIT 1  // long folds in two levels (vg_fold_batch_split); 0: vg_fold_batch (A/B)
+#endif
+constexpr int64_t kFoldWsFloats = 1 << 17;  // the split folds' chunk sums
+
 struct Folds {
   std::vector<vg_fold> folds;
   std::vector<vg_tn> prods;  // planned, not yet launched
+  float* ws = nullptr;       // kFoldWsFloats of the arena
 
   void add(const vg_fold* f, int n) { folds.insert(folds.end(), f, f + n); }
 
@@ -131,7 +137,8 @@ struct Folds {
     }
     if (!cur.empty()) batches.push_back(cur);
     for (auto& b : batches) {
-      const int rc = vg_fold_batch(b.data(), (int32_t)b.size(), cx.stream);
+      const int rc = VG_CRITIC_FOLD_SPLIT ? vg_fold_batch_split(b.data(), (int32_t)b.size(), ws, kFoldWsFloats, cx.stream)
+                                          : vg_fold_batch(b.data(), (int32_t)b.size(), cx.stream);
       if (rc) return rc;
     }
     folds.clear();
@@ -168,6 +175,7 @@ int run(Ctx& cx, const vg_critic_model* md, const vg_critic_batch* bt, float* ou
   const vg_csr_ref& g3 = bt->g3;
   auto rows = [](float* t, int r0, int width) { return t ? t + (int64_t)r0 * width : nullptr; };
   Folds folds;
+  folds.ws = cx.take(kFoldWsFloats);
 
   // ------------------------------------------------------------ pass A
   float* X0 = cx.take((int64_t)X4 * W0);

@@ -31,8 +31,17 @@ struct FoldBatch {
   int32_t block0[VG_FOLD_MAX + 1];  // first workgroup of fold i; block0[n] = grid size
   int32_t waves[VG_FOLD_MAX];       // waves per 64-column group: 16, or 4 for short folds
   int32_t cw[VG_FOLD_MAX];          // narrow long folds: lanes per partial row (pow2 >= width, <= 32); else 0
+  // split folds (vg_fold_batch_split, first level): chunks of kChunkRows
+  // partial rows of src 0 (then src 1), chunk c's column sums into
+  // ws[ws_off[i] + c * width ...]; 0 chunks: an ordinary fold
+  int32_t chunks0[VG_FOLD_MAX], chunks[VG_FOLD_MAX], ws_off[VG_FOLD_MAX];
+  float* ws;
   vg_fold f[VG_FOLD_MAX];
 };
+#ifndef VG_FOLD_SPLIT_ROWS
+#define VG_FOLD_SPLIT_ROWS 768  // vg_fold_batch_split: folds with more partial rows go two-level
+#endif
+constexpr int kChunkRows = 128;
 
 // Sixteen rows in flight per wave and iteration (the GAT / LayerNorm partial
 // sets have up to a few thousand rows: a short dependent loop, not one round
@@ -97,6 +106,26 @@ __global__ void __launch_bounds__(1024) k_fold_batch(const FoldBatch b) {
   int d = 0;
   while (d + 1 < b.n && (int)blockIdx.x >= b.block0[d + 1]) ++d;
   const vg_fold& f = b.f[d];
+  if (b.chunks[d] > 0) {  // first level of a split fold: one chunk of one source, 64 columns
+    const int groups = (f.width + 63) / 64;
+    const int lb = blockIdx.x - b.block0[d];
+    const int chunk = lb / groups, grp = lb % groups;
+    const int si = chunk < b.chunks0[d] ? 0 : 1;
+    const int r0 = (si == 0 ? chunk : chunk - b.chunks0[d]) * kChunkRows;
+    const int rows = min(kChunkRows, f.src[si].rows - r0);
+    const long long w = (long long)grp * 64 + lane;
+    __shared__ float redc[16][64];
+    redc[wave][lane] = w < f.width && rows > 0
+                           ? fold_rows_sum(f.src[si].part + (size_t)r0 * f.src[si].ld, rows, f.src[si].ld, w, wave, 16)
+                           : 0.f;
+    __syncthreads();
+    if (wave == 0 && w < f.width) {
+      float v = 0.f;
+      for (int k = 0; k < 16; ++k) v += redc[k][lane];
+      b.ws[(size_t)b.ws_off[d] + (size_t)chunk * f.width + w] = v;
+    }
+    return;
+  }
   if (b.cw[d] > 0) {  // narrow long fold: one workgroup, packed lanes
     const int cw = b.cw[d], rpl = 64 / cw;
     const int col = lane & (cw - 1);
@@ -141,23 +170,41 @@ __global__ void __launch_bounds__(1024) k_fold_batch(const FoldBatch b) {
 
 }  // namespace
 
-extern "C" int vg_fold_batch(const vg_fold* folds, int32_t n, void* stream) {
-  if (n < 0 || n > VG_FOLD_MAX || (n > 0 && !folds)) return VG_EINVAL;
-  if (n == 0) return 0;
+// validate fold i; its partial rows (the longer source)
+static int fold_rows_of(const vg_fold& f) {
+  if (!f.out || f.width <= 0 || f.k <= 0 || f.ldo < f.k || f.nsrc < 1 || f.nsrc > 2) return -1;
+  int rows = 0;
+  for (int s = 0; s < f.nsrc; ++s) {
+    if (!f.src[s].part || f.src[s].rows < 0 || f.src[s].ld < f.width) return -1;
+    rows = f.src[s].rows > rows ? f.src[s].rows : rows;
+  }
+  return rows;
+}
+
+// one launch over folds[0, n); split[i] > 0: fold i's first level (chunk count)
+static int launch_batch(const vg_fold* folds, int32_t n, const int* split, const int* chunks0, const int* ws_off,
+                        float* ws, void* stream) {
   FoldBatch b;
   b.n = n;
+  b.ws = ws;
   int blocks = 0;
   for (int i = 0; i < n; ++i) {
     const vg_fold& f = folds[i];
-    if (!f.out || f.width <= 0 || f.k <= 0 || f.ldo < f.k || f.nsrc < 1 || f.nsrc > 2) return VG_EINVAL;
-    for (int s = 0; s < f.nsrc; ++s)
-      if (!f.src[s].part || f.src[s].rows < 0 || f.src[s].ld < f.width) return VG_EINVAL;
-    int rows = 0;
-    for (int s = 0; s < f.nsrc; ++s) rows = f.src[s].rows > rows ? f.src[s].rows : rows;
+    const int rows = fold_rows_of(f);
+    if (rows < 0) return VG_EINVAL;
     b.f[i] = f;
-    b.waves[i] = rows <= kShortRows ? 4 : 16;
     b.block0[i] = blocks;
+    b.chunks[i] = split ? split[i] : 0;
+    b.chunks0[i] = split ? chunks0[i] : 0;
+    b.ws_off[i] = split ? ws_off[i] : 0;
+    b.waves[i] = rows <= kShortRows ? 4 : 16;
     int cw = 0;
+    if (b.chunks[i] > 0) {
+      b.waves[i] = 16;
+      b.cw[i] = 0;
+      blocks += (f.width + 63) / 64 * b.chunks[i];
+      continue;
+    }
     if (VG_FOLD_PACK && rows > kShortRows && f.width <= 32) {
       cw = 1;
       while (cw < f.width) cw <<= 1;
@@ -169,4 +216,58 @@ extern "C" int vg_fold_batch(const vg_fold* folds, int32_t n, void* stream) {
   k_fold_batch<<<blocks, 1024, 0, static_cast<hipStream_t>(stream)>>>(b);
   VG_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int vg_fold_batch(const vg_fold* folds, int32_t n, void* stream) {
+  if (n < 0 || n > VG_FOLD_MAX || (n > 0 && !folds)) return VG_EINVAL;
+  if (n == 0) return 0;
+  return launch_batch(folds, n, nullptr, nullptr, nullptr, nullptr, stream);
+}
+
+extern "C" int64_t vg_fold_split_ws_floats(const vg_fold* folds, int32_t n) {
+  if (n < 0 || n > VG_FOLD_MAX || (n > 0 && !folds)) return VG_EINVAL;
+  int64_t need = 0;
+  for (int i = 0; i < n; ++i) {
+    const int rows = fold_rows_of(folds[i]);
+    if (rows < 0) return VG_EINVAL;
+    if (rows > VG_FOLD_SPLIT_ROWS)
+      for (int s = 0; s < folds[i].nsrc; ++s)
+        need += (int64_t)((folds[i].src[s].rows + kChunkRows - 1) / kChunkRows) * folds[i].width;
+  }
+  return need;
+}
+
+extern "C" int vg_fold_batch_split(const vg_fold* folds, int32_t n, float* ws, int64_t ws_floats, void* stream) {
+  if (n < 0 || n > VG_FOLD_MAX || (n > 0 && !folds) || ws_floats < 0 || ws_floats > (int64_t)1 << 31) return VG_EINVAL;
+  if (n == 0) return 0;
+  // folds with more than VG_FOLD_SPLIT_ROWS partial rows (while ws lasts) go
+  // two-level: their chunks' column sums in the same launch as the short
+  // folds, then one fold of those sums into the destination (src 0's chunks,
+  // then src 1's: the same (out + src 0) + src 1 order)
+  int split[VG_FOLD_MAX], c0[VG_FOLD_MAX], off[VG_FOLD_MAX];
+  vg_fold second[VG_FOLD_MAX];
+  int n2 = 0;
+  int64_t used = 0;
+  for (int i = 0; i < n; ++i) {
+    const vg_fold& f = folds[i];
+    const int rows = fold_rows_of(f);
+    if (rows < 0) return VG_EINVAL;
+    split[i] = c0[i] = off[i] = 0;
+    if (rows <= VG_FOLD_SPLIT_ROWS || !ws) continue;
+    const int k0 = (f.src[0].rows + kChunkRows - 1) / kChunkRows;
+    const int k1 = f.nsrc > 1 ? (f.src[1].rows + kChunkRows - 1) / kChunkRows : 0;
+    const int64_t need = (int64_t)(k0 + k1) * f.width;
+    if (used + need > ws_floats) continue;  // no room: an ordinary fold
+    split[i] = k0 + k1;
+    c0[i] = k0;
+    off[i] = static_cast<int>(used);
+    vg_fold g = f;
+    g.src[0] = vg_fold_src{ws + used, k0, f.width};
+    if (f.nsrc > 1) g.src[1] = vg_fold_src{ws + used + (int64_t)k0 * f.width, k1, f.width};
+    second[n2++] = g;
+    used += need;
+  }
+  const int rc = launch_batch(folds, n, split, c0, off, ws, stream);
+  if (rc || n2 == 0) return rc;
+  return launch_batch(second, n2, nullptr, nullptr, nullptr, nullptr, stream);
 }

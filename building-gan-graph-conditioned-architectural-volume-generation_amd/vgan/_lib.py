@@ -59,6 +59,9 @@ VG_JVP_GROUP_MAX = 16
 # before pass D.  Off: measured 0.07 ms per step slower than one launch per
 # block right after its destination-row pass
 _JVP_GROUP = os.environ.get("VGAN_JVP_GROUP", "0") == "1"
+# folds of more than 768 partial rows in two levels (vg_fold_batch_split),
+# as the critic engine does; 0: vg_fold_batch
+_FOLD_SPLIT = os.environ.get("VGAN_FOLD_SPLIT", "1") == "1"
 
 
 class VgGnBwdIn(ctypes.Structure):
@@ -212,6 +215,8 @@ class VgHgenBatch(ctypes.Structure):
 # name -> (restype, argtypes); every function listed here is declared in include/vgan.h
 SIGNATURES = {
     "vg_fold_batch": (ctypes.c_int, [_c_p, _c_i32, _c_p]),
+    "vg_fold_split_ws_floats": (_c_i64, [_c_p, _c_i32]),
+    "vg_fold_batch_split": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i64, _c_p]),
     "vg_gemm_tn_plan": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_i32, _c_p,
                                        _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p]),
     "vg_gemm_tn_group": (ctypes.c_int, [_c_p, _c_i32, _c_p]),
@@ -640,5 +645,10 @@ class FoldCollector:
             batches.append(cur)
         for b in batches:
             arr = (VgFold * len(b))(*b)
-            check(LIB.vg_fold_batch(arr, len(b), stream), "vg_fold_batch")
+            need = int(LIB.vg_fold_split_ws_floats(arr, len(b))) if _FOLD_SPLIT else 0
+            if need > 0:  # the chunk sums' workspace, on the current stream (the folds' own: stream-ordered reuse)
+                ws = torch.empty(need, dtype=torch.float32, device="cuda")
+                check(LIB.vg_fold_batch_split(arr, len(b), ws.data_ptr(), need, stream), "vg_fold_batch_split")
+            else:
+                check(LIB.vg_fold_batch(arr, len(b), stream), "vg_fold_batch")
         self.folds, self.keep = [], []

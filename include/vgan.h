@@ -430,6 +430,15 @@ typedef struct {
  * workspaces alive until vg_fold_batch is enqueued. */
 int vg_fold_batch(const vg_fold* folds, int32_t n, void* stream);
 
+/* vg_fold_batch, with folds of more than 768 partial rows done in two levels
+ * (one fold's rows in one workgroup were the batch's long pole): the column
+ * sums of each 128-row chunk land in `ws` in the same launch as the short
+ * folds, then a second launch folds those sums into the destinations in the
+ * same (out + src 0) + src 1 order.  `ws` (device, ws_floats floats) takes
+ * vg_fold_split_ws_floats(folds, n); folds that do not fit run in one level. */
+int64_t vg_fold_split_ws_floats(const vg_fold* folds, int32_t n);
+int vg_fold_batch_split(const vg_fold* folds, int32_t n, float* ws, int64_t ws_floats, void* stream);
+
 /* vg_gemm_tn_ex without its fold: writes up to 2 descriptors (C, then db when
  * non-NULL) to folds_out and their count to *n_out (host memory). */
 int vg_gemm_tn_deferred(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t N,
