@@ -2406,6 +2406,11 @@ static inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) 
 #ifndef VG_WRES
 #define VG_WRES 1
 #endif
+// K from which the f32 LayerNorm GEMMs (64 < M <= 128) take 64-row tiles:
+// W (M x K) streamed from L2 per tile dominates there
+#ifndef VG_LN_TM64_K
+#define VG_LN_TM64_K 384
+#endif
 #ifndef VG_WRES_MIN_ROWS
 #define VG_WRES_MIN_ROWS 16384
 #endif
@@ -2474,6 +2479,9 @@ static int gemm_ln_act(const float* A, int32_t lda, const float* W, int32_t N, i
     else if (M <= TN)
       k_gemm_ln16<1, TM><<<grid, 1024, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma, beta, eps, slope, H, Y, mean,
                                               rstd);
+    else if (VG_LN_TM32 && ql && K >= VG_LN_TM64_K)  // long K: 64-row tiles stream W half as often
+      k_gemm_ln16<2, TM, false, false, true><<<grid, 1024, 0, s>>>(A, lda, W, K, bias, N, M, K, gamma, beta, eps,
+                                                                  slope, H, Y, mean, rstd);
     else if (VG_LN_TM32 && ql)
       k_gemm_ln16<2, 32, false, false, true><<<dim3((N + 31) / 32, 1), 1024, 0, s>>>(
           A, lda, W, K, bias, N, M, K, gamma, beta, eps, slope, H, Y, mean, rstd);
@@ -2547,7 +2555,11 @@ static int gemm_ln_act_ms(const vg_asrc* src, int32_t nsrc, const float* W, int3
   for (int i = 0; i < nsrc; ++i) ql = ql && src[i].ld % 4 == 0 && src[i].w_col0 % 4 == 0 && al16(src[i].ptr);
   if (!BF && ql && try_wres<true>(nullptr, 0, W, ldw, bias, N, M, K, gamma, beta, eps, slope, nullptr, Y, nullptr,
                                   nullptr, ldy, d, s)) {
-  } else if (!BF && VG_LN16 && ql)
+  } else if (!BF && VG_LN16 && ql && K >= VG_LN_TM64_K)  // long K: 64-row tiles stream W half as often
+    k_gemm_ln16<2, TM, false, true, true><<<dim3((N + TM - 1) / TM, 1), 1024, 0, s>>>(
+        nullptr, 0, W, ldw, bias, N, M, K, gamma, beta, eps, slope, nullptr, Y, nullptr, nullptr, nullptr, nullptr,
+        nullptr, nullptr, ldy, d);
+  else if (!BF && VG_LN16 && ql)
     k_gemm_ln16<2, 32, false, true, true><<<dim3((N + 31) / 32, 1), 1024, 0, s>>>(
         nullptr, 0, W, ldw, bias, N, M, K, gamma, beta, eps, slope, nullptr, Y, nullptr, nullptr, nullptr, nullptr,
         nullptr, nullptr, ldy, d);

@@ -866,3 +866,41 @@ def test_grouped_weight_gradient_products_match_f64(cuda):
         ref = c0.double() + a.double().t() @ b.double()
         assert rel_err(c, ref) < 1e-5, a.shape
         assert rel_err(db, db0.double() + a[:dbr].double().sum(0)) < 1e-5, a.shape
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [384, 524])
+def test_gemm_ln_act_long_k_64_row_tiles(cuda, k):
+    """Long-K LayerNorm GEMMs (K >= VG_LN_TM64_K) run on 64-row tiles, single-
+    and multi-source: Y, H, mean and rstd against the f64 LayerNorm of the
+    product (the multi-source call as three column blocks with their own
+    strides and a row-broadcast addend against the concatenated product)."""
+    from vgan._lib import LIB, VgASrc, check, ptr
+
+    torch.manual_seed(k)
+    n, m = 5003, 128
+    w = torch.randn(m, k, device=cuda) / k ** 0.5
+    bias, g, be = torch.randn(m, device=cuda), 1 + 0.1 * torch.randn(m, device=cuda), 0.1 * torch.randn(m, device=cuda)
+    st = ops.stream_handle(cuda)
+
+    def ref(pre):
+        return torch.nn.functional.leaky_relu(torch.nn.functional.layer_norm(pre, (m,), g.double(), be.double(), 1e-5), 0.2)
+
+    x = torch.randn(n, k, device=cuda)
+    h, y = torch.empty(n, m, device=cuda), torch.empty(n, m, device=cuda)
+    mu, rs = torch.empty(n, device=cuda), torch.empty(n, device=cuda)
+    check(LIB.vg_gemm_ln_act(ptr(x), k, ptr(w), n, m, k, ptr(bias), ptr(g), ptr(be), 1e-5, 0.2, ptr(h), ptr(y),
+                             ptr(mu), ptr(rs), st), "vg_gemm_ln_act")
+    pre = x.double() @ w.double().t() + bias.double()
+    assert rel_err(h, pre) < 1e-5 and rel_err(y, ref(pre)) < 1e-5
+    assert rel_err(mu, pre.mean(1)) < 1e-4
+    if k % 32 == 0:  # the multi-source entry: three 128-column blocks in buffers of other widths
+        blocks = [torch.randn(n, 128 + 8 * i, device=cuda) for i in range(3)]
+        add = torch.randn(64, m, device=cuda)
+        src = (VgASrc * 3)(*[VgASrc(b.data_ptr(), b.shape[1], 128, 128 * i, 0) for i, b in enumerate(blocks)])
+        y2 = torch.empty(n, m, device=cuda)
+        check(LIB.vg_gemm_ln_act_ms(src, 3, ptr(w), k, n, m, None, ptr(add), m, 64, ptr(g), ptr(be), 1e-5, 0.2,
+                                    ptr(y2), m, st), "vg_gemm_ln_act_ms")
+        xc = torch.cat([b[:, :128] for b in blocks], dim=1).double()
+        pre2 = xc @ w.double().t() + add.double()[torch.arange(n, device=cuda) % 64]
+        assert rel_err(y2, ref(pre2)) < 1e-5

@@ -228,8 +228,11 @@ def test_gloo_two_ranks_full_steps_identical_parameters(cuda):
     ranks (averaged gradients, identical Adam), the losses differ (different
     buildings and draws)."""
     out = _run_worker(["gloo2"])
-    lines = [l for l in out.splitlines() if l.startswith("RANK")]
-    assert len(lines) == 2
+    # the two ranks share one stdout: a line may land inside the other's
+    import re
+
+    lines = re.findall(r"RANK \d+ \S+ \S+ \S+ \d+", out)
+    assert len(lines) == 2, out
     r0, r1 = (l.split() for l in sorted(lines))
     assert r0[2] == r1[2] and r0[3] == r1[3]  # parameter digests (G, D)
     assert r0[4] != r1[4]  # d_loss of the last step: own batch, own draws
