@@ -41,7 +41,10 @@ struct FoldBatch {
 #ifndef VG_FOLD_SPLIT_ROWS
 #define VG_FOLD_SPLIT_ROWS 768  // vg_fold_batch_split: folds with more partial rows go two-level
 #endif
-constexpr int kChunkRows = 128;
+#ifndef VG_FOLD_CHUNK_ROWS
+#define VG_FOLD_CHUNK_ROWS 256  // partial rows per first-level chunk (64 / 128 / 256 / 384 / 512 measured)
+#endif
+constexpr int kChunkRows = VG_FOLD_CHUNK_ROWS;
 
 // Sixteen rows in flight per wave and iteration (the GAT / LayerNorm partial
 // sets have up to a few thousand rows: a short dependent loop, not one round

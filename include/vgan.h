@@ -432,7 +432,7 @@ int vg_fold_batch(const vg_fold* folds, int32_t n, void* stream);
 
 /* vg_fold_batch, with folds of more than 768 partial rows done in two levels
  * (one fold's rows in one workgroup were the batch's long pole): the column
- * sums of each 128-row chunk land in `ws` in the same launch as the short
+ * sums of each 256-row chunk land in `ws` in the same launch as the short
  * folds, then a second launch folds those sums into the destinations in the
  * same (out + src 0) + src 1 order.  `ws` (device, ws_floats floats) takes
  * vg_fold_split_ws_floats(folds, n); folds that do not fit run in one level. */
