@@ -232,7 +232,7 @@ def test_b32_graphed_step_matches_eager(cuda, b32):
     prep = vdata.prepared(loc, vox, cfg.NUM_CLASSES)
     assert prep.csr.ell()[0] is not None and ops._GN_FWD_FUSE  # the variants the bench times
     assert graphed._stacked_labels()
-    graphs = graphed.capture(loc, vox)
+    graphs = graphed.capture(loc, vox, whole=False)  # the per-piece graphs, replayed one by one
     assert torch.equal(graphed.flat_g.param, eager.flat_g.param)  # capture left no trace
     graphs["labels"].replay()
     labels_e = eager._critic_labels(loc, vox)

@@ -46,7 +46,7 @@ def test_graph_iterations_match_eager_bodies(cuda, tiny):
     cfg.runtime["rng"] = "fixed"
     eager, graphed = _trainer(cfg), _trainer(cfg)
     loc, vox = _batch(cuda)
-    graphs = graphed.capture(loc, vox)
+    graphs = graphed.capture(loc, vox, whole=False)  # the per-piece graphs, replayed one by one
     acc_e = torch.zeros(2, device=cuda)
     for it in range(cfg.N_CRITIC):
         graphed.flat_d.param.copy_(eager.flat_d.param)  # same state in, one iteration out
@@ -96,3 +96,28 @@ def test_graph_replays_draw_fresh_noise(cuda):
     assert len(set(outs)) == 3  # different z / dropout / Gumbel / GP eps each replay
     assert all(abs(v) < 1e4 for v in outs)
     assert int(tr.adam_d.step_t.item()) == 3 * cfg.N_CRITIC and int(tr.adam_g.step_t.item()) == 3
+
+
+def test_whole_step_graph_equals_piece_graphs(cuda):
+    """step_graphed over ONE graph of the whole step (stacked labels, the
+    critic iterations, the generator iteration) and over the per-piece graphs
+    replayed back to back: the same launches in the same order, so losses,
+    labels and every parameter and Adam moment bit for bit over three steps."""
+    cfg = Configuration()
+    cfg.runtime["rng"] = "device"
+    a, b = _trainer(cfg), _trainer(cfg)
+    assert a._stacked_labels() and b._stacked_labels()
+    la, va = _batch(cuda)
+    lb, vb = _batch(cuda)
+    ga = a.capture(la, va, whole=True)
+    gb = b.capture(lb, vb, whole=False)
+    assert ga.get("whole") is not None and gb.get("whole") is None and len(gb["critic"]) == cfg.N_CRITIC
+    for _ in range(3):
+        oa, ob = a.step_graphed(la, va), b.step_graphed(lb, vb)
+        torch.cuda.synchronize()
+        assert torch.equal(oa["d_losses"], ob["d_losses"]) and torch.equal(oa["g_loss"], ob["g_loss"])
+        assert torch.equal(oa["label_hard"], ob["label_hard"])
+    for fa, fb in ((a.flat_g, b.flat_g), (a.flat_d, b.flat_d)):
+        assert torch.equal(fa.param, fb.param)
+    for ma, mb in ((a.adam_g, b.adam_g), (a.adam_d, b.adam_d)):
+        assert torch.equal(ma.exp_avg, mb.exp_avg) and torch.equal(ma.exp_avg_sq, mb.exp_avg_sq)
