@@ -74,6 +74,7 @@ __device__ __forceinline__ float act_fn(float v, float aux) {
   if constexpr (ACT == 1) return v > 0.f ? v : 0.f;
   else if constexpr (ACT == 2) return v > 0.f ? v : 0.2f * v;
   else if constexpr (ACT == 3) return aux > 0.f ? v : 0.f;
+  else if constexpr (ACT == 4) return v + aux;  // a second adjoint summed in (torch's add_ after the GEMM)
   else return v;
 }
 
@@ -354,7 +355,7 @@ __global__ void __launch_bounds__(256) k_gemm(const float* __restrict__ A, int l
   for (int r = 0; r < 16; ++r) {
     const int n = n0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
     if (n < N && m < M) {
-      const float av = ACT == 3 ? aux[(size_t)n * ldaux + m] : 0.f;
+      const float av = ACT >= 3 ? aux[(size_t)n * ldaux + m] : 0.f;
       C[(size_t)n * ldc + m] = act_fn<ACT>(acc[r] + bv, av);
     }
   }
@@ -674,7 +675,7 @@ __device__ __forceinline__ void gemm16_body(const float* __restrict__ A, int lda
     for (int r = 0; r < 4; ++r) {
       const int n = n0 + wr * 16 + 4 * (lane >> 4) + r;
       if (n < N && mc < M) {
-        const float av = ACT == 3 ? aux[(size_t)n * ldaux + mc] : 0.f;
+        const float av = ACT >= 3 ? aux[(size_t)n * ldaux + mc] : 0.f;
         C[(size_t)n * ldc + mc] = act_fn<ACT>(acc[r] + bv, av);
       }
     }
@@ -2089,8 +2090,8 @@ template <bool BF>
 static int gemm(const float* A, int32_t lda, const float* B, int32_t ldb, int32_t b_trans, const float* bias,
                 int32_t act, const float* aux, int32_t ldaux, float* C, int32_t ldc, int32_t N, int32_t M,
                 int32_t K, void* stream) {
-  if (N < 0 || M <= 0 || K <= 0 || !A || !B || !C || act < 0 || act > 3) return VG_EINVAL;
-  if (act == 3 && !aux) return VG_EINVAL;
+  if (N < 0 || M <= 0 || K <= 0 || !A || !B || !C || act < 0 || act > 4) return VG_EINVAL;
+  if (act >= 3 && !aux) return VG_EINVAL;
   if (N == 0) return 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
   dim3 grid((N + TM - 1) / TM, (M + TN - 1) / TN);
@@ -2124,10 +2125,10 @@ static int gemm(const float* A, int32_t lda, const float* B, int32_t ldb, int32_
   } while (0)
   if (b_trans) {
     if (act == 0) VG_G(true, 0); else if (act == 1) VG_G(true, 1);
-    else if (act == 2) VG_G(true, 2); else VG_G(true, 3);
+    else if (act == 2) VG_G(true, 2); else if (act == 3) VG_G(true, 3); else VG_G(true, 4);
   } else {
     if (act == 0) VG_G(false, 0); else if (act == 1) VG_G(false, 1);
-    else if (act == 2) VG_G(false, 2); else VG_G(false, 3);
+    else if (act == 2) VG_G(false, 2); else if (act == 3) VG_G(false, 3); else VG_G(false, 4);
   }
 #undef VG_G
   VG_CHECK_LAUNCH();

@@ -45,7 +45,7 @@ from ._lib import (_GN_ROWS, LIB, FoldCollector, VgGnApply, VgGnBwdIn, VgGnJvp, 
                    linear_chain, ptr, stream_handle, sync_counter)
 from . import _lib
 
-ACT_NONE, ACT_RELU, ACT_MASK = 0, 1, 3
+ACT_NONE, ACT_RELU, ACT_MASK, ACT_ADD = 0, 1, 3, 4  # vg_gemm act codes (include/vgan.h)
 _CHAIN_TANGENT = os.environ.get("VGAN_CHAIN_TANGENT", "1") == "1"
 # VGAN_GN_FUSE=0: the GraphNorm backward's column partials in their own pass
 # instead of the epilogue of the GEMM producing its g_y (A/B knob)

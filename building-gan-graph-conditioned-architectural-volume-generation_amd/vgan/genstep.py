@@ -35,6 +35,7 @@ differs only in the summation grouping of fused reductions
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import List
 
 import torch
@@ -43,7 +44,11 @@ import torch.nn as nn
 from . import data as vdata
 from . import ops
 from ._lib import _GN_ROWS, LIB, FoldCollector, VgGnBwdIn, check, dense, linear_chain, ptr, stream_handle, sync_counter
-from .critic import _GN_FUSE, ACT_MASK, ACT_NONE, ACT_RELU, _f, _off
+from .critic import _GN_FUSE, ACT_ADD, ACT_MASK, ACT_NONE, ACT_RELU, _f, _off
+
+# VGAN_GEN_ADD_FUSE=0: the summed adjoints (label_hard, x, em) as a product
+# then a torch add_ instead of the product's add epilogue (A/B knob)
+_ADD_FUSE = os.environ.get("VGAN_GEN_ADD_FUSE", "1") == "1"
 
 
 class GeneratorEngine:
@@ -100,6 +105,16 @@ class GeneratorEngine:
     @staticmethod
     def _gemm(st, A, lda, B, ldb, bt, C, ldc, n, m, k, bias=None, act=ACT_NONE, aux=None, ldaux=0):
         check(dense("vg_gemm")(A, lda, B, ldb, bt, bias, act, aux, ldaux, C, ldc, n, m, k, st), "vg_gemm")
+
+    def _gemm_sum(self, st, A, lda, B, ldb, C, ldc, n, m, k, other, col):
+        """C [n, m] = A B + other[:, col:col + m]: the sum of a tensor's two
+        adjoints, added in the product's epilogue (act 4) -- bit-identical to
+        the product then torch's add_ (VGAN_GEN_ADD_FUSE=0, the A/B leg)."""
+        if _ADD_FUSE:
+            self._gemm(st, A, lda, B, ldb, 0, ptr(C), ldc, n, m, k, None, ACT_ADD, _off(other, col), other.shape[1])
+        else:
+            self._gemm(st, A, lda, B, ldb, 0, ptr(C), ldc, n, m, k)
+            C.add_(other[:, col:col + m])
 
     @staticmethod
     def _tn(folds, st, dev, A, lda, B, ldb, n, m, k, C, ldc, db=None):
@@ -376,9 +391,10 @@ class GeneratorEngine:
             self._gemm(st, ptr(adj_m[i]), o, ptr(self.d_mlp[i].weight), m, 0, ptr(adj_m[i - 1]), m, n, m, o, None,
                        ACT_MASK, ptr(d_mlp_out[i - 1]), m)
         W0 = self.d_mlp[0].weight
-        g_lab = _f(n, K, dev=dev)
-        self._gemm(st, ptr(adj_m[0]), W0.shape[0], _off(W0, F), W0.shape[1], 0, ptr(g_lab), K, n, K, W0.shape[0])
-        g_hard.add_(g_lab)  # label_hard feeds the loss head and D (models.py:229-239)
+        g_lab = _f(n, K, dev=dev)  # label_hard feeds the loss head and D (models.py:229-239): both adjoints summed
+        self._gemm_sum(st, ptr(adj_m[0]), W0.shape[0], _off(W0, F), W0.shape[1], g_lab, K, n, K, W0.shape[0],
+                       g_hard, 0)
+        g_hard = g_lab
 
         # --------------------------------------------------- Gumbel backward
         g_logits = _f(n, K, dev=dev)
@@ -418,9 +434,8 @@ class GeneratorEngine:
                 g_y = _f(n, cin, dev=dev)
                 tp = self._gemm_dy(st, dev, ptr(dH), c, ptr(Wl), cin, g_y, n, cin, c, genc[b - 1])
             else:
-                g_x = _f(n, cin, dev=dev)
-                self._gemm(st, ptr(dH), c, ptr(Wl), cin, 0, ptr(g_x), cin, n, cin, c)
-        g_x.add_(g_xem[:, :hg])  # x feeds the encoder and the decoder (models.py:132-145)
+                g_x = _f(n, cin, dev=dev)  # x feeds the encoder and the decoder (models.py:132-145)
+                self._gemm_sum(st, ptr(dH), c, ptr(Wl), cin, g_x, cin, n, cin, c, g_xem, 0)
         g = g_x
         for i in range(len(mlp_s) - 1, -1, -1):
             S = mlp_s[i]
@@ -430,9 +445,8 @@ class GeneratorEngine:
                 g = _f(n, k, dev=dev)
                 self._gemm(st, ptr(g_h), m, ptr(W_), k, 0, ptr(g), k, n, k, m)
             else:  # the em columns of [em | voxel.x | z]
-                g = _f(n, hl, dev=dev)
-                self._gemm(st, ptr(g_h), m, ptr(W_), k, 0, ptr(g), hl, n, hl, m)
-        g.add_(g_xem[:, hg:])  # em feeds the MLP encoder and the decoder
+                g = _f(n, hl, dev=dev)  # em feeds the MLP encoder and the decoder
+                self._gemm_sum(st, ptr(g_h), m, ptr(W_), k, g, hl, n, hl, m, g_xem, hg)
         for i in range(len(mfe_s) - 1, -1, -1):
             S = mfe_s[i]
             g_h = self._ln_bwd(folds, st, dev, S, g, n)

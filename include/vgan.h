@@ -344,7 +344,9 @@ int vg_confusion(const int64_t* truth, const float* label, int32_t classes, cons
 
 /* C[N, M] = A[N, K] . op(B) (+ bias[M]) then act (0 none, 1 ReLU, 2 LeakyReLU
  * 0.2, 3 multiply by [aux > 0] with aux [N, M] row stride ldaux -- a ReLU mask
- * applied to an adjoint or tangent; aux may be NULL otherwise).
+ * applied to an adjoint or tangent; 4 add aux -- a second adjoint of the same
+ * tensor summed in, as torch's add_ after the product; aux may be NULL for
+ * act 0-2, and must not alias C).
  * b_trans = 1: B is [M, K] (op = transpose; the nn.Linear forward X W^T);
  * b_trans = 0: B is [K, M] (dX = dY W).  f32 MFMA (v_mfma_f32_32x32x2_f32).
  * Replaces the torch.nn.Linear GEMMs at models.py:33-47,49-66,92-113,

@@ -139,3 +139,13 @@ def test_graphed_sweep_refuses_bad_arguments_host_only():
     a, b = ct.c_int32(7), ct.c_int32(7)
     assert lib.vg_hgen_graph_stats(None, ct.byref(a), ct.byref(b)) == VG_EINVAL
     lib.vg_hgen_graph_destroy(None)  # a NULL handle is a no-op
+
+
+def test_gemm_act_codes_checked_host_only():
+    """vg_gemm refuses an act code outside 0-4, and act 3 / 4 (mask, add)
+    without aux, before any launch."""
+    from vgan._lib import LIB as lib
+
+    VG_EINVAL = -1
+    for act, aux in ((5, 1), (-1, 1), (3, None), (4, None)):
+        assert lib.vg_gemm(1, 8, 1, 8, 1, None, act, aux, 8, 1, 8, 8, 8, 8, None) == VG_EINVAL, act

@@ -36,6 +36,27 @@ def _close(got, ref, tol=1e-5):
 
 
 # ------------------------------------------------------------------ GEMM
+@pytest.mark.parametrize("sym", ["vg_gemm", "vg_gemm_bf16"])
+@pytest.mark.parametrize("bt", [0, 1])
+def test_gemm_add_epilogue_equals_product_then_add(cuda, sym, bt):
+    """act 4 (C = A op(B) + aux, aux a strided column window): bit-exact with
+    the act-0 product followed by torch's add_ -- the generator engine's
+    summed adjoints (genstep.py) rely on it."""
+    g = torch.Generator().manual_seed(1)
+    n, k, m, ld = 1000, 96, 40, 72
+    A = torch.randn(n, k, generator=g).to(cuda)
+    W = torch.randn(*((m, k) if bt else (k, m)), generator=g).to(cuda)
+    wide = torch.randn(n, ld, generator=g).to(cuda)  # aux = wide[:, 9:9+m]
+    C0, C4 = torch.empty(n, m, device=cuda), torch.empty(n, m, device=cuda)
+    st = stream_handle(cuda)
+    fn = getattr(LIB, sym)
+    ldb = k if bt else m
+    check(fn(ptr(A), k, ptr(W), ldb, bt, None, 0, None, 0, ptr(C0), m, n, m, k, st), sym)
+    check(fn(ptr(A), k, ptr(W), ldb, bt, None, 4, wide.data_ptr() + 4 * 9, ld, ptr(C4), m, n, m, k, st), sym)
+    assert torch.equal(C4, C0.add_(wide[:, 9:9 + m]))
+    assert fn(ptr(A), k, ptr(W), ldb, bt, None, 4, None, 0, ptr(C4), m, n, m, k, st) != 0  # aux required
+
+
 def test_gemm_mask_epilogue_and_strided_accumulate(cuda):
     g = torch.Generator().manual_seed(0)
     n, k, m = 300, 37, 45
