@@ -106,8 +106,11 @@ __device__ __forceinline__ float fold_rows_packed(const float* __restrict__ part
 // grid ran 8+ rounds of 1024-thread workgroups, each one round trip long.
 __global__ void __launch_bounds__(1024) k_fold_batch(const FoldBatch b) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int d = 0;
-  while (d + 1 < b.n && (int)blockIdx.x >= b.block0[d + 1]) ++d;
+  int d = 0, hi = b.n - 1;  // the fold owning this workgroup: the last d with block0[d] <= blockIdx.x
+  while (d < hi) {          // (binary search: up to VG_FOLD_MAX dependent argument loads otherwise)
+    const int mid = (d + hi + 1) >> 1;
+    if ((int)blockIdx.x >= b.block0[mid]) d = mid; else hi = mid - 1;
+  }
   const vg_fold& f = b.f[d];
   if (b.chunks[d] > 0) {  // first level of a split fold: one chunk of one source, 64 columns
     const int groups = (f.width + 63) / 64;

@@ -31,7 +31,9 @@ class VgFold(ctypes.Structure):
                 ("nsrc", _c_i32), ("src", VgFoldSrc * 2)]
 
 
-VG_FOLD_MAX = 40
+VG_FOLD_MAX = 120
+# VGAN_FOLD_BATCH: folds per vg_fold_batch launch (<= VG_FOLD_MAX; 40 was the round-4 limit, A/B knob)
+_FOLD_BATCH = max(1, min(int(os.environ.get("VGAN_FOLD_BATCH", str(VG_FOLD_MAX))), VG_FOLD_MAX))
 
 
 class VgTn(ctypes.Structure):
@@ -636,7 +638,7 @@ class FoldCollector:
                     continue
                 batches.append(cur)  # cannot merge: later batch, so the two never race
                 cur, where = [], {}
-            if len(cur) == VG_FOLD_MAX:
+            if len(cur) == _FOLD_BATCH:
                 batches.append(cur)
                 cur, where = [], {}
             where[f.out] = len(cur)

@@ -423,7 +423,7 @@ typedef struct {
   vg_fold_src src[2];
 } vg_fold;
 
-#define VG_FOLD_MAX 40
+#define VG_FOLD_MAX 120 /* the descriptors ride in the kernel arguments (~11 KB) */
 
 /* Run up to VG_FOLD_MAX folds (a HOST array, passed to the kernel by value)
  * in one launch.  The parameter gradients of a backward are needed only by

@@ -72,3 +72,30 @@ def test_fold_batch_split_matches_f64(cuda, ws_scale):
     if ws_scale == 0.0:  # nothing split: the same launch as vg_fold_batch, bit for bit
         for a, b in zip(outs, outs2):
             assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_full_fold_batch_every_workgroup_finds_its_fold(cuda):
+    """VG_FOLD_MAX folds in one launch (the descriptors in the kernel
+    arguments, each workgroup's fold found by binary search over block0),
+    mixed sizes including one-workgroup folds between many-workgroup ones:
+    every destination equals its f64 column sums, split and unsplit alone;
+    one fold more is refused."""
+    from vgan._lib import VG_FOLD_MAX
+    shapes = [(5, 0, 4, 4, 1), (900, 300, 64, 64, 1), (40, 0, 300, 100, 0), (1300, 0, 16, 16, 1), (7, 7, 1, 1, 1)]
+    specs = [shapes[i % len(shapes)] for i in range(VG_FOLD_MAX)]
+    st = ops.stream_handle(cuda)
+    for split in (False, True):
+        arr, outs, want, keep = _folds(cuda, specs, 11)
+        if split:
+            need = int(LIB.vg_fold_split_ws_floats(arr, len(specs)))
+            ws = torch.empty(max(1, need), device=cuda)
+            check(LIB.vg_fold_batch_split(arr, len(specs), ctypes.c_void_p(ws.data_ptr()), need, st),
+                  "vg_fold_batch_split")
+        else:
+            check(LIB.vg_fold_batch(arr, len(specs), st), "vg_fold_batch")
+        torch.cuda.synchronize()
+        for i, (o, w) in enumerate(zip(outs, want)):
+            assert torch.allclose(o.double(), w, rtol=1e-5, atol=1e-3), (split, i, (o.double() - w).abs().max())
+    big = (VgFold * (VG_FOLD_MAX + 1))()
+    assert LIB.vg_fold_batch(big, VG_FOLD_MAX + 1, st) != 0
