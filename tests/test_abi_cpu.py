@@ -149,3 +149,14 @@ def test_gemm_act_codes_checked_host_only():
     VG_EINVAL = -1
     for act, aux in ((5, 1), (-1, 1), (3, None), (4, None)):
         assert lib.vg_gemm(1, 8, 1, 8, 1, None, act, aux, 8, 1, 8, 8, 8, 8, None) == VG_EINVAL, act
+
+
+def test_fold_batch_limit_matches_header():
+    """vgan._lib.VG_FOLD_MAX (the Python batcher's limit) is the header's."""
+    import re
+
+    from vgan import _lib
+
+    hdr = open(os.path.join(ROOT, "include", "vgan.h")).read()
+    assert int(re.search(r"#define VG_FOLD_MAX (\d+)", hdr).group(1)) == _lib.VG_FOLD_MAX
+    assert 1 <= _lib._FOLD_BATCH <= _lib.VG_FOLD_MAX
