@@ -261,7 +261,7 @@ def gemm_family_roofline(tr, n: int, device, reps: int = 20):
             "timing": "hipGraph-replayed between HIP events on the replay stream (f32 operands)"}
 
 
-def load_pmc_traffic(name: str = "r05_pmc_aggregate_gnp.json"):
+def load_pmc_traffic(name: str = "r06_pmc_aggregate_gnp.json"):
     """Per-launch HBM-side bytes of the scatter kernel from the committed
     rocprofv3 PMC summary of the variant the step runs (tools/pmc_roofline.sh
     --gnp), or (None, None) when this round has not measured it: an older
@@ -272,6 +272,81 @@ def load_pmc_traffic(name: str = "r05_pmc_aggregate_gnp.json"):
     with open(path) as f:
         d = json.load(f)
     return d.get("traffic_bytes_per_launch"), os.path.relpath(path, ROOT)
+
+
+# rocprofv3 kernel-trace summaries the roofline fractions are priced on
+# (tools/roofline_trace.sh, tools/stress_trace.sh); the live HIP-event figures
+# of the same launches are reported beside them
+ROOFLINE_TRACE = "r06_roofline_kernel_trace_gnp.txt"
+STRESS_TRACE = "r06_stress_ring_kernel_trace.txt"
+
+
+def load_trace_mean(name: str):
+    """{launches, avg_us, source} from the first line of a committed
+    rocprofv3 summary ("... launches traced: L; average duration T us ..."),
+    or None when this round has not committed it."""
+    import re
+
+    path = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        m = re.search(r"launches traced: (\d+); average duration ([0-9.]+) us", f.readline())
+    if not m:
+        return None
+    return {"launches": int(m.group(1)), "avg_us": float(m.group(2)), "source": os.path.relpath(path, ROOT)}
+
+
+def stress_model_leg(device, reps: int = 5):
+    """configs[3] through the drop-in: ``VoxelGNNGenerator.forward`` (eval,
+    no grad: the fused encoder, 14 GAT blocks) on the 8 x 50k stress batch,
+    voxels in lattice-block numbering, with the LDS ring dispatched for the
+    64 / 128-channel layers (ops.CSR.ring_on) and with it switched off (the
+    register gather); median of ``reps`` warm forwards between HIP events."""
+    from vgan import ops
+    from vgan.config import Configuration
+    from vgan.graph import GraphBatch
+    from vgan.locality import blocked
+    from vgan.models import VoxelGNNGenerator
+    from vgan.synth import make_stress_building
+
+    items = [make_stress_building(777, i) for i in range(8)]
+    loc = GraphBatch.from_data_list([lo for lo, _ in items]).to(device)
+    vox = GraphBatch.from_data_list([blocked(v)[0] for _, v in items]).to(device)
+    cfg = Configuration()
+    cfg.DEVICE = str(device)
+    cfg.runtime["rng"] = "device"
+    torch.manual_seed(cfg.SEED)
+    G = VoxelGNNGenerator(cfg, 17, 12).eval()
+    n = vox.num_nodes
+    z = torch.randn(1, n, cfg.Z_DIM, device=device)
+    out = {"workload": f"VoxelGNNGenerator.forward, eval, no grad, 8 x 50k-voxel stress buildings (N={n}), "
+                       f"lattice-block numbering, {G.encoder.num_blocks} GAT blocks of widths {G.encoder.widths}"}
+    saved = ops._RING
+    try:
+        for label, on in (("ring", True), ("register", False)):
+            ops._RING = on
+            with torch.no_grad():
+                for _ in range(2):
+                    G(loc, vox, z)
+                torch.cuda.synchronize()
+                d0 = ops.RING_DISPATCHES
+                times = []
+                for _ in range(reps):
+                    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    st.record()
+                    G(loc, vox, z)
+                    en.record()
+                    torch.cuda.synchronize()
+                    times.append(st.elapsed_time(en))
+            ms = sorted(times)[len(times) // 2]
+            out[label] = {"ms_per_forward": round(ms, 3), "graphs_per_s": round(8 / (ms * 1e-3), 1),
+                          "ring_launches_per_forward": (ops.RING_DISPATCHES - d0) // reps}
+            log(f"stress model forward ({label}): {ms:.2f} ms, {out[label]['ring_launches_per_forward']} ring launches")
+    finally:
+        ops._RING = saved
+    out["speedup"] = round(out["register"]["ms_per_forward"] / out["ring"]["ms_per_forward"], 3)
+    return out
 
 
 def make_pool(cfg, rank: int, world: int, pool: int, batch: int, device):
@@ -349,7 +424,7 @@ def timed_steps(tr, pool, steps: int, warmup: int, world: int, device, profile: 
     return elapsed
 
 
-def stress_roofline(device, channels=(128, 64, 1), reps: int = 20, order: str = "rowmajor"):
+def stress_roofline(device, channels=(128, 64, 1), reps: int = 20, order: str = "rowmajor", ring_only: bool = False):
     """vg_gat_aggregate_fwd on config #4 (8 x 50k-node buildings), cold MALL;
     for C a multiple of 64 also vg_gat_aggregate_fwd_lds (16-row tiles'
     distinct source rows staged through LDS) and, for C = 64 / 128,
@@ -380,7 +455,7 @@ def stress_roofline(device, channels=(128, 64, 1), reps: int = 20, order: str = 
         f"64-row {s_uniq:.1f} for {4 * e / tiles:.1f} ({staged_tiles} staged, "
         f"{int((uc < 0).sum().item())} from global memory)")
     scratch = torch.empty(512 * 1024 * 1024 // 4, device=device)  # flush the 256 MB MALL between reps
-    res, res_lds, res_st, res_ring = {}, {}, {}, {}
+    res, res_lds, res_st, res_ring, res_ring_gnp = {}, {}, {}, {}, {}
     for c in channels:
         h = torch.randn(n, c, device=device)
         a_s, a_d = 0.3 * torch.randn(n, device=device), 0.3 * torch.randn(n, device=device)
@@ -411,6 +486,14 @@ def stress_roofline(device, channels=(128, 64, 1), reps: int = 20, order: str = 
                                                 stream_handle(device)),
                   "vg_gat_aggregate_fwd_ring")
 
+        gnp_r = torch.empty(int(LIB.vg_gat_ring_gnp_floats(n, c)), device=device) if c in (64, 128) else None
+
+        def run_ring_gnp():  # as the drop-in runs it: with the following GraphNorm's column partials
+            check(LIB.vg_gat_aggregate_fwd_ring_gnp(ptr(csr.row_ptr), ptr(csr.col), n, c, ptr(h), ptr(a_s),
+                                                    ptr(a_d), ptr(bias), 0.2, ptr(out), ptr(alpha), ptr(rplan), n,
+                                                    ptr(gnp_r), ptr(ring_err), stream_handle(device)),
+                  "vg_gat_aggregate_fwd_ring_gnp")
+
         def timed(fn):
             for _ in range(3):
                 fn()
@@ -426,22 +509,28 @@ def stress_roofline(device, channels=(128, 64, 1), reps: int = 20, order: str = 
             return sum(times) / len(times)
 
         b, gb = agg_bytes(n, e, c), agg_gather_bytes(n, e, c)
-        avg = timed(run)
-        res[c] = {"avg_us": avg * 1e3, "bytes": b, "achieved_gbs": b / (avg * 1e-3) / 1e9,
-                  "gather_gbs": gb / (avg * 1e-3) / 1e9}
-        if c % 64 == 0:
-            avg = timed(run_lds)
-            res_lds[c] = {"avg_us": avg * 1e3, "bytes": b, "achieved_gbs": b / (avg * 1e-3) / 1e9}
+        if not ring_only:
+            avg = timed(run)
+            res[c] = {"avg_us": avg * 1e3, "bytes": b, "achieved_gbs": b / (avg * 1e-3) / 1e9,
+                      "gather_gbs": gb / (avg * 1e-3) / 1e9}
+            if c % 64 == 0:
+                avg = timed(run_lds)
+                res_lds[c] = {"avg_us": avg * 1e3, "bytes": b, "achieved_gbs": b / (avg * 1e-3) / 1e9}
         if c in (64, 128):
-            avg = timed(run_staged)
-            res_st[c] = {"avg_us": avg * 1e3, "bytes": b, "achieved_gbs": b / (avg * 1e-3) / 1e9}
+            if not ring_only:
+                avg = timed(run_staged)
+                res_st[c] = {"avg_us": avg * 1e3, "bytes": b, "achieved_gbs": b / (avg * 1e-3) / 1e9}
             avg = timed(run_ring)
             if int(ring_err.item()) != 0:
                 raise RuntimeError("vg_gat_aggregate_fwd_ring: a hand-over wait expired")
             res_ring[c] = {"avg_us": avg * 1e3, "bytes": b, "achieved_gbs": b / (avg * 1e-3) / 1e9}
+            avg = timed(run_ring_gnp)
+            if int(ring_err.item()) != 0:
+                raise RuntimeError("vg_gat_aggregate_fwd_ring_gnp: a hand-over wait expired")
+            res_ring_gnp[c] = {"avg_us": avg * 1e3, "bytes": b, "achieved_gbs": b / (avg * 1e-3) / 1e9}
     del scratch
     return {"nodes": n, "edges": e, "per_channels": res, "per_channels_lds": res_lds, "per_channels_staged": res_st,
-            "per_channels_ring": res_ring,
+            "per_channels_ring": res_ring, "per_channels_ring_gnp": res_ring_gnp,
             "order": order, "distinct_sources_per_tile": round(uniq / tiles, 1), "edges_per_tile": round(e / tiles, 1),
             "staged_plan": {"distinct_sources_per_64_row_tile": round(s_uniq, 1),
                             "edges_per_64_row_tile": round(4 * e / tiles, 1), "staged_tiles": staged_tiles,
@@ -467,12 +556,25 @@ def fresh_batch_leg(cfg, precision: str, steps: int, warmup: int, batch: int, de
     tmp = tempfile.mkdtemp(prefix=f"vgan_fresh_{rank}_")
     ds = SyntheticDataset(n_batches * batch * world, seed=4321)
     store = write_store(os.path.join(tmp, "store"), ds)
+    lstats = {}
     loader = GraphLoader(store, batch_size=batch, shuffle=True, device=device, prefetch=3, rank=rank,
-                         world_size=world, seed=4321, prepare=cfg.NUM_CLASSES)
+                         world_size=world, seed=4321, prepare=cfg.NUM_CLASSES, phase_stats=lstats)
     torch.manual_seed(cfg.SEED + rank)
     tr = build_trainer(cfg, precision)
     cfg.runtime["train_step"] = "auto"
     from vgan.gcscope import gc_frozen
+
+    # host seconds per phase of the timed steps: the loader's pipeline
+    # (GraphLoader phase_stats) and step_fresh's own phases (Trainer.phase_hook
+    # marks: prepare, labels, capture = recording + executable-graph update,
+    # replays, gen, release) -- where a slower host shows up on a fresh box
+    phases = {}
+    clock = [0.0]
+
+    def mark(name):
+        now = time.perf_counter()
+        phases[name] = phases.get(name, 0.0) + now - clock[0]
+        clock[0] = now
 
     it = iter(loader)
     with gc_frozen():  # as Trainer._train_each_epoch's batch loop
@@ -482,14 +584,20 @@ def fresh_batch_leg(cfg, precision: str, steps: int, warmup: int, batch: int, de
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
+        lstats.clear()
+        tr.phase_hook = mark
         t0 = time.perf_counter()
         for _ in range(steps):
+            clock[0] = time.perf_counter()
             loc, vox = next(it)
+            mark("next_batch")
             tr._train_batch(loc, vox)
+        t_host = time.perf_counter() - t0
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t0
+        tr.phase_hook = None
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -498,8 +606,18 @@ def fresh_batch_leg(cfg, precision: str, steps: int, warmup: int, batch: int, de
     import shutil
 
     shutil.rmtree(tmp, ignore_errors=True)
+    per = lambda sec: round(sec / steps * 1e3, 4)  # noqa: E731
+    host = {"enqueue_ms_per_step": per(t_host), "drain_ms": round((elapsed - t_host) * 1e3, 3),
+            "step_phases_ms_per_step": {k: per(v) for k, v in phases.items()},
+            "loader_ms_per_batch": {k: per(v) for k, v in lstats.items() if k != "batches"},
+            "how": "host perf_counter per phase over the timed steps: next_batch = the consumer's wait in the "
+                   "loader iterator (queue_wait + upload_wait of loader_ms_per_batch), then step_fresh's phases "
+                   "(prepare, labels, capture = critic recording + executable-graph update, replays, gen, "
+                   "release); loader collate / upload_issue run on its worker thread; enqueue = host time of "
+                   "the loop, drain = the device finishing after it"}
     return {"value": round(batch * world * steps / elapsed, 3), "unit": "graphs/s",
             "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps, "warmup": warmup,
+            "host_phases": host,
             "execution": "Trainer._train_batch per new batch (step_fresh: critic iteration captured once per batch, "
                          "replayed N_CRITIC times; label forward and generator iteration eager), GraphLoader "
                          "prefetch 3: host collate + host-built per-batch structures, one upload per batch"}
@@ -751,24 +869,10 @@ def rehearse(args, rank: int, world: int) -> None:
                           "elapsed_s_max_over_ranks": round(float(el), 6)}), flush=True)
 
 
-def median_leg(tr, pool, steps: int, world: int, device):
-    """SURVEY.md 8(d)'s statistic: the median of ``steps`` steps' HIP-event
-    durations (max over ranks of each rank's median), after the pool's
-    batches have run once."""
-    per = []
-    timed_steps(tr, pool, steps, 0, world, device, per_step=per)
-    med = sorted(per)[len(per) // 2]
-    if world > 1:
-        t = torch.tensor([med], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        med = float(t.item())
-    return med
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--pool", type=int, default=4, help="pre-staged batches per rank")
@@ -787,10 +891,11 @@ def main():
                     help="only the scatter-kernel roofline replays (--steps of them), for rocprofv3 --pmc passes")
     ap.add_argument("--gnp", action="store_true",
                     help="with --roofline-only: the variant the step runs (vg_gat_aggregate_fwd_gnp)")
+    ap.add_argument("--stress-only", action="store_true",
+                    help="only the configs[3] ring aggregations (blocked numbering, C=128, cold MALL), for "
+                         "tools/stress_trace.sh")
     ap.add_argument("--no-fresh", action="store_true", help="skip the fresh-batch (Trainer.train path) leg")
     ap.add_argument("--no-sweep", action="store_true", help="skip the configs[4] inference-sweep leg")
-    ap.add_argument("--median-steps", type=int, default=50,
-                    help="steps of the extra median leg (SURVEY.md 8(d): median of 50); 0 skips it")
     ap.add_argument("--rehearse", action="store_true",
                     help="the N-rank launch / barrier / max-over-ranks plumbing on the CPU (no GPU, no throughput)")
     args = ap.parse_args()
@@ -841,6 +946,11 @@ def main():
     cfg.runtime["rank"], cfg.runtime["world_size"] = rank, world  # per-rank device RNG streams
     torch.manual_seed(cfg.SEED + rank)
     torch.cuda.manual_seed(cfg.SEED + rank)
+    if args.stress_only:  # for rocprofv3: the ring launches of roofline_stress only
+        r = stress_roofline(device, channels=(128,), order="blocked", ring_only=True)
+        print(json.dumps({"stress_only": True, "ring": r["per_channels_ring"], "ring_gnp": r["per_channels_ring_gnp"]},
+                         default=float), flush=True)
+        return
     log(f"rank {rank}/{world}: staging {args.pool} batches of {args.batch} buildings")
     pool = make_pool(cfg, rank, world, args.pool, args.batch, device)
     tr = build_trainer(cfg, args.precision)
@@ -857,21 +967,32 @@ def main():
     per_step = []
     elapsed = timed_steps(tr, pool, args.steps, args.warmup, world, device, profile=args.profile,
                           per_step=None if args.profile else per_step)
-    value = args.batch * world * args.steps / elapsed
-    ms_per_step = elapsed / args.steps * 1e3
-    log(f"timed ({'hipGraph' if GRAPHED else 'eager'}, {args.precision}): {ms_per_step:.2f} ms/step, "
-        f"{value:.1f} graphs/s")
+    mean_ms = elapsed / args.steps * 1e3
+    # SURVEY.md 8(d)'s statistic: the MEDIAN step of the K timed steps (HIP
+    # events between the steps on the replay stream, no host sync inside the
+    # timed region), max over ranks; the wall-clock mean of the same region
+    # beside it
+    ms_per_step = mean_ms
+    if per_step:
+        ms_per_step = sorted(per_step)[len(per_step) // 2]
+        if world > 1:
+            t = torch.tensor([ms_per_step], device=device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ms_per_step = float(t.item())
+    value = args.batch * world / (ms_per_step * 1e-3)
+    log(f"timed ({'hipGraph' if GRAPHED else 'eager'}, {args.precision}): median {ms_per_step:.3f} ms/step "
+        f"({value:.1f} graphs/s), mean {mean_ms:.3f} ms/step over {args.steps} steps")
     median = None
-    if not args.profile and args.median_steps > 0:
-        med = median_leg(tr, pool, args.median_steps, world, device)
-        k_med = sorted(per_step)[len(per_step) // 2] if per_step else None
-        median = {"ms_per_step": round(med, 4), "value": round(args.batch * world / (med * 1e-3), 3),
-                  "steps": args.median_steps,
-                  "timed_region_median_ms": round(k_med, 4) if k_med is not None else None,
-                  "how": f"median of {args.median_steps} further steps' HIP-event durations (events between "
-                         f"steps on the replay stream, no host sync inside), max over ranks; "
-                         f"timed_region_median_ms: the same over the {args.steps} steps of the timed region"}
-        log(f"median of {args.median_steps} steps: {med:.3f} ms/step ({median['value']:.1f} graphs/s)")
+    if per_step:
+        median = {"ms_per_step": round(ms_per_step, 4), "value": round(value, 3), "steps": args.steps,
+                  "mean_ms_per_step": round(mean_ms, 4),
+                  "mean_value": round(args.batch * world * args.steps / elapsed, 3),
+                  "p10_p90_ms": [round(sorted(per_step)[len(per_step) // 10], 4),
+                                 round(sorted(per_step)[(9 * len(per_step)) // 10], 4)],
+                  "how": f"value / ms_per_step: the median of the {args.steps} timed steps' HIP-event durations "
+                         f"(events between steps on the replay stream, no host sync inside), max over ranks; "
+                         f"mean_*: wall clock of the same timed region (barrier + synchronize on both sides) / "
+                         f"{args.steps}"}
 
     if args.profile:
         if rank == 0:
@@ -944,12 +1065,21 @@ def main():
     if rank == 0:
         stress_orders = {} if args.no_stress else {o: stress_roofline(device, order=o)
                                                    for o in ("rowmajor", "tiled", "blocked")}
+        stress_model = None if args.no_stress else stress_model_leg(device)
         for o, st_ in stress_orders.items():
             for kind, key in (("register", "per_channels"), ("LDS 16-row", "per_channels_lds"),
                               ("staged", "per_channels_staged"), ("ring", "per_channels_ring")):
                 for c, r in st_[key].items():
                     log(f"stress ({o}) C={c} ({kind}): {r['avg_us']:.1f} us, {r['achieved_gbs']:.0f} GB/s")
         sweep = None if store_job is None else sweep_leg(device, store_job)
+        # the headline fraction priced on the committed rocprofv3 mean of the
+        # same replays (tools/roofline_trace.sh --gnp), the live HIP-event
+        # figure beside it
+        trace = load_trace_mean(ROOFLINE_TRACE)
+        roof_us = trace["avg_us"] if trace else head["avg_us"]
+        roof_gbs = head["avg_bytes"] / (roof_us * 1e-6) / 1e9
+        roof_src = (f"rocprofv3 kernel trace, {trace['source']}: mean of {trace['launches']} launches of the same "
+                    f"replays (bench.py --roofline-only --gnp)") if trace else "HIP events of this run (no trace)"
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args.batch, args.cpu_seconds)
@@ -986,13 +1116,19 @@ def main():
                 "kernel": "vg_gat_aggregate_fwd_gnp (the scatter kernel as the step runs it: GAT edge softmax + "
                           "CSR gather-sum + bias, with the following GraphNorm's column partials in the epilogue)",
                 "bound": "hbm",
-                "achieved": round(head["achieved_gbs"], 2),
+                "achieved": round(roof_gbs, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": round(head["achieved_gbs"] / HBM_PEAK_GBS, 5),
+                "frac": round(roof_gbs / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "avg_launch_us": round(head["avg_us"], 3),
+                "avg_launch_us": round(roof_us, 3),
+                "duration_source": roof_src,
+                "live_hip_events": {"avg_launch_us": round(head["avg_us"], 3),
+                                    "achieved": round(head["achieved_gbs"], 2),
+                                    "frac": round(head["achieved_gbs"] / HBM_PEAK_GBS, 5),
+                                    "note": "the same replays timed in this run with HIP events on the replay "
+                                            "stream; frac above is priced on the committed rocprofv3 mean"},
                 "avg_algorithmic_bytes": int(head["avg_bytes"]),
                 "algorithmic_bytes": "SURVEY.md 8(d) compulsory: 2*N*C*4 (h in, out) + 2*N*4 (a_src, a_dst) + "
                                      "E'*4 (col) + (N+1)*4 (row_ptr); alpha and the GraphNorm partials written "
@@ -1047,6 +1183,8 @@ def main():
                                           "rows by LDS-DMA, index loads two stages ahead; 12 consumer waves claim "
                                           "(tile, 4-row group) units and aggregate out of LDS; LDS-counter "
                                           "hand-over, no barrier)"}
+            kinds["per_channels_ring_gnp"] = ("vg_gat_aggregate_fwd_ring_gnp (the ring as the drop-in dispatches it: "
+                                              "with the following GraphNorm's column partials per 64-row tile)")
             cands = [(r[key][128]["avg_us"], o, key) for o, r in stress_orders.items() for key in kinds
                      if 128 in r.get(key, {})]
             _, o_best, k_best = min(cands)
@@ -1056,6 +1194,13 @@ def main():
                      "tiled": "4 x 4 (y, x) tiles per floor, vgan.locality.tile_order",
                      "blocked": "4 x 4 x 4 lattice blocks, vgan.locality.block_order"}
             gb = agg_gather_bytes(best["nodes"], best["edges"], 128)
+            # priced on the committed rocprofv3 trace of the ring's cold-MALL
+            # launches (tools/stress_trace.sh) when the fastest pair is the ring
+            st_trace = load_trace_mean(STRESS_TRACE) if k_best == "per_channels_ring" else None
+            st_us = st_trace["avg_us"] if st_trace else c128["avg_us"]
+            st_gbs = c128["bytes"] / (st_us * 1e-6) / 1e9
+            st_src = (f"rocprofv3 kernel trace, {st_trace['source']}: mean of {st_trace['launches']} cold-MALL "
+                      f"launches (bench.py --stress-only)") if st_trace else "HIP events of this run"
             result["roofline_stress"] = {
                 "workload": f"configs[3]: 8 x 50k-node buildings, N={best['nodes']}, E'={best['edges']}, "
                             f"C=128 fp32, cold MALL, voxels numbered {names[o_best]}",
@@ -1065,8 +1210,14 @@ def main():
                               if k_best in ("per_channels_staged", "per_channels_ring") else
                               f"{best['distinct_sources_per_tile']} distinct source rows for "
                               f"{best['edges_per_tile']} edges per 16-row tile"),
-                "bound": "hbm", "achieved": round(c128["achieved_gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(c128["achieved_gbs"] / HBM_PEAK_GBS, 4), "avg_launch_us": round(c128["avg_us"], 2),
+                "bound": "hbm", "achieved": round(st_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(st_gbs / HBM_PEAK_GBS, 4), "avg_launch_us": round(st_us, 2),
+                "duration_source": st_src,
+                "live_hip_events": {"avg_launch_us": round(c128["avg_us"], 2),
+                                    "achieved": round(c128["achieved_gbs"], 1),
+                                    "frac": round(c128["achieved_gbs"] / HBM_PEAK_GBS, 4),
+                                    "kernel_key": k_best},
+                "model_forward": stress_model,
                 "algorithmic_bytes": int(c128["bytes"]),
                 "edge_gather_bytes": int(gb),
                 "by_order": {o: {"distinct_sources_per_16_row_tile": r["distinct_sources_per_tile"],

@@ -24,6 +24,7 @@
 #include <memory>
 #include <mutex>
 #include <thread>
+#include <unistd.h>
 #include <vector>
 
 #include "../../include/vgan_host.h"
@@ -68,8 +69,21 @@ constexpr int64_t kWorkPerThread = 1 << 16;
 // another call's work.
 class Pool {
  public:
+  // One pool per PROCESS: a child forked while a helper held mu_ (or after
+  // helpers started -- they do not exist in the child) gets a fresh pool on
+  // its first call instead of the parent's, whose mutex may be locked forever
+  // and whose thread list counts threads the child does not have.  Pools are
+  // never destroyed: helpers may outlive static teardown, and a forked child
+  // must not touch the parent's.
   static Pool& get() {
-    static Pool* p = new Pool();  // never destroyed: helpers may outlive static teardown
+    static std::atomic<Pool*> cur{nullptr};
+    const pid_t me = getpid();
+    Pool* p = cur.load(std::memory_order_acquire);
+    while (!p || p->pid_ != me) {
+      Pool* fresh = new Pool(me);
+      if (cur.compare_exchange_strong(p, fresh, std::memory_order_acq_rel)) return *fresh;
+      delete fresh;  // another thread installed one first: p holds it now, re-checked
+    }
     return *p;
   }
 
@@ -122,6 +136,13 @@ class Pool {
         }
       });
   }
+  explicit Pool(pid_t pid) : pid_(pid) {}
+
+ public:
+  pid_t owner() const { return pid_; }
+
+ private:
+  const pid_t pid_;
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<std::function<void()>> jobs_;
@@ -143,6 +164,8 @@ void parallel_buildings(int32_t count, int32_t threads, int64_t work, F&& fn) {
 }
 
 }  // namespace
+
+extern "C" int64_t vgh_pool_pid(void) { return static_cast<int64_t>(Pool::get().owner()); }
 
 extern "C" int vgh_collate_sizes(const int64_t* node_ptr, const int64_t* edge_ptr, const int32_t* esrc,
                                  const int32_t* edst, int64_t num_buildings, const int64_t* index,

@@ -623,13 +623,56 @@ struct RingRow {
   float ad, m, denom;
 };
 
+// GNP: the following GraphNorm's column partials (count, mean, M2) per 64-row
+// tile and 64-channel slice, in gat_fused.hip's gnp layout with 64-row blocks
+// ([tile][2][C][3], slot 0; vg_graphnorm_stats_gnp / _fwd_gnp fold them with
+// gnp_rows = 64).  A consumer unit forms its 4-row group's two-pass (mean, M2)
+// from the values it stores (xor shuffles across the wave's four 16-lane rows,
+// as gnp_block) and writes them to the workgroup's scratch [NS][Groups][2][64];
+// the slot's FREE counter (release) hands them to loader wave 0, which -- after
+// issuing the DMA that refills the slot, so the loads share its wait -- merges
+// the tile's 16 groups in group order with Chan's formula (deterministic) and
+// writes the tile partial.  The last NS items are merged after the loop.
 template <class G>
+__device__ __forceinline__ void ring_gnp_load(float (&pv)[G::Groups][2], const float* __restrict__ scratch, int s,
+                                              int lane) {
+  const float* sp = scratch + ((size_t)blockIdx.x * G::NS + s) * G::Groups * 128;
+#pragma unroll
+  for (int g = 0; g < G::Groups; ++g) {
+    pv[g][0] = sp[g * 128 + lane];
+    pv[g][1] = sp[g * 128 + 64 + lane];
+  }
+}
+
+template <class G>
+__device__ __forceinline__ void ring_gnp_store(const float (&pv)[G::Groups][2], int t, int sl, int N, int C, int lane,
+                                               float* __restrict__ gnp) {
+  const int r0 = t * G::RT;
+  float n = static_cast<float>(min(4, N - r0)), mu = pv[0][0], m2 = pv[0][1];
+#pragma unroll
+  for (int g = 1; g < G::Groups; ++g) {  // Chan's merge, group order
+    const int k = min(4, N - (r0 + 4 * g));
+    if (k > 0) {
+      const float nb = static_cast<float>(k), nt = n + nb;
+      const float delta = pv[g][0] - mu, fb = nb / nt;
+      mu += delta * fb;
+      m2 += pv[g][1] + delta * delta * n * fb;
+      n = nt;
+    }
+  }
+  float* p = gnp + ((size_t)t * 2 * C + sl * 64 + lane) * 3;
+  p[0] = n;
+  p[1] = mu;
+  p[2] = m2;
+}
+
+template <class G, bool GNP = false>
 __global__ void __launch_bounds__(kRNT) k_gat_fwd_ring(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, int N, int C,
     const float* __restrict__ h, const float* __restrict__ a_src, const float* __restrict__ a_dst,
     const float* __restrict__ bias, float slope, float* __restrict__ out, float* __restrict__ alpha,
     const int32_t* __restrict__ ucount, const int32_t* __restrict__ usrc, const uint16_t* __restrict__ lidx,
-    int tiles, int* __restrict__ err) {
+    int tiles, int* __restrict__ err, float* __restrict__ gnp = nullptr, float* __restrict__ scratch = nullptr) {
   extern __shared__ float4 ring4[];
   char* base = reinterpret_cast<char*>(ring4);
   int* cnt = reinterpret_cast<int*>(base + G::NS * G::SlotB);  // full[NS], free[NS], the next unit
@@ -740,13 +783,37 @@ __global__ void __launch_bounds__(kRNT) k_gat_fwd_ring(
           }
         }
       }
+      // GNP: item k - NS's group partials (its groups are done: FREE above),
+      // loaded under this slot's DMA wait, merged once it is handed over
+      float pv[GNP ? G::Groups : 1][2];
+      const bool merge = GNP && wave == 0 && k >= G::NS;
+      if constexpr (GNP) {
+        if (merge) ring_gnp_load<G>(pv, scratch, s, lane);
+      }
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 #if VG_RING_PROF == 2
       t_soft += __builtin_readcyclecounter() - f0_;  // FREE -> loaded
       t_gath += 1;
 #endif
       if (lane == 0) __hip_atomic_fetch_add(&cnt[s], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if constexpr (GNP) {
+        if (merge) {
+          const int kp = k - G::NS;
+          ring_gnp_store<G>(pv, tb + wslot + (kp / slices) * per, kp % slices, N, C, lane, gnp);
+        }
+      }
       if (pre) cur = nxt;
+    }
+    if constexpr (GNP) {  // the last NS items: wait for their groups, merge
+      if (wave == 0) {
+        for (int kp = max(0, items - G::NS); kp < items; ++kp) {
+          const int s = kp % G::NS, gen = kp / G::NS;
+          VG_RING_WAIT(&cnt[G::NS + s], G::Groups * (gen + 1), 1);
+          float pv[G::Groups][2];
+          ring_gnp_load<G>(pv, scratch, s, lane);
+          ring_gnp_store<G>(pv, tb + wslot + (kp / slices) * per, kp % slices, N, C, lane, gnp);
+        }
+      }
     }
 #if VG_RING_PROF
     prof_out();
@@ -891,9 +958,36 @@ __global__ void __launch_bounds__(kRNT) k_gat_fwd_ring(
         acc[2] = fmaf(aa, v.z, acc[2]);
         acc[3] = fmaf(aa, v.w, acc[3]);
       }
-      if (w.r < N)
-        *reinterpret_cast<float4*>(out + (size_t)w.r * C + sl * 64 + l16 * 4) =
-            make_float4(acc[0] + bv.x, acc[1] + bv.y, acc[2] + bv.z, acc[3] + bv.w);
+      const float4 ov = make_float4(acc[0] + bv.x, acc[1] + bv.y, acc[2] + bv.z, acc[3] + bv.w);
+      if (w.r < N) *reinterpret_cast<float4*>(out + (size_t)w.r * C + sl * 64 + l16 * 4) = ov;
+      if constexpr (GNP) {  // the group's 4-row column partials of this slice (two passes, as gnp_block)
+        const int nw = min(4, max(0, N - (r0 + 4 * grp)));
+        const bool lv = w.r < N;
+        const float inv = nw > 0 ? 1.f / static_cast<float>(nw) : 0.f;
+        const float xv[4] = {ov.x, ov.y, ov.z, ov.w};
+        float sm[4], mu[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sm[q] = lv ? xv[q] : 0.f;
+#pragma unroll
+        for (int off = 16; off < 64; off <<= 1)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) sm[q] += __shfl_xor(sm[q], off, 64);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          mu[q] = sm[q] * inv;
+          const float d = lv ? xv[q] - mu[q] : 0.f;
+          sm[q] = d * d;
+        }
+#pragma unroll
+        for (int off = 16; off < 64; off <<= 1)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) sm[q] += __shfl_xor(sm[q], off, 64);
+        if (lane < 16 && nw > 0) {
+          float* sp = scratch + (((size_t)blockIdx.x * G::NS + s) * G::Groups + grp) * 128;
+          *reinterpret_cast<float4*>(sp + l16 * 4) = make_float4(mu[0], mu[1], mu[2], mu[3]);
+          *reinterpret_cast<float4*>(sp + 64 + l16 * 4) = make_float4(sm[0], sm[1], sm[2], sm[3]);
+        }
+      }
 #if VG_RING_PROF == 1
       t_gath += __builtin_readcyclecounter() - p1;
 #endif
@@ -949,13 +1043,21 @@ extern "C" int vg_gat_ring_plan(const int32_t* row_ptr, const int32_t* col, int3
   return 0;
 }
 
-extern "C" int vg_gat_aggregate_fwd_ring(const int32_t* row_ptr, const int32_t* col, int32_t N, int32_t C,
-                                         const float* h, const float* a_src, const float* a_dst, const float* bias,
-                                         float slope, float* out, float* alpha, const int32_t* plan, int32_t* err,
-                                         void* stream) {
+// one workgroup per CU (the ring takes the LDS), a multiple of 8 (the XCD schedule)
+static int ring_grid(int tiles) {
+  int grid = num_cu();
+  const int need = (tiles + 7) / 8 * 8;
+  if (grid > need) grid = need;
+  return (grid + 7) / 8 * 8;
+}
+
+template <bool GNP>
+static int ring_launch(const int32_t* row_ptr, const int32_t* col, int32_t N, int32_t C, const float* h,
+                       const float* a_src, const float* a_dst, const float* bias, float slope, float* out,
+                       float* alpha, const int32_t* plan, int32_t* err, float* gnp, void* stream) {
   if (N <= 0 || (C != 64 && C != 128) || !row_ptr || !col || !h || !a_src || !a_dst || !bias || !out || !alpha ||
       !plan || !err || (reinterpret_cast<uintptr_t>(h) & 15) || (reinterpret_cast<uintptr_t>(out) & 15) ||
-      (reinterpret_cast<uintptr_t>(bias) & 15))
+      (reinterpret_cast<uintptr_t>(bias) & 15) || (GNP && (!gnp || (reinterpret_cast<uintptr_t>(gnp) & 15))))
     return VG_EINVAL;
   const int tiles = (N + RingG::RT - 1) / RingG::RT;
   const int32_t* ucount = plan;
@@ -963,19 +1065,44 @@ extern "C" int vg_gat_aggregate_fwd_ring(const int32_t* row_ptr, const int32_t* 
   const uint16_t* lidx = reinterpret_cast<const uint16_t*>(usrc + (size_t)tiles * RingG::SU);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gat_fwd_ring<RingG>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gat_fwd_ring<RingG, GNP>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, RingG::RingB);
     attr = true;
   }
-  // one workgroup per CU (the ring takes the LDS), a multiple of 8 (the XCD schedule)
-  int grid = num_cu();
-  const int need = (tiles + 7) / 8 * 8;
-  if (grid > need) grid = need;
-  grid = (grid + 7) / 8 * 8;
-  k_gat_fwd_ring<RingG><<<grid, kRNT, RingG::RingB, static_cast<hipStream_t>(stream)>>>(
-      row_ptr, col, N, C, h, a_src, a_dst, bias, slope, out, alpha, ucount, usrc, lidx, tiles, err);
+  const int grid = ring_grid(tiles);
+  float* scratch = GNP ? gnp + (size_t)tiles * 2 * C * 3 : nullptr;  // after the tile partials
+  k_gat_fwd_ring<RingG, GNP><<<grid, kRNT, RingG::RingB, static_cast<hipStream_t>(stream)>>>(
+      row_ptr, col, N, C, h, a_src, a_dst, bias, slope, out, alpha, ucount, usrc, lidx, tiles, err, gnp, scratch);
   VG_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int vg_gat_aggregate_fwd_ring(const int32_t* row_ptr, const int32_t* col, int32_t N, int32_t C,
+                                         const float* h, const float* a_src, const float* a_dst, const float* bias,
+                                         float slope, float* out, float* alpha, const int32_t* plan, int32_t* err,
+                                         void* stream) {
+  return ring_launch<false>(row_ptr, col, N, C, h, a_src, a_dst, bias, slope, out, alpha, plan, err, nullptr,
+                            stream);
+}
+
+extern "C" int32_t vg_gat_ring_tile_rows(void) { return RingG::RT; }
+
+extern "C" int64_t vg_gat_ring_gnp_floats(int32_t N, int32_t C) {
+  if (N <= 0 || (C != 64 && C != 128)) return 0;
+  const int64_t tiles = ((int64_t)N + RingG::RT - 1) / RingG::RT;
+  // the tile partials [tiles][2][C][3], then the group scratch of every workgroup
+  const int64_t grid = (num_cu() + 7) / 8 * 8;
+  return tiles * 2 * C * 3 + grid * RingG::NS * RingG::Groups * 128;
+}
+
+extern "C" int vg_gat_aggregate_fwd_ring_gnp(const int32_t* row_ptr, const int32_t* col, int32_t N, int32_t C,
+                                             const float* h, const float* a_src, const float* a_dst,
+                                             const float* bias, float slope, float* out, float* alpha,
+                                             const int32_t* plan, int32_t seg_rows, float* gnp, int32_t* err,
+                                             void* stream) {
+  // one segment, or segments of whole tiles: a segment's partials are its own tiles'
+  if (seg_rows <= 0 || N % seg_rows != 0 || (seg_rows != N && seg_rows % RingG::RT != 0)) return VG_EINVAL;
+  return ring_launch<true>(row_ptr, col, N, C, h, a_src, a_dst, bias, slope, out, alpha, plan, err, gnp, stream);
 }
 
 #if VG_RING_PROF

@@ -272,7 +272,7 @@ int run(Arena& ar, const vg_hgen_model* md, const vg_hgen_batch* bt, int8_t* lab
 }  // namespace
 
 extern "C" int64_t vg_hgen_arena_bytes(const vg_hgen_model* model, const vg_hgen_batch* batch) {
-  if (!model || !batch) return -VG_EINVAL;
+  if (!model || !batch) return VG_EINVAL;  // negative: an error, never a size
   Arena ar{true, nullptr};
   const int rc = run(ar, model, batch, nullptr, nullptr, nullptr);
   return rc ? (rc < 0 ? rc : -rc) : ar.off;
@@ -311,6 +311,7 @@ struct HgenGraph {
   hipStream_t cap = nullptr;
   bool used[2] = {false, false};
   int next = 0;
+  int dev = -1;  // the device current at creation: the capture stream's
   int32_t instantiations = 0, updates = 0;
 };
 }  // namespace
@@ -320,7 +321,7 @@ extern "C" void vg_hgen_graph_destroy(void* handle);
 extern "C" void* vg_hgen_graph_create(void) {
   HgenGraph* g = new (std::nothrow) HgenGraph();
   if (!g) return nullptr;
-  bool ok = hipStreamCreateWithFlags(&g->cap, hipStreamNonBlocking) == hipSuccess;
+  bool ok = hipGetDevice(&g->dev) == hipSuccess && hipStreamCreateWithFlags(&g->cap, hipStreamNonBlocking) == hipSuccess;
   for (int i = 0; ok && i < 2; ++i) ok = hipEventCreateWithFlags(&g->done[i], hipEventDisableTiming) == hipSuccess;
   if (!ok) {
     vg_hgen_graph_destroy(g);
@@ -354,6 +355,8 @@ extern "C" int vg_hgen_sweep_graphed(void* handle, const vg_hgen_model* model, c
                                      void* stream) {
   HgenGraph* G = static_cast<HgenGraph*>(handle);
   if (!G || !model || !batch || !arena) return VG_EINVAL;
+  int cur = -1;  // captured on the handle's stream, launched on the caller's: one device for both
+  if (hipGetDevice(&cur) != hipSuccess || cur != G->dev) return VG_EINVAL;
   const int64_t need = vg_hgen_arena_bytes(model, batch);
   if (need < 0) return static_cast<int>(need);
   if (arena_bytes < need || (reinterpret_cast<uintptr_t>(arena) & 255)) return VG_EINVAL;

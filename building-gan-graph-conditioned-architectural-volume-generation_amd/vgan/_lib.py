@@ -233,6 +233,10 @@ SIGNATURES = {
     "vg_gat_ring_plan": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p]),
     "vg_gat_aggregate_fwd_ring": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p,
                                                  _c_p, _c_p, _c_p, _c_p]),
+    "vg_gat_ring_tile_rows": (_c_i32, []),
+    "vg_gat_ring_gnp_floats": (_c_i64, [_c_i32, _c_i32]),
+    "vg_gat_aggregate_fwd_ring_gnp": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32,
+                                                     _c_p, _c_p, _c_p, _c_i32, _c_p, _c_p, _c_p]),
     "vg_gat_aggregate_fwd_lds": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p,
                                                 _c_p, _c_p, _c_i32, _c_p]),
     "vg_gat_jvp2_plan": (ctypes.c_int, [_c_p] * 5 + [_c_i32] * 3 + [_c_p] * 8 + [_c_f32] + [_c_p] * 7 + [_c_p] * 4),

@@ -117,6 +117,8 @@ def _build(local_graph, voxel_graph, n_classes: int) -> Prepared:
     else:
         csr = ops.CSR(voxel_graph.edge_index, n)
     csr.ell()  # the padded column array before any graph capture (one host sync unless the degree is known)
+    if csr.num_nodes >= ops.RING_MIN_ROWS:
+        csr.ring_on(64)  # large graphs: the LDS ring's tile plan measured before any capture (one host sync)
     mv = torch.empty(n, fl + fv, dtype=torch.float32, device=vx.device)
     ops.type_mean(lx, local_graph.type, voxel_graph.type, n_classes, out=mv, col0=0)
     mv[:, fl:].copy_(vx)

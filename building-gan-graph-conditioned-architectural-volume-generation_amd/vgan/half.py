@@ -262,6 +262,10 @@ class HalfGenerator:
         vx, mx = prep.voxel_x.contiguous(), prep.matched_x.contiguous()
         csr = prep.csr
         n = int(vx.shape[0])
+        for name, t in (("taus", taus), ("voxel_x", vx), ("matched_x", mx), ("csr.row_ptr", csr.row_ptr),
+                        ("csr.col", csr.col)):
+            if t.device != dev:  # raw pointers go to device kernels: a host or other-device tensor is refused
+                raise ValueError(f"sweep_labels: {name} is on {t.device}, the generator on {dev}")
         tt = taus.reshape(-1).to(torch.float32).contiguous()
         if tt.numel() != copies:
             raise ValueError("one temperature per stacked copy")
@@ -279,20 +283,24 @@ class HalfGenerator:
         arena = self.__dict__.get("_arena")
         if arena is None or arena.numel() < need:
             # earlier arenas stay alive: a captured sweep graph may still replay on them
-            self.__dict__.setdefault("_old_arenas", []).append(arena)
+            if arena is not None:
+                self.__dict__.setdefault("_old_arenas", []).append(arena)
             arena = self._arena = torch.empty(need + need // 4, dtype=torch.uint8, device=dev)
         labels = torch.empty(copies, n, dtype=torch.int8, device=dev)
         if logits is not None and (logits.dtype != torch.float32 or not logits.is_contiguous() or
                                    logits.numel() != copies * n * self.head[2]):
             raise ValueError("logits must be a contiguous f32 [copies * N, classes] tensor")
         lg = None if logits is None else logits.data_ptr()
-        if (_GRAPH if graph is None else graph) and not torch.cuda.is_current_stream_capturing():
-            check(LIB.vg_hgen_sweep_graphed(self._graph_handle(), ctypes.byref(md), ctypes.byref(bt),
-                                            arena.data_ptr(), arena.numel(), labels.data_ptr(), lg,
-                                            stream_handle(dev)), "vg_hgen_sweep_graphed")
-        else:
-            check(LIB.vg_hgen_sweep(ctypes.byref(md), ctypes.byref(bt), arena.data_ptr(), arena.numel(),
-                                    labels.data_ptr(), lg, stream_handle(dev)), "vg_hgen_sweep")
+        # the generator's device is current for the native calls: the graph
+        # handle's capture stream belongs to the device current at its creation
+        with torch.cuda.device(dev):
+            if (_GRAPH if graph is None else graph) and not torch.cuda.is_current_stream_capturing():
+                check(LIB.vg_hgen_sweep_graphed(self._graph_handle(), ctypes.byref(md), ctypes.byref(bt),
+                                                arena.data_ptr(), arena.numel(), labels.data_ptr(), lg,
+                                                stream_handle(dev)), "vg_hgen_sweep_graphed")
+            else:
+                check(LIB.vg_hgen_sweep(ctypes.byref(md), ctypes.byref(bt), arena.data_ptr(), arena.numel(),
+                                        labels.data_ptr(), lg, stream_handle(dev)), "vg_hgen_sweep")
         return labels
 
     def _graph_handle(self) -> int:
@@ -300,7 +308,8 @@ class HalfGenerator:
         this object (after their last launches complete)."""
         h = self.__dict__.get("_hgraph")
         if h is None:
-            h = LIB.vg_hgen_graph_create()
+            with torch.cuda.device(self.device):  # the capture stream is made on the current device
+                h = LIB.vg_hgen_graph_create()
             if not h:
                 raise RuntimeError("vg_hgen_graph_create failed")
             self._hgraph = h

@@ -24,6 +24,7 @@ import os
 import queue
 import sys
 import threading
+import time
 from typing import Iterator, List, Optional, Sequence, Tuple
 
 import torch
@@ -57,7 +58,8 @@ class GraphLoader:
     def __init__(self, store: GraphStore, indices: Optional[Sequence[int]] = None, batch_size: int = 1,
                  shuffle: bool = True, drop_last: bool = False, device=None, prefetch: int = 2,
                  threads: int = 4, rank: int = 0, world_size: int = 1, seed: Optional[int] = None,
-                 even: bool = True, resident: bool = False, prepare=None, workers: int = 1):
+                 even: bool = True, resident: bool = False, prepare=None, workers: int = 1,
+                 phase_stats: Optional[dict] = None):
         """``rank`` / ``world_size``: data-parallel sharding -- every rank draws
         the same epoch plan and takes batches rank, rank + world, ... of it, so
         ranks see disjoint buildings (weak scaling, one batch of
@@ -79,6 +81,11 @@ class GraphLoader:
         columns, the critic's stacked graph, the type-matched mean, the float
         one-hot, the critic's seeds), built by the host collate and uploaded
         with the batch in its one host-to-device copy.
+
+        ``phase_stats`` (a dict): host seconds accumulated per phase of the
+        prefetching pipeline -- ``collate`` and ``upload_issue`` on the worker
+        threads, ``queue_wait`` (the consumer waiting for a collated batch) and
+        ``upload_wait`` (for its copy) on the consumer's -- plus ``batches``.
 
         ``resident``: the first epoch's batches stay on the device and every
         later epoch yields the same batch objects in the same order (no
@@ -110,6 +117,7 @@ class GraphLoader:
         self._resident_batches: Optional[List[Tuple[GraphBatch, GraphBatch]]] = None
         self.prepare = prepare
         self.workers = max(1, int(workers))
+        self.phase_stats = phase_stats
 
     def __len__(self) -> int:
         n = len(self.indices)
@@ -148,7 +156,8 @@ class GraphLoader:
         if dev is None or dev.type != "cuda":
             it = (self.store.collate(idx, pin=False, threads=self.threads, prepare=self.prepare) for idx in plan)
         else:
-            it = _prefetched(self.store, plan, dev, self.prefetch, self.threads, self.prepare, self.workers)
+            it = _prefetched(self.store, plan, dev, self.prefetch, self.threads, self.prepare, self.workers,
+                             self.phase_stats)
         for pair in it:
             if kept is not None:
                 kept.append(pair)
@@ -182,8 +191,19 @@ def _switch_exit() -> None:
 
 
 def _prefetched(store: GraphStore, plan: List[List[int]], dev: torch.device, depth: int, threads: int,
-                prepare=None, workers: int = 1):
+                prepare=None, workers: int = 1, stats: Optional[dict] = None):
     copy_stream = torch.cuda.Stream(device=dev)
+    clock = time.perf_counter
+    if stats is not None:
+        for k in ("collate", "upload_issue", "queue_wait", "upload_wait", "batches"):
+            stats.setdefault(k, 0.0)
+        stats_lock = threading.Lock()
+
+    def add(key: str, t0: float) -> float:  # seconds since t0 into stats[key]; returns now
+        t1 = clock()
+        with stats_lock:  # the caller may clear the dict between steps
+            stats[key] = stats.get(key, 0.0) + t1 - t0
+        return t1
     nw = max(1, min(int(workers), len(plan) or 1))
     # worker w collates batches w, w + nw, ...; its own queue keeps them in plan order
     qs: List["queue.Queue"] = [queue.Queue(maxsize=max(1, -(-depth // nw))) for _ in range(nw)]
@@ -196,11 +216,16 @@ def _prefetched(store: GraphStore, plan: List[List[int]], dev: torch.device, dep
             for idx in plan[w::nw]:
                 if stop.is_set():
                     return
+                t0 = clock() if stats is not None else 0.0
                 host = store.collate(idx, pin=True, threads=threads, prepare=prepare)
+                if stats is not None:
+                    t0 = add("collate", t0)
                 with torch.cuda.stream(copy_stream):
                     moved = upload_pair(*host, dev, non_blocking=True)  # one copy of the pair's buffer
                     ev = torch.cuda.Event()
                     ev.record(copy_stream)
+                if stats is not None:
+                    add("upload_issue", t0)
                 q.put((moved, host, ev))  # host buffers stay referenced until the copy is waited on
             q.put(_END)
         except BaseException as exc:  # surfaced on the consumer thread
@@ -219,7 +244,10 @@ def _prefetched(store: GraphStore, plan: List[List[int]], dev: torch.device, dep
         th.start()
     try:
         for i in range(len(plan) + 1):
+            t0 = clock() if stats is not None else 0.0
             item = qs[i % nw].get()
+            if stats is not None:
+                t0 = add("queue_wait", t0)
             if item is _END:
                 return
             if isinstance(item, BaseException):
@@ -231,6 +259,9 @@ def _prefetched(store: GraphStore, plan: List[List[int]], dev: torch.device, dep
             # batch, which took the fresh-batch step to 7.72-8.36 ms against
             # 7.69-7.71 (profiles/r04_loader_wait_ab.txt)
             ev.synchronize()
+            if stats is not None:
+                add("upload_wait", t0)
+                stats["batches"] = stats.get("batches", 0.0) + 1
             for g in moved:  # the consumer stream now owns these allocations
                 for t in _tensors(g):
                     t.record_stream(torch.cuda.current_stream(dev))

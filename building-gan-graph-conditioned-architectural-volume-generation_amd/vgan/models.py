@@ -130,6 +130,7 @@ class GATEncoder(nn.Module):
             h = conv(x, csr)
             keep = rng.keep_mask(h.shape, self.dropout, h.device) if self.training else None
             x = ops.graphnorm_relu_dropout(h, norm.weight, norm.bias, norm.mean_scale, keep, norm.eps, segments)
+        _ring_checked(csr)
         return x
 
 
@@ -208,7 +209,16 @@ class GATEncoder(nn.Module):
                                            None, *drop, float(norm.eps), ptr(y), None, ptr(stats), ptr(gnp), g, st),
                   "vg_graphnorm_fwd_gnp")
             x = y
+        _ring_checked(csr)
         return x
+
+
+def _ring_checked(csr: ops.CSR) -> None:
+    """After an encoder forward that aggregated on the LDS ring (large graphs,
+    ops.CSR.ring_on): raise if one of its bounded hand-over waits expired --
+    one host sync per such forward, none inside a stream capture."""
+    if csr.__dict__.pop("_ring_used", False) and not torch.cuda.is_current_stream_capturing():
+        csr.ring_check()
 
 
 def _mlp(widths: List[int], norm: bool, act) -> MLP:

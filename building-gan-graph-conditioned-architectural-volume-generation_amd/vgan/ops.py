@@ -35,6 +35,16 @@ SOFTMAX_EPS = 1e-16
 # (A/B knob for the padded column array, CSR.ell)
 _ELL = os.environ.get("VGAN_ELL", "1") == "1"
 ELL_WIDTHS = (8, 16, 32)
+# Large graphs aggregate on the wave-specialised LDS ring (vg_gat_aggregate_fwd_ring
+# and its _gnp form) when the graph has at least
+# VGAN_RING_MIN_ROWS rows and its tile plan stages at least VGAN_RING_MIN_STAGED
+# of the 64-row tiles (voxels numbered in lattice blocks, vgan.locality.blocked;
+# the reference's row-major numbering stages almost none and keeps the register
+# gather).  VGAN_RING=0: never.
+_RING = os.environ.get("VGAN_RING", "1") == "1"
+RING_MIN_ROWS = int(os.environ.get("VGAN_RING_MIN_ROWS", "131072"))
+RING_MIN_STAGED = float(os.environ.get("VGAN_RING_MIN_STAGED", "0.9"))
+RING_TILE_ROWS = int(LIB.vg_gat_ring_tile_rows())
 
 
 # --------------------------------------------------------------------- CSR
@@ -193,9 +203,10 @@ class CSR:
         return (self.num_nodes + 63) // 64
 
     def ring_plan(self) -> torch.Tensor:
-        """The ring aggregation's tile plan (vg_gat_ring_plan: per 32-row tile
-        the distinct sources and every edge's LDS slot), built once and
-        cached; consumed by vg_gat_aggregate_fwd_ring."""
+        """The ring aggregation's tile plan (vg_gat_ring_plan: per
+        RING_TILE_ROWS-row tile the distinct sources -- -1 for a tile left to
+        global memory -- and every edge's LDS slot), built once and cached;
+        consumed by vg_gat_aggregate_fwd_ring."""
         plan = self.__dict__.get("_ring_plan")
         if plan is None:
             n_ints = int(LIB.vg_gat_ring_plan_ints(self.num_nodes, self.num_edges))
@@ -206,12 +217,68 @@ class CSR:
         return plan
 
 
+    def ring_staged(self) -> float:
+        """Fraction of the ring plan's tiles staged through LDS (built once,
+        one host sync per graph; taken by data.prepared before any capture)."""
+        frac = self.__dict__.get("_ring_staged")
+        if frac is None:
+            tiles = -(-self.num_nodes // RING_TILE_ROWS)
+            frac = float((self.ring_plan()[:tiles] > 0).sum().item()) / tiles
+            self._ring_err = torch.zeros(1, dtype=torch.int32, device=self.device)
+            self._ring_staged = frac
+        return frac
+
+    def ring_on(self, c: int) -> bool:
+        """True when the aggregation over this graph at ``c`` channels runs on
+        the LDS ring (vg_gat_aggregate_fwd_ring[_gnp]): C = 64 / 128, at least
+        RING_MIN_ROWS rows, GraphNorm segments of whole tiles, and a plan that
+        stages at least RING_MIN_STAGED of the tiles.  A graph whose plan has
+        not been measured yet is measured now -- outside a stream capture; a
+        capture keeps the register gather for it."""
+        if not _RING or c not in (64, 128) or self.num_nodes < RING_MIN_ROWS:
+            return False
+        if self.seg_rows != self.num_nodes and self.seg_rows % RING_TILE_ROWS:
+            return False  # stacked segments must be whole tiles
+        if "_ring_staged" not in self.__dict__ and torch.cuda.is_current_stream_capturing():
+            return False
+        return self.ring_staged() >= RING_MIN_STAGED
+
+    def ring_check(self) -> None:
+        """Raise if a ring aggregation over this graph expired a hand-over wait
+        (its output is then invalid; one host sync).  GATEncoder.forward calls
+        it after a forward that dispatched the ring, outside captures."""
+        err = self.__dict__.get("_ring_err")
+        if err is not None and int(err.item()) != 0:
+            raise RuntimeError("vg_gat_aggregate_fwd_ring: a hand-over wait expired (output invalid)")
+
+
 def aggregate_fwd_raw(csr: "CSR", c: int, h, a_src, a_dst, bias, slope: float, out, alpha, stream,
                       gnp=None) -> None:
     """vg_gat_aggregate_fwd over raw device pointers (ctypes), through the
     padded column array when the graph has one (vg_gat_aggregate_fwd_ell);
     bit-identical either way.  gnp (``gnp_buffer``): also the following
-    GraphNorm's column partials (vg_gat_aggregate_fwd_gnp)."""
+    GraphNorm's column partials (vg_gat_aggregate_fwd_gnp).  Large graphs
+    whose plan stages most tiles (CSR.ring_on) run the LDS ring instead
+    (vg_gat_aggregate_fwd_ring, bit-identical output and alpha; with gnp its
+    _gnp form, whose partials cover 64-row tiles -- gnp_buffer sized them)."""
+    if csr.ring_on(c):
+        if (h | out | bias) & 15:
+            if gnp is not None:  # the buffer holds 64-row partials: no other kernel may fill it
+                raise ValueError("ring aggregation: h, out and bias must be 16-byte aligned")
+        else:
+            if gnp is not None:
+                check(LIB.vg_gat_aggregate_fwd_ring_gnp(ptr(csr.row_ptr), ptr(csr.col), csr.num_nodes, c, h, a_src,
+                                                        a_dst, bias, float(slope), out, alpha, ptr(csr.ring_plan()),
+                                                        csr.seg_rows, ptr(gnp), ptr(csr._ring_err), stream),
+                      "vg_gat_aggregate_fwd_ring_gnp")
+            else:
+                check(LIB.vg_gat_aggregate_fwd_ring(ptr(csr.row_ptr), ptr(csr.col), csr.num_nodes, c, h, a_src, a_dst,
+                                                    bias, float(slope), out, alpha, ptr(csr.ring_plan()),
+                                                    ptr(csr._ring_err), stream), "vg_gat_aggregate_fwd_ring")
+            csr._ring_used = True
+            global RING_DISPATCHES
+            RING_DISPATCHES += 1
+            return
     ell, w = csr.ell()
     if gnp is not None:
         check(LIB.vg_gat_aggregate_fwd_gnp(ptr(csr.row_ptr), ptr(csr.col), ptr(ell) if ell is not None else None,
@@ -235,12 +302,20 @@ def aggregate_fwd_raw(csr: "CSR", c: int, h, a_src, a_dst, bias, slope: float, o
 _GN_FWD_FUSE = os.environ.get("VGAN_GN_FWD_FUSE", "1") == "1"
 
 
+# ring aggregations dispatched by aggregate_fwd_raw (tests assert the model path takes it)
+RING_DISPATCHES = 0
+
+
 def gnp_buffer(csr: "CSR", c: int, device):
     """(gnp, rows per partial) for an aggregation over ``csr`` at ``c``
     channels, or (None, 0) when its workgroups would span more than two
-    GraphNorm segments."""
+    GraphNorm segments.  On the LDS ring (CSR.ring_on) the partials cover
+    its 64-row tiles (vg_gat_ring_gnp_floats, with the kernel's scratch)."""
     if not _GN_FWD_FUSE:
         return None, 0
+    if csr.ring_on(c):
+        return torch.empty(int(LIB.vg_gat_ring_gnp_floats(csr.num_nodes, c)), dtype=torch.float32,
+                           device=device), RING_TILE_ROWS
     g = int(LIB.vg_gat_gnp_rows(csr.num_nodes, c))
     if g <= 0 or csr.seg_rows < g or csr.num_nodes % csr.seg_rows:
         return None, 0

@@ -47,6 +47,7 @@ HOST_SIGNATURES = {
     "vgh_collate_rows": (ctypes.c_int, [_p, _i64, _p, _i64, _p, _i32, _p, _i32]),
     "vgh_collate_graph": (ctypes.c_int, [_p, _p, _p, _p, _i64, _p, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _p]),
     "vgh_collate_max_in_degree": (ctypes.c_int, [_p, _p, _p, _p, _i64, _p, _i32, _p]),
+    "vgh_pool_pid": (_i64, []),
     "vgh_csr_ell": (ctypes.c_int, [_p, _p, _i32, _i32, _p]),
     "vgh_csr_stacked": (ctypes.c_int, [_p, _p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p]),
     "vgh_type_mean": (ctypes.c_int, [_p, _p, _i32, _i32, _p, _i32, _i32, _p, _i32, _i32]),

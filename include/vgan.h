@@ -786,21 +786,40 @@ int vg_gat_aggregate_fwd_staged(const int32_t* row_ptr, const int32_t* col, int3
                                 const float* h, const float* a_src, const float* a_dst, const float* bias,
                                 float slope, float* out, float* alpha, const int32_t* plan, void* stream);
 
-/* The same aggregation with wave-specialised workgroups (one per CU): loader
- * waves fill a three-slot LDS ring with each 32-row tile's metadata and
- * distinct source rows (LDS-DMA, one 64-channel slice at a time) while
- * consumer waves aggregate the slots already filled out of LDS in 16-lane row
- * groups; the slots are handed over by LDS counters, no workgroup barrier.
- * Bit-identical to vg_gat_aggregate_fwd.  C = 64 or 128; h, out, bias 16-B
- * aligned; plan from vg_gat_ring_plan over the same CSR (its tile plan:
- * vg_gat_ring_plan_ints(N, E') int32s).  *err (a zeroed int32) is left
- * nonzero if a hand-over wait expired (the output is then invalid). */
+/* The same aggregation with wave-specialised workgroups (one per CU): 4 loader
+ * waves fill a two-slot LDS ring with each tile's metadata and distinct
+ * source rows (tiles of vg_gat_ring_tile_rows() = 64 destination rows;
+ * LDS-DMA, one 64-channel slice at a time) while 12 consumer waves aggregate
+ * the slots already filled out of LDS in 16-lane row groups; the slots are
+ * handed over by LDS counters, no workgroup barrier.  Bit-identical to
+ * vg_gat_aggregate_fwd.  C = 64 or 128; h, out, bias 16-B aligned; plan from
+ * vg_gat_ring_plan over the same CSR (its tile plan: vg_gat_ring_plan_ints(N,
+ * E') int32s: ucount[tiles] -- a tile's distinct sources, -1 for a tile left
+ * to global memory -- then the sources and the edges' slots).  *err (a zeroed
+ * int32) is left nonzero if a hand-over wait expired (the output is then
+ * invalid).  The drop-in's aggregation (vgan.ops.aggregate_fwd_raw)
+ * dispatches it for graphs of at least VGAN_RING_MIN_ROWS rows whose plan
+ * stages most tiles (GATConv, models.py:72 via models.py:144,242). */
 int64_t vg_gat_ring_plan_ints(int32_t num_nodes, int32_t num_edges);
 int vg_gat_ring_plan(const int32_t* row_ptr, const int32_t* col, int32_t num_nodes, int32_t num_edges,
                      int32_t* plan_out, void* stream);
+int32_t vg_gat_ring_tile_rows(void);
 int vg_gat_aggregate_fwd_ring(const int32_t* row_ptr, const int32_t* col, int32_t num_nodes, int32_t channels,
                               const float* h, const float* a_src, const float* a_dst, const float* bias, float slope,
                               float* out, float* alpha, const int32_t* plan, int32_t* err, void* stream);
+
+/* The ring aggregation with the following GraphNorm's column partials in its
+ * epilogue (as vg_gat_aggregate_fwd_gnp, models.py:73-75,193-195): gnp holds
+ * vg_gat_ring_gnp_floats(N, C) floats, 16-B aligned -- the partials (count,
+ * mean, M2) of every 64-row tile and column in the vg_gat_aggregate_fwd_gnp
+ * layout with 64-row blocks, which vg_graphnorm_stats_gnp / vg_graphnorm_fwd_gnp
+ * fold with gnp_rows = vg_gat_ring_tile_rows(), then the kernel's scratch.
+ * seg_rows: the GraphNorm segment (a multiple of the tile rows dividing N). */
+int64_t vg_gat_ring_gnp_floats(int32_t num_nodes, int32_t channels);
+int vg_gat_aggregate_fwd_ring_gnp(const int32_t* row_ptr, const int32_t* col, int32_t num_nodes, int32_t channels,
+                                  const float* h, const float* a_src, const float* a_dst, const float* bias,
+                                  float slope, float* out, float* alpha, const int32_t* plan, int32_t seg_rows,
+                                  float* gnp, int32_t* err, void* stream);
 
 /* ---- GraphNorm backward partials in the producing GEMM -------------------- */
 
@@ -1154,7 +1173,10 @@ int vg_hgen_sweep(const vg_hgen_model* model, const vg_hgen_batch* batch, void* 
  * update is refused), after the event behind that executable graph's
  * previous launch has completed.  Same results bit for bit.  A handle holds
  * the two executable graphs; vg_hgen_graph_stats reports how many were
- * instantiated and how many updated in place. */
+ * instantiated and how many updated in place.  A handle belongs to the device
+ * current at vg_hgen_graph_create (its capture stream's); vg_hgen_sweep_graphed
+ * returns VG_EINVAL when another device is current.  vg_hgen_arena_bytes
+ * returns a negative code for invalid arguments. */
 void* vg_hgen_graph_create(void);
 void vg_hgen_graph_destroy(void* handle);
 int vg_hgen_graph_stats(const void* handle, int32_t* instantiations, int32_t* updates);

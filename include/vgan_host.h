@@ -74,6 +74,12 @@ int vgh_type_mean(const float* local_x, const int64_t* local_type, int32_t n_loc
                   const int64_t* voxel_type, int32_t n_voxel, int32_t n_types, float* out, int32_t out_stride,
                   int32_t out_col0);
 
+/* The process id that owns the collate helper pool serving the calling
+ * process (the pool is created on first use, and afresh in a forked child:
+ * never the parent's, whose mutex a helper may have held at the fork).
+ * Introspection for tests. */
+int64_t vgh_pool_pid(void);
+
 #ifdef __cplusplus
 }
 #endif

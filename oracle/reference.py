@@ -33,7 +33,7 @@ from . import pyg
 def type_matched_mean(local_x, local_type, voxel_type) -> torch.Tensor:
     """models.py:122-129 -- for every voxel type present, the mean program-node
     feature of that type over the whole mini-batch (zeros if no program node)."""
-    out = torch.zeros(voxel_type.shape[0], local_x.shape[1], dtype=local_x.dtype)
+    out = torch.zeros(voxel_type.shape[0], local_x.shape[1], dtype=local_x.dtype, device=local_x.device)
     for t in torch.unique(voxel_type):
         sel = local_type == t
         if sel.sum() > 0:

@@ -22,6 +22,10 @@ step_tiny.pt      the same step for a 4-building batch and a reduced config
                   (hidden 16, GAT depth 2) -- exercises the per-building loops.
 forward_b32_f64.pt  forward_b32.pt's generator loss and G gradients in f64
                   (same models, draws and reference code; default dtype f64).
+                  Also the WGAN-GP critic loss and its second-order D
+                  gradients in f64 (the f32 job's labels and GP eps).
+forward_b32_perturbed_f64.pt  the same f64 job at forward_b32_perturbed.pt's
+                  parameters (perturb seed 3001).
 forward_b32_perturbed.pt  forward_b32.pt's outputs with every G / D parameter
                   moved off its initial value (``perturb``: GraphNorm weight /
                   bias / mean_scale in U(0.3, 1.5) / U(-0.5, 0.5) / U(0.2, 1.2),
@@ -213,14 +217,18 @@ def make_forward_b32(cfgmod, models, trainer_mod, perturb_seed=None):
     return out
 
 
-def make_forward_b32_f64(cfgmod, models, trainer_mod):
-    """forward_b32.pt's generator loss and G gradients once more, in f64: the
-    same reference code, the same f32-initialised models widened to f64
-    (exactly), the same z and Gumbel draws (f32, widened; F.gumbel_softmax
-    gets the draw injected instead of drawing in f64), every default-dtype
-    tensor the reference creates in f64.  It measures the f32 rounding error
-    of the reference's own gradients, so tests/test_b32_gpu.py can hold the
-    GPU's per parameter to a small multiple of it instead of a flat 5e-2."""
+def make_forward_b32_f64(cfgmod, models, trainer_mod, perturb_seed=None):
+    """forward_b32.pt's (perturb_seed: forward_b32_perturbed.pt's) generator
+    loss and G gradients, and its WGAN-GP critic loss and second-order D
+    gradients, once more in f64: the same reference code, the same
+    f32-initialised (and perturbed) models widened to f64 (exactly), the same
+    z and Gumbel draws (f32, widened; F.gumbel_softmax gets the draw injected
+    instead of drawing in f64), every default-dtype tensor the reference
+    creates in f64.  The critic sees the f32 job's labels (its no-grad f32
+    forward, widened) and the f32 gradient-penalty eps (torch.rand injected
+    with the f32 draw of manual_seed(2003)).  It measures the f32 rounding
+    error of the reference's own gradients, so tests/test_b32_gpu.py can hold
+    the GPU's per parameter to a small multiple of it instead of a flat bound."""
     import torch.nn.functional as F
 
     cfg = cfgmod.Configuration()
@@ -229,23 +237,37 @@ def make_forward_b32_f64(cfgmod, models, trainer_mod):
     torch.manual_seed(777)
     G = models.VoxelGNNGenerator(cfg, 17, 12)
     D = models.VoxelGNNDiscriminator(cfg, 17, 12)
+    if perturb_seed is not None:
+        gen = torch.Generator().manual_seed(perturb_seed)
+        perturb(G, gen)
+        perturb(D, gen)
     G.eval()
     D.eval()
     n = voxel.num_nodes
     torch.manual_seed(2001)
     z = torch.randn(1, n, cfg.Z_DIM)
     torch.manual_seed(2002)
+    with torch.no_grad():  # the f32 job's labels, as make_forward_b32 draws them
+        _, hard32, soft32 = G(local, voxel, z)
+    torch.manual_seed(2002)
     noise = torch.empty(n, 7).exponential_()  # the draw F.gumbel_softmax makes after manual_seed(2002)
+    torch.manual_seed(2003)
+    gp_eps = torch.rand(n, 1)  # the reference's GP draw (trainer.py:297) after manual_seed(2003), in f32
     G.double()
     D.double()
-    for key in ("x",):
-        setattr(local, key, getattr(local, key).double())
-        setattr(voxel, key, getattr(voxel, key).double())
-    real_gs = F.gumbel_softmax
+    for key in ("x", "types_onehot"):
+        for g in (local, voxel):
+            if hasattr(g, key) and torch.is_tensor(getattr(g, key)) and getattr(g, key).is_floating_point():
+                setattr(g, key, getattr(g, key).double())
+    real_gs, real_rand = F.gumbel_softmax, torch.rand
 
     def injected(logits, tau=1, hard=False, eps=1e-10, dim=-1):
         gumbels = -noise.to(logits.dtype).log()
         return ((logits + gumbels) / tau).softmax(dim)
+
+    def injected_rand(*size, **kw):
+        assert tuple(size) == (n, 1), size
+        return gp_eps.to(torch.float64)
 
     opt = torch.optim.Adam(D.parameters())
     prev = torch.get_default_dtype()
@@ -260,12 +282,30 @@ def make_forward_b32_f64(cfgmod, models, trainer_mod):
         logits_g, hard_g, _ = G(local, voxel, z.double())
         g_loss = tr._compute_generator_loss(local, voxel, logits_g, hard_g.unsqueeze(0))
         g_loss.backward()
+        g_grads = {k: p.grad.detach().clone() for k, p in G.named_parameters()}
+        G.zero_grad()
+        D.zero_grad()
+        torch.rand = injected_rand
+        try:
+            d_loss = tr._compute_discriminator_loss(local, voxel, hard32.double().unsqueeze(0),
+                                                    soft32.double().unsqueeze(0))
+            d_loss.backward()
+        finally:
+            torch.rand = real_rand
     finally:
         F.gumbel_softmax = real_gs
         torch.set_default_dtype(prev)
-    return {"batch_checksum": batch_checksum(local, voxel), "g_loss": g_loss.detach(),
-            "label_argmax": hard_g.argmax(1).to(torch.int8),
-            "g_grads": {k: p.grad.detach().clone() for k, p in G.named_parameters()}}
+    out = {"batch_checksum": batch_checksum(local, voxel), "g_loss": g_loss.detach(),
+           "label_argmax": hard_g.argmax(1).to(torch.int8), "g_grads": g_grads,
+           "d_loss": d_loss.detach(), "d_grads": {k: p.grad.detach().clone() for k, p in D.named_parameters()},
+           "label_argmax_f32": hard32.argmax(1).to(torch.int8)}
+    if perturb_seed is not None:
+        out["perturb_seed"] = perturb_seed
+    return out
+
+
+def make_forward_b32_perturbed_f64(cfgmod, models, trainer_mod):
+    return make_forward_b32_f64(cfgmod, models, trainer_mod, perturb_seed=3001)
 
 
 def batch_checksum(local, voxel):
@@ -377,6 +417,7 @@ def main():
         "forward_b32.pt": lambda: make_forward_b32(cfgmod, models, trainer_mod),
         "forward_b32_f64.pt": lambda: make_forward_b32_f64(cfgmod, models, trainer_mod),
         "forward_b32_perturbed.pt": lambda: make_forward_b32_perturbed(cfgmod, models, trainer_mod),
+        "forward_b32_perturbed_f64.pt": lambda: make_forward_b32_perturbed_f64(cfgmod, models, trainer_mod),
         "step_sanity.pt": lambda: make_step_sanity(cfgmod, models, trainer_mod),
         "step_tiny.pt": lambda: make_step_tiny(cfgmod, models, trainer_mod),
         "ops_small.pt": make_ops_small,

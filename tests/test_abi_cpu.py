@@ -139,6 +139,10 @@ def test_graphed_sweep_refuses_bad_arguments_host_only():
     a, b = ct.c_int32(7), ct.c_int32(7)
     assert lib.vg_hgen_graph_stats(None, ct.byref(a), ct.byref(b)) == VG_EINVAL
     lib.vg_hgen_graph_destroy(None)  # a NULL handle is a no-op
+    # the arena query's errors are negative, never a size a caller could allocate
+    assert lib.vg_hgen_arena_bytes(None, ct.byref(bt)) == VG_EINVAL
+    assert lib.vg_hgen_arena_bytes(ct.byref(md), None) == VG_EINVAL
+    assert lib.vg_hgen_arena_bytes(ct.byref(md), ct.byref(bt)) < 0  # an empty model: n_matched = 0
 
 
 def test_gemm_act_codes_checked_host_only():

@@ -127,9 +127,75 @@ def test_b32_generator_loss_and_grads(cuda, b32):
     assert ok, (worst, total)
 
 
+def _f64_fixture(f):
+    """The f64 run of the reference matching fixture ``f``: forward_b32_f64.pt
+    at the initial parameters, forward_b32_perturbed_f64.pt at the perturbed
+    ones (the same perturb seed)."""
+    if "G" not in f:
+        return load_fixture("forward_b32_f64.pt")
+    f64 = load_fixture("forward_b32_perturbed_f64.pt")
+    assert int(f64["perturb_seed"]) == int(f["perturb_seed"])
+    return f64
+
+
+def _per_parameter_vs_f64(named_grads, ref32, ref64, slack: float = 3.0):
+    """(worst fraction of its bound, its parameter, GPU total rel err, f32
+    reference total rel err): each parameter's GPU gradient error against the
+    f64 reference held to ``slack`` x the f32 reference's own error + 2e-3 of
+    the parameter's gradient + 1e-6 of the whole gradient (the floor for the
+    exactly-zero GAT biases at init)."""
+    ref64 = {k: v.double() for k, v in ref64.items()}
+    scale = float(torch.cat([v.reshape(-1) for v in ref64.values()]).norm())
+    worst, worst_k, tot_g, tot_c = 0.0, None, 0.0, 0.0
+    for k, g in named_grads:
+        r = ref64[k]
+        e_gpu = float((g.detach().double().cpu() - r).norm())
+        e_cpu = float((ref32[k].double() - r).norm())
+        tot_g += e_gpu ** 2
+        tot_c += e_cpu ** 2
+        lim = slack * e_cpu + 2e-3 * float(r.norm()) + 1e-6 * scale
+        if e_gpu / lim > worst:
+            worst, worst_k = e_gpu / lim, k
+    return worst, worst_k, tot_g ** 0.5 / scale, tot_c ** 0.5 / scale
+
+
+def test_b32_critic_grads_against_f64_reference(cuda, b32):
+    """The WGAN-GP critic's second-order D gradient per parameter against the
+    reference's own code run in f64 (forward_b32[_perturbed]_f64.pt: the same
+    models, the f32 job's labels and gradient-penalty eps), at the initial and
+    the trained-like parameters: each parameter within 3x the f32 reference's
+    own error + 2e-3 of its gradient, the whole within the reference's error +
+    2e-3.  Match: trainer.py:291-332 (the GP with create_graph=True),
+    models.py:229-245."""
+    f, inp = b32
+    f64 = _f64_fixture(f)
+    assert torch.equal(f64["batch_checksum"], f["batch_checksum"])
+    assert torch.equal(f64["label_argmax_f32"], f["label_argmax"])
+    cfg = Configuration()
+    G, D = _models(cfg, f)
+    G.eval()
+    D.eval()
+    loc, vox = inp["vgan"]
+    ref_hard = torch.nn.functional.one_hot(f["label_argmax"].long(), 7).float().to(cuda)
+    ref_hard = ref_hard - f["label_soft"].to(cuda) + f["label_soft"].to(cuda)
+    tr = Trainer(G, D, None, None, None, None, cfg)
+    tr.rng = _FixedUniform(inp["gp_eps"].to(cuda))
+    tr.adam_d.zero_grad()
+    d_loss = tr._critic_loss_backward(loc, vox, ref_hard.unsqueeze(0), f["label_soft"].to(cuda).unsqueeze(0))
+    ref64 = float(f64["d_loss"])
+    assert abs(d_loss.item() - ref64) <= 1e-5 * abs(ref64), (d_loss.item(), ref64)
+    worst, worst_k, tot_g, tot_c = _per_parameter_vs_f64(((k, p.grad) for k, p in D.named_parameters()),
+                                                         f["d_grads"], f64["d_grads"])
+    print(f"batch 32 vs f64 reference: D gradient rel err GPU {tot_g:.2e}, f32 reference {tot_c:.2e}; "
+          f"worst parameter {worst_k} at {worst:.2f} of its bound")
+    assert worst <= 1.0, (worst_k, worst)
+    assert tot_g <= tot_c + 2e-3
+
+
 def test_b32_generator_grads_against_f64_reference(cuda, b32):
     """The G gradient per parameter against the reference's own code run in
-    f64 (tests/golden/forward_b32_f64.pt: same models, draws and labels --
+    f64 (tests/golden/forward_b32_f64.pt, forward_b32_perturbed_f64.pt at the
+    trained-like parameters: same models, draws and labels --
     no argmax differs).  The f32 reference is itself 0.7% off that overall and
     up to ~25% on single parameters (a GraphNorm mean_scale column sum that
     cancels over 12.7k rows); the GPU is held, per parameter, to three times
@@ -138,12 +204,8 @@ def test_b32_generator_grads_against_f64_reference(cuda, b32):
     overall to the reference's error plus 2e-3.  A bug in one small parameter
     group shows as an error far above the f32 reference's, which the flat
     5e-2 of test_b32_generator_loss_and_grads would not catch."""
-    from parity_util import load_fixture
-
     f, inp = b32
-    if "G" in f:
-        pytest.skip("the f64 reference fixture is at the initial parameters")
-    f64 = load_fixture("forward_b32_f64.pt")
+    f64 = _f64_fixture(f)
     assert torch.equal(f64["batch_checksum"], f["batch_checksum"])
     assert torch.equal(f64["label_argmax"], f["label_argmax"])
     cfg = Configuration()
@@ -156,24 +218,13 @@ def test_b32_generator_grads_against_f64_reference(cuda, b32):
     logits, hard, _ = G(loc, vox, inp["z"].to(cuda), noise=inp["noise"].to(cuda))
     g_loss = tr._compute_generator_loss(loc, vox, logits, hard.unsqueeze(0))
     g_loss.backward()
-    ref64 = {k: v.double() for k, v in f64["g_grads"].items()}
-    scale = float(torch.cat([v.reshape(-1) for v in ref64.values()]).norm())
-    worst, worst_k, tot_g, tot_c = 0.0, None, 0.0, 0.0
-    for k, p in G.named_parameters():
-        r = ref64[k]
-        e_gpu = float((p.grad.detach().double().cpu() - r).norm())
-        e_cpu = float((f["g_grads"][k].double() - r).norm())
-        tot_g += e_gpu ** 2
-        tot_c += e_cpu ** 2
-        # 3x: the mean_scale gradients are -mu w A / d with mu and A cancelling
-        # column sums over 12.7k rows; their f32 error depends on the summation
-        # tree (GPU tiles + folds vs the CPU's vectorised pairwise sums) and
-        # measured up to 2.2x the reference's own at the round-5 fixture
-        # (encoder.module_13.mean_scale); a wrong formula is off by far more
-        lim = 3.0 * e_cpu + 2e-3 * float(r.norm()) + 1e-6 * scale
-        if e_gpu / lim > worst:
-            worst, worst_k = e_gpu / lim, k
-    tot_g, tot_c = tot_g ** 0.5 / scale, tot_c ** 0.5 / scale
+    # 3x: the mean_scale gradients are -mu w A / d with mu and A cancelling
+    # column sums over 12.7k rows; their f32 error depends on the summation
+    # tree (GPU tiles + folds vs the CPU's vectorised pairwise sums) and
+    # measured up to 2.2x the reference's own at the round-5 fixture
+    # (encoder.module_13.mean_scale); a wrong formula is off by far more
+    worst, worst_k, tot_g, tot_c = _per_parameter_vs_f64(((k, p.grad) for k, p in G.named_parameters()),
+                                                         f["g_grads"], f64["g_grads"])
     print(f"batch 32 vs f64 reference: G gradient rel err GPU {tot_g:.2e}, f32 reference {tot_c:.2e}; "
           f"worst parameter {worst_k} at {worst:.2f} of its bound")
     assert worst <= 1.0, (worst_k, worst)

@@ -196,34 +196,59 @@ def test_oracle_matches_reference_at_batch_32(name):
         assert torch.equal(p.grad, f["g_grads"][k]), k
 
 
-def test_oracle_matches_f64_reference_at_batch_32():
-    """The restatement run in f64 (the f32-initialised models widened, the same
-    draws) against the reference's own code run in f64
-    (forward_b32_f64.pt): generator loss and every G gradient to f64
-    rounding -- the baseline tests/test_b32_gpu.py measures f32 errors from."""
+@pytest.mark.parametrize("name,f64name", [("forward_b32.pt", "forward_b32_f64.pt"),
+                                           ("forward_b32_perturbed.pt", "forward_b32_perturbed_f64.pt")])
+def test_oracle_matches_f64_reference_at_batch_32(name, f64name):
+    """The restatement run in f64 (the f32-initialised -- and, for the
+    perturbed fixture, perturbed -- models widened, the same draws) against
+    the reference's own code run in f64 (forward_b32[_perturbed]_f64.pt): the
+    generator loss and every G gradient, the WGAN-GP critic loss (on the f32
+    forward's labels and the f32 GP eps, as the f64 job feeds it) and every
+    second-order D gradient, to f64 rounding -- the baseline
+    tests/test_b32_gpu.py measures f32 errors from."""
     from parity_util import b32_inputs
 
-    f = load_fixture("forward_b32.pt")
-    f64 = load_fixture("forward_b32_f64.pt")
+    f = load_fixture(name)
+    f64 = load_fixture(f64name)
+    assert torch.equal(f64["batch_checksum"], f["batch_checksum"])
     inp = b32_inputs(f, device=None)
     local, voxel = inp["oracle"]
-    local.x, voxel.x = local.x.double(), voxel.x.double()
     cfg = Configuration()
     torch.manual_seed(int(f["init_seed"]))
-    G, D = R.Generator(cfg).double(), R.Discriminator(cfg).double()
+    G, D = R.Generator(cfg), R.Discriminator(cfg)
+    if "G" in f:
+        G.load_state_dict(f["G"])
+        D.load_state_dict(f["D"])
     G.eval()
     D.eval()
+    with torch.no_grad():
+        _, hard32, soft32 = G(local, voxel, inp["z"], noise=inp["noise"])
+    assert torch.equal(hard32.argmax(1).to(torch.int8), f64["label_argmax_f32"])
+    G, D = G.double(), D.double()
+    local.x, voxel.x = local.x.double(), voxel.x.double()
+    voxel.types_onehot = voxel.types_onehot.double()
     prev = torch.get_default_dtype()
     torch.set_default_dtype(torch.float64)
     try:
         logits, hard, _ = G(local, voxel, inp["z"].double(), noise=inp["noise"].double())
         g_loss = R.generator_loss(D, cfg, local, voxel, logits, hard.unsqueeze(0))
         g_loss.backward()
+        g_grads = {k: p.grad.clone() for k, p in G.named_parameters()}
+        G.zero_grad()
+        D.zero_grad()
+        d_real = D(local, voxel, voxel.types_onehot.unsqueeze(0))
+        d_fake = D(local, voxel, hard32.double().unsqueeze(0))
+        d_loss = d_fake.mean() - d_real.mean() + R.gradient_penalty(D, cfg, local, voxel,
+                                                                     soft32.double().unsqueeze(0),
+                                                                     eps=inp["gp_eps"].double())
+        d_loss.backward()
     finally:
         torch.set_default_dtype(prev)
     assert torch.equal(hard.argmax(1).to(torch.int8), f64["label_argmax"])
-    assert abs(float(g_loss) - float(f64["g_loss"])) <= 1e-12 * abs(float(f64["g_loss"]))
-    scale = float(torch.cat([v.reshape(-1) for v in f64["g_grads"].values()]).norm())
-    for k, p in G.named_parameters():
-        want = f64["g_grads"][k]
-        assert float((p.grad - want).norm()) <= 1e-9 * float(want.norm()) + 1e-12 * scale, k
+    for loss, want in ((g_loss, f64["g_loss"]), (d_loss, f64["d_loss"])):
+        assert abs(float(loss) - float(want)) <= 1e-12 * abs(float(want))
+    for got, want_all in ((g_grads, f64["g_grads"]), ({k: p.grad for k, p in D.named_parameters()}, f64["d_grads"])):
+        scale = float(torch.cat([v.reshape(-1) for v in want_all.values()]).norm())
+        for k, g in got.items():
+            want = want_all[k]
+            assert float((g - want).norm()) <= 1e-9 * float(want.norm()) + 1e-12 * scale, k

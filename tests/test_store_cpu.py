@@ -375,3 +375,48 @@ def test_prefetch_switch_interval_restored_after_the_last_prefetcher():
     assert sys.getswitchinterval() == low
     loader._switch_exit()
     assert sys.getswitchinterval() == base
+
+
+def test_collate_pool_survives_fork(tmp_path):
+    """libvgan_host's persistent helper pool is per process: a child forked
+    after the parent's helpers started (one may hold the pool's mutex at the
+    fork) gets a fresh pool on its first collate instead of deadlocking on
+    the parent's, and its result is the parent's (csrc/collate.cpp Pool::get)."""
+    import signal
+    import time
+
+    from vgan import store, synth
+
+    ds = synth.SyntheticDataset(96, seed=5)
+    st = store.write_store(str(tmp_path / "s"), ds)
+    idx = list(range(96))
+    want = st.collate(idx, threads=4)  # past 64k items of work: helper threads start
+    st.collate(idx, threads=4)
+    from vgan.store import host_lib
+
+    assert host_lib().vgh_pool_pid() == os.getpid()
+    pid = os.fork()
+    if pid == 0:  # child: collate with the pool it inherited, compare, exit without cleanup
+        ok = 1
+        try:
+            from vgan.store import host_lib
+
+            got = st.collate(idx, threads=4)
+            if host_lib().vgh_pool_pid() != os.getpid():
+                os._exit(3)  # served by the parent's pool
+            # numpy comparisons: torch's CPU thread pool is not fork-safe
+            ok = 0 if all(np.array_equal(getattr(a, k).numpy(), getattr(b, k).numpy()) for a, b in zip(got, want)
+                          for k in a.keys() if torch.is_tensor(getattr(a, k))) else 2
+        finally:
+            os._exit(ok)
+    deadline = time.time() + 60
+    while True:
+        done, status = os.waitpid(pid, os.WNOHANG)
+        if done:
+            break
+        if time.time() > deadline:
+            os.kill(pid, signal.SIGKILL)
+            os.waitpid(pid, 0)
+            pytest.fail("the forked child's collate hung")
+        time.sleep(0.05)
+    assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0, status

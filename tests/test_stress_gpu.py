@@ -167,7 +167,7 @@ def test_ring_aggregation_ragged_graph_bitwise(cuda, C):
     """The wave-specialised ring kernel on a graph that exercises its other
     paths: a ragged last tile (N % 64 != 0), rows with no in-edges, hub rows
     longer than 64 edges (their tiles aggregated from global memory) and tiles
-    with more distinct sources than the ring's 192-row image -- bit-identical to the
+    with more distinct sources than the ring's 288-row image -- bit-identical to the
     register kernel, with the hand-over flag untouched."""
     from vgan import ops
 
@@ -188,6 +188,85 @@ def test_ring_aggregation_ragged_graph_bitwise(cuda, C):
     ref_out, ref_alpha = _run("register", csr, C, h, a_s, a_d, b)
     out, alpha = _run("ring", csr, C, h, a_s, a_d, b)
     torch.cuda.synchronize()
-    ucount = csr.ring_plan()[:(n + 31) // 32].cpu()
+    ucount = csr.ring_plan()[:-(-n // LIB.vg_gat_ring_tile_rows())].cpu()  # the plan's per-tile counts
     assert (ucount < 0).any() and (ucount > 0).any()  # both tile kinds ran
     assert torch.equal(out, ref_out) and torch.equal(alpha, ref_alpha)
+
+
+def _ragged_graph(n, seed):
+    g = torch.Generator().manual_seed(seed)
+    e_loc = torch.randint(0, 40, (2, 6 * n), generator=g)
+    e_loc[1] = (e_loc[0] + torch.randint(0, 40, (6 * n,), generator=g)) % n
+    e_loc[0] = (e_loc[0] * 97 + torch.randint(0, n, (6 * n,), generator=g) // 50) % n
+    hubs = torch.stack([torch.randint(0, n, (300,), generator=g), torch.full((300,), 7)])  # a 300-edge row
+    return torch.cat([e_loc, hubs], 1)
+
+
+def _tile_partials_f64(out, rt, seg_rows):
+    """(n, mean, M2) of every rt-row block of every segment, per column, f64."""
+    x = out.double().cpu()
+    rows, c = x.shape
+    res = []
+    for s0 in range(0, rows, seg_rows):
+        for r0 in range(s0, s0 + seg_rows, rt):
+            blk = x[r0:min(r0 + rt, s0 + seg_rows)]
+            mu = blk.mean(0)
+            res.append((blk.shape[0], mu, ((blk - mu) ** 2).sum(0)))
+    return res
+
+
+@pytest.mark.parametrize("C", [64, 128])
+@pytest.mark.parametrize("shape", ["ragged", "stacked3"])
+def test_ring_gnp_partials_and_statistics(cuda, C, shape):
+    """vg_gat_aggregate_fwd_ring_gnp: output and alpha bit-identical to the
+    register kernel; every 64-row tile's (count, mean, M2) per column against
+    f64 of the output; the GraphNorm statistics folded from them
+    (vg_graphnorm_stats_gnp with gnp_rows = 64) against f64 column statistics
+    of each segment -- one ragged segment (N % 64 != 0, a 300-edge hub row left
+    to global memory) and three stacked copies of a 64-row-aligned graph.
+    Match: models.py:73-75 (GraphNorm after each GATConv)."""
+    rt = int(LIB.vg_gat_ring_tile_rows())
+    if shape == "ragged":
+        n = 5000 + 37
+        csr = ops.CSR(_ragged_graph(n, C).to(cuda), n)
+    else:
+        n1 = 64 * 79
+        csr = ops.CSR(_ragged_graph(n1, C + 1).to(cuda), n1).stacked(3)
+    n, seg = csr.num_nodes, csr.seg_rows
+    S = n // seg
+    torch.manual_seed(C)
+    h = torch.randn(n, C, device=cuda) * 2 + 0.5
+    a_s, a_d = 0.5 * torch.randn(n, device=cuda), 0.5 * torch.randn(n, device=cuda)
+    b = torch.randn(C, device=cuda)
+    ref_out, ref_alpha = _run("register", csr, C, h, a_s, a_d, b)
+    out, alpha = torch.empty_like(ref_out), torch.empty_like(ref_alpha)
+    gnp = torch.full((int(LIB.vg_gat_ring_gnp_floats(n, C)),), float("nan"), device=cuda)
+    err = torch.zeros(1, dtype=torch.int32, device=cuda)
+    check(LIB.vg_gat_aggregate_fwd_ring_gnp(ptr(csr.row_ptr), ptr(csr.col), n, C, ptr(h), ptr(a_s), ptr(a_d), ptr(b),
+                                            0.2, ptr(out), ptr(alpha), ptr(csr.ring_plan()), seg, ptr(gnp), ptr(err),
+                                            csr.stream()), "vg_gat_aggregate_fwd_ring_gnp")
+    ms = torch.rand(C, device=cuda) + 0.2
+    stats = torch.empty(S * 2 * C, device=cuda)
+    check(LIB.vg_graphnorm_stats_gnp(S, seg, C, ptr(gnp), rt, ptr(ms), 1e-5, ptr(stats), csr.stream()),
+          "vg_graphnorm_stats_gnp")
+    torch.cuda.synchronize()
+    assert int(err.item()) == 0
+    assert torch.equal(out, ref_out) and torch.equal(alpha, ref_alpha)
+    tiles = -(-n // rt)
+    assert (csr.ring_plan()[:tiles] < 0).any() and (csr.ring_plan()[:tiles] > 0).any()
+    part = gnp[:tiles * 2 * C * 3].view(tiles, 2, C, 3)[:, 0].double().cpu()
+    want = _tile_partials_f64(out, rt, seg)
+    assert len(want) == tiles
+    wn = torch.tensor([w[0] for w in want], dtype=torch.float64)
+    wmu = torch.stack([w[1] for w in want])
+    wm2 = torch.stack([w[2] for w in want])
+    assert torch.equal(part[:, 0, 0], wn)
+    assert rel_err(part[:, :, 1], wmu) < 1e-6
+    assert rel_err(part[:, :, 2], wm2) < 1e-5
+    x = out.double().cpu().view(S, seg, C)
+    mu = x.mean(1)
+    o = x - ms.double().cpu() * mu.unsqueeze(1)
+    d = (o.pow(2).mean(1) + 1e-5).sqrt()
+    st = stats.double().cpu().view(S, 2, C)
+    print(f"{shape} C={C}: stats rel err mean {rel_err(st[:, 0], mu):.2e}, denom {rel_err(st[:, 1], d):.2e}")
+    assert rel_err(st[:, 0], mu) < 1e-6 and rel_err(st[:, 1], d) < 1e-6
