@@ -626,44 +626,79 @@ struct RingRow {
 // GNP: the following GraphNorm's column partials (count, mean, M2) per 64-row
 // tile and 64-channel slice, in gat_fused.hip's gnp layout with 64-row blocks
 // ([tile][2][C][3], slot 0; vg_graphnorm_stats_gnp / _fwd_gnp fold them with
-// gnp_rows = 64).  A consumer unit forms its 4-row group's two-pass (mean, M2)
-// from the values it stores (xor shuffles across the wave's four 16-lane rows,
-// as gnp_block) and writes them to the workgroup's scratch [NS][Groups][2][64];
-// the slot's FREE counter (release) hands them to loader wave 0, which -- after
-// issuing the DMA that refills the slot, so the loads share its wait -- merges
-// the tile's 16 groups in group order with Chan's formula (deterministic) and
-// writes the tile partial.  The last NS items are merged after the loop.
+// gnp_rows = 64), formed by the loader waves from the output rows once a
+// slot's FREE counter says its consumers are done (ring_gnp_load / _store).
+// The loaders run NS items past their last one for the last items' partials.
+// One column partial (count, mean, M2) and Chan's merge of two, in a fixed
+// order (a then b); an empty side passes the other through
+struct RingWel {
+  float n, mu, m2;
+};
+__device__ __forceinline__ RingWel ring_chan(const RingWel& a, const RingWel& b) {
+  if (b.n <= 0.f) return a;
+  if (a.n <= 0.f) return b;
+  const float nt = a.n + b.n, fb = b.n / nt, delta = b.mu - a.mu;
+  return {nt, a.mu + delta * fb, a.m2 + b.m2 + delta * delta * a.n * fb};
+}
+// the lane 16 / 32 apart's partial by gfx950's v_permlane16_swap /
+// v_permlane32_swap (VALU, no LDS round trip; with both operands w each lane
+// gets the lower and the upper row's value), merged lower row (block) first,
+// so both lanes of a pair hold the same
+__device__ __forceinline__ RingWel ring_chan_x16(const RingWel& w) {
+  const auto n = __builtin_amdgcn_permlane16_swap(__float_as_uint(w.n), __float_as_uint(w.n), false, false);
+  const auto m = __builtin_amdgcn_permlane16_swap(__float_as_uint(w.mu), __float_as_uint(w.mu), false, false);
+  const auto q = __builtin_amdgcn_permlane16_swap(__float_as_uint(w.m2), __float_as_uint(w.m2), false, false);
+  return ring_chan({__uint_as_float(n[0]), __uint_as_float(m[0]), __uint_as_float(q[0])},
+                   {__uint_as_float(n[1]), __uint_as_float(m[1]), __uint_as_float(q[1])});
+}
+__device__ __forceinline__ RingWel ring_chan_x32(const RingWel& w) {
+  const auto n = __builtin_amdgcn_permlane32_swap(__float_as_uint(w.n), __float_as_uint(w.n), false, false);
+  const auto m = __builtin_amdgcn_permlane32_swap(__float_as_uint(w.mu), __float_as_uint(w.mu), false, false);
+  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(w.m2), __float_as_uint(w.m2), false, false);
+  return ring_chan({__uint_as_float(n[0]), __uint_as_float(m[0]), __uint_as_float(q[0])},
+                   {__uint_as_float(n[1]), __uint_as_float(m[1]), __uint_as_float(q[1])});
+}
+
+// The tile partial of item k - NS (tile t, slice sl; its consumers are done:
+// FREE) formed by the 4 loader waves from the output rows the consumers
+// wrote (L2-resident, just written): wave w takes columns 16 w .. 16 w + 15,
+// lane l column 16 w + l % 16 and rows 16 (l / 16) .. + 15 of the tile -- 16
+// loads a lane, in flight with the slot's DMA -- then an exact two-pass
+// (mean, M2) over its 16 rows, and the four lanes of a column merged by
+// permlane swaps with Chan's formula in a fixed tree (deterministic, the same
+// in every lane of the column).  The consumers do nothing extra: in their
+// epilogue the partials cost the ring ~20 % (their issue slots).
 template <class G>
-__device__ __forceinline__ void ring_gnp_load(float (&pv)[G::Groups][2], const float* __restrict__ scratch, int s,
-                                              int lane) {
-  const float* sp = scratch + ((size_t)blockIdx.x * G::NS + s) * G::Groups * 128;
+__device__ __forceinline__ void ring_gnp_load(float (&pv)[16], const float* __restrict__ out, int t, int sl, int N,
+                                              int C, int wave, int lane) {
+  const int c = sl * 64 + 16 * wave + (lane & 15), r = t * G::RT + 16 * (lane >> 4);
 #pragma unroll
-  for (int g = 0; g < G::Groups; ++g) {
-    pv[g][0] = sp[g * 128 + lane];
-    pv[g][1] = sp[g * 128 + 64 + lane];
-  }
+  for (int i = 0; i < 16; ++i) pv[i] = r + i < N ? out[(size_t)(r + i) * C + c] : 0.f;
 }
 
 template <class G>
-__device__ __forceinline__ void ring_gnp_store(const float (&pv)[G::Groups][2], int t, int sl, int N, int C, int lane,
-                                               float* __restrict__ gnp) {
-  const int r0 = t * G::RT;
-  float n = static_cast<float>(min(4, N - r0)), mu = pv[0][0], m2 = pv[0][1];
+__device__ __forceinline__ void ring_gnp_store(const float (&pv)[16], int t, int sl, int N, int C, int wave,
+                                               int lane, float* __restrict__ gnp) {
+  static_assert(G::RT == 64 && kRLW == 4, "four loader waves, 16 rows a lane");
+  const int r = t * G::RT + 16 * (lane >> 4);
+  const int n = max(0, min(16, N - r));
+  float sum = 0.f;
 #pragma unroll
-  for (int g = 1; g < G::Groups; ++g) {  // Chan's merge, group order
-    const int k = min(4, N - (r0 + 4 * g));
-    if (k > 0) {
-      const float nb = static_cast<float>(k), nt = n + nb;
-      const float delta = pv[g][0] - mu, fb = nb / nt;
-      mu += delta * fb;
-      m2 += pv[g][1] + delta * delta * n * fb;
-      n = nt;
-    }
+  for (int i = 0; i < 16; ++i) sum += i < n ? pv[i] : 0.f;
+  const float mu = n > 0 ? sum / static_cast<float>(n) : 0.f;
+  float m2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const float d = i < n ? pv[i] - mu : 0.f;
+    m2 = fmaf(d, d, m2);
   }
-  float* p = gnp + ((size_t)t * 2 * C + sl * 64 + lane) * 3;
-  p[0] = n;
-  p[1] = mu;
-  p[2] = m2;
+  const RingWel w = ring_chan_x32(ring_chan_x16({static_cast<float>(n), mu, m2}));
+  if (lane < 16) {
+    float* p = gnp + ((size_t)t * 2 * C + sl * 64 + 16 * wave + lane) * 3;
+    p[0] = w.n;
+    p[1] = w.mu;
+    p[2] = w.m2;
+  }
 }
 
 template <class G, bool GNP = false>
@@ -672,7 +707,7 @@ __global__ void __launch_bounds__(kRNT) k_gat_fwd_ring(
     const float* __restrict__ h, const float* __restrict__ a_src, const float* __restrict__ a_dst,
     const float* __restrict__ bias, float slope, float* __restrict__ out, float* __restrict__ alpha,
     const int32_t* __restrict__ ucount, const int32_t* __restrict__ usrc, const uint16_t* __restrict__ lidx,
-    int tiles, int* __restrict__ err, float* __restrict__ gnp = nullptr, float* __restrict__ scratch = nullptr) {
+    int tiles, int* __restrict__ err, float* __restrict__ gnp = nullptr) {
   extern __shared__ float4 ring4[];
   char* base = reinterpret_cast<char*>(ring4);
   int* cnt = reinterpret_cast<int*>(base + G::NS * G::SlotB);  // full[NS], free[NS], the next unit
@@ -737,16 +772,22 @@ __global__ void __launch_bounds__(kRNT) k_gat_fwd_ring(
       if (my_tiles > 1) ring_load_head<G>(hn, tb + wslot + per, N, wave, lane, row_ptr, a_dst, ucount);
     }
     float av[G::AsQ];
-    for (int k = 0; k < items; ++k) {
+    // GNP: the loaders run NS items past the last one, so the last items'
+    // group partials are merged by the same loop body as the others (a
+    // separate tail block after the loop made the whole kernel ~45 % slower:
+    // its extra live registers and code reshaped the loop)
+    const int kend = GNP ? items + G::NS : items;
+    for (int k = 0; k < kend; ++k) {
+      const bool real = k < items;
       const int s = k % G::NS, gen = k / G::NS, sl = k % slices;
       const int j = k / slices;
       const int t = tb + wslot + j * per;
-      const bool pre = sl == slices - 1 && j + 1 < my_tiles;
+      const bool pre = real && sl == slices - 1 && j + 1 < my_tiles;
       if (pre) {
         ring_load_body<G>(nxt, hn, t + per, wave, lane, usrc, lidx);
         if (j + 2 < my_tiles) ring_load_head<G>(hn, t + 2 * per, N, wave, lane, row_ptr, a_dst, ucount);
       }
-      if (sl == 0 && cur.U > 0)
+      if (real && sl == 0 && cur.U > 0)
 #pragma unroll
         for (int q = 0; q < G::AsQ; ++q) av[q] = a_src[cur.ua[q]];
       if (k >= G::NS) VG_RING_WAIT(&cnt[G::NS + s], G::Groups * gen, 1);
@@ -754,7 +795,7 @@ __global__ void __launch_bounds__(kRNT) k_gat_fwd_ring(
       const unsigned long long f0_ = __builtin_readcyclecounter();
 #endif
       RingSlot R = ring_slot<G>(base, s);
-      if (sl == 0) {  // the tile's metadata: row_ptr, a_dst, edge slots, a_src (consumers keep them per tile)
+      if (real && sl == 0) {  // the tile's metadata: row_ptr, a_dst, edge slots, a_src (consumers keep them per tile)
         if (lt <= G::RT) R.rp[lt] = cur.rp;
         if (lt < G::RT) R.ad[lt] = cur.ad;
         if (cur.U > 0) {
@@ -771,7 +812,7 @@ __global__ void __launch_bounds__(kRNT) k_gat_fwd_ring(
         }
       }
       // this slice's rows by LDS-DMA
-      if (cur.U > 0) {
+      if (real && cur.U > 0) {
         const int ni = (cur.U + 3) / 4;
 #pragma unroll
         for (int q = 0; q < G::RowI; ++q) {
@@ -783,37 +824,24 @@ __global__ void __launch_bounds__(kRNT) k_gat_fwd_ring(
           }
         }
       }
-      // GNP: item k - NS's group partials (its groups are done: FREE above),
-      // loaded under this slot's DMA wait, merged once it is handed over
-      float pv[GNP ? G::Groups : 1][2];
-      const bool merge = GNP && wave == 0 && k >= G::NS;
+      // GNP: item k - NS's output rows (its groups are done: FREE above),
+      // loaded under this slot's DMA wait, folded once it is handed over
+      float pv[16];
+      const bool merge = GNP && k >= G::NS;
+      const int kp = k - G::NS, tp = tb + wslot + (kp / slices) * per;
       if constexpr (GNP) {
-        if (merge) ring_gnp_load<G>(pv, scratch, s, lane);
+        if (merge) ring_gnp_load<G>(pv, out, tp, kp % slices, N, C, wave, lane);
       }
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 #if VG_RING_PROF == 2
       t_soft += __builtin_readcyclecounter() - f0_;  // FREE -> loaded
       t_gath += 1;
 #endif
-      if (lane == 0) __hip_atomic_fetch_add(&cnt[s], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (real && lane == 0) __hip_atomic_fetch_add(&cnt[s], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       if constexpr (GNP) {
-        if (merge) {
-          const int kp = k - G::NS;
-          ring_gnp_store<G>(pv, tb + wslot + (kp / slices) * per, kp % slices, N, C, lane, gnp);
-        }
+        if (merge) ring_gnp_store<G>(pv, tp, kp % slices, N, C, wave, lane, gnp);
       }
       if (pre) cur = nxt;
-    }
-    if constexpr (GNP) {  // the last NS items: wait for their groups, merge
-      if (wave == 0) {
-        for (int kp = max(0, items - G::NS); kp < items; ++kp) {
-          const int s = kp % G::NS, gen = kp / G::NS;
-          VG_RING_WAIT(&cnt[G::NS + s], G::Groups * (gen + 1), 1);
-          float pv[G::Groups][2];
-          ring_gnp_load<G>(pv, scratch, s, lane);
-          ring_gnp_store<G>(pv, tb + wslot + (kp / slices) * per, kp % slices, N, C, lane, gnp);
-        }
-      }
     }
 #if VG_RING_PROF
     prof_out();
@@ -960,34 +988,6 @@ __global__ void __launch_bounds__(kRNT) k_gat_fwd_ring(
       }
       const float4 ov = make_float4(acc[0] + bv.x, acc[1] + bv.y, acc[2] + bv.z, acc[3] + bv.w);
       if (w.r < N) *reinterpret_cast<float4*>(out + (size_t)w.r * C + sl * 64 + l16 * 4) = ov;
-      if constexpr (GNP) {  // the group's 4-row column partials of this slice (two passes, as gnp_block)
-        const int nw = min(4, max(0, N - (r0 + 4 * grp)));
-        const bool lv = w.r < N;
-        const float inv = nw > 0 ? 1.f / static_cast<float>(nw) : 0.f;
-        const float xv[4] = {ov.x, ov.y, ov.z, ov.w};
-        float sm[4], mu[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) sm[q] = lv ? xv[q] : 0.f;
-#pragma unroll
-        for (int off = 16; off < 64; off <<= 1)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) sm[q] += __shfl_xor(sm[q], off, 64);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          mu[q] = sm[q] * inv;
-          const float d = lv ? xv[q] - mu[q] : 0.f;
-          sm[q] = d * d;
-        }
-#pragma unroll
-        for (int off = 16; off < 64; off <<= 1)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) sm[q] += __shfl_xor(sm[q], off, 64);
-        if (lane < 16 && nw > 0) {
-          float* sp = scratch + (((size_t)blockIdx.x * G::NS + s) * G::Groups + grp) * 128;
-          *reinterpret_cast<float4*>(sp + l16 * 4) = make_float4(mu[0], mu[1], mu[2], mu[3]);
-          *reinterpret_cast<float4*>(sp + 64 + l16 * 4) = make_float4(sm[0], sm[1], sm[2], sm[3]);
-        }
-      }
 #if VG_RING_PROF == 1
       t_gath += __builtin_readcyclecounter() - p1;
 #endif
@@ -1070,9 +1070,8 @@ static int ring_launch(const int32_t* row_ptr, const int32_t* col, int32_t N, in
     attr = true;
   }
   const int grid = ring_grid(tiles);
-  float* scratch = GNP ? gnp + (size_t)tiles * 2 * C * 3 : nullptr;  // after the tile partials
   k_gat_fwd_ring<RingG, GNP><<<grid, kRNT, RingG::RingB, static_cast<hipStream_t>(stream)>>>(
-      row_ptr, col, N, C, h, a_src, a_dst, bias, slope, out, alpha, ucount, usrc, lidx, tiles, err, gnp, scratch);
+      row_ptr, col, N, C, h, a_src, a_dst, bias, slope, out, alpha, ucount, usrc, lidx, tiles, err, gnp);
   VG_CHECK_LAUNCH();
   return 0;
 }
@@ -1090,9 +1089,7 @@ extern "C" int32_t vg_gat_ring_tile_rows(void) { return RingG::RT; }
 extern "C" int64_t vg_gat_ring_gnp_floats(int32_t N, int32_t C) {
   if (N <= 0 || (C != 64 && C != 128)) return 0;
   const int64_t tiles = ((int64_t)N + RingG::RT - 1) / RingG::RT;
-  // the tile partials [tiles][2][C][3], then the group scratch of every workgroup
-  const int64_t grid = (num_cu() + 7) / 8 * 8;
-  return tiles * 2 * C * 3 + grid * RingG::NS * RingG::Groups * 128;
+  return tiles * 2 * C * 3;  // the tile partials [tiles][2][C][3]
 }
 
 extern "C" int vg_gat_aggregate_fwd_ring_gnp(const int32_t* row_ptr, const int32_t* col, int32_t N, int32_t C,

@@ -813,7 +813,7 @@ int vg_gat_aggregate_fwd_ring(const int32_t* row_ptr, const int32_t* col, int32_
  * vg_gat_ring_gnp_floats(N, C) floats, 16-B aligned -- the partials (count,
  * mean, M2) of every 64-row tile and column in the vg_gat_aggregate_fwd_gnp
  * layout with 64-row blocks, which vg_graphnorm_stats_gnp / vg_graphnorm_fwd_gnp
- * fold with gnp_rows = vg_gat_ring_tile_rows(), then the kernel's scratch.
+ * fold with gnp_rows = vg_gat_ring_tile_rows().
  * seg_rows: the GraphNorm segment (a multiple of the tile rows dividing N). */
 int64_t vg_gat_ring_gnp_floats(int32_t num_nodes, int32_t channels);
 int vg_gat_aggregate_fwd_ring_gnp(const int32_t* row_ptr, const int32_t* col, int32_t num_nodes, int32_t channels,

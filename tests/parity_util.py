@@ -370,9 +370,16 @@ def step_iterations_bf16_vs_oracle(cuda, cfg, g0, d0, vgan_pair, oracle_pair, st
     print("bf16 step vs f32 oracle:", {k: (f"{v:.3e}" if isinstance(v, float) else v) for k, v in m.items()})
     m["d_iterations"] = [tuple(round(x, 4) for x in t) for t in d_its]
     for k, v in bounds.items():
-        if k == "d_grad_over_cond":  # per critic iteration, against that iteration's conditioning (+ 0.05)
+        if k == "d_grad_over_cond":  # per critic iteration, against that iteration's conditioning
             for it, (rel, cos, c_rel, c_cos) in enumerate(d_its):
-                assert rel <= v * c_rel + 0.05, (k, it, rel, c_rel, v)
+                # a well-conditioned iteration (the reference's own gradient moves
+                # <= 0.15 when its dense operands are rounded to bf16) is held to
+                # 0.2 relative L2; an ill-conditioned one (a ReLU kink crossed --
+                # iteration 3 of forward_b32 at 0.70) to v x its conditioning + 0.05
+                lim = 0.2 if c_rel <= 0.15 else v * c_rel + 0.05
+                print(f"critic iteration {it}: bf16 D gradient rel {rel:.4f} (cos {cos:.5f}), conditioning "
+                      f"{c_rel:.4f} (cos {c_cos:.5f}), bound {lim:.4f}")
+                assert rel <= lim, (k, it, rel, c_rel, lim)
                 assert 1 - cos <= v * v * (1 - c_cos) + 0.02, (k, it, cos, c_cos, v)
         elif k == "g_grad_over_cond":  # bf16 deviation within v x the conditioning's (+ 0.05)
             assert m["g_grad"] <= v * m["g_cond"] + 0.05, (k, m["g_grad"], m["g_cond"], v)

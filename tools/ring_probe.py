@@ -25,6 +25,8 @@ sys.path.insert(0, os.path.join(ROOT, "building-gan-graph-conditioned-architectu
 
 import torch  # noqa: E402
 
+GNP = os.environ.get("RING_GNP", "0") == "1"  # RING_GNP=1: vg_gat_aggregate_fwd_ring_gnp
+
 
 def main():
     from vgan import ops
@@ -46,7 +48,14 @@ def main():
         out, alpha = torch.empty(n, c, device=dev), torch.empty(csr.num_edges, device=dev)
         err = torch.zeros(1, dtype=torch.int32, device=dev)
 
+        gnp = torch.empty(int(LIB.vg_gat_ring_gnp_floats(n, c)), device=dev) if GNP else None
+
         def run():
+            if GNP:  # the _gnp form the drop-in dispatches (GraphNorm partials per 64-row tile)
+                check(LIB.vg_gat_aggregate_fwd_ring_gnp(ptr(csr.row_ptr), ptr(csr.col), n, c, ptr(h), ptr(a_s),
+                                                        ptr(a_d), ptr(bias), 0.2, ptr(out), ptr(alpha), ptr(rplan), n,
+                                                        ptr(gnp), ptr(err), stream_handle(dev)), "ring_gnp")
+                return
             check(LIB.vg_gat_aggregate_fwd_ring(ptr(csr.row_ptr), ptr(csr.col), n, c, ptr(h), ptr(a_s), ptr(a_d),
                                                 ptr(bias), 0.2, ptr(out), ptr(alpha), ptr(rplan), ptr(err),
                                                 stream_handle(dev)), "ring")
@@ -54,15 +63,18 @@ def main():
         for _ in range(3):
             run()
         torch.cuda.synchronize()
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
-        run()
-        b.record()
-        torch.cuda.synchronize()
+        reps = []
+        for _ in range(int(os.environ.get("RING_REPS", "1"))):  # warm launches, each between events
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            run()
+            b.record()
+            torch.cuda.synchronize()
+            reps.append(round(a.elapsed_time(b) * 1e3, 1))
         buf = (ctypes.c_ulonglong * (grid * 16 * 4))()
         rc = LIB.vg_ring_prof_read(buf, grid * 16 * 4)
         vals = list(buf)
-        rec = {"C": c, "us": round(a.elapsed_time(b) * 1e3, 1), "err": int(err.item()), "rc": rc}
+        rec = {"gnp": GNP, "C": c, "us": reps[-1], "us_reps": reps, "err": int(err.item()), "rc": rc}
         for role, waves in (("loader", range(0, int(os.environ.get("RING_LW", "4")))), ("consumer", range(int(os.environ.get("RING_LW", "4")), 16))):
             w = [vals[(g * 16 + v) * 4] for g in range(grid) for v in waves]
             t = [vals[(g * 16 + v) * 4 + 1] for g in range(grid) for v in waves]
