@@ -322,10 +322,13 @@ def stress_model_leg(device, reps: int = 5):
     z = torch.randn(1, n, cfg.Z_DIM, device=device)
     out = {"workload": f"VoxelGNNGenerator.forward, eval, no grad, 8 x 50k-voxel stress buildings (N={n}), "
                        f"lattice-block numbering, {G.encoder.num_blocks} GAT blocks of widths {G.encoder.widths}"}
-    saved = ops._RING
+    saved = ops._RING, ops._RING_GNP
     try:
-        for label, on in (("ring", True), ("register", False)):
-            ops._RING = on
+        # the ring with the GraphNorm partials in its loaders (as dispatched),
+        # the ring with the GraphNorm reading its input for the statistics,
+        # the register gather (with partials)
+        for label, on, gnp in (("ring", True, True), ("ring_stats_pass", True, False), ("register", False, True)):
+            ops._RING, ops._RING_GNP = on, gnp
             with torch.no_grad():
                 for _ in range(2):
                     G(loc, vox, z)
@@ -344,7 +347,7 @@ def stress_model_leg(device, reps: int = 5):
                           "ring_launches_per_forward": (ops.RING_DISPATCHES - d0) // reps}
             log(f"stress model forward ({label}): {ms:.2f} ms, {out[label]['ring_launches_per_forward']} ring launches")
     finally:
-        ops._RING = saved
+        ops._RING, ops._RING_GNP = saved
     out["speedup"] = round(out["register"]["ms_per_forward"] / out["ring"]["ms_per_forward"], 3)
     return out
 

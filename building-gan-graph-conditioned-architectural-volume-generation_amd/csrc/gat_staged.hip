@@ -499,6 +499,9 @@ __device__ __forceinline__ int row_bcast16(int v) {
 #ifndef VG_RING_GDEPTH
 #define VG_RING_GDEPTH 8  // source rows read out of LDS before their FMAs (8 or 4)
 #endif
+#ifndef VG_RING_GNP_NOSTORE
+#define VG_RING_GNP_NOSTORE 0  // A/B builds only: the loaders form the GraphNorm partials but do not store them
+#endif
 #ifndef VG_RING_DPPRED
 #define VG_RING_DPPRED 1  // the softmax's group reductions by DPP row rotations (0: group_max / group_sum)
 #endif
@@ -693,7 +696,7 @@ __device__ __forceinline__ void ring_gnp_store(const float (&pv)[16], int t, int
     m2 = fmaf(d, d, m2);
   }
   const RingWel w = ring_chan_x32(ring_chan_x16({static_cast<float>(n), mu, m2}));
-  if (lane < 16) {
+  if (lane < 16 && (!VG_RING_GNP_NOSTORE || N < 0)) {
     float* p = gnp + ((size_t)t * 2 * C + sl * 64 + 16 * wave + lane) * 3;
     p[0] = w.n;
     p[1] = w.mu;
@@ -812,12 +815,16 @@ __global__ void __launch_bounds__(kRNT) k_gat_fwd_ring(
         }
       }
       // this slice's rows by LDS-DMA
+      // GNP: every instruction issued (the slots past U get copies of the last
+      // source row, unread): with a branch per instruction hipcc laid the
+      // GNP kernel's DMA blocks out as jump targets and waited vmcnt(0) at
+      // each -- 17 of 18 refill instructions serialised, the kernel 1.9x slower
       if (real && cur.U > 0) {
         const int ni = (cur.U + 3) / 4;
 #pragma unroll
         for (int q = 0; q < G::RowI; ++q) {
           const int i = wave + q * kRLW;
-          if (i < ni) {
+          if (GNP || i < ni) {
             const float* src = h + (size_t)cur.sr[q] * C + sl * 64 + (lane & 15) * 4;
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
                                              (__attribute__((address_space(3))) void*)(R.rows + 4 * i * 16), 16, 0, 0);

@@ -1049,6 +1049,18 @@ extern "C" int vg_graphnorm_fwd_gnp(const float* x, int32_t S, int32_t N, int32_
                 iter ? seed : 0, iter, iter ? salt : 0, iter ? keep_out : nullptr, nullptr, stream, gnp, gnp_rows);
 }
 
+extern "C" int vg_graphnorm_stats(const float* x, int32_t S, int32_t N, int32_t C, const float* mean_scale,
+                                  float eps, float* stats, float* ws, void* stream) {
+  if (S <= 0 || N <= 0 || C <= 0 || !x || !mean_scale || !stats || !ws) return VG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int chunks = chunks_for(N);
+  k_stats_partial<float><<<dim3(chunks, (C + 63) / 64, S), kBlock, 0, s>>>(x, N, C, C, ws, stats, nullptr);
+  k_stats_final<<<dim3(vg_blocks(C, kFoldWaves), S), 64 * kFoldWaves, 0, s>>>(ws, chunks, C, S, mean_scale, eps,
+                                                                           stats);
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int vg_graphnorm_stats_gnp(int32_t S, int32_t N, int32_t C, const float* gnp, int32_t gnp_rows,
                                       const float* mean_scale, float eps, float* stats, void* stream) {
   if (S <= 0 || N <= 0 || C <= 0 || !gnp || !mean_scale || !stats || gnp_rows <= 0 || gnp_rows > N)

@@ -290,6 +290,7 @@ SIGNATURES = {
     "vg_gat_lin_att_gn": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p,
                                          ctypes.POINTER(VgGnApply), _c_p]),
     "vg_graphnorm_stats_gnp": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_f32, _c_p, _c_p]),
+    "vg_graphnorm_stats": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_f32, _c_p, _c_p, _c_p]),
     "vg_gat_jvp2_blocks": (_c_i32, [_c_i32, _c_i32]),
     "vg_gat_jvp2_gn_deferred": (ctypes.c_int, [_c_p] * 5 + [_c_i32] * 3 + [_c_p] * 8 + [_c_f32] + [_c_p] * 7 +
                                 [ctypes.POINTER(VgGnJvp), _c_p, _c_p, _c_p]),

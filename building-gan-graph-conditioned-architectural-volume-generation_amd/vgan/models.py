@@ -146,7 +146,7 @@ class GATEncoder(nn.Module):
         apply kernel's values up to FMA contraction (1e-6,
         tests/test_gnp_gpu.py).  None (the caller runs the module path) for
         host-drawn masks, C > 64 projections or short segments."""
-        from ._lib import LIB, VgGnApply, check, dense, ptr, stream_handle
+        from ._lib import LIB, VgGnApply, check, dense, ptr, stream_handle, sync_counter
 
         rows = x.shape[0]
         S = int(segments)
@@ -186,18 +186,22 @@ class GATEncoder(nn.Module):
                                               ptr(conv.att_dst), ptr(H), ptr(a_s), ptr(a_d), st), "vg_gat_lin_att")
             O = torch.empty(rows, c, dtype=torch.float32, device=dev)
             alpha = torch.empty(csr.num_edges, dtype=torch.float32, device=dev)
-            gnp, g = ops.gnp_buffer(csr, c, dev)
-            if gnp is None:
-                raise RuntimeError("GraphNorm partials unavailable (VGAN_GN_FWD_FUSE=0 disables the fused path)")
+            gnp, g = ops.gnp_buffer(csr, c, dev)  # None: a ring layer without partials (VGAN_RING_GNP=0)
             ops.aggregate_fwd_raw(csr, c, ptr(H), ptr(a_s), ptr(a_d), ptr(conv.bias), float(conv.negative_slope),
                                   ptr(O), ptr(alpha), st, gnp)
             stats = torch.empty(S * 2 * c, dtype=torch.float32, device=dev)
+            ws = None if gnp is not None else \
+                torch.empty(int(LIB.vg_graphnorm_seg_ws_floats(S, n, c)), dtype=torch.float32, device=dev)
             nxt = getattr(self, f"module_{4 * (b + 1)}").out_channels if b + 1 < self.num_blocks else 0
             drop = (float(spec.p), int(spec.seed), ptr(spec.iter), int(spec.salt) & 0xFFFFFFFF) if spec is not None \
                 else (0.0, 0, None, 0)
             if 0 < nxt <= 64 and c <= 128 and c % 4 == 0:
-                check(LIB.vg_graphnorm_stats_gnp(S, n, c, ptr(gnp), g, ptr(norm.mean_scale), float(norm.eps),
-                                                 ptr(stats), st), "vg_graphnorm_stats_gnp")
+                if gnp is not None:
+                    check(LIB.vg_graphnorm_stats_gnp(S, n, c, ptr(gnp), g, ptr(norm.mean_scale), float(norm.eps),
+                                                     ptr(stats), st), "vg_graphnorm_stats_gnp")
+                else:
+                    check(LIB.vg_graphnorm_stats(ptr(O), S, n, c, ptr(norm.mean_scale), float(norm.eps), ptr(stats),
+                                                 ptr(ws), st), "vg_graphnorm_stats")
                 desc = VgGnApply(stats=stats.data_ptr(), weight=norm.weight.data_ptr(), bias=norm.bias.data_ptr(),
                                  mean_scale=norm.mean_scale.data_ptr(), keep=None, eps=float(norm.eps),
                                  p_drop=drop[0], seg_rows=n, salt=drop[3], seed=drop[1], iter=drop[2], y=None,
@@ -205,9 +209,16 @@ class GATEncoder(nn.Module):
                 pend = (O, desc, stats, c)  # stats / O stay referenced until the GEMM is enqueued
                 continue
             y = torch.empty(rows, c, dtype=torch.float32, device=dev)
-            check(LIB.vg_graphnorm_fwd_gnp(ptr(O), S, n, c, ptr(norm.weight), ptr(norm.bias), ptr(norm.mean_scale),
-                                           None, *drop, float(norm.eps), ptr(y), None, ptr(stats), ptr(gnp), g, st),
-                  "vg_graphnorm_fwd_gnp")
+            w_, b_, ms_ = ptr(norm.weight), ptr(norm.bias), ptr(norm.mean_scale)
+            if gnp is not None:
+                check(LIB.vg_graphnorm_fwd_gnp(ptr(O), S, n, c, w_, b_, ms_, None, *drop, float(norm.eps), ptr(y), None,
+                                               ptr(stats), ptr(gnp), g, st), "vg_graphnorm_fwd_gnp")
+            elif spec is not None:
+                check(LIB.vg_graphnorm_fwd_drop(ptr(O), S, n, c, w_, b_, ms_, *drop, float(norm.eps), ptr(y), None,
+                                                ptr(stats), ptr(ws), sync_counter(dev), st), "vg_graphnorm_fwd_drop")
+            else:
+                check(LIB.vg_graphnorm_fwd_seg(ptr(O), S, n, c, w_, b_, ms_, None, float(norm.eps), ptr(y), ptr(stats),
+                                               ptr(ws), sync_counter(dev), st), "vg_graphnorm_fwd_seg")
             x = y
         _ring_checked(csr)
         return x

@@ -45,6 +45,12 @@ _RING = os.environ.get("VGAN_RING", "1") == "1"
 RING_MIN_ROWS = int(os.environ.get("VGAN_RING_MIN_ROWS", "131072"))
 RING_MIN_STAGED = float(os.environ.get("VGAN_RING_MIN_STAGED", "0.9"))
 RING_TILE_ROWS = int(LIB.vg_gat_ring_tile_rows())
+# Ring layers form no GraphNorm partials by default: the GraphNorm reads its
+# input for the statistics (one pass over the output, ~40 us at 400k x 128),
+# which measured faster than the ring's _gnp form -- the configs[3] G forward
+# 7.45 vs 7.56 ms (register gather 8.00).  VGAN_RING_GNP=1:
+# vg_gat_aggregate_fwd_ring_gnp (the loaders form the partials).
+_RING_GNP = os.environ.get("VGAN_RING_GNP", "0") == "1"
 
 
 # --------------------------------------------------------------------- CSR
@@ -309,11 +315,14 @@ RING_DISPATCHES = 0
 def gnp_buffer(csr: "CSR", c: int, device):
     """(gnp, rows per partial) for an aggregation over ``csr`` at ``c``
     channels, or (None, 0) when its workgroups would span more than two
-    GraphNorm segments.  On the LDS ring (CSR.ring_on) the partials cover
-    its 64-row tiles (vg_gat_ring_gnp_floats, with the kernel's scratch)."""
+    GraphNorm segments.  On the LDS ring (CSR.ring_on): (None, 0) -- the
+    GraphNorm forms its statistics -- or, with VGAN_RING_GNP=1, partials over
+    its 64-row tiles (vg_gat_ring_gnp_floats)."""
     if not _GN_FWD_FUSE:
         return None, 0
     if csr.ring_on(c):
+        if not _RING_GNP:
+            return None, 0
         return torch.empty(int(LIB.vg_gat_ring_gnp_floats(csr.num_nodes, c)), dtype=torch.float32,
                            device=device), RING_TILE_ROWS
     g = int(LIB.vg_gat_gnp_rows(csr.num_nodes, c))

@@ -602,6 +602,11 @@ int vg_gat_lin_att_gn(const float* X, const float* W, int32_t N, int32_t Cin, in
  * aggregation's partials), for vg_gat_lin_att_gn. */
 int vg_graphnorm_stats_gnp(int32_t segments, int32_t rows, int32_t channels, const float* gnp, int32_t gnp_rows,
                            const float* mean_scale, float eps, float* stats, void* stream);
+/* The same column statistics from a pass over x [segments * rows, channels]
+ * (vg_graphnorm_fwd_seg's statistics: ws of vg_graphnorm_seg_ws_floats), for
+ * an aggregation that formed no partials. */
+int vg_graphnorm_stats(const float* x, int32_t segments, int32_t rows, int32_t channels, const float* mean_scale,
+                       float eps, float* stats, float* ws, void* stream);
 
 /* ---- the tangent sweep's GraphNorm sums in the GAT tangent pass ------------ */
 

@@ -2,9 +2,10 @@
 50k-voxel stress batch (N = 400,000, E' = 8.6M with the self loops), voxels
 numbered in 4 x 4 x 4 lattice blocks (vgan.locality.blocked), so the
 aggregation's tile plan stages every tile and ``ops.aggregate_fwd_raw``
-dispatches the wave-specialised LDS ring (vg_gat_aggregate_fwd_ring_gnp, with
-the following GraphNorm's column partials per 64-row tile) for the encoder's
-64- and 128-channel layers.
+dispatches the wave-specialised LDS ring for the encoder's 64- and 128-channel
+layers -- both forms: the GraphNorm forming its statistics from its input (the
+default) and vg_gat_aggregate_fwd_ring_gnp (the following GraphNorm's column
+partials per 64-row tile formed by the ring's loaders).
 
 * the no-grad eval forward (the fused encoder path: partials folded, GraphNorm
   applied in the next projection) against the reference restatement
@@ -62,7 +63,16 @@ def _draws(cfg, n):
     return torch.randn(1, n, cfg.Z_DIM, generator=g), torch.empty(n, cfg.NUM_CLASSES).exponential_(generator=g)
 
 
-def test_generator_forward_runs_the_ring_and_matches_f64(cuda, stress_batch):
+@pytest.fixture(params=[False, True], ids=["stats_pass", "ring_gnp"])
+def ring_gnp(request, monkeypatch):
+    """The ring's two GraphNorm statistics forms: the GraphNorm's own pass over
+    its input (the default) and the ring's loaders forming the partials
+    (vg_gat_aggregate_fwd_ring_gnp, VGAN_RING_GNP=1)."""
+    monkeypatch.setattr(ops, "_RING_GNP", request.param)
+    return request.param
+
+
+def test_generator_forward_runs_the_ring_and_matches_f64(cuda, stress_batch, ring_gnp):
     loc, vox = stress_batch
     cfg = Configuration()
     G = _model(cfg).eval()
@@ -82,13 +92,13 @@ def test_generator_forward_runs_the_ring_and_matches_f64(cuda, stress_batch):
     with torch.no_grad():
         lo, _, so = Go(ol, ov, z.double().to(cuda), noise=noise.double().to(cuda))
     err = (logits.double() - lo).abs().max().item()
-    print(f"stress forward: {ring_layers} ring layers, max |logits - f64 reference| = {err:.2e}, "
-          f"rel {rel_err(logits, lo):.2e}")
+    print(f"stress forward (ring_gnp={ring_gnp}): {ring_layers} ring layers, "
+          f"max |logits - f64 reference| = {err:.2e}, rel {rel_err(logits, lo):.2e}")
     assert err < 1e-3
     assert (soft.double() - so).abs().max().item() < 1e-3
 
 
-def test_generator_autograd_with_the_ring_against_f64(cuda, stress_batch, monkeypatch):
+def test_generator_autograd_with_the_ring_against_f64(cuda, stress_batch, ring_gnp, monkeypatch):
     """The autograd forward + backward (gat_conv's _gnp hint ->
     graphnorm_relu_dropout, the ring's 64-row partials) against the reference
     restatement's autograd in f64 on the GPU, beside the same model with the
@@ -139,7 +149,8 @@ def test_generator_autograd_with_the_ring_against_f64(cuda, stress_batch, monkey
             worst, worst_k = e_r / lim, k
     tot = {k: v ** 0.5 / scale for k, v in tot.items()}
     e_out = rel_err(out_r, out_g)
-    print(f"logits rel ring vs register {e_out:.2e}; whole gradient rel err vs f64: ring {tot['ring']:.2e}, "
+    print(f"(ring_gnp={ring_gnp}) logits rel ring vs register {e_out:.2e}; whole gradient rel err vs f64: "
+          f"ring {tot['ring']:.2e}, "
           f"register {tot['register']:.2e}; worst parameter {worst_k} at {worst:.2f} of its bound")
     assert e_out < 1e-5
     assert worst <= 1.0, (worst_k, worst)
