@@ -301,8 +301,10 @@ def stress_model_leg(device, reps: int = 5):
     """configs[3] through the drop-in: ``VoxelGNNGenerator.forward`` (eval,
     no grad: the fused encoder, 14 GAT blocks) on the 8 x 50k stress batch,
     voxels in lattice-block numbering, with the LDS ring dispatched for the
-    64 / 128-channel layers (ops.CSR.ring_on) and with it switched off (the
-    register gather); median of ``reps`` warm forwards between HIP events."""
+    64 / 128-channel layers (ops.CSR.ring_on; its GraphNorm statistics from
+    their own pass, or from the ring's loaders: ring_gnp) and with it
+    switched off (the register gather); median of ``reps`` warm forwards
+    between HIP events."""
     from vgan import ops
     from vgan.config import Configuration
     from vgan.graph import GraphBatch
@@ -324,10 +326,10 @@ def stress_model_leg(device, reps: int = 5):
                        f"lattice-block numbering, {G.encoder.num_blocks} GAT blocks of widths {G.encoder.widths}"}
     saved = ops._RING, ops._RING_GNP
     try:
-        # the ring with the GraphNorm partials in its loaders (as dispatched),
-        # the ring with the GraphNorm reading its input for the statistics,
-        # the register gather (with partials)
-        for label, on, gnp in (("ring", True, True), ("ring_stats_pass", True, False), ("register", False, True)):
+        # the ring as dispatched (the GraphNorm forms its statistics from its
+        # input), the ring with the partials from its loaders (VGAN_RING_GNP=1),
+        # the register gather (with the _gnp partials)
+        for label, on, gnp in (("ring", True, False), ("ring_gnp", True, True), ("register", False, True)):
             ops._RING, ops._RING_GNP = on, gnp
             with torch.no_grad():
                 for _ in range(2):

@@ -1,7 +1,7 @@
 """configs[3] through the drop-in: bench.stress_model_leg alone -- the
 VoxelGNNGenerator forward (eval, no grad) on the 8 x 50k stress batch with
-the ring (GraphNorm partials in its loaders), the ring with the GraphNorm
-reading its input for the statistics, and the register gather.
+the ring (the GraphNorm reading its input for the statistics: the default),
+the ring with the partials from its loaders, and the register gather.
 
     python tools/stress_model_probe.py [--reps 7]
 """
