@@ -499,6 +499,9 @@ __device__ __forceinline__ int row_bcast16(int v) {
 #ifndef VG_RING_GDEPTH
 #define VG_RING_GDEPTH 8  // source rows read out of LDS before their FMAs (8 or 4)
 #endif
+#ifndef VG_RING_DMA_ALL
+#define VG_RING_DMA_ALL 0  // 1: the plain ring also issues every DMA instruction (A/B knob)
+#endif
 #ifndef VG_RING_GNP_NOSTORE
 #define VG_RING_GNP_NOSTORE 0  // A/B builds only: the loaders form the GraphNorm partials but do not store them
 #endif
@@ -824,7 +827,7 @@ __global__ void __launch_bounds__(kRNT) k_gat_fwd_ring(
 #pragma unroll
         for (int q = 0; q < G::RowI; ++q) {
           const int i = wave + q * kRLW;
-          if (GNP || i < ni) {
+          if (GNP || VG_RING_DMA_ALL || i < ni) {
             const float* src = h + (size_t)cur.sr[q] * C + sl * 64 + (lane & 15) * 4;
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
                                              (__attribute__((address_space(3))) void*)(R.rows + 4 * i * 16), 16, 0, 0);
