@@ -11,153 +11,16 @@
 // cost per launch changes (Python: marshalling + one torch allocation per
 // temporary; here: a bump allocator over the caller's arena).  Host code
 // only: every launch goes through the library's own extern "C" entry points.
-#include <stdint.h>
-
-#include <algorithm>
-#include <vector>
-
-#include "../../include/vgan.h"
+#include "engine.h"
 
 namespace {
 
-constexpr int kActNone = 0, kActRelu = 1, kActMask = 3;
-
-struct Ctx {
-  bool dry;  // size the arena only: no launches, no plans
-  int bf16;
-  void* stream;
-  float* base;
-  int64_t cap, off;
-
-  // 256-byte aligned temporaries (the quad / float4 kernel forms need 16 B)
-  float* take(int64_t floats) {
-    const int64_t at = off;
-    off += (std::max<int64_t>(floats, 1) + 63) / 64 * 64;
-    return dry ? nullptr : base + at;
-  }
-
-  int gemm(const float* A, int lda, const float* B, int ldb, int bt, float* C, int ldc, int n, int m, int k,
-           const float* bias = nullptr, int act = kActNone, const float* aux = nullptr, int ldaux = 0) const {
-    if (dry) return 0;
-    return bf16 ? vg_gemm_bf16(A, lda, B, ldb, bt, bias, act, aux, ldaux, C, ldc, n, m, k, stream)
-                : vg_gemm(A, lda, B, ldb, bt, bias, act, aux, ldaux, C, ldc, n, m, k, stream);
-  }
-
-  // vg_linear_chain: 1 launched, 0 no kernel for this width chain (the caller
-  // runs its per-layer GEMMs), < 0 error
-  int chain(const float* x, int ldx, int rows, const std::vector<int32_t>& widths,
-            const std::vector<vg_chain_layer>& layers) const {
-    if (dry) return 1;
-    const int rc = bf16 ? vg_linear_chain_bf16(x, ldx, rows, widths.data(), (int32_t)layers.size(), layers.data(), stream)
-                        : vg_linear_chain(x, ldx, rows, widths.data(), (int32_t)layers.size(), layers.data(), stream);
-    if (rc == VG_EINVAL) return 0;
-    return rc == 0 ? 1 : (rc > 0 ? -rc : rc);
-  }
-};
-
-// FoldCollector (vgan/_lib.py): the backward's weight-gradient products run in
-// grouped launches and their folds (and the GAT / GraphNorm parameter folds)
-// in vg_fold_batch launches at the end, merged exactly as the Python
-// collector merges them.
-#ifndef VG_CRITIC_FOLD_SPLIT
-#define VG_CRITIC_FOLD_SPLIT 1  // long folds in two levels (vg_fold_batch_split); 0: vg_fold_batch (A/B)
-#endif
+using vg_engine::Ctx;
+using vg_engine::Folds;
+using vg_engine::kActMask;
+using vg_engine::kActNone;
+using vg_engine::kActRelu;
 constexpr int64_t kFoldWsFloats = 1 << 17;  // the split folds' chunk sums
-
-struct Folds {
-  std::vector<vg_fold> folds;
-  std::vector<vg_tn> prods;  // planned, not yet launched
-  float* ws = nullptr;       // kFoldWsFloats of the arena
-
-  void add(const vg_fold* f, int n) { folds.insert(folds.end(), f, f + n); }
-
-  int tn(const Ctx& cx, const float* A, int lda, const float* B, int ldb, int N, int M, int K, float* C, int ldc,
-         float* db, int db_rows, float* ws) {
-    if (cx.dry) return 0;
-    vg_tn p;
-    vg_fold f[2];
-    int32_t n = 0;
-    const int rc = cx.bf16 ? vg_gemm_tn_plan_bf16(A, lda, B, ldb, N, M, K, C, ldc, db, db_rows, 1, ws, &p, f, &n)
-                           : vg_gemm_tn_plan(A, lda, B, ldb, N, M, K, C, ldc, db, db_rows, 1, ws, &p, f, &n);
-    if (rc) return rc;
-    prods.push_back(p);
-    add(f, n);
-    return 0;
-  }
-
-  int launch_products(void* stream) {
-    for (int bf = 0; bf < 2; ++bf) {
-      std::vector<vg_tn> sel;
-      for (const vg_tn& p : prods)
-        if ((p.bf16 != 0) == (bf != 0)) sel.push_back(p);
-      for (size_t i = 0; i < sel.size(); i += VG_TN_GROUP_MAX) {
-        const int n = (int)std::min<size_t>(VG_TN_GROUP_MAX, sel.size() - i);
-        const int rc = vg_gemm_tn_group(sel.data() + i, n, stream);
-        if (rc) return rc;
-      }
-    }
-    prods.clear();
-    return 0;
-  }
-
-  int flush(Ctx& cx) {
-    if (cx.dry) return 0;
-    int rc = launch_products(cx.stream);  // the products first: their partials feed the folds
-    if (rc) return rc;
-    // folds into one destination merge into a two-source fold (applied in
-    // call order); one that cannot merge starts a new batch, so the two never race
-    std::vector<std::vector<vg_fold>> batches;
-    std::vector<vg_fold> cur;
-    std::vector<std::pair<float*, int>> where;
-    auto find = [&](float* out) -> int {
-      for (auto& w : where)
-        if (w.first == out) return w.second;
-      return -1;
-    };
-    for (const vg_fold& f : folds) {
-      const int j = find(f.out);
-      if (j >= 0) {
-        vg_fold& g = cur[j];
-        if (g.nsrc == 1 && f.nsrc == 1 && f.accumulate && g.width == f.width && g.k == f.k && g.ldo == f.ldo) {
-          g.src[1] = f.src[0];
-          g.nsrc = 2;
-          continue;
-        }
-        batches.push_back(cur);
-        cur.clear();
-        where.clear();
-      }
-      if ((int)cur.size() == VG_FOLD_MAX) {
-        batches.push_back(cur);
-        cur.clear();
-        where.clear();
-      }
-      where.emplace_back(f.out, (int)cur.size());
-      cur.push_back(f);
-    }
-    if (!cur.empty()) batches.push_back(cur);
-    for (auto& b : batches) {
-      const int rc = VG_CRITIC_FOLD_SPLIT ? vg_fold_batch_split(b.data(), (int32_t)b.size(), ws, kFoldWsFloats, cx.stream)
-                                          : vg_fold_batch(b.data(), (int32_t)b.size(), cx.stream);
-      if (rc) return rc;
-    }
-    folds.clear();
-    return 0;
-  }
-};
-
-#define VG_TRY(expr)          \
-  do {                        \
-    const int _rc = (expr);   \
-    if (_rc) return _rc;      \
-  } while (0)
-#define VG_RUN(expr)                  \
-  do {                                \
-    if (!cx.dry) {                    \
-      const int _rc = (expr);         \
-      if (_rc) return _rc;            \
-    }                                 \
-  } while (0)
 
 // per-block state of the forward (critic.py's blk dicts)
 struct Blk {
@@ -176,6 +39,7 @@ int run(Ctx& cx, const vg_critic_model* md, const vg_critic_batch* bt, float* ou
   auto rows = [](float* t, int r0, int width) { return t ? t + (int64_t)r0 * width : nullptr; };
   Folds folds;
   folds.ws = cx.take(kFoldWsFloats);
+  folds.ws_floats = kFoldWsFloats;
 
   // ------------------------------------------------------------ pass A
   float* X0 = cx.take((int64_t)X4 * W0);

@@ -180,6 +180,41 @@ class VgCriticBatch(ctypes.Structure):
                 ("gp_counter", _c_p)]
 
 
+VG_GEN_MAX_LAYERS = 8
+VG_GEN_MAX_BLOCKS = 32
+
+
+class VgGenLnLayer(ctypes.Structure):
+    """vg_gen_ln_layer (include/vgan.h): Linear -> LayerNorm -> LeakyReLU."""
+    _fields_ = [(k, _c_p) for k in ("weight", "bias", "ln_weight", "ln_bias", "g_weight", "g_bias", "g_ln_weight",
+                                    "g_ln_bias")] + [("ln_eps", _c_f32), ("slope", _c_f32), ("in_", _c_i32),
+                                                     ("out", _c_i32)]
+
+
+class VgGenModel(ctypes.Structure):
+    """vg_gen_model (include/vgan.h)."""
+    _fields_ = [(k, _c_i32) for k in ("n_mfe", "n_mlp", "n_gblocks", "n_dec", "n_dmlp", "n_dblocks", "n_ddec",
+                                      "bf16")] + \
+               [(k, _c_f32) for k in ("tau", "p_drop_g", "p_drop_d", "lambda_adv", "lambda_label", "lambda_ratio",
+                                      "lambda_void", "lambda_far", "dim_scale")] + \
+               [("void_class", _c_i32), ("mfe", VgGenLnLayer * VG_GEN_MAX_LAYERS),
+                ("mlp", VgGenLnLayer * VG_GEN_MAX_LAYERS), ("gblock", VgCriticBlock * VG_GEN_MAX_BLOCKS),
+                ("dec", VgGenLnLayer * VG_GEN_MAX_LAYERS), ("dec_last", VgCriticLinear),
+                ("dmlp", VgCriticLinear * VG_GEN_MAX_LAYERS), ("dblock", VgCriticBlock * VG_GEN_MAX_BLOCKS),
+                ("ddec", VgCriticLinear * VG_GEN_MAX_LAYERS)]
+
+
+class VgGenBatch(ctypes.Structure):
+    """vg_gen_batch (include/vgan.h)."""
+    _fields_ = [(k, _c_i32) for k in ("n", "classes", "mx_w", "vx_w", "mvx_w", "z_dim")] + \
+               [(k, _c_p) for k in ("mx", "vx", "mvx", "onehot", "type", "graph_ptr", "site_area")] + \
+               [(k, _c_i32) for k in ("num_graphs", "far_col", "dy_col", "dx_col")] + \
+               [("g", VgCsrRef), ("seg_rows", _c_i32), ("sync", _c_p), ("one", _c_p), ("seed", ctypes.c_uint64),
+                ("iter", _c_p), ("z_salt", ctypes.c_uint32), ("noise_salt", ctypes.c_uint32),
+                ("g_keep_salt", ctypes.c_uint32 * VG_GEN_MAX_BLOCKS),
+                ("d_keep_salt", ctypes.c_uint32 * VG_GEN_MAX_BLOCKS)]
+
+
 VG_HGEN_MAX_LAYERS = 8
 VG_HGEN_MAX_BLOCKS = 32
 
@@ -310,6 +345,9 @@ SIGNATURES = {
     "vg_critic_arena_floats": (ctypes.c_int64, [ctypes.POINTER(VgCriticModel), ctypes.POINTER(VgCriticBatch)]),
     "vg_critic_loss_and_grad": (ctypes.c_int, [ctypes.POINTER(VgCriticModel), ctypes.POINTER(VgCriticBatch), _c_p,
                                                _c_i64, _c_p, _c_p]),
+    "vg_gen_arena_floats": (ctypes.c_int64, [ctypes.POINTER(VgGenModel), ctypes.POINTER(VgGenBatch)]),
+    "vg_gen_loss_and_grad": (ctypes.c_int, [ctypes.POINTER(VgGenModel), ctypes.POINTER(VgGenBatch), _c_p, _c_i64,
+                                            _c_p, _c_p, _c_p]),
     "vg_linear_chain_bf16": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p]),
     "vg_gat_gnp_rows": (_c_i32, [_c_i32, _c_i32]),
     "vg_gat_gnp_floats": (_c_i64, [_c_i32, _c_i32]),

@@ -41,14 +41,19 @@ from typing import List
 import torch
 import torch.nn as nn
 
+from . import _lib
 from . import data as vdata
 from . import ops
-from ._lib import _GN_ROWS, LIB, FoldCollector, VgGnBwdIn, check, dense, linear_chain, ptr, stream_handle, sync_counter
-from .critic import _GN_FUSE, ACT_ADD, ACT_MASK, ACT_NONE, ACT_RELU, _f, _off
+from ._lib import (_GN_ROWS, LIB, FoldCollector, VgGnBwdIn, check, dense, gemm_precision, linear_chain, ptr,
+                   stream_handle, sync_counter)
+from .critic import _GN_FUSE, ACT_ADD, ACT_MASK, ACT_NONE, ACT_RELU, CriticEngine, _f, _off
 
 # VGAN_GEN_ADD_FUSE=0: the summed adjoints (label_hard, x, em) as a product
 # then a torch add_ instead of the product's add epilogue (A/B knob)
 _ADD_FUSE = os.environ.get("VGAN_GEN_ADD_FUSE", "1") == "1"
+# VGAN_GEN_NATIVE=0: the iteration issued from Python (the A/B leg of
+# vg_gen_loss_and_grad, which is bit-identical)
+_NATIVE = os.environ.get("VGAN_GEN_NATIVE", "1") == "1"
 
 
 class GeneratorEngine:
@@ -245,6 +250,162 @@ class GeneratorEngine:
             check(LIB.vg_gat_bwd_ex(*gat_args, ptr(dO), *tail, st), "vg_gat_bwd_ex")
         return dH
 
+    # --------------------------------------------------- native engine
+    # vg_gen_loss_and_grad issues loss_and_grad's launches from C++ (same
+    # kernels, order, arguments and draws: bit-identical) with every
+    # temporary in one arena: ~1-2 us of host time per launch instead of ~10.
+    # Used in loss_and_grad's default configuration (the knobs at their
+    # defaults, device-drawn randomness, both models in train mode, no early
+    # hook, no ring aggregation); anything else runs the Python schedule.
+    def _native_config_ok(self, n: int, rng, early) -> bool:
+        return (_NATIVE and early is None and getattr(rng, "mode", None) == "device" and hasattr(rng, "_salt")
+                and _GN_FUSE and _ADD_FUSE and _GN_ROWS and _lib._CHAIN and _lib._TN_GROUP and _lib._FOLD_SPLIT
+                and _lib._FOLD_BATCH == _lib.VG_FOLD_MAX and ops._GN_FWD_FUSE and n >= 64
+                and self.G.encoder.training and self.D.encoder.training
+                and max(len(self.mfe), len(self.mlp), len(self.dec), len(self.d_mlp),
+                        len(self.d_dec)) <= _lib.VG_GEN_MAX_LAYERS
+                and max(len(self.gblocks), len(self.dblocks)) <= _lib.VG_GEN_MAX_BLOCKS)
+
+    def _native_model(self):
+        """The vg_gen_model of G's parameters and gradient views and D's
+        parameters (rebuilt when any address changes), or None."""
+        G, D = self.G, self.D
+        dparams = self.__dict__.get("_dparams")
+        if dparams is None:
+            dparams = self._dparams = list(D.parameters())
+        key = (gemm_precision(),) + tuple(p.data_ptr() for p in self._params) + \
+            tuple(p.grad.data_ptr() for p in self._params) + tuple(p.data_ptr() for p in dparams)
+        if self.__dict__.get("_native_key") == key:
+            return self._native_md
+        m = _lib.VgGenModel()
+        m.n_mfe, m.n_mlp, m.n_gblocks, m.n_dec = len(self.mfe), len(self.mlp), len(self.gblocks), len(self.dec)
+        m.n_dmlp, m.n_dblocks, m.n_ddec = len(self.d_mlp), len(self.dblocks), len(self.d_dec)
+        m.bf16 = 1 if gemm_precision() == "bf16" else 0
+        m.tau, m.p_drop_g, m.p_drop_d = float(G.tau), float(G.encoder.dropout), float(D.encoder.dropout)
+        (m.lambda_adv, m.lambda_label, m.lambda_ratio, m.lambda_void, m.lambda_far) = self.lambdas
+        m.dim_scale, m.void_class = self.dim_scale, self.void_class
+
+        def ln_layer(dst, blk):
+            lin, ln, act = blk
+            if lin.bias is None or ln.weight is None or ln.bias is None:
+                return False
+            dst.weight, dst.bias, dst.ln_weight, dst.ln_bias = (lin.weight.data_ptr(), lin.bias.data_ptr(),
+                                                                ln.weight.data_ptr(), ln.bias.data_ptr())
+            dst.g_weight, dst.g_bias = lin.weight.grad.data_ptr(), lin.bias.grad.data_ptr()
+            dst.g_ln_weight, dst.g_ln_bias = ln.weight.grad.data_ptr(), ln.bias.grad.data_ptr()
+            dst.ln_eps, dst.slope = float(ln.eps), float(act.negative_slope)
+            dst.in_, dst.out = lin.in_features, lin.out_features
+            return True
+
+        def linear(dst, lin, grads):
+            if lin.bias is None:
+                return False
+            dst.weight, dst.bias = lin.weight.data_ptr(), lin.bias.data_ptr()
+            if grads:
+                dst.g_weight, dst.g_bias = lin.weight.grad.data_ptr(), lin.bias.grad.data_ptr()
+            dst.in_, dst.out = lin.in_features, lin.out_features
+            return True
+
+        def block(dst, conv, norm, grads):
+            if getattr(conv.lin, "bias", None) is not None:  # (GATConv's lin has none)
+                return False
+            dst.lin_weight, dst.att_src, dst.att_dst, dst.bias = (conv.lin.weight.data_ptr(), conv.att_src.data_ptr(),
+                                                                  conv.att_dst.data_ptr(), conv.bias.data_ptr())
+            dst.gn_weight, dst.gn_bias, dst.gn_mean_scale = (norm.weight.data_ptr(), norm.bias.data_ptr(),
+                                                             norm.mean_scale.data_ptr())
+            if grads:
+                dst.g_lin_weight, dst.g_att_src, dst.g_att_dst, dst.g_bias = (
+                    conv.lin.weight.grad.data_ptr(), conv.att_src.grad.data_ptr(), conv.att_dst.grad.data_ptr(),
+                    conv.bias.grad.data_ptr())
+                dst.g_gn_weight, dst.g_gn_bias, dst.g_gn_mean_scale = (
+                    norm.weight.grad.data_ptr(), norm.bias.grad.data_ptr(), norm.mean_scale.grad.data_ptr())
+            dst.gn_eps, dst.slope = float(norm.eps), float(conv.negative_slope)
+            dst.in_, dst.out = conv.in_channels, conv.out_channels
+            return True
+
+        ok = all(ln_layer(m.mfe[i], b) for i, b in enumerate(self.mfe))
+        ok = ok and all(ln_layer(m.mlp[i], b) for i, b in enumerate(self.mlp))
+        ok = ok and all(ln_layer(m.dec[i], b) for i, b in enumerate(self.dec))
+        ok = ok and linear(m.dec_last, self.dec_last, True)
+        ok = ok and all(block(m.gblock[i], c, nm, True) for i, (c, nm) in enumerate(self.gblocks))
+        ok = ok and all(linear(m.dmlp[i], l, False) for i, l in enumerate(self.d_mlp))
+        ok = ok and all(block(m.dblock[i], c, nm, False) for i, (c, nm) in enumerate(self.dblocks))
+        ok = ok and all(linear(m.ddec[i], l, False) for i, l in enumerate(self.d_dec))
+        if not ok:
+            return None
+        self._native_key, self._native_md = key, m
+        return m
+
+    def _arena_for(self, model, batch, dev):
+        """(arena tensor, floats, 256-byte aligned base) for this batch, grown
+        outside a capture (25 % ahead); a replaced arena is kept alive, since
+        recorded graphs may still reference it.  None when it is too small and
+        a capture is running, or the model / batch is not the engine's."""
+        need = int(LIB.vg_gen_arena_floats(ctypes.byref(model), ctypes.byref(batch)))
+        if need < 0:
+            return None
+        cur = self.__dict__.get("_arena")
+        if cur is not None and cur[1] >= need and cur[0].device == dev:
+            return cur
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        floats = (need * 5 // 4 + 63) // 64 * 64
+        t = torch.empty(floats + 64, dtype=torch.float32, device=dev)
+        off = (-t.data_ptr() % 256) // 4
+        if cur is not None:
+            self.__dict__.setdefault("_old_arenas", []).append(cur)
+        self._arena = (t, floats, t.data_ptr() + 4 * off)
+        return self._arena
+
+    def _native(self, prep, voxel_graph, rng, dev, st, sy):
+        """loss_and_grad through vg_gen_loss_and_grad, or None (this batch or
+        model is not the native engine's: nothing drawn, nothing launched)."""
+        csr = prep.csr
+        if any(csr.ring_on(conv.out_channels) for conv, _ in self.gblocks + self.dblocks):
+            return None
+        mx, vx, mvx, oh = prep.matched_x, prep.voxel_x, prep.matched_voxel_x, prep.onehot_f
+        if any(t.dtype != torch.float32 or not t.is_contiguous() or t.dim() != 2 for t in (mx, vx, mvx, oh)):
+            return None
+        vtype, gptr = voxel_graph.type, voxel_graph.ptr
+        if vtype.dtype != torch.int64 or gptr.dtype != torch.int64:
+            return None
+        vtype, gptr = vtype.contiguous(), gptr.contiguous()
+        sa = voxel_graph.site_area
+        sa = sa if sa.dtype == torch.float32 and sa.is_contiguous() else sa.float().contiguous()
+        model = self._native_model()
+        if model is None:
+            return None
+        n, K = vx.shape[0], self.n_classes
+        b = _lib.VgGenBatch()
+        b.n, b.classes, b.mx_w, b.vx_w, b.mvx_w, b.z_dim = n, K, mx.shape[1], vx.shape[1], mvx.shape[1], self.z_dim
+        b.mx, b.vx, b.mvx, b.onehot = mx.data_ptr(), vx.data_ptr(), mvx.data_ptr(), oh.data_ptr()
+        b.type, b.graph_ptr, b.site_area = vtype.data_ptr(), gptr.data_ptr(), sa.data_ptr()
+        b.num_graphs, b.far_col, b.dy_col, b.dx_col = gptr.numel() - 1, 9, 4, 5
+        ell, w = csr.ell()
+        CriticEngine._csr_ref(b.g, csr, ell, w)
+        b.seg_rows, b.sync = csr.seg_rows, sy
+        b.one = self._const(("one", dev), lambda: torch.ones(1, dtype=torch.float32, device=dev)).data_ptr()
+        it = rng._iter(dev)
+        b.seed, b.iter = int(rng.seed) & ((1 << 64) - 1), it.data_ptr()
+        arena = self._arena_for(model, b, dev)
+        if arena is None:
+            return None
+        # the draws of the Python schedule, in its order: z, G's masks, the
+        # Gumbel noise, D's masks (RNG.normal / keep_mask / exponential salts)
+        s, nbg, nbd = rng._salt, len(self.gblocks), len(self.dblocks)
+        b.z_salt = (0x40000000 | (s + 1)) & 0xFFFFFFFF
+        for i in range(nbg):
+            b.g_keep_salt[i] = (s + 2 + i) & 0xFFFFFFFF
+        b.noise_salt = (0x40000000 | (s + 2 + nbg)) & 0xFFFFFFFF
+        for i in range(nbd):
+            b.d_keep_salt[i] = (s + 3 + nbg + i) & 0xFFFFFFFF
+        rng._salt = s + 2 + nbg + nbd
+        out, hard = _f(K + 3, dev=dev), _f(n, K, dev=dev)
+        check(LIB.vg_gen_loss_and_grad(ctypes.byref(model), ctypes.byref(b), arena[2], arena[1], ptr(out), ptr(hard),
+                                       st), "vg_gen_loss_and_grad")
+        self.native_calls = self.__dict__.get("native_calls", 0) + 1
+        return out[0], hard.unsqueeze(0)
+
     # ------------------------------------------------------------ engine
     def loss_and_grad(self, local_graph, voxel_graph, rng, early=None):
         """(g_loss device scalar, label_hard [1, N, K]) of trainer.py:483-490;
@@ -268,6 +429,10 @@ class GeneratorEngine:
         for p in params:
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
+        if self._native_config_ok(n, rng, early):
+            r = self._native(prep, voxel_graph, rng, dev, st, sy)
+            if r is not None:
+                return r
         folds = FoldCollector()
         z = rng.normal((1, n, self.z_dim), dev).reshape(n, self.z_dim)
 

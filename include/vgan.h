@@ -1097,6 +1097,83 @@ int64_t vg_critic_arena_floats(const vg_critic_model* model, const vg_critic_bat
 int vg_critic_loss_and_grad(const vg_critic_model* model, const vg_critic_batch* batch, float* arena,
                             int64_t arena_floats, float* out, void* stream);
 
+/* ---- one generator iteration issued from C++ ------------------------------ */
+
+/* The generator half of the training step (trainer.py:483-491: G(z) ->
+ * Gumbel labels -> D(label_hard) -> _compute_generator_loss, trainer.py:334-385
+ * -> backward into G's parameters only) -- vgan/genstep.py
+ * GeneratorEngine.loss_and_grad in its default configuration, issued from
+ * C++: the same entry points in the same order with the same arguments and
+ * the same device-RNG draws (z, G's dropout masks, the Gumbel noise, D's
+ * masks), so loss, labels and gradients are bit-identical to the Python
+ * engine's; the host pays ~1-2 us per launch instead of ~10 (the generator
+ * iteration of a fresh batch runs eagerly).  G's gradients are ACCUMULATED
+ * into the g_* buffers; D's g_* fields are not read.  Every temporary lives in
+ * `arena` (vg_gen_arena_floats floats, 256-byte aligned), the same contract as
+ * vg_critic_loss_and_grad's. */
+#define VG_GEN_MAX_LAYERS 8
+#define VG_GEN_MAX_BLOCKS 32
+
+/* [Linear -> LayerNorm -> LeakyReLU] (models.py:33-47,49-66,92-113) */
+typedef struct {
+  const float* weight; /* [out][in] */
+  const float* bias;
+  const float* ln_weight;
+  const float* ln_bias;
+  float* g_weight;
+  float* g_bias;
+  float* g_ln_weight;
+  float* g_ln_bias;
+  float ln_eps, slope;
+  int32_t in, out;
+} vg_gen_ln_layer;
+
+typedef struct {
+  int32_t n_mfe, n_mlp, n_gblocks, n_dec;   /* G: matched-features encoder, MLP encoder, GAT blocks, decoder */
+  int32_t n_dmlp, n_dblocks, n_ddec;        /* D: MLP encoder, GAT blocks, decoder */
+  int32_t bf16;                             /* dense products on bf16 operands */
+  float tau, p_drop_g, p_drop_d;
+  float lambda_adv, lambda_label, lambda_ratio, lambda_void, lambda_far;
+  float dim_scale;
+  int32_t void_class;
+  vg_gen_ln_layer mfe[VG_GEN_MAX_LAYERS];
+  vg_gen_ln_layer mlp[VG_GEN_MAX_LAYERS];
+  vg_critic_block gblock[VG_GEN_MAX_BLOCKS];
+  vg_gen_ln_layer dec[VG_GEN_MAX_LAYERS];
+  vg_critic_linear dec_last; /* the decoder's last Linear (logits) */
+  vg_critic_linear dmlp[VG_GEN_MAX_LAYERS];
+  vg_critic_block dblock[VG_GEN_MAX_BLOCKS];
+  vg_critic_linear ddec[VG_GEN_MAX_LAYERS];
+} vg_gen_model;
+
+typedef struct {
+  int32_t n, classes;             /* voxel nodes, K */
+  int32_t mx_w, vx_w, mvx_w, z_dim; /* widths of matched_x, voxel.x, matched_voxel_x, z */
+  const float* mx;                /* [n][mx_w] type-matched program features (the generator's) */
+  const float* vx;                /* [n][vx_w] voxel features */
+  const float* mvx;               /* [n][mvx_w] the discriminator's matched features */
+  const float* onehot;            /* [n][K] float one-hot of the true types */
+  const int64_t* type;            /* [n] true types */
+  const int64_t* graph_ptr;       /* [num_graphs + 1] building row offsets */
+  const float* site_area;         /* per node (read at each building's first row) */
+  int32_t num_graphs, far_col, dy_col, dx_col;
+  vg_csr_ref g;                   /* the batch graph (ell optional) */
+  int32_t seg_rows;               /* GraphNorm segment rows of the aggregation partials (= n) */
+  int32_t* sync;                  /* vg_graphnorm_bwd_seg's counter */
+  const float* one;               /* device 1.0f: the loss's seed */
+  uint64_t seed;                  /* device RNG: seed, iteration counter, salts */
+  const int64_t* iter;
+  uint32_t z_salt, noise_salt;
+  uint32_t g_keep_salt[VG_GEN_MAX_BLOCKS];
+  uint32_t d_keep_salt[VG_GEN_MAX_BLOCKS];
+} vg_gen_batch;
+
+int64_t vg_gen_arena_floats(const vg_gen_model* model, const vg_gen_batch* batch);
+/* out [classes + 3]: vg_gen_loss_fwd's (out[0] = the generator loss); hard
+ * [n][classes]: label_hard. */
+int vg_gen_loss_and_grad(const vg_gen_model* model, const vg_gen_batch* batch, float* arena, int64_t arena_floats,
+                         float* out, float* hard, void* stream);
+
 /* ---- the f16 inference-sweep forward as one native call (configs[4]) ----- */
 
 /* One batch of the configs[4] sweep -- InferenceSweep._forward with the f16

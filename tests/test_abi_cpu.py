@@ -95,6 +95,62 @@ def test_hgen_arena_sizing_is_host_only():
     assert size(1000, 10) < 0
 
 
+def test_gen_arena_sizing_is_host_only():
+    """vg_gen_arena_floats runs the native generator iteration's schedule dry
+    (no launch, no device pointer read): the reference's layer pattern sizes
+    an arena that grows with the batch; a decoder input width that is not
+    [enc | x | em | voxel.x | z], a batch under 64 nodes or segment rows
+    other than the batch's are refused (the Python schedule runs them)."""
+    import ctypes as ct
+
+    from vgan._lib import LIB as lib, VgGenBatch, VgGenModel
+
+    K, fl, vd, zd, h, F = 7, 17, 12, 128, 128, 29
+    md = VgGenModel()
+    md.n_mfe, md.n_mlp, md.n_gblocks, md.n_dec = 2, 2, 4, 2
+    md.n_dmlp, md.n_dblocks, md.n_ddec = 2, 2, 2
+    md.tau, md.p_drop_g, md.p_drop_d = 1.0, 0.2, 0.2
+
+    def ln(d, i, o):
+        d.in_, d.out, d.ln_eps, d.slope = i, o, 1e-5, 0.2
+
+    def blk(d, i, o):
+        d.in_, d.out, d.gn_eps, d.slope = i, o, 1e-5, 0.2
+
+    ln(md.mfe[0], fl, h)
+    ln(md.mfe[1], h, h)
+    ln(md.mlp[0], h + vd + zd, h)
+    ln(md.mlp[1], h, h)
+    for b, (i, o) in enumerate(((h, 64), (64, 2), (2, 1), (1, 8))):
+        blk(md.gblock[b], i, o)
+    ln(md.dec[0], 8 + h + h + vd + zd, 64)
+    ln(md.dec[1], 64, 16)
+    md.dec_last.in_, md.dec_last.out = 16, K
+    md.dmlp[0].in_, md.dmlp[0].out = F + K, 64
+    md.dmlp[1].in_, md.dmlp[1].out = 64, 64
+    blk(md.dblock[0], 64, 32)
+    blk(md.dblock[1], 32, 16)
+    md.ddec[0].in_, md.ddec[0].out = 16, 8
+    md.ddec[1].in_, md.ddec[1].out = 8, 1
+
+    def size(n):
+        bt = VgGenBatch()
+        bt.n, bt.classes, bt.mx_w, bt.vx_w, bt.mvx_w, bt.z_dim = n, K, fl, vd, F, zd
+        bt.num_graphs, bt.seg_rows = 4, n
+        bt.g.num_nodes, bt.g.num_edges = n, 9 * n
+        return int(lib.vg_gen_arena_floats(ct.byref(md), ct.byref(bt))), bt
+
+    (a, _), (b, bt) = size(1000), size(4000)
+    assert a > 0 and b > a and a % 64 == 0
+    assert size(32)[0] < 0
+    bt.seg_rows = 2000
+    assert int(lib.vg_gen_arena_floats(ct.byref(md), ct.byref(bt))) < 0
+    md.dec[0].in_ = h + h + vd + zd  # not the [enc | x | em | voxel.x | z] width
+    assert size(1000)[0] < 0
+    VG_EINVAL = -1
+    assert lib.vg_gen_loss_and_grad(ct.byref(md), ct.byref(bt), None, 0, None, None, None) == VG_EINVAL
+
+
 def test_ops_refuse_cpu_tensors():
     import torch
 
