@@ -34,6 +34,7 @@
 #include "gnbwd.h"
 #include "gnjvp.h"
 
+#include <algorithm>
 #include <initializer_list>
 
 namespace {
@@ -877,6 +878,127 @@ __global__ void k_gn_apply4(const float* __restrict__ x, int quads, int N, int C
   }
 }
 
+// The statistics fold and the apply in ONE launch (vg_graphnorm_fwd_gnp on
+// narrow layers, where a segment's block partials fit in LDS): every
+// workgroup owns kFuseQ quads per thread of one contiguous range and puts
+// their x (and keep, or draws their dropout multipliers) in flight; stages the
+// slot-0 partials of the segment(s) the range touches into LDS with coalesced
+// 16-B loads (a column's partials are 12 C bytes apart in HBM: gathered
+// straight from global memory, every lane's load is its own cache line and the
+// L1 address path, not bandwidth, bounds the fold); folds them per column in
+// exactly k_stats_final_gnp's order (lane l merges blocks l, l + 64, ...
+// ascending, then the xor butterfly), so the same bits; and applies as
+// k_gn_apply4.  The workgroup holding a segment's first quad stores that
+// segment's [mu | d] for the backward.  One dependent launch and the
+// statistics' write + read fewer per GraphNorm, for each workgroup reading its
+// segment's partials from L2.
+constexpr int kFuseThreads = 512;
+constexpr int kFuseQ = 2;      // quads per thread
+constexpr int kFuseLd = 8;     // float4 partial loads per thread in flight
+__global__ void __launch_bounds__(kFuseThreads) k_gn_apply4_gnp(
+    const float* __restrict__ x, int quads, int N, int C, const float* __restrict__ w,
+    const float* __restrict__ b, const float* __restrict__ ms, const float* __restrict__ keep, float eps,
+    const float* __restrict__ gnp, int G, float* __restrict__ stats, float* __restrict__ y, float p_drop,
+    unsigned long long seed, const long long* __restrict__ iter, unsigned int salt, float* __restrict__ keep_out,
+    int nseg) {
+  extern __shared__ float4 sh4[];
+  float* sh = reinterpret_cast<float*>(sh4);
+  float* pl = sh + 3 * C + 2 * C * nseg;  // the staged partials [nb][C][3]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, waves = kFuseThreads / 64;
+  const int q_begin = blockIdx.x * kFuseThreads * kFuseQ;
+  const int q_end = min(quads, q_begin + kFuseThreads * kFuseQ);
+  const int sg_lo = (4 * q_begin / C) / N, sg_hi = ((4 * q_end - 1) / C) / N;
+  const bool draw = iter != nullptr;
+  const long long it = draw ? *iter : 0;
+  // this thread's quads: x and keep in flight, dropout drawn, during the fold
+  F4 xv[kFuseQ], kv[kFuseQ];
+#pragma unroll
+  for (int j = 0; j < kFuseQ; ++j) {
+    const int q = q_begin + threadIdx.x + j * kFuseThreads;
+    xv[j] = F4{{0.f, 0.f, 0.f, 0.f}};
+    kv[j] = F4{{1.f, 1.f, 1.f, 1.f}};
+    if (q < q_end) {
+      xv[j] = ld4(x + 4 * q);
+      if (draw) {
+        const float4 k = vg_keep4_raw(q, salt, it, seed, p_drop);
+        kv[j] = F4{{k.x, k.y, k.z, k.w}};
+      } else if (keep) {
+        kv[j] = ld4(keep + 4 * q);
+      }
+    }
+  }
+  for (int i = threadIdx.x; i < C; i += kFuseThreads) {
+    sh[i] = w[i];
+    sh[C + i] = b[i];
+    sh[2 * C + i] = ms[i];
+  }
+  const int nb = (N + G - 1) / G;
+  const int row4 = 3 * C / 4;  // float4s per block's slot-0 partials
+  const int total4 = nb * row4;
+  for (int sg = sg_lo; sg <= sg_hi; ++sg) {
+    const float* src = gnp + (size_t)sg * nb * 2 * C * 3;
+    if (sg > sg_lo) __syncthreads();  // the previous segment's fold has read pl
+    for (int i0 = threadIdx.x; i0 < total4; i0 += kFuseThreads * kFuseLd) {
+      float4 v[kFuseLd];
+#pragma unroll
+      for (int u = 0; u < kFuseLd; ++u) {
+        const int i = i0 + u * kFuseThreads;
+        const int r = i / row4;
+        v[u] = i < total4 ? *reinterpret_cast<const float4*>(src + (size_t)r * 2 * C * 3 + 4 * (i - r * row4))
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < kFuseLd; ++u) {
+        const int i = i0 + u * kFuseThreads;
+        if (i < total4) sh4[(3 * C + 2 * C * nseg) / 4 + i] = v[u];
+      }
+    }
+    __syncthreads();
+    float* st = sh + 3 * C + 2 * C * (sg - sg_lo);
+    for (int c = wave; c < C; c += waves) {
+      Welford acc = {0.f, 0.f, 0.f};
+      for (int bk = lane; bk < nb; bk += 64) {
+        const float* p = pl + (bk * C + c) * 3;
+        acc = merge(acc, Welford{p[0], p[1], p[2]});
+      }
+      acc = wave_merge(acc);
+      if (lane == 0) {
+        st[c] = acc.mean;
+        st[C + c] = gn_denom(acc, sh[2 * C + c], eps);
+      }
+    }
+  }
+  __syncthreads();
+  // [mu | d] of every segment whose first quad is in this range
+  for (int sg = sg_lo; sg <= sg_hi; ++sg) {
+    const long long first = (long long)sg * N * C / 4;
+    if (first >= q_begin && first < q_end)
+      for (int i = threadIdx.x; i < 2 * C; i += kFuseThreads)
+        stats[(size_t)sg * 2 * C + i] = sh[3 * C + 2 * C * (sg - sg_lo) + i];
+  }
+#pragma unroll
+  for (int j = 0; j < kFuseQ; ++j) {
+    const int q = q_begin + threadIdx.x + j * kFuseThreads;
+    if (q >= q_end) break;
+    const int t0 = q * 4;
+    const int row = t0 / C;
+    const int c0 = t0 - row * C;
+    const float* st = sh + 3 * C + 2 * C * (row / N - sg_lo);
+    if (draw && keep_out) st4(keep_out + t0, kv[j]);
+    const F4 wv = ld4(sh + c0), bv = ld4(sh + C + c0), mv = ld4(sh + 2 * C + c0);
+    const F4 muv = ld4(st + c0), sdv = ld4(st + C + c0);
+    F4 r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float o = xv[j].v[i] - muv.v[i] * mv.v[i];
+      const float z = (o / sdv.v[i]) * wv.v[i] + bv.v[i];
+      r.v[i] = z > 0.f ? z : 0.f;
+      if (draw || keep) r.v[i] *= kv[j].v[i];
+    }
+    st4(y + t0, r);
+  }
+}
+
 __global__ void k_gn_bwd_apply4(const float* __restrict__ x, const float* __restrict__ gy, int quads,
                                 int N, int C, int S, const float* __restrict__ w,
                                 const float* __restrict__ b, const float* __restrict__ ms,
@@ -950,6 +1072,22 @@ static inline bool quad_ok(long long total, int C, int lds_floats,
   return true;
 }
 
+// k_gn_apply4_gnp (statistics fold + apply in one launch) when one segment's
+// block partials are at most VG_GN_FUSE_BYTES (0: never; the A/B build): every
+// workgroup reads them, so only the narrow layers qualify (batch 32: C <= 16)
+#ifndef VG_GN_FUSE_BYTES
+#define VG_GN_FUSE_BYTES 49152
+#endif
+constexpr long long kFuseLdsBytes = 160 * 1024;
+static inline bool gn_fuse_ok(int N, int C, int G) {
+  const long long nb = (N + (long long)G - 1) / G;
+  return G > 0 && nb * C * 12 <= (long long)VG_GN_FUSE_BYTES;
+}
+
+extern "C" int32_t vg_graphnorm_fwd_gnp_fused(int32_t N, int32_t C, int32_t gnp_rows) {
+  return gn_fuse_ok(N, C, gnp_rows) && C % 4 == 0 ? 1 : 0;
+}
+
 extern "C" int64_t vg_graphnorm_seg_ws_floats(int32_t segments, int32_t rows_per_segment,
                                               int32_t channels) {
   (void)rows_per_segment;
@@ -971,6 +1109,27 @@ static int gn_fwd(const float* x, int32_t S, int32_t N, int32_t C, const float* 
       (gnp && (gnp_rows <= 0 || gnp_rows > N)))
     return VG_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  const long long total = (long long)S * N * C;
+  if (gnp && gn_fuse_ok(N, C, gnp_rows) && quad_ok(total, C, 0, {x, keep, y, keep_out})) {
+    const int quads = static_cast<int>(total / 4);
+    const int per_wg = kFuseThreads * kFuseQ;
+    const int nseg = per_wg * 4 / C / N + 2;  // segments one workgroup's range can touch
+    const long long nb = (N + gnp_rows - 1) / gnp_rows;
+    const long long lds_f = 3 * C + 2 * C * nseg + nb * C * 3;
+    if (lds_f * 4 <= kFuseLdsBytes) {
+      static bool attr = false;  // beyond the default 64 KB of dynamic LDS
+      if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gn_apply4_gnp),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFuseLdsBytes);
+        attr = true;
+      }
+      k_gn_apply4_gnp<<<vg_blocks(quads, per_wg), kFuseThreads, lds_f * 4, s>>>(
+          x, quads, N, C, weight, bias, mean_scale, keep, eps, gnp, gnp_rows, stats, y, p_drop,
+          (unsigned long long)seed, reinterpret_cast<const long long*>(iter), salt, keep_out, nseg);
+      VG_CHECK_LAUNCH();
+      return 0;
+    }
+  }
   if (gnp) {
     k_stats_final_gnp<<<dim3(vg_blocks(C, kFoldWaves), S), 64 * kFoldWaves, 0, s>>>(gnp, gnp_rows, N, C, S, mean_scale,
                                                                                  eps, stats);
@@ -982,7 +1141,6 @@ static int gn_fwd(const float* x, int32_t S, int32_t N, int32_t C, const float* 
                                                                              stats);
   }
   (void)sync;  // former last-block-fold counter: accepted, unused
-  const long long total = (long long)S * N * C;
   const int lds_f = 3 * C + 2 * C * S;
   if (quad_ok(total, C, lds_f, {x, keep, y, keep_out}))
     k_gn_apply4<<<apply_blocks(total / 4), 256, lds_f * 4, s>>>(

@@ -350,6 +350,7 @@ SIGNATURES = {
                                             _c_p, _c_p, _c_p]),
     "vg_linear_chain_bf16": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p]),
     "vg_gat_gnp_rows": (_c_i32, [_c_i32, _c_i32]),
+    "vg_graphnorm_fwd_gnp_fused": (_c_i32, [_c_i32, _c_i32, _c_i32]),
     "vg_gat_gnp_floats": (_c_i64, [_c_i32, _c_i32]),
     "vg_gat_aggregate_fwd_gnp": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p,
                                                 _c_f32, _c_p, _c_p, _c_i32, _c_p, _c_p]),

@@ -75,21 +75,44 @@ def renumber(voxel: GraphData, perm: torch.Tensor) -> GraphData:
     return GraphData(**out)
 
 
-def block_order(location: torch.Tensor, block=(4, 4, 4)) -> torch.Tensor:
+def _morton3(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor, bits: int) -> torch.Tensor:
+    """Interleaved bits (a, b, c), a's the most significant of each triple."""
+    key = torch.zeros_like(a)
+    for i in range(bits - 1, -1, -1):
+        key = (key << 3) | (((a >> i) & 1) << 2) | (((b >> i) & 1) << 1) | ((c >> i) & 1)
+    return key
+
+
+def block_order(location: torch.Tensor, block=(4, 4, 4), blocks: str = "rowmajor") -> torch.Tensor:
     """perm [n] numbering voxels in (floor, y, x) blocks of ``block`` = (bf, by,
-    bx), blocks in (floor, y, x) order, row-major inside a block.  A 64-row
-    aggregation tile is then a 4 x 4 x 4 block of the lattice: on the stress
-    lattice its sources are the block grown by one voxel in y and x on each of
-    its floors and on the floors just above and below -- about 6 x 6 x 6 =
-    216 distinct rows for ~1,400 edges (6.4 edges per distinct source row,
-    against 3.1 for the 4 x 4 floor tiles of ``tile_order``)."""
+    bx), row-major inside a block.  A 64-row aggregation tile is then a 4 x 4 x 4
+    block of the lattice: on the stress lattice its sources are the block grown
+    by one voxel in y and x on each of its floors and on the floors just above
+    and below -- about 6 x 6 x 6 = 216 distinct rows for ~1,400 edges (6.4
+    edges per distinct source row, against 3.1 for the 4 x 4 floor tiles of
+    ``tile_order``).
+
+    ``blocks`` orders the blocks themselves: "rowmajor" (floor, y, x), or
+    "morton" (Z-order of the block coordinates), under which any run of
+    consecutive tiles -- what one XCD's workgroups aggregate at a time -- is a
+    compact 3-D region, so a tile's halo rows on the floors above and below
+    are those its neighbours in the run stage too (row-major blocks put the
+    vertical neighbour a whole block layer, ~170 tiles, later)."""
     loc = location.to(torch.int64)
     bf, by, bx = (int(b) for b in block)
     f, y, x = loc[:, 0], loc[:, 1], loc[:, 2]
     ny = int(y.max()) // by + 1 if loc.numel() else 1
     nx = int(x.max()) // bx + 1 if loc.numel() else 1
-    key = (((f // bf) * ny + y // by) * nx + x // bx) * (bf * by * bx) + ((f % bf) * by + y % by) * bx + x % bx
-    return torch.argsort(key, stable=True)
+    inner = ((f % bf) * by + y % by) * bx + x % bx
+    if blocks == "morton":
+        nf = int(f.max()) // bf + 1 if loc.numel() else 1
+        bits = max(1, max(nf, ny, nx) - 1).bit_length()
+        outer = _morton3(f // bf, y // by, x // bx, bits)
+    elif blocks == "rowmajor":
+        outer = ((f // bf) * ny + y // by) * nx + x // bx
+    else:
+        raise ValueError(f"block_order: blocks must be 'rowmajor' or 'morton', not {blocks!r}")
+    return torch.argsort(outer * (bf * by * bx) + inner, stable=True)
 
 
 def tiled(voxel: GraphData, tile: int = 4) -> Tuple[GraphData, torch.Tensor]:
@@ -98,7 +121,7 @@ def tiled(voxel: GraphData, tile: int = 4) -> Tuple[GraphData, torch.Tensor]:
     return renumber(voxel, perm), perm
 
 
-def blocked(voxel: GraphData, block=(4, 4, 4)) -> Tuple[GraphData, torch.Tensor]:
+def blocked(voxel: GraphData, block=(4, 4, 4), blocks: str = "rowmajor") -> Tuple[GraphData, torch.Tensor]:
     """(renumbered building, perm) in ``block_order`` of its ``location``."""
-    perm = block_order(voxel.location, block)
+    perm = block_order(voxel.location, block, blocks)
     return renumber(voxel, perm), perm

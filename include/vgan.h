@@ -251,6 +251,12 @@ int vg_graphnorm_fwd_gnp(const float* x, int32_t segments, int32_t rows, int32_t
                          const float* bias, const float* mean_scale, const float* keep, float p_drop, uint64_t seed,
                          const int64_t* iter, uint32_t salt, float eps, float* y, float* keep_out, float* stats,
                          const float* gnp, int32_t gnp_rows, void* stream);
+/* 1 when vg_graphnorm_fwd_gnp over (rows, channels, gnp_rows) runs as ONE
+ * launch -- every workgroup folds its segment's partials (the narrow layers:
+ * a segment's partials within the build's VG_GN_FUSE_BYTES) and applies;
+ * statistics and output bit-identical to the two-launch form -- else 0.
+ * Host-only. */
+int32_t vg_graphnorm_fwd_gnp_fused(int32_t rows, int32_t channels, int32_t gnp_rows);
 /* Backward over the segments; parameter gradients sum over segments and are
  * written (accumulate = 0) or added (1); g_w may be NULL (no parameter
  * gradients: g_b, g_ms are then ignored).  inj (nullable) is added to g_x

@@ -53,6 +53,10 @@ def test_workspace_queries_are_host_only():
 
     assert lib.vg_csr_ws_ints(100, 10) == 4 * 10 + 100 + 10
     assert lib.vg_graphnorm_ws_floats(1000, 16) >= 2 * 16
+    # the one-launch GraphNorm forward: narrow layers at batch 32, not the wide ones
+    assert lib.vg_graphnorm_fwd_gnp_fused(12600, 16, 64) == 1
+    assert lib.vg_graphnorm_fwd_gnp_fused(12600, 128, 8) == 0
+    assert lib.vg_graphnorm_fwd_gnp_fused(12600, 2, 32) == 0
 
 
 def test_hgen_arena_sizing_is_host_only():

@@ -369,3 +369,55 @@ def test_stacked_statistics_bitwise_equal_separate(cuda, C):
         o1, s1 = run(csr, hs[k], ass[k], ads[k], 1)
         assert torch.equal(out3[k * n:(k + 1) * n], o1)
         assert torch.equal(s3[k * 2 * C:(k + 1) * 2 * C], s1), k
+
+
+@pytest.mark.parametrize("graph,copies", [("lattice", 1), ("lattice", 3), ("lattice", 5), ("stress", 1),
+                                          ("stress", 3), ("star", 3)])
+@pytest.mark.parametrize("C", [4, 8, 12, 16, 24])
+@pytest.mark.parametrize("drop", [False, True])
+def test_fused_fold_apply_bitwise_equal_two_launches(cuda, graph, copies, C, drop):
+    """vg_graphnorm_fwd_gnp as ONE launch on the narrow layers (k_gn_apply4_gnp:
+    every workgroup folds its segment's partials, then applies): the statistics
+    it stores are bit for bit vg_graphnorm_stats_gnp's (k_stats_final_gnp's fold
+    order), every segment's are written (buffer pre-filled with NaN; small
+    segments put several in one workgroup's range), y matches an fp32 apply of
+    those statistics and the dropout multipliers are vg_graphnorm_fwd_drop's."""
+    torch.manual_seed(C + 11 * copies)
+    csr = _csr(cuda, graph, copies)
+    n, seg = csr.num_nodes, csr.seg_rows
+    S = n // seg
+    gnp, g = ops.gnp_buffer(csr, C, cuda)
+    fused = int(LIB.vg_graphnorm_fwd_gnp_fused(seg, C, g))
+    if graph != "stress":
+        assert fused == 1, (seg, C, g)
+    h = torch.randn(n, C, device=cuda)
+    a_s, a_d = 0.5 * torch.randn(n, device=cuda), 0.5 * torch.randn(n, device=cuda)
+    b = torch.randn(C, device=cuda)
+    out, alpha = torch.empty_like(h), torch.empty(csr.num_edges, device=cuda)
+    st = ops.stream_handle(cuda)
+    ops.aggregate_fwd_raw(csr, C, ptr(h), ptr(a_s), ptr(a_d), ptr(b), 0.2, ptr(out), ptr(alpha), st, gnp)
+    w = 1 + 0.2 * torch.randn(C, device=cuda)
+    bb = 0.2 * torch.randn(C, device=cuda)
+    ms = torch.rand(C, device=cuda) + 0.2
+    it = torch.tensor([3], dtype=torch.int64, device=cuda)
+    y1, k1 = torch.empty_like(out), torch.empty_like(out)
+    s1 = torch.full((S * 2 * C,), float("nan"), device=cuda)
+    check(LIB.vg_graphnorm_fwd_gnp(ptr(out), S, seg, C, ptr(w), ptr(bb), ptr(ms), None, 0.2 if drop else 0.0,
+                                   99, ptr(it) if drop else None, 5, EPS, ptr(y1), ptr(k1) if drop else None,
+                                   ptr(s1), ptr(gnp), g, st), "vg_graphnorm_fwd_gnp")
+    s2 = torch.empty(S * 2 * C, device=cuda)
+    check(LIB.vg_graphnorm_stats_gnp(S, seg, C, ptr(gnp), g, ptr(ms), EPS, ptr(s2), st), "vg_graphnorm_stats_gnp")
+    torch.cuda.synchronize()
+    assert torch.equal(s1, s2)
+    sv = s2.view(S, 2, C)
+    mu, d = sv[:, 0].repeat_interleave(seg, 0), sv[:, 1].repeat_interleave(seg, 0)
+    y_ref = torch.relu((out - mu * ms) / d * w + bb)
+    if drop:
+        y2, k2 = torch.empty_like(out), torch.empty_like(out)
+        ws = torch.empty(int(LIB.vg_graphnorm_seg_ws_floats(S, seg, C)), device=cuda)
+        check(LIB.vg_graphnorm_fwd_drop(ptr(out), S, seg, C, ptr(w), ptr(bb), ptr(ms), 0.2, 99, ptr(it), 5, EPS,
+                                        ptr(y2), ptr(k2), ptr(s2), ptr(ws), None, st), "vg_graphnorm_fwd_drop")
+        torch.cuda.synchronize()
+        assert torch.equal(k1, k2)
+        y_ref = y_ref * k1
+    assert (y1 - y_ref).abs().max().item() <= 1e-5 * max(1.0, y_ref.abs().max().item())

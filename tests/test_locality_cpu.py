@@ -75,6 +75,28 @@ def test_block_order_is_a_3d_block_permutation():
     assert distinct(v2.edge_index) < 0.8 * distinct(tiled(v, 4)[0].edge_index)
 
 
+def test_morton_block_order_keeps_blocks_and_groups_neighbours():
+    """blocks="morton": still a permutation whose 64-row groups are whole 4 x 4 x
+    4 blocks, the blocks in Z-order -- so every aligned run of 8 tiles is a 2 x 2
+    x 2 region of blocks (row-major blocks: a strip along x)."""
+    _, v = make_stress_building(777, 0, F=8, Y=16, X=16)
+    v2, perm = blocked(v, (4, 4, 4), blocks="morton")
+    n = v.num_nodes
+    assert sorted(perm.tolist()) == list(range(n))
+    bl = []
+    for g in range(n // 64):
+        loc = v2.location[64 * g:64 * g + 64]
+        for c in range(3):
+            assert int(loc[:, c].max() - loc[:, c].min()) == 3 and int(loc[:, c].min()) % 4 == 0
+        bl.append(tuple(int(t) // 4 for t in loc.min(0).values))
+    for r in range(0, len(bl), 8):
+        run = bl[r:r + 8]
+        for c in range(3):
+            assert max(b[c] for b in run) - min(b[c] for b in run) == 1
+    with pytest.raises(ValueError):
+        block_order(v.location, (4, 4, 4), blocks="hilbert")
+
+
 def test_block_order_ragged_edges():
     loc = torch.tensor([[0, 0, 5], [0, 0, 0], [5, 0, 0], [0, 4, 0], [1, 1, 1]])
     # blocks (f//4, y//4, x//4): (0,0,1) (0,0,0) (1,0,0) (0,1,0) (0,0,0); ny = 2, nx = 2

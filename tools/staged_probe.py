@@ -3,7 +3,7 @@
 (vg_gat_aggregate_fwd_ring) in three voxel numberings, cold MALL, HIP events.
 One JSON line per (order, kernel, C).
 
-    python tools/staged_probe.py [--reps 20] [--orders rowmajor,tiled,blocked]
+    python tools/staged_probe.py [--reps 20] [--orders rowmajor,tiled,blocked,morton]
 """
 import argparse
 import json
@@ -39,7 +39,8 @@ def main():
     scratch = torch.empty(512 * 1024 * 1024 // 4, device=dev)
     st = stream_handle(dev)
     for order in args.orders.split(","):
-        vs = items if order == "rowmajor" else [tiled(v, 4)[0] if order == "tiled" else blocked(v)[0] for v in items]
+        vs = (items if order == "rowmajor" else [tiled(v, 4)[0] for v in items] if order == "tiled"
+              else [blocked(v, blocks="morton" if order == "morton" else "rowmajor")[0] for v in items])
         vox = GraphBatch.from_data_list(vs).to(dev)
         csr = ops.CSR(vox.edge_index, vox.num_nodes)
         n, e = csr.num_nodes, csr.num_edges
