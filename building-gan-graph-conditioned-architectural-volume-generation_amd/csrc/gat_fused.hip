@@ -71,95 +71,7 @@ __device__ __forceinline__ void load_param(Vec<CPL>& r, const float* __restrict_
   load_row<CPL, false>(r, p, c0, C);  // parameters live at arbitrary offsets of the flat buffer
 }
 
-// GraphNorm column partials of the rows a workgroup aggregated: the forward
-// statistics of the GraphNorm that follows every GATConv (models.py:73-75,
-// 193-195; graphnorm.hip's k_stats_partial re-read the whole output for them).
-// Per column (count, mean, M2) of the block's rows.  Each wave takes its own
-// rows' two-pass statistics from the values still in registers (sum by
-// xor-shuffles across the wave's L-lane row groups -- every lane ends with the
-// total -- the wave mean, then the squared deviations the same way); the four
-// waves' (count, mean, M2) meet in LDS behind ONE barrier and are merged in
-// wave order with Chan's formula (deterministic).  (The first form took the
-// block's two passes through LDS: three barriers, ~1 us per launch more.)
-// Blocks are SEGMENT-ALIGNED (gnp_rows): a stacked forward over S copies
-// (seg_rows rows each) gives every copy ceil(seg_rows / G) blocks of its own,
-// the last one short, so each copy's partials -- and the statistics folded
-// from them -- are bit for bit those of a separate forward over that copy.
-// (Blocks dealt over the stacked rows straddled copies at offsets that
-// depended on the copy: the critic engine's stacked real / fake / mix forward
-// then normalised with statistics ~1e-7 off the three separate forwards of
-// autograd's double backward, enough to flip bf16 operand roundings.)
-// gnp [blocks][2][ldc][3], column cb + c, slot 0 (slot 1 unused).  v: this
-// lane's CPL columns c0.. of its row (lanes past C hold anything: their
-// columns are not written).
-// (A first form folded each column serially over the block's rows with
-// Welford updates in one wave: +4 us per launch, slower than the separate
-// statistics pass it replaced.)
-struct GnpRows {
-  int lb, row0, end;  // logical block, its first row, the end of its segment
-};
-
-template <int G>
-__device__ __forceinline__ GnpRows gnp_rows(int seg_rows) {
-  const int lb = xcd_remap(blockIdx.x, gridDim.x);
-  const int bps = (seg_rows + G - 1) / G;
-  const int seg = lb / bps;
-  return {lb, seg * seg_rows + (lb - seg * bps) * G, (seg + 1) * seg_rows};
-}
-
-template <int L, int CPL>
-__device__ __forceinline__ void gnp_block(const float (&v)[CPL], int row, const GnpRows& gr, int C, int c0,
-                                          int cb, int ldc, float* __restrict__ gnp) {
-  constexpr int W = L * CPL, RW = 64 / L, NW = kBlock / 64;  // columns, rows per wave, waves
-  __shared__ float red[NW][2][W];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const bool in0 = row < gr.end;
-  const int nw = max(0, min(RW, gr.end - (gr.row0 + wave * RW)));  // this wave's rows in the segment
-  const float inv = nw > 0 ? 1.f / static_cast<float>(nw) : 0.f;
-  float s[CPL], mean[CPL];
-#pragma unroll
-  for (int q = 0; q < CPL; ++q) s[q] = in0 ? v[q] : 0.f;
-#pragma unroll
-  for (int off = L; off < 64; off <<= 1)
-#pragma unroll
-    for (int q = 0; q < CPL; ++q) s[q] += __shfl_xor(s[q], off, 64);
-#pragma unroll
-  for (int q = 0; q < CPL; ++q) {
-    mean[q] = s[q] * inv;
-    const float d = in0 ? v[q] - mean[q] : 0.f;
-    s[q] = d * d;
-  }
-#pragma unroll
-  for (int off = L; off < 64; off <<= 1)
-#pragma unroll
-    for (int q = 0; q < CPL; ++q) s[q] += __shfl_xor(s[q], off, 64);
-  if (lane < L)
-#pragma unroll
-    for (int q = 0; q < CPL; ++q) {
-      red[wave][0][c0 + q] = mean[q];
-      red[wave][1][c0 + q] = s[q];
-    }
-  __syncthreads();
-  const int c = threadIdx.x;
-  if (c < C) {
-    const int n_blk = min(gr.end, gr.row0 + kBlock / L) - gr.row0;
-    float n = static_cast<float>(min(RW, n_blk)), mu = red[0][0][c], m2 = red[0][1][c];
-#pragma unroll
-    for (int w = 1; w < NW; ++w) {  // Chan's merge, wave order
-      const int k = min(RW, n_blk - w * RW);
-      if (k <= 0) break;
-      const float nb = static_cast<float>(k), nt = n + nb;
-      const float delta = red[w][0][c] - mu, fb = nb / nt;
-      mu += delta * fb;
-      m2 += red[w][1][c] + delta * delta * n * fb;
-      n = nt;
-    }
-    float* p = gnp + ((size_t)gr.lb * 2 * ldc + cb + c) * 3;
-    p[0] = n;
-    p[1] = mu;
-    p[2] = m2;
-  }
-}
+// GraphNorm column partials (GnpRows, gnp_rows, gnp_block): rowgroup.h
 
 // ===================================================================== forward
 // C >= 9, pass A: per-row attention projections a_src_i = <h_i, att_src>,

@@ -1177,6 +1177,25 @@ extern "C" int vg_graphnorm_fwd_h(const uint16_t* x, int32_t ld, int32_t S, int3
   return 0;
 }
 
+extern "C" int vg_graphnorm_fwd_h_gnp(const uint16_t* x, int32_t ld, int32_t S, int32_t N, int32_t C,
+                                      const float* weight, const float* bias, const float* mean_scale, float eps,
+                                      uint16_t* y, int32_t ldy, float* stats, const float* gnp, int32_t gnp_rows,
+                                      void* stream) {
+  const int wcols = (C + 7) / 8 * 8;
+  if (S <= 0 || N <= 0 || C <= 0 || ld < wcols || ld % 8 || ldy < wcols || ldy % 8 || !x || !weight || !bias ||
+      !mean_scale || !y || !stats || !gnp || gnp_rows <= 0 || gnp_rows > N)
+    return VG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  k_stats_final_gnp<<<dim3(vg_blocks(C, kFoldWaves), S), 64 * kFoldWaves, 0, s>>>(gnp, gnp_rows, N, C, S, mean_scale,
+                                                                               eps, stats);
+  const long long pairs = (long long)S * N * (wcols / 2);
+  k_gn_apply_h<<<apply_blocks(pairs), 256, 0, s>>>(reinterpret_cast<const _Float16*>(x), pairs, C, ld, wcols,
+                                                   (long long)N, weight, bias, mean_scale, eps, stats,
+                                                   reinterpret_cast<_Float16*>(y), ldy);
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int vg_graphnorm_fwd_seg(const float* x, int32_t S, int32_t N, int32_t C,
                                     const float* weight, const float* bias,
                                     const float* mean_scale, const float* keep, float eps,

@@ -239,15 +239,28 @@ __device__ __forceinline__ void load_hrow(float* dst, const _Float16* __restrict
   for (int q = 0; q < CPL; ++q) dst[q] = (float)t.v[q];
 }
 
-template <int L, int CPL>
+// GNP: also the following GraphNorm's column partials over the rows' f16
+// outputs (vg::gnp_block: segment-aligned blocks of kBlock / L rows, the
+// statistics vg_graphnorm_fwd_h would form from the stored halves), so the
+// GraphNorm folds them (vg_graphnorm_fwd_h_gnp) instead of re-reading the
+// output; every group stays to the block barrier (a group past its segment
+// recomputes the segment's last row and stores nothing).
+template <int L, int CPL, bool GNP = false>
 __global__ void __launch_bounds__(kBlock) k_hgat_fwd(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, int N, int C, int ld,
     const _Float16* __restrict__ h, const float* __restrict__ a_src, const float* __restrict__ a_dst,
-    const float* __restrict__ bias, float slope, _Float16* __restrict__ out, int ldo) {
+    const float* __restrict__ bias, float slope, _Float16* __restrict__ out, int ldo, float* __restrict__ gnp = nullptr,
+    int seg_rows = 0) {
   constexpr int T = 4;  // edges per lane kept in registers
-  const vg::GroupIdx g = vg::group_index<L>();
-  if (g.row >= N) return;
-  const int i = g.row;
+  vg::GroupIdx g = vg::group_index<L>();
+  vg::GnpRows gr{0, 0, N};
+  if constexpr (GNP) {
+    gr = vg::gnp_rows<kBlock / L>(seg_rows);
+    g.row = gr.row0 + threadIdx.x / L;
+  }
+  const bool live = g.row < gr.end;
+  if (!GNP && !live) return;
+  const int i = live ? g.row : gr.end - 1;
   const int beg = row_ptr[i], end = row_ptr[i + 1];
   const int deg = end - beg;
   const float ad = a_dst[i];
@@ -317,7 +330,13 @@ __global__ void __launch_bounds__(kBlock) k_hgat_fwd(
     const int c = c0 + q;
     o.v[q] = (_Float16)(c < C ? acc[q] + bias[c] : 0.f);
   }
-  *reinterpret_cast<HVec<CPL>*>(out + (size_t)i * ldo + c0) = o;
+  if (live) *reinterpret_cast<HVec<CPL>*>(out + (size_t)i * ldo + c0) = o;
+  if constexpr (GNP) {
+    float v[CPL];
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) v[q] = static_cast<float>(o.v[q]);
+    vg::gnp_block<L, CPL>(v, g.row, gr, C, c0, 0, C, gnp);
+  }
 }
 
 }  // namespace
@@ -387,6 +406,73 @@ extern "C" int vg_hgat_lin_att(const uint16_t* x, int32_t ldx, const uint16_t* w
   return 0;
 }
 
+// lanes per destination row of the f16 aggregation, by row width ld (halves).
+// The first form gave every row 8-16 lanes of 2-16 B each: a 16-32-B row took
+// 8 load instructions with most of the wave's lanes idle on the ~6-edge
+// softmax, and the wide rows moved 8-16 B a lane.  Measured at the sweep's
+// shapes (131k rows, tools/hgat_probe.py, profiles/r06_hgat_lanes_probe.txt),
+// us per launch, first form -> now: ld 8 (2 lanes x 8 B) 8.4-8.6 -> 5.5-5.8;
+// ld 16 (4 x 8 B) 9.0 -> 6.9; ld 32 (2 x 32 B) 11.3 -> 9.2; ld 64 (4 x 32 B)
+// 23.0 -> 15.5; ld 128 (8 x 32 B) 45.7 -> 33.9.  A/B builds: VG_HGAT_L<ld>.
+#ifndef VG_HGAT_L8
+#define VG_HGAT_L8 2
+#endif
+#ifndef VG_HGAT_L16
+#define VG_HGAT_L16 4
+#endif
+#ifndef VG_HGAT_L32
+#define VG_HGAT_L32 2
+#endif
+#ifndef VG_HGAT_L64
+#define VG_HGAT_L64 4
+#endif
+#ifndef VG_HGAT_L128
+#define VG_HGAT_L128 8
+#endif
+constexpr int kHNarrowL = VG_HGAT_L8, kHNarrowL16 = VG_HGAT_L16;
+constexpr int kHL32 = VG_HGAT_L32, kHL64 = VG_HGAT_L64, kHL128 = VG_HGAT_L128;
+
+// lanes per row the aggregation uses for a row of ld halves (0: unsupported)
+static int hgat_lanes(int ld) {
+  switch (ld) {
+    case 8: return kHNarrowL;
+    case 16: return kHNarrowL16;
+    case 32: return kHL32;
+    case 64: return kHL64;
+    case 128: return kHL128;
+    default: return 0;
+  }
+}
+
+static int hgat_launch(const int32_t* row_ptr, const int32_t* col, int n, int c, int ld, const _Float16* H,
+                       const float* a_src, const float* a_dst, const float* bias, float slope, _Float16* O, int ldo,
+                       float* gnp, int seg_rows, hipStream_t s) {
+  // gnp: segment-aligned blocks, S * ceil(seg_rows / G)
+  auto grid = [&](int L) {
+    if (!gnp) return vg::grid_for(n, L);
+    const int G = kBlock / L;
+    return (n / seg_rows) * ((seg_rows + G - 1) / G);
+  };
+#define VG_HA(L_, CPL_)                                                                                            \
+  do {                                                                                                             \
+    if (gnp)                                                                                                       \
+      k_hgat_fwd<L_, CPL_, true><<<grid(L_), kBlock, 0, s>>>(row_ptr, col, n, c, ld, H, a_src, a_dst, bias, slope, \
+                                                             O, ldo, gnp, seg_rows);                               \
+    else                                                                                                           \
+      k_hgat_fwd<L_, CPL_><<<grid(L_), kBlock, 0, s>>>(row_ptr, col, n, c, ld, H, a_src, a_dst, bias, slope, O,    \
+                                                       ldo);                                                       \
+  } while (0)
+  if (ld == 8) VG_HA(kHNarrowL, 8 / kHNarrowL);
+  else if (ld == 16) VG_HA(kHNarrowL16, 16 / kHNarrowL16);
+  else if (ld == 32) VG_HA(kHL32, 32 / kHL32);
+  else if (ld == 64) VG_HA(kHL64, 64 / kHL64);
+  else if (ld == 128) VG_HA(kHL128, 128 / kHL128);
+  else return VG_EINVAL;
+#undef VG_HA
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int vg_hgat_fwd(const int32_t* row_ptr, const int32_t* col, int32_t n, int32_t c, int32_t ld,
                            const uint16_t* h, const float* a_src, const float* a_dst, const float* bias, float slope,
                            uint16_t* out, int32_t ldo, void* stream) {
@@ -396,16 +482,32 @@ extern "C" int vg_hgat_fwd(const int32_t* row_ptr, const int32_t* col, int32_t n
   hipStream_t s = static_cast<hipStream_t>(stream);
   const _Float16* H = reinterpret_cast<const _Float16*>(h);
   _Float16* O = reinterpret_cast<_Float16*>(out);
-#define VG_HA(L_, CPL_)                                                                                     \
-  k_hgat_fwd<L_, CPL_><<<vg::grid_for(n, L_), kBlock, 0, s>>>(row_ptr, col, n, c, ld, H, a_src, a_dst, bias, \
-                                                              slope, O, ldo)
-  if (ld == 8) VG_HA(8, 1);
-  else if (ld == 16) VG_HA(8, 2);
-  else if (ld <= 32) { if (ld != 32) return VG_EINVAL; VG_HA(8, 4); }
-  else if (ld == 64) VG_HA(16, 4);
-  else if (ld == 128) VG_HA(16, 8);
-  else return VG_EINVAL;
-#undef VG_HA
-  VG_CHECK_LAUNCH();
-  return 0;
+  return hgat_launch(row_ptr, col, n, c, ld, H, a_src, a_dst, bias, slope, O, ldo, nullptr, 0, s);
+}
+
+// VG_HGAT_GNP=0 (A/B build): no partials (rows 0), the sweep takes the
+// GraphNorm's own statistics pass
+#ifndef VG_HGAT_GNP
+#define VG_HGAT_GNP 1
+#endif
+extern "C" int32_t vg_hgat_gnp_rows(int32_t n, int32_t ld) {
+  const int L = hgat_lanes(ld);
+  return VG_HGAT_GNP && n > 0 && L > 0 ? kBlock / L : 0;
+}
+
+extern "C" int64_t vg_hgat_gnp_floats(int32_t n, int32_t ld) {
+  const int g = vg_hgat_gnp_rows(n, ld);
+  if (g == 0) return 0;
+  // segment-aligned blocks: S * ceil(seg_rows / g) <= ceil(n / g) + S, S <= n / g
+  return 2 * (((int64_t)n + g - 1) / g) * 2 * (int64_t)ld * 3;
+}
+
+extern "C" int vg_hgat_fwd_gnp(const int32_t* row_ptr, const int32_t* col, int32_t n, int32_t c, int32_t ld,
+                               const uint16_t* h, const float* a_src, const float* a_dst, const float* bias,
+                               float slope, uint16_t* out, int32_t ldo, int32_t seg_rows, float* gnp, void* stream) {
+  if (n <= 0 || c <= 0 || ld % 8 || ldo % 8 || ldo < ld || ld < c || ld > 128 || !row_ptr || !col || !h || !a_src ||
+      !a_dst || !bias || !out || !gnp || seg_rows < vg_hgat_gnp_rows(n, ld) || n % seg_rows)
+    return VG_EINVAL;
+  return hgat_launch(row_ptr, col, n, c, ld, reinterpret_cast<const _Float16*>(h), a_src, a_dst, bias, slope,
+                     reinterpret_cast<_Float16*>(out), ldo, gnp, seg_rows, static_cast<hipStream_t>(stream));
 }

@@ -232,7 +232,14 @@ int run(Arena& ar, const vg_hgen_model* md, const vg_hgen_batch* bt, int8_t* lab
     VG_RUN(vg_hgat_lin_att(x, ldx, B.lin_weight, B.ldw, rows, r8(B.in), cout, B.att_src, B.att_dst, h, ldh, a_s, a_d,
                            s));
     uint16_t* agg = ar.take<uint16_t>((int64_t)rows * ldh);
-    VG_RUN(vg_hgat_fwd(rp, cl, rows, cout, ldh, h, a_s, a_d, B.bias, B.slope, agg, ldh, s));
+    // the GraphNorm's column partials from the aggregation's epilogue when one
+    // copy spans a partial block (half.py makes the same choice)
+    const int g = vg_hgat_gnp_rows(rows, ldh);
+    float* gnp = g > 0 && g <= n ? ar.take<float>(vg_hgat_gnp_floats(rows, ldh)) : nullptr;
+    if (gnp)
+      VG_RUN(vg_hgat_fwd_gnp(rp, cl, rows, cout, ldh, h, a_s, a_d, B.bias, B.slope, agg, ldh, n, gnp, s));
+    else
+      VG_RUN(vg_hgat_fwd(rp, cl, rows, cout, ldh, h, a_s, a_d, B.bias, B.slope, agg, ldh, s));
     uint16_t* y;
     int ldy;
     if (b == nb - 1) {  // the last block writes enc into columns [0, enc_c)
@@ -243,9 +250,14 @@ int run(Arena& ar, const vg_hgen_model* md, const vg_hgen_batch* bt, int8_t* lab
       ldy = ldh;
     }
     float* stats = ar.take<float>((int64_t)kk * 2 * cout);
-    float* ws = ar.take<float>(vg_graphnorm_seg_ws_floats(kk, n, cout));
-    VG_RUN(vg_graphnorm_fwd_h(agg, ldh, kk, n, cout, B.gn_weight, B.gn_bias, B.gn_mean_scale, B.gn_eps, y, ldy, stats,
-                              ws, s));
+    if (gnp) {
+      VG_RUN(vg_graphnorm_fwd_h_gnp(agg, ldh, kk, n, cout, B.gn_weight, B.gn_bias, B.gn_mean_scale, B.gn_eps, y, ldy,
+                                    stats, gnp, g, s));
+    } else {
+      float* ws = ar.take<float>(vg_graphnorm_seg_ws_floats(kk, n, cout));
+      VG_RUN(vg_graphnorm_fwd_h(agg, ldh, kk, n, cout, B.gn_weight, B.gn_bias, B.gn_mean_scale, B.gn_eps, y, ldy, stats,
+                                ws, s));
+    }
     x = y;
     ldx = ldy;
   }

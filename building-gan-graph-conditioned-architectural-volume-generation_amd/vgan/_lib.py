@@ -309,6 +309,12 @@ SIGNATURES = {
                                    _c_p]),
     "vg_graphnorm_fwd_h": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_f32, _c_p,
                                           _c_i32, _c_p, _c_p, _c_p]),
+    "vg_hgat_gnp_rows": (_c_i32, [_c_i32, _c_i32]),
+    "vg_hgat_gnp_floats": (_c_i64, [_c_i32, _c_i32]),
+    "vg_hgat_fwd_gnp": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p,
+                                       _c_i32, _c_i32, _c_p, _c_p]),
+    "vg_graphnorm_fwd_h_gnp": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_f32, _c_p,
+                                              _c_i32, _c_p, _c_p, _c_i32, _c_p]),
     "vg_rng_fill": (ctypes.c_int, [_c_p, _c_i64, _c_i32, ctypes.c_uint64, _c_p, ctypes.c_uint32, _c_p]),
     "vg_gemm_ln_act_ms": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_i32, _c_i32, _c_p,
                                          _c_p, _c_f32, _c_f32, _c_p, _c_i32, _c_p]),

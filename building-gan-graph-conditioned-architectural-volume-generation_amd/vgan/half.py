@@ -171,16 +171,30 @@ class HalfGenerator:
             check(LIB.vg_hgat_lin_att(ptr(x), ldx, ptr(w), w.shape[1], rows, _r8(cin), cout, ptr(att_s),
                                       ptr(att_d), ptr(h), ldh, ptr(a_s), ptr(a_d), s), "vg_hgat_lin_att")
             agg = torch.empty_like(h)
-            check(LIB.vg_hgat_fwd(ptr(csr.row_ptr), ptr(csr.col), rows, cout, ldh, ptr(h), ptr(a_s), ptr(a_d),
-                                  ptr(bias), slope, ptr(agg), ldh, s), "vg_hgat_fwd")
+            # the GraphNorm's column partials from the aggregation's epilogue
+            # when one copy spans a partial block (always, at sweep sizes);
+            # hgen_engine.hip makes the same choice
+            g = int(LIB.vg_hgat_gnp_rows(rows, ldh))
+            gnp = torch.empty(int(LIB.vg_hgat_gnp_floats(rows, ldh)), dtype=torch.float32, device=dev) \
+                if 0 < g <= n else None
+            if gnp is not None:
+                check(LIB.vg_hgat_fwd_gnp(ptr(csr.row_ptr), ptr(csr.col), rows, cout, ldh, ptr(h), ptr(a_s), ptr(a_d),
+                                          ptr(bias), slope, ptr(agg), ldh, n, ptr(gnp), s), "vg_hgat_fwd_gnp")
+            else:
+                check(LIB.vg_hgat_fwd(ptr(csr.row_ptr), ptr(csr.col), rows, cout, ldh, ptr(h), ptr(a_s), ptr(a_d),
+                                      ptr(bias), slope, ptr(agg), ldh, s), "vg_hgat_fwd")
             if b == nb - 1:
                 y, ldy = buf, ld  # the last block writes enc into columns [0, enc_c)
             else:
                 y, ldy = torch.empty_like(h), ldh
             stats = torch.empty(kk * 2 * cout, dtype=torch.float32, device=dev)
-            ws = torch.empty(int(LIB.vg_graphnorm_seg_ws_floats(kk, n, cout)), dtype=torch.float32, device=dev)
-            check(LIB.vg_graphnorm_fwd_h(ptr(agg), ldh, kk, n, cout, ptr(gw), ptr(gb), ptr(gms), eps, ptr(y), ldy,
-                                         ptr(stats), ptr(ws), s), "vg_graphnorm_fwd_h")
+            if gnp is not None:
+                check(LIB.vg_graphnorm_fwd_h_gnp(ptr(agg), ldh, kk, n, cout, ptr(gw), ptr(gb), ptr(gms), eps, ptr(y),
+                                                 ldy, ptr(stats), ptr(gnp), g, s), "vg_graphnorm_fwd_h_gnp")
+            else:
+                ws = torch.empty(int(LIB.vg_graphnorm_seg_ws_floats(kk, n, cout)), dtype=torch.float32, device=dev)
+                check(LIB.vg_graphnorm_fwd_h(ptr(agg), ldh, kk, n, cout, ptr(gw), ptr(gb), ptr(gms), eps, ptr(y), ldy,
+                                             ptr(stats), ptr(ws), s), "vg_graphnorm_fwd_h")
             x, ldx = y, ldy
             self._t(f"gat{b}", y, cout)
         # decoder over the whole row buffer, f32 logits

@@ -999,6 +999,24 @@ int vg_graphnorm_fwd_h(const uint16_t* x, int32_t ld, int32_t S, int32_t N, int3
                        const float* weight, const float* bias, const float* mean_scale, float eps,
                        uint16_t* y, int32_t ldy, float* stats, float* ws, void* stream);
 
+/* vg_hgat_fwd that also writes the following GraphNorm's column partials of
+ * its f16 outputs (vg_gat_aggregate_fwd_gnp's layout and segment-aligned
+ * blocks: gnp [blocks][2][C][3], seg_rows the rows of one stacked copy,
+ * dividing n, at least vg_hgat_gnp_rows), so vg_graphnorm_fwd_h_gnp need not
+ * re-read the output: one launch fewer per block of the f16 sweep
+ * (models.py:144 + 73-75). */
+int32_t vg_hgat_gnp_rows(int32_t n, int32_t ld);
+int64_t vg_hgat_gnp_floats(int32_t n, int32_t ld);
+int vg_hgat_fwd_gnp(const int32_t* row_ptr, const int32_t* col, int32_t n, int32_t c, int32_t ld,
+                    const uint16_t* h, const float* a_src, const float* a_dst, const float* bias, float slope,
+                    uint16_t* out, int32_t ldo, int32_t seg_rows, float* gnp, void* stream);
+/* vg_graphnorm_fwd_h with the statistics folded from vg_hgat_fwd_gnp's
+ * partials (gnp_rows = vg_hgat_gnp_rows of that call). */
+int vg_graphnorm_fwd_h_gnp(const uint16_t* x, int32_t ld, int32_t S, int32_t N, int32_t C,
+                           const float* weight, const float* bias, const float* mean_scale, float eps,
+                           uint16_t* y, int32_t ldy, float* stats, const float* gnp, int32_t gnp_rows,
+                           void* stream);
+
 /* ---- step-graph re-use (host runtime calls, no kernels) ------------------- */
 
 /* Update the executable graph `exec` (a hipGraphExec_t) in place from the

@@ -57,6 +57,10 @@ def test_workspace_queries_are_host_only():
     assert lib.vg_graphnorm_fwd_gnp_fused(12600, 16, 64) == 1
     assert lib.vg_graphnorm_fwd_gnp_fused(12600, 128, 8) == 0
     assert lib.vg_graphnorm_fwd_gnp_fused(12600, 2, 32) == 0
+    # the f16 aggregation's partial blocks: kBlock / lanes per row of the width
+    assert [lib.vg_hgat_gnp_rows(1000, ld) for ld in (8, 16, 32, 64, 128)] == [128, 64, 128, 64, 32]
+    assert lib.vg_hgat_gnp_rows(1000, 24) == 0 and lib.vg_hgat_gnp_floats(1000, 24) == 0
+    assert lib.vg_hgat_gnp_floats(1000, 128) >= (1000 // 32 + 1) * 2 * 128 * 3
 
 
 def test_hgen_arena_sizing_is_host_only():

@@ -124,6 +124,58 @@ def test_graphnorm_fwd_h(cuda, c, segs):
     assert torch.isnan(y[:, ld:]).all()
 
 
+@pytest.mark.parametrize("copies", [1, 3, 10])
+@pytest.mark.parametrize("c", [1, 4, 8, 16, 32, 64, 128])
+def test_hgat_gnp_partials_and_graphnorm(cuda, c, copies):
+    """vg_hgat_fwd_gnp: the same f16 output as vg_hgat_fwd bit for bit, plus the
+    following GraphNorm's column partials per segment-aligned block, from which
+    vg_graphnorm_fwd_h_gnp's statistics match vg_graphnorm_fwd_h's statistics
+    pass over the stored halves (f32 Welford in another grouping: 1e-5) and
+    an f64 GraphNorm of the f16 output; every partial the fold reads is
+    written (buffer pre-filled with NaN).  Stacked copies: the sweep's
+    temperatures, each normalised on its own."""
+    loc, vox = SyntheticDataset(8, seed=4).batch(range(3))
+    loc, vox = loc.to(cuda), vox.to(cuda)
+    base = vdata.prepared(loc, vox, 7).csr
+    n = vox.num_nodes
+    csr = base.stacked(copies) if copies > 1 else base
+    rows = csr.num_nodes
+    ld = _r8(c)
+    h = _h16(rows, c, ld, cuda, seed=8)
+    a_s, a_d = 0.4 * torch.randn(rows, device=cuda), 0.4 * torch.randn(rows, device=cuda)
+    bias = torch.randn(c, device=cuda)
+    s = stream_handle(cuda)
+    g = int(LIB.vg_hgat_gnp_rows(rows, ld))
+    assert 0 < g <= n
+    gnp = torch.full((int(LIB.vg_hgat_gnp_floats(rows, ld)),), float("nan"), device=cuda)
+    o1, o2 = torch.empty(rows, ld, dtype=torch.float16, device=cuda), torch.empty(rows, ld, dtype=torch.float16,
+                                                                                   device=cuda)
+    check(LIB.vg_hgat_fwd_gnp(ptr(csr.row_ptr), ptr(csr.col), rows, c, ld, ptr(h), ptr(a_s), ptr(a_d), ptr(bias), 0.2,
+                              ptr(o1), ld, n, ptr(gnp), s), "vg_hgat_fwd_gnp")
+    check(LIB.vg_hgat_fwd(ptr(csr.row_ptr), ptr(csr.col), rows, c, ld, ptr(h), ptr(a_s), ptr(a_d), ptr(bias), 0.2,
+                          ptr(o2), ld, s), "vg_hgat_fwd")
+    w, b, ms = torch.rand(c, device=cuda) + 0.5, torch.randn(c, device=cuda), torch.rand(c, device=cuda)
+    y1, y2 = torch.empty_like(o1), torch.empty_like(o1)
+    st1 = torch.full((copies * 2 * c,), float("nan"), device=cuda)
+    st2 = torch.empty(copies * 2 * c, device=cuda)
+    check(LIB.vg_graphnorm_fwd_h_gnp(ptr(o1), ld, copies, n, c, ptr(w), ptr(b), ptr(ms), 1e-5, ptr(y1), ld, ptr(st1),
+                                     ptr(gnp), g, s), "vg_graphnorm_fwd_h_gnp")
+    ws = torch.empty(int(LIB.vg_graphnorm_seg_ws_floats(copies, n, c)), device=cuda)
+    check(LIB.vg_graphnorm_fwd_h(ptr(o2), ld, copies, n, c, ptr(w), ptr(b), ptr(ms), 1e-5, ptr(y2), ld, ptr(st2),
+                                 ptr(ws), s), "vg_graphnorm_fwd_h")
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2)
+    assert torch.isfinite(st1).all()
+    assert (st1 - st2).abs().max().item() <= 1e-5 * max(1.0, st2.abs().max().item())
+    xs = o1[:, :c].double().view(copies, n, c)
+    mu = xs.mean(1, keepdim=True)
+    d = ((xs - mu * ms.double()).pow(2).mean(1, keepdim=True) + 1e-5).sqrt()
+    ref = torch.relu(w.double() * (xs - mu * ms.double()) / d + b.double()).reshape(rows, c)
+    _close(y1[:, :c], ref)
+    _close(y1[:, :c], y2[:, :c].float())
+    assert torch.all(y1[:, c:] == 0)
+
+
 @pytest.fixture(scope="module")
 def gen_batch(cuda):
     cfg = Configuration()
