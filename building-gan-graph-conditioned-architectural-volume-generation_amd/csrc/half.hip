@@ -36,6 +36,33 @@ __device__ __forceinline__ h8_t load_h8(const _Float16* p, bool ok) {
   return *reinterpret_cast<const h8_t*>(p);
 }
 
+// The GraphNorm + ReLU of the previous GAT block applied to the A operand as
+// it is loaded (vg_hgat_lin_att_gn): its column operands and every segment's
+// [mu | d] staged in LDS, the expression of k_gn_apply_h element for element
+// (the same f16 values reach the MFMA), pad columns 0.
+constexpr int kGnaMaxSeg = 16;
+constexpr int kGnaFloats = 3 * 128 + 2 * 128 * kGnaMaxSeg;
+struct HGnA {
+  const float *w, *b, *ms, *stats;
+  int C, S, seg_rows;
+};
+
+__device__ __forceinline__ h8_t gn_a(h8_t a, int k0, const float* __restrict__ g, const float* __restrict__ st,
+                                     int C) {
+  h8_t o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = k0 + j;
+    float z = 0.f;
+    if (k < C) {
+      z = ((static_cast<float>(a[j]) - st[k] * g[256 + k]) / st[C + k]) * g[k] + g[128 + k];
+      z = z > 0.f ? z : 0.f;
+    }
+    o[j] = static_cast<_Float16>(z);
+  }
+  return o;
+}
+
 __device__ __forceinline__ float half_sum32(float v) {  // sum over the 32 lanes of a half-wave
 #pragma unroll
   for (int off = 1; off < 32; off <<= 1) v += __shfl_xor(v, off, 64);
@@ -48,13 +75,13 @@ __device__ __forceinline__ float act_apply(float v, int act, float slope) {
   return v;
 }
 
-template <int NT, int EPI, bool OUTF32>
+template <int NT, int EPI, bool OUTF32, bool GNA = false>
 __global__ void __launch_bounds__(256) k_hgemm(
     const _Float16* __restrict__ A, int lda, const _Float16* __restrict__ W, int ldw, int N, int M, int K,
     const float* __restrict__ bias, int act, float slope, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, const float* __restrict__ att_s,
     const float* __restrict__ att_d, float* __restrict__ a_s, float* __restrict__ a_d, void* __restrict__ out,
-    int ldo) {
+    int ldo, const HGnA gna = HGnA{}) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int row0 = (xcd_remap(blockIdx.x, gridDim.x) * 4 + wave) * 32;
   const bool live = row0 < N;  // every wave joins the W staging (block barriers)
@@ -99,6 +126,17 @@ __global__ void __launch_bounds__(256) k_hgemm(
     load_w(0);
     store_w(0);
   }
+  __shared__ float gsh[GNA ? kGnaFloats : 1];
+  const float* gst = gsh;  // this lane's row's segment statistics (GNA)
+  if constexpr (GNA) {
+    for (int i = threadIdx.x; i < gna.C; i += 256) {
+      gsh[i] = gna.w[i];
+      gsh[128 + i] = gna.b[i];
+      gsh[256 + i] = gna.ms[i];
+    }
+    for (int i = threadIdx.x; i < 2 * gna.C * gna.S; i += 256) gsh[384 + i] = gna.stats[i];
+    gst = gsh + 384 + 2 * gna.C * (min(row0 + r, N - 1) / gna.seg_rows);
+  }
   __syncthreads();
   const int nchunks = (K + 31) / 32;
   h8_t a0 = load_h8(ap, 8 * hh < K), a1 = load_h8(ap + 16, 16 + 8 * hh < K);
@@ -119,6 +157,10 @@ __global__ void __launch_bounds__(256) k_hgemm(
     }
     const h8_t an0 = load_h8(ap + kn, more && kn + 8 * hh < K);
     const h8_t an1 = load_h8(ap + kn + 16, more && kn + 16 + 8 * hh < K);
+    if constexpr (GNA) {
+      a0 = gn_a(a0, 32 * kc + 8 * hh, gsh, gst, gna.C);
+      a1 = gn_a(a1, 32 * kc + 16 + 8 * hh, gsh, gst, gna.C);
+    }
     if (live) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, Ws[buf][32 * t + r][hh],
@@ -400,6 +442,33 @@ extern "C" int vg_hgat_lin_att(const uint16_t* x, int32_t ldx, const uint16_t* w
 #define VG_HG(NT_)                                                                                       \
   k_hgemm<NT_, kEpiAtt, false><<<grid, 256, 0, s>>>(A, ldx, W, ldw, n, cout, cin, nullptr, 0, 0.f, nullptr, \
                                                     nullptr, 0.f, att_src, att_dst, a_src, a_dst, h, ldh)
+  if (nt == 1) VG_HG(1); else if (nt == 2) VG_HG(2); else VG_HG(4);
+#undef VG_HG
+  VG_CHECK_LAUNCH();
+  return 0;
+}
+
+
+extern "C" int vg_hgat_lin_att_gn(const uint16_t* x, int32_t ldx, const uint16_t* w, int32_t ldw, int32_t n,
+                                  int32_t cin, int32_t cout, const float* att_src, const float* att_dst, uint16_t* h,
+                                  int32_t ldh, float* a_src, float* a_dst, const float* gn_weight,
+                                  const float* gn_bias, const float* gn_mean_scale, const float* stats,
+                                  int32_t segments, int32_t seg_rows, int32_t gn_channels, void* stream) {
+  if (n <= 0 || cout <= 0 || cout > 128 || cin <= 0 || cin % 8 || cin > 128 || ldx % 8 || ldw % 8 || ldh % 8 ||
+      ldx < cin || ldw < cin || ldh < (cout + 7) / 8 * 8 || !x || !w || !att_src || !att_dst || !h || !a_src ||
+      !a_dst || !gn_weight || !gn_bias || !gn_mean_scale || !stats || segments <= 0 || segments > kGnaMaxSeg ||
+      seg_rows <= 0 || (int64_t)segments * seg_rows != n || gn_channels <= 0 || gn_channels > cin ||
+      (gn_channels + 7) / 8 * 8 != cin)
+    return VG_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const _Float16* A = reinterpret_cast<const _Float16*>(x);
+  const _Float16* W = reinterpret_cast<const _Float16*>(w);
+  const HGnA g{gn_weight, gn_bias, gn_mean_scale, stats, gn_channels, segments, seg_rows};
+  const int grid = (n + 127) / 128;
+  const int nt = (cout + 31) / 32;
+#define VG_HG(NT_)                                                                                             \
+  k_hgemm<NT_, kEpiAtt, false, true><<<grid, 256, 0, s>>>(A, ldx, W, ldw, n, cout, cin, nullptr, 0, 0.f, nullptr, \
+                                                          nullptr, 0.f, att_src, att_dst, a_src, a_dst, h, ldh, g)
   if (nt == 1) VG_HG(1); else if (nt == 2) VG_HG(2); else VG_HG(4);
 #undef VG_HG
   VG_CHECK_LAUNCH();

@@ -115,6 +115,8 @@ struct Arena {
 
 int launched() { return static_cast<int>(hipGetLastError()); }
 
+constexpr int kGnaMaxSeg = 16;  // segments vg_hgat_lin_att_gn stages (half.hip; half.py VG_HGAT_GNA_MAX_SEG)
+
 int blocks_for(long long work) {
   const long long b = (work + 255) / 256;
   return static_cast<int>(std::min<long long>(std::max<long long>(b, 1), 4096));
@@ -223,23 +225,45 @@ int run(Arena& ar, const vg_hgen_model* md, const vg_hgen_batch* bt, int8_t* lab
   }
   const uint16_t* x = buf + o_x;
   int ldx = ld;
+  // a block's GraphNorm + ReLU applied by the next block's projection
+  // (vg_hgat_lin_att_gn) when its statistics come from the aggregation's
+  // partials; the last block's stored -- half.py's choices
+  struct Pend {
+    const uint16_t* agg;
+    int ld;
+    const vg_hgen_block* blk;
+    const float* stats;
+  } pend{nullptr, 0, nullptr, nullptr};
   for (int b = 0; b < nb; ++b) {
     const vg_hgen_block& B = md->block[b];
     const int cout = B.out, ldh = r8(cout);
     uint16_t* h = ar.take<uint16_t>((int64_t)rows * ldh);
     float* a_s = ar.take<float>(rows);
     float* a_d = ar.take<float>(rows);
-    VG_RUN(vg_hgat_lin_att(x, ldx, B.lin_weight, B.ldw, rows, r8(B.in), cout, B.att_src, B.att_dst, h, ldh, a_s, a_d,
-                           s));
+    if (pend.agg) {
+      const vg_hgen_block& P = *pend.blk;
+      VG_RUN(vg_hgat_lin_att_gn(pend.agg, pend.ld, B.lin_weight, B.ldw, rows, r8(B.in), cout, B.att_src, B.att_dst, h,
+                                ldh, a_s, a_d, P.gn_weight, P.gn_bias, P.gn_mean_scale, pend.stats, kk, n, P.out, s));
+      pend = Pend{nullptr, 0, nullptr, nullptr};
+    } else {
+      VG_RUN(vg_hgat_lin_att(x, ldx, B.lin_weight, B.ldw, rows, r8(B.in), cout, B.att_src, B.att_dst, h, ldh, a_s,
+                             a_d, s));
+    }
     uint16_t* agg = ar.take<uint16_t>((int64_t)rows * ldh);
     // the GraphNorm's column partials from the aggregation's epilogue when one
-    // copy spans a partial block (half.py makes the same choice)
+    // copy spans a partial block
     const int g = vg_hgat_gnp_rows(rows, ldh);
     float* gnp = g > 0 && g <= n ? ar.take<float>(vg_hgat_gnp_floats(rows, ldh)) : nullptr;
     if (gnp)
       VG_RUN(vg_hgat_fwd_gnp(rp, cl, rows, cout, ldh, h, a_s, a_d, B.bias, B.slope, agg, ldh, n, gnp, s));
     else
       VG_RUN(vg_hgat_fwd(rp, cl, rows, cout, ldh, h, a_s, a_d, B.bias, B.slope, agg, ldh, s));
+    float* stats = ar.take<float>((int64_t)kk * 2 * cout);
+    if (gnp && b < nb - 1 && kk <= kGnaMaxSeg) {
+      VG_RUN(vg_graphnorm_stats_gnp(kk, n, cout, gnp, g, B.gn_mean_scale, B.gn_eps, stats, s));
+      pend = Pend{agg, ldh, &B, stats};
+      continue;
+    }
     uint16_t* y;
     int ldy;
     if (b == nb - 1) {  // the last block writes enc into columns [0, enc_c)
@@ -249,7 +273,6 @@ int run(Arena& ar, const vg_hgen_model* md, const vg_hgen_batch* bt, int8_t* lab
       y = ar.take<uint16_t>((int64_t)rows * ldh);
       ldy = ldh;
     }
-    float* stats = ar.take<float>((int64_t)kk * 2 * cout);
     if (gnp) {
       VG_RUN(vg_graphnorm_fwd_h_gnp(agg, ldh, kk, n, cout, B.gn_weight, B.gn_bias, B.gn_mean_scale, B.gn_eps, y, ldy,
                                     stats, gnp, g, s));

@@ -39,6 +39,8 @@ from ._lib import LIB, check, ptr, stream_handle
 # native call captured, an executable graph updated in place); 0: the native
 # call launches its kernels directly (vg_hgen_sweep)
 _GRAPH = os.environ.get("VGAN_HGEN_GRAPH", "1") == "1"
+# segments (stacked temperatures) vg_hgat_lin_att_gn stages (kGnaMaxSeg, half.hip)
+VG_HGAT_GNA_MAX_SEG = 16
 
 
 def _r8(c: int) -> int:
@@ -163,17 +165,29 @@ class HalfGenerator:
         csr = prep.csr if kk == 1 else prep.csr.stacked(kk)
         x, ldx = buf[:, o_x:], ld
         nb = len(self.gat)
+        # a block's GraphNorm + ReLU is applied by the next block's projection
+        # as it loads its operand (vg_hgat_lin_att_gn) when the statistics come
+        # from the aggregation's partials; the last block's is stored (it
+        # feeds the decoder's row buffer).  hgen_engine.hip makes the same
+        # choices.  pend: (agg, gw, gb, gms, stats, channels) of that GraphNorm
+        pend = None
         for b, (w, att_s, att_d, bias, cin, cout, slope, gw, gb, gms, eps) in enumerate(self.gat):
             ldh = _r8(cout)
             h = torch.empty(rows, ldh, dtype=torch.float16, device=dev)
             a_s = torch.empty(rows, dtype=torch.float32, device=dev)
             a_d = torch.empty(rows, dtype=torch.float32, device=dev)
-            check(LIB.vg_hgat_lin_att(ptr(x), ldx, ptr(w), w.shape[1], rows, _r8(cin), cout, ptr(att_s),
-                                      ptr(att_d), ptr(h), ldh, ptr(a_s), ptr(a_d), s), "vg_hgat_lin_att")
+            if pend is not None:
+                p_agg, p_w, p_b, p_ms, p_st, p_c = pend
+                check(LIB.vg_hgat_lin_att_gn(ptr(p_agg), p_agg.shape[1], ptr(w), w.shape[1], rows, _r8(cin), cout,
+                                             ptr(att_s), ptr(att_d), ptr(h), ldh, ptr(a_s), ptr(a_d), ptr(p_w),
+                                             ptr(p_b), ptr(p_ms), ptr(p_st), kk, n, p_c, s), "vg_hgat_lin_att_gn")
+                pend = None
+            else:
+                check(LIB.vg_hgat_lin_att(ptr(x), ldx, ptr(w), w.shape[1], rows, _r8(cin), cout, ptr(att_s),
+                                          ptr(att_d), ptr(h), ldh, ptr(a_s), ptr(a_d), s), "vg_hgat_lin_att")
             agg = torch.empty_like(h)
             # the GraphNorm's column partials from the aggregation's epilogue
-            # when one copy spans a partial block (always, at sweep sizes);
-            # hgen_engine.hip makes the same choice
+            # when one copy spans a partial block (always, at sweep sizes)
             g = int(LIB.vg_hgat_gnp_rows(rows, ldh))
             gnp = torch.empty(int(LIB.vg_hgat_gnp_floats(rows, ldh)), dtype=torch.float32, device=dev) \
                 if 0 < g <= n else None
@@ -183,11 +197,16 @@ class HalfGenerator:
             else:
                 check(LIB.vg_hgat_fwd(ptr(csr.row_ptr), ptr(csr.col), rows, cout, ldh, ptr(h), ptr(a_s), ptr(a_d),
                                       ptr(bias), slope, ptr(agg), ldh, s), "vg_hgat_fwd")
+            stats = torch.empty(kk * 2 * cout, dtype=torch.float32, device=dev)
+            if gnp is not None and b < nb - 1 and kk <= VG_HGAT_GNA_MAX_SEG and self.trace is None:
+                check(LIB.vg_graphnorm_stats_gnp(kk, n, cout, ptr(gnp), g, ptr(gms), eps, ptr(stats), s),
+                      "vg_graphnorm_stats_gnp")
+                pend = (agg, gw, gb, gms, stats, cout)
+                continue
             if b == nb - 1:
                 y, ldy = buf, ld  # the last block writes enc into columns [0, enc_c)
             else:
                 y, ldy = torch.empty_like(h), ldh
-            stats = torch.empty(kk * 2 * cout, dtype=torch.float32, device=dev)
             if gnp is not None:
                 check(LIB.vg_graphnorm_fwd_h_gnp(ptr(agg), ldh, kk, n, cout, ptr(gw), ptr(gb), ptr(gms), eps, ptr(y),
                                                  ldy, ptr(stats), ptr(gnp), g, s), "vg_graphnorm_fwd_h_gnp")

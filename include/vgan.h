@@ -985,6 +985,19 @@ int vg_hgat_lin_att(const uint16_t* x, int32_t ldx, const uint16_t* w, int32_t l
                     int32_t cin, int32_t cout, const float* att_src, const float* att_dst,
                     uint16_t* h, int32_t ldh, float* a_src, float* a_dst, void* stream);
 
+/* vg_hgat_lin_att whose operand x is the PREVIOUS block's aggregation output
+ * (gn_channels columns, padded to cin = gn_channels rounded up to 8): its
+ * GraphNorm + ReLU (models.py:73-74, eval) applied as the operand is loaded,
+ * with the statistics [segments][2 gn_channels] of vg_graphnorm_stats_gnp over
+ * segments x seg_rows = n rows (segments <= 16) -- the f16 values
+ * vg_graphnorm_fwd_h_gnp would have stored, without the launch or the
+ * [n, cin] write + read. */
+int vg_hgat_lin_att_gn(const uint16_t* x, int32_t ldx, const uint16_t* w, int32_t ldw, int32_t n, int32_t cin,
+                       int32_t cout, const float* att_src, const float* att_dst, uint16_t* h, int32_t ldh,
+                       float* a_src, float* a_dst, const float* gn_weight, const float* gn_bias,
+                       const float* gn_mean_scale, const float* stats, int32_t segments, int32_t seg_rows,
+                       int32_t gn_channels, void* stream);
+
 /* GATConv edge softmax + CSR gather-sum + bias over f16 rows of ld = c
  * rounded up to 8 channels (8 / 16 / 32 / 64 / 128): the f16
  * vg_gat_aggregate_fwd (torch_geometric GATConv.propagate, models.py:144). */

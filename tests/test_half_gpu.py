@@ -176,6 +176,64 @@ def test_hgat_gnp_partials_and_graphnorm(cuda, c, copies):
     assert torch.all(y1[:, c:] == 0)
 
 
+@pytest.mark.parametrize("copies", [1, 4, 16])
+@pytest.mark.parametrize("cprev,cout", [(64, 32), (1, 2), (4, 8), (16, 128), (128, 64)])
+def test_hgat_lin_att_gn_equals_apply_then_project(cuda, cprev, cout, copies):
+    """vg_hgat_lin_att_gn (the previous block's GraphNorm + ReLU applied as the
+    projection loads its operand) against vg_graphnorm_fwd_h_gnp's stored f16
+    output projected by vg_hgat_lin_att: h, a_src and a_dst bit for bit (the
+    same f16 operand values reach the MFMA); copies up to the 16 segments the
+    kernel stages; the statistics of vg_graphnorm_stats_gnp are those the
+    apply folds."""
+    loc, vox = SyntheticDataset(8, seed=4).batch(range(3))
+    loc, vox = loc.to(cuda), vox.to(cuda)
+    base = vdata.prepared(loc, vox, 7).csr
+    n = vox.num_nodes
+    csr = base.stacked(copies) if copies > 1 else base
+    rows = csr.num_nodes
+    ldp, ldh = _r8(cprev), _r8(cout)
+    s = stream_handle(cuda)
+    hp = _h16(rows, cprev, ldp, cuda, seed=9)
+    a_s0, a_d0 = 0.4 * torch.randn(rows, device=cuda), 0.4 * torch.randn(rows, device=cuda)
+    bias = torch.randn(cprev, device=cuda)
+    g = int(LIB.vg_hgat_gnp_rows(rows, ldp))
+    gnp = torch.empty(int(LIB.vg_hgat_gnp_floats(rows, ldp)), device=cuda)
+    agg = torch.empty(rows, ldp, dtype=torch.float16, device=cuda)
+    check(LIB.vg_hgat_fwd_gnp(ptr(csr.row_ptr), ptr(csr.col), rows, cprev, ldp, ptr(hp), ptr(a_s0), ptr(a_d0),
+                              ptr(bias), 0.2, ptr(agg), ldp, n, ptr(gnp), s), "vg_hgat_fwd_gnp")
+    gw, gb, gms = torch.rand(cprev, device=cuda) + 0.5, 0.3 * torch.randn(cprev, device=cuda), torch.rand(cprev,
+                                                                                                        device=cuda)
+    st1, st2 = torch.empty(copies * 2 * cprev, device=cuda), torch.empty(copies * 2 * cprev, device=cuda)
+    y = torch.empty_like(agg)
+    check(LIB.vg_graphnorm_fwd_h_gnp(ptr(agg), ldp, copies, n, cprev, ptr(gw), ptr(gb), ptr(gms), 1e-5, ptr(y), ldp,
+                                     ptr(st1), ptr(gnp), g, s), "vg_graphnorm_fwd_h_gnp")
+    check(LIB.vg_graphnorm_stats_gnp(copies, n, cprev, ptr(gnp), g, ptr(gms), 1e-5, ptr(st2), s),
+          "vg_graphnorm_stats_gnp")
+    w = _h16(cout, cprev, ldp, cuda, scale=0.2, seed=10)
+    att_s, att_d = torch.randn(cout, device=cuda) * 0.3, torch.randn(cout, device=cuda) * 0.3
+    outs = []
+    for fused in (True, False):
+        h = torch.full((rows, ldh), float("nan"), dtype=torch.float16, device=cuda)
+        a_s, a_d = torch.empty(rows, device=cuda), torch.empty(rows, device=cuda)
+        if fused:
+            check(LIB.vg_hgat_lin_att_gn(ptr(agg), ldp, ptr(w), ldp, rows, ldp, cout, ptr(att_s), ptr(att_d), ptr(h),
+                                         ldh, ptr(a_s), ptr(a_d), ptr(gw), ptr(gb), ptr(gms), ptr(st2), copies, n,
+                                         cprev, s), "vg_hgat_lin_att_gn")
+        else:
+            check(LIB.vg_hgat_lin_att(ptr(y), ldp, ptr(w), ldp, rows, ldp, cout, ptr(att_s), ptr(att_d), ptr(h), ldh,
+                                      ptr(a_s), ptr(a_d), s), "vg_hgat_lin_att")
+        outs.append((h, a_s, a_d))
+    torch.cuda.synchronize()
+    assert torch.equal(st1, st2)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert torch.all(outs[0][0][:, cout:] == 0)
+    bad = LIB.vg_hgat_lin_att_gn(ptr(agg), ldp, ptr(w), ldp, rows, ldp, cout, ptr(att_s), ptr(att_d), ptr(outs[0][0]),
+                                 ldh, ptr(outs[0][1]), ptr(outs[0][2]), ptr(gw), ptr(gb), ptr(gms), ptr(st2), 17,
+                                 rows // 17 if rows % 17 == 0 else 1, cprev, s)
+    assert bad != 0  # more segments than the kernel stages, or a split that does not cover n
+
+
 @pytest.fixture(scope="module")
 def gen_batch(cuda):
     cfg = Configuration()

@@ -51,8 +51,34 @@ def main():
 
         us = timed(run)
         b = agg_bytes(rows, e, c, elem=2)
-        print(json.dumps({"C": c, "ld": ld, "rows": rows, "edges": e, "us": round(us, 2),
-                          "algorithmic_bytes": b, "gbs": round(b / (us * 1e-6) / 1e9, 1)}), flush=True)
+        rec = {"C": c, "ld": ld, "rows": rows, "edges": e, "us": round(us, 2), "algorithmic_bytes": b,
+               "gbs": round(b / (us * 1e-6) / 1e9, 1)}
+        if os.environ.get("HGAT_GN") == "1":  # the block's aggregation + GraphNorm, with / without the partials
+            n = rows // copies
+            g = int(LIB.vg_hgat_gnp_rows(rows, ld))
+            gnp = torch.empty(max(1, int(LIB.vg_hgat_gnp_floats(rows, ld))), device=dev)
+            w, bb, ms = torch.rand(c, device=dev) + 0.5, torch.randn(c, device=dev), torch.rand(c, device=dev)
+            y = torch.empty_like(o)
+            stats = torch.empty(copies * 2 * c, device=dev)
+            ws = torch.empty(int(LIB.vg_graphnorm_seg_ws_floats(copies, n, c)), device=dev)
+
+            def run_gnp():
+                check(LIB.vg_hgat_fwd_gnp(ptr(csr.row_ptr), ptr(csr.col), rows, c, ld, ptr(h), ptr(a_s), ptr(a_d),
+                                          ptr(bias), 0.2, ptr(o), ld, n, ptr(gnp), stream_handle(dev)), "gnp")
+
+            def pair_old():
+                run()
+                check(LIB.vg_graphnorm_fwd_h(ptr(o), ld, copies, n, c, ptr(w), ptr(bb), ptr(ms), 1e-5, ptr(y), ld,
+                                             ptr(stats), ptr(ws), stream_handle(dev)), "gn")
+
+            def pair_new():
+                run_gnp()
+                check(LIB.vg_graphnorm_fwd_h_gnp(ptr(o), ld, copies, n, c, ptr(w), ptr(bb), ptr(ms), 1e-5, ptr(y), ld,
+                                                 ptr(stats), ptr(gnp), g, stream_handle(dev)), "gn_gnp")
+
+            rec.update({"gnp_us": round(timed(run_gnp), 2), "block_stats_pass_us": round(timed(pair_old), 2),
+                        "block_partials_us": round(timed(pair_new), 2)})
+        print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":
