@@ -75,8 +75,22 @@ __device__ __forceinline__ float act_apply(float v, int act, float slope) {
   return v;
 }
 
+// Waves per SIMD the register allocation targets (0: the compiler's choice).
+// Left to itself hipcc kept the accumulators in AGPRs beside 120 VGPRs, 184
+// registers a lane: 2 waves a SIMD, two workgroups a CU, so the sweep's
+// 1,024-workgroup LayerNorm GEMMs ran in two rounds.  At 4 every k_hgemm
+// instantiation fits 128 registers without a spill: the 131k-row LayerNorm
+// GEMMs 30.8 -> 26.1 us (K = 128), 41.4 -> 32.7 (K = 272), 59.6 -> 46.8
+// (K = 528) (tools/hgemm_ln_probe.py, profiles/r06_hgemm_ln_probe.txt).
+#ifndef VG_HGEMM_WPE
+#define VG_HGEMM_WPE 4
+#endif
 template <int NT, int EPI, bool OUTF32, bool GNA = false>
-__global__ void __launch_bounds__(256) k_hgemm(
+__global__ void __launch_bounds__(256)
+#if VG_HGEMM_WPE
+__attribute__((amdgpu_waves_per_eu(VG_HGEMM_WPE)))
+#endif
+k_hgemm(
     const _Float16* __restrict__ A, int lda, const _Float16* __restrict__ W, int ldw, int N, int M, int K,
     const float* __restrict__ bias, int act, float slope, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, const float* __restrict__ att_s,
