@@ -36,6 +36,12 @@
 #include "gnbwd.h"
 #include "rowgroup.h"
 
+#ifndef VG_BWD_ROWS_WPE
+#define VG_BWD_ROWS_WPE 4  // workgroups per CU the register allocation of k_gat_bwd_rows_cp targets for CPL <= 4
+                           // (0: the compiler's choice, 3 at 132-138 VGPRs; 4 fits without a spill: step -0.01 ms,
+                           // profiles/r06_occupancy_ab.txt)
+#endif
+
 namespace {
 
 using namespace vg;
@@ -410,7 +416,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_ep(
 // backward of the layer's output (gnbwd.h, vg_gat_bwd_gn) -- and written to
 // gn.g_out for the source pass (one launch and one pass over g_out fewer).
 template <int L, int CPL, bool VEC, bool GN = false>
-__global__ void __launch_bounds__(kBlock) k_gat_bwd_rows_cp(
+__global__ void __launch_bounds__(kBlock, CPL <= 4 && VG_BWD_ROWS_WPE ? VG_BWD_ROWS_WPE : 1) k_gat_bwd_rows_cp(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, int N, int C,
     const float* __restrict__ h, const float* __restrict__ a_src, const float* __restrict__ a_dst,
     const float* __restrict__ alpha, const float* __restrict__ g_out, float slope,

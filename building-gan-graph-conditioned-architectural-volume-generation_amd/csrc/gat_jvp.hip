@@ -24,6 +24,10 @@
 #include "gnjvp.h"
 #include "rowgroup.h"
 
+#ifndef VG_JVP_ROWS_WPE
+#define VG_JVP_ROWS_WPE 0  // workgroups per CU the register allocation of k_jvp_rows targets for CPL <= 4 (0: the compiler's choice)
+#endif
+
 namespace {
 
 using namespace vg;
@@ -93,7 +97,7 @@ __device__ __forceinline__ void gnj_block_sums(const Vec<CPL> (&v)[5], int C, fl
 
 // e_u / e_h: per-edge U, H written by the lane that reads them back (no restrict).
 template <int L, int CPL, bool VEC, bool GNJ = false>
-__global__ void __launch_bounds__(kBlock) k_jvp_rows(
+__global__ void __launch_bounds__(kBlock, CPL <= 4 && VG_JVP_ROWS_WPE ? VG_JVP_ROWS_WPE : 1) k_jvp_rows(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, int N, int C,
     const float* __restrict__ h, const float* __restrict__ u, const float* __restrict__ gv,
     const float* __restrict__ a_src, const float* __restrict__ a_dst,

@@ -169,12 +169,21 @@ inline bool pick_fused_shape(int C, Shape& sh) {
 // Every group accumulates per-channel partials in registers over the rows it
 // visits (grid-stride); the block folds its groups through LDS and writes one
 // row of `part` ([gridDim.x][W]).  W <= 3 * 256.
+// The LDS image of block_partials: ONE buffer per kernel, whatever row shapes
+// the kernel instantiates (a static __shared__ array inside the template gave
+// every instantiation its own 16 KB: the grouped / merged source passes, which
+// switch over six shapes, took 96 KB of LDS and ran one workgroup per CU).
+__device__ __forceinline__ float* block_partials_lds() {
+  __shared__ float red[kBlock * 8 * 2];  // (256/L) groups x L*CPL channels (CPL <= 8) x up to 2 vectors
+  return red;
+}
+
 template <int L, int CPL>
 __device__ void block_partials(const Vec<CPL>* vals, int nvec, int C, float* __restrict__ part,
                                int bid = -1) {
   if (bid < 0) bid = blockIdx.x;  // the partial row (grouped launches pass their own block index)
   constexpr int G = kBlock / L;
-  __shared__ float red[kBlock * 8 * 2];  // (256/L) groups x L*CPL channels (CPL <= 8) x up to 2 vectors
+  float* red = block_partials_lds();
   const int grp = threadIdx.x / L, lane = threadIdx.x & (L - 1);
   const int Wg = L * CPL;
   for (int v = 0; v < nvec; ++v)
