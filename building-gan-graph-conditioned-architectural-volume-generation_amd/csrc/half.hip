@@ -463,6 +463,8 @@ extern "C" int vg_hgat_lin_att(const uint16_t* x, int32_t ldx, const uint16_t* w
 }
 
 
+extern "C" int32_t vg_hgat_gna_max_segments(void) { return kGnaMaxSeg; }
+
 extern "C" int vg_hgat_lin_att_gn(const uint16_t* x, int32_t ldx, const uint16_t* w, int32_t ldw, int32_t n,
                                   int32_t cin, int32_t cout, const float* att_src, const float* att_dst, uint16_t* h,
                                   int32_t ldh, float* a_src, float* a_dst, const float* gn_weight,

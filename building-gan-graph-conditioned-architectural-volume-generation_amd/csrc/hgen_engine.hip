@@ -115,7 +115,6 @@ struct Arena {
 
 int launched() { return static_cast<int>(hipGetLastError()); }
 
-constexpr int kGnaMaxSeg = 16;  // segments vg_hgat_lin_att_gn stages (half.hip; half.py VG_HGAT_GNA_MAX_SEG)
 
 int blocks_for(long long work) {
   const long long b = (work + 255) / 256;
@@ -259,7 +258,7 @@ int run(Arena& ar, const vg_hgen_model* md, const vg_hgen_batch* bt, int8_t* lab
     else
       VG_RUN(vg_hgat_fwd(rp, cl, rows, cout, ldh, h, a_s, a_d, B.bias, B.slope, agg, ldh, s));
     float* stats = ar.take<float>((int64_t)kk * 2 * cout);
-    if (gnp && b < nb - 1 && kk <= kGnaMaxSeg) {
+    if (gnp && b < nb - 1 && kk <= vg_hgat_gna_max_segments()) {
       VG_RUN(vg_graphnorm_stats_gnp(kk, n, cout, gnp, g, B.gn_mean_scale, B.gn_eps, stats, s));
       pend = Pend{agg, ldh, &B, stats};
       continue;

@@ -305,6 +305,7 @@ SIGNATURES = {
                                        _c_f32, _c_p, _c_i32, _c_p]),
     "vg_hgat_lin_att": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_i32,
                                        _c_p, _c_p, _c_p]),
+    "vg_hgat_gna_max_segments": (_c_i32, []),
     "vg_hgat_lin_att_gn": (ctypes.c_int, [_c_p, _c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p,
                                           _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p]),
     "vg_hgat_fwd": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_p, _c_i32,

@@ -39,8 +39,7 @@ from ._lib import LIB, check, ptr, stream_handle
 # native call captured, an executable graph updated in place); 0: the native
 # call launches its kernels directly (vg_hgen_sweep)
 _GRAPH = os.environ.get("VGAN_HGEN_GRAPH", "1") == "1"
-# segments (stacked temperatures) vg_hgat_lin_att_gn stages (kGnaMaxSeg, half.hip)
-VG_HGAT_GNA_MAX_SEG = 16
+
 
 
 def _r8(c: int) -> int:
@@ -198,7 +197,8 @@ class HalfGenerator:
                 check(LIB.vg_hgat_fwd(ptr(csr.row_ptr), ptr(csr.col), rows, cout, ldh, ptr(h), ptr(a_s), ptr(a_d),
                                       ptr(bias), slope, ptr(agg), ldh, s), "vg_hgat_fwd")
             stats = torch.empty(kk * 2 * cout, dtype=torch.float32, device=dev)
-            if gnp is not None and b < nb - 1 and kk <= VG_HGAT_GNA_MAX_SEG and self.trace is None:
+            if gnp is not None and b < nb - 1 and kk <= int(LIB.vg_hgat_gna_max_segments()) \
+                    and self.trace is None:
                 check(LIB.vg_graphnorm_stats_gnp(kk, n, cout, ptr(gnp), g, ptr(gms), eps, ptr(stats), s),
                       "vg_graphnorm_stats_gnp")
                 pend = (agg, gw, gb, gms, stats, cout)

@@ -992,6 +992,8 @@ int vg_hgat_lin_att(const uint16_t* x, int32_t ldx, const uint16_t* w, int32_t l
  * segments x seg_rows = n rows (segments <= 16) -- the f16 values
  * vg_graphnorm_fwd_h_gnp would have stored, without the launch or the
  * [n, cin] write + read. */
+/* The most segments (stacked copies) vg_hgat_lin_att_gn stages.  Host-only. */
+int32_t vg_hgat_gna_max_segments(void);
 int vg_hgat_lin_att_gn(const uint16_t* x, int32_t ldx, const uint16_t* w, int32_t ldw, int32_t n, int32_t cin,
                        int32_t cout, const float* att_src, const float* att_dst, uint16_t* h, int32_t ldh,
                        float* a_src, float* a_dst, const float* gn_weight, const float* gn_bias,

@@ -60,6 +60,7 @@ def test_workspace_queries_are_host_only():
     # the f16 aggregation's partial blocks: kBlock / lanes per row of the width
     assert [lib.vg_hgat_gnp_rows(1000, ld) for ld in (8, 16, 32, 64, 128)] == [128, 64, 128, 64, 32]
     assert lib.vg_hgat_gnp_rows(1000, 24) == 0 and lib.vg_hgat_gnp_floats(1000, 24) == 0
+    assert lib.vg_hgat_gna_max_segments() == 16
     assert lib.vg_hgat_gnp_floats(1000, 128) >= (1000 // 32 + 1) * 2 * 128 * 3
 
 
