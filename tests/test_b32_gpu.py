@@ -117,11 +117,14 @@ def test_b32_generator_loss_and_grads(cuda, b32):
     g_loss.backward()
     ref = float(f["g_loss"])
     assert abs(g_loss.item() - ref) <= 1e-3 * max(1.0, abs(ref))
-    # per parameter 5e-2: a GraphNorm mean_scale gradient is -mu w A / s with A a
-    # column sum over 12.7k rows that cancels to ~1% of its terms, so its f32
-    # summation order (GPU tree vs the CPU's) shows at the percent level; the
-    # whole gradient is held to 2e-3 (measured 1.0e-3)
-    ok, worst, total = grads_close({k: p.grad for k, p in G.named_parameters()}, f["g_grads"], rtol=5e-2,
+    # per parameter 2.5e-2: a GraphNorm mean_scale gradient is -mu w A / s with A
+    # a column sum over 12.7k rows that cancels to ~1% of its terms, so its f32
+    # summation order (GPU tree vs the CPU's) shows at the percent level --
+    # measured worst 0.25 of 5e-2 at init (encoder.module_16.att_src) and 0.04
+    # at the perturbed parameters (round 6), so 2.5e-2 keeps 2x margin; the
+    # per-parameter check that a wrong formula cannot pass is the f64 one
+    # below.  The whole gradient is held to 2e-3 (measured 1.6e-3 / 2.1e-4)
+    ok, worst, total = grads_close({k: p.grad for k, p in G.named_parameters()}, f["g_grads"], rtol=2.5e-2,
                                    total_rtol=2e-3)
     print(f"batch 32: G gradient relative error {total:.2e}, worst parameter {worst}")
     assert ok, (worst, total)
