@@ -69,6 +69,91 @@ __device__ __forceinline__ float half_sum32(float v) {  // sum over the 32 lanes
   return v;
 }
 
+// Sums of 16 values across the 32 lanes of a half-wave, transposed: each
+// xor step hands half of the lane's remaining values to its partner and keeps
+// the other half (16 -> 8 -> 4 -> 2 -> 1), so 16 shuffles reduce all 16
+// instead of 5 each (80).  Returns the total of value index
+// i = 8 b4 + 4 b3 + 2 b2 + b1 (bits of the lane id r), held by lanes 2i and
+// 2i + 1.  Summation order differs from half_sum32 (f32 rounding).
+__device__ __forceinline__ float half_sum32x16(const float (&v)[16], int r) {
+  float a[8];
+  {
+    const bool b = (r & 16) != 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float keep = b ? v[k + 8] : v[k], give = b ? v[k] : v[k + 8];
+      a[k] = keep + __shfl_xor(give, 16, 64);
+    }
+  }
+  float c[4];
+  {
+    const bool b = (r & 8) != 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float keep = b ? a[k + 4] : a[k], give = b ? a[k] : a[k + 4];
+      c[k] = keep + __shfl_xor(give, 8, 64);
+    }
+  }
+  float d[2];
+  {
+    const bool b = (r & 4) != 0;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const float keep = b ? c[k + 2] : c[k], give = b ? c[k] : c[k + 2];
+      d[k] = keep + __shfl_xor(give, 4, 64);
+    }
+  }
+  const bool b1 = (r & 2) != 0;
+  float e = (b1 ? d[1] : d[0]) + __shfl_xor(b1 ? d[0] : d[1], 2, 64);
+  return e + __shfl_xor(e, 1, 64);
+}
+
+// The inverse: lanes 2i, 2i + 1 hold the value of index i (half_sum32x16's
+// layout); every lane of the half-wave gets all 16 (15 shuffles).
+__device__ __forceinline__ void half_gather32x16(float x, int r, float (&out)[16]) {
+  float a1[2], a2[4], a3[8];
+  {
+    const bool b = (r & 2) != 0;
+    const float o = __shfl_xor(x, 2, 64);
+    a1[0] = b ? o : x;
+    a1[1] = b ? x : o;
+  }
+  {
+    const bool b = (r & 4) != 0;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const float o = __shfl_xor(a1[k], 4, 64);
+      a2[k] = b ? o : a1[k];
+      a2[k + 2] = b ? a1[k] : o;
+    }
+  }
+  {
+    const bool b = (r & 8) != 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float o = __shfl_xor(a2[k], 8, 64);
+      a3[k] = b ? o : a2[k];
+      a3[k + 4] = b ? a2[k] : o;
+    }
+  }
+  {
+    const bool b = (r & 16) != 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float o = __shfl_xor(a3[k], 16, 64);
+      out[k] = b ? o : a3[k];
+      out[k + 8] = b ? a3[k] : o;
+    }
+  }
+}
+
+#ifndef VG_HGEMM_XRED
+#define VG_HGEMM_XRED 1  // the attention epilogue's row sums by half_sum32x16 (0: half_sum32 per row)
+#endif
+#ifndef VG_HGEMM_XRED_LN
+#define VG_HGEMM_XRED_LN 1  // the LayerNorm epilogue's mean / variance the same way, gathered back
+#endif
+
 __device__ __forceinline__ float act_apply(float v, int act, float slope) {
   if (act == 1) return v > 0.f ? v : 0.f;
   if (act == 2) return v > 0.f ? v : v * slope;
@@ -213,6 +298,37 @@ k_hgemm(
       g[t] = wok[t] ? gamma[32 * t + r] : 0.f;
       be[t] = wok[t] ? beta[32 * t + r] : 0.f;
     }
+    if constexpr (VG_HGEMM_XRED_LN) {
+      // two-pass statistics of the 16 rows: transposed sums, gathered back;
+      // one 16-float array (the sums, then each row's mean, then its
+      // reciprocal deviation), the accumulators centred in place
+      float v[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        v[i] = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) v[i] += wok[t] ? acc[t][i] : 0.f;
+      }
+      half_gather32x16(half_sum32x16(v, r) * inv_m, r, v);
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t][i] -= v[i];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        v[i] = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) v[i] += wok[t] ? acc[t][i] * acc[t][i] : 0.f;
+      }
+      half_gather32x16(rsqrtf(half_sum32x16(v, r) * inv_m + eps), r, v);
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const float y = acc[t][i] * v[i] * g[t] + be[t];
+          acc[t][i] = y > 0.f ? y : y * slope;
+        }
+    } else
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       float s = 0.f;
@@ -239,20 +355,41 @@ k_hgemm(
       vs[t] = wok[t] ? att_s[32 * t + r] : 0.f;
       vd[t] = wok[t] ? att_d[32 * t + r] : 0.f;
     }
+    if constexpr (VG_HGEMM_XRED) {
+      float ps[16], pd[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      float ps = 0.f, pd = 0.f;
+      for (int i = 0; i < 16; ++i) {
+        ps[i] = 0.f;
+        pd[i] = 0.f;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        ps = fmaf(acc[t][i], vs[t], ps);
-        pd = fmaf(acc[t][i], vd[t], pd);
+        for (int t = 0; t < NT; ++t) {
+          ps[i] = fmaf(acc[t][i], vs[t], ps[i]);
+          pd[i] = fmaf(acc[t][i], vd[t], pd[i]);
+        }
       }
-      ps = half_sum32(ps);
-      pd = half_sum32(pd);
+      const float ss = half_sum32x16(ps, r), sd = half_sum32x16(pd, r);
+      const int i = 8 * ((r >> 4) & 1) + 4 * ((r >> 3) & 1) + 2 * ((r >> 2) & 1) + ((r >> 1) & 1);
       const int row = row0 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-      if (r == 0 && row < N) {
-        a_s[row] = ps;
-        a_d[row] = pd;
+      if ((r & 1) == 0 && row < N) {
+        a_s[row] = ss;
+        a_d[row] = sd;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float ps = 0.f, pd = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          ps = fmaf(acc[t][i], vs[t], ps);
+          pd = fmaf(acc[t][i], vd[t], pd);
+        }
+        ps = half_sum32(ps);
+        pd = half_sum32(pd);
+        const int row = row0 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+        if (r == 0 && row < N) {
+          a_s[row] = ps;
+          a_d[row] = pd;
+        }
       }
     }
   } else {

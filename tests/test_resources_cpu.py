@@ -75,8 +75,13 @@ def test_merged_source_passes_hold_one_partials_image(usage):
 
 
 def test_f16_gemm_at_four_waves_without_spills(usage):
+    """Every k_hgemm at 4 waves a SIMD; no spills, except the 128-wide
+    LayerNorm GEMM's one VGPR (8 B of scratch a lane, in the epilogue's
+    transposed statistics), measured faster than the spill-free epilogue
+    (profiles/r06_hgemm_ln_probe.txt)."""
     for name, u in _named(usage["half.hip"], "k_hgemm").items():
-        assert u["occ"] >= 4 and u.get("spill", 0) == 0, (name, u)
+        allowed = 1 if name.startswith("_ZN12_GLOBAL__N_17k_hgemmILi4ELi1E") else 0
+        assert u["occ"] >= 4 and u.get("spill", 0) <= allowed, (name, u)
 
 
 def test_narrow_gat_backward_rows_at_four_waves_without_spills(usage):
