@@ -63,6 +63,42 @@ __global__ void k_hg_pack(const PackDesc d) {
   }
 }
 
+// The same packing four columns a thread (one 8-B store) when every source's
+// col0 and span and the row stride are multiples of 4 (the sweep's row
+// buffer: em at 256, voxel.x at 384, z at 396 of 528): a quarter of the
+// integer divisions and stores of k_hg_pack; the same bits.
+__global__ void k_hg_pack4(const PackDesc d) {
+  const int q = blockIdx.y;
+  if (q >= d.ns) return;
+  const PackSrc& p = d.s[q];
+  const int span4 = (p.zero_to > p.w ? p.zero_to : p.w) / 4;
+  const long long total = (long long)d.rows * span4;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int r = static_cast<int>(t / span4), j0 = 4 * static_cast<int>(t - (long long)r * span4);
+    const int sr = r % p.src_rows;
+    uint16_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int j = j0 + k;
+      v[k] = 0;
+      if (j < p.w) {
+        if (p.is_f16) {
+          v[k] = static_cast<const uint16_t*>(p.src)[(size_t)sr * p.ld + j];
+        } else {
+          const __half h = __float2half_rn(static_cast<const float*>(p.src)[(size_t)sr * p.ld + j]);
+          v[k] = __half_as_ushort(h);
+        }
+      }
+    }
+    *reinterpret_cast<uint2*>(d.dst + (size_t)r * d.ldd + p.col0 + j0) =
+        make_uint2(v[0] | (static_cast<uint32_t>(v[1]) << 16), v[2] | (static_cast<uint32_t>(v[3]) << 16));
+  }
+}
+
+// k_hg_pack4 when the layout allows it, else k_hg_pack (both grids y = sources)
+int hg_pack(const PackDesc& d, long long work, hipStream_t s);
+
 // block-diagonal stack of `copies` copies of a destination CSR (vgan.ops
 // CSR.stacked: node ids offset by c * n, edge slots by c * e)
 __global__ void k_hg_stack_csr(const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, int n, int e,
@@ -119,6 +155,23 @@ int launched() { return static_cast<int>(hipGetLastError()); }
 int blocks_for(long long work) {
   const long long b = (work + 255) / 256;
   return static_cast<int>(std::min<long long>(std::max<long long>(b, 1), 4096));
+}
+
+#ifndef VG_HG_PACK4
+#define VG_HG_PACK4 1
+#endif
+
+int hg_pack(const PackDesc& d, long long work, hipStream_t s) {
+  bool quad = VG_HG_PACK4 && d.ldd % 4 == 0 && (reinterpret_cast<uintptr_t>(d.dst) & 7) == 0;
+  for (int q = 0; q < d.ns; ++q) {
+    const int span = d.s[q].zero_to > d.s[q].w ? d.s[q].zero_to : d.s[q].w;
+    quad = quad && d.s[q].col0 % 4 == 0 && span % 4 == 0;
+  }
+  if (quad)
+    k_hg_pack4<<<dim3(blocks_for(work / 4), d.ns), 256, 0, s>>>(d);
+  else
+    k_hg_pack<<<dim3(blocks_for(work), d.ns), 256, 0, s>>>(d);
+  return launched();
 }
 
 // HalfGenerator._run_mlp: the blocks over `rows` rows of a (stride lda); the
@@ -180,14 +233,14 @@ int run(Arena& ar, const vg_hgen_model* md, const vg_hgen_batch* bt, int8_t* lab
     d.s[0] = PackSrc{bt->voxel_x, vd, vd, n, o_vx, vd, 0};
     d.s[1] = PackSrc{z, zd, zd, rows, o_z, ld - o_z, 0};  // z, then the zero pad columns
     d.ns = 2;
-    VG_RUN((k_hg_pack<<<dim3(blocks_for((long long)rows * (ld - o_z)), 2), 256, 0, s>>>(d), launched()));
+    VG_RUN(hg_pack(d, (long long)rows * (ld - o_z), s));
     PackDesc e{};
     e.dst = a0;
     e.ldd = r8(fl);
     e.rows = n;
     e.s[0] = PackSrc{bt->matched_x, fl, fl, n, 0, r8(fl), 0};
     e.ns = 1;
-    VG_RUN((k_hg_pack<<<dim3(blocks_for((long long)n * r8(fl)), 1), 256, 0, s>>>(e), launched()));
+    VG_RUN(hg_pack(e, (long long)n * r8(fl), s));
   }
   // program-feature encoder once on n rows, broadcast into every copy
   const uint16_t* em;
@@ -200,7 +253,7 @@ int run(Arena& ar, const vg_hgen_model* md, const vg_hgen_batch* bt, int8_t* lab
     d.rows = rows;
     d.s[0] = PackSrc{em, ld_em, hl, n, o_em, hl, 1};
     d.ns = 1;
-    VG_RUN((k_hg_pack<<<dim3(blocks_for((long long)rows * hl), 1), 256, 0, s>>>(d), launched()));
+    VG_RUN(hg_pack(d, (long long)rows * hl, s));
   }
   // MLP encoder: reads [em | voxel.x | z] in place, writes x into its slice
   {
